@@ -1,0 +1,63 @@
+// flexible_llm_sharding_amd — native C ABI shared by the HIP kernel library
+// (libfls_kernels.so) and the host runtime (libfls_runtime.so).
+//
+// Everything is exported with C linkage and raw pointers so Python binds it
+// through ctypes with no PyTorch headers in the build (fast, hermetic
+// builds; hipcc --offload-arch=gfx950 only).  Streams are passed as
+// hipStream_t (the value of torch.cuda.Stream.cuda_stream on ROCm).
+#pragma once
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* fls_stream_t;
+
+// ----------------------------------------------------------------- runtime
+int   fls_rt_version(void);
+void* fls_pinned_alloc(uint64_t bytes);                  // hipHostMalloc; NULL on failure
+int   fls_pinned_free(void* p);
+int   fls_pinned_register(void* p, uint64_t bytes);      // hipHostRegister an existing range
+int   fls_pinned_unregister(void* p);
+int   fls_memcpy_async(void* dst, const void* src, uint64_t bytes, int kind, fls_stream_t s);
+int64_t fls_pread_into(const char* path, uint64_t offset, uint64_t bytes, void* dst, int nthreads);
+int64_t fls_pwrite_from(const char* path, uint64_t offset, uint64_t bytes, const void* src,
+                        int nthreads, int truncate);
+int   fls_gather_blocks(void* dst, const void* src, uint64_t block_bytes, const int64_t* src_block,
+                        int64_t n_blocks, int nthreads);
+// safetensors header index
+void* fls_st_open(const char* path);
+int   fls_st_count(void* h);
+int   fls_st_info(void* h, int i, char* name, int name_cap, char* dtype, int dtype_cap,
+                  int64_t* shape, int* ndim, uint64_t* begin, uint64_t* end);
+uint64_t fls_st_data_offset(void* h);
+void  fls_st_close(void* h);
+int   fls_mem_info(uint64_t* free_b, uint64_t* total_b);
+
+// ----------------------------------------------------------------- kernels
+int fls_kernels_version(void);
+// epilogue codes for fls_gemm
+enum { FLS_EPI_NONE = 0, FLS_EPI_RESID = 1, FLS_EPI_SWIGLU = 2, FLS_EPI_ROPE = 3 };
+// C[M, N'] = epi(A[M,K] . W[N,K]^T).  fp16 in / fp32 accumulate / fp16 out.
+//   RESID : C = acc + R (R may alias C)
+//   SWIGLU: W rows gate/up interleaved per 16; C has N/2 columns = silu(g)*u
+//   ROPE  : columns < rope_cols are rotated (RoPE-pair-permuted heads of
+//           head_dim) with pos[m] and fp32 tables cos/sin [maxpos, head_dim/2]
+int fls_gemm(const void* A, const void* W, void* C, const void* R, int M, int N, int K,
+             int lda, int ldw, int ldc, int ldr, int epi, const int* pos, const float* cos_t,
+             const float* sin_t, int rope_cols, int head_dim, fls_stream_t s);
+// shared-prefix / varlen flash attention over packed work items (int32 x8)
+int fls_attention(const void* qkv, void* out, const int* work, int n_items, int n_q_heads,
+                  int n_kv_heads, int head_dim, int ld_qkv, int ld_out, float scale, fls_stream_t s);
+int fls_rmsnorm(const void* x, const void* w, void* y, const int* row_idx, int rows, int H,
+                int ldx, int ldy, float eps, fls_stream_t s);
+int fls_embed(const int* ids, const void* table, void* out, int T, int H, int V, fls_stream_t s);
+int fls_softmax_rows(const void* logits, void* probs, int rows, int V, fls_stream_t s);
+int fls_fill_random(void* dst, uint64_t n_elems, uint64_t seed, float mean, float std,
+                    fls_stream_t s);
+
+#ifdef __cplusplus
+}
+#endif

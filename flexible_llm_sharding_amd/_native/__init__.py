@@ -1,0 +1,96 @@
+"""ctypes bindings of the in-tree native libraries (see ``csrc/include/fls.h``).
+
+``kernels()`` / ``runtime()`` raise if the library is missing — on a GPU the
+HIP path must be the one that runs (no silent fallback); CPU-only code paths
+call ``runtime_or_none()``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_KERNELS = os.path.join(HERE, "libfls_kernels.so")
+_RUNTIME = os.path.join(HERE, "libfls_runtime.so")
+
+_lock = threading.Lock()
+_libs = {}
+
+c_void_p, c_int, c_int64, c_uint64, c_float, c_char_p = (
+    ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float, ctypes.c_char_p)
+
+
+def _bind(lib, name, restype, *argtypes):
+    f = getattr(lib, name)
+    f.restype = restype
+    f.argtypes = list(argtypes)
+
+
+def _load_runtime():
+    lib = ctypes.CDLL(_RUNTIME)
+    _bind(lib, "fls_rt_version", c_int)
+    _bind(lib, "fls_pinned_alloc", c_void_p, c_uint64)
+    _bind(lib, "fls_pinned_free", c_int, c_void_p)
+    _bind(lib, "fls_pinned_register", c_int, c_void_p, c_uint64)
+    _bind(lib, "fls_pinned_unregister", c_int, c_void_p)
+    _bind(lib, "fls_memcpy_async", c_int, c_void_p, c_void_p, c_uint64, c_int, c_void_p)
+    _bind(lib, "fls_pread_into", c_int64, c_char_p, c_uint64, c_uint64, c_void_p, c_int)
+    _bind(lib, "fls_pwrite_from", c_int64, c_char_p, c_uint64, c_uint64, c_void_p, c_int, c_int)
+    _bind(lib, "fls_gather_blocks", c_int, c_void_p, c_void_p, c_uint64, c_void_p, c_int64, c_int)
+    _bind(lib, "fls_st_open", c_void_p, c_char_p)
+    _bind(lib, "fls_st_count", c_int, c_void_p)
+    _bind(lib, "fls_st_info", c_int, c_void_p, c_int, c_char_p, c_int, c_char_p, c_int,
+          c_void_p, c_void_p, c_void_p, c_void_p)
+    _bind(lib, "fls_st_data_offset", c_uint64, c_void_p)
+    _bind(lib, "fls_st_close", None, c_void_p)
+    _bind(lib, "fls_mem_info", c_int, c_void_p, c_void_p)
+    return lib
+
+
+def _load_kernels():
+    lib = ctypes.CDLL(_KERNELS)
+    _bind(lib, "fls_kernels_version", c_int)
+    _bind(lib, "fls_gemm", c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+          c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p)
+    _bind(lib, "fls_attention", c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+          c_int, c_int, c_float, c_void_p)
+    _bind(lib, "fls_rmsnorm", c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+          c_int, c_float, c_void_p)
+    _bind(lib, "fls_embed", c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p)
+    _bind(lib, "fls_softmax_rows", c_int, c_void_p, c_void_p, c_int, c_int, c_void_p)
+    _bind(lib, "fls_fill_random", c_int, c_void_p, c_uint64, c_uint64, c_float, c_float, c_void_p)
+    return lib
+
+
+def _get(key, path, loader, required):
+    with _lock:
+        if key in _libs:
+            return _libs[key]
+        if not os.path.exists(path):
+            if required:
+                raise RuntimeError(
+                    f"native library {path} is missing — build it with "
+                    f"`python -m flexible_llm_sharding_amd._native.build`")
+            return None
+        _libs[key] = loader()
+        return _libs[key]
+
+
+def kernels():
+    return _get("k", _KERNELS, _load_kernels, True)
+
+
+def runtime():
+    return _get("r", _RUNTIME, _load_runtime, True)
+
+
+def runtime_or_none():
+    try:
+        return _get("r", _RUNTIME, _load_runtime, False)
+    except OSError:
+        return None
+
+
+def loaded_libraries():
+    return {k: getattr(v, "_name", None) for k, v in _libs.items()}

@@ -1,0 +1,196 @@
+"""End-to-end driver: ``main.py`` semantics on one process per GPU.
+
+Reference (``/root/reference/main.py:52-98``): load the prompt pickle, split
+it into ``--num_batch`` contiguous batches, run every batch through the
+sharded model on all GPUs (threads; DP = ``np.array_split`` of prompts, MP =
+the same list on every GPU), then ``--num_gen_token`` times extend every
+suffix with the greedy argmax token (re-running the whole model each time),
+and finally dump ``<prompts>_updated.pkl`` and the score list.
+
+Here >1 GPU means >1 process (spawned by :func:`main` or launched by
+``torchrun``), RCCL between them, and every rank runs the same loop; rank 0
+owns the file I/O.
+"""
+from __future__ import annotations
+
+import copy
+import json
+import os
+import pickle
+import socket
+import sys
+import time
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from .config import ModelConfig
+from .engine import ShardedRunner
+from .parallel.comm import Comm
+from .parallel.planner import make_plan
+from .runtime.weights import FileLayerSource, HostStore
+from .utils.cli import parse_args
+from .utils.tokenizer import load_tokenizer
+
+
+def batch_ranges(n: int, num_batch: int):
+    """main.py:19-20 (contiguous batches; the last one takes the remainder)."""
+    ends = [n // num_batch * i for i in range(1, num_batch)] + [n]
+    return list(zip([0] + ends[:-1], ends))
+
+
+def build_source(args, cfg: ModelConfig, comm: Comm, device: torch.device):
+    src = FileLayerSource(cfg, args.model_path)
+    if args.weight_cache == "disk":
+        return src
+    names = cfg.layer_names()
+    plan = make_plan(len(names), args.layer_num_per_shard, comm.world, comm.rank, args.data_parallel)
+    mine = sorted({i for sh in plan.my_shards for i in sh})
+    return HostStore.from_source(src, pinned=device.type == "cuda", names=[names[i] for i in mine])
+
+
+def build_runner(args, cfg: ModelConfig, device, comm: Comm, tok) -> ShardedRunner:
+    device = torch.device(device)
+    if args.data_parallel and comm.world > 1 and args.dp_weight_shard and device.type == "cuda":
+        from .parallel.data_parallel import build_dp_sharded_runner
+        return build_dp_sharded_runner(args, cfg, device, comm, tok)
+    src = build_source(args, cfg, comm, device)
+    act = None
+    if args.dtype:
+        act = torch.float16 if args.dtype == "float16" else torch.float32
+    return ShardedRunner(cfg, src, device, tok, layer_num_per_shard=args.layer_num_per_shard,
+                         storage_location=args.storage_location, disk_folder=args.disk_folder,
+                         max_activation_in_cpu=args.max_activation_in_cpu,
+                         prefix_attention=args.prefix_attention, token_budget=args.token_budget,
+                         resident=args.resident, comm=comm, data_parallel=args.data_parallel,
+                         act_dtype=act, verbose=args.verbose)
+
+
+def run_all(args, runner: ShardedRunner, comm: Comm, prompts: Sequence) -> List[np.ndarray]:
+    """One full pass over ``prompts`` on every rank; returns the ordered score list on rank 0."""
+    if args.data_parallel and comm.world > 1:
+        idx = np.array_split(np.arange(len(prompts)), comm.world)[comm.rank]
+        mine = [prompts[i] for i in idx]
+    else:
+        mine = list(prompts)
+    outs: List[np.ndarray] = []
+    for b0, b1 in batch_ranges(len(mine), args.num_batch):
+        if b1 > b0:
+            outs += runner(mine[b0:b1])
+    if comm.world == 1:
+        return outs
+    allv = comm.gather_object(outs, dst=0)
+    if comm.rank != 0:
+        return []
+    if args.data_parallel:
+        return sum(allv, [])
+    # model parallel: the rank owning lm_head holds every score
+    for v in allv:
+        if v and all(x is not None for x in v):
+            return v
+    raise RuntimeError("no rank produced scores")
+
+
+def generation_loop(args, runner, comm: Comm, tok, original_prompts: Sequence):
+    """main.py:63-90 — greedy extension of every suffix, full re-run per step."""
+    input_prompts = copy.deepcopy(list(original_prompts))
+    output_scores: List[np.ndarray] = []
+    for i_new in range(args.num_gen_token):
+        outputs = run_all(args, runner, comm, input_prompts)
+        if comm.rank == 0:
+            if i_new == 0:
+                output_scores = outputs
+            else:
+                output_scores = [np.concatenate((old, new), axis=1) for old, new in zip(output_scores, outputs)]
+            for pi in range(len(input_prompts)):
+                prefix, suffix = original_prompts[pi]
+                new_tokens = np.argmax(output_scores[pi], axis=-1)
+                new_suffix = tuple(s + tok.decode(t) for s, t in zip(suffix, new_tokens))
+                input_prompts[pi] = (prefix, new_suffix)
+        if comm.world > 1:
+            input_prompts = comm.broadcast_object(input_prompts, src=0)
+    return output_scores, input_prompts
+
+
+def _device_for(args, comm: Comm) -> torch.device:
+    if comm.world > 1:
+        return comm.device
+    n = torch.cuda.device_count() if args.num_gpus is None else args.num_gpus
+    return torch.device("cuda", 0) if n > 0 and torch.cuda.is_available() else torch.device("cpu")
+
+
+def run_rank(args, comm: Comm) -> Optional[dict]:
+    device = _device_for(args, comm)
+    if args.storage_location == "disk":
+        os.makedirs(args.disk_folder, exist_ok=True)
+    with open(args.prompt_pickle, "rb") as f:
+        original = pickle.load(f)      # the user's own prompt file (reference format)
+    cfg = ModelConfig.from_pretrained(args.model_path)
+    tok = load_tokenizer(args.model_path)
+    t0 = time.perf_counter()
+    runner = build_runner(args, cfg, device, comm, tok)
+    t_build = time.perf_counter() - t0
+    t1 = time.perf_counter()
+    scores, updated = generation_loop(args, runner, comm, tok, original)
+    t_run = time.perf_counter() - t1
+    tokens = comm.all_reduce_sum(runner.stats.get("tokens", 0.0)) if not (
+        comm.world > 1 and not args.data_parallel) else runner.stats.get("tokens", 0.0)
+    metrics = {"device": str(device), "world": comm.world, "build_s": t_build, "run_s": t_run,
+               "tokens_last_pass": tokens, "stats": runner.stats}
+    if device.type == "cuda":
+        metrics["peak_hbm_bytes"] = torch.cuda.max_memory_allocated(device)
+    if comm.rank == 0:
+        if args.data_parallel and comm.world > 1:
+            updated = np.array(updated, dtype=object)   # reference quirk: main.py:69 makes it an ndarray
+        with open(args.prompt_pickle.replace(".pkl", "_updated.pkl"), "wb") as f:
+            pickle.dump(updated, f)
+        with open(args.output_file, "wb") as f:
+            pickle.dump(scores, f)
+        if args.verbose:
+            print(json.dumps(metrics, default=float))
+        if args.metrics_json:
+            with open(args.metrics_json, "w") as f:
+                json.dump(metrics, f, default=float, indent=1)
+    runner.close()
+    return metrics
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _spawn_worker(local_rank: int, world: int, port: int, argv: List[str]):
+    os.environ.update({"RANK": str(local_rank), "LOCAL_RANK": str(local_rank), "WORLD_SIZE": str(world),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    args = parse_args(argv)
+    comm = Comm.from_env("cuda")
+    try:
+        run_rank(args, comm)
+    finally:
+        comm.destroy()
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse_args(argv)
+    print(args)
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) > 1:
+        comm = Comm.from_env("cuda" if torch.cuda.device_count() > 0 else "cpu")
+        try:
+            run_rank(args, comm)
+        finally:
+            comm.destroy()
+        return 0
+    n = torch.cuda.device_count() if args.num_gpus is None else args.num_gpus
+    if n > 1:
+        import torch.multiprocessing as mp
+        port = _free_port()
+        mp.start_processes(_spawn_worker, args=(n, port, argv), nprocs=n, start_method="spawn", join=True)
+        return 0
+    run_rank(args, Comm(0, 1))
+    return 0

@@ -1,0 +1,153 @@
+"""Model configuration (Llama family) read from an HF ``config.json``.
+
+The reference builds the model shell from ``AutoConfig.from_pretrained``
+(``/root/reference/utils.py:101``) and instantiates HF ``LlamaForCausalLM`` on
+the meta device (``utils.py:111-113``).  We only need the architecture
+numbers: the model itself is our own packed-weight implementation.
+"""
+from __future__ import annotations
+
+import json
+import os
+from dataclasses import asdict, dataclass, field
+from typing import Optional
+
+# Reference hard-codes the maximum sequence length (utils.py:14).
+MAX_TOKEN_LEN = 4096
+
+
+@dataclass
+class ModelConfig:
+    hidden_size: int = 4096
+    intermediate_size: int = 11008
+    num_attention_heads: int = 32
+    num_key_value_heads: int = 32
+    num_hidden_layers: int = 32
+    vocab_size: int = 32000
+    rms_norm_eps: float = 1e-5
+    rope_theta: float = 10000.0
+    max_position_embeddings: int = 4096
+    tie_word_embeddings: bool = False
+    bos_token_id: int = 1
+    eos_token_id: int = 2
+    torch_dtype: str = "float16"
+    model_type: str = "llama"
+    architectures: list = field(default_factory=lambda: ["LlamaForCausalLM"])
+
+    # ------------------------------------------------------------------ derived
+    @property
+    def head_dim(self) -> int:
+        return self.hidden_size // self.num_attention_heads
+
+    @property
+    def q_size(self) -> int:
+        return self.num_attention_heads * self.head_dim
+
+    @property
+    def kv_size(self) -> int:
+        return self.num_key_value_heads * self.head_dim
+
+    @property
+    def qkv_size(self) -> int:
+        return self.q_size + 2 * self.kv_size
+
+    @property
+    def num_layers_total(self) -> int:
+        """embed + decoder layers + final norm + lm_head (reference utils.py:106-107)."""
+        return self.num_hidden_layers + 3
+
+    def layer_names(self) -> list:
+        """Ordered layer list, identical to ``ShardedLlama.layer_names`` (utils.py:106-107)."""
+        return (["model.embed_tokens"]
+                + [f"model.layers.{i}" for i in range(self.num_hidden_layers)]
+                + ["model.norm", "lm_head"])
+
+    def decoder_layer_params(self) -> int:
+        h, i = self.hidden_size, self.intermediate_size
+        return h * self.qkv_size + h * h + 3 * h * i + 2 * h
+
+    def total_params(self) -> int:
+        emb = self.vocab_size * self.hidden_size
+        head = 0 if self.tie_word_embeddings else emb
+        return emb + head + self.hidden_size + self.num_hidden_layers * self.decoder_layer_params()
+
+    def validate(self) -> None:
+        if self.hidden_size % self.num_attention_heads:
+            raise ValueError("hidden_size must be divisible by num_attention_heads")
+        if self.num_attention_heads % self.num_key_value_heads:
+            raise ValueError("num_attention_heads must be a multiple of num_key_value_heads")
+        if self.head_dim % 32:
+            raise ValueError("head_dim must be a multiple of 32 (RoPE pair blocks of 16)")
+
+    # ---------------------------------------------------------------------- io
+    @classmethod
+    def from_dict(cls, d: dict) -> "ModelConfig":
+        kw = {}
+        for f in cls.__dataclass_fields__:
+            if f in d and d[f] is not None:
+                kw[f] = d[f]
+        if "num_key_value_heads" not in d or d.get("num_key_value_heads") is None:
+            kw["num_key_value_heads"] = d.get("num_attention_heads", cls.num_attention_heads)
+        rs = d.get("rope_scaling")
+        if rs:
+            raise NotImplementedError(f"rope_scaling={rs} is not supported (Llama-2 has none)")
+        if isinstance(kw.get("eos_token_id"), list):
+            kw["eos_token_id"] = kw["eos_token_id"][0]
+        cfg = cls(**kw)
+        cfg.validate()
+        return cfg
+
+    @classmethod
+    def from_pretrained(cls, model_path: str) -> "ModelConfig":
+        with open(os.path.join(model_path, "config.json")) as f:
+            return cls.from_dict(json.load(f))
+
+    def to_dict(self) -> dict:
+        d = asdict(self)
+        d["head_dim"] = self.head_dim
+        return d
+
+    def save(self, model_path: str) -> None:
+        os.makedirs(model_path, exist_ok=True)
+        d = asdict(self)
+        with open(os.path.join(model_path, "config.json"), "w") as f:
+            json.dump(d, f, indent=2)
+
+
+# Standard HF configs (computed sizes in SURVEY.md §2.3).
+PRESETS = {
+    "llama2-7b": dict(hidden_size=4096, intermediate_size=11008, num_attention_heads=32,
+                      num_key_value_heads=32, num_hidden_layers=32),
+    "llama2-13b": dict(hidden_size=5120, intermediate_size=13824, num_attention_heads=40,
+                       num_key_value_heads=40, num_hidden_layers=40),
+    "llama2-70b": dict(hidden_size=8192, intermediate_size=28672, num_attention_heads=64,
+                       num_key_value_heads=8, num_hidden_layers=80),
+    # tiny configs for tests (GQA 2:1, head_dim 64)
+    "tiny": dict(hidden_size=256, intermediate_size=512, num_attention_heads=4,
+                 num_key_value_heads=2, num_hidden_layers=2, vocab_size=512,
+                 max_position_embeddings=4096),
+    "small": dict(hidden_size=1024, intermediate_size=2816, num_attention_heads=8,
+                  num_key_value_heads=2, num_hidden_layers=4, vocab_size=32000),
+}
+
+
+def preset(name: str, **overrides) -> ModelConfig:
+    if name not in PRESETS:
+        raise KeyError(f"unknown preset {name!r}; choose from {sorted(PRESETS)}")
+    d = dict(PRESETS[name])
+    d.update(overrides)
+    cfg = ModelConfig(**d)
+    cfg.validate()
+    return cfg
+
+
+def resolve_dtype(name: Optional[str]):
+    import torch
+    table = {"float16": torch.float16, "fp16": torch.float16, "half": torch.float16,
+             "bfloat16": torch.bfloat16, "bf16": torch.bfloat16,
+             "float32": torch.float32, "fp32": torch.float32}
+    if name is None:
+        return torch.float16
+    if name not in table:
+        raise ValueError(f"unsupported dtype {name}")
+    return table[name]

@@ -1,0 +1,213 @@
+"""ShardedRunner — the shard-streaming executor (capability of ``ShardedLlama``).
+
+Reference hot loop (``/root/reference/utils.py:223-305``)::
+
+    for shard in model_shards:                 # weights: load (blocking) ... unload
+        for prompt in prompts:                 # one prompt at a time
+            for layer in shard: fetch | compute | store
+
+MI355X design of the same schedule:
+
+* weights of shard k+1 stream into the second HBM slot on a copy stream while
+  shard k computes (:class:`~.runtime.prefetch.ShardPrefetcher`);
+* prompts are packed into micro-batches of up to ``token_budget`` tokens so
+  each projection is one large MFMA GEMM (:mod:`.runtime.batch`);
+* activations between shards go through the async
+  :class:`~.runtime.activations.ActivationStore` (gpu / cpu / disk), the next
+  micro-batch's H2D overlapping the current one's compute;
+* model parallel (reference default for >1 GPU): shard k runs on rank
+  k mod G exactly like ``utils.py:151-153``; hand-offs between ranks are
+  RCCL ``isend``/``irecv`` over xGMI with every receive posted at shard start
+  (no polling, no shared state), keyed by micro-batch.
+* data parallel: each rank runs all shards on its slice of prompts; weights
+  can be scatter-loaded 1/G per rank and all-gathered over xGMI
+  (:mod:`.parallel.data_parallel`).
+"""
+from __future__ import annotations
+
+import time
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from .config import MAX_TOKEN_LEN, ModelConfig
+from .models.layout import layer_kind
+from .models.llama import ExecContext, layer_flops, rope_tables, run_layer
+from .ops import get_ops
+from .parallel.comm import Comm
+from .parallel.planner import ShardPlan, make_plan
+from .runtime.activations import ActivationStore
+from .runtime.batch import PackedBatch, pack_prompts, split_microbatches
+from .runtime.prefetch import ShardPrefetcher
+from .runtime.weights import LayerSource
+from .utils.tokenizer import TokenizedPrompt, tokenize_prompts
+
+
+class ShardedRunner:
+    def __init__(self, cfg: ModelConfig, source: LayerSource, device="cpu", tokenizer=None,
+                 layer_num_per_shard: int = 1, storage_location: str = "cpu",
+                 disk_folder: str = "./temp", max_activation_in_cpu: int = 100,
+                 prefix_attention: str = "bidirectional", token_budget: int = 16384,
+                 resident: bool = False, comm: Optional[Comm] = None, data_parallel: bool = False,
+                 act_dtype: Optional[torch.dtype] = None, n_slots: int = 2,
+                 mlp_chunk: int = 16384, prefetcher: Optional[ShardPrefetcher] = None,
+                 verbose: bool = False):
+        self.cfg = cfg
+        self.src = source
+        self.dev = torch.device(device)
+        self.cuda = self.dev.type == "cuda"
+        self.tok = tokenizer
+        self.lnps = layer_num_per_shard
+        self.storage = storage_location
+        self.disk_folder = disk_folder
+        self.max_act = max_activation_in_cpu
+        self.prefix_attention = prefix_attention
+        self.token_budget = token_budget
+        self.comm = comm or Comm(0, 1, self.dev)
+        self.data_parallel = data_parallel
+        self.verbose = verbose
+        self.names = cfg.layer_names()
+        self.L = len(self.names)
+        self.plan: ShardPlan = make_plan(self.L, layer_num_per_shard, self.comm.world, self.comm.rank,
+                                         data_parallel)
+        self.act_dtype = act_dtype or (torch.float16 if self.cuda else torch.float32)
+        self.ops = get_ops(self.dev)
+        cos, sin = rope_tables(cfg, max(cfg.max_position_embeddings, MAX_TOKEN_LEN),
+                               torch.float16, self.dev)
+        self.ctx = ExecContext(cfg, self.ops, self.dev, self.act_dtype, cos, sin, mlp_chunk)
+        my = [s for s in self.plan.my_shards if len(s)]
+        self.my_shards = my
+        self.prefetcher = prefetcher or ShardPrefetcher(source, self.names, my, self.dev,
+                                                        n_slots=n_slots, resident=resident)
+        self.stats: Dict[str, float] = {}
+        self.h2d_stream = torch.cuda.Stream(self.dev) if self.cuda else None
+        self.d2h_stream = torch.cuda.Stream(self.dev) if self.cuda else None
+
+    # ----------------------------------------------------------- helpers
+    def tokenize(self, prompts) -> List[TokenizedPrompt]:
+        if self.tok is None:
+            raise RuntimeError("no tokenizer")
+        return tokenize_prompts(self.tok, prompts, MAX_TOKEN_LEN)
+
+    def _owner(self, layer_idx: int) -> int:
+        return self.plan.owner_of_layer(layer_idx)
+
+    def _state_shape(self, layer_idx: int, batch: PackedBatch):
+        """Shape of the activation produced by ``layer_idx`` (utils.py:281-286)."""
+        kind = layer_kind(self.names[layer_idx])
+        if kind in ("embed", "decoder"):
+            return (batch.num_tokens, self.cfg.hidden_size)
+        if kind == "norm":
+            return (batch.n_scored, self.cfg.hidden_size)
+        return (batch.n_scored, self.cfg.vocab_size)
+
+    # ------------------------------------------------------------- main
+    def __call__(self, prompts) -> List[np.ndarray]:
+        """Reference API: list of (prefix, suffixes) -> list of [n_s, 1, V] fp16 arrays."""
+        return self.run_tokenized(self.tokenize(prompts))
+
+    def run_tokenized(self, tps: Sequence[TokenizedPrompt]) -> List[Optional[np.ndarray]]:
+        t_start = time.perf_counter()
+        n = len(tps)
+        groups = split_microbatches(tps, self.token_budget)
+        batches = [pack_prompts([tps[i] for i in g], g, self.prefix_attention) for g in groups]
+        store = ActivationStore(self.storage, self.dev, self.disk_folder,
+                                tag=str(self.comm.rank) if self.comm.world > 1 else "",
+                                h2d_stream=self.h2d_stream, d2h_stream=self.d2h_stream)
+        outputs: List[Optional[np.ndarray]] = [None] * n
+        out_pending = []     # (batch, host tensor, event)
+        comm = self.comm
+        mp = self.plan.mode == "mp"
+        pf = self.prefetcher
+        flops = 0.0
+        compute_s = 0.0
+        sends = []
+        if self.my_shards:
+            pf.prefetch(0)
+        for k, shard in enumerate(self.my_shards):
+            W = pf.acquire(k)
+            pf.prefetch(k + 1)
+            first, last = shard[0], shard[-1]
+            src_rank = self._owner(first - 1) if (mp and first > 0) else comm.rank
+            dst_rank = self._owner(last + 1) if (mp and last + 1 < self.L) else comm.rank
+            recvs = {}
+            if first > 0 and src_rank != comm.rank:
+                # post every receive of this shard up front (matches the sender's order)
+                for b, batch in enumerate(batches):
+                    buf = torch.empty(self._state_shape(first - 1, batch), dtype=self.act_dtype, device=self.dev)
+                    recvs[b] = (buf, comm.irecv(buf, src_rank))
+            for b, batch in enumerate(batches):
+                meta = batch.device_tensors(self.dev)
+                if first == 0:
+                    state = None
+                elif b in recvs:
+                    buf, work = recvs.pop(b)
+                    work.wait()
+                    state = buf
+                else:
+                    state = store.get(b)
+                    if b + 1 < len(batches):
+                        store.prefetch(b + 1)
+                tc = time.perf_counter()
+                for li in shard:
+                    name = self.names[li]
+                    state = run_layer(self.ctx, name, W[name], state, batch, meta)
+                    if layer_kind(name) == "decoder":
+                        flops += layer_flops(self.cfg, batch)
+                compute_s += time.perf_counter() - tc
+                if last == self.L - 1:
+                    out_pending.append(self._start_output_copy(batch, state))
+                elif dst_rank != comm.rank:
+                    st = state.contiguous()
+                    sends.append((st, comm.isend(st, dst_rank)))
+                else:
+                    store.put(b, state)
+                    if b == 0 and len(batches) > 1 and first != 0:
+                        pass
+                del state
+            if recvs:
+                raise RuntimeError("unconsumed receives")
+            pf.release(k)
+            # retire finished sends to bound memory
+            sends = [(t, w) for (t, w) in sends if not w.is_completed()]
+        for t, w in sends:
+            w.wait()
+        if self.cuda:
+            torch.cuda.synchronize(self.dev)
+        for batch, host, ev in out_pending:
+            probs = host.numpy() if host.dtype != torch.bfloat16 else host.float().numpy()
+            r = 0
+            for j, pid in enumerate(batch.prompt_ids):
+                ns = batch.n_suffix[j]
+                outputs[pid] = np.expand_dims(probs[r:r + ns].astype(np.float16, copy=True), axis=1)
+                r += ns
+        store.close()
+        wall = time.perf_counter() - t_start
+        self.stats = {
+            "wall_s": wall, "compute_launch_s": compute_s,
+            "tokens": float(sum(b.num_tokens for b in batches)),
+            "padded_tokens": float(sum(b.padded_tokens for b in batches)),
+            "decoder_flops": flops, "micro_batches": float(len(batches)),
+            "weight_wait_s": pf.wait_seconds, "weight_h2d_bytes": float(pf.bytes_h2d),
+            "act_d2h_bytes": float(store.bytes_d2h), "act_h2d_bytes": float(store.bytes_h2d),
+        }
+        if self.verbose:
+            print(f"{self.dev} rank{comm.rank}: {len(self.my_shards)} shards, {len(batches)} micro-batches, "
+                  f"{self.stats['tokens']:.0f} tokens in {wall:.2f}s")
+        return outputs
+
+    def _start_output_copy(self, batch: PackedBatch, probs: torch.Tensor):
+        if not self.cuda:
+            return batch, probs.detach().to(torch.float16).cpu(), None
+        host = torch.empty(probs.shape, dtype=probs.dtype, pin_memory=True)
+        self.d2h_stream.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(self.d2h_stream):
+            host.copy_(probs, non_blocking=True)
+            probs.record_stream(self.d2h_stream)
+            ev = torch.cuda.Event()
+            ev.record(self.d2h_stream)
+        return batch, host, ev
+
+    def close(self):
+        self.prefetcher.close()

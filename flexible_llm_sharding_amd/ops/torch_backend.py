@@ -1,0 +1,134 @@
+"""Plain-PyTorch implementation of every op (CPU path + numerics oracle).
+
+Semantics follow the HF Llama block the reference drives
+(``/root/reference/utils.py:266-290``): RMSNorm with fp32
+statistics, RoPE rotate-half with fp16-rounded cos/sin tables, softmax in
+fp32, SwiGLU MLP.  Activations use the packed-weight conventions of
+:mod:`..models.layout` (RoPE-pair-permuted q/k head dims, 16-row gate/up
+interleave) so this backend is a drop-in oracle for the HIP kernels.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from ..models.layout import PAIR_BLOCK
+
+
+class TorchOps:
+    name = "torch"
+
+    def __init__(self, compute_dtype: torch.dtype = torch.float32):
+        self.cdt = compute_dtype
+
+    # ---------------------------------------------------------------- helpers
+    def _c(self, t: torch.Tensor) -> torch.Tensor:
+        return t if t.dtype == self.cdt else t.to(self.cdt)
+
+    # ------------------------------------------------------------------- ops
+    def embed(self, ids: torch.Tensor, table: torch.Tensor, out_dtype) -> torch.Tensor:
+        return table.index_select(0, ids.long()).to(out_dtype)
+
+    def rmsnorm(self, x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
+        # LlamaRMSNorm: fp32 variance, normalise, cast back, scale by weight.
+        xf = x.float()
+        var = xf.pow(2).mean(-1, keepdim=True)
+        y = (xf * torch.rsqrt(var + eps)).to(x.dtype)
+        return (self._c(w) * self._c(y)).to(x.dtype)
+
+    def linear(self, x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+        return (self._c(x) @ self._c(w).t()).to(x.dtype)
+
+    def linear_residual(self, x: torch.Tensor, w: torch.Tensor, resid: torch.Tensor) -> torch.Tensor:
+        y = self._c(x) @ self._c(w).t()
+        return (self._c(resid) + y).to(resid.dtype)
+
+    def swiglu_up(self, x: torch.Tensor, wgu: torch.Tensor) -> torch.Tensor:
+        y = self._c(x) @ self._c(wgu).t()                     # [T, 2I] interleaved
+        T, I2 = y.shape
+        y = y.view(T, I2 // (2 * PAIR_BLOCK), 2, PAIR_BLOCK)
+        g, u = y[:, :, 0, :], y[:, :, 1, :]
+        return (F.silu(g) * u).reshape(T, I2 // 2).to(x.dtype)
+
+    def qkv_rope(self, x: torch.Tensor, wqkv: torch.Tensor, positions: torch.Tensor,
+                 cos: torch.Tensor, sin: torch.Tensor, n_q_heads: int, n_kv_heads: int,
+                 head_dim: int) -> torch.Tensor:
+        y = self._c(x) @ self._c(wqkv).t()
+        qk_cols = (n_q_heads + n_kv_heads) * head_dim
+        T = y.shape[0]
+        qk = y[:, :qk_cols].reshape(T, n_q_heads + n_kv_heads, head_dim // (2 * PAIR_BLOCK), 2, PAIR_BLOCK)
+        c = cos.index_select(0, positions.long()).to(self.cdt)   # [T, hd/2]
+        s = sin.index_select(0, positions.long()).to(self.cdt)
+        c = c.reshape(T, 1, head_dim // (2 * PAIR_BLOCK), PAIR_BLOCK)
+        s = s.reshape(T, 1, head_dim // (2 * PAIR_BLOCK), PAIR_BLOCK)
+        x1, x2 = qk[:, :, :, 0, :], qk[:, :, :, 1, :]
+        o1 = x1 * c - x2 * s
+        o2 = x2 * c + x1 * s
+        qk_out = torch.stack([o1, o2], dim=3).reshape(T, qk_cols)
+        return torch.cat([qk_out, y[:, qk_cols:]], dim=1).to(x.dtype)
+
+    def attention(self, qkv: torch.Tensor, segments, n_q_heads: int, n_kv_heads: int,
+                  head_dim: int) -> torch.Tensor:
+        """Shared-prefix attention over packed segments (see runtime.batch)."""
+        T = qkv.shape[0]
+        qs = n_q_heads * head_dim
+        ks = n_kv_heads * head_dim
+        q_all = qkv[:, :qs].view(T, n_q_heads, head_dim)
+        k_all = qkv[:, qs:qs + ks].view(T, n_kv_heads, head_dim)
+        v_all = qkv[:, qs + ks:qs + 2 * ks].view(T, n_kv_heads, head_dim)
+        out = torch.empty(T, qs, dtype=qkv.dtype, device=qkv.device)
+        rep = n_q_heads // n_kv_heads
+        scale = head_dim ** -0.5
+        dev = qkv.device
+        for sg in segments:
+            q = self._c(q_all[sg.q_start:sg.q_start + sg.q_len])                # [q, nh, d]
+            kr = [(sg.r0_start, sg.r0_len, sg.r0_causal)]
+            if sg.r1_len:
+                kr.append((sg.r1_start, sg.r1_len, 1))
+            ks_, vs_, masks = [], [], []
+            qi = torch.arange(sg.q_len, device=dev)
+            for st, ln, causal in kr:
+                ks_.append(k_all[st:st + ln])
+                vs_.append(v_all[st:st + ln])
+                kj = torch.arange(ln, device=dev)
+                m = torch.ones(sg.q_len, ln, dtype=torch.bool, device=dev)
+                if causal:
+                    m = kj[None, :] <= qi[:, None]
+                masks.append(m)
+            k = self._c(torch.cat(ks_, 0)).repeat_interleave(rep, dim=1)        # [k, nh, d]
+            v = self._c(torch.cat(vs_, 0)).repeat_interleave(rep, dim=1)
+            mask = torch.cat(masks, 1)                                          # [q, k]
+            s = torch.einsum("qhd,khd->hqk", q.float(), k.float()) * scale
+            s = s.masked_fill(~mask[None], float("-inf"))
+            p = torch.softmax(s, dim=-1)
+            o = torch.einsum("hqk,khd->qhd", p, v.float())
+            out[sg.q_start:sg.q_start + sg.q_len] = o.reshape(sg.q_len, qs).to(qkv.dtype)
+        return out
+
+    def gather_rmsnorm(self, x: torch.Tensor, idx: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
+        return self.rmsnorm(x.index_select(0, idx.long()), w, eps)
+
+    def lm_head_softmax(self, h: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+        logits = (self._c(h) @ self._c(w).t()).to(h.dtype)   # fp16 logits like nn.Linear in fp16
+        return torch.softmax(logits.float(), dim=-1).to(torch.float16)
+
+    def synchronize(self):
+        pass
+
+    # ------------------------------------------------------- synthetic init
+    def fill_layer_random(self, buf: torch.Tensor, layout, seed: int, std: float = 0.02) -> None:
+        """Random-init one packed layer in place (norm weights ~ 1, embeddings ~ N(0,1))."""
+        g = torch.Generator(device=buf.device).manual_seed(int(seed))
+        views = layout.views(buf, torch.float16)
+        for name, v in views.items():
+            mean, sd = fill_params(name, std)
+            v.copy_(torch.randn(v.shape, generator=g, device=buf.device) * sd + mean)
+
+
+def fill_params(slot_name: str, std: float):
+    """(mean, std) of the synthetic distribution of a packed slot."""
+    if slot_name in ("ln1", "ln2", "norm"):
+        return 1.0, 0.1
+    if slot_name == "embed":
+        return 0.0, 1.0
+    return 0.0, std

@@ -1,0 +1,113 @@
+"""Process-per-GPU communication over ``torch.distributed``.
+
+The reference has no collectives library: GPUs are threads of one process
+that exchange activations through a shared Python dict with 1-second
+sleep-polling (``/root/reference/utils.py:159-213``) and share weights through
+a host-RAM cache guarded by a Condition/Lock pair (``utils.py:24-75``; ABBA
+lock order).
+
+Here each GPU is its own process.  On ROCm the ``"nccl"`` backend *is* RCCL,
+so pipeline hand-offs are point-to-point ``isend``/``irecv`` over xGMI, the
+data-parallel weight fan-out is ``all_gather_into_tensor`` and results are
+gathered to rank 0.  On CPU (tests) the same code runs over ``gloo``.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+import pickle
+from typing import Any, List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+class Comm:
+    """Thin wrapper; ``world == 1`` works without an initialised process group."""
+
+    def __init__(self, rank: int = 0, world: int = 1, device=None, backend: Optional[str] = None):
+        self.rank, self.world = rank, world
+        self.device = torch.device(device) if device is not None else torch.device("cpu")
+        self.backend = backend
+
+    @property
+    def active(self) -> bool:
+        return self.world > 1
+
+    # ------------------------------------------------------------ factory
+    @classmethod
+    def from_env(cls, device_type: str = "cuda", timeout_s: int = 1800) -> "Comm":
+        """Initialise from RANK/WORLD_SIZE/MASTER_ADDR/MASTER_PORT (torchrun)."""
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", str(rank)))
+        if device_type == "cuda":
+            dev = torch.device("cuda", local)
+            torch.cuda.set_device(dev)
+        else:
+            dev = torch.device("cpu")
+        if world <= 1:
+            return cls(0, 1, dev)
+        backend = "nccl" if device_type == "cuda" else "gloo"
+        if not dist.is_initialized():
+            kw = dict(backend=backend, rank=rank, world_size=world,
+                      timeout=datetime.timedelta(seconds=timeout_s))
+            if backend == "nccl":
+                kw["device_id"] = dev
+            dist.init_process_group(**kw)
+        return cls(rank, world, dev, backend)
+
+    # -------------------------------------------------------------- p2p
+    def isend(self, t: torch.Tensor, dst: int):
+        return dist.isend(t, dst)
+
+    def irecv(self, t: torch.Tensor, src: int):
+        return dist.irecv(t, src)
+
+    # -------------------------------------------------------- collectives
+    def barrier(self):
+        if self.active:
+            if self.backend == "nccl":
+                dist.barrier(device_ids=[self.device.index])
+            else:
+                dist.barrier()
+
+    def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False):
+        return dist.all_gather_into_tensor(out, inp, async_op=async_op)
+
+    def all_reduce_max(self, x: float) -> float:
+        if not self.active:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=self.device if self.backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def all_reduce_sum(self, x: float) -> float:
+        if not self.active:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=self.device if self.backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return float(t.item())
+
+    def broadcast_object(self, obj: Any, src: int = 0) -> Any:
+        if not self.active:
+            return obj
+        lst = [obj if self.rank == src else None]
+        dist.broadcast_object_list(lst, src=src, device=self.device if self.backend == "nccl" else None)
+        return lst[0]
+
+    def gather_object(self, obj: Any, dst: int = 0) -> Optional[List[Any]]:
+        if not self.active:
+            return [obj]
+        out = [None] * self.world if self.rank == dst else None
+        if self.backend == "nccl":
+            # gather_object over NCCL needs device tensors; use all_gather_object for simplicity
+            allv = [None] * self.world
+            dist.all_gather_object(allv, obj)
+            return allv if self.rank == dst else None
+        dist.gather_object(obj, out, dst=dst)
+        return out
+
+    def destroy(self):
+        if self.active and dist.is_initialized():
+            dist.destroy_process_group()

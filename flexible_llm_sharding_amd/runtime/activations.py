@@ -1,0 +1,250 @@
+"""Activation store between shards: ``--storage_location gpu | cpu | disk``.
+
+Reference (``/root/reference/utils.py:159-213``): after the last layer of a
+shard each prompt's (prefix, suffix) hidden states are kept on the GPU, moved
+to host RAM with a blocking ``.cpu()``, or ``np.save``d; they are fetched back
+with blocking ``.to(device)`` / ``np.load`` before the next shard.
+
+Here the store keys whole micro-batches and reuses the copy engine:
+
+* ``gpu``  — the device tensor stays in HBM;
+* ``cpu``  — async D2H into a per-key pinned buffer on a dedicated D2H stream
+  (event-fenced, ``record_stream`` keeps the source alive), and async H2D on
+  the H2D stream when prefetched for the next shard;
+* ``disk`` — the same D2H, then a writer thread stores an ``.npy`` file (raw
+  fp16 after a standard header) with the native ``pwrite`` engine; a reader
+  thread ``pread``s it back into pinned memory ahead of use.
+
+Pinned buffers are pooled by size so the steady state allocates nothing.
+"""
+from __future__ import annotations
+
+import os
+import threading
+from collections import defaultdict
+from concurrent.futures import Future, ThreadPoolExecutor
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from . import hostmem
+
+_NP_DT = {torch.float16: np.float16, torch.float32: np.float32, torch.bfloat16: None}
+
+
+def _npy_header(shape, dtype: torch.dtype) -> bytes:
+    """Standard .npy v1.0 header (magic + dict), so spills are np.load-able."""
+    import io
+    npdt = _NP_DT.get(dtype)
+    descr = np.lib.format.dtype_to_descr(np.dtype(npdt)) if npdt is not None else "<u2"
+    bio = io.BytesIO()
+    np.lib.format.write_array_header_1_0(bio, {"descr": descr, "fortran_order": False,
+                                               "shape": tuple(shape)})
+    return bio.getvalue()
+
+
+class _Entry:
+    __slots__ = ("dev", "host", "event", "shape", "dtype", "path", "write_fut")
+
+    def __init__(self):
+        self.dev = self.host = self.event = self.path = self.write_fut = None
+        self.shape = None
+        self.dtype = None
+
+
+class ActivationStore:
+    def __init__(self, mode: str, device, disk_folder: str = "./temp", tag: str = "",
+                 h2d_stream=None, d2h_stream=None):
+        if mode not in ("gpu", "cpu", "disk"):
+            raise ValueError(f"storage_location must be gpu/cpu/disk, got {mode!r}")
+        self.mode = mode
+        self.dev = torch.device(device)
+        self.cuda = self.dev.type == "cuda"
+        self.disk_folder = disk_folder
+        self.tag = tag
+        if mode == "disk":
+            os.makedirs(disk_folder, exist_ok=True)
+        self.h2d = h2d_stream if h2d_stream is not None else (torch.cuda.Stream(self.dev) if self.cuda else None)
+        self.d2h = d2h_stream if d2h_stream is not None else (torch.cuda.Stream(self.dev) if self.cuda else None)
+        self._e: Dict[object, _Entry] = {}
+        self._pool: Dict[int, List[torch.Tensor]] = defaultdict(list)
+        self._io = ThreadPoolExecutor(2, thread_name_prefix="fls-spill") if mode == "disk" else None
+        self._inflight: Dict[object, Tuple[Future, None]] = {}
+        self._recycle: List[Tuple[torch.Tensor, torch.cuda.Event]] = []
+        self.bytes_d2h = 0
+        self.bytes_h2d = 0
+        self.lock = threading.Lock()
+
+    # ------------------------------------------------------------- pool
+    def _get_host(self, nbytes: int) -> torch.Tensor:
+        with self.lock:
+            keep = []
+            for h, ev in self._recycle:
+                if ev.query():
+                    self._pool[h.numel()].append(h)
+                else:
+                    keep.append((h, ev))
+            self._recycle = keep
+            lst = self._pool.get(nbytes)
+            if lst:
+                return lst.pop()
+        return hostmem.alloc_host(nbytes, pinned=self.cuda)
+
+    def _put_host(self, buf: torch.Tensor) -> None:
+        with self.lock:
+            self._pool[buf.numel()].append(buf)
+
+    def path_for(self, key) -> str:
+        return os.path.join(self.disk_folder, f"act{self.tag}-{int(key):05d}.npy")
+
+    def __len__(self):
+        return len(self._e)
+
+    def keys(self):
+        return list(self._e)
+
+    # -------------------------------------------------------------- put
+    def put(self, key, t: torch.Tensor) -> None:
+        old = self._e.pop(key, None)
+        if old is not None:
+            self._drop(old)
+        e = _Entry()
+        e.shape, e.dtype = tuple(t.shape), t.dtype
+        if self.mode == "gpu":
+            e.dev = t
+            self._e[key] = e
+            return
+        nbytes = t.numel() * t.element_size()
+        if not self.cuda:
+            if self.mode == "cpu":
+                e.host = t
+            else:
+                e.path = self.path_for(key)
+                self._write_npy(e.path, t.contiguous(), e.shape, e.dtype)
+            self._e[key] = e
+            return
+        host = self._get_host(nbytes)
+        cur = torch.cuda.current_stream(self.dev)
+        self.d2h.wait_stream(cur)
+        with torch.cuda.stream(self.d2h):
+            host.view(t.dtype).view(e.shape).copy_(t, non_blocking=True)
+            t.record_stream(self.d2h)
+            ev = torch.cuda.Event()
+            ev.record(self.d2h)
+        self.bytes_d2h += nbytes
+        e.host, e.event = host, ev
+        if self.mode == "disk":
+            e.path = self.path_for(key)
+
+            def _write(ent=e):
+                ent.event.synchronize()
+                self._write_npy(ent.path, ent.host.view(ent.dtype)[:int(np.prod(ent.shape))].view(ent.shape),
+                                ent.shape, ent.dtype)
+                self._put_host(ent.host)
+                ent.host = None
+            e.write_fut = self._io.submit(_write)
+        self._e[key] = e
+
+    def _write_npy(self, path: str, t: torch.Tensor, shape, dtype) -> None:
+        hdr = _npy_header(shape, dtype)
+        data = t.contiguous().view(-1).view(torch.uint8)
+        with open(path, "wb") as f:
+            f.write(hdr)
+        rt = None
+        from .. import _native
+        rt = _native.runtime_or_none()
+        if rt is not None:
+            r = rt.fls_pwrite_from(path.encode(), len(hdr), data.numel(), data.data_ptr(), 4, 0)
+            if r != data.numel():
+                raise IOError(f"spill write failed {path}: {r}")
+        else:
+            with open(path, "ab") as f:
+                f.write(data.numpy().tobytes())
+
+    def _read_npy_into(self, path: str, shape, dtype, dst: torch.Tensor) -> None:
+        with open(path, "rb") as f:
+            np.lib.format.read_magic(f)
+            np.lib.format.read_array_header_1_0(f)
+            off = f.tell()
+        n = int(np.prod(shape)) * torch.empty((), dtype=dtype).element_size()
+        hostmem.pread_into(path, off, n, dst)
+
+    # -------------------------------------------------------------- get
+    def prefetch(self, key) -> None:
+        """Start bringing ``key`` back to the device (no-op for gpu mode)."""
+        if self.mode == "gpu" or key in self._inflight or key not in self._e:
+            return
+        e = self._e[key]
+        if not self.cuda:
+            return
+        if self.mode == "disk":
+            def _read(ent=e):
+                if ent.write_fut is not None:
+                    ent.write_fut.result()
+                nbytes = int(np.prod(ent.shape)) * torch.empty((), dtype=ent.dtype).element_size()
+                host = self._get_host(nbytes)
+                self._read_npy_into(ent.path, ent.shape, ent.dtype, host)
+                return host
+            self._inflight[key] = (self._io.submit(_read), None)
+        else:
+            self._inflight[key] = (None, None)
+
+    def get(self, key, pop: bool = True) -> torch.Tensor:
+        e = self._e.pop(key) if pop else self._e[key]
+        if self.mode == "gpu":
+            return e.dev
+        if not self.cuda:
+            if self.mode == "cpu":
+                return e.host
+            arr = np.load(e.path)
+            t = torch.from_numpy(arr.view(np.uint16)).view(e.dtype) if e.dtype == torch.bfloat16 else torch.from_numpy(arr)
+            if pop:
+                os.remove(e.path)
+            return t
+        fut, _ = self._inflight.pop(key, (None, None))
+        if self.mode == "disk":
+            if fut is None:
+                self.prefetch(key)
+                fut, _ = self._inflight.pop(key)
+            host = fut.result()
+        else:
+            host = e.host
+        nbytes = int(np.prod(e.shape)) * torch.empty((), dtype=e.dtype).element_size()
+        out = torch.empty(e.shape, dtype=e.dtype, device=self.dev)
+        if e.event is not None:
+            self.h2d.wait_event(e.event)     # D2H finished before reading the host copy back
+        with torch.cuda.stream(self.h2d):
+            out.copy_(host[:nbytes].view(e.dtype).view(e.shape), non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self.h2d)
+        self.bytes_h2d += nbytes
+        torch.cuda.current_stream(self.dev).wait_event(ev)
+        out.record_stream(torch.cuda.current_stream(self.dev))
+        if pop:
+            # host buffer is reusable once the H2D has completed (checked lazily)
+            with self.lock:
+                self._recycle.append((host, ev))
+            if self.mode == "disk" and e.path and os.path.exists(e.path):
+                try:
+                    os.remove(e.path)
+                except OSError:
+                    pass
+        return out
+
+    def _drop(self, e: _Entry) -> None:
+        if e.write_fut is not None:
+            e.write_fut.result()
+        if e.host is not None and self.cuda:
+            if e.event is not None:
+                e.event.synchronize()
+            self._put_host(e.host)
+
+    def clear(self):
+        for k in list(self._e):
+            self._drop(self._e.pop(k))
+
+    def close(self):
+        self.clear()
+        if self._io is not None:
+            self._io.shutdown(wait=True)

@@ -1,0 +1,133 @@
+"""Packed micro-batches of (prefix, suffixes) prompts.
+
+The reference runs prompts one at a time through each layer: the prefix as a
+batch of 1 (``utils.py:272``) and the ``n_s`` right-padded suffixes as a batch
+against the prefix K/V expanded ``n_s`` times (``utils.py:274-279``).
+
+On MI355X we pack MANY prompts into one token matrix ``[T, H]`` so every
+projection is one large MFMA GEMM, and describe the attention structure with
+*work items* consumed by the shared-prefix flash-attention kernel:
+
+* prefix segment: queries = prefix tokens; keys = the prefix
+  (bidirectional — the reference's ``attention_mask=None`` on transformers
+  <= 4.35, SURVEY §A.4 — or causal);
+* suffix segment: queries = the suffix's real tokens at positions
+  ``Lp .. Lp+len-1`` (``utils.py:275``); keys = the whole prefix (shared, read
+  in place, never expanded) + the suffix itself causally (``utils.py:276``).
+
+Padding tokens after a suffix's scored position are never computed: under the
+causal mask they cannot influence it.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import List, Sequence
+
+import numpy as np
+import torch
+
+from ..utils.tokenizer import TokenizedPrompt
+
+Q_BLOCK = 64            # query rows per attention work item (kernel tile)
+WORK_ITEM_FIELDS = 8    # q_start q_len q_off r0_start r0_len r0_causal r1_start r1_len
+
+
+@dataclass
+class Segment:
+    q_start: int
+    q_len: int
+    r0_start: int
+    r0_len: int
+    r0_causal: int
+    r1_start: int
+    r1_len: int          # r1 (own suffix) is always causal
+
+
+@dataclass
+class PackedBatch:
+    prompt_ids: List[int]                 # global prompt indices in this micro-batch
+    n_suffix: List[int]                   # per prompt
+    ids: np.ndarray                       # [T] int32
+    positions: np.ndarray                 # [T] int32
+    segments: List[Segment]
+    work: np.ndarray                      # [n_items, 8] int32
+    last_idx: np.ndarray                  # [S_total] int32 rows scored
+    num_tokens: int
+    padded_tokens: int                    # reference-equivalent token count
+    max_pos: int
+    _dev: dict = field(default_factory=dict, repr=False)
+
+    @property
+    def n_scored(self) -> int:
+        return int(self.last_idx.shape[0])
+
+    def device_tensors(self, device) -> dict:
+        """int32 metadata on ``device`` (cached; uploaded once, reused by all layers)."""
+        key = str(device)
+        if key not in self._dev:
+            d = torch.device(device)
+            nb = d.type != "cpu"
+            self._dev[key] = {
+                "ids": torch.from_numpy(self.ids).to(d, non_blocking=nb),
+                "positions": torch.from_numpy(self.positions).to(d, non_blocking=nb),
+                "work": torch.from_numpy(self.work).to(d, non_blocking=nb),
+                "last_idx": torch.from_numpy(self.last_idx).to(d, non_blocking=nb),
+            }
+        return self._dev[key]
+
+
+def pack_prompts(tps: Sequence[TokenizedPrompt], prompt_ids: Sequence[int],
+                 prefix_attention: str = "bidirectional") -> PackedBatch:
+    if prefix_attention not in ("bidirectional", "causal"):
+        raise ValueError(prefix_attention)
+    pcausal = 1 if prefix_attention == "causal" else 0
+    ids, pos, segs, last, nsuf = [], [], [], [], []
+    t = 0
+    padded = 0
+    max_pos = 0
+    for tp in tps:
+        Lp = len(tp.prefix)
+        p0 = t
+        ids.extend(tp.prefix)
+        pos.extend(range(Lp))
+        segs.append(Segment(p0, Lp, p0, Lp, pcausal, 0, 0))
+        t += Lp
+        for s in tp.suffixes:
+            n = len(s)
+            s0 = t
+            ids.extend(s)
+            pos.extend(range(Lp, Lp + n))
+            segs.append(Segment(s0, n, p0, Lp, 0, s0, n))
+            last.append(s0 + n - 1)
+            t += n
+        max_pos = max(max_pos, Lp + max([len(s) for s in tp.suffixes] or [0]))
+        nsuf.append(tp.n_suffix)
+        padded += tp.padded_tokens
+    work = []
+    for sg in segs:
+        for off in range(0, sg.q_len, Q_BLOCK):
+            work.append((sg.q_start + off, min(Q_BLOCK, sg.q_len - off), off,
+                         sg.r0_start, sg.r0_len, sg.r0_causal, sg.r1_start, sg.r1_len))
+    return PackedBatch(
+        prompt_ids=list(prompt_ids), n_suffix=nsuf,
+        ids=np.asarray(ids, dtype=np.int32), positions=np.asarray(pos, dtype=np.int32),
+        segments=segs, work=np.asarray(work, dtype=np.int32).reshape(-1, WORK_ITEM_FIELDS),
+        last_idx=np.asarray(last, dtype=np.int32), num_tokens=t, padded_tokens=padded,
+        max_pos=max_pos)
+
+
+def split_microbatches(tps: Sequence[TokenizedPrompt], token_budget: int,
+                       max_prompts: int = 0) -> List[List[int]]:
+    """Group consecutive prompts so each micro-batch holds <= token_budget tokens
+    (a single oversized prompt still forms its own micro-batch)."""
+    groups, cur, cur_t = [], [], 0
+    for i, tp in enumerate(tps):
+        n = tp.num_tokens
+        if cur and (cur_t + n > token_budget or (max_prompts and len(cur) >= max_prompts)):
+            groups.append(cur)
+            cur, cur_t = [], 0
+        cur.append(i)
+        cur_t += n
+    if cur:
+        groups.append(cur)
+    return groups

@@ -1,0 +1,140 @@
+"""Host memory + file I/O helpers on top of the native runtime.
+
+* :func:`alloc_host` — exact-size pinned buffers from ``hipHostMalloc``
+  (PyTorch's caching host allocator rounds to powers of two: a 1.71 GB 70B
+  layer would take 2 GB), wrapped as uint8 CPU tensors; falls back to
+  pageable memory when no GPU is present.
+* :func:`read_safetensors` — header via the native index, tensor bytes with
+  the multi-threaded ``pread`` engine into one host buffer, zero-copy views.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import weakref
+from typing import Dict
+
+import torch
+
+from .. import _native
+from ..utils import safetensors_io
+
+_IO_THREADS = int(os.environ.get("FLS_IO_THREADS", "8"))
+
+
+class _PinnedOwner:
+    __slots__ = ("ptr", "lib", "__weakref__")
+
+    def __init__(self, ptr, lib):
+        self.ptr, self.lib = ptr, lib
+
+    def __del__(self):
+        try:
+            if self.ptr:
+                self.lib.fls_pinned_free(self.ptr)
+                self.ptr = None
+        except Exception:
+            pass
+
+
+_owners = weakref.WeakValueDictionary()
+
+
+def _gpu_present() -> bool:
+    try:
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+def alloc_host(nbytes: int, pinned: bool = True) -> torch.Tensor:
+    """uint8 CPU tensor of exactly ``nbytes`` (pinned when a GPU is present)."""
+    if pinned and _gpu_present():
+        rt = _native.runtime_or_none()
+        if rt is not None:
+            ptr = rt.fls_pinned_alloc(max(1, nbytes))
+            if ptr:
+                owner = _PinnedOwner(ptr, rt)
+                buf = (ctypes.c_uint8 * max(1, nbytes)).from_address(ptr)
+                t = torch.frombuffer(buf, dtype=torch.uint8)[:nbytes]
+                # keep the owner alive as long as the base tensor lives
+                t._fls_owner = owner  # type: ignore[attr-defined]
+                _owners[id(owner)] = owner
+                return t
+        return torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    return torch.empty(nbytes, dtype=torch.uint8)
+
+
+def pread_into(path: str, offset: int, nbytes: int, dst: torch.Tensor) -> None:
+    """Read ``nbytes`` at ``offset`` of ``path`` into a contiguous CPU tensor."""
+    assert dst.device.type == "cpu" and dst.is_contiguous()
+    assert dst.numel() * dst.element_size() >= nbytes
+    if nbytes == 0:
+        return
+    rt = _native.runtime_or_none()
+    if rt is not None:
+        r = rt.fls_pread_into(path.encode(), offset, nbytes, dst.data_ptr(), _IO_THREADS)
+        if r != nbytes:
+            raise IOError(f"pread {path} @{offset}+{nbytes} failed: {r}")
+        return
+    with open(path, "rb") as f:
+        f.seek(offset)
+        mv = memoryview(dst.view(-1).view(torch.uint8).numpy())[:nbytes]
+        if f.readinto(mv) != nbytes:
+            raise IOError(f"short read {path}")
+
+
+def pwrite_from(path: str, src: torch.Tensor, nbytes: int = None) -> None:
+    n = src.numel() * src.element_size() if nbytes is None else nbytes
+    rt = _native.runtime_or_none()
+    if rt is not None:
+        r = rt.fls_pwrite_from(path.encode(), 0, n, src.data_ptr(), _IO_THREADS, 1)
+        if r != n:
+            raise IOError(f"pwrite {path} failed: {r}")
+        return
+    with open(path, "wb") as f:
+        f.write(memoryview(src.contiguous().view(-1).view(torch.uint8).numpy())[:n])
+
+
+def read_header_native(path: str):
+    rt = _native.runtime_or_none()
+    if rt is None:
+        return None
+    h = rt.fls_st_open(path.encode())
+    if not h:
+        raise ValueError(f"{path}: cannot parse safetensors header")
+    try:
+        out = {}
+        name = ctypes.create_string_buffer(1024)
+        dt = ctypes.create_string_buffer(16)
+        shape = (ctypes.c_int64 * 8)()
+        nd = ctypes.c_int()
+        b, e = ctypes.c_uint64(), ctypes.c_uint64()
+        for i in range(rt.fls_st_count(h)):
+            rc = rt.fls_st_info(h, i, name, 1024, dt, 16, ctypes.addressof(shape), ctypes.byref(nd),
+                                ctypes.byref(b), ctypes.byref(e))
+            if rc != 0:
+                raise ValueError(f"{path}: bad entry {i} ({rc})")
+            nm = name.value.decode()
+            out[nm] = safetensors_io.TensorInfo(nm, safetensors_io.DTYPES[dt.value.decode()],
+                                                tuple(shape[:nd.value]), b.value, e.value)
+        return out
+    finally:
+        rt.fls_st_close(h)
+
+
+def read_safetensors(path: str) -> Dict[str, torch.Tensor]:
+    infos = read_header_native(path)
+    if infos is None:
+        return safetensors_io.load_file(path)
+    if not infos:
+        return {}
+    lo = min(t.begin for t in infos.values())
+    hi = max(t.end for t in infos.values())
+    buf = torch.empty(hi - lo, dtype=torch.uint8)
+    pread_into(path, lo, hi - lo, buf)
+    out = {}
+    for n, t in infos.items():
+        v = buf[t.begin - lo:t.end - lo]
+        out[n] = v.view(t.dtype).view(t.shape) if t.nbytes else torch.empty(t.shape, dtype=t.dtype)
+    return out

@@ -1,0 +1,189 @@
+"""Double-buffered shard prefetcher: host (pinned / file) -> HBM weight slots.
+
+Reference: each shard's layers are loaded synchronously before compute
+(``/root/reference/utils.py:230-233``) and unloaded to ``meta`` with
+``empty_cache`` afterwards (``utils.py:299-302``) — compute and weight I/O
+never overlap.
+
+Here HBM holds ``n_slots`` fixed weight slots (2 = double buffer, allocated
+once; no per-shard free).  Shard ``k+1`` is copied into the other slot on a
+dedicated copy stream while shard ``k`` computes; the compute stream waits on
+a per-shard *ready* event, and the copy stream waits on the slot's *free*
+event recorded when the compute stream finished with its previous occupant.
+File-backed sources are read by a loader thread into two pinned staging
+buffers so disk reads, PCIe DMA and compute all overlap.
+
+``resident=True`` gives every shard its own slot and never evicts (the whole
+model stays in the 288 GB HBM — BASELINE config 5).
+"""
+from __future__ import annotations
+
+import threading
+import time
+from concurrent.futures import Future, ThreadPoolExecutor
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from ..models.layout import ALIGN_BYTES
+from . import hostmem
+from .weights import LayerSource
+
+
+def _align(n: int) -> int:
+    return (n + ALIGN_BYTES - 1) // ALIGN_BYTES * ALIGN_BYTES
+
+
+class ShardPrefetcher:
+    def __init__(self, source: LayerSource, layer_names: Sequence[str],
+                 shards: Sequence[Tuple[int, ...]], device, n_slots: int = 2,
+                 resident: bool = False, dtype=torch.float16):
+        self.src = source
+        self.names = list(layer_names)
+        self.shards = [tuple(s) for s in shards]
+        self.dev = torch.device(device)
+        self.cuda = self.dev.type == "cuda"
+        self.dtype = dtype
+        self.resident = resident
+        sizes = [self.shard_bytes(k) for k in range(len(self.shards))]
+        self.slot_bytes = max(sizes) if sizes else 0
+        self.n_slots = max(1, len(self.shards)) if resident else max(1, min(n_slots, len(self.shards) or 1))
+        self._slots: List[Optional[torch.Tensor]] = [None] * self.n_slots
+        self._slot_sizes = ([sizes[k] for k in range(len(self.shards))] if resident else
+                            [self.slot_bytes] * self.n_slots)
+        self._free_ev: List[Optional[torch.cuda.Event]] = [None] * self.n_slots
+        self._pending: Dict[int, Future] = {}
+        self._ready: Dict[int, Tuple[Optional[torch.cuda.Event], Dict[str, Dict[str, torch.Tensor]], int]] = {}
+        self._loaded_resident = set()
+        self.copy_stream = torch.cuda.Stream(self.dev) if self.cuda else None
+        needs_thread = self.cuda and any(source.host_buffer(self.names[i]) is None
+                                         for sh in self.shards for i in sh)
+        self._pool = ThreadPoolExecutor(1, thread_name_prefix="fls-loader") if needs_thread else None
+        self._staging: List[Optional[torch.Tensor]] = [None, None]
+        self._staging_ev: List[Optional[torch.cuda.Event]] = [None, None]
+        self._staging_i = 0
+        # stats
+        self.bytes_h2d = 0
+        self.wait_seconds = 0.0
+        self.load_seconds = 0.0
+        self.lock = threading.Lock()
+
+    # ------------------------------------------------------------ helpers
+    def shard_bytes(self, k: int) -> int:
+        return sum(_align(self.src.nbytes(self.names[i])) for i in self.shards[k])
+
+    def slot_of(self, k: int) -> int:
+        return k if self.resident else k % self.n_slots
+
+    def _slot(self, s: int) -> torch.Tensor:
+        if self._slots[s] is None:
+            self._slots[s] = torch.empty(max(1, self._slot_sizes[s]), dtype=torch.uint8, device=self.dev)
+        return self._slots[s]
+
+    def hbm_bytes(self) -> int:
+        return sum(t.numel() for t in self._slots if t is not None)
+
+    def _stage_buf(self, nbytes: int) -> Tuple[torch.Tensor, int]:
+        i = self._staging_i
+        self._staging_i ^= 1
+        if self._staging_ev[i] is not None:
+            self._staging_ev[i].synchronize()          # previous DMA out of this buffer done
+        b = self._staging[i]
+        if b is None or b.numel() < nbytes:
+            self._staging[i] = b = hostmem.alloc_host(max(nbytes, self.max_layer_bytes()), pinned=True)
+        return b, i
+
+    def max_layer_bytes(self) -> int:
+        return max(self.src.nbytes(n) for n in self.names)
+
+    # -------------------------------------------------------------- load
+    def _load(self, k: int):
+        t0 = time.perf_counter()
+        s = self.slot_of(k)
+        views: Dict[str, Dict[str, torch.Tensor]] = {}
+        if not self.cuda:
+            for i in self.shards[k]:
+                name = self.names[i]
+                hb = self.src.host_buffer(name)
+                if hb is None:
+                    hb = torch.empty(self.src.nbytes(name), dtype=torch.uint8)
+                    self.src.read_into(name, hb)
+                views[name] = self.src.layout(name).views(hb, self.dtype)
+            self.load_seconds += time.perf_counter() - t0
+            return None, views, s
+        slot = self._slot(s)
+        ev = torch.cuda.Event()
+        with torch.cuda.stream(self.copy_stream):
+            if self._free_ev[s] is not None:
+                self.copy_stream.wait_event(self._free_ev[s])
+            off = 0
+            for i in self.shards[k]:
+                name = self.names[i]
+                nb = self.src.nbytes(name)
+                dst = slot[off:off + nb]
+                hb = self.src.host_buffer(name)
+                if hb is None:
+                    stage, si = self._stage_buf(nb)
+                    self.src.read_into(name, stage)
+                    dst.copy_(stage[:nb], non_blocking=True)
+                    e = torch.cuda.Event()
+                    e.record(self.copy_stream)
+                    self._staging_ev[si] = e
+                else:
+                    dst.copy_(hb[:nb], non_blocking=True)
+                views[name] = self.src.layout(name).views(dst, self.dtype)
+                off += _align(nb)
+                self.bytes_h2d += nb
+            ev.record(self.copy_stream)
+        self.load_seconds += time.perf_counter() - t0
+        return ev, views, s
+
+    def prefetch(self, k: int) -> None:
+        if k < 0 or k >= len(self.shards):
+            return
+        with self.lock:
+            if k in self._ready or k in self._pending:
+                return
+            if self.resident and k in self._loaded_resident:
+                return
+            if self._pool is not None:
+                self._pending[k] = self._pool.submit(self._load, k)
+                return
+        r = self._load(k)
+        with self.lock:
+            self._ready[k] = r
+
+    def acquire(self, k: int) -> Dict[str, Dict[str, torch.Tensor]]:
+        t0 = time.perf_counter()
+        self.prefetch(k)
+        fut = None
+        with self.lock:
+            fut = self._pending.pop(k, None)
+        if fut is not None:
+            r = fut.result()
+            with self.lock:
+                self._ready[k] = r
+        ev, views, _ = self._ready[k]
+        if ev is not None:
+            torch.cuda.current_stream(self.dev).wait_event(ev)
+        if self.resident:
+            self._loaded_resident.add(k)
+        self.wait_seconds += time.perf_counter() - t0
+        return views
+
+    def release(self, k: int) -> None:
+        if self.resident:
+            return
+        with self.lock:
+            ent = self._ready.pop(k, None)
+        if ent is None:
+            return
+        _, _, s = ent
+        if self.cuda:
+            e = torch.cuda.Event()
+            e.record(torch.cuda.current_stream(self.dev))
+            self._free_ev[s] = e
+
+    def close(self):
+        if self._pool is not None:
+            self._pool.shutdown(wait=True)

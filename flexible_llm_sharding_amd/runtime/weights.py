@@ -1,0 +1,175 @@
+"""Weight sources: where packed layer bytes come from before they reach HBM.
+
+Reference behaviour (``/root/reference/utils.py:121-131``, DP cache
+``utils.py:24-75``): every time a layer is needed its safetensors file is read
+whole from disk, deserialized to CPU tensors and copied parameter by parameter
+(pageable, synchronous) to the GPU; the whole thing repeats for every batch,
+generation step and GPU.
+
+Here a source yields the *packed* layer (see :mod:`..models.layout`):
+
+* :class:`FileLayerSource` — per-layer safetensors files, read with the native
+  multi-threaded ``pread`` engine (or Python ``readinto``) and packed on the
+  host; used when host RAM is scarce (``--weight_cache disk``).
+* :class:`HostStore` — every packed layer resident in pinned host memory
+  (read once), so each shard H2D is one DMA at PCIe line rate; default when
+  RAM allows.  Also built directly from synthetic random-init weights
+  (generated on the GPU and copied down) for the 70B benchmark.
+* ``shard_fraction`` (data-parallel scatter-load): a rank keeps only its
+  1/G byte-slice of every layer; the full layer is re-assembled in HBM with an
+  RCCL all-gather over xGMI (:mod:`..parallel.data_parallel`).
+"""
+from __future__ import annotations
+
+import os
+import threading
+import time
+from typing import Dict, List, Optional, Sequence
+
+import torch
+
+from ..config import ModelConfig
+from ..models.layout import LayerLayout, layer_kind, layer_layout, pack_layer
+from ..utils.layer_format import layer_file
+from ..utils.safetensors_io import load_file, read_header
+from . import hostmem
+
+
+class LayerSource:
+    cfg: ModelConfig
+    dtype: torch.dtype = torch.float16
+
+    def layout(self, name: str) -> LayerLayout:
+        return layer_layout(self.cfg, layer_kind(name), torch.empty((), dtype=self.dtype).element_size())
+
+    def nbytes(self, name: str) -> int:
+        return self.layout(name).nbytes
+
+    def host_buffer(self, name: str) -> Optional[torch.Tensor]:
+        """Pinned uint8 buffer holding the packed layer, if resident on the host."""
+        return None
+
+    def read_into(self, name: str, dst: torch.Tensor) -> None:
+        raise NotImplementedError
+
+
+class FileLayerSource(LayerSource):
+    """Per-layer safetensors files in ``model_path`` (format of prepare_weights.py)."""
+
+    def __init__(self, cfg: ModelConfig, model_path: str, dtype=torch.float16):
+        self.cfg, self.model_path, self.dtype = cfg, model_path, dtype
+        missing = [n for n in cfg.layer_names() if not os.path.exists(layer_file(model_path, n))]
+        if missing:
+            raise FileNotFoundError(f"{model_path}: missing layer files {missing[:4]}...")
+        self.read_seconds = 0.0
+        self.read_bytes = 0
+
+    def read_into(self, name: str, dst: torch.Tensor) -> None:
+        t0 = time.perf_counter()
+        path = layer_file(self.model_path, name)
+        sd = hostmem.read_safetensors(path)
+        self.read_bytes += sum(v.numel() * v.element_size() for v in sd.values())
+        pack_layer(self.cfg, name, sd, self.dtype, out=dst[:self.nbytes(name)])
+        self.read_seconds += time.perf_counter() - t0
+
+
+class HostStore(LayerSource):
+    """All packed layers resident in (pinned) host memory."""
+
+    def __init__(self, cfg: ModelConfig, dtype=torch.float16, pinned: bool = True,
+                 names: Optional[Sequence[str]] = None):
+        self.cfg, self.dtype, self.pinned = cfg, dtype, pinned
+        self.names = list(names) if names is not None else cfg.layer_names()
+        self.buffers: Dict[str, torch.Tensor] = {}
+
+    @property
+    def total_bytes(self) -> int:
+        return sum(b.numel() for b in self.buffers.values())
+
+    def host_buffer(self, name: str) -> Optional[torch.Tensor]:
+        return self.buffers.get(name)
+
+    def read_into(self, name: str, dst: torch.Tensor) -> None:
+        src = self.buffers[name]
+        dst[:src.numel()].copy_(src)
+
+    def alloc(self, name: str) -> torch.Tensor:
+        buf = hostmem.alloc_host(self.nbytes(name), pinned=self.pinned)
+        self.buffers[name] = buf
+        return buf
+
+    @classmethod
+    def from_source(cls, src: LayerSource, pinned: bool = True, threads: int = 4,
+                    names: Optional[Sequence[str]] = None) -> "HostStore":
+        st = cls(src.cfg, src.dtype, pinned, names)
+        for n in st.names:
+            st.alloc(n)
+        errs: List[BaseException] = []
+        todo = list(st.names)
+        lock = threading.Lock()
+
+        def worker():
+            while True:
+                with lock:
+                    if not todo or errs:
+                        return
+                    n = todo.pop(0)
+                try:
+                    src.read_into(n, st.buffers[n])
+                except BaseException as e:  # noqa: BLE001
+                    errs.append(e)
+                    return
+
+        ts = [threading.Thread(target=worker, daemon=True) for _ in range(max(1, threads))]
+        [t.start() for t in ts]
+        [t.join() for t in ts]
+        if errs:
+            raise errs[0]
+        return st
+
+    @classmethod
+    def from_model_path(cls, cfg: ModelConfig, model_path: str, dtype=torch.float16,
+                        pinned: bool = True, threads: int = 4) -> "HostStore":
+        return cls.from_source(FileLayerSource(cfg, model_path, dtype), pinned, threads)
+
+    @classmethod
+    def synthetic(cls, cfg: ModelConfig, device: torch.device, seed: int = 0, std: float = 0.02,
+                  pinned: bool = True, names: Optional[Sequence[str]] = None,
+                  byte_range=None) -> "HostStore":
+        """Random-init packed layers generated on ``device`` and copied to pinned host memory.
+
+        ``byte_range=(r, G)`` keeps only slice r of G equal byte slices of every
+        layer (data-parallel scatter-load).  Generation is deterministic in
+        (seed, layer index, byte offset) so every rank's slices tile one model.
+        """
+        from ..ops import get_ops
+        st = cls(cfg, torch.float16, pinned, names)
+        dev = torch.device(device)
+        ops = get_ops(dev)
+        maxb = max(st.nbytes(n) for n in st.names)
+        stage = torch.empty(maxb, dtype=torch.uint8, device=dev)
+        for n in st.names:
+            lay = st.layout(n)
+            full = stage[:lay.nbytes]
+            ops.fill_layer_random(full, lay, seed=seed * 7919 + cfg.layer_names().index(n), std=std)
+            if byte_range is None:
+                buf = st.alloc(n)
+                buf.copy_(full, non_blocking=False)
+            else:
+                r, G = byte_range
+                chunk = shard_chunk_bytes(lay.nbytes, G)
+                buf = hostmem.alloc_host(chunk, pinned=pinned)
+                lo = r * chunk
+                hi = min(lay.nbytes, lo + chunk)
+                if hi > lo:
+                    buf[:hi - lo].copy_(full[lo:hi])
+                st.buffers[n] = buf
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        del stage
+        return st
+
+
+def shard_chunk_bytes(nbytes: int, world: int, align: int = 4096) -> int:
+    c = (nbytes + world - 1) // world
+    return (c + align - 1) // align * align

@@ -1,0 +1,60 @@
+"""Command-line interface — the reference flags verbatim plus additive ones.
+
+Reference: ``/root/reference/main.py:30-49``.  Deliberate fix:
+``--data_parallel`` is parsed as a real boolean (the reference uses
+``type=bool``, so ``--data_parallel False`` silently meant True); a bare
+``--data_parallel`` also enables it.
+"""
+from __future__ import annotations
+
+import argparse
+
+
+def str2bool(v) -> bool:
+    if isinstance(v, bool):
+        return v
+    s = str(v).strip().lower()
+    if s in ("1", "true", "t", "yes", "y", "on"):
+        return True
+    if s in ("0", "false", "f", "no", "n", "off", ""):
+        return False
+    raise argparse.ArgumentTypeError(f"boolean expected, got {v!r}")
+
+
+def build_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(description="MI355X-native layer-sharded Llama scoring / generation")
+    # ---- reference flags (main.py:31-46)
+    p.add_argument("--model_path", type=str, default="./")
+    p.add_argument("--prompt_pickle", type=str, required=True, help="Path to the input prompt pickle file")
+    p.add_argument("--output_file", type=str, required=True, help="Path to the LLM output scores file")
+    p.add_argument("--num_batch", type=int, default=1)
+    p.add_argument("--layer_num_per_shard", type=int, default=1,
+                   help="upper bound on layers per shard (balanced split)")
+    p.add_argument("--storage_location", type=str, default="cpu", choices=["gpu", "cpu", "disk"],
+                   help="'gpu': keep intermediate activations in HBM, 'cpu': pinned host RAM, 'disk': spill files")
+    p.add_argument("--max_activation_in_cpu", type=int, default=100)
+    p.add_argument("--data_parallel", type=str2bool, nargs="?", const=True, default=False,
+                   help="multi-GPU: data parallel if true, model (pipeline) parallel otherwise")
+    p.add_argument("--disk_folder", type=str, default="./temp",
+                   help="folder for intermediate activation files in 'disk' mode")
+    p.add_argument("--num_gen_token", type=int, default=1, help="how many new tokens to be generated")
+    # ---- additive flags
+    p.add_argument("--num_gpus", type=int, default=None, help="GPUs to use (default: all visible; 0 = CPU)")
+    p.add_argument("--prefix_attention", choices=["bidirectional", "causal"], default="bidirectional",
+                   help="prefix self-attention: reference-compatible bidirectional (default) or causal")
+    p.add_argument("--resident", type=str2bool, nargs="?", const=True, default=False,
+                   help="keep every shard resident in HBM after first load (288 GB fits 70B)")
+    p.add_argument("--weight_cache", choices=["host", "disk"], default="host",
+                   help="host: pinned-RAM layer cache read once; disk: re-read layer files every pass")
+    p.add_argument("--dp_weight_shard", type=str2bool, nargs="?", const=True, default=True,
+                   help="data parallel: scatter-load 1/G of each layer per GPU + RCCL all-gather")
+    p.add_argument("--token_budget", type=int, default=16384, help="max tokens per packed micro-batch")
+    p.add_argument("--dtype", choices=["float16", "float32"], default=None,
+                   help="activation dtype (default fp16 on GPU, fp32 on CPU)")
+    p.add_argument("--verbose", type=str2bool, nargs="?", const=True, default=False)
+    p.add_argument("--metrics_json", type=str, default=None, help="write run metrics here (rank 0)")
+    return p
+
+
+def parse_args(argv=None):
+    return build_parser().parse_args(argv)

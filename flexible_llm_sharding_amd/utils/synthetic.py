@@ -1,0 +1,94 @@
+"""Synthetic (no-network) checkpoints and prompts.
+
+* :func:`write_synthetic_checkpoint` writes a complete per-layer model
+  directory (``config.json``, tokenizer, ``{layer}.safetensors`` with full HF
+  names) with random-init weights of a given architecture — the same format
+  ``prepare_weights.py`` produces from a real HF checkpoint.
+* :func:`synthetic_prompts` builds ``(prefix, suffixes)`` prompts with exact
+  token counts under the synthetic tokenizer (Kaggle LLM-science-exam shape:
+  one context, several answer options).
+"""
+from __future__ import annotations
+
+import os
+import random
+from typing import Dict, List, Tuple
+
+import torch
+
+from ..config import ModelConfig
+from .layer_format import layer_file
+from .safetensors_io import save_file
+from .tokenizer import synthetic_word, write_synthetic_tokenizer
+
+
+def synthetic_layer_state_dict(cfg: ModelConfig, layer_name: str, seed: int = 0,
+                               std: float = 0.02, dtype=torch.float16) -> Dict[str, torch.Tensor]:
+    idx = cfg.layer_names().index(layer_name)
+    g = torch.Generator().manual_seed(seed * 1000003 + idx)
+    H, I, V = cfg.hidden_size, cfg.intermediate_size, cfg.vocab_size
+
+    def rnd(*shape):
+        return (torch.randn(*shape, generator=g) * std).to(dtype)
+
+    def norm_w(n):
+        return (1.0 + 0.1 * torch.randn(n, generator=g)).to(dtype)
+
+    if layer_name == "model.embed_tokens":
+        return {"model.embed_tokens.weight": (torch.randn(V, H, generator=g) * 1.0).to(dtype)}
+    if layer_name == "model.norm":
+        return {"model.norm.weight": norm_w(H)}
+    if layer_name == "lm_head":
+        return {"lm_head.weight": rnd(V, H)}
+    p = layer_name
+    return {
+        f"{p}.self_attn.q_proj.weight": rnd(cfg.q_size, H),
+        f"{p}.self_attn.k_proj.weight": rnd(cfg.kv_size, H),
+        f"{p}.self_attn.v_proj.weight": rnd(cfg.kv_size, H),
+        f"{p}.self_attn.o_proj.weight": rnd(H, cfg.q_size),
+        f"{p}.mlp.gate_proj.weight": rnd(I, H),
+        f"{p}.mlp.up_proj.weight": rnd(I, H),
+        f"{p}.mlp.down_proj.weight": rnd(H, I),
+        f"{p}.input_layernorm.weight": norm_w(H),
+        f"{p}.post_attention_layernorm.weight": norm_w(H),
+    }
+
+
+def write_synthetic_checkpoint(cfg: ModelConfig, out_dir: str, seed: int = 0,
+                               std: float = 0.02, dtype=torch.float16) -> None:
+    os.makedirs(out_dir, exist_ok=True)
+    cfg.save(out_dir)
+    write_synthetic_tokenizer(out_dir, cfg.vocab_size)
+    for name in cfg.layer_names():
+        sd = synthetic_layer_state_dict(cfg, name, seed, std, dtype)
+        save_file(sd, layer_file(out_dir, name))
+
+
+def load_full_state_dict(cfg: ModelConfig, model_path: str) -> Dict[str, torch.Tensor]:
+    from .safetensors_io import load_file
+    sd = {}
+    for name in cfg.layer_names():
+        sd.update(load_file(layer_file(model_path, name)))
+    return sd
+
+
+def _words(rng: random.Random, n: int, vocab_size: int) -> str:
+    return " ".join(synthetic_word(rng.randrange(3, vocab_size)) for _ in range(n))
+
+
+def synthetic_prompts(n_prompts: int, prefix_len: int, n_suffix: int, suffix_len: int,
+                      vocab_size: int = 32000, seed: int = 0,
+                      vary: bool = False) -> List[Tuple[str, Tuple[str, ...]]]:
+    """Prompts whose tokenization gives Lp = prefix_len (BOS incl.) and, per
+    suffix, suffix_len tokens after the BOS drop (``vary`` randomises lengths)."""
+    rng = random.Random(seed)
+    out = []
+    for _ in range(n_prompts):
+        lp = prefix_len if not vary else rng.randint(max(2, prefix_len // 2), prefix_len)
+        pre = _words(rng, lp - 1, vocab_size)
+        sufs = []
+        for _ in range(n_suffix):
+            ls = suffix_len if not vary else rng.randint(1, suffix_len)
+            sufs.append(_words(rng, ls, vocab_size))
+        out.append((pre, tuple(sufs)))
+    return out
