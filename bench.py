@@ -1,0 +1,149 @@
+"""Benchmark: tokens/s + peak GPU memory of sharded Llama-2-70B scoring (lnps=1).
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1
+launched by ``torch.distributed.run`` (one rank per GPU, RCCL).  One *step*
+is one full pass of the sharded model over a batch of synthetic
+(prefix, 5 suffixes) prompts — the reference's ``ShardedLlama.__call__``
+(``/root/reference/utils.py:133-305``): every layer's weights streamed from
+pinned host RAM into HBM (layer_num_per_shard=1, double-buffered), every
+prompt scored, fp16 probabilities copied back to the host.  Weights are
+random-init Llama-2-70B generated on the GPU and parked in pinned host
+memory before timing (no network, no checkpoint); prompts are synthetic text
+tokenized inside the timed step by a synthetic tokenizer.
+
+Scaling is weak: each GPU adds ``--prompts-per-gpu`` prompts.  N>1 runs the
+reference's default model-parallel schedule (shard k on GPU k mod N, RCCL
+send/recv of activations over xGMI; each GPU streams only its own shards) or
+``--mode dp``.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+METRIC = "tokens/sec + peak GPU mem, Llama-2-70B layer_num_per_shard=1 at 1/2/4/8 MI355X"
+
+
+def log(rank, *a):
+    if rank == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--model", default="llama2-70b")
+    ap.add_argument("--num-layers", type=int, default=None, help="override (debug only; result not comparable)")
+    ap.add_argument("--prompts-per-gpu", type=int, default=32)
+    ap.add_argument("--prefix-len", type=int, default=1024)
+    ap.add_argument("--n-suffix", type=int, default=5)
+    ap.add_argument("--suffix-len", type=int, default=64)
+    ap.add_argument("--lnps", type=int, default=1)
+    ap.add_argument("--storage", default="cpu", choices=["gpu", "cpu", "disk"])
+    ap.add_argument("--mode", default="auto", choices=["auto", "mp", "dp"])
+    ap.add_argument("--token-budget", type=int, default=16384)
+    ap.add_argument("--resident", action="store_true")
+    ap.add_argument("--prefix-attention", default="bidirectional")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--json-out", default=None)
+    a = ap.parse_args(argv)
+
+    from flexible_llm_sharding_amd.config import preset
+    from flexible_llm_sharding_amd.engine import ShardedRunner
+    from flexible_llm_sharding_amd.parallel.comm import Comm
+    from flexible_llm_sharding_amd.parallel.planner import make_plan
+    from flexible_llm_sharding_amd.runtime.weights import HostStore
+    from flexible_llm_sharding_amd.utils.synthetic import synthetic_prompts
+    from flexible_llm_sharding_amd.utils.tokenizer import load_tokenizer, write_synthetic_tokenizer
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        if a.gpus > 1:
+            raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch with torch.distributed.run")
+    comm = Comm.from_env("cuda")
+    rank = comm.rank
+    dev = comm.device if world > 1 else torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    mode = a.mode if a.mode != "auto" else ("mp" if world > 1 else "single")
+    dp = mode == "dp"
+
+    kw = {} if a.num_layers is None else {"num_hidden_layers": a.num_layers}
+    cfg = preset(a.model, **kw)
+    names = cfg.layer_names()
+    plan = make_plan(len(names), a.lnps, world, rank, dp)
+    mine = sorted({i for sh in plan.my_shards for i in sh})
+    t0 = time.perf_counter()
+    log(rank, f"[bench] generating {len(mine)} random-init {a.model} layers on {dev} -> pinned host ...")
+    store = HostStore.synthetic(cfg, dev, seed=a.seed, names=[names[i] for i in mine],
+                                progress=lambda i, n: log(rank, f"[bench]   layer {i}/{n} ({time.perf_counter() - t0:.0f}s)"))
+    log(rank, f"[bench] host store {store.total_bytes / 1e9:.1f} GB in {time.perf_counter() - t0:.1f}s")
+
+    tok_dir = f"/tmp/fls_bench_tok_{os.getpid()}"
+    write_synthetic_tokenizer(tok_dir, cfg.vocab_size)
+    tok = load_tokenizer(tok_dir)
+    n_prompts = a.prompts_per_gpu * (world if mode == "mp" else 1)
+    prompts = synthetic_prompts(n_prompts, a.prefix_len, a.n_suffix, a.suffix_len, cfg.vocab_size,
+                                seed=a.seed + (rank if dp else 0))
+    runner = ShardedRunner(cfg, store, dev, tok, layer_num_per_shard=a.lnps, storage_location=a.storage,
+                           disk_folder=f"/tmp/fls_bench_spill_{rank}", prefix_attention=a.prefix_attention,
+                           token_budget=a.token_budget, resident=a.resident, comm=comm, data_parallel=dp)
+    torch.cuda.reset_peak_memory_stats(dev)
+
+    for i in range(a.warmup):
+        tw = time.perf_counter()
+        runner(prompts)
+        log(rank, f"[bench] warmup {i}: {time.perf_counter() - tw:.2f}s")
+    comm.barrier()
+    torch.cuda.synchronize(dev)
+    t_start = time.perf_counter()
+    for i in range(a.steps):
+        ts = time.perf_counter()
+        runner(prompts)
+        log(rank, f"[bench] step {i}: {time.perf_counter() - ts:.2f}s  stats={json.dumps({k: round(v, 3) for k, v in runner.stats.items()})}")
+    torch.cuda.synchronize(dev)
+    comm.barrier()
+    elapsed = time.perf_counter() - t_start
+    elapsed = comm.all_reduce_max(elapsed)
+
+    tok_step = runner.stats["tokens"]
+    padded_step = runner.stats["padded_tokens"]
+    if dp:
+        tok_step = comm.all_reduce_sum(tok_step)
+        padded_step = comm.all_reduce_sum(padded_step)
+    peak = comm.all_reduce_max(float(torch.cuda.max_memory_allocated(dev)))
+    ms = elapsed / a.steps * 1000.0
+    value = tok_step * a.steps / elapsed
+    out = {
+        "metric": METRIC, "value": round(value, 2), "unit": "tokens/s", "n_gpus": world,
+        "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms, 2), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "fp16",
+        "data": "synthetic prompts (synthetic tokenizer) + random-init Llama-2-70B weights in pinned host RAM",
+        "peak_gpu_mem_gb": round(peak / 1e9, 3),
+        "config": {"model": a.model if a.num_layers is None else f"{a.model}-L{a.num_layers}",
+                   "global_batch": n_prompts * (world if dp else 1),
+                   "seq_len": a.prefix_len + a.suffix_len,
+                   "prefix_len": a.prefix_len, "n_suffix": a.n_suffix, "suffix_len": a.suffix_len,
+                   "tokens_per_step": tok_step, "padded_tokens_per_step": padded_step,
+                   "layer_num_per_shard": a.lnps, "storage_location": a.storage,
+                   "parallelism": (f"pp{world}-roundrobin" if mode == "mp" else (f"dp{world}" if dp else "single")),
+                   "resident": a.resident, "token_budget": a.token_budget},
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                json.dump(out, f, indent=1)
+    runner.close()
+    comm.destroy()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

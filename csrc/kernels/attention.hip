@@ -1,0 +1,210 @@
+// Shared-prefix / varlen flash attention forward on gfx950 (MI355X).
+//
+// Replaces the reference's eager attention (HF LlamaAttention via
+// utils.py:272-279): prefix K/V expanded to every suffix, concatenated, then
+// repeat_kv'd to every query head — materialised n_s * (nh/nkv) times — and a
+// [1, nh, Lp, Lp] fp32 probability matrix.
+//
+// Here K/V are read IN PLACE from the packed QKV activation: a work item is
+// a block of <= 64 query rows of one segment plus up to two key ranges
+//   range 0: the prompt's prefix (bidirectional, or causal for prefix queries
+//            in --prefix_attention causal),
+//   range 1: the suffix's own tokens, causal (key j visible to query i iff j <= i),
+// so every suffix of a prompt reads the single shared prefix K/V, GQA-native
+// (query head h uses kv head h / (nh/nkv)).
+//
+// Structure (4 waves x 16 query rows; K/V tiles of 64 keys in LDS):
+//   * S^T = K . Q^T with v_mfma_f32_16x16x32_f16 (A = K fragment from LDS,
+//     B = Q fragment in registers), so each lane owns ONE query row's scores:
+//     the online-softmax max/sum needs only 2 cross-lane xor steps and the
+//     P fragment for the next MFMA is lane-local (no LDS round trip);
+//   * O^T += V^T . P^T: the V^T operand comes from ds_read_b64_tr_b16
+//     (hardware transpose read, guide T10) of a row-major, XOR-swizzled V
+//     tile; O^T keeps the query on the lane too, so rescaling by
+//     exp2(m_old - m_new) is lane-local;
+//   * K tile XOR-swizzled per 16-byte chunk for conflict-free ds_read_b128.
+#include "common.h"
+#include "fls.h"
+
+namespace {
+
+constexpr int KT = 64;       // keys per tile
+constexpr int QB = 64;       // query rows per work item (4 waves x 16)
+
+template <int HD>
+struct Lds {
+  static constexpr int ROW = HD * 2;            // bytes per row
+  static constexpr int NCH = HD / 8;            // 16-byte chunks per row
+  // K: ds_read_b128 row reads -> chunk ^ (row & (NCH-1))
+  __device__ static int k_off(int row, int ch) { return row * ROW + ((ch ^ (row & (NCH - 1))) << 4); }
+  // V: ds_read_b64_tr_b16 -> chunk ^ ((row & (NCH/2-1)) << 1)
+  __device__ static int v_off(int row, int ch) { return row * ROW + ((ch ^ ((row & (NCH / 2 - 1)) << 1)) << 4); }
+};
+
+template <int HD>
+__global__ __launch_bounds__(256) void attn_fwd(const half_t* __restrict__ qkv, half_t* __restrict__ out,
+                                              const int* __restrict__ work, int nh, int nkv, int ld_qkv,
+                                              int ld_out, float scale_log2) {
+  constexpr int NS = HD / 32;     // k-steps of the QK^T product
+  constexpr int NU = HD / 16;     // 16-wide d subtiles of O
+  __shared__ __attribute__((aligned(16))) char smem[2 * KT * HD * 2];
+  char* Ks = smem;
+  char* Vs = smem + KT * HD * 2;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int fr = lane & 15, grp = lane >> 4;
+  const int h = blockIdx.y;
+  const int g = h / (nh / nkv);
+
+  const int* wi = work + blockIdx.x * 8;
+  const int q_start = wi[0], q_len = wi[1], q_off = wi[2];
+  const int r_start[2] = {wi[3], wi[6]};
+  const int r_len[2] = {wi[4], wi[7]};
+  const int r_causal[2] = {wi[5], 1};
+
+  const int q_col = h * HD;
+  const int k_col = nh * HD + g * HD;
+  const int v_col = (nh + nkv) * HD + g * HD;
+
+  // Q fragments (B operand of S^T = K Q^T): lane holds Q[row fr][32s + 8grp .. +8]
+  const int qrow = wave * 16 + fr;
+  const int qrow_c = min(qrow, q_len - 1);
+  half8 qf[NS];
+  {
+    const half_t* qp = qkv + (size_t)(q_start + qrow_c) * ld_qkv + q_col + grp * 8;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) qf[s] = *(const half8*)(qp + s * 32);
+  }
+  const int qi = q_off + qrow;   // query index within its segment (causal compare)
+
+  floatx4 o[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) o[u] = floatx4{0.f, 0.f, 0.f, 0.f};
+  float m_run = -1e30f;
+  float l_run = 0.f;
+
+  for (int rg = 0; rg < 2; ++rg) {
+    const int klen = r_len[rg];
+    if (klen <= 0) continue;
+    const int kbase = r_start[rg];
+    const bool causal = r_causal[rg] != 0;
+    // keys needed by the last valid query of this block
+    const int kend = causal ? min(klen, q_off + q_len) : klen;
+    for (int k0 = 0; k0 < kend; k0 += KT) {
+      __syncthreads();
+      // ---- stage K and V tiles (64 rows x HD) into LDS, 16 B per thread-chunk
+      constexpr int CHUNKS = KT * HD / 8;
+#pragma unroll
+      for (int c = tid; c < CHUNKS; c += 256) {
+        const int row = c / (HD / 8), ch = c % (HD / 8);
+        const int key = min(k0 + row, klen - 1);
+        const half_t* src = qkv + (size_t)(kbase + key) * ld_qkv;
+        const half8 kv = *(const half8*)(src + k_col + ch * 8);
+        const half8 vv = *(const half8*)(src + v_col + ch * 8);
+        *(half8*)(Ks + Lds<HD>::k_off(row, ch)) = kv;
+        *(half8*)(Vs + Lds<HD>::v_off(row, ch)) = vv;
+      }
+      __syncthreads();
+
+      // ---- S^T tile: 4 subtiles of 16 keys; lane holds keys 16t + 4grp + r of query fr
+      floatx4 sc[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        sc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+        const int krow = t * 16 + fr;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          const half8 kf = *(const half8*)(Ks + Lds<HD>::k_off(krow, s * 4 + grp));
+          sc[t] = mfma16x16x32(kf, qf[s], sc[t]);
+        }
+      }
+      // ---- scale, mask, online softmax (query = lane's fr row)
+      float mx = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = k0 + t * 16 + grp * 4 + r;
+          const bool vis = key < klen && (!causal || key <= qi);
+          const float v = vis ? sc[t][r] * scale_log2 : -INFINITY;
+          sc[t][r] = v;
+          mx = fmaxf(mx, v);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float m_new = fmaxf(m_run, mx);
+      const float alpha = fast_exp2(m_run - m_new);
+      m_run = m_new;
+      float psum = 0.f;
+      half8 pf[2];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = fast_exp2(sc[t][r] - m_new);
+          psum += p;
+          pf[t >> 1][(t & 1) * 4 + r] = (half_t)p;
+        }
+      l_run = l_run * alpha + psum;
+#pragma unroll
+      for (int u = 0; u < NU; ++u) o[u] *= alpha;
+
+      // ---- O^T += V^T P^T ; V^T fragment via two transposed 4x16 reads
+      const int q4 = (lane & 15) >> 2, p4 = lane & 3;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int row_a = ks * 32 + grp * 4 + q4;
+        const int row_b = row_a + 16;
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+          const int ch = u * 2 + (p4 >> 1);
+          const half4 va = ds_read_tr16(Vs + Lds<HD>::v_off(row_a, ch) + (p4 & 1) * 8);
+          const half4 vb = ds_read_tr16(Vs + Lds<HD>::v_off(row_b, ch) + (p4 & 1) * 8);
+          const half8 vf = {va[0], va[1], va[2], va[3], vb[0], vb[1], vb[2], vb[3]};
+          o[u] = mfma16x16x32(vf, pf[ks], o[u]);
+        }
+      }
+    }
+  }
+  // ---- normalise and store: lane holds O[q = fr][d = 16u + 4grp + r]
+  l_run += __shfl_xor(l_run, 16, 64);
+  l_run += __shfl_xor(l_run, 32, 64);
+  if (qrow < q_len) {
+    const float inv = 1.f / l_run;
+    half_t* op = out + (size_t)(q_start + qrow) * ld_out + h * HD + grp * 4;
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      half4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = (half_t)(o[u][r] * inv);
+      *(half4*)(op + u * 16) = v;
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int fls_attention(const void* qkv, void* out, const int* work, int n_items, int n_q_heads,
+                             int n_kv_heads, int head_dim, int ld_qkv, int ld_out, float scale, fls_stream_t s) {
+  if (n_items <= 0) return 0;
+  if (n_q_heads % n_kv_heads) return -2;
+  const float scale_log2 = scale * 1.4426950408889634f;
+  dim3 grid(n_items, n_q_heads);
+  auto st = (hipStream_t)s;
+  switch (head_dim) {
+    case 64:
+      hipLaunchKernelGGL(attn_fwd<64>, grid, dim3(256), 0, st, (const half_t*)qkv, (half_t*)out, work, n_q_heads,
+                         n_kv_heads, ld_qkv, ld_out, scale_log2);
+      break;
+    case 128:
+      hipLaunchKernelGGL(attn_fwd<128>, grid, dim3(256), 0, st, (const half_t*)qkv, (half_t*)out, work, n_q_heads,
+                         n_kv_heads, ld_qkv, ld_out, scale_log2);
+      break;
+    default:
+      return -3;
+  }
+  FLS_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,218 @@
+// Memory-bound kernels (gfx950): RMSNorm (optionally row-gathered), token
+// embedding gather, vocab softmax, synthetic weight fill.
+// All loads/stores are 16-byte vectors (guide G13: scalar fp16 loads cost
+// ~2x); one 256-thread block per row; fp32 statistics.
+#include "common.h"
+#include "fls.h"
+
+namespace {
+
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = warp_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  float t = 0.f;
+  const int nw = blockDim.x >> 6;
+  for (int i = 0; i < nw; ++i) t += red[i];
+  return t;
+}
+
+__device__ __forceinline__ float block_max(float v, float* red) {
+  v = warp_max(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  float t = -INFINITY;
+  const int nw = blockDim.x >> 6;
+  for (int i = 0; i < nw; ++i) t = fmaxf(t, red[i]);
+  return t;
+}
+
+// LlamaRMSNorm: y = w * fp16( x * rsqrt(mean(x^2) + eps) )   (HF cast points)
+// row r of y <- row (row_idx ? row_idx[r] : r) of x.   H % 8 == 0.
+template <int VPT>   // 16-byte vectors per thread held in registers
+__global__ __launch_bounds__(256) void rmsnorm_kernel(const half_t* __restrict__ x, const half_t* __restrict__ w,
+                                                    half_t* __restrict__ y, const int* __restrict__ row_idx, int H,
+                                                    int ldx, int ldy, float eps) {
+  __shared__ float red[4];
+  const int r = blockIdx.x;
+  const int src = row_idx ? row_idx[r] : r;
+  const half_t* xr = x + (size_t)src * ldx;
+  half_t* yr = y + (size_t)r * ldy;
+  const int nvec = H / 8;
+  half8 v[VPT];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = threadIdx.x + i * 256;
+    if (c < nvec) {
+      v[i] = *(const half8*)(xr + c * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += (float)v[i][j] * (float)v[i][j];
+    }
+  }
+  // remainder beyond the register-held part (very large H)
+  for (int c = threadIdx.x + VPT * 256; c < nvec; c += 256) {
+    const half8 t = *(const half8*)(xr + c * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ss += (float)t[j] * (float)t[j];
+  }
+  const float tot = block_sum(ss, red);
+  const float inv = rsqrtf(tot / (float)H + eps);
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = threadIdx.x + i * 256;
+    if (c < nvec) {
+      const half8 wv = *(const half8*)(w + c * 8);
+      half8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (half_t)((float)wv[j] * (float)(half_t)((float)v[i][j] * inv));
+      *(half8*)(yr + c * 8) = o;
+    }
+  }
+  for (int c = threadIdx.x + VPT * 256; c < nvec; c += 256) {
+    const half8 t = *(const half8*)(xr + c * 8);
+    const half8 wv = *(const half8*)(w + c * 8);
+    half8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (half_t)((float)wv[j] * (float)(half_t)((float)t[j] * inv));
+    *(half8*)(yr + c * 8) = o;
+  }
+}
+
+__global__ __launch_bounds__(256) void embed_kernel(const int* __restrict__ ids, const half_t* __restrict__ table,
+                                                  half_t* __restrict__ out, int H, int V) {
+  const int t = blockIdx.x;
+  int id = ids[t];
+  id = id < 0 ? 0 : (id >= V ? V - 1 : id);
+  const half8* src = (const half8*)(table + (size_t)id * H);
+  half8* dst = (half8*)(out + (size_t)t * H);
+  for (int c = threadIdx.x; c < H / 8; c += 256) dst[c] = src[c];
+}
+
+// softmax over a row of fp16 logits -> fp16 probabilities (fp32 math),
+// online max/sum in one pass, normalisation in a second (row stays in L2).
+__global__ __launch_bounds__(256) void softmax_kernel(const half_t* __restrict__ logits, half_t* __restrict__ probs,
+                                                    int V) {
+  __shared__ float red[4];
+  const half_t* lr = logits + (size_t)blockIdx.x * V;
+  half_t* pr = probs + (size_t)blockIdx.x * V;
+  float m = -INFINITY, s = 0.f;
+  const bool vec = (V % 8) == 0;
+  if (vec) {
+    for (int c = threadIdx.x; c < V / 8; c += 256) {
+      const half8 v = *(const half8*)(lr + c * 8);
+      float vm = (float)v[0];
+#pragma unroll
+      for (int j = 1; j < 8; ++j) vm = fmaxf(vm, (float)v[j]);
+      const float nm = fmaxf(m, vm);
+      s *= __expf(m - nm);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += __expf((float)v[j] - nm);
+      m = nm;
+    }
+  } else {
+    for (int c = threadIdx.x; c < V; c += 256) {
+      const float v = (float)lr[c];
+      const float nm = fmaxf(m, v);
+      s = s * __expf(m - nm) + __expf(v - nm);
+      m = nm;
+    }
+  }
+  const float gm = block_max(m, red);
+  const float gs = block_sum(m == -INFINITY ? 0.f : s * __expf(m - gm), red);
+  const float inv = 1.f / gs;
+  if (vec) {
+    for (int c = threadIdx.x; c < V / 8; c += 256) {
+      const half8 v = *(const half8*)(lr + c * 8);
+      half8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (half_t)(__expf((float)v[j] - gm) * inv);
+      *(half8*)(pr + c * 8) = o;
+    }
+  } else {
+    for (int c = threadIdx.x; c < V; c += 256) pr[c] = (half_t)(__expf((float)lr[c] - gm) * inv);
+  }
+}
+
+// counter-based normal generator (splitmix64 -> Box-Muller), 8 values/thread
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void fill_random_kernel(half_t* __restrict__ dst, uint64_t n, uint64_t seed,
+                                                        float mean, float stdv) {
+  const uint64_t base = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (base >= n) return;
+  half8 o;
+#pragma unroll
+  for (int j = 0; j < 8; j += 2) {
+    const uint64_t h = splitmix64(seed * 0x2545F4914F6CDD1Dull + base + j);
+    const float u1 = ((float)(uint32_t)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);
+    const float u2 = (float)(uint32_t)(h & 0xFFFFFF) * (1.0f / 16777216.0f);
+    const float rr = sqrtf(-2.f * __logf(u1));
+    float sn, cs;
+    __sincosf(6.28318530718f * u2, &sn, &cs);
+    o[j] = (half_t)(mean + stdv * rr * cs);
+    o[j + 1] = (half_t)(mean + stdv * rr * sn);
+  }
+  if (base + 8 <= n) {
+    *(half8*)(dst + base) = o;
+  } else {
+    for (int j = 0; j < 8 && base + j < n; ++j) dst[base + j] = o[j];
+  }
+}
+
+}  // namespace
+
+extern "C" int fls_rmsnorm(const void* x, const void* w, void* y, const int* row_idx, int rows, int H, int ldx,
+                           int ldy, float eps, fls_stream_t s) {
+  if (rows <= 0) return 0;
+  if (H % 8 || ldx % 8 || ldy % 8) return -2;
+  auto st = (hipStream_t)s;
+  const int nvec = H / 8;
+  if (nvec <= 256)
+    hipLaunchKernelGGL(rmsnorm_kernel<1>, dim3(rows), dim3(256), 0, st, (const half_t*)x, (const half_t*)w,
+                       (half_t*)y, row_idx, H, ldx, ldy, eps);
+  else if (nvec <= 512)
+    hipLaunchKernelGGL(rmsnorm_kernel<2>, dim3(rows), dim3(256), 0, st, (const half_t*)x, (const half_t*)w,
+                       (half_t*)y, row_idx, H, ldx, ldy, eps);
+  else
+    hipLaunchKernelGGL(rmsnorm_kernel<4>, dim3(rows), dim3(256), 0, st, (const half_t*)x, (const half_t*)w,
+                       (half_t*)y, row_idx, H, ldx, ldy, eps);
+  FLS_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int fls_embed(const int* ids, const void* table, void* out, int T, int H, int V, fls_stream_t s) {
+  if (T <= 0) return 0;
+  if (H % 8) return -2;
+  hipLaunchKernelGGL(embed_kernel, dim3(T), dim3(256), 0, (hipStream_t)s, ids, (const half_t*)table, (half_t*)out,
+                     H, V);
+  FLS_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int fls_softmax_rows(const void* logits, void* probs, int rows, int V, fls_stream_t s) {
+  if (rows <= 0) return 0;
+  hipLaunchKernelGGL(softmax_kernel, dim3(rows), dim3(256), 0, (hipStream_t)s, (const half_t*)logits,
+                     (half_t*)probs, V);
+  FLS_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int fls_fill_random(void* dst, uint64_t n_elems, uint64_t seed, float mean, float stdv, fls_stream_t s) {
+  if (n_elems == 0) return 0;
+  const uint64_t threads = (n_elems + 7) / 8;
+  const uint64_t blocks = (threads + 255) / 256;
+  hipLaunchKernelGGL(fill_random_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)s, (half_t*)dst, n_elems,
+                     seed, mean, stdv);
+  FLS_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,300 @@
+// MFMA GEMM for the Llama projections on gfx950 (MI355X / CDNA4).
+//
+//   C[M, N'] = epilogue( A[M, K] . W[N, K]^T )      fp16 in, fp32 accumulate
+//
+// A = activations (tokens x hidden, row-major), W = nn.Linear weight [out, in]
+// (row-major) — both operands are K-contiguous, the natural MFMA layout.
+//
+// Main kernel (M any, N % 256 == 0, K % 64 == 0):
+//   * 256 x 256 x 64 block tile, 512 threads = 8 waves (4 along N x 2 along M),
+//     each wave 64 (N) x 128 (M) = 4 x 8 tiles of v_mfma_f32_16x16x32_f16
+//     (16x16x32 holds a higher clock than 32x32x16 on random data — guide §5.4 r28);
+//   * operands staged global -> LDS by global_load_lds_dwordx4 (LDS-DMA, no
+//     VGPR round trip), double-buffered (2 x 64 KiB), with the XOR chunk
+//     swizzle applied on the per-lane SOURCE address so ds_read_b128 fragment
+//     reads are bank-conflict free (guide T2 / rule 21);
+//   * the MFMA computes C^T tiles (A operand = W fragment, B operand = X
+//     fragment) so each lane ends up with 4 consecutive output columns of one
+//     row: 8-byte stores, and the epilogue partners (RoPE pair, gate/up) sit
+//     in neighbouring 16-column subtiles of the SAME lane — fused in registers;
+//   * XCD-aware bijective block remap + grouped (8 M-tiles) ordering so the
+//     32 blocks resident on one XCD share W/X K-panels in that XCD's L2.
+// Epilogues: NONE, RESID (C = acc + R, R may alias C), SWIGLU (gate/up rows
+// interleaved per 16 -> C has N/2 columns), ROPE (rotate RoPE-pair-permuted
+// q/k columns < rope_cols with fp32 cos/sin tables).
+//
+// Generic fallback kernel (any M, N % 16 == 0, K) for odd test shapes.
+#include "common.h"
+#include "fls.h"
+
+namespace {
+
+constexpr int BM = 256, BN = 256, BK = 64, NT = 512;
+constexpr int TILE_BYTES = BM * BK * 2;          // 32 KiB per operand tile
+constexpr int STAGE_BYTES = 2 * TILE_BYTES;       // W + X
+constexpr int LDS_BYTES = 2 * STAGE_BYTES;        // double buffered: 128 KiB
+
+struct Epi {
+  const half_t* R;
+  int ldr;
+  const int* pos;
+  const float* cos_t;
+  const float* sin_t;
+  int rope_cols;
+  int head_dim;
+};
+
+// Store one pair of 16-column subtiles (cols n_first + 4*grp + r and +16)
+// for output row m.  acc_a: first subtile, acc_b: second (its partner).
+template <int EPI>
+__device__ __forceinline__ void store_pair(half_t* __restrict__ C, int ldc, int m, int n_first, int grp,
+                                           const floatx4& acc_a, const floatx4& acc_b, const Epi& ep) {
+  const int c0 = n_first + 4 * grp;
+  if constexpr (EPI == FLS_EPI_SWIGLU) {
+    // pair = (gate, up) of intermediate columns [n_first/2, n_first/2 + 16)
+    const int oc = n_first / 2 + 4 * grp;
+    half4 o;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[r] = (half_t)(silu(acc_a[r]) * acc_b[r]);
+    *(half4*)(C + (size_t)m * ldc + oc) = o;
+    return;
+  } else {
+    floatx4 a = acc_a, b = acc_b;
+    if constexpr (EPI == FLS_EPI_ROPE) {
+      if (n_first < ep.rope_cols) {
+        const int hd = ep.head_dim, half_hd = hd >> 1;
+        const int o = c0 % hd;
+        const int f0 = (o >> 5) * 16 + (o & 15);
+        const int p = ep.pos[m];
+        const float* cr = ep.cos_t + (size_t)p * half_hd + f0;
+        const float* sr = ep.sin_t + (size_t)p * half_hd + f0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float cs = cr[r], sn = sr[r];
+          const float x1 = acc_a[r], x2 = acc_b[r];
+          a[r] = x1 * cs - x2 * sn;
+          b[r] = x2 * cs + x1 * sn;
+        }
+      }
+    }
+    if constexpr (EPI == FLS_EPI_RESID) {
+      const half4 ra = *(const half4*)(ep.R + (size_t)m * ep.ldr + c0);
+      const half4 rb = *(const half4*)(ep.R + (size_t)m * ep.ldr + c0 + 16);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { a[r] += (float)ra[r]; b[r] += (float)rb[r]; }
+    }
+    half4 oa, ob;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { oa[r] = (half_t)a[r]; ob[r] = (half_t)b[r]; }
+    *(half4*)(C + (size_t)m * ldc + c0) = oa;
+    *(half4*)(C + (size_t)m * ldc + c0 + 16) = ob;
+  }
+}
+
+template <int EPI>
+__global__ __launch_bounds__(NT, 2) void gemm_nt_256x256(const half_t* __restrict__ A, const half_t* __restrict__ W,
+                                                        half_t* __restrict__ C, int M, int N, int K, int lda, int ldw,
+                                                        int ldc, Epi ep) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  // ---- XCD-aware bijective remap, then grouped tile order
+  const int nwg = gridDim.x;
+  int bid = blockIdx.x;
+  {
+    const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7, loc = bid >> 3;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+  }
+  const int tiles_m = (M + BM - 1) / BM;
+  const int tiles_n = N / BN;
+  constexpr int GROUP_M = 8;
+  const int group = bid / (GROUP_M * tiles_n);
+  const int first_m = group * GROUP_M;
+  const int gsz = min(tiles_m - first_m, GROUP_M);
+  const int in_g = bid - group * GROUP_M * tiles_n;
+  const int tm = first_m + in_g % gsz;
+  const int tn = in_g / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // ---- staging sources: each wave fills 4 x 1 KiB of the W tile and of the X tile.
+  const int lr = lane >> 3;              // row inside the 8-row piece
+  const int lc = (lane & 7) ^ lr;        // source chunk (inverse swizzle on the source)
+  const half_t* wsrc[4];
+  const half_t* xsrc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int piece = wave * 4 + j;
+    const int rw = n0 + piece * 8 + lr;
+    const int rx = min(m0 + piece * 8 + lr, M - 1);
+    wsrc[j] = W + (size_t)rw * ldw + lc * 8;
+    xsrc[j] = A + (size_t)rx * lda + lc * 8;
+  }
+  auto stage = [&](int buf, int k0) {
+    char* base = smem + buf * STAGE_BYTES;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) glds16(wsrc[j] + k0, base + (wave * 4 + j) * 1024);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) glds16(xsrc[j] + k0, base + TILE_BYTES + (wave * 4 + j) * 1024);
+  };
+
+  const int wn = wave & 3, wm = wave >> 2;
+  const int fr = lane & 15, grp = lane >> 4;
+  floatx4 acc[8][4];
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[u][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment byte offsets inside a stage (row*128 + swizzled chunk*16)
+  const int wrow0 = wn * 64 + fr;
+  const int xrow0 = wm * 128 + fr;
+  const int swz = lane & 7;  // row & 7 == fr & 7 for every fragment row
+
+  const int nk = K / BK;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * BK);
+    const char* Ws = smem + cur * STAGE_BYTES;
+    const char* Xs = Ws + TILE_BYTES;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int ch = ((s * 4 + grp) ^ swz) << 4;
+      half8 wf[4], xf[8];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) wf[t] = *(const half8*)(Ws + (wrow0 + t * 16) * 128 + ch);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) xf[u] = *(const half8*)(Xs + (xrow0 + u * 16) * 128 + ch);
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[u][t] = mfma16x16x32(wf[t], xf[u], acc[u][t]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---- epilogue: lane holds C[m][n_sub + 4*grp + r]
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int m = m0 + wm * 128 + u * 16 + fr;
+    if (m < M) {
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+        store_pair<EPI>(C, ldc, m, n0 + wn * 64 + p * 32, grp, acc[u][2 * p], acc[u][2 * p + 1], ep);
+    }
+  }
+}
+
+// ------------------------------------------------------------- generic
+// Block = 4 waves; block tile 32 (M) x 256 (N); wave tile 32 x 64.
+// Operands loaded straight from global with bounds masks (zero fill).
+template <int EPI>
+__global__ __launch_bounds__(256) void gemm_nt_generic(const half_t* __restrict__ A, const half_t* __restrict__ W,
+                                                     half_t* __restrict__ C, int M, int N, int K, int lda, int ldw,
+                                                     int ldc, Epi ep) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fr = lane & 15, grp = lane >> 4;
+  const int m0 = blockIdx.x * 32;
+  const int nw = blockIdx.y * 256 + wave * 64;
+  floatx4 acc[2][4];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[u][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < K; k0 += 32) {
+    half8 wf[4], xf[2];
+    const int kb = k0 + grp * 8;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int n = nw + t * 16 + fr;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        wf[t][j] = (n < N && kb + j < K) ? W[(size_t)n * ldw + kb + j] : (half_t)0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int m = m0 + u * 16 + fr;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        xf[u][j] = (m < M && kb + j < K) ? A[(size_t)m * lda + kb + j] : (half_t)0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[u][t] = mfma16x16x32(wf[t], xf[u], acc[u][t]);
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int m = m0 + u * 16 + fr;
+    if (m >= M) continue;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int nf = nw + p * 32;
+      if (nf + 32 <= N) {
+        store_pair<EPI>(C, ldc, m, nf, grp, acc[u][2 * p], acc[u][2 * p + 1], ep);
+      } else if constexpr (EPI == FLS_EPI_NONE || EPI == FLS_EPI_RESID) {
+        // ragged tail (N % 32 != 0): scalar stores
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int n = nf + h * 16 + 4 * grp + r;
+            if (n < N) {
+              float v = h ? acc[u][2 * p + 1][r] : acc[u][2 * p][r];
+              if constexpr (EPI == FLS_EPI_RESID) v += (float)ep.R[(size_t)m * ep.ldr + n];
+              C[(size_t)m * ldc + n] = (half_t)v;
+            }
+          }
+      }
+    }
+  }
+}
+
+template <int EPI>
+int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int lda, int ldw, int ldc,
+           const Epi& ep, hipStream_t s) {
+  const bool fast = (N % BN == 0) && (K % BK == 0) && (lda % 8 == 0) && (ldw % 8 == 0) && M > 0;
+  if (fast) {
+    static bool attr_set = false;
+    if (!attr_set) {
+      (void)hipFuncSetAttribute((const void*)gemm_nt_256x256<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+      attr_set = true;
+    }
+    const int tiles = ((M + BM - 1) / BM) * (N / BN);
+    hipLaunchKernelGGL(gemm_nt_256x256<EPI>, dim3(tiles), dim3(NT), LDS_BYTES, s, A, W, C, M, N, K, lda, ldw, ldc, ep);
+  } else {
+    dim3 grid((M + 31) / 32, (N + 255) / 256);
+    hipLaunchKernelGGL(gemm_nt_generic<EPI>, grid, dim3(256), 0, s, A, W, C, M, N, K, lda, ldw, ldc, ep);
+  }
+  FLS_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int fls_kernels_version(void) { return 1; }
+
+extern "C" int fls_gemm(const void* A, const void* W, void* C, const void* R, int M, int N, int K, int lda, int ldw,
+                        int ldc, int ldr, int epi, const int* pos, const float* cos_t, const float* sin_t,
+                        int rope_cols, int head_dim, fls_stream_t s) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  if ((epi == FLS_EPI_SWIGLU || epi == FLS_EPI_ROPE) && (N % 32)) return -2;
+  if (epi == FLS_EPI_ROPE && (head_dim % 32 || rope_cols % 32)) return -3;
+  Epi ep{(const half_t*)R, ldr, pos, cos_t, sin_t, rope_cols, head_dim};
+  auto a = (const half_t*)A;
+  auto w = (const half_t*)W;
+  auto c = (half_t*)C;
+  auto st = (hipStream_t)s;
+  switch (epi) {
+    case FLS_EPI_NONE: return launch<FLS_EPI_NONE>(a, w, c, M, N, K, lda, ldw, ldc, ep, st);
+    case FLS_EPI_RESID: return launch<FLS_EPI_RESID>(a, w, c, M, N, K, lda, ldw, ldc, ep, st);
+    case FLS_EPI_SWIGLU: return launch<FLS_EPI_SWIGLU>(a, w, c, M, N, K, lda, ldw, ldc, ep, st);
+    case FLS_EPI_ROPE: return launch<FLS_EPI_ROPE>(a, w, c, M, N, K, lda, ldw, ldc, ep, st);
+  }
+  return -1;
+}

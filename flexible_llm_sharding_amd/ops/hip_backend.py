@@ -1,0 +1,139 @@
+"""HIP backend: every op is a hand-written gfx950 kernel in ``libfls_kernels.so``.
+
+Kernels run on the caller's current HIP stream (``torch.cuda.current_stream``)
+so they compose with the copy/comm streams of the runtime; outputs are
+allocated through PyTorch's caching allocator.  There is deliberately no
+fallback: a missing library raises (see ``_native.kernels``).
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import _native
+from .torch_backend import fill_params
+
+EPI_NONE, EPI_RESID, EPI_SWIGLU, EPI_ROPE = 0, 1, 2, 3
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _chk(rc: int, what: str):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed with code {rc}")
+
+
+def _f16(t: torch.Tensor, name: str):
+    if t.dtype != torch.float16 or not t.is_cuda:
+        raise TypeError(f"{name}: expected fp16 CUDA tensor, got {t.dtype} on {t.device}")
+    if t.stride(-1) != 1:
+        raise ValueError(f"{name}: last dim must be contiguous")
+
+
+class HipOps:
+    name = "hip"
+    uses_work_items = True
+
+    def __init__(self):
+        self.k = _native.kernels()
+
+    # ---------------------------------------------------------------- GEMM
+    def gemm(self, x: torch.Tensor, w: torch.Tensor, epi: int = EPI_NONE, out: torch.Tensor = None,
+             resid: torch.Tensor = None, positions=None, cos=None, sin=None, rope_cols: int = 0,
+             head_dim: int = 0) -> torch.Tensor:
+        _f16(x, "x")
+        _f16(w, "w")
+        M, K = x.shape
+        N, K2 = w.shape
+        if K != K2:
+            raise ValueError(f"gemm K mismatch {x.shape} x {w.shape}")
+        ncols = N // 2 if epi == EPI_SWIGLU else N
+        if out is None:
+            out = torch.empty(M, ncols, dtype=torch.float16, device=x.device)
+        R = resid if resid is not None else out
+        rc = self.k.fls_gemm(x.data_ptr(), w.data_ptr(), out.data_ptr(), R.data_ptr(), M, N, K,
+                             x.stride(0), w.stride(0), out.stride(0), R.stride(0), epi,
+                             positions.data_ptr() if positions is not None else None,
+                             cos.data_ptr() if cos is not None else None,
+                             sin.data_ptr() if sin is not None else None,
+                             rope_cols, head_dim, _stream())
+        _chk(rc, "fls_gemm")
+        return out
+
+    def linear(self, x, w):
+        return self.gemm(x, w)
+
+    def linear_residual(self, x, w, resid):
+        _f16(resid, "resid")
+        return self.gemm(x, w, EPI_RESID, out=resid, resid=resid)
+
+    def swiglu_up(self, x, wgu):
+        return self.gemm(x, wgu, EPI_SWIGLU)
+
+    def qkv_rope(self, x, wqkv, positions, cos, sin, n_q_heads, n_kv_heads, head_dim):
+        if positions.dtype != torch.int32:
+            raise TypeError("positions must be int32")
+        return self.gemm(x, wqkv, EPI_ROPE, positions=positions, cos=cos, sin=sin,
+                         rope_cols=(n_q_heads + n_kv_heads) * head_dim, head_dim=head_dim)
+
+    # ----------------------------------------------------------- attention
+    def attention(self, qkv, work, n_q_heads, n_kv_heads, head_dim):
+        _f16(qkv, "qkv")
+        if work.dtype != torch.int32 or not work.is_cuda:
+            raise TypeError("work items must be an int32 CUDA tensor")
+        T = qkv.shape[0]
+        out = torch.empty(T, n_q_heads * head_dim, dtype=torch.float16, device=qkv.device)
+        rc = self.k.fls_attention(qkv.data_ptr(), out.data_ptr(), work.data_ptr(), work.shape[0],
+                                  n_q_heads, n_kv_heads, head_dim, qkv.stride(0), out.stride(0),
+                                  head_dim ** -0.5, _stream())
+        _chk(rc, "fls_attention")
+        return out
+
+    # ------------------------------------------------------- elementwise
+    def rmsnorm(self, x, w, eps, row_idx=None):
+        _f16(x, "x")
+        _f16(w, "w")
+        rows = row_idx.shape[0] if row_idx is not None else x.shape[0]
+        H = x.shape[1]
+        y = torch.empty(rows, H, dtype=torch.float16, device=x.device)
+        rc = self.k.fls_rmsnorm(x.data_ptr(), w.data_ptr(), y.data_ptr(),
+                                row_idx.data_ptr() if row_idx is not None else None,
+                                rows, H, x.stride(0), y.stride(0), float(eps), _stream())
+        _chk(rc, "fls_rmsnorm")
+        return y
+
+    def gather_rmsnorm(self, x, idx, w, eps):
+        if idx.dtype != torch.int32:
+            raise TypeError("row indices must be int32")
+        return self.rmsnorm(x, w, eps, row_idx=idx)
+
+    def embed(self, ids, table, out_dtype):
+        _f16(table, "table")
+        if out_dtype != torch.float16:
+            raise TypeError("HIP path runs fp16 activations")
+        T = ids.shape[0]
+        V, H = table.shape
+        out = torch.empty(T, H, dtype=torch.float16, device=table.device)
+        _chk(self.k.fls_embed(ids.data_ptr(), table.data_ptr(), out.data_ptr(), T, H, V, _stream()), "fls_embed")
+        return out
+
+    def softmax(self, logits):
+        _f16(logits, "logits")
+        rows, V = logits.shape
+        probs = torch.empty_like(logits)
+        _chk(self.k.fls_softmax_rows(logits.data_ptr(), probs.data_ptr(), rows, V, _stream()), "fls_softmax")
+        return probs
+
+    def lm_head_softmax(self, h, w):
+        return self.softmax(self.gemm(h, w))
+
+    def fill_layer_random(self, buf: torch.Tensor, layout, seed: int, std: float = 0.02) -> None:
+        views = layout.views(buf, torch.float16)
+        for i, (name, v) in enumerate(views.items()):
+            mean, sd = fill_params(name, std)
+            _chk(self.k.fls_fill_random(v.data_ptr(), v.numel(), int(seed) * 131 + i, float(mean),
+                                        float(sd), _stream()), "fls_fill_random")
+
+    def synchronize(self):
+        torch.cuda.synchronize()

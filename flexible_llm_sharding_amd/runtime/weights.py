@@ -135,7 +135,7 @@ class HostStore(LayerSource):
     @classmethod
     def synthetic(cls, cfg: ModelConfig, device: torch.device, seed: int = 0, std: float = 0.02,
                   pinned: bool = True, names: Optional[Sequence[str]] = None,
-                  byte_range=None) -> "HostStore":
+                  byte_range=None, progress=None) -> "HostStore":
         """Random-init packed layers generated on ``device`` and copied to pinned host memory.
 
         ``byte_range=(r, G)`` keeps only slice r of G equal byte slices of every
@@ -148,7 +148,9 @@ class HostStore(LayerSource):
         ops = get_ops(dev)
         maxb = max(st.nbytes(n) for n in st.names)
         stage = torch.empty(maxb, dtype=torch.uint8, device=dev)
-        for n in st.names:
+        for li, n in enumerate(st.names):
+            if progress is not None and li % 10 == 0:
+                progress(li, len(st.names))
             lay = st.layout(n)
             full = stage[:lay.nbytes]
             ops.fill_layer_random(full, lay, seed=seed * 7919 + cfg.layer_names().index(n), std=std)
