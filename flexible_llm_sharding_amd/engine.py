@@ -83,6 +83,7 @@ class ShardedRunner:
         self.stats: Dict[str, float] = {}
         self.h2d_stream = torch.cuda.Stream(self.dev) if self.cuda else None
         self.d2h_stream = torch.cuda.Stream(self.dev) if self.cuda else None
+        self._store: Optional[ActivationStore] = None
 
     # ----------------------------------------------------------- helpers
     def tokenize(self, prompts) -> List[TokenizedPrompt]:
@@ -107,14 +108,39 @@ class ShardedRunner:
         """Reference API: list of (prefix, suffixes) -> list of [n_s, 1, V] fp16 arrays."""
         return self.run_tokenized(self.tokenize(prompts))
 
+    def _get_store(self) -> ActivationStore:
+        if self._store is None:
+            self._store = ActivationStore(self.storage, self.dev, self.disk_folder,
+                                          tag=str(self.comm.rank) if self.comm.world > 1 else "",
+                                          h2d_stream=self.h2d_stream, d2h_stream=self.d2h_stream)
+        return self._store
+
+    def schedule(self, n_batches: int):
+        """Flat (shard, micro-batch) order.
+
+        Single-GPU / data-parallel runs visit micro-batches in zigzag order
+        (0..n-1, then n-1..0, ...) so the micro-batch that ends shard k starts
+        shard k+1 and its activation never leaves HBM; the model-parallel
+        pipeline keeps the natural order every rank's send/recv sequence
+        expects.
+        """
+        zig = self.plan.mode != "mp"
+        items = []
+        for k in range(len(self.my_shards)):
+            order = range(n_batches)
+            if zig and k % 2 == 1:
+                order = reversed(range(n_batches))
+            items += [(k, b) for b in order]
+        return items
+
     def run_tokenized(self, tps: Sequence[TokenizedPrompt]) -> List[Optional[np.ndarray]]:
         t_start = time.perf_counter()
         n = len(tps)
         groups = split_microbatches(tps, self.token_budget)
         batches = [pack_prompts([tps[i] for i in g], g, self.prefix_attention) for g in groups]
-        store = ActivationStore(self.storage, self.dev, self.disk_folder,
-                                tag=str(self.comm.rank) if self.comm.world > 1 else "",
-                                h2d_stream=self.h2d_stream, d2h_stream=self.d2h_stream)
+        metas = [b.device_tensors(self.dev) for b in batches]   # all uploads before any compute
+        store = self._get_store()
+        store.bytes_d2h = store.bytes_h2d = 0
         outputs: List[Optional[np.ndarray]] = [None] * n
         out_pending = []     # (batch, host tensor, event)
         comm = self.comm
@@ -123,73 +149,93 @@ class ShardedRunner:
         flops = 0.0
         compute_s = 0.0
         sends = []
+        h2d0 = pf.bytes_h2d
+        items = self.schedule(len(batches))
+        carry = {}                     # micro-batch -> device activation kept across a shard boundary
+        recvs = {}
+        cur_k = -1
+        W = None
         if self.my_shards:
             pf.prefetch(0)
-        for k, shard in enumerate(self.my_shards):
-            W = pf.acquire(k)
-            pf.prefetch(k + 1)
+        for idx, (k, b) in enumerate(items):
+            shard = self.my_shards[k]
             first, last = shard[0], shard[-1]
-            src_rank = self._owner(first - 1) if (mp and first > 0) else comm.rank
-            dst_rank = self._owner(last + 1) if (mp and last + 1 < self.L) else comm.rank
-            recvs = {}
-            if first > 0 and src_rank != comm.rank:
-                # post every receive of this shard up front (matches the sender's order)
-                for b, batch in enumerate(batches):
-                    buf = torch.empty(self._state_shape(first - 1, batch), dtype=self.act_dtype, device=self.dev)
-                    recvs[b] = (buf, comm.irecv(buf, src_rank))
-            for b, batch in enumerate(batches):
-                meta = batch.device_tensors(self.dev)
-                if first == 0:
-                    state = None
-                elif b in recvs:
-                    buf, work = recvs.pop(b)
-                    work.wait()
-                    state = buf
-                else:
-                    state = store.get(b)
-                    if b + 1 < len(batches):
-                        store.prefetch(b + 1)
-                tc = time.perf_counter()
-                for li in shard:
-                    name = self.names[li]
-                    state = run_layer(self.ctx, name, W[name], state, batch, meta)
-                    if layer_kind(name) == "decoder":
-                        flops += layer_flops(self.cfg, batch)
-                compute_s += time.perf_counter() - tc
-                if last == self.L - 1:
-                    out_pending.append(self._start_output_copy(batch, state))
-                elif dst_rank != comm.rank:
-                    st = state.contiguous()
-                    sends.append((st, comm.isend(st, dst_rank)))
-                else:
-                    store.put(b, state)
-                    if b == 0 and len(batches) > 1 and first != 0:
-                        pass
-                del state
-            if recvs:
-                raise RuntimeError("unconsumed receives")
-            pf.release(k)
-            # retire finished sends to bound memory
-            sends = [(t, w) for (t, w) in sends if not w.is_completed()]
+            if k != cur_k:
+                if cur_k >= 0:
+                    pf.release(cur_k)
+                    sends = [(t, w) for (t, w) in sends if not w.is_completed()]   # bound memory
+                W = pf.acquire(k)
+                pf.prefetch(k + 1)
+                cur_k = k
+                src_rank = self._owner(first - 1) if (mp and first > 0) else comm.rank
+                dst_rank = self._owner(last + 1) if (mp and last + 1 < self.L) else comm.rank
+                if first > 0 and src_rank != comm.rank:
+                    # post every receive of this shard up front (matches the sender's order)
+                    for bb, batch in enumerate(batches):
+                        buf = torch.empty(self._state_shape(first - 1, batch), dtype=self.act_dtype,
+                                          device=self.dev)
+                        recvs[bb] = (buf, comm.irecv(buf, src_rank))
+            batch, meta = batches[b], metas[b]
+            if first == 0:
+                state = None
+            elif b in recvs:
+                buf, work = recvs.pop(b)
+                work.wait()
+                state = buf
+            elif b in carry:
+                state = carry.pop(b)
+            else:
+                state = store.get(b)
+            # one-ahead activation prefetch (crosses shard boundaries)
+            if idx + 1 < len(items):
+                k2, b2 = items[idx + 1]
+                if self.my_shards[k2][0] > 0 and k2 == k:
+                    store.prefetch(b2)
+                elif k2 != k and idx + 2 < len(items):
+                    store.prefetch(items[idx + 2][1])
+            tc = time.perf_counter()
+            for li in shard:
+                name = self.names[li]
+                state = run_layer(self.ctx, name, W[name], state, batch, meta)
+                if layer_kind(name) == "decoder":
+                    flops += layer_flops(self.cfg, batch)
+            compute_s += time.perf_counter() - tc
+            nxt = items[idx + 1] if idx + 1 < len(items) else None
+            if last == self.L - 1:
+                out_pending.append(self._start_output_copy(batch, state))
+            elif dst_rank != comm.rank:
+                st = state.contiguous()
+                sends.append((st, comm.isend(st, dst_rank)))
+            elif nxt is not None and nxt[0] == k + 1 and nxt[1] == b and self.storage != "gpu":
+                carry[b] = state           # boundary micro-batch stays in HBM (zigzag)
+            else:
+                store.put(b, state)
+            del state
+        if cur_k >= 0:
+            pf.release(cur_k)
+        if recvs:
+            raise RuntimeError("unconsumed receives")
         for t, w in sends:
             w.wait()
         if self.cuda:
             torch.cuda.synchronize(self.dev)
-        for batch, host, ev in out_pending:
-            probs = host.numpy() if host.dtype != torch.bfloat16 else host.float().numpy()
+        for batch, host, ev, pool_buf in out_pending:
+            probs = host.numpy()
             r = 0
             for j, pid in enumerate(batch.prompt_ids):
                 ns = batch.n_suffix[j]
                 outputs[pid] = np.expand_dims(probs[r:r + ns].astype(np.float16, copy=True), axis=1)
                 r += ns
-        store.close()
+            if pool_buf is not None:
+                store.recycle_host(pool_buf)
+        store.clear()
         wall = time.perf_counter() - t_start
         self.stats = {
             "wall_s": wall, "compute_launch_s": compute_s,
             "tokens": float(sum(b.num_tokens for b in batches)),
             "padded_tokens": float(sum(b.padded_tokens for b in batches)),
             "decoder_flops": flops, "micro_batches": float(len(batches)),
-            "weight_wait_s": pf.wait_seconds, "weight_h2d_bytes": float(pf.bytes_h2d),
+            "weight_wait_s": pf.wait_seconds, "weight_h2d_bytes": float(pf.bytes_h2d - h2d0),
             "act_d2h_bytes": float(store.bytes_d2h), "act_h2d_bytes": float(store.bytes_h2d),
         }
         if self.verbose:
@@ -199,15 +245,21 @@ class ShardedRunner:
 
     def _start_output_copy(self, batch: PackedBatch, probs: torch.Tensor):
         if not self.cuda:
-            return batch, probs.detach().to(torch.float16).cpu(), None
-        host = torch.empty(probs.shape, dtype=probs.dtype, pin_memory=True)
+            return batch, probs.detach().to(torch.float16).cpu(), None, None
+        store = self._get_store()
+        nbytes = probs.numel() * probs.element_size()
+        pool_buf = store.host_buffer(nbytes)
+        host = pool_buf[:nbytes].view(probs.dtype).view(probs.shape)
         self.d2h_stream.wait_stream(torch.cuda.current_stream(self.dev))
         with torch.cuda.stream(self.d2h_stream):
             host.copy_(probs, non_blocking=True)
             probs.record_stream(self.d2h_stream)
             ev = torch.cuda.Event()
             ev.record(self.d2h_stream)
-        return batch, host, ev
+        return batch, host, ev, pool_buf
 
     def close(self):
         self.prefetcher.close()
+        if self._store is not None:
+            self._store.close()
+            self._store = None

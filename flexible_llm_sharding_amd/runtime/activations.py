@@ -95,6 +95,14 @@ class ActivationStore:
         with self.lock:
             self._pool[buf.numel()].append(buf)
 
+    def host_buffer(self, nbytes: int) -> torch.Tensor:
+        """A pooled pinned buffer (rounded up to 1 MiB buckets) for other D2H users."""
+        return self._get_host((nbytes + (1 << 20) - 1) >> 20 << 20)
+
+    def recycle_host(self, buf: torch.Tensor) -> None:
+        """Return a buffer obtained from :meth:`host_buffer` to the pool."""
+        self._put_host(buf)
+
     def path_for(self, key) -> str:
         return os.path.join(self.disk_folder, f"act{self.tag}-{int(key):05d}.npy")
 
@@ -205,9 +213,12 @@ class ActivationStore:
         fut, _ = self._inflight.pop(key, (None, None))
         if self.mode == "disk":
             if fut is None:
-                self.prefetch(key)
-                fut, _ = self._inflight.pop(key)
-            host = fut.result()
+                if e.write_fut is not None:
+                    e.write_fut.result()
+                host = self._get_host(int(np.prod(e.shape)) * torch.empty((), dtype=e.dtype).element_size())
+                self._read_npy_into(e.path, e.shape, e.dtype, host)
+            else:
+                host = fut.result()
         else:
             host = e.host
         nbytes = int(np.prod(e.shape)) * torch.empty((), dtype=e.dtype).element_size()

@@ -11,7 +11,6 @@ from __future__ import annotations
 
 import ctypes
 import os
-import weakref
 from typing import Dict
 
 import torch
@@ -37,9 +36,6 @@ class _PinnedOwner:
             pass
 
 
-_owners = weakref.WeakValueDictionary()
-
-
 def _gpu_present() -> bool:
     try:
         return torch.cuda.is_available()
@@ -48,19 +44,22 @@ def _gpu_present() -> bool:
 
 
 def alloc_host(nbytes: int, pinned: bool = True) -> torch.Tensor:
-    """uint8 CPU tensor of exactly ``nbytes`` (pinned when a GPU is present)."""
+    """uint8 CPU tensor of exactly ``nbytes`` (pinned when a GPU is present).
+
+    The pinned block is owned by a ctypes array object that every tensor view
+    keeps alive (``torch.frombuffer`` holds a reference), so the memory is
+    ``hipHostFree``d exactly when the last view dies.
+    """
     if pinned and _gpu_present():
         rt = _native.runtime_or_none()
         if rt is not None:
-            ptr = rt.fls_pinned_alloc(max(1, nbytes))
+            n = max(1, nbytes)
+            ptr = rt.fls_pinned_alloc(n)
             if ptr:
-                owner = _PinnedOwner(ptr, rt)
-                buf = (ctypes.c_uint8 * max(1, nbytes)).from_address(ptr)
-                t = torch.frombuffer(buf, dtype=torch.uint8)[:nbytes]
-                # keep the owner alive as long as the base tensor lives
-                t._fls_owner = owner  # type: ignore[attr-defined]
-                _owners[id(owner)] = owner
-                return t
+                arr_t = type("PinnedBlock", (ctypes.c_uint8 * n,), {})
+                arr = arr_t.from_address(ptr)
+                arr.owner = _PinnedOwner(ptr, rt)
+                return torch.frombuffer(arr, dtype=torch.uint8)[:nbytes]
         return torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
     return torch.empty(nbytes, dtype=torch.uint8)
 
@@ -135,6 +134,12 @@ def read_safetensors(path: str) -> Dict[str, torch.Tensor]:
     pread_into(path, lo, hi - lo, buf)
     out = {}
     for n, t in infos.items():
+        if not t.nbytes:
+            out[n] = torch.empty(t.shape, dtype=t.dtype)
+            continue
         v = buf[t.begin - lo:t.end - lo]
-        out[n] = v.view(t.dtype).view(t.shape) if t.nbytes else torch.empty(t.shape, dtype=t.dtype)
+        es = torch.empty((), dtype=t.dtype).element_size()
+        if (t.begin - lo) % es:
+            v = v.clone()          # misaligned tensor start: realign before the dtype view
+        out[n] = v.view(t.dtype).view(t.shape)
     return out
