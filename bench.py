@@ -12,9 +12,11 @@ memory before timing (no network, no checkpoint); prompts are synthetic text
 tokenized inside the timed step by a synthetic tokenizer.
 
 Scaling is weak: each GPU adds ``--prompts-per-gpu`` prompts.  N>1 runs the
-reference's default model-parallel schedule (shard k on GPU k mod N, RCCL
-send/recv of activations over xGMI; each GPU streams only its own shards) or
-``--mode dp``.
+data-parallel schedule (each GPU scores its own prompts; every layer is
+scatter-loaded 1/N per GPU over its own PCIe link and re-assembled in HBM by
+an RCCL all-gather over xGMI), or with ``--mode mp`` the reference's default
+model-parallel schedule (shard k on GPU k mod N, RCCL send/recv of
+activations; each GPU streams only its own shards).
 """
 from __future__ import annotations
 
@@ -53,11 +55,13 @@ def main(argv=None):
     ap.add_argument("--prefix-attention", default="bidirectional")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--cpu", action="store_true", help="CPU/gloo rehearsal of the same code path (tests only)")
     a = ap.parse_args(argv)
 
     from flexible_llm_sharding_amd.config import preset
     from flexible_llm_sharding_amd.engine import ShardedRunner
     from flexible_llm_sharding_amd.parallel.comm import Comm
+    from flexible_llm_sharding_amd.parallel.data_parallel import AllGatherPrefetcher, SlicedHostStore
     from flexible_llm_sharding_amd.parallel.planner import make_plan
     from flexible_llm_sharding_amd.runtime.weights import HostStore
     from flexible_llm_sharding_amd.utils.synthetic import synthetic_prompts
@@ -67,11 +71,15 @@ def main(argv=None):
     if world != a.gpus:
         if a.gpus > 1:
             raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch with torch.distributed.run")
-    comm = Comm.from_env("cuda")
+    comm = Comm.from_env("cpu" if a.cpu else "cuda")
     rank = comm.rank
-    dev = comm.device if world > 1 else torch.device("cuda", 0)
-    torch.cuda.set_device(dev)
-    mode = a.mode if a.mode != "auto" else ("mp" if world > 1 else "single")
+    if a.cpu:
+        dev = torch.device("cpu")
+    else:
+        dev = comm.device if world > 1 else torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+    sync = (lambda: None) if a.cpu else (lambda: torch.cuda.synchronize(dev))
+    mode = a.mode if a.mode != "auto" else ("dp" if world > 1 else "single")
     dp = mode == "dp"
 
     kw = {} if a.num_layers is None else {"num_hidden_layers": a.num_layers}
@@ -81,8 +89,13 @@ def main(argv=None):
     mine = sorted({i for sh in plan.my_shards for i in sh})
     t0 = time.perf_counter()
     log(rank, f"[bench] generating {len(mine)} random-init {a.model} layers on {dev} -> pinned host ...")
-    store = HostStore.synthetic(cfg, dev, seed=a.seed, names=[names[i] for i in mine],
-                                progress=lambda i, n: log(rank, f"[bench]   layer {i}/{n} ({time.perf_counter() - t0:.0f}s)"))
+    prog = lambda i, n: log(rank, f"[bench]   layer {i}/{n} ({time.perf_counter() - t0:.0f}s)")  # noqa: E731
+    if dp:
+        # scatter-load: this rank keeps 1/G of every layer; layers re-assembled by RCCL all-gather
+        store = SlicedHostStore.synthetic(cfg, dev, rank, world, seed=a.seed, names=[names[i] for i in mine],
+                                          progress=prog)
+    else:
+        store = HostStore.synthetic(cfg, dev, seed=a.seed, names=[names[i] for i in mine], progress=prog)
     log(rank, f"[bench] host store {store.total_bytes / 1e9:.1f} GB in {time.perf_counter() - t0:.1f}s")
 
     tok_dir = f"/tmp/fls_bench_tok_{os.getpid()}"
@@ -91,23 +104,29 @@ def main(argv=None):
     n_prompts = a.prompts_per_gpu * (world if mode == "mp" else 1)
     prompts = synthetic_prompts(n_prompts, a.prefix_len, a.n_suffix, a.suffix_len, cfg.vocab_size,
                                 seed=a.seed + (rank if dp else 0))
+    pf = None
+    if dp:
+        pf = AllGatherPrefetcher(store, names, [s for s in plan.my_shards if len(s)], dev, comm,
+                                 resident=a.resident)
     runner = ShardedRunner(cfg, store, dev, tok, layer_num_per_shard=a.lnps, storage_location=a.storage,
                            disk_folder=f"/tmp/fls_bench_spill_{rank}", prefix_attention=a.prefix_attention,
-                           token_budget=a.token_budget, resident=a.resident, comm=comm, data_parallel=dp)
-    torch.cuda.reset_peak_memory_stats(dev)
+                           token_budget=a.token_budget, resident=a.resident, comm=comm, data_parallel=dp,
+                           prefetcher=pf)
+    if not a.cpu:
+        torch.cuda.reset_peak_memory_stats(dev)
 
     for i in range(a.warmup):
         tw = time.perf_counter()
         runner(prompts)
         log(rank, f"[bench] warmup {i}: {time.perf_counter() - tw:.2f}s")
     comm.barrier()
-    torch.cuda.synchronize(dev)
+    sync()
     t_start = time.perf_counter()
     for i in range(a.steps):
         ts = time.perf_counter()
         runner(prompts)
         log(rank, f"[bench] step {i}: {time.perf_counter() - ts:.2f}s  stats={json.dumps({k: round(v, 3) for k, v in runner.stats.items()})}")
-    torch.cuda.synchronize(dev)
+    sync()
     comm.barrier()
     elapsed = time.perf_counter() - t_start
     elapsed = comm.all_reduce_max(elapsed)
@@ -117,13 +136,13 @@ def main(argv=None):
     if dp:
         tok_step = comm.all_reduce_sum(tok_step)
         padded_step = comm.all_reduce_sum(padded_step)
-    peak = comm.all_reduce_max(float(torch.cuda.max_memory_allocated(dev)))
+    peak = comm.all_reduce_max(0.0 if a.cpu else float(torch.cuda.max_memory_allocated(dev)))
     ms = elapsed / a.steps * 1000.0
     value = tok_step * a.steps / elapsed
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "tokens/s", "n_gpus": world,
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms, 2), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "fp16",
+        "scaling": "weak", "vs_baseline": None, "dtype": "fp32-cpu-rehearsal" if a.cpu else "fp16",
         "data": "synthetic prompts (synthetic tokenizer) + random-init Llama-2-70B weights in pinned host RAM",
         "peak_gpu_mem_gb": round(peak / 1e9, 3),
         "config": {"model": a.model if a.num_layers is None else f"{a.model}-L{a.num_layers}",
@@ -132,7 +151,8 @@ def main(argv=None):
                    "prefix_len": a.prefix_len, "n_suffix": a.n_suffix, "suffix_len": a.suffix_len,
                    "tokens_per_step": tok_step, "padded_tokens_per_step": padded_step,
                    "layer_num_per_shard": a.lnps, "storage_location": a.storage,
-                   "parallelism": (f"pp{world}-roundrobin" if mode == "mp" else (f"dp{world}" if dp else "single")),
+                   "parallelism": (f"pp{world}-roundrobin" if mode == "mp" else
+                                   (f"dp{world}-allgather-weights" if dp else "single")),
                    "resident": a.resident, "token_budget": a.token_budget},
     }
     if rank == 0:

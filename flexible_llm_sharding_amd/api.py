@@ -52,7 +52,7 @@ def build_source(args, cfg: ModelConfig, comm: Comm, device: torch.device):
 
 def build_runner(args, cfg: ModelConfig, device, comm: Comm, tok) -> ShardedRunner:
     device = torch.device(device)
-    if args.data_parallel and comm.world > 1 and args.dp_weight_shard and device.type == "cuda":
+    if args.data_parallel and comm.world > 1 and args.dp_weight_shard:
         from .parallel.data_parallel import build_dp_sharded_runner
         return build_dp_sharded_runner(args, cfg, device, comm, tok)
     src = build_source(args, cfg, comm, device)

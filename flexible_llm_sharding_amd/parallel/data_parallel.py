@@ -1,0 +1,158 @@
+"""Data parallelism with scatter-loaded, all-gathered layer weights.
+
+Reference DP (``/root/reference/utils.py:24-75, 122-124``): one host-RAM copy
+of the current layer shared by every GPU thread; each GPU then copies the
+whole layer over its own PCIe link (G x the host traffic) and the GPUs move
+in lock-step under a Condition/Lock pair (ABBA order).
+
+MI355X design: each rank keeps only ITS 1/G byte-slice of every packed layer
+in pinned host memory (138/G GB for 70B), DMAs that slice into HBM over its
+own PCIe link, and the full layer is re-assembled in the HBM weight slot by
+``all_gather_into_tensor`` — RCCL over the fully connected xGMI fabric
+(7 links per GPU) — on the copy side of the double buffer, so shard k+1's
+H2D + all-gather overlap shard k's compute.  Per layer and GPU the PCIe
+traffic drops G-fold; every rank issues the same collectives in the same
+order (no P2P ordering hazards, no polling).  Prompts are split with
+``np.array_split`` like ``main.py:69-70``; scores are gathered to rank 0.
+"""
+from __future__ import annotations
+
+import time
+from typing import Dict, List, Optional, Sequence
+
+import torch
+
+from ..models.layout import ALIGN_BYTES
+from ..runtime import hostmem
+from ..runtime.prefetch import ShardPrefetcher
+from ..runtime.weights import HostStore, LayerSource, shard_chunk_bytes
+from .comm import Comm
+
+
+def _align(n: int) -> int:
+    return (n + ALIGN_BYTES - 1) // ALIGN_BYTES * ALIGN_BYTES
+
+
+class SlicedHostStore(HostStore):
+    """Rank ``rank``'s byte slice of every packed layer (pinned)."""
+
+    def __init__(self, cfg, rank: int, world: int, dtype=torch.float16, pinned=True, names=None):
+        super().__init__(cfg, dtype, pinned, names)
+        self.rank, self.world = rank, world
+
+    def chunk_bytes(self, name: str) -> int:
+        return shard_chunk_bytes(self.nbytes(name), self.world)
+
+    def read_into(self, name: str, dst: torch.Tensor) -> None:   # pragma: no cover - not a full source
+        raise RuntimeError("a sliced store holds only 1/G of each layer")
+
+    @classmethod
+    def from_source(cls, src: LayerSource, rank: int, world: int, pinned: bool = True,
+                    names: Optional[Sequence[str]] = None) -> "SlicedHostStore":
+        st = cls(src.cfg, rank, world, src.dtype, pinned, names)
+        full = None
+        for n in st.names:
+            nb = st.nbytes(n)
+            if full is None or full.numel() < nb:
+                full = torch.empty(max(nb, max(st.nbytes(x) for x in st.names)), dtype=torch.uint8)
+            src.read_into(n, full)
+            c = st.chunk_bytes(n)
+            buf = hostmem.alloc_host(c, pinned=pinned)
+            lo, hi = rank * c, min(nb, (rank + 1) * c)
+            if hi > lo:
+                buf[:hi - lo].copy_(full[lo:hi])
+            st.buffers[n] = buf
+        return st
+
+    @classmethod
+    def synthetic(cls, cfg, device, rank: int, world: int, seed: int = 0, std: float = 0.02,
+                  pinned: bool = True, names=None, progress=None) -> "SlicedHostStore":
+        base = HostStore.synthetic(cfg, device, seed=seed, std=std, pinned=pinned, names=names,
+                                   byte_range=(rank, world), progress=progress)
+        st = cls(cfg, rank, world, torch.float16, pinned, names)
+        st.buffers = base.buffers
+        return st
+
+
+class AllGatherPrefetcher(ShardPrefetcher):
+    """Shard prefetcher whose H2D moves only this rank's slice; the layer is
+    completed in HBM with one all-gather per layer over xGMI."""
+
+    def __init__(self, store: SlicedHostStore, layer_names, shards, device, comm: Comm,
+                 n_slots: int = 2, resident: bool = False):
+        self.comm = comm
+        self.store = store
+        super().__init__(store, layer_names, shards, device, n_slots=n_slots, resident=resident)
+        self._pool = None                     # slices are host-resident: no loader thread
+        self._chunks: Dict[tuple, torch.Tensor] = {}
+
+    def shard_bytes(self, k: int) -> int:
+        G = self.comm.world
+        return sum(_align(self.store.chunk_bytes(self.names[i]) * G) for i in self.shards[k])
+
+    def _chunk_buf(self, s: int, j: int, nbytes: int) -> torch.Tensor:
+        key = (s, j)
+        b = self._chunks.get(key)
+        if b is None or b.numel() < nbytes:
+            b = torch.empty(nbytes, dtype=torch.uint8, device=self.dev)
+            self._chunks[key] = b
+        return b
+
+    def _load(self, k: int):
+        t0 = time.perf_counter()
+        s = self.slot_of(k)
+        slot = self._slot(s)
+        G = self.comm.world
+        views: Dict[str, Dict[str, torch.Tensor]] = {}
+        works: List = []
+        ctx = torch.cuda.stream(self.copy_stream) if self.cuda else _nullctx()
+        with ctx:
+            if self.cuda and self._free_ev[s] is not None:
+                self.copy_stream.wait_event(self._free_ev[s])
+            off = 0
+            for j, i in enumerate(self.shards[k]):
+                name = self.names[i]
+                nb = self.store.nbytes(name)
+                c = self.store.chunk_bytes(name)
+                region = slot[off:off + c * G]
+                cb = self._chunk_buf(s, j, c)[:c]
+                cb.copy_(self.store.buffers[name][:c], non_blocking=self.cuda)
+                w = self.comm.all_gather_into(region, cb, async_op=self.cuda)
+                if self.cuda:
+                    works.append(w)
+                views[name] = self.store.layout(name).views(region[:nb], self.dtype)
+                off += _align(c * G)
+                self.bytes_h2d += c
+        self.load_seconds += time.perf_counter() - t0
+        return works, views, s
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def build_dp_sharded_runner(args, cfg, device, comm: Comm, tok, store: Optional[SlicedHostStore] = None):
+    from ..engine import ShardedRunner
+    from ..runtime.weights import FileLayerSource
+    from .planner import make_plan
+    device = torch.device(device)
+    if store is None:
+        store = SlicedHostStore.from_source(FileLayerSource(cfg, args.model_path), comm.rank, comm.world,
+                                            pinned=device.type == "cuda")
+    names = cfg.layer_names()
+    plan = make_plan(len(names), args.layer_num_per_shard, comm.world, comm.rank, True)
+    shards = [s for s in plan.my_shards if len(s)]
+    pf = AllGatherPrefetcher(store, names, shards, device, comm, resident=getattr(args, "resident", False))
+    act = None
+    if getattr(args, "dtype", None):
+        act = torch.float16 if args.dtype == "float16" else torch.float32
+    return ShardedRunner(cfg, store, device, tok, layer_num_per_shard=args.layer_num_per_shard,
+                         storage_location=args.storage_location, disk_folder=args.disk_folder,
+                         max_activation_in_cpu=args.max_activation_in_cpu,
+                         prefix_attention=args.prefix_attention, token_budget=args.token_budget,
+                         resident=getattr(args, "resident", False), comm=comm, data_parallel=True,
+                         act_dtype=act, prefetcher=pf, verbose=getattr(args, "verbose", False))

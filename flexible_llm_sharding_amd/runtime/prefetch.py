@@ -164,7 +164,10 @@ class ShardPrefetcher:
             with self.lock:
                 self._ready[k] = r
         ev, views, _ = self._ready[k]
-        if ev is not None:
+        if isinstance(ev, list):          # collective works (data-parallel all-gather)
+            for w in ev:
+                w.wait()
+        elif ev is not None:
             torch.cuda.current_stream(self.dev).wait_event(ev)
         if self.resident:
             self._loaded_resident.add(k)

@@ -1,0 +1,103 @@
+"""main.py / prepare_weights.py CLI parity (reference main.py:30-98, prepare_weights.py:56-62)."""
+import os
+import pickle
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from flexible_llm_sharding_amd.api import batch_ranges
+from flexible_llm_sharding_amd.utils.cli import parse_args
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_reference_flags_and_defaults():
+    a = parse_args(["--prompt_pickle", "p.pkl", "--output_file", "o.pkl"])
+    assert a.model_path == "./" and a.num_batch == 1 and a.layer_num_per_shard == 1
+    assert a.storage_location == "cpu" and a.max_activation_in_cpu == 100
+    assert a.data_parallel is False and a.disk_folder == "./temp" and a.num_gen_token == 1
+    with pytest.raises(SystemExit):
+        parse_args(["--output_file", "o.pkl"])          # prompt_pickle required
+
+
+@pytest.mark.parametrize("val,exp", [("True", True), ("False", False), ("1", True), ("0", False)])
+def test_data_parallel_bool(val, exp):
+    # reference type=bool turned "False" into True; we parse it as a boolean
+    a = parse_args(["--prompt_pickle", "p", "--output_file", "o", "--data_parallel", val])
+    assert a.data_parallel is exp
+    a = parse_args(["--prompt_pickle", "p", "--output_file", "o", "--data_parallel"])
+    assert a.data_parallel is True
+
+
+def test_batch_ranges_matches_reference():
+    for n in range(0, 23):
+        for nb in range(1, 6):
+            ends = [n // nb * i for i in range(1, nb)] + [n]
+            ref = list(zip([0] + ends[:-1], ends))
+            assert batch_ranges(n, nb) == ref
+
+
+def _run(args, cwd):
+    env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "main.py")] + args, cwd=cwd, env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return r
+
+
+@pytest.mark.parametrize("storage,lnps,nb", [("cpu", 1, 1), ("disk", 2, 2), ("gpu", 100, 3)])
+def test_main_end_to_end(tiny_model, tmp_path, storage, lnps, nb):
+    from flexible_llm_sharding_amd.utils.synthetic import synthetic_prompts
+    path, cfg = tiny_model
+    prompts = synthetic_prompts(5, 15, 3, 4, cfg.vocab_size, seed=4, vary=True)
+    pp = tmp_path / "prompts.pkl"
+    pickle.dump(prompts, open(pp, "wb"))
+    out = tmp_path / "scores.pkl"
+    _run(["--model_path", path, "--prompt_pickle", str(pp), "--output_file", str(out),
+          "--num_gen_token", "3", "--layer_num_per_shard", str(lnps), "--storage_location", storage,
+          "--num_batch", str(nb), "--disk_folder", str(tmp_path / "spill")], str(tmp_path))
+    scores = pickle.load(open(out, "rb"))
+    assert len(scores) == 5
+    for (pre, sufs), s in zip(prompts, scores):
+        assert s.shape == (len(sufs), 3, cfg.vocab_size) and s.dtype == np.float16
+        assert np.allclose(s.astype(np.float32).sum(-1), 1.0, atol=2e-2)
+    upd = pickle.load(open(tmp_path / "prompts_updated.pkl", "rb"))
+    assert isinstance(upd, list) and len(upd) == 5
+    for (pre, sufs), (pre2, sufs2) in zip(prompts, upd):
+        assert pre2 == pre and all(b.startswith(a) and len(b) > len(a) for a, b in zip(sufs, sufs2))
+
+
+def test_generation_is_greedy_rerun(tiny_model, tmp_path):
+    """Step t's scores equal a fresh scoring of the prompts extended by steps < t (main.py:85-90)."""
+    from flexible_llm_sharding_amd.engine import ShardedRunner
+    from flexible_llm_sharding_amd.runtime.weights import FileLayerSource
+    from flexible_llm_sharding_amd.utils.synthetic import synthetic_prompts
+    from flexible_llm_sharding_amd.utils.tokenizer import load_tokenizer
+    path, cfg = tiny_model
+    prompts = synthetic_prompts(2, 12, 2, 3, cfg.vocab_size, seed=9)
+    pp = tmp_path / "p.pkl"
+    pickle.dump(prompts, open(pp, "wb"))
+    _run(["--model_path", path, "--prompt_pickle", str(pp), "--output_file", str(tmp_path / "s.pkl"),
+          "--num_gen_token", "2"], str(tmp_path))
+    scores = pickle.load(open(tmp_path / "s.pkl", "rb"))
+    tok = load_tokenizer(path)
+    r = ShardedRunner(cfg, FileLayerSource(cfg, path), "cpu", tok)
+    ext = []
+    for (pre, sufs), s in zip(prompts, scores):
+        t0 = np.argmax(s[:, :1], -1)
+        ext.append((pre, tuple(a + tok.decode(t) for a, t in zip(sufs, t0))))
+    step1 = r(ext)
+    for s, o in zip(scores, step1):
+        assert np.abs(s[:, 1].astype(np.float32) - o[:, 0].astype(np.float32)).max() < 1e-3
+
+
+def test_prepare_weights_synthetic_cli(tmp_path):
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "prepare_weights.py"), "tiny", str(tmp_path / "m"),
+                        "--synthetic", "--num_hidden_layers", "1"], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr
+    files = sorted(os.listdir(tmp_path / "m"))
+    assert "model.layers.0.safetensors" in files and "lm_head.safetensors" in files and "config.json" in files

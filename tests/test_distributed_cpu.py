@@ -90,3 +90,39 @@ def test_data_parallel(single, tmp_path, world):
     assert len(got) == len(ref)
     for a, b in zip(got, ref):
         assert _close(a, b)
+
+
+def _dp_shard_worker(rank, world, port, path, prompts, lnps, out_dir):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    torch.set_num_threads(1)
+    from types import SimpleNamespace
+    from flexible_llm_sharding_amd.config import ModelConfig
+    from flexible_llm_sharding_amd.parallel.comm import Comm
+    from flexible_llm_sharding_amd.parallel.data_parallel import build_dp_sharded_runner
+    from flexible_llm_sharding_amd.utils.tokenizer import load_tokenizer
+    comm = Comm.from_env("cpu", timeout_s=120)
+    cfg = ModelConfig.from_pretrained(path)
+    args = SimpleNamespace(model_path=path, layer_num_per_shard=lnps, storage_location="cpu",
+                           disk_folder=out_dir, max_activation_in_cpu=100, prefix_attention="bidirectional",
+                           token_budget=50, resident=False, dtype=None, verbose=False)
+    r = build_dp_sharded_runner(args, cfg, "cpu", comm, load_tokenizer(path))
+    assert r.prefetcher.__class__.__name__ == "AllGatherPrefetcher"
+    idx = np.array_split(np.arange(len(prompts)), world)[rank]
+    outs = r([prompts[i] for i in idx])
+    allv = comm.gather_object(outs, dst=0)
+    if rank == 0:
+        with open(os.path.join(out_dir, "out.pkl"), "wb") as f:
+            pickle.dump(allv, f)
+    comm.destroy()
+
+
+@pytest.mark.parametrize("world,lnps", [(2, 1), (3, 2)])
+def test_data_parallel_sharded_weights(single, tmp_path, world, lnps):
+    path, prompts, ref = single
+    mp.start_processes(_dp_shard_worker, args=(world, _port(), path, prompts, lnps, str(tmp_path)),
+                       nprocs=world, start_method="spawn", join=True)
+    got = sum(pickle.load(open(tmp_path / "out.pkl", "rb")), [])
+    assert len(got) == len(ref)
+    for a, b in zip(got, ref):
+        assert _close(a, b)
