@@ -27,6 +27,8 @@
 #include "common.h"
 #include "fls.h"
 
+#include <cstdlib>
+
 namespace {
 
 constexpr int BM = 256, BN = 256, BK = 64, NT = 512;
@@ -255,17 +257,174 @@ __global__ __launch_bounds__(256) void gemm_nt_generic(const half_t* __restrict_
   }
 }
 
+// ------------------------------------------------------------------ v3
+// Ping-pong: the 8 waves form two groups (waves 0-3 / 4-7; the hardware puts
+// one wave of each group on every SIMD).  Group 1 runs one barrier-slot
+// behind group 0, so in every slot one wave per SIMD issues the 64 MFMAs of
+// a whole 256x256x64 K-tile (1024 matrix-pipe cycles) while its partner
+// reads its next K-tile's fragments from LDS and issues LDS-DMA for the tile
+// after — the matrix pipe alternates between the two waves instead of both
+// waves reading, then both computing.
+//   group 0, K-tile t: [R(t) + DMA(t+1)] bar [M(t) + vmcnt(0)] bar
+//   group 1, K-tile t: [M(t-1) + DMA(t+1)] bar [R(t) + vmcnt(0) + lgkmcnt(0)] bar
+// DMA(t+1) overwrites buffer (t+1)%2 whose last reader (group 1, slot 2t-1)
+// retired its reads before that slot's barrier; K-tile t+1 is waited for by
+// every issuing wave before the barrier ending slot 2t+1 and first read in
+// slot 2t+2 — both by barrier count, independent of timing.
+namespace v3 {
+__device__ __forceinline__ void bar() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+}  // namespace v3
+
+template <int EPI>
+__global__ __launch_bounds__(NT, 2) void gemm_nt_v3(const half_t* __restrict__ A, const half_t* __restrict__ W,
+                                                   half_t* __restrict__ C, int M, int N, int K, int lda, int ldw,
+                                                   int ldc, Epi ep) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp_id = wave >> 2;             // ping-pong group (== wm)
+
+  const int nwg = gridDim.x;
+  int bid = blockIdx.x;
+  {
+    const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7, loc = bid >> 3;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+  }
+  const int tiles_m = (M + BM - 1) / BM;
+  const int tiles_n = N / BN;
+  constexpr int GROUP_M = 8;
+  const int group = bid / (GROUP_M * tiles_n);
+  const int first_m = group * GROUP_M;
+  const int gsz = min(tiles_m - first_m, GROUP_M);
+  const int in_g = bid - group * GROUP_M * tiles_n;
+  const int tm = first_m + in_g % gsz;
+  const int tn = in_g / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // staging pointers: one per-lane base per operand; the 4 pieces of a wave are 8 rows apart
+  const int lr = lane >> 3;
+  const int lc = (lane & 7) ^ lr;
+  const half_t* wbase = W + (size_t)(n0 + wave * 32 + lr) * ldw + lc * 8;
+  const int xrow0 = m0 + wave * 32 + lr;
+  const half_t* xcol = A + lc * 8;
+#define V3_STAGE(buf, k0)                                                                 \
+  {                                                                                       \
+    char* base_ = smem + (buf) * STAGE_BYTES;                                             \
+    _Pragma("unroll") for (int j_ = 0; j_ < 4; ++j_)                                      \
+      glds16(wbase + (size_t)(j_ * 8) * ldw + (k0), base_ + (wave * 4 + j_) * 1024);      \
+    _Pragma("unroll") for (int j_ = 0; j_ < 4; ++j_)                                      \
+      glds16(xcol + (size_t)min(xrow0 + j_ * 8, M - 1) * lda + (k0),                      \
+             base_ + TILE_BYTES + (wave * 4 + j_) * 1024);                                \
+  }
+
+  const int wn = wave & 3, wm = wave >> 2;
+  const int fr = lane & 15, grp = lane >> 4;
+  const int swz = lane & 7;
+  const int wrow = (wn * 64 + fr) * 128;
+  const int xrow = TILE_BYTES + (wm * 128 + fr) * 128;
+  const int ch0 = ((0 * 4 + grp) ^ swz) << 4;
+  const int ch1 = ((1 * 4 + grp) ^ swz) << 4;
+
+  floatx4 acc[8][4];
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[u][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  half8 wf0[4], wf1[4], xf0[8], xf1[8];   // k-halves 0/1 of the wave's K-tile fragments
+
+#define V3_READ(buf)                                                                      \
+  {                                                                                       \
+    const char* b_ = smem + (buf) * STAGE_BYTES;                                          \
+    _Pragma("unroll") for (int t_ = 0; t_ < 4; ++t_) wf0[t_] = *(const half8*)(b_ + wrow + t_ * 2048 + ch0); \
+    _Pragma("unroll") for (int u_ = 0; u_ < 8; ++u_) xf0[u_] = *(const half8*)(b_ + xrow + u_ * 2048 + ch0); \
+    _Pragma("unroll") for (int t_ = 0; t_ < 4; ++t_) wf1[t_] = *(const half8*)(b_ + wrow + t_ * 2048 + ch1); \
+    _Pragma("unroll") for (int u_ = 0; u_ < 8; ++u_) xf1[u_] = *(const half8*)(b_ + xrow + u_ * 2048 + ch1); \
+  }
+#define V3_MMA()                                                                          \
+  {                                                                                       \
+    __builtin_amdgcn_s_setprio(1);                                                        \
+    _Pragma("unroll") for (int u_ = 0; u_ < 8; ++u_)                                      \
+    _Pragma("unroll") for (int t_ = 0; t_ < 4; ++t_)                                      \
+      acc[u_][t_] = mfma16x16x32(wf0[t_], xf0[u_], acc[u_][t_]);                          \
+    _Pragma("unroll") for (int u_ = 0; u_ < 8; ++u_)                                      \
+    _Pragma("unroll") for (int t_ = 0; t_ < 4; ++t_)                                      \
+      acc[u_][t_] = mfma16x16x32(wf1[t_], xf1[u_], acc[u_][t_]);                          \
+    __builtin_amdgcn_s_setprio(0);                                                        \
+  }
+
+  const int nk = K / BK;
+  V3_STAGE(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  v3::bar();
+  if (grp_id == 0) {
+    for (int t = 0; t < nk; ++t) {
+      V3_READ(t & 1);
+      if (t + 1 < nk) V3_STAGE((t + 1) & 1, (t + 1) * BK);
+      v3::bar();
+      V3_MMA();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      v3::bar();
+    }
+  } else {
+    for (int t = 0; t < nk; ++t) {
+      if (t > 0) V3_MMA();
+      if (t + 1 < nk) V3_STAGE((t + 1) & 1, (t + 1) * BK);
+      v3::bar();
+      V3_READ(t & 1);
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      v3::bar();
+    }
+    V3_MMA();
+  }
+#undef V3_MMA
+#undef V3_READ
+#undef V3_STAGE
+
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int m = m0 + wm * 128 + u * 16 + fr;
+    if (m < M) {
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+        store_pair<EPI>(C, ldc, m, n0 + wn * 64 + p * 32, grp, acc[u][2 * p], acc[u][2 * p + 1], ep);
+    }
+  }
+}
+
+int g_variant = -1;   // -1: from env FLS_GEMM_VARIANT (default 3)
+
+int variant() {
+  if (g_variant < 0) {
+    const char* e = getenv("FLS_GEMM_VARIANT");
+    g_variant = e ? atoi(e) : 3;
+  }
+  return g_variant;
+}
+
 template <int EPI>
 int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int lda, int ldw, int ldc,
            const Epi& ep, hipStream_t s) {
+  const int var = variant();
   const bool fast = (N % BN == 0) && (K % BK == 0) && (lda % 8 == 0) && (ldw % 8 == 0) && M > 0;
-  if (fast) {
+  const int tiles = ((M + BM - 1) / BM) * (N / BN);
+  if (var == 3 && fast) {
+    static bool attr3 = false;
+    if (!attr3) {
+      (void)hipFuncSetAttribute((const void*)gemm_nt_v3<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+      attr3 = true;
+    }
+    hipLaunchKernelGGL(gemm_nt_v3<EPI>, dim3(tiles), dim3(NT), LDS_BYTES, s, A, W, C, M, N, K, lda, ldw, ldc, ep);
+  } else if (var >= 1 && fast) {
     static bool attr_set = false;
     if (!attr_set) {
       (void)hipFuncSetAttribute((const void*)gemm_nt_256x256<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
       attr_set = true;
     }
-    const int tiles = ((M + BM - 1) / BM) * (N / BN);
     hipLaunchKernelGGL(gemm_nt_256x256<EPI>, dim3(tiles), dim3(NT), LDS_BYTES, s, A, W, C, M, N, K, lda, ldw, ldc, ep);
   } else {
     dim3 grid((M + 31) / 32, (N + 255) / 256);
@@ -277,7 +436,14 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
 
 }  // namespace
 
-extern "C" int fls_kernels_version(void) { return 1; }
+extern "C" int fls_kernels_version(void) { return 2; }
+
+// select the GEMM main-loop variant (0 generic, 1 = 256x256x64 2-stage, 3 = ping-pong 2-stage)
+extern "C" int fls_gemm_set_variant(int v) {
+  const int old = variant();
+  g_variant = v;
+  return old;
+}
 
 extern "C" int fls_gemm(const void* A, const void* W, void* C, const void* R, int M, int N, int K, int lda, int ldw,
                         int ldc, int ldr, int epi, const int* pos, const float* cos_t, const float* sin_t,

@@ -121,6 +121,9 @@ def _device_for(args, comm: Comm) -> torch.device:
 
 
 def run_rank(args, comm: Comm) -> Optional[dict]:
+    if getattr(args, "profile", False):
+        from .utils import trace
+        trace.enable(True)
     device = _device_for(args, comm)
     if args.storage_location == "disk":
         os.makedirs(args.disk_folder, exist_ok=True)

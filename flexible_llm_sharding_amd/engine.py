@@ -41,6 +41,7 @@ from .runtime.activations import ActivationStore
 from .runtime.batch import PackedBatch, pack_prompts, split_microbatches
 from .runtime.prefetch import ShardPrefetcher
 from .runtime.weights import LayerSource
+from .utils import trace
 from .utils.tokenizer import TokenizedPrompt, tokenize_prompts
 
 
@@ -164,8 +165,10 @@ class ShardedRunner:
                 if cur_k >= 0:
                     pf.release(cur_k)
                     sends = [(t, w) for (t, w) in sends if not w.is_completed()]   # bound memory
-                W = pf.acquire(k)
-                pf.prefetch(k + 1)
+                with trace.range(f"shard{k}:acquire"):
+                    W = pf.acquire(k)
+                with trace.range(f"shard{k + 1}:prefetch"):
+                    pf.prefetch(k + 1)
                 cur_k = k
                 src_rank = self._owner(first - 1) if (mp and first > 0) else comm.rank
                 dst_rank = self._owner(last + 1) if (mp and last + 1 < self.L) else comm.rank
@@ -194,11 +197,12 @@ class ShardedRunner:
                 elif k2 != k and idx + 2 < len(items):
                     store.prefetch(items[idx + 2][1])
             tc = time.perf_counter()
-            for li in shard:
-                name = self.names[li]
-                state = run_layer(self.ctx, name, W[name], state, batch, meta)
-                if layer_kind(name) == "decoder":
-                    flops += layer_flops(self.cfg, batch)
+            with trace.range(f"shard{k}:mb{b}:compute"):
+                for li in shard:
+                    name = self.names[li]
+                    state = run_layer(self.ctx, name, W[name], state, batch, meta)
+                    if layer_kind(name) == "decoder":
+                        flops += layer_flops(self.cfg, batch)
             compute_s += time.perf_counter() - tc
             nxt = items[idx + 1] if idx + 1 < len(items) else None
             if last == self.L - 1:

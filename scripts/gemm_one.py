@@ -1,0 +1,31 @@
+"""Run one GEMM shape for profiling (rocprofv3 --pmc): python scripts/gemm_one.py VARIANT [M N K] [iters]"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from flexible_llm_sharding_amd.ops.hip_backend import HipOps, EPI_NONE  # noqa: E402
+
+
+def main():
+    var = int(sys.argv[1])
+    M, N, K = (int(x) for x in sys.argv[2:5]) if len(sys.argv) >= 5 else (16128, 57344, 8192)
+    iters = int(sys.argv[5]) if len(sys.argv) >= 6 else 10
+    dev = torch.device("cuda", 0)
+    ops = HipOps()
+    ops.k.fls_gemm_set_variant(var)
+    x = (torch.rand(M, K, device=dev) * 2 - 1).half()
+    w = ((torch.rand(N, K, device=dev) * 2 - 1) * 0.02).half()
+    out = torch.empty(M, N, dtype=torch.float16, device=dev)
+    for _ in range(iters):
+        ops.gemm(x, w, EPI_NONE, out=out)
+    torch.cuda.synchronize()
+    if var == 0:
+        for _ in range(iters):
+            torch.matmul(x, w.t(), out=out)
+        torch.cuda.synchronize()
+
+
+if __name__ == "__main__":
+    main()

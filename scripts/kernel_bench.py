@@ -55,11 +55,21 @@ def main():
             kw = dict(out=r, resid=r)
         if epi == EPI_ROPE:
             kw = dict(positions=pos, cos=cos, sin=sin, rope_cols=(nh + nkv) * hd, head_dim=hd)
-        t = timeit(lambda: ops.gemm(x, w, epi, **kw), a.iters)
-        tl = timeit(lambda: torch.matmul(x, w.t()), a.iters)
         fl = 2.0 * m * N * K
-        row = {"op": name, "M": m, "N": N, "K": K, "ours_ms": t * 1e3, "ours_tflops": fl / t / 1e12,
-               "hipblaslt_ms": tl * 1e3, "hipblaslt_tflops": fl / tl / 1e12}
+        row = {"op": name, "M": m, "N": N, "K": K}
+        # correctness of each variant vs hipBLASLt (plain epilogue)
+        ref = torch.matmul(x, w.t()).float()
+        for var in (1, 3):
+            ops.k.fls_gemm_set_variant(var)
+            y = ops.gemm(x, w)
+            err = ((y.float() - ref).norm() / ref.norm()).item()
+            t = timeit(lambda: ops.gemm(x, w, epi, **kw), a.iters)
+            row[f"v{var}_ms"] = t * 1e3
+            row[f"v{var}_tflops"] = fl / t / 1e12
+            row[f"v{var}_relerr"] = err
+        ops.k.fls_gemm_set_variant(3)
+        tl = timeit(lambda: torch.matmul(x, w.t()), a.iters)
+        row.update({"hipblaslt_ms": tl * 1e3, "hipblaslt_tflops": fl / tl / 1e12})
         res.append(row)
         print(json.dumps(row), flush=True)
     # attention: 12 prompts of prefix 1024 + 5 x 64 suffixes
