@@ -93,7 +93,9 @@ __device__ __forceinline__ void store_pair(half_t* __restrict__ C, int ldc, int 
   }
 }
 
-template <int EPI>
+// ABL (ablation, microbenchmarks only): bit0 = no LDS-DMA in the K loop,
+// bit1 = no fragment ds_reads (stale registers), bit2 = no MFMAs.
+template <int EPI, int ABL = 0>
 __global__ __launch_bounds__(NT, 2) void gemm_nt_256x256(const half_t* __restrict__ A, const half_t* __restrict__ W,
                                                         half_t* __restrict__ C, int M, int N, int K, int lda, int ldw,
                                                         int ldc, Epi ep) {
@@ -158,23 +160,41 @@ __global__ __launch_bounds__(NT, 2) void gemm_nt_256x256(const half_t* __restric
   stage(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  half8 wf[4], xf[8];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) wf[t] = half8{};
+#pragma unroll
+  for (int u = 0; u < 8; ++u) xf[u] = half8{};
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * BK);
+    if (!(ABL & 1) && kt + 1 < nk) stage(cur ^ 1, (kt + 1) * BK);
     const char* Ws = smem + cur * STAGE_BYTES;
     const char* Xs = Ws + TILE_BYTES;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int ch = ((s * 4 + grp) ^ swz) << 4;
-      half8 wf[4], xf[8];
+      if (!(ABL & 2)) {
 #pragma unroll
-      for (int t = 0; t < 4; ++t) wf[t] = *(const half8*)(Ws + (wrow0 + t * 16) * 128 + ch);
+        for (int t = 0; t < 4; ++t) wf[t] = *(const half8*)(Ws + (wrow0 + t * 16) * 128 + ch);
 #pragma unroll
-      for (int u = 0; u < 8; ++u) xf[u] = *(const half8*)(Xs + (xrow0 + u * 16) * 128 + ch);
+        for (int u = 0; u < 8; ++u) xf[u] = *(const half8*)(Xs + (xrow0 + u * 16) * 128 + ch);
+      } else {
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
+        for (int t = 0; t < 4; ++t) asm volatile("" : "+v"(wf[t]));
 #pragma unroll
-        for (int t = 0; t < 4; ++t) acc[u][t] = mfma16x16x32(wf[t], xf[u], acc[u][t]);
+        for (int u = 0; u < 8; ++u) asm volatile("" : "+v"(xf[u]));
+      }
+      if (!(ABL & 4)) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) acc[u][t] = mfma16x16x32(wf[t], xf[u], acc[u][t]);
+      } else {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) asm volatile("" :: "v"(wf[t]));
+#pragma unroll
+        for (int u = 0; u < 8; ++u) asm volatile("" :: "v"(xf[u]));
+      }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -396,6 +416,164 @@ __global__ __launch_bounds__(NT, 2) void gemm_nt_v3(const half_t* __restrict__ A
   }
 }
 
+// ------------------------------------------------------------------ v4
+// Latency-hiding ring.  The ablation (scripts/gemm_ablate.py) shows the
+// 2-stage loop is bound by LDS-DMA latency: ~64 KiB per CU in flight, ~1.5 us
+// per K-step under full-chip load, while MFMA alone would run at 2.2 PF.
+// v4 keeps up to 4 BK=32 tiles (128 KiB) in flight in a 5-stage ring that
+// uses the whole 160 KiB LDS: tile t+4 is issued while tile t computes and
+// the loop only ever waits for tile t+2 (`s_waitcnt vmcnt(8)`, never a
+// drain in steady state; raw s_barrier so no implicit vmcnt(0)).
+// Fragments are register double-buffered: the ds_reads of tile t+1 are
+// issued between the two MFMA halves of tile t.
+// LDS image per operand per stage: [256 rows][32 k] fp16 (64-B rows); 16-B
+// chunk c of row r stored at c ^ G[(r >> 2) & 3], G = {0,2,3,1}
+// (conflict-free for every ds_read_b128 lane group of the fragment read).
+namespace v4 {
+constexpr int BK4 = 32, NSTAGE = 5;
+constexpr int OP_BYTES = 256 * BK4 * 2;      // 16 KiB per operand per stage
+constexpr int STAGE4 = 2 * OP_BYTES;          // 32 KiB
+constexpr int LDS4 = NSTAGE * STAGE4;         // 160 KiB (the whole CU LDS)
+__device__ __forceinline__ int swz_g(int q) { return (0x1320 >> (q * 4)) & 0xF; }
+__device__ __forceinline__ void bar() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+}  // namespace v4
+
+template <int EPI>
+__global__ __launch_bounds__(NT, 2) void gemm_nt_v4(const half_t* __restrict__ A, const half_t* __restrict__ W,
+                                                   half_t* __restrict__ C, int M, int N, int K, int lda, int ldw,
+                                                   int ldc, Epi ep) {
+  using namespace v4;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  const int nwg = gridDim.x;
+  int bid = blockIdx.x;
+  {
+    const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7, loc = bid >> 3;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+  }
+  const int tiles_m = (M + BM - 1) / BM;
+  const int tiles_n = N / BN;
+  constexpr int GROUP_M = 8;
+  const int group = bid / (GROUP_M * tiles_n);
+  const int first_m = group * GROUP_M;
+  const int gsz = min(tiles_m - first_m, GROUP_M);
+  const int in_g = bid - group * GROUP_M * tiles_n;
+  const int tm = first_m + in_g % gsz;
+  const int tn = in_g / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // staging: a 1 KiB LDS-DMA piece = 16 rows x 64 B; a wave fills 2 pieces per operand per tile
+  const int lr = lane >> 2;
+  const int lc = (lane & 3) ^ swz_g(lr >> 2);
+  const half_t* wbase = W + (size_t)(n0 + wave * 32 + lr) * ldw + lc * 8;
+  const int xrow0 = m0 + wave * 32 + lr;
+  const half_t* xcol = A + lc * 8;
+#define V4_STAGE(st, k0)                                                                  \
+  {                                                                                       \
+    char* base_ = smem + (st) * STAGE4;                                                   \
+    _Pragma("unroll") for (int j_ = 0; j_ < 2; ++j_)                                      \
+      glds16(wbase + (size_t)(j_ * 16) * ldw + (k0), base_ + (wave * 2 + j_) * 1024);     \
+    _Pragma("unroll") for (int j_ = 0; j_ < 2; ++j_)                                      \
+      glds16(xcol + (size_t)min(xrow0 + j_ * 16, M - 1) * lda + (k0),                     \
+             base_ + OP_BYTES + (wave * 2 + j_) * 1024);                                  \
+  }
+
+  const int wn = wave & 3, wm = wave >> 2;
+  const int fr = lane & 15, grp = lane >> 4;
+  const int fch = (grp ^ swz_g(fr >> 2)) << 4;
+  const int woff = (wn * 64 + fr) * 64 + fch;
+  const int xoff = OP_BYTES + (wm * 128 + fr) * 64 + fch;
+
+  floatx4 acc[8][4];
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[u][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  half8 wa[4], xa[8], wb[4], xb[8];
+  const int nk = K / BK4;   // even (host guarantees), >= 2
+
+#define V4_FRAG_W(st, wf)                                                           \
+  {                                                                                 \
+    const char* fb_ = smem + (st) * STAGE4 + woff;                                  \
+    _Pragma("unroll") for (int t_ = 0; t_ < 4; ++t_) wf[t_] = *(const half8*)(fb_ + t_ * 1024); \
+  }
+#define V4_FRAG_X(st, xf, h)                                                        \
+  {                                                                                 \
+    const char* fb_ = smem + (st) * STAGE4 + xoff + (h) * 4096;                     \
+    _Pragma("unroll") for (int u_ = 0; u_ < 4; ++u_) xf[(h) * 4 + u_] = *(const half8*)(fb_ + u_ * 1024); \
+  }
+#define V4_MMA(wf, xf, h)                                                           \
+  {                                                                                 \
+    __builtin_amdgcn_s_setprio(1);                                                  \
+    _Pragma("unroll") for (int u_ = 0; u_ < 4; ++u_)                                \
+    _Pragma("unroll") for (int t_ = 0; t_ < 4; ++t_)                                \
+      acc[(h) * 4 + u_][t_] = mfma16x16x32(wf[t_], xf[(h) * 4 + u_], acc[(h) * 4 + u_][t_]); \
+    __builtin_amdgcn_s_setprio(0);                                                  \
+  }
+  // iteration T: issue tile T+4, compute tile T from (WC, XC) while reading
+  // tile T+1 into (WN, XN), then wait until tile T+2 has landed.
+#define V4_BODY(T, WC, XC, WN, XN)                                                  \
+  {                                                                                 \
+    const int t_ = (T);                                                             \
+    if (t_ + 4 < nk) V4_STAGE((t_ + 4) % NSTAGE, (t_ + 4) * BK4);                   \
+    const int sn_ = (t_ + 1) % NSTAGE;                                              \
+    V4_MMA(WC, XC, 0);                                                              \
+    __builtin_amdgcn_sched_barrier(0);                                              \
+    V4_FRAG_W(sn_, WN);                                                             \
+    V4_FRAG_X(sn_, XN, 0);                                                          \
+    __builtin_amdgcn_sched_barrier(0);                                              \
+    V4_MMA(WC, XC, 1);                                                              \
+    __builtin_amdgcn_sched_barrier(0);                                              \
+    V4_FRAG_X(sn_, XN, 1);                                                          \
+    __builtin_amdgcn_sched_barrier(0);                                              \
+    if (t_ + 4 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");               \
+    else if (t_ + 3 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");          \
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                           \
+    v4::bar();                                                                      \
+  }
+
+  // prologue: tiles 0..3 in flight, wait for 0 and 1
+  const int pro = nk < 4 ? nk : 4;
+  for (int i = 0; i < pro; ++i) V4_STAGE(i, i * BK4);
+  if (pro == 4) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if (pro == 3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  v4::bar();
+  V4_FRAG_W(0, wa);
+  V4_FRAG_X(0, xa, 0);
+  V4_FRAG_X(0, xa, 1);
+  if (pro == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (pro == 3) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  v4::bar();
+  for (int t = 0; t < nk; t += 2) {
+    V4_BODY(t, wa, xa, wb, xb);
+    V4_BODY(t + 1, wb, xb, wa, xa);
+  }
+#undef V4_BODY
+#undef V4_MMA
+#undef V4_FRAG_X
+#undef V4_FRAG_W
+#undef V4_STAGE
+
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int m = m0 + wm * 128 + u * 16 + fr;
+    if (m < M) {
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+        store_pair<EPI>(C, ldc, m, n0 + wn * 64 + p * 32, grp, acc[u][2 * p], acc[u][2 * p + 1], ep);
+    }
+  }
+}
+
 int g_variant = -1;   // -1: from env FLS_GEMM_VARIANT (default 3)
 
 int variant() {
@@ -412,7 +590,15 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
   const int var = variant();
   const bool fast = (N % BN == 0) && (K % BK == 0) && (lda % 8 == 0) && (ldw % 8 == 0) && M > 0;
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
-  if (var == 3 && fast) {
+  const bool fast4 = fast && (K % (2 * v4::BK4) == 0);
+  if (var == 4 && fast4) {
+    static bool attr4 = false;
+    if (!attr4) {
+      (void)hipFuncSetAttribute((const void*)gemm_nt_v4<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, v4::LDS4);
+      attr4 = true;
+    }
+    hipLaunchKernelGGL(gemm_nt_v4<EPI>, dim3(tiles), dim3(NT), v4::LDS4, s, A, W, C, M, N, K, lda, ldw, ldc, ep);
+  } else if (var == 3 && fast) {
     static bool attr3 = false;
     if (!attr3) {
       (void)hipFuncSetAttribute((const void*)gemm_nt_v3<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
@@ -437,6 +623,31 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
 }  // namespace
 
 extern "C" int fls_kernels_version(void) { return 2; }
+
+// microbenchmark-only entry: v1 main loop with parts removed (results are garbage)
+extern "C" int fls_gemm_ablate(int abl, const void* A, const void* W, void* C, int M, int N, int K,
+                               fls_stream_t s) {
+  if (N % BN || K % BK) return -2;
+  Epi ep{nullptr, 0, nullptr, nullptr, nullptr, 0, 0};
+  const int tiles = ((M + BM - 1) / BM) * (N / BN);
+  auto a = (const half_t*)A;
+  auto w = (const half_t*)W;
+  auto c = (half_t*)C;
+#define FLS_ABL_CASE(X)                                                                                      \
+  case X:                                                                                                    \
+    (void)hipFuncSetAttribute((const void*)gemm_nt_256x256<0, X>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                              LDS_BYTES);                                                                   \
+    hipLaunchKernelGGL((gemm_nt_256x256<0, X>), dim3(tiles), dim3(NT), LDS_BYTES, (hipStream_t)s, a, w, c, M, N, K, \
+                       K, K, N, ep);                                                                         \
+    break;
+  switch (abl) {
+    FLS_ABL_CASE(0) FLS_ABL_CASE(1) FLS_ABL_CASE(2) FLS_ABL_CASE(3) FLS_ABL_CASE(4) FLS_ABL_CASE(5) FLS_ABL_CASE(6)
+    default: return -3;
+  }
+#undef FLS_ABL_CASE
+  FLS_CHECK_LAUNCH();
+  return 0;
+}
 
 // select the GEMM main-loop variant (0 generic, 1 = 256x256x64 2-stage, 3 = ping-pong 2-stage)
 extern "C" int fls_gemm_set_variant(int v) {

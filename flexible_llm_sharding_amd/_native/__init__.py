@@ -54,6 +54,7 @@ def _load_kernels():
     _bind(lib, "fls_gemm", c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
           c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p)
     _bind(lib, "fls_gemm_set_variant", c_int, c_int)
+    _bind(lib, "fls_gemm_ablate", c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p)
     _bind(lib, "fls_attention", c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
           c_int, c_int, c_float, c_void_p)
     _bind(lib, "fls_rmsnorm", c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,

@@ -14,14 +14,16 @@ def main():
     iters = int(sys.argv[5]) if len(sys.argv) >= 6 else 10
     dev = torch.device("cuda", 0)
     ops = HipOps()
-    ops.k.fls_gemm_set_variant(var)
+    if var >= 0:
+        ops.k.fls_gemm_set_variant(var)
     x = (torch.rand(M, K, device=dev) * 2 - 1).half()
     w = ((torch.rand(N, K, device=dev) * 2 - 1) * 0.02).half()
     out = torch.empty(M, N, dtype=torch.float16, device=dev)
-    for _ in range(iters):
-        ops.gemm(x, w, EPI_NONE, out=out)
-    torch.cuda.synchronize()
-    if var == 0:
+    if var >= 0:
+        for _ in range(iters):
+            ops.gemm(x, w, EPI_NONE, out=out)
+        torch.cuda.synchronize()
+    if var < 0:
         for _ in range(iters):
             torch.matmul(x, w.t(), out=out)
         torch.cuda.synchronize()
