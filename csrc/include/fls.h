@@ -57,6 +57,9 @@ int fls_rmsnorm(const void* x, const void* w, void* y, const int* row_idx, int r
                 int ldx, int ldy, float eps, fls_stream_t s);
 int fls_embed(const int* ids, const void* table, void* out, int T, int H, int V, fls_stream_t s);
 int fls_softmax_rows(const void* logits, void* probs, int rows, int V, fls_stream_t s);
+int fls_rope_inplace(void* y, const int* pos, const float* cos_t, const float* sin_t, int M, int ld,
+                     int rope_cols, int head_dim, fls_stream_t s);
+int fls_swiglu(const void* y, void* out, int M, int I, int ldy, int ldo, fls_stream_t s);
 int fls_fill_random(void* dst, uint64_t n_elems, uint64_t seed, float mean, float std,
                     fls_stream_t s);
 

@@ -169,6 +169,60 @@ __global__ __launch_bounds__(256) void fill_random_kernel(half_t* __restrict__ d
   }
 }
 
+
+// ---------------------------------------------------------------- epilogues
+// Stand-alone versions of the GEMM epilogues, for when the projection itself
+// runs as a plain library GEMM (hipBLASLt): RoPE on the pair-permuted q/k
+// columns in place, and SwiGLU over 16-column interleaved gate/up blocks.
+// 8 columns (16 B) per thread, fp32 math.
+__global__ __launch_bounds__(256) void rope_inplace_kernel(half_t* __restrict__ y, const int* __restrict__ pos,
+                                                         const float* __restrict__ cos_t,
+                                                         const float* __restrict__ sin_t, int M, int ld,
+                                                         int rope_cols, int head_dim) {
+  // work item = (row, 32-column pair block, 8-column quarter of its first half)
+  const int per_row = (rope_cols / 32) * 2;
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long long)M * per_row) return;
+  const int m = (int)(idx / per_row);
+  const int r = (int)(idx % per_row);
+  const int blk = r >> 1, q = r & 1;          // pair block, 8-col quarter (0/1) inside 16
+  const int c1 = blk * 32 + q * 8;            // first-half columns c1..c1+7, partner +16
+  const int o = c1 % head_dim;
+  const int f0 = (o >> 5) * 16 + (o & 15);
+  const int p = pos[m];
+  const float* cr = cos_t + (size_t)p * (head_dim >> 1) + f0;
+  const float* sr = sin_t + (size_t)p * (head_dim >> 1) + f0;
+  half_t* row = y + (size_t)m * ld;
+  half8 a = *(half8*)(row + c1);
+  half8 b = *(half8*)(row + c1 + 16);
+  half8 oa, ob;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float cs = cr[j], sn = sr[j], x1 = (float)a[j], x2 = (float)b[j];
+    oa[j] = (half_t)(x1 * cs - x2 * sn);
+    ob[j] = (half_t)(x2 * cs + x1 * sn);
+  }
+  *(half8*)(row + c1) = oa;
+  *(half8*)(row + c1 + 16) = ob;
+}
+
+__global__ __launch_bounds__(256) void swiglu_kernel(const half_t* __restrict__ y, half_t* __restrict__ out, int M,
+                                                   int I, int ldy, int ldo) {
+  const int per_row = I / 8;
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long long)M * per_row) return;
+  const int m = (int)(idx / per_row);
+  const int c = (int)(idx % per_row) * 8;      // output columns c..c+7
+  const int blk = c >> 4, in = c & 15;
+  const half_t* row = y + (size_t)m * ldy + blk * 32 + in;
+  const half8 g = *(const half8*)row;
+  const half8 u = *(const half8*)(row + 16);
+  half8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (half_t)(silu((float)g[j]) * (float)u[j]);
+  *(half8*)(out + (size_t)m * ldo + c) = o;
+}
+
 }  // namespace
 
 extern "C" int fls_rmsnorm(const void* x, const void* w, void* y, const int* row_idx, int rows, int H, int ldx,
@@ -213,6 +267,27 @@ extern "C" int fls_fill_random(void* dst, uint64_t n_elems, uint64_t seed, float
   const uint64_t blocks = (threads + 255) / 256;
   hipLaunchKernelGGL(fill_random_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)s, (half_t*)dst, n_elems,
                      seed, mean, stdv);
+  FLS_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int fls_rope_inplace(void* y, const int* pos, const float* cos_t, const float* sin_t, int M, int ld,
+                                int rope_cols, int head_dim, fls_stream_t s) {
+  if (M <= 0 || rope_cols <= 0) return 0;
+  if (rope_cols % 32 || head_dim % 32 || ld % 8) return -2;
+  const long long items = (long long)M * (rope_cols / 32) * 2;
+  hipLaunchKernelGGL(rope_inplace_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, (hipStream_t)s,
+                     (half_t*)y, pos, cos_t, sin_t, M, ld, rope_cols, head_dim);
+  FLS_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int fls_swiglu(const void* y, void* out, int M, int I, int ldy, int ldo, fls_stream_t s) {
+  if (M <= 0 || I <= 0) return 0;
+  if (I % 16 || ldy % 8 || ldo % 8) return -2;
+  const long long items = (long long)M * (I / 8);
+  hipLaunchKernelGGL(swiglu_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, (hipStream_t)s,
+                     (const half_t*)y, (half_t*)out, M, I, ldy, ldo);
   FLS_CHECK_LAUNCH();
   return 0;
 }

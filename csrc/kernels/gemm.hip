@@ -95,7 +95,7 @@ __device__ __forceinline__ void store_pair(half_t* __restrict__ C, int ldc, int 
 
 // ABL (ablation, microbenchmarks only): bit0 = no LDS-DMA in the K loop,
 // bit1 = no fragment ds_reads (stale registers), bit2 = no MFMAs.
-template <int EPI, int ABL = 0>
+template <int EPI, int ABL = 0, int ORD = 0>
 __global__ __launch_bounds__(NT, 2) void gemm_nt_256x256(const half_t* __restrict__ A, const half_t* __restrict__ W,
                                                         half_t* __restrict__ C, int M, int N, int K, int lda, int ldw,
                                                         int ldc, Epi ep) {
@@ -113,13 +113,24 @@ __global__ __launch_bounds__(NT, 2) void gemm_nt_256x256(const half_t* __restric
   }
   const int tiles_m = (M + BM - 1) / BM;
   const int tiles_n = N / BN;
-  constexpr int GROUP_M = 8;
-  const int group = bid / (GROUP_M * tiles_n);
-  const int first_m = group * GROUP_M;
-  const int gsz = min(tiles_m - first_m, GROUP_M);
-  const int in_g = bid - group * GROUP_M * tiles_n;
-  const int tm = first_m + in_g % gsz;
-  const int tn = in_g / gsz;
+  int tm, tn;
+  if constexpr (ORD == 0) {          // groups of 8 M-tiles sweep N (W streamed per group)
+    constexpr int GROUP_M = 8;
+    const int group = bid / (GROUP_M * tiles_n);
+    const int first_m = group * GROUP_M;
+    const int gsz = min(tiles_m - first_m, GROUP_M);
+    const int in_g = bid - group * GROUP_M * tiles_n;
+    tm = first_m + in_g % gsz;
+    tn = in_g / gsz;
+  } else {                           // groups of 8 N-tiles sweep M (X streamed per group)
+    constexpr int GROUP_N = 8;
+    const int group = bid / (GROUP_N * tiles_m);
+    const int first_n = group * GROUP_N;
+    const int gsz = min(tiles_n - first_n, GROUP_N);
+    const int in_g = bid - group * GROUP_N * tiles_m;
+    tn = first_n + in_g % gsz;
+    tm = in_g / gsz;
+  }
   const int m0 = tm * BM, n0 = tn * BN;
 
   // ---- staging sources: each wave fills 4 x 1 KiB of the W tile and of the X tile.
@@ -442,7 +453,7 @@ __device__ __forceinline__ void bar() {
 }
 }  // namespace v4
 
-template <int EPI>
+template <int EPI, int ABL = 0>
 __global__ __launch_bounds__(NT, 2) void gemm_nt_v4(const half_t* __restrict__ A, const half_t* __restrict__ W,
                                                    half_t* __restrict__ C, int M, int N, int K, int lda, int ldw,
                                                    int ldc, Epi ep) {
@@ -512,9 +523,14 @@ __global__ __launch_bounds__(NT, 2) void gemm_nt_v4(const half_t* __restrict__ A
 #define V4_MMA(wf, xf, h)                                                           \
   {                                                                                 \
     __builtin_amdgcn_s_setprio(1);                                                  \
+    if (!(ABL & 4)) {                                                               \
     _Pragma("unroll") for (int u_ = 0; u_ < 4; ++u_)                                \
     _Pragma("unroll") for (int t_ = 0; t_ < 4; ++t_)                                \
       acc[(h) * 4 + u_][t_] = mfma16x16x32(wf[t_], xf[(h) * 4 + u_], acc[(h) * 4 + u_][t_]); \
+    } else {                                                                        \
+    _Pragma("unroll") for (int t_ = 0; t_ < 4; ++t_) asm volatile("" :: "v"(wf[t_])); \
+    _Pragma("unroll") for (int u_ = 0; u_ < 4; ++u_) asm volatile("" :: "v"(xf[(h) * 4 + u_])); \
+    }                                                                               \
     __builtin_amdgcn_s_setprio(0);                                                  \
   }
   // iteration T: issue tile T+4, compute tile T from (WC, XC) while reading
@@ -522,7 +538,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_nt_v4(const half_t* __restrict__ A
 #define V4_BODY(T, WC, XC, WN, XN)                                                  \
   {                                                                                 \
     const int t_ = (T);                                                             \
-    if (t_ + 4 < nk) V4_STAGE((t_ + 4) % NSTAGE, (t_ + 4) * BK4);                   \
+    if (!(ABL & 1) && t_ + 4 < nk) V4_STAGE((t_ + 4) % NSTAGE, (t_ + 4) * BK4);     \
     const int sn_ = (t_ + 1) % NSTAGE;                                              \
     V4_MMA(WC, XC, 0);                                                              \
     __builtin_amdgcn_sched_barrier(0);                                              \
@@ -574,6 +590,134 @@ __global__ __launch_bounds__(NT, 2) void gemm_nt_v4(const half_t* __restrict__ A
   }
 }
 
+// ------------------------------------------------------------------ v5
+// v1's 2-stage 256x256x64 LDS-DMA loop (whose DMA-only time equals hipBLASLt's
+// whole kernel: the L2->LDS stream is the bound, scripts/gemm_ablate.py), with
+// the staging work hidden in MFMA issue gaps instead of clustered:
+//   * fragments register double-buffered: the 12 ds_reads of k-half 1 are
+//     issued inside k-half 0's 32 MFMAs;
+//   * the 8 LDS-DMA pieces of tile k+1 are spread 1 per 8 MFMAs;
+//   * sched_group_barrier pins the interleave {8 MFMA, 3 DS read, 1 VMEM}.
+template <int EPI>
+__global__ __launch_bounds__(NT, 2) void gemm_nt_v5(const half_t* __restrict__ A, const half_t* __restrict__ W,
+                                                   half_t* __restrict__ C, int M, int N, int K, int lda, int ldw,
+                                                   int ldc, Epi ep) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  const int nwg = gridDim.x;
+  int bid = blockIdx.x;
+  {
+    const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7, loc = bid >> 3;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+  }
+  const int tiles_m = (M + BM - 1) / BM;
+  const int tiles_n = N / BN;
+  constexpr int GROUP_M = 8;
+  const int group = bid / (GROUP_M * tiles_n);
+  const int first_m = group * GROUP_M;
+  const int gsz = min(tiles_m - first_m, GROUP_M);
+  const int in_g = bid - group * GROUP_M * tiles_n;
+  const int tm = first_m + in_g % gsz;
+  const int tn = in_g / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int lr = lane >> 3;
+  const int lc = (lane & 7) ^ lr;
+  const half_t* wbase = W + (size_t)(n0 + wave * 32 + lr) * ldw + lc * 8;
+  const int xrow0 = m0 + wave * 32 + lr;
+  const half_t* xcol = A + lc * 8;
+  // piece j (0..7): j < 4 -> W rows wave*32 + 8j, else X rows wave*32 + 8(j-4)
+#define V5_PIECE(buf, k0, j)                                                              \
+  {                                                                                       \
+    char* base_ = smem + (buf) * STAGE_BYTES;                                             \
+    if ((j) < 4)                                                                          \
+      glds16(wbase + (size_t)((j) * 8) * ldw + (k0), base_ + (wave * 4 + (j)) * 1024);    \
+    else                                                                                  \
+      glds16(xcol + (size_t)min(xrow0 + ((j) - 4) * 8, M - 1) * lda + (k0),               \
+             base_ + TILE_BYTES + (wave * 4 + (j) - 4) * 1024);                           \
+  }
+
+  const int wn = wave & 3, wm = wave >> 2;
+  const int fr = lane & 15, grp = lane >> 4;
+  const int swz = lane & 7;
+  const int wrow = (wn * 64 + fr) * 128;
+  const int xrow = TILE_BYTES + (wm * 128 + fr) * 128;
+  const int ch0 = ((0 * 4 + grp) ^ swz) << 4;
+  const int ch1 = ((1 * 4 + grp) ^ swz) << 4;
+
+  floatx4 acc[8][4];
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[u][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  half8 wa[4], xa[8], wb[4], xb[8];
+
+#define V5_READ(buf, ch, wf, xf)                                                          \
+  {                                                                                       \
+    const char* b_ = smem + (buf) * STAGE_BYTES;                                          \
+    _Pragma("unroll") for (int t_ = 0; t_ < 4; ++t_) wf[t_] = *(const half8*)(b_ + wrow + t_ * 2048 + (ch)); \
+    _Pragma("unroll") for (int u_ = 0; u_ < 8; ++u_) xf[u_] = *(const half8*)(b_ + xrow + u_ * 2048 + (ch)); \
+  }
+#define V5_MMA(wf, xf)                                                                    \
+  {                                                                                       \
+    _Pragma("unroll") for (int u_ = 0; u_ < 8; ++u_)                                      \
+    _Pragma("unroll") for (int t_ = 0; t_ < 4; ++t_)                                      \
+      acc[u_][t_] = mfma16x16x32(wf[t_], xf[u_], acc[u_][t_]);                            \
+  }
+
+  const int nk = K / BK;
+  _Pragma("unroll") for (int j = 0; j < 8; ++j) V5_PIECE(0, 0, j);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  V5_READ(0, ch0, wa, xa);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    // the last iteration re-stages the final tile into the idle buffer (never read):
+    // no branch, so each k-half stays one basic block for sched_group_barrier
+    const int kn = min(kt + 1, nk - 1) * BK;
+    // ---- k-half 0: MFMAs on (wa, xa); read k-half 1 into (wb, xb); 4 DMA pieces
+    __builtin_amdgcn_sched_barrier(0);
+    V5_READ(cur, ch1, wb, xb);
+    V5_PIECE(cur ^ 1, kn, 0) V5_PIECE(cur ^ 1, kn, 1) V5_PIECE(cur ^ 1, kn, 2) V5_PIECE(cur ^ 1, kn, 3)
+    V5_MMA(wa, xa);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);   // 8 MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);   // 3 DS read
+      __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);   // 1 VMEM (LDS-DMA piece)
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- k-half 1: MFMAs on (wb, xb); remaining 4 DMA pieces
+    V5_PIECE(cur ^ 1, kn, 4) V5_PIECE(cur ^ 1, kn, 5) V5_PIECE(cur ^ 1, kn, 6) V5_PIECE(cur ^ 1, kn, 7)
+    V5_MMA(wb, xb);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+      __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    V5_READ(cur ^ 1, ch0, wa, xa);
+  }
+#undef V5_MMA
+#undef V5_READ
+#undef V5_PIECE
+
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int m = m0 + wm * 128 + u * 16 + fr;
+    if (m < M) {
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+        store_pair<EPI>(C, ldc, m, n0 + wn * 64 + p * 32, grp, acc[u][2 * p], acc[u][2 * p + 1], ep);
+    }
+  }
+}
+
 int g_variant = -1;   // -1: from env FLS_GEMM_VARIANT (default 3)
 
 int variant() {
@@ -591,7 +735,14 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
   const bool fast = (N % BN == 0) && (K % BK == 0) && (lda % 8 == 0) && (ldw % 8 == 0) && M > 0;
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
   const bool fast4 = fast && (K % (2 * v4::BK4) == 0);
-  if (var == 4 && fast4) {
+  if (var == 5 && fast) {
+    static bool attr5 = false;
+    if (!attr5) {
+      (void)hipFuncSetAttribute((const void*)gemm_nt_v5<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+      attr5 = true;
+    }
+    hipLaunchKernelGGL(gemm_nt_v5<EPI>, dim3(tiles), dim3(NT), LDS_BYTES, s, A, W, C, M, N, K, lda, ldw, ldc, ep);
+  } else if (var == 4 && fast4) {
     static bool attr4 = false;
     if (!attr4) {
       (void)hipFuncSetAttribute((const void*)gemm_nt_v4<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, v4::LDS4);
@@ -640,10 +791,31 @@ extern "C" int fls_gemm_ablate(int abl, const void* A, const void* W, void* C, i
     hipLaunchKernelGGL((gemm_nt_256x256<0, X>), dim3(tiles), dim3(NT), LDS_BYTES, (hipStream_t)s, a, w, c, M, N, K, \
                        K, K, N, ep);                                                                         \
     break;
+#define FLS_ABL4_CASE(X)                                                                                     \
+  case 10 + X:                                                                                               \
+    (void)hipFuncSetAttribute((const void*)gemm_nt_v4<0, X>, hipFuncAttributeMaxDynamicSharedMemorySize,     \
+                              v4::LDS4);                                                                     \
+    hipLaunchKernelGGL((gemm_nt_v4<0, X>), dim3(tiles), dim3(NT), v4::LDS4, (hipStream_t)s, a, w, c, M, N, K, \
+                       K, K, N, ep);                                                                         \
+    break;
   switch (abl) {
     FLS_ABL_CASE(0) FLS_ABL_CASE(1) FLS_ABL_CASE(2) FLS_ABL_CASE(3) FLS_ABL_CASE(4) FLS_ABL_CASE(5) FLS_ABL_CASE(6)
+    FLS_ABL4_CASE(0) FLS_ABL4_CASE(1) FLS_ABL4_CASE(4)
+    case 20:
+      (void)hipFuncSetAttribute((const void*)gemm_nt_256x256<0, 0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                LDS_BYTES);
+      hipLaunchKernelGGL((gemm_nt_256x256<0, 0, 1>), dim3(tiles), dim3(NT), LDS_BYTES, (hipStream_t)s, a, w, c, M, N,
+                         K, K, K, N, ep);
+      break;
+    case 26:
+      (void)hipFuncSetAttribute((const void*)gemm_nt_256x256<0, 6, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                LDS_BYTES);
+      hipLaunchKernelGGL((gemm_nt_256x256<0, 6, 1>), dim3(tiles), dim3(NT), LDS_BYTES, (hipStream_t)s, a, w, c, M, N,
+                         K, K, K, N, ep);
+      break;
     default: return -3;
   }
+#undef FLS_ABL4_CASE
 #undef FLS_ABL_CASE
   FLS_CHECK_LAUNCH();
   return 0;

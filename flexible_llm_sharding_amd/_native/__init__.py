@@ -61,6 +61,9 @@ def _load_kernels():
           c_int, c_float, c_void_p)
     _bind(lib, "fls_embed", c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p)
     _bind(lib, "fls_softmax_rows", c_int, c_void_p, c_void_p, c_int, c_int, c_void_p)
+    _bind(lib, "fls_rope_inplace", c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+          c_void_p)
+    _bind(lib, "fls_swiglu", c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p)
     _bind(lib, "fls_fill_random", c_int, c_void_p, c_uint64, c_uint64, c_float, c_float, c_void_p)
     return lib
 

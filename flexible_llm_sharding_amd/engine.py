@@ -45,6 +45,16 @@ from .utils import trace
 from .utils.tokenizer import TokenizedPrompt, tokenize_prompts
 
 
+def _parse_fault(rank: int):
+    """FLS_FAULT="rank:shard" — fault injection for failure-handling tests."""
+    import os
+    spec = os.environ.get("FLS_FAULT", "")
+    if not spec:
+        return None
+    r, _, k = spec.partition(":")
+    return int(k or 0) if int(r) == rank else None
+
+
 class ShardedRunner:
     def __init__(self, cfg: ModelConfig, source: LayerSource, device="cpu", tokenizer=None,
                  layer_num_per_shard: int = 1, storage_location: str = "cpu",
@@ -82,6 +92,14 @@ class ShardedRunner:
         self.prefetcher = prefetcher or ShardPrefetcher(source, self.names, my, self.dev,
                                                         n_slots=n_slots, resident=resident)
         self.stats: Dict[str, float] = {}
+        if self.plan.mode == "mp" and self.comm.active:
+            edges = []
+            for li in range(self.L - 1):
+                a, b = self.plan.owner_of_layer(li), self.plan.owner_of_layer(li + 1)
+                if a != b:
+                    edges.append((a, b))
+            self.comm.setup_p2p_edges(edges)
+        self._fault = _parse_fault(self.comm.rank)
         self.h2d_stream = torch.cuda.Stream(self.dev) if self.cuda else None
         self.d2h_stream = torch.cuda.Stream(self.dev) if self.cuda else None
         self._store: Optional[ActivationStore] = None
@@ -162,6 +180,8 @@ class ShardedRunner:
             shard = self.my_shards[k]
             first, last = shard[0], shard[-1]
             if k != cur_k:
+                if self._fault is not None and k == self._fault:
+                    raise RuntimeError(f"FLS_FAULT injected on rank {comm.rank} at shard {k}")
                 if cur_k >= 0:
                     pf.release(cur_k)
                     sends = [(t, w) for (t, w) in sends if not w.is_completed()]   # bound memory

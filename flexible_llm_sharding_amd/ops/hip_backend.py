@@ -4,8 +4,19 @@ Kernels run on the caller's current HIP stream (``torch.cuda.current_stream``)
 so they compose with the copy/comm streams of the runtime; outputs are
 allocated through PyTorch's caching allocator.  There is deliberately no
 fallback: a missing library raises (see ``_native.kernels``).
+
+Projection GEMMs: ``FLS_GEMM_BACKEND`` selects
+  * ``hip``       — our fused MFMA kernels (RoPE / SwiGLU / residual epilogues in registers);
+  * ``hipblaslt`` — the plain GEMM on hipBLASLt (residual via beta=1) followed by our
+                    stand-alone RoPE / SwiGLU epilogue kernels;
+  * ``auto``      — (default) per (op, N, K, M-bucket) the faster of the two, timed once on
+                    first use (scratch outputs, so in-place ops are not applied twice).
+Both paths are numerically checked against each other in tests/test_kernels_gpu.py.
+Measured trade-off on 70B shapes: profiles/r1_gemm_ablation/README.md.
 """
 from __future__ import annotations
+
+import os
 
 import torch
 
@@ -37,6 +48,41 @@ class HipOps:
 
     def __init__(self):
         self.k = _native.kernels()
+        self.backend = os.environ.get("FLS_GEMM_BACKEND", "auto")
+        if self.backend not in ("auto", "hip", "hipblaslt"):
+            raise ValueError(f"FLS_GEMM_BACKEND={self.backend!r}")
+        self.choice = {}          # (op, N, K, M-bucket) -> "hip" | "hipblaslt"
+        self.timings = {}
+
+    # ------------------------------------------------------- backend choice
+    def _pick(self, op, x, w, run_hip, run_blt, scratch_hip, scratch_blt):
+        if self.backend == "hip":
+            return run_hip()
+        if self.backend == "hipblaslt":
+            return run_blt()
+        M = x.shape[0]
+        key = (op, w.shape[0], w.shape[1], max(M, 1).bit_length())
+        ch = self.choice.get(key)
+        if ch is None:
+            ch = self._tune(key, scratch_hip, scratch_blt)
+        return run_hip() if ch == "hip" else run_blt()
+
+    def _tune(self, key, f_hip, f_blt, reps: int = 3):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        f_hip(); f_blt()                      # warm (kernel load / heuristics)
+        ev[0].record()
+        for _ in range(reps):
+            f_hip()
+        ev[1].record()
+        for _ in range(reps):
+            f_blt()
+        ev[2].record()
+        ev[2].synchronize()
+        th, tb = ev[0].elapsed_time(ev[1]) / reps, ev[1].elapsed_time(ev[2]) / reps
+        ch = "hip" if th <= tb else "hipblaslt"
+        self.choice[key] = ch
+        self.timings[key] = {"hip_ms": th, "hipblaslt_ms": tb, "choice": ch}
+        return ch
 
     # ---------------------------------------------------------------- GEMM
     def gemm(self, x: torch.Tensor, w: torch.Tensor, epi: int = EPI_NONE, out: torch.Tensor = None,
@@ -62,20 +108,62 @@ class HipOps:
         return out
 
     def linear(self, x, w):
-        return self.gemm(x, w)
+        return self._pick("linear", x, w, lambda: self.gemm(x, w), lambda: torch.matmul(x, w.t()),
+                          lambda: self.gemm(x, w), lambda: torch.matmul(x, w.t()))
 
     def linear_residual(self, x, w, resid):
         _f16(resid, "resid")
-        return self.gemm(x, w, EPI_RESID, out=resid, resid=resid)
+
+        def hip():
+            return self.gemm(x, w, EPI_RESID, out=resid, resid=resid)
+
+        def blt():
+            return resid.addmm_(x, w.t())
+
+        scratch = [None]
+
+        def s_hip():
+            if scratch[0] is None:
+                scratch[0] = torch.empty_like(resid)
+            return self.gemm(x, w, EPI_RESID, out=scratch[0], resid=resid)
+
+        def s_blt():
+            if scratch[0] is None:
+                scratch[0] = torch.empty_like(resid)
+            return torch.addmm(resid, x, w.t(), out=scratch[0])
+
+        return self._pick("resid", x, w, hip, blt, s_hip, s_blt)
 
     def swiglu_up(self, x, wgu):
-        return self.gemm(x, wgu, EPI_SWIGLU)
+        def hip():
+            return self.gemm(x, wgu, EPI_SWIGLU)
+
+        def blt():
+            y = torch.matmul(x, wgu.t())
+            out = torch.empty(y.shape[0], y.shape[1] // 2, dtype=torch.float16, device=y.device)
+            _chk(self.k.fls_swiglu(y.data_ptr(), out.data_ptr(), y.shape[0], y.shape[1] // 2, y.stride(0),
+                                   out.stride(0), _stream()), "fls_swiglu")
+            return out
+
+        return self._pick("swiglu", x, wgu, hip, blt, hip, blt)
 
     def qkv_rope(self, x, wqkv, positions, cos, sin, n_q_heads, n_kv_heads, head_dim):
         if positions.dtype != torch.int32:
             raise TypeError("positions must be int32")
-        return self.gemm(x, wqkv, EPI_ROPE, positions=positions, cos=cos, sin=sin,
-                         rope_cols=(n_q_heads + n_kv_heads) * head_dim, head_dim=head_dim)
+        rope_cols = (n_q_heads + n_kv_heads) * head_dim
+
+        def hip():
+            return self.gemm(x, wqkv, EPI_ROPE, positions=positions, cos=cos, sin=sin,
+                             rope_cols=rope_cols, head_dim=head_dim)
+
+        def blt():
+            y = torch.matmul(x, wqkv.t())
+            _chk(self.k.fls_rope_inplace(y.data_ptr(), positions.data_ptr(), cos.data_ptr(), sin.data_ptr(),
+                                         y.shape[0], y.stride(0), rope_cols, head_dim, _stream()),
+                 "fls_rope_inplace")
+            return y
+
+        return self._pick("qkv_rope", x, wqkv, hip, blt, hip, blt)
 
     # ----------------------------------------------------------- attention
     def attention(self, qkv, work, n_q_heads, n_kv_heads, head_dim):
@@ -126,7 +214,7 @@ class HipOps:
         return probs
 
     def lm_head_softmax(self, h, w):
-        return self.softmax(self.gemm(h, w))
+        return self.softmax(self.linear(h, w))
 
     def fill_layer_random(self, buf: torch.Tensor, layout, seed: int, std: float = 0.02) -> None:
         views = layout.views(buf, torch.float16)

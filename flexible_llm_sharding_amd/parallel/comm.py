@@ -58,11 +58,30 @@ class Comm:
         return cls(rank, world, dev, backend)
 
     # -------------------------------------------------------------- p2p
+    def setup_p2p_edges(self, edges) -> None:
+        """Create one process group per DIRECTED hand-off edge (src, dst).
+
+        Every rank must call this with the same edge list (it is collective).
+        With one communicator per direction, each NCCL/RCCL stream carries only
+        sends on one side and receives on the other, so the order in which a
+        receiver posts its receives can never deadlock against its own sends
+        to the same peer (the G=2 pipeline has traffic both ways between the
+        same two ranks).
+        """
+        self._edge_groups = {}
+        if not self.active:
+            return
+        for (a, b) in sorted(set(edges)):
+            self._edge_groups[(a, b)] = dist.new_group(ranks=sorted([a, b]))
+
+    def _group(self, src: int, dst: int):
+        return getattr(self, "_edge_groups", {}).get((src, dst))
+
     def isend(self, t: torch.Tensor, dst: int):
-        return dist.isend(t, dst)
+        return dist.isend(t, dst, group=self._group(self.rank, dst))
 
     def irecv(self, t: torch.Tensor, src: int):
-        return dist.irecv(t, src)
+        return dist.irecv(t, src, group=self._group(src, self.rank))
 
     # -------------------------------------------------------- collectives
     def barrier(self):

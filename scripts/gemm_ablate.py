@@ -11,7 +11,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from flexible_llm_sharding_amd import _native  # noqa: E402
 
 NAMES = {0: "full", 1: "no_dma", 2: "no_lds_read", 3: "mfma_only", 4: "no_mfma", 5: "lds_read_only",
-         6: "dma_only"}
+         6: "dma_only", 10: "v4_full", 11: "v4_no_dma", 14: "v4_no_mfma",
+         20: "v1_groupN_full", 26: "v1_groupN_dma_only"}
 
 
 def main():

@@ -126,3 +126,20 @@ def test_data_parallel_sharded_weights(single, tmp_path, world, lnps):
     assert len(got) == len(ref)
     for a, b in zip(got, ref):
         assert _close(a, b)
+
+
+def _fault_worker(rank, world, port, path, prompts, out_dir):
+    os.environ["FLS_FAULT"] = "1:1"
+    _worker(rank, world, port, path, prompts, 1, False, "gpu", out_dir, 40)
+
+
+def test_rank_failure_terminates_job(single, tmp_path):
+    """A rank dying mid-pipeline must end the whole job (no peer left blocked in recv)."""
+    import time
+    path, prompts, ref = single
+    t0 = time.time()
+    with pytest.raises(Exception) as ei:
+        mp.start_processes(_fault_worker, args=(2, _port(), path, prompts, str(tmp_path)), nprocs=2,
+                           start_method="spawn", join=True)
+    assert "FLS_FAULT" in str(ei.value) or "exited" in str(ei.value) or "ProcessRaised" in type(ei.value).__name__
+    assert time.time() - t0 < 120

@@ -21,6 +21,7 @@ DEV = torch.device("cuda", 0)
 @pytest.fixture(scope="module")
 def ops():
     o = HipOps()
+    o.backend = "hip"          # exercise the hand-written fused kernels (hipBLASLt path: test_gemm_backends_agree)
     assert _native.loaded_libraries().get("k"), "libfls_kernels.so not loaded"
     return o
 
@@ -186,3 +187,39 @@ def test_fill_random(ops):
     torch.cuda.synchronize()
     f = buf.float()
     assert abs(f.mean().item()) < 0.01 and abs(f.std().item() - 1) < 0.01
+
+
+@pytest.mark.parametrize("M", [300, 2048])
+def test_gemm_backends_agree(M):
+    """Fused-epilogue MFMA kernels vs hipBLASLt + stand-alone epilogue kernels."""
+    from flexible_llm_sharding_amd.config import ModelConfig
+    from flexible_llm_sharding_amd.models.llama import rope_tables
+    a, b = HipOps(), HipOps()
+    a.backend, b.backend = "hip", "hipblaslt"
+    H, I, nh, nkv, hd = 512, 768, 4, 2, 128
+    x = rnd(M, H, seed=21)
+    wqkv = rnd((nh + 2 * nkv) * hd, H, scale=0.05, seed=22)
+    wgu = rnd(2 * I, H, scale=0.05, seed=23)
+    wd = rnd(H, I, scale=0.05, seed=24)
+    pos = torch.randint(0, 4000, (M,), dtype=torch.int32, device=DEV)
+    cfg = ModelConfig(hidden_size=nh * hd, num_attention_heads=nh, num_key_value_heads=nkv)
+    cos, sin = (t.to(DEV) for t in rope_tables(cfg, 4096))
+    q1 = a.qkv_rope(x, wqkv, pos, cos, sin, nh, nkv, hd)
+    q2 = b.qkv_rope(x, wqkv, pos, cos, sin, nh, nkv, hd)
+    s1, s2 = a.swiglu_up(x, wgu), b.swiglu_up(x, wgu)
+    r0 = rnd(M, H, seed=25)
+    r1 = a.linear_residual(s1, wd, r0.clone())
+    r2 = b.linear_residual(s1, wd, r0.clone())
+    torch.cuda.synchronize()
+    assert rel_err(q1, q2) < 2e-3 and rel_err(s1, s2) < 3e-3 and rel_err(r1, r2) < 2e-3
+
+
+def test_gemm_autotune_choice():
+    o = HipOps()
+    o.backend = "auto"
+    x = rnd(1024, 1024, seed=26)
+    w = rnd(2048, 1024, scale=0.05, seed=27)
+    y = o.linear(x, w)
+    torch.cuda.synchronize()
+    assert len(o.choice) == 1 and list(o.timings.values())[0]["choice"] in ("hip", "hipblaslt")
+    assert rel_err(y, x.float() @ w.float().t()) < 2e-3
