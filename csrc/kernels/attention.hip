@@ -41,21 +41,23 @@ struct Lds {
   __device__ static int v_off(int row, int ch) { return row * ROW + ((ch ^ ((row & (NCH / 2 - 1)) << 1)) << 4); }
 };
 
-template <int HD>
-__global__ __launch_bounds__(256) void attn_fwd(const half_t* __restrict__ qkv, half_t* __restrict__ out,
-                                              const int* __restrict__ work, int nh, int nkv, int ld_qkv,
-                                              int ld_out, float scale_log2) {
+// HPB query heads of the same KV group per block (GQA): waves 4*j .. 4*j+3
+// serve head h0 + j, so every K/V tile staged in LDS feeds 4*HPB waves.
+template <int HD, int HPB>
+__global__ __launch_bounds__(256 * HPB) void attn_fwd(const half_t* __restrict__ qkv, half_t* __restrict__ out,
+                                                    const int* __restrict__ work, int nh, int nkv, int ld_qkv,
+                                                    int ld_out, float scale_log2) {
   constexpr int NS = HD / 32;     // k-steps of the QK^T product
   constexpr int NU = HD / 16;     // 16-wide d subtiles of O
   __shared__ __attribute__((aligned(16))) char smem[2 * KT * HD * 2];
   char* Ks = smem;
   char* Vs = smem + KT * HD * 2;
 
+  constexpr int NT_ = 256 * HPB;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int fr = lane & 15, grp = lane >> 4;
-  const int h = blockIdx.y;
+  const int wave = (tid >> 6) & 3;          // row group inside the 64-row item
+  const int h = blockIdx.y * HPB + (tid >> 8);
   const int g = h / (nh / nkv);
 
   const int* wi = work + blockIdx.x * 8;
@@ -64,6 +66,7 @@ __global__ __launch_bounds__(256) void attn_fwd(const half_t* __restrict__ qkv, 
   const int r_len[2] = {wi[4], wi[7]};
   const int r_causal[2] = {wi[5], 1};
 
+  const int fr = lane & 15, grp = lane >> 4;
   const int q_col = h * HD;
   const int k_col = nh * HD + g * HD;
   const int v_col = (nh + nkv) * HD + g * HD;
@@ -97,7 +100,7 @@ __global__ __launch_bounds__(256) void attn_fwd(const half_t* __restrict__ qkv, 
       // ---- stage K and V tiles (64 rows x HD) into LDS, 16 B per thread-chunk
       constexpr int CHUNKS = KT * HD / 8;
 #pragma unroll
-      for (int c = tid; c < CHUNKS; c += 256) {
+      for (int c = tid; c < CHUNKS; c += NT_) {
         const int row = c / (HD / 8), ch = c % (HD / 8);
         const int key = min(k0 + row, klen - 1);
         const half_t* src = qkv + (size_t)(kbase + key) * ld_qkv;
@@ -191,20 +194,24 @@ extern "C" int fls_attention(const void* qkv, void* out, const int* work, int n_
   if (n_items <= 0) return 0;
   if (n_q_heads % n_kv_heads) return -2;
   const float scale_log2 = scale * 1.4426950408889634f;
-  dim3 grid(n_items, n_q_heads);
   auto st = (hipStream_t)s;
+  const int group = n_q_heads / n_kv_heads;
+  const bool two = (group % 2) == 0;        // pair up query heads of one KV group
+  dim3 grid(n_items, two ? n_q_heads / 2 : n_q_heads);
+#define FLS_ATTN_LAUNCH(HD_, HPB_)                                                                          \
+  hipLaunchKernelGGL((attn_fwd<HD_, HPB_>), grid, dim3(256 * HPB_), 0, st, (const half_t*)qkv, (half_t*)out, \
+                     work, n_q_heads, n_kv_heads, ld_qkv, ld_out, scale_log2)
   switch (head_dim) {
     case 64:
-      hipLaunchKernelGGL(attn_fwd<64>, grid, dim3(256), 0, st, (const half_t*)qkv, (half_t*)out, work, n_q_heads,
-                         n_kv_heads, ld_qkv, ld_out, scale_log2);
+      if (two) FLS_ATTN_LAUNCH(64, 2); else FLS_ATTN_LAUNCH(64, 1);
       break;
     case 128:
-      hipLaunchKernelGGL(attn_fwd<128>, grid, dim3(256), 0, st, (const half_t*)qkv, (half_t*)out, work, n_q_heads,
-                         n_kv_heads, ld_qkv, ld_out, scale_log2);
+      if (two) FLS_ATTN_LAUNCH(128, 2); else FLS_ATTN_LAUNCH(128, 1);
       break;
     default:
       return -3;
   }
+#undef FLS_ATTN_LAUNCH
   FLS_CHECK_LAUNCH();
   return 0;
 }

@@ -718,6 +718,149 @@ __global__ __launch_bounds__(NT, 2) void gemm_nt_v5(const half_t* __restrict__ A
   }
 }
 
+// ------------------------------------------------------------------ v6
+// One wave per SIMD: 4 waves (256 threads) per 256x256x64 block tile, each
+// wave owning a 128x128 output quadrant = 8 x 8 tiles of v_mfma_f32_16x16x32_f16
+// (256 fp32 accumulators, allocated in AGPRs: launch bounds admit 512
+// registers per lane at one wave per SIMD).  Per K-tile a wave issues 128
+// MFMAs (2048 matrix-pipe cycles) and only 32 fragment ds_reads (a 128x128
+// quadrant re-uses each fragment 8 times — 1/3 fewer LDS reads per FLOP than
+// the 8-wave layout) plus 16 LDS-DMA pieces; fragments for the second k-half
+// and the next tile's DMA are issued while the current k-half's MFMAs run.
+// Same LDS image / swizzle / XCD-aware order as v1.
+template <int EPI>
+__global__ __launch_bounds__(256, 1) void gemm_nt_v6(const half_t* __restrict__ A, const half_t* __restrict__ W,
+                                                    half_t* __restrict__ C, int M, int N, int K, int lda, int ldw,
+                                                    int ldc, Epi ep) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  const int nwg = gridDim.x;
+  int bid = blockIdx.x;
+  {
+    const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7, loc = bid >> 3;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+  }
+  const int tiles_m = (M + BM - 1) / BM;
+  const int tiles_n = N / BN;
+  constexpr int GROUP_M = 8;
+  const int group = bid / (GROUP_M * tiles_n);
+  const int first_m = group * GROUP_M;
+  const int gsz = min(tiles_m - first_m, GROUP_M);
+  const int in_g = bid - group * GROUP_M * tiles_n;
+  const int tm = first_m + in_g % gsz;
+  const int tn = in_g / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // staging: 32 pieces (1 KiB = 8 rows x 128 B) per operand; a wave fills 8 of each
+  const int lr = lane >> 3;
+  const int lc = (lane & 7) ^ lr;
+  const half_t* wbase = W + (size_t)(n0 + wave * 64 + lr) * ldw + lc * 8;
+  const int xrow0 = m0 + wave * 64 + lr;
+  const half_t* xcol = A + lc * 8;
+#define V6_PIECE(buf, k0, j)                                                              \
+  {                                                                                       \
+    char* base_ = smem + (buf) * STAGE_BYTES;                                             \
+    if ((j) < 8)                                                                          \
+      glds16(wbase + (size_t)((j) * 8) * ldw + (k0), base_ + (wave * 8 + (j)) * 1024);    \
+    else                                                                                  \
+      glds16(xcol + (size_t)min(xrow0 + ((j) - 8) * 8, M - 1) * lda + (k0),               \
+             base_ + TILE_BYTES + (wave * 8 + (j) - 8) * 1024);                           \
+  }
+
+  const int wp = wave & 1, wq = wave >> 1;       // P (W rows) half, Q (X rows) half
+  const int fr = lane & 15, grp = lane >> 4;
+  const int swz = lane & 7;
+  const int wrow = (wp * 128 + fr) * 128;
+  const int xrow = TILE_BYTES + (wq * 128 + fr) * 128;
+  const int ch0 = ((0 * 4 + grp) ^ swz) << 4;
+  const int ch1 = ((1 * 4 + grp) ^ swz) << 4;
+
+  floatx4 acc[8][8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc[u][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  half8 wa[8], xa[8], wb[8], xb[8];
+
+#define V6_READ(buf, ch, wf, xf)                                                          \
+  {                                                                                       \
+    const char* b_ = smem + (buf) * STAGE_BYTES;                                          \
+    _Pragma("unroll") for (int t_ = 0; t_ < 8; ++t_) wf[t_] = *(const half8*)(b_ + wrow + t_ * 2048 + (ch)); \
+    _Pragma("unroll") for (int u_ = 0; u_ < 8; ++u_) xf[u_] = *(const half8*)(b_ + xrow + u_ * 2048 + (ch)); \
+  }
+#define V6_MMA(wf, xf)                                                                    \
+  {                                                                                       \
+    _Pragma("unroll") for (int u_ = 0; u_ < 8; ++u_)                                      \
+    _Pragma("unroll") for (int t_ = 0; t_ < 8; ++t_)                                      \
+      acc[u_][t_] = mfma16x16x32(wf[t_], xf[u_], acc[u_][t_]);                            \
+  }
+
+  const int nk = K / BK;
+  _Pragma("unroll") for (int j = 0; j < 16; ++j) V6_PIECE(0, 0, j);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  V6_READ(0, ch0, wa, xa);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const int kn = min(kt + 1, nk - 1) * BK;    // last iteration re-stages into the idle buffer
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- k-half 0 (64 MFMAs): first the k-half-1 fragments from `cur`, then
+    // the next tile's 16 DMA pieces into `cur^1` (reads before writes: the
+    // compiler must assume the LDS accesses alias, so this order lets it interleave)
+    V6_READ(cur, ch1, wb, xb);
+    _Pragma("unroll") for (int j = 0; j < 16; ++j) V6_PIECE(cur ^ 1, kn, j);
+    V6_MMA(wa, xa);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);   // 4 MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);   // 4 DS read
+    }
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);   // 3 MFMA
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);   // 1 VMEM read (LDS-DMA piece)
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- k-half 1: 32 MFMAs, then wait for the DMA + barrier (every wave is
+    // done reading `cur`, so the next iteration may overwrite it), then the
+    // next tile's k-half-0 fragments are read under the remaining 32 MFMAs.
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int t = 0; t < 8; ++t) acc[u][t] = mfma16x16x32(wb[t], xb[u], acc[u][t]);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    V6_READ(cur ^ 1, ch0, wa, xa);
+#pragma unroll
+    for (int u = 4; u < 8; ++u)
+#pragma unroll
+      for (int t = 0; t < 8; ++t) acc[u][t] = mfma16x16x32(wb[t], xb[u], acc[u][t]);
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);   // 4 MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // 2 DS read
+    }
+  }
+#undef V6_MMA
+#undef V6_READ
+#undef V6_PIECE
+
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int m = m0 + wq * 128 + u * 16 + fr;
+    if (m < M) {
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+        store_pair<EPI>(C, ldc, m, n0 + wp * 128 + p * 32, grp, acc[u][2 * p], acc[u][2 * p + 1], ep);
+    }
+  }
+}
+
 int g_variant = -1;   // -1: from env FLS_GEMM_VARIANT (default 3)
 
 int variant() {
@@ -735,7 +878,14 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
   const bool fast = (N % BN == 0) && (K % BK == 0) && (lda % 8 == 0) && (ldw % 8 == 0) && M > 0;
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
   const bool fast4 = fast && (K % (2 * v4::BK4) == 0);
-  if (var == 5 && fast) {
+  if (var == 6 && fast) {
+    static bool attr6 = false;
+    if (!attr6) {
+      (void)hipFuncSetAttribute((const void*)gemm_nt_v6<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+      attr6 = true;
+    }
+    hipLaunchKernelGGL(gemm_nt_v6<EPI>, dim3(tiles), dim3(256), LDS_BYTES, s, A, W, C, M, N, K, lda, ldw, ldc, ep);
+  } else if (var == 5 && fast) {
     static bool attr5 = false;
     if (!attr5) {
       (void)hipFuncSetAttribute((const void*)gemm_nt_v5<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);

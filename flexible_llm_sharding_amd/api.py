@@ -64,7 +64,9 @@ def build_runner(args, cfg: ModelConfig, device, comm: Comm, tok) -> ShardedRunn
                          max_activation_in_cpu=args.max_activation_in_cpu,
                          prefix_attention=args.prefix_attention, token_budget=args.token_budget,
                          resident=args.resident, comm=comm, data_parallel=args.data_parallel,
-                         act_dtype=act, verbose=args.verbose)
+                         act_dtype=act, verbose=args.verbose,
+                         resume_dir=getattr(args, "resume_dir", None),
+                         checkpoint_every=getattr(args, "checkpoint_every", 0))
 
 
 def run_all(args, runner: ShardedRunner, comm: Comm, prompts: Sequence) -> List[np.ndarray]:

@@ -63,7 +63,7 @@ class ShardedRunner:
                  resident: bool = False, comm: Optional[Comm] = None, data_parallel: bool = False,
                  act_dtype: Optional[torch.dtype] = None, n_slots: int = 2,
                  mlp_chunk: int = 16384, prefetcher: Optional[ShardPrefetcher] = None,
-                 verbose: bool = False):
+                 verbose: bool = False, resume_dir: Optional[str] = None, checkpoint_every: int = 0):
         self.cfg = cfg
         self.src = source
         self.dev = torch.device(device)
@@ -78,6 +78,8 @@ class ShardedRunner:
         self.comm = comm or Comm(0, 1, self.dev)
         self.data_parallel = data_parallel
         self.verbose = verbose
+        self.resume_dir = resume_dir
+        self.checkpoint_every = checkpoint_every
         self.names = cfg.layer_names()
         self.L = len(self.names)
         self.plan: ShardPlan = make_plan(self.L, layer_num_per_shard, self.comm.world, self.comm.rank,
@@ -170,16 +172,26 @@ class ShardedRunner:
         sends = []
         h2d0 = pf.bytes_h2d
         items = self.schedule(len(batches))
+        ck, k0 = self._open_checkpoint(tps)
+        if k0 > 0:
+            for b, t in ck.load(k0).items():
+                store.put(b, t.to(self.dev))
+            items = [it for it in items if it[0] >= k0]
         carry = {}                     # micro-batch -> device activation kept across a shard boundary
         recvs = {}
+        recv_src = None
+        recv_next = 0
         cur_k = -1
         W = None
-        if self.my_shards:
-            pf.prefetch(0)
+        if self.my_shards and items:
+            pf.prefetch(items[0][0])
+        pbar = self._progress(len(items))
         for idx, (k, b) in enumerate(items):
             shard = self.my_shards[k]
             first, last = shard[0], shard[-1]
             if k != cur_k:
+                if ck is not None and cur_k >= 0 and self._ckpt_due(cur_k):
+                    ck.commit(cur_k + 1, range(len(batches)), self.act_dtype)
                 if self._fault is not None and k == self._fault:
                     raise RuntimeError(f"FLS_FAULT injected on rank {comm.rank} at shard {k}")
                 if cur_k >= 0:
@@ -192,16 +204,26 @@ class ShardedRunner:
                 cur_k = k
                 src_rank = self._owner(first - 1) if (mp and first > 0) else comm.rank
                 dst_rank = self._owner(last + 1) if (mp and last + 1 < self.L) else comm.rank
-                if first > 0 and src_rank != comm.rank:
-                    # post every receive of this shard up front (matches the sender's order)
-                    for bb, batch in enumerate(batches):
-                        buf = torch.empty(self._state_shape(first - 1, batch), dtype=self.act_dtype,
-                                          device=self.dev)
-                        recvs[bb] = (buf, comm.irecv(buf, src_rank))
+                recv_next = 0
+                recv_src = src_rank if (first > 0 and src_rank != comm.rank) else None
+
+            def post_recvs(upto):
+                # receives are posted in the sender's order, at most `window` ahead: the
+                # reference's max_activation_in_cpu back-pressure (utils.py:179-180) — a
+                # producer blocks (on its own RCCL stream, not the host) until we post
+                nonlocal recv_next
+                while recv_next < min(upto, len(batches)):
+                    bb = recv_next
+                    buf = torch.empty(self._state_shape(first - 1, batches[bb]), dtype=self.act_dtype,
+                                      device=self.dev)
+                    recvs[bb] = (buf, comm.irecv(buf, recv_src))
+                    recv_next += 1
+
             batch, meta = batches[b], metas[b]
             if first == 0:
                 state = None
-            elif b in recvs:
+            elif recv_src is not None:
+                post_recvs(b + self.recv_window(len(tps), len(batches)))
                 buf, work = recvs.pop(b)
                 work.wait()
                 state = buf
@@ -224,6 +246,10 @@ class ShardedRunner:
                     if layer_kind(name) == "decoder":
                         flops += layer_flops(self.cfg, batch)
             compute_s += time.perf_counter() - tc
+            if pbar is not None:
+                pbar.update(1)
+            if ck is not None and self._ckpt_due(k):
+                ck.save_state(k + 1, b, state)
             nxt = items[idx + 1] if idx + 1 < len(items) else None
             if last == self.L - 1:
                 out_pending.append(self._start_output_copy(batch, state))
@@ -253,6 +279,10 @@ class ShardedRunner:
             if pool_buf is not None:
                 store.recycle_host(pool_buf)
         store.clear()
+        if pbar is not None:
+            pbar.close()
+        if ck is not None:
+            ck.clear()                     # run complete: nothing to resume
         wall = time.perf_counter() - t_start
         self.stats = {
             "wall_s": wall, "compute_launch_s": compute_s,
@@ -261,11 +291,60 @@ class ShardedRunner:
             "decoder_flops": flops, "micro_batches": float(len(batches)),
             "weight_wait_s": pf.wait_seconds, "weight_h2d_bytes": float(pf.bytes_h2d - h2d0),
             "act_d2h_bytes": float(store.bytes_d2h), "act_h2d_bytes": float(store.bytes_h2d),
+            "resumed_from_shard": float(k0),
         }
         if self.verbose:
-            print(f"{self.dev} rank{comm.rank}: {len(self.my_shards)} shards, {len(batches)} micro-batches, "
+            # utils.py:304 prints "loaded N layers in Ts" per device
+            n_layers = sum(len(s) for s in self.my_shards[k0:])
+            print(f"{self.dev} rank{comm.rank}: loaded {n_layers} layers in {pf.wait_seconds:.2f}s "
+                  f"(exposed weight wait); {len(self.my_shards)} shards, {len(batches)} micro-batches, "
                   f"{self.stats['tokens']:.0f} tokens in {wall:.2f}s")
         return outputs
+
+    # ------------------------------------------------- progress / resume
+    def _progress(self, total: int):
+        """tqdm bar on rank 0 when verbose (the reference's tqdm over shards, utils.py:226-238)."""
+        if not (self.verbose and self.comm.rank == 0):
+            return None
+        try:
+            from tqdm import tqdm
+        except ImportError:
+            return None
+        return tqdm(total=total, desc=f"{self.dev} shard x micro-batch", unit="step")
+
+    def _ckpt_due(self, k: int) -> bool:
+        """Checkpoint after shard k (index into my_shards)?  Never after the shard with lm_head."""
+        e = self.checkpoint_every
+        return (e > 0 and (k + 1) % e == 0 and k + 1 < len(self.my_shards)
+                and self.my_shards[k][-1] < self.L - 1)
+
+    def _open_checkpoint(self, tps):
+        """-> (RunCheckpoint or None, first shard to run).  DP ranks agree on a common shard."""
+        if not self.resume_dir or not self.my_shards:
+            return None, 0
+        if self.plan.mode == "mp":
+            if self.verbose:
+                print("--resume_dir: ignored in model-parallel mode (in-flight pipeline state)")
+            return None, 0
+        from .runtime.checkpoint import RunCheckpoint, run_fingerprint
+        fp = run_fingerprint(self.cfg, [tp.prefix + [t for s in tp.suffixes for t in s] + [-1] for tp in tps],
+                             lnps=self.lnps, budget=self.token_budget, attn=self.prefix_attention,
+                             world=self.comm.world, rank=self.comm.rank, dp=self.data_parallel,
+                             dtype=str(self.act_dtype), every=self.checkpoint_every)
+        ck = RunCheckpoint(self.resume_dir, fp, self.comm.rank)
+        have = set(ck.available())
+        if self.comm.world > 1:
+            for other in self.comm.all_gather_object(sorted(have)):
+                have &= set(other)
+        k0 = max(have) if have else 0
+        if k0 and self.verbose:
+            print(f"rank{self.comm.rank}: resuming at shard {k0} from {ck.dir}")
+        return ck, k0
+
+    def recv_window(self, n_prompts: int, n_batches: int) -> int:
+        """Micro-batches a pipeline stage may have received but not consumed."""
+        per_mb = max(1.0, n_prompts / max(1, n_batches))
+        return max(2, int(self.max_act // per_mb))
 
     def _start_output_copy(self, batch: PackedBatch, probs: torch.Tensor):
         if not self.cuda:

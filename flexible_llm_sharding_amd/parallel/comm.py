@@ -127,6 +127,13 @@ class Comm:
         dist.gather_object(obj, out, dst=dst)
         return out
 
+    def all_gather_object(self, obj: Any) -> List[Any]:
+        if not self.active:
+            return [obj]
+        allv = [None] * self.world
+        dist.all_gather_object(allv, obj)
+        return allv
+
     def destroy(self):
         if self.active and dist.is_initialized():
             dist.destroy_process_group()

@@ -155,4 +155,6 @@ def build_dp_sharded_runner(args, cfg, device, comm: Comm, tok, store: Optional[
                          max_activation_in_cpu=args.max_activation_in_cpu,
                          prefix_attention=args.prefix_attention, token_budget=args.token_budget,
                          resident=getattr(args, "resident", False), comm=comm, data_parallel=True,
-                         act_dtype=act, prefetcher=pf, verbose=getattr(args, "verbose", False))
+                         act_dtype=act, prefetcher=pf, verbose=getattr(args, "verbose", False),
+                         resume_dir=getattr(args, "resume_dir", None),
+                         checkpoint_every=getattr(args, "checkpoint_every", 0))

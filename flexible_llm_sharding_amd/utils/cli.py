@@ -53,6 +53,10 @@ def build_parser() -> argparse.ArgumentParser:
                    help="activation dtype (default fp16 on GPU, fp32 on CPU)")
     p.add_argument("--verbose", type=str2bool, nargs="?", const=True, default=False)
     p.add_argument("--metrics_json", type=str, default=None, help="write run metrics here (rank 0)")
+    p.add_argument("--resume_dir", type=str, default=None,
+                   help="checkpoint inter-shard activations here and resume a crashed run from them "
+                        "(single-GPU / data-parallel)")
+    p.add_argument("--checkpoint_every", type=int, default=8, help="shards between checkpoints (with --resume_dir)")
     p.add_argument("--profile", type=str2bool, nargs="?", const=True, default=False,
                    help="emit roctx ranges (shard load / micro-batch compute) for rocprofv3 --marker-trace")
     return p

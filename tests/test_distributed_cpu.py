@@ -49,9 +49,12 @@ def _worker(rank, world, port, path, prompts, lnps, dp, storage, out_dir, budget
     for a, b in zip(outs, outs2):
         assert (a is None and b is None) or np.array_equal(a, b)
     allv = comm.gather_object(outs, dst=0)
+    resumed = comm.gather_object(r.stats["resumed_from_shard"], dst=0)
     if rank == 0:
         with open(os.path.join(out_dir, "out.pkl"), "wb") as f:
             pickle.dump(allv, f)
+        with open(os.path.join(out_dir, "resumed.pkl"), "wb") as f:
+            pickle.dump(resumed, f)
     comm.destroy()
 
 
@@ -92,7 +95,9 @@ def test_data_parallel(single, tmp_path, world):
         assert _close(a, b)
 
 
-def _dp_shard_worker(rank, world, port, path, prompts, lnps, out_dir):
+def _dp_shard_worker(rank, world, port, path, prompts, lnps, out_dir, resume_dir=None, fault=""):
+    if fault:
+        os.environ["FLS_FAULT"] = fault
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
                        "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
     torch.set_num_threads(1)
@@ -105,15 +110,19 @@ def _dp_shard_worker(rank, world, port, path, prompts, lnps, out_dir):
     cfg = ModelConfig.from_pretrained(path)
     args = SimpleNamespace(model_path=path, layer_num_per_shard=lnps, storage_location="cpu",
                            disk_folder=out_dir, max_activation_in_cpu=100, prefix_attention="bidirectional",
-                           token_budget=50, resident=False, dtype=None, verbose=False)
+                           token_budget=50, resident=False, dtype=None, verbose=False,
+                           resume_dir=resume_dir, checkpoint_every=2)
     r = build_dp_sharded_runner(args, cfg, "cpu", comm, load_tokenizer(path))
     assert r.prefetcher.__class__.__name__ == "AllGatherPrefetcher"
     idx = np.array_split(np.arange(len(prompts)), world)[rank]
     outs = r([prompts[i] for i in idx])
     allv = comm.gather_object(outs, dst=0)
+    resumed = comm.gather_object(r.stats["resumed_from_shard"], dst=0)
     if rank == 0:
         with open(os.path.join(out_dir, "out.pkl"), "wb") as f:
             pickle.dump(allv, f)
+        with open(os.path.join(out_dir, "resumed.pkl"), "wb") as f:
+            pickle.dump(resumed, f)
     comm.destroy()
 
 
@@ -143,3 +152,18 @@ def test_rank_failure_terminates_job(single, tmp_path):
                            start_method="spawn", join=True)
     assert "FLS_FAULT" in str(ei.value) or "exited" in str(ei.value) or "ProcessRaised" in type(ei.value).__name__
     assert time.time() - t0 < 120
+
+
+def test_data_parallel_resume_after_rank_fault(single, tmp_path):
+    """DP + --resume_dir: rank 1 dies at shard 3; the relaunch resumes every rank at shard 2."""
+    path, prompts, ref = single
+    ck = str(tmp_path / "ck")
+    with pytest.raises(Exception):
+        mp.start_processes(_dp_shard_worker, args=(2, _port(), path, prompts, 1, str(tmp_path), ck, "1:3"),
+                           nprocs=2, start_method="spawn", join=True)
+    mp.start_processes(_dp_shard_worker, args=(2, _port(), path, prompts, 1, str(tmp_path), ck, ""),
+                       nprocs=2, start_method="spawn", join=True)
+    assert pickle.load(open(tmp_path / "resumed.pkl", "rb")) == [2.0, 2.0]
+    got = sum(pickle.load(open(tmp_path / "out.pkl", "rb")), [])
+    for a, b in zip(got, ref):
+        assert _close(a, b)

@@ -1,4 +1,6 @@
 """CPU engine: mode equivalence, oracle parity, HF transformers parity (causal mode)."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -106,3 +108,42 @@ def test_bidirectional_differs_from_causal(ctx):
     ref = reference_scores(cfg, sd, tok, prompts, prefix_attention="causal")
     for x, rf in zip(a, ref):
         assert np.abs(x.astype(np.float32) - rf).max() < 1e-4
+
+
+def test_checkpoint_resume_after_fault(ctx, tmp_path, monkeypatch):
+    """--resume_dir: a run that dies at shard 3 restarts from the step-2 checkpoint and matches a clean run."""
+    path, cfg, tok, prompts, sd = ctx
+    src = FileLayerSource(cfg, path)
+
+    def runner():
+        return ShardedRunner(cfg, src, "cpu", tok, layer_num_per_shard=1, storage_location="cpu",
+                             token_budget=40, resume_dir=str(tmp_path / "ck"), checkpoint_every=2)
+
+    clean = ShardedRunner(cfg, src, "cpu", tok, layer_num_per_shard=1, token_budget=40)(prompts)
+    monkeypatch.setenv("FLS_FAULT", "0:3")          # tiny: 5 layers = 5 shards, checkpoint after shards 1, 3
+    with pytest.raises(RuntimeError, match="FLS_FAULT"):
+        runner()(prompts)
+    assert sorted(os.listdir(tmp_path / "ck" / "rank0")) == ["step2"]
+    monkeypatch.delenv("FLS_FAULT")
+    r = runner()
+    out = r(prompts)
+    assert r.stats["resumed_from_shard"] == 2
+    assert not (tmp_path / "ck").exists()             # cleared on completion
+    for a, b in zip(out, clean):
+        np.testing.assert_array_equal(a, b)
+    # different prompts -> fingerprint mismatch -> no resume
+    monkeypatch.setenv("FLS_FAULT", "0:4")
+    with pytest.raises(RuntimeError):
+        runner()(prompts)
+    monkeypatch.delenv("FLS_FAULT")
+    r = runner()
+    r(prompts[:3])
+    assert r.stats["resumed_from_shard"] == 0
+    # keep-last-two pruning
+    from flexible_llm_sharding_amd.runtime.checkpoint import RunCheckpoint
+    ck = RunCheckpoint(str(tmp_path / "k2"), "fp")
+    for k in (1, 2, 3):
+        ck.save_state(k, 0, torch.ones(2, 3))
+        ck.commit(k, [0], torch.float32)
+    assert ck.available() == [2, 3]
+    assert torch.equal(ck.load(3)[0], torch.ones(2, 3))

@@ -223,3 +223,33 @@ def test_gemm_autotune_choice():
     torch.cuda.synchronize()
     assert len(o.choice) == 1 and list(o.timings.values())[0]["choice"] in ("hip", "hipblaslt")
     assert rel_err(y, x.float() @ w.float().t()) < 2e-3
+
+
+@pytest.mark.parametrize("var", [1, 3, 6])
+def test_gemm_variants_all_epilogues(ops, ref, var):
+    """Every main-loop variant (v1 8-wave, v3 ping-pong, v6 one-wave-per-SIMD)
+    against fp32 references, with all four epilogues and a ragged M."""
+    from flexible_llm_sharding_amd.config import ModelConfig
+    from flexible_llm_sharding_amd.models.llama import rope_tables
+    M, H, I, nh, nkv, hd = 517, 512, 768, 4, 2, 128
+    ops.k.fls_gemm_set_variant(var)
+    try:
+        x = rnd(M, H, seed=31)
+        w = rnd(H, H, scale=0.05, seed=32)
+        assert rel_err(ops.gemm(x, w), x.float() @ w.float().t()) < 2e-3
+        r0 = rnd(M, H, seed=33)
+        out = ops.gemm(x, w, EPI_RESID, out=r0.clone(), resid=r0.clone())
+        assert rel_err(out, r0.float() + x.float() @ w.float().t()) < 2e-3
+        wgu = rnd(2 * I, H, scale=0.05, seed=34)
+        assert rel_err(ops.gemm(x, wgu, EPI_SWIGLU).cpu(), ref.swiglu_up(x.float().cpu(), wgu.float().cpu())) < 3e-3
+        wqkv = rnd((nh + 2 * nkv) * hd, H, scale=0.05, seed=35)
+        pos = torch.randint(0, 4000, (M,), dtype=torch.int32, device=DEV)
+        cfg = ModelConfig(hidden_size=nh * hd, num_attention_heads=nh, num_key_value_heads=nkv)
+        cos, sin = rope_tables(cfg, 4096)
+        y = ops.gemm(x, wqkv, EPI_ROPE, positions=pos, cos=cos.to(DEV), sin=sin.to(DEV),
+                     rope_cols=(nh + nkv) * hd, head_dim=hd)
+        r = ref.qkv_rope(x.float().cpu(), wqkv.float().cpu(), pos.cpu(), cos, sin, nh, nkv, hd)
+        assert rel_err(y.cpu(), r) < 3e-3
+        torch.cuda.synchronize()
+    finally:
+        ops.k.fls_gemm_set_variant(3)
