@@ -18,6 +18,20 @@ __device__ __forceinline__ floatx4 mfma16x16x32(half8 a, half8 b, floatx4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 
+// In-place accumulate on an AGPR-resident accumulator (dst tied to srcC).
+// Used where all 256 AGPRs hold accumulators: the builtin lets the register
+// allocator rename dst != srcC, which with zero spare AGPRs turns into copies
+// and spills.  The caller owns MFMA->VALU hazards on `c` after the last use.
+__device__ __forceinline__ void mfma_acc_inplace(floatx4& c, const half8& a, const half8& b) {
+  asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+}
+
+// Same, but also a compiler memory barrier: LDS reads / LDS-DMA written between
+// these statements issue exactly in source order (hand-interleaved schedules).
+__device__ __forceinline__ void mfma_acc_inplace_ordered(floatx4& c, const half8& a, const half8& b) {
+  asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b) : "memory");
+}
+
 // 16-byte global -> LDS DMA (dest = wave-uniform base + lane*16)
 __device__ __forceinline__ void glds16(const void* gsrc, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((const GLB_AS void*)gsrc, (LDS_AS void*)lds_wave_base, 16, 0, 0);

@@ -861,12 +861,512 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_v6(const half_t* __restrict__ 
   }
 }
 
+// ------------------------------------------------------------------ v7
+// 8 waves (2 M x 4 N, 128x64 outputs each), 256x256x64 tiles, 4 phases per
+// K-tile; each phase = {fragment ds_reads || one half-tile LDS-DMA} ->
+// barrier -> lgkmcnt(0) -> 16 MFMAs (one 64x32 C-quadrant x K=64, at raised
+// priority) -> barrier.  The four half-tiles of a stage are the row sets the
+// phases read, so each is re-filled as soon as its last reader has passed a
+// barrier:
+//   XA = X rows {0-63, 128-191}  (read phase 0)   XB = X rows {64-127, 192-255} (phase 2)
+//   WA = W rows {64w + 0..31}    (read phase 0)   WB = W rows {64w + 32..63}    (phase 1)
+// Issue order per K-tile t: ph0 XB(t+1) -> buf t+1; ph1 XA(t+2), ph2 WA(t+2),
+// ph3 WB(t+2) -> buf t (their regions were consumed in this tile).  One
+// counted `vmcnt(6)` (3 half-tiles x 2 pieces left in flight) before phase
+// 3's first barrier retires everything tile t+1 reads; no vmcnt(0) in the
+// loop, so staging latency overlaps ~1.5 K-tiles of MFMA work.
+// Out-of-range prefetches are clamped to the last K-tile (harmless re-loads into
+// consumed regions) so the wait count is uniform.
+namespace v7 {
+constexpr int BUF = 65536;        // one stage: X image 32 KiB + W image 32 KiB
+constexpr int WIMG = 32768;
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_nt_v7(const half_t* __restrict__ A, const half_t* __restrict__ W,
+                                                    half_t* __restrict__ C, int M, int N, int K, int lda, int ldw,
+                                                    int ldc, Epi ep) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  const int nwg = gridDim.x;
+  int bid = blockIdx.x;
+  {
+    const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7, loc = bid >> 3;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+  }
+  const int tiles_m = (M + BM - 1) / BM;
+  const int tiles_n = N / BN;
+  constexpr int GROUP_M = 8;
+  const int group = bid / (GROUP_M * tiles_n);
+  const int first_m = group * GROUP_M;
+  const int gsz = min(tiles_m - first_m, GROUP_M);
+  const int in_g = bid - group * GROUP_M * tiles_n;
+  const int tm = first_m + in_g % gsz;
+  const int tn = in_g / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // ---- staging: each wave moves pieces j = 2*wave, 2*wave+1 (8 rows x 128 B) of a half-tile
+  const int lr = lane >> 3;
+  const int lc = (lane & 7) ^ lr;              // source-side XOR swizzle (LDS image stays lane-linear)
+  const int j0 = 2 * wave, j1 = 2 * wave + 1;
+  const int xr0 = (j0 >> 3) * 128 + (j0 & 7) * 8, xr1 = (j1 >> 3) * 128 + (j1 & 7) * 8;   // XA rows; XB = +64
+  const int wr0 = (j0 >> 2) * 64 + (j0 & 3) * 8, wr1 = (j1 >> 2) * 64 + (j1 & 3) * 8;     // WA rows; WB = +32
+  const half_t* xa0 = A + (size_t)min(m0 + xr0 + lr, M - 1) * lda + lc * 8;
+  const half_t* xa1 = A + (size_t)min(m0 + xr1 + lr, M - 1) * lda + lc * 8;
+  const half_t* xb0 = A + (size_t)min(m0 + xr0 + 64 + lr, M - 1) * lda + lc * 8;
+  const half_t* xb1 = A + (size_t)min(m0 + xr1 + 64 + lr, M - 1) * lda + lc * 8;
+  const half_t* wa0 = W + (size_t)(n0 + wr0 + lr) * ldw + lc * 8;
+  const half_t* wa1 = W + (size_t)(n0 + wr1 + lr) * ldw + lc * 8;
+  const size_t wb_off = (size_t)32 * ldw;
+#define V7_XA(buf, k0) { glds16(xa0 + (k0), smem + (buf) * v7::BUF + xr0 * 128); \
+                         glds16(xa1 + (k0), smem + (buf) * v7::BUF + xr1 * 128); }
+#define V7_XB(buf, k0) { glds16(xb0 + (k0), smem + (buf) * v7::BUF + (xr0 + 64) * 128); \
+                         glds16(xb1 + (k0), smem + (buf) * v7::BUF + (xr1 + 64) * 128); }
+#define V7_WA(buf, k0) { glds16(wa0 + (k0), smem + (buf) * v7::BUF + v7::WIMG + wr0 * 128); \
+                         glds16(wa1 + (k0), smem + (buf) * v7::BUF + v7::WIMG + wr1 * 128); }
+#define V7_WB(buf, k0) { glds16(wa0 + wb_off + (k0), smem + (buf) * v7::BUF + v7::WIMG + (wr0 + 32) * 128); \
+                         glds16(wa1 + wb_off + (k0), smem + (buf) * v7::BUF + v7::WIMG + (wr1 + 32) * 128); }
+
+  // ---- fragments: lane (fr, grp) reads row fr of a 16-row fragment, k chunk s*4+grp
+  const int wm = wave >> 2, wn = wave & 3;
+  const int fr = lane & 15, grp = lane >> 4;
+  const int sw = fr & 7;
+  const int c0 = ((0 + grp) ^ sw) << 4;         // k-step 0 chunk
+  const int c1 = ((4 + grp) ^ sw) << 4;         // k-step 1 chunk
+  const int xrow = (wm * 128 + fr) * 128;
+  const int wrow = v7::WIMG + (wn * 64 + fr) * 128;
+
+  floatx4 acc[8][4];
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[u][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  half8 xf[8][2], wf[4][2];
+
+#define V7_RX(buf, u0)                                                                              \
+  _Pragma("unroll") for (int u_ = (u0); u_ < (u0) + 4; ++u_) {                                      \
+    xf[u_][0] = *(const half8*)(smem + (buf) * v7::BUF + xrow + u_ * 2048 + c0);                    \
+    xf[u_][1] = *(const half8*)(smem + (buf) * v7::BUF + xrow + u_ * 2048 + c1);                    \
+  }
+#define V7_RW(buf, t0)                                                                              \
+  _Pragma("unroll") for (int t_ = (t0); t_ < (t0) + 2; ++t_) {                                      \
+    wf[t_][0] = *(const half8*)(smem + (buf) * v7::BUF + wrow + t_ * 2048 + c0);                    \
+    wf[t_][1] = *(const half8*)(smem + (buf) * v7::BUF + wrow + t_ * 2048 + c1);                    \
+  }
+#define V7_MMA(u0, t0)                                                                              \
+  {                                                                                                 \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                              \
+    __builtin_amdgcn_s_setprio(1);                                                                  \
+    _Pragma("unroll") for (int s_ = 0; s_ < 2; ++s_)                                                \
+    _Pragma("unroll") for (int u_ = (u0); u_ < (u0) + 4; ++u_)                                      \
+    _Pragma("unroll") for (int t_ = (t0); t_ < (t0) + 2; ++t_)                                      \
+      acc[u_][t_] = mfma16x16x32(wf[t_][s_], xf[u_][s_], acc[u_][t_]);                              \
+    __builtin_amdgcn_s_setprio(0);                                                                  \
+  }
+
+  const int nk = K / BK;
+  const int k1p = min(1, nk - 1) * BK;
+  V7_XA(0, 0); V7_WA(0, 0); V7_WB(0, 0); V7_XB(0, 0);
+  V7_XA(1, k1p); V7_WA(1, k1p); V7_WB(1, k1p);
+  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const int k1 = min(kt + 1, nk - 1) * BK;
+    const int k2 = min(kt + 2, nk - 1) * BK;
+    // phase 0: read X-half0 + W-half0; stage XB(t+1)
+    V7_RX(cur, 0); V7_RW(cur, 0);
+    V7_XB(cur ^ 1, k1);
+    __builtin_amdgcn_s_barrier();
+    V7_MMA(0, 0);
+    __builtin_amdgcn_s_barrier();
+    // phase 1: read W-half1; stage XA(t+2)
+    V7_RW(cur, 2);
+    V7_XA(cur, k2);
+    __builtin_amdgcn_s_barrier();
+    V7_MMA(0, 2);
+    __builtin_amdgcn_s_barrier();
+    // phase 2: read X-half1; stage WA(t+2)
+    V7_RX(cur, 4);
+    V7_WA(cur, k2);
+    __builtin_amdgcn_s_barrier();
+    V7_MMA(4, 2);
+    __builtin_amdgcn_s_barrier();
+    // phase 3: stage WB(t+2); retire everything tile t+1 reads
+    V7_WB(cur, k2);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    V7_MMA(4, 0);
+    __builtin_amdgcn_s_barrier();
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may land after the block exits
+#undef V7_MMA
+#undef V7_RW
+#undef V7_RX
+#undef V7_WB
+#undef V7_WA
+#undef V7_XB
+#undef V7_XA
+
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int m = m0 + wm * 128 + u * 16 + fr;
+    if (m < M) {
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+        store_pair<EPI>(C, ldc, m, n0 + wn * 64 + p * 32, grp, acc[u][2 * p], acc[u][2 * p + 1], ep);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ v8
+// v7's tile/wave geometry with the fragment reads moved ONE PHASE AHEAD of
+// the MFMAs that use them, so LDS read latency hides behind a phase of MFMA
+// work instead of being exposed before it.  This works without extra
+// registers because the quadrant order alternates with tile parity:
+//   even tile: (x0,w0) (x0,w1) (x1,w1) (x1,w0)    odd tile: (x0,w1) (x0,w0) (x1,w0) (x1,w1)
+// so in every phase exactly one fragment half (4 or 8 ds_read_b128) is free
+// and is refilled for a later phase:
+//   even t: ph0 w1(t)  ph1 x1(t)  ph2 x0(t+1)  ph3 w1(t+1)
+//   odd t:  ph0 w0(t)  ph1 x1(t)  ph2 x0(t+1)  ph3 w0(t+1)
+// Half-tile k of tile t+2 is DMA'd in phase k of tile t (XA, W-first, W-second,
+// XB), each exactly 6 phases before its first read; per phase:
+//   lgkmcnt(0) -> ds_reads (next) -> 2 glds -> vmcnt(10) -> s_barrier -> 16 MFMA
+// One barrier per phase covers both hazards: RAW (every wave's counted vmcnt
+// precedes the barrier before the read) and WAR (a region is refilled >= 2
+// phases after its reads were issued, i.e. after a barrier that follows their
+// lgkmcnt(0)).  Up to 6 half-tiles (96 KiB) of staging are in flight per CU.
+// Requires an even number of K-tiles (2-tile unrolled body).
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_nt_v8(const half_t* __restrict__ A, const half_t* __restrict__ W,
+                                                    half_t* __restrict__ C, int M, int N, int K, int lda, int ldw,
+                                                    int ldc, Epi ep) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  const int nwg = gridDim.x;
+  int bid = blockIdx.x;
+  {
+    const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7, loc = bid >> 3;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+  }
+  const int tiles_m = (M + BM - 1) / BM;
+  const int tiles_n = N / BN;
+  constexpr int GROUP_M = 8;
+  const int group = bid / (GROUP_M * tiles_n);
+  const int first_m = group * GROUP_M;
+  const int gsz = min(tiles_m - first_m, GROUP_M);
+  const int in_g = bid - group * GROUP_M * tiles_n;
+  const int tm = first_m + in_g % gsz;
+  const int tn = in_g / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int lr = lane >> 3;
+  const int lc = (lane & 7) ^ lr;
+  const int j0 = 2 * wave, j1 = 2 * wave + 1;
+  const int xr0 = (j0 >> 3) * 128 + (j0 & 7) * 8, xr1 = (j1 >> 3) * 128 + (j1 & 7) * 8;
+  const int wr0 = (j0 >> 2) * 64 + (j0 & 3) * 8, wr1 = (j1 >> 2) * 64 + (j1 & 3) * 8;
+  const half_t* xa0 = A + (size_t)min(m0 + xr0 + lr, M - 1) * lda + lc * 8;
+  const half_t* xa1 = A + (size_t)min(m0 + xr1 + lr, M - 1) * lda + lc * 8;
+  const half_t* xb0 = A + (size_t)min(m0 + xr0 + 64 + lr, M - 1) * lda + lc * 8;
+  const half_t* xb1 = A + (size_t)min(m0 + xr1 + 64 + lr, M - 1) * lda + lc * 8;
+  const half_t* wa0 = W + (size_t)(n0 + wr0 + lr) * ldw + lc * 8;
+  const half_t* wa1 = W + (size_t)(n0 + wr1 + lr) * ldw + lc * 8;
+  const size_t wb_off = (size_t)32 * ldw;
+#define V8_XA(buf, k0) { glds16(xa0 + (k0), smem + (buf) * v7::BUF + xr0 * 128); \
+                         glds16(xa1 + (k0), smem + (buf) * v7::BUF + xr1 * 128); }
+#define V8_XB(buf, k0) { glds16(xb0 + (k0), smem + (buf) * v7::BUF + (xr0 + 64) * 128); \
+                         glds16(xb1 + (k0), smem + (buf) * v7::BUF + (xr1 + 64) * 128); }
+#define V8_WA(buf, k0) { glds16(wa0 + (k0), smem + (buf) * v7::BUF + v7::WIMG + wr0 * 128); \
+                         glds16(wa1 + (k0), smem + (buf) * v7::BUF + v7::WIMG + wr1 * 128); }
+#define V8_WB(buf, k0) { glds16(wa0 + wb_off + (k0), smem + (buf) * v7::BUF + v7::WIMG + (wr0 + 32) * 128); \
+                         glds16(wa1 + wb_off + (k0), smem + (buf) * v7::BUF + v7::WIMG + (wr1 + 32) * 128); }
+
+  const int wm = wave >> 2, wn = wave & 3;
+  const int fr = lane & 15, grp = lane >> 4;
+  const int sw = fr & 7;
+  const int c0 = ((0 + grp) ^ sw) << 4;
+  const int c1 = ((4 + grp) ^ sw) << 4;
+  const int xrow = (wm * 128 + fr) * 128;
+  const int wrow = v7::WIMG + (wn * 64 + fr) * 128;
+
+  floatx4 acc[8][4];
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[u][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  half8 xf[8][2], wf[4][2];
+
+#define V8_RX(buf, h)                                                                               \
+  _Pragma("unroll") for (int u_ = (h) * 4; u_ < (h) * 4 + 4; ++u_) {                                \
+    xf[u_][0] = *(const half8*)(smem + (buf) * v7::BUF + xrow + u_ * 2048 + c0);                    \
+    xf[u_][1] = *(const half8*)(smem + (buf) * v7::BUF + xrow + u_ * 2048 + c1);                    \
+  }
+#define V8_RW(buf, h)                                                                               \
+  _Pragma("unroll") for (int t_ = (h) * 2; t_ < (h) * 2 + 2; ++t_) {                                \
+    wf[t_][0] = *(const half8*)(smem + (buf) * v7::BUF + wrow + t_ * 2048 + c0);                    \
+    wf[t_][1] = *(const half8*)(smem + (buf) * v7::BUF + wrow + t_ * 2048 + c1);                    \
+  }
+#define V8_PHASE(xh, wh, READ, DMA)                                                                 \
+  {                                                                                                 \
+    __builtin_amdgcn_s_waitcnt(0xC07F);     /* lgkmcnt(0), visible to the waitcnt pass */          \
+    READ;                                                                                           \
+    DMA;                                                                                            \
+    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");                                               \
+    __builtin_amdgcn_s_barrier();                                                                   \
+    __builtin_amdgcn_s_setprio(1);                                                                  \
+    _Pragma("unroll") for (int s_ = 0; s_ < 2; ++s_)                                                \
+    _Pragma("unroll") for (int u_ = (xh) * 4; u_ < (xh) * 4 + 4; ++u_)                              \
+    _Pragma("unroll") for (int t_ = (wh) * 2; t_ < (wh) * 2 + 2; ++t_)                              \
+      acc[u_][t_] = mfma16x16x32(wf[t_][s_], xf[u_][s_], acc[u_][t_]);                              \
+    __builtin_amdgcn_s_setprio(0);                                                                  \
+  }
+
+  const int nk = K / BK;                       // even (host-checked)
+  // prologue = virtual phases -8..-1: tile 0 -> buf 0 (XA, WA, WB, XB), tile 1 -> buf 1 (XA, WB, WA, XB)
+  V8_XA(0, 0); V8_WA(0, 0); V8_WB(0, 0); V8_XB(0, 0);
+  V8_XA(1, BK); V8_WB(1, BK); V8_WA(1, BK); V8_XB(1, BK);
+  asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  V8_RX(0, 0); V8_RW(0, 0);                    // x0(0), w0(0): tile 0's first quadrant
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int kt = 0; kt < nk; kt += 2) {
+    const int ka = min(kt + 2, nk - 1) * BK;   // tile kt+2 -> buf 0
+    const int kb = min(kt + 3, nk - 1) * BK;   // tile kt+3 -> buf 1
+    // even tile kt (buf 0)
+    V8_PHASE(0, 0, V8_RW(0, 1), V8_XA(0, ka));
+    V8_PHASE(0, 1, V8_RX(0, 1), V8_WA(0, ka));
+    V8_PHASE(1, 1, V8_RX(1, 0), V8_WB(0, ka));
+    V8_PHASE(1, 0, V8_RW(1, 1), V8_XB(0, ka));
+    // odd tile kt+1 (buf 1)
+    V8_PHASE(0, 1, V8_RW(1, 0), V8_XA(1, kb));
+    V8_PHASE(0, 0, V8_RX(1, 1), V8_WB(1, kb));
+    V8_PHASE(1, 0, V8_RX(0, 0), V8_WA(1, kb));
+    V8_PHASE(1, 1, V8_RW(0, 0), V8_XB(1, kb));
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#undef V8_PHASE
+#undef V8_RW
+#undef V8_RX
+#undef V8_WB
+#undef V8_WA
+#undef V8_XB
+#undef V8_XA
+
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int m = m0 + wm * 128 + u * 16 + fr;
+    if (m < M) {
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+        store_pair<EPI>(C, ldc, m, n0 + wn * 64 + p * 32, grp, acc[u][2 * p], acc[u][2 * p + 1], ep);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ v9
+// v6's geometry (4 waves = one per SIMD, 128x128 outputs per wave in 256
+// AGPR accumulators: 2/3 of the LDS fragment reads per FLOP of the 8-wave
+// kernels) with v8's read-ahead schedule, and the LDS reads and DMA
+// interleaved INTO the MFMA stream (one wave per SIMD: nothing else would
+// fill the matrix pipe while they issue).  Per phase (one 64x64 quadrant x
+// K=64 = 32 MFMAs):
+//   32 MFMA || {8 ds_read_b128 of a fragment half for a later phase, then one
+//   half-tile of LDS-DMA (4 per lane)}  ->  lgkmcnt(0), vmcnt(24)  ->  s_barrier
+// Quadrant order alternates with tile parity exactly as in v8.  Reads issued
+// in phase P complete before barrier P+1, so their region is refilled in
+// phase P+1; each half-tile is read 7 phases after it is issued (6 younger
+// half-tiles = 24 LDS-DMA ops stay in flight across every barrier).
+// Half-tile issue in tile t: ph0 W-first(t+2), ph1 W-second(t+2), ph2 XB(t+2),
+// ph3 XA(t+3).  Requires an even number of K-tiles.
+namespace v9 {
+constexpr int BUF = 65536, WIMG = 32768;
+}
+
+template <int EPI>
+__global__ __launch_bounds__(256, 1) void gemm_nt_v9(const half_t* __restrict__ A, const half_t* __restrict__ W,
+                                                    half_t* __restrict__ C, int M, int N, int K, int lda, int ldw,
+                                                    int ldc, Epi ep) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  const int nwg = gridDim.x;
+  int bid = blockIdx.x;
+  {
+    const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7, loc = bid >> 3;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+  }
+  const int tiles_m = (M + BM - 1) / BM;
+  const int tiles_n = N / BN;
+  constexpr int GROUP_M = 8;
+  const int group = bid / (GROUP_M * tiles_n);
+  const int first_m = group * GROUP_M;
+  const int gsz = min(tiles_m - first_m, GROUP_M);
+  const int in_g = bid - group * GROUP_M * tiles_n;
+  const int tm = first_m + in_g % gsz;
+  const int tn = in_g / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // staging: a half-tile = 16 pieces of 8 rows x 128 B, rows {(j>>3)*128 + (j&7)*8} (+64 for the B half);
+  // wave w moves pieces 4w .. 4w+3
+  const int lr = lane >> 3;
+  const int lc = (lane & 7) ^ lr;
+  int prow[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int j = 4 * wave + i;
+    prow[i] = (j >> 3) * 128 + (j & 7) * 8;
+  }
+  // per-lane 32-bit byte offsets; the K offset goes into the (scalar) base pointer so every
+  // LDS-DMA is the saddr + voffset form (no per-lane 64-bit address registers)
+  unsigned xo[8], wo[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    xo[i] = (unsigned)(min(m0 + prow[i] + lr, M - 1) * lda + lc * 8) * 2u;
+    xo[4 + i] = (unsigned)(min(m0 + prow[i] + 64 + lr, M - 1) * lda + lc * 8) * 2u;
+    wo[i] = (unsigned)((prow[i] + lr) * ldw + lc * 8) * 2u;
+  }
+  const char* Ab = (const char*)A;
+  const char* Wb = (const char*)(W + (size_t)n0 * ldw);
+  const size_t wb_off = (size_t)64 * ldw * 2;
+#define V9_X(buf, hb, k0)                                                                         \
+  _Pragma("unroll") for (int i_ = 0; i_ < 4; ++i_)                                                \
+    glds16(Ab + (size_t)(k0) * 2 + xo[(hb) * 4 + i_], smem + (buf) * v9::BUF + (prow[i_] + (hb) * 64) * 128);
+#define V9_W(buf, hb, k0)                                                                         \
+  _Pragma("unroll") for (int i_ = 0; i_ < 4; ++i_)                                                \
+    glds16(Wb + (hb) * wb_off + (size_t)(k0) * 2 + wo[i_], smem + (buf) * v9::BUF + v9::WIMG + (prow[i_] + (hb) * 64) * 128);
+
+  const int wm = wave >> 1, wn = wave & 1;
+  const int fr = lane & 15, grp = lane >> 4;
+  const int sw = fr & 7;
+  const int c0 = ((0 + grp) ^ sw) << 4;
+  const int c1 = ((4 + grp) ^ sw) << 4;
+  const int xrow = (wm * 128 + fr) * 128;
+  const int wrow = v9::WIMG + (wn * 128 + fr) * 128;
+
+  floatx4 acc[8][8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc[u][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  half8 xf[8][2], wf[8][2];
+#define V9_FENCE_ACC()                                                                            \
+  _Pragma("unroll") for (int u_ = 0; u_ < 8; ++u_)                                                \
+  _Pragma("unroll") for (int t_ = 0; t_ < 8; ++t_) asm volatile("" : "+a"(acc[u_][t_]));
+  // zero-init (VALU AGPR writes) must not sit right before the first asm MFMA reading them
+  V9_FENCE_ACC();
+  asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+
+#define V9_RX(buf, h)                                                                             \
+  _Pragma("unroll") for (int u_ = (h) * 4; u_ < (h) * 4 + 4; ++u_) {                              \
+    xf[u_][0] = *(const half8*)(smem + (buf) * v9::BUF + xrow + u_ * 2048 + c0);                  \
+    xf[u_][1] = *(const half8*)(smem + (buf) * v9::BUF + xrow + u_ * 2048 + c1);                  \
+  }
+#define V9_RW(buf, h)                                                                             \
+  _Pragma("unroll") for (int t_ = (h) * 4; t_ < (h) * 4 + 4; ++t_) {                              \
+    wf[t_][0] = *(const half8*)(smem + (buf) * v9::BUF + wrow + t_ * 2048 + c0);                  \
+    wf[t_][1] = *(const half8*)(smem + (buf) * v9::BUF + wrow + t_ * 2048 + c1);                  \
+  }
+  // one phase: reads for a later phase, one half-tile of DMA, 32 MFMAs (interleaved), waits, barrier
+// one phase: 32 MFMAs (k-step outer, 4x4 tiles of the quadrant) with, in issue order,
+// one ds_read after each of the first 16 even-numbered MFMAs (the 8 reads of the half
+// needed later) and the half-tile's 4 LDS-DMA ops after MFMAs 17, 20, 23, 26;
+// then lgkmcnt(0) + counted vmcnt + barrier.  RX: 1 = read an X half, 0 = a W half.
+#define V9_PHASE(xh, wh, RX, rbuf, rh, DX, dbuf, dhb, dk0)                                        \
+  {                                                                                               \
+    _Pragma("unroll") for (int i_ = 0; i_ < 32; ++i_) {                                           \
+      const int s_ = i_ >> 4, u_ = (xh) * 4 + ((i_ >> 2) & 3), t_ = (wh) * 4 + (i_ & 3);          \
+      mfma_acc_inplace_ordered(acc[u_][t_], wf[t_][s_], xf[u_][s_]);                              \
+      if (i_ < 16 && (i_ & 1) == 0) {                                                             \
+        const int f_ = (rh) * 4 + (i_ >> 2), k_ = (i_ >> 1) & 1;                                  \
+        if (RX)                                                                                   \
+          xf[f_][k_] = *(const half8*)(smem + (rbuf) * v9::BUF + xrow + f_ * 2048 + (k_ ? c1 : c0)); \
+        else                                                                                      \
+          wf[f_][k_] = *(const half8*)(smem + (rbuf) * v9::BUF + wrow + f_ * 2048 + (k_ ? c1 : c0)); \
+      }                                                                                           \
+      if (i_ >= 17 && i_ <= 26 && (i_ - 17) % 3 == 0) {                                           \
+        const int p_ = (i_ - 17) / 3;                                                             \
+        if (DX)                                                                                   \
+          glds16(Ab + (size_t)(dk0) * 2 + xo[(dhb) * 4 + p_],                                     \
+                 smem + (dbuf) * v9::BUF + (prow[p_] + (dhb) * 64) * 128);                        \
+        else                                                                                      \
+          glds16(Wb + (dhb) * wb_off + (size_t)(dk0) * 2 + wo[p_],                                \
+                 smem + (dbuf) * v9::BUF + v9::WIMG + (prow[p_] + (dhb) * 64) * 128);             \
+      }                                                                                           \
+    }                                                                                             \
+    __builtin_amdgcn_s_waitcnt(0xC07F);                   /* lgkmcnt(0) */                        \
+    asm volatile("s_waitcnt vmcnt(24)" ::: "memory");                                             \
+    __builtin_amdgcn_s_barrier();                                                                 \
+  }
+
+  const int nk = K / BK;                       // even (host-checked)
+  const int kc1 = min(1, nk - 1) * BK, kc2 = min(2, nk - 1) * BK;
+  // prologue: XA0 WA0 WB0 XB0 | XA1 WB1 WA1 XB1 ; read x0(0), w0(0) ; then XA2
+  V9_X(0, 0, 0); V9_W(0, 0, 0); V9_W(0, 1, 0); V9_X(0, 1, 0);
+  V9_X(1, 0, kc1); V9_W(1, 1, kc1); V9_W(1, 0, kc1); V9_X(1, 1, kc1);
+  asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  V9_RX(0, 0); V9_RW(0, 0);
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_s_barrier();
+  V9_X(0, 0, kc2);
+  asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  for (int kt = 0; kt < nk; kt += 2) {
+    const int ka = min(kt + 2, nk - 1) * BK;   // tile kt+2 (even, buf 0)
+    const int kb = min(kt + 3, nk - 1) * BK;   // tile kt+3 (odd, buf 1)
+    const int kc = min(kt + 4, nk - 1) * BK;   // tile kt+4 (even, buf 0)
+    // even tile kt, buf 0: W-first = WA, W-second = WB
+    V9_PHASE(0, 0, 0, 0, 1, 0, 0, 0, ka);    // read w1(kt)        ; DMA WA(kt+2)
+    V9_PHASE(0, 1, 1, 0, 1, 0, 0, 1, ka);    // read x1(kt)        ; DMA WB(kt+2)
+    V9_PHASE(1, 1, 1, 1, 0, 1, 0, 1, ka);    // read x0(kt+1)      ; DMA XB(kt+2)
+    V9_PHASE(1, 0, 0, 1, 1, 1, 1, 0, kb);    // read w1(kt+1)      ; DMA XA(kt+3)
+    // odd tile kt+1, buf 1: W-first = WB, W-second = WA
+    V9_PHASE(0, 1, 0, 1, 0, 0, 1, 1, kb);    // read w0(kt+1)      ; DMA WB(kt+3)
+    V9_PHASE(0, 0, 1, 1, 1, 0, 1, 0, kb);    // read x1(kt+1)      ; DMA WA(kt+3)
+    V9_PHASE(1, 0, 1, 0, 0, 1, 1, 1, kb);    // read x0(kt+2)      ; DMA XB(kt+3)
+    V9_PHASE(1, 1, 0, 0, 0, 1, 0, 0, kc);    // read w0(kt+2)      ; DMA XA(kt+4)
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // the accumulators were written by inline-asm MFMAs the hazard recognizer cannot see:
+  // the nops give the last ones their passes, and the tied empty asms (ordered after the
+  // nops, being volatile too) make every later AGPR read depend on them
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  V9_FENCE_ACC();
+#undef V9_FENCE_ACC
+#undef V9_PHASE
+#undef V9_RW
+#undef V9_RX
+#undef V9_W
+#undef V9_X
+
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int m = m0 + wm * 128 + u * 16 + fr;
+    if (m < M) {
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+        store_pair<EPI>(C, ldc, m, n0 + wn * 128 + p * 32, grp, acc[u][2 * p], acc[u][2 * p + 1], ep);
+    }
+  }
+}
+
 int g_variant = -1;   // -1: from env FLS_GEMM_VARIANT (default 3)
 
 int variant() {
   if (g_variant < 0) {
     const char* e = getenv("FLS_GEMM_VARIANT");
-    g_variant = e ? atoi(e) : 3;
+    g_variant = e ? atoi(e) : 9;
   }
   return g_variant;
 }
@@ -874,11 +1374,35 @@ int variant() {
 template <int EPI>
 int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int lda, int ldw, int ldc,
            const Epi& ep, hipStream_t s) {
-  const int var = variant();
+  int var = variant();
   const bool fast = (N % BN == 0) && (K % BK == 0) && (lda % 8 == 0) && (ldw % 8 == 0) && M > 0;
+  // v8/v9 need an even K-tile count (2-tile unrolled body), v9 32-bit X offsets; else v3
+  const bool even_k = (K / BK) % 2 == 0;
+  if ((var == 9 && !(even_k && (size_t)M * lda * 2 < (1ull << 32))) || (var == 8 && !even_k)) var = 3;
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
   const bool fast4 = fast && (K % (2 * v4::BK4) == 0);
-  if (var == 6 && fast) {
+  if (var == 9 && fast) {
+    static bool attr9 = false;
+    if (!attr9) {
+      (void)hipFuncSetAttribute((const void*)gemm_nt_v9<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * v9::BUF);
+      attr9 = true;
+    }
+    hipLaunchKernelGGL(gemm_nt_v9<EPI>, dim3(tiles), dim3(256), 2 * v9::BUF, s, A, W, C, M, N, K, lda, ldw, ldc, ep);
+  } else if (var == 8 && fast) {
+    static bool attr8 = false;
+    if (!attr8) {
+      (void)hipFuncSetAttribute((const void*)gemm_nt_v8<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * v7::BUF);
+      attr8 = true;
+    }
+    hipLaunchKernelGGL(gemm_nt_v8<EPI>, dim3(tiles), dim3(512), 2 * v7::BUF, s, A, W, C, M, N, K, lda, ldw, ldc, ep);
+  } else if (var == 7 && fast) {
+    static bool attr7 = false;
+    if (!attr7) {
+      (void)hipFuncSetAttribute((const void*)gemm_nt_v7<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * v7::BUF);
+      attr7 = true;
+    }
+    hipLaunchKernelGGL(gemm_nt_v7<EPI>, dim3(tiles), dim3(512), 2 * v7::BUF, s, A, W, C, M, N, K, lda, ldw, ldc, ep);
+  } else if (var == 6 && fast) {
     static bool attr6 = false;
     if (!attr6) {
       (void)hipFuncSetAttribute((const void*)gemm_nt_v6<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);

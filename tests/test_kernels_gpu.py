@@ -225,9 +225,9 @@ def test_gemm_autotune_choice():
     assert rel_err(y, x.float() @ w.float().t()) < 2e-3
 
 
-@pytest.mark.parametrize("var", [1, 3, 6])
+@pytest.mark.parametrize("var", [1, 3, 6, 7, 8, 9])
 def test_gemm_variants_all_epilogues(ops, ref, var):
-    """Every main-loop variant (v1 8-wave, v3 ping-pong, v6 one-wave-per-SIMD)
+    """Every main-loop variant (v1 8-wave, v3 ping-pong, v6 one-wave-per-SIMD, v7 counted-vmcnt phases)
     against fp32 references, with all four epilogues and a ragged M."""
     from flexible_llm_sharding_amd.config import ModelConfig
     from flexible_llm_sharding_amd.models.llama import rope_tables
@@ -252,4 +252,4 @@ def test_gemm_variants_all_epilogues(ops, ref, var):
         assert rel_err(y.cpu(), r) < 3e-3
         torch.cuda.synchronize()
     finally:
-        ops.k.fls_gemm_set_variant(3)
+        ops.k.fls_gemm_set_variant(9)
