@@ -60,6 +60,9 @@ int fls_softmax_rows(const void* logits, void* probs, int rows, int V, fls_strea
 int fls_rope_inplace(void* y, const int* pos, const float* cos_t, const float* sin_t, int M, int ld,
                      int rope_cols, int head_dim, fls_stream_t s);
 int fls_swiglu(const void* y, void* out, int M, int I, int ldy, int ldo, fls_stream_t s);
+// C[M,N] = X[M,K] W[N,K]^T for M <= 16 (skinny LM head); K % 32 == 0
+int fls_gemv_skinny(const void* x, const void* w, void* c, int M, int N, int K, int ldx, int ldw, int ldc,
+                    fls_stream_t s);
 int fls_fill_random(void* dst, uint64_t n_elems, uint64_t seed, float mean, float std,
                     fls_stream_t s);
 

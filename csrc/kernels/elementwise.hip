@@ -223,6 +223,57 @@ __global__ __launch_bounds__(256) void swiglu_kernel(const half_t* __restrict__ 
   *(half8*)(out + (size_t)m * ldo + c) = o;
 }
 
+
+// ---------------------------------------------------------------- skinny GEMV
+// C[M, N] = X[M, K] . W[N, K]^T for M <= 16 (LM head of a small batch, K12):
+// weight-streaming, one wave per 32 W rows (two v_mfma_f32_16x16x32_f16 tiles
+// sharing the X fragment; X rows >= M are zero lanes), four K-steps of loads in
+// flight per wave.  W is read exactly once; X (<= 256 KB) stays in L2.
+constexpr int GV_U = 4;
+__global__ __launch_bounds__(256) void gemv_skinny_kernel(const half_t* __restrict__ X, const half_t* __restrict__ W,
+                                                          half_t* __restrict__ C, int M, int N, int K, int ldx,
+                                                          int ldw, int ldc) {
+  const int lane = threadIdx.x & 63;
+  const int n0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 32;
+  if (n0 >= N) return;
+  const int fr = lane & 15, grp = lane >> 4;
+  const half_t* wa = W + (size_t)min(n0 + fr, N - 1) * ldw + grp * 8;
+  const half_t* wb = W + (size_t)min(n0 + 16 + fr, N - 1) * ldw + grp * 8;
+  const bool xrow = fr < M;
+  const half_t* xp = X + (size_t)(xrow ? fr : 0) * ldx + grp * 8;
+  floatx4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+  const half8 zero = {};
+  int k = 0;
+  for (; k + 32 * GV_U <= K; k += 32 * GV_U) {
+    half8 fa[GV_U], fb[GV_U], fx[GV_U];
+#pragma unroll
+    for (int u = 0; u < GV_U; ++u) {
+      fa[u] = __builtin_nontemporal_load((const half8*)(wa + k + u * 32));
+      fb[u] = __builtin_nontemporal_load((const half8*)(wb + k + u * 32));
+      fx[u] = xrow ? *(const half8*)(xp + k + u * 32) : zero;
+    }
+#pragma unroll
+    for (int u = 0; u < GV_U; ++u) {
+      a0 = mfma16x16x32(fa[u], fx[u], a0);
+      a1 = mfma16x16x32(fb[u], fx[u], a1);
+    }
+  }
+  for (; k < K; k += 32) {
+    const half8 fa = *(const half8*)(wa + k), fb = *(const half8*)(wb + k);
+    const half8 fx = xrow ? *(const half8*)(xp + k) : zero;
+    a0 = mfma16x16x32(fa, fx, a0);
+    a1 = mfma16x16x32(fb, fx, a1);
+  }
+  // lane holds D[n = 4*grp + r][m = fr] of each 16x16 tile
+  if (!xrow) return;
+  half_t* cp = C + (size_t)fr * ldc;
+  const int na = n0 + 4 * grp, nb = n0 + 16 + 4 * grp;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    if (na + r < N) cp[na + r] = (half_t)a0[r];
+    if (nb + r < N) cp[nb + r] = (half_t)a1[r];
+  }
+}
 }  // namespace
 
 extern "C" int fls_rmsnorm(const void* x, const void* w, void* y, const int* row_idx, int rows, int H, int ldx,
@@ -288,6 +339,17 @@ extern "C" int fls_swiglu(const void* y, void* out, int M, int I, int ldy, int l
   const long long items = (long long)M * (I / 8);
   hipLaunchKernelGGL(swiglu_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, (hipStream_t)s,
                      (const half_t*)y, (half_t*)out, M, I, ldy, ldo);
+  FLS_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int fls_gemv_skinny(const void* x, const void* w, void* c, int M, int N, int K, int ldx, int ldw, int ldc,
+                               fls_stream_t s) {
+  if (M <= 0 || N <= 0) return 0;
+  if (M > 16 || K % 32 || ldx % 8 || ldw % 8) return -2;
+  const int waves = (N + 31) / 32;
+  hipLaunchKernelGGL(gemv_skinny_kernel, dim3((waves + 3) / 4), dim3(256), 0, (hipStream_t)s, (const half_t*)x,
+                     (const half_t*)w, (half_t*)c, M, N, K, ldx, ldw, ldc);
   FLS_CHECK_LAUNCH();
   return 0;
 }

@@ -64,6 +64,8 @@ def _load_kernels():
     _bind(lib, "fls_rope_inplace", c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
           c_void_p)
     _bind(lib, "fls_swiglu", c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p)
+    _bind(lib, "fls_gemv_skinny", c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
+          c_void_p)
     _bind(lib, "fls_fill_random", c_int, c_void_p, c_uint64, c_uint64, c_float, c_float, c_void_p)
     return lib
 

@@ -19,13 +19,14 @@ import os
 import pickle
 import socket
 import sys
+import tempfile
 import time
 from typing import List, Optional, Sequence
 
 import numpy as np
 import torch
 
-from .config import ModelConfig
+from .config import MAX_TOKEN_LEN, ModelConfig
 from .engine import ShardedRunner
 from .parallel.comm import Comm
 from .parallel.planner import make_plan
@@ -41,13 +42,15 @@ def batch_ranges(n: int, num_batch: int):
 
 
 def build_source(args, cfg: ModelConfig, comm: Comm, device: torch.device):
+    names = cfg.layer_names()
+    plan = make_plan(len(names), args.layer_num_per_shard, comm.world, comm.rank, args.data_parallel)
+    mine = [names[i] for i in sorted({i for sh in plan.my_shards for i in sh})]
+    if getattr(args, "synthetic", None):
+        return HostStore.synthetic(cfg, device, seed=0, pinned=device.type == "cuda", names=mine)
     src = FileLayerSource(cfg, args.model_path)
     if args.weight_cache == "disk":
         return src
-    names = cfg.layer_names()
-    plan = make_plan(len(names), args.layer_num_per_shard, comm.world, comm.rank, args.data_parallel)
-    mine = sorted({i for sh in plan.my_shards for i in sh})
-    return HostStore.from_source(src, pinned=device.type == "cuda", names=[names[i] for i in mine])
+    return HostStore.from_source(src, pinned=device.type == "cuda", names=mine)
 
 
 def build_runner(args, cfg: ModelConfig, device, comm: Comm, tok) -> ShardedRunner:
@@ -66,7 +69,20 @@ def build_runner(args, cfg: ModelConfig, device, comm: Comm, tok) -> ShardedRunn
                          resident=args.resident, comm=comm, data_parallel=args.data_parallel,
                          act_dtype=act, verbose=args.verbose,
                          resume_dir=getattr(args, "resume_dir", None),
-                         checkpoint_every=getattr(args, "checkpoint_every", 0))
+                         checkpoint_every=getattr(args, "checkpoint_every", 0),
+                         max_token_len=getattr(args, "max_token_len", None) or MAX_TOKEN_LEN)
+
+
+def load_model_meta(args):
+    """(config, tokenizer) from --model_path, or a preset + synthetic tokenizer for --synthetic."""
+    if getattr(args, "synthetic", None):
+        from .config import preset
+        from .utils.tokenizer import write_synthetic_tokenizer
+        cfg = preset(args.synthetic)
+        tok_dir = os.path.join(tempfile.gettempdir(), f"fls_synth_tok_{cfg.vocab_size}_{os.getpid()}")
+        write_synthetic_tokenizer(tok_dir, cfg.vocab_size)
+        return cfg, load_tokenizer(tok_dir)
+    return ModelConfig.from_pretrained(args.model_path), load_tokenizer(args.model_path)
 
 
 def run_all(args, runner: ShardedRunner, comm: Comm, prompts: Sequence) -> List[np.ndarray]:
@@ -131,8 +147,7 @@ def run_rank(args, comm: Comm) -> Optional[dict]:
         os.makedirs(args.disk_folder, exist_ok=True)
     with open(args.prompt_pickle, "rb") as f:
         original = pickle.load(f)      # the user's own prompt file (reference format)
-    cfg = ModelConfig.from_pretrained(args.model_path)
-    tok = load_tokenizer(args.model_path)
+    cfg, tok = load_model_meta(args)
     t0 = time.perf_counter()
     runner = build_runner(args, cfg, device, comm, tok)
     t_build = time.perf_counter() - t0

@@ -63,7 +63,8 @@ class ShardedRunner:
                  resident: bool = False, comm: Optional[Comm] = None, data_parallel: bool = False,
                  act_dtype: Optional[torch.dtype] = None, n_slots: int = 2,
                  mlp_chunk: int = 16384, prefetcher: Optional[ShardPrefetcher] = None,
-                 verbose: bool = False, resume_dir: Optional[str] = None, checkpoint_every: int = 0):
+                 verbose: bool = False, resume_dir: Optional[str] = None, checkpoint_every: int = 0,
+                 max_token_len: int = MAX_TOKEN_LEN):
         self.cfg = cfg
         self.src = source
         self.dev = torch.device(device)
@@ -78,6 +79,7 @@ class ShardedRunner:
         self.comm = comm or Comm(0, 1, self.dev)
         self.data_parallel = data_parallel
         self.verbose = verbose
+        self.max_token_len = max_token_len
         self.resume_dir = resume_dir
         self.checkpoint_every = checkpoint_every
         self.names = cfg.layer_names()
@@ -86,7 +88,7 @@ class ShardedRunner:
                                          data_parallel)
         self.act_dtype = act_dtype or (torch.float16 if self.cuda else torch.float32)
         self.ops = get_ops(self.dev)
-        cos, sin = rope_tables(cfg, max(cfg.max_position_embeddings, MAX_TOKEN_LEN),
+        cos, sin = rope_tables(cfg, max(cfg.max_position_embeddings, max_token_len),
                                torch.float16, self.dev)
         self.ctx = ExecContext(cfg, self.ops, self.dev, self.act_dtype, cos, sin, mlp_chunk)
         my = [s for s in self.plan.my_shards if len(s)]
@@ -110,7 +112,7 @@ class ShardedRunner:
     def tokenize(self, prompts) -> List[TokenizedPrompt]:
         if self.tok is None:
             raise RuntimeError("no tokenizer")
-        return tokenize_prompts(self.tok, prompts, MAX_TOKEN_LEN)
+        return tokenize_prompts(self.tok, prompts, self.max_token_len)
 
     def _owner(self, layer_idx: int) -> int:
         return self.plan.owner_of_layer(layer_idx)

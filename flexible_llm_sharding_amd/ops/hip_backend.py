@@ -107,7 +107,20 @@ class HipOps:
         _chk(rc, "fls_gemm")
         return out
 
+    def gemv_skinny(self, x, w):
+        """Weight-streaming GEMV for M <= 16 rows (skinny LM head)."""
+        _f16(x, "x")
+        _f16(w, "w")
+        M, K = x.shape
+        N = w.shape[0]
+        out = torch.empty(M, N, dtype=torch.float16, device=x.device)
+        _chk(self.k.fls_gemv_skinny(x.data_ptr(), w.data_ptr(), out.data_ptr(), M, N, K, x.stride(0), w.stride(0),
+                                    out.stride(0), _stream()), "fls_gemv_skinny")
+        return out
+
     def linear(self, x, w):
+        if x.shape[0] <= 16 and x.shape[1] % 32 == 0 and self.backend != "hipblaslt":
+            return self.gemv_skinny(x, w)
         return self._pick("linear", x, w, lambda: self.gemm(x, w), lambda: torch.matmul(x, w.t()),
                           lambda: self.gemm(x, w), lambda: torch.matmul(x, w.t()))
 

@@ -136,11 +136,14 @@ class _nullctx:
 
 
 def build_dp_sharded_runner(args, cfg, device, comm: Comm, tok, store: Optional[SlicedHostStore] = None):
+    from ..config import MAX_TOKEN_LEN
     from ..engine import ShardedRunner
     from ..runtime.weights import FileLayerSource
     from .planner import make_plan
     device = torch.device(device)
-    if store is None:
+    if store is None and getattr(args, "synthetic", None):
+        store = SlicedHostStore.synthetic(cfg, device, comm.rank, comm.world, pinned=device.type == "cuda")
+    elif store is None:
         store = SlicedHostStore.from_source(FileLayerSource(cfg, args.model_path), comm.rank, comm.world,
                                             pinned=device.type == "cuda")
     names = cfg.layer_names()
@@ -157,4 +160,5 @@ def build_dp_sharded_runner(args, cfg, device, comm: Comm, tok, store: Optional[
                          resident=getattr(args, "resident", False), comm=comm, data_parallel=True,
                          act_dtype=act, prefetcher=pf, verbose=getattr(args, "verbose", False),
                          resume_dir=getattr(args, "resume_dir", None),
-                         checkpoint_every=getattr(args, "checkpoint_every", 0))
+                         checkpoint_every=getattr(args, "checkpoint_every", 0),
+                         max_token_len=getattr(args, "max_token_len", None) or MAX_TOKEN_LEN)

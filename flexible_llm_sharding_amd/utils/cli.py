@@ -53,6 +53,11 @@ def build_parser() -> argparse.ArgumentParser:
                    help="activation dtype (default fp16 on GPU, fp32 on CPU)")
     p.add_argument("--verbose", type=str2bool, nargs="?", const=True, default=False)
     p.add_argument("--metrics_json", type=str, default=None, help="write run metrics here (rank 0)")
+    p.add_argument("--max_token_len", type=int, default=None,
+                   help="token cap per prefix / suffix (reference: 4096, utils.py:14); also sizes the RoPE tables")
+    p.add_argument("--synthetic", type=str, default=None, metavar="PRESET",
+                   help="random-init weights of a preset architecture (tiny|small|llama2-7b|llama2-13b|llama2-70b) "
+                        "generated in pinned host RAM, plus a synthetic tokenizer; --model_path is not read")
     p.add_argument("--resume_dir", type=str, default=None,
                    help="checkpoint inter-shard activations here and resume a crashed run from them "
                         "(single-GPU / data-parallel)")

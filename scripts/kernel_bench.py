@@ -72,6 +72,15 @@ def main():
         row.update({"hipblaslt_ms": tl * 1e3, "hipblaslt_tflops": fl / tl / 1e12})
         res.append(row)
         print(json.dumps(row), flush=True)
+    # skinny LM head (one prompt x 5 suffixes): weight-streaming GEMV vs hipBLASLt
+    xs = (torch.rand(5, H, device=dev) * 2 - 1).half()
+    wl = ((torch.rand(32000, H, device=dev) * 2 - 1) * 0.02).half()
+    tg = timeit(lambda: ops.gemv_skinny(xs, wl), a.iters)
+    tb = timeit(lambda: torch.matmul(xs, wl.t()), a.iters)
+    row = {"op": "lm_head_m5_gemv", "ours_ms": tg * 1e3, "ours_GBps": wl.numel() * 2 / tg / 1e9,
+           "hipblaslt_ms": tb * 1e3}
+    res.append(row)
+    print(json.dumps(row), flush=True)
     # attention: 12 prompts of prefix 1024 + 5 x 64 suffixes
     from flexible_llm_sharding_amd.runtime.batch import pack_prompts
     from flexible_llm_sharding_amd.utils.tokenizer import TokenizedPrompt

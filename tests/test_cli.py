@@ -101,3 +101,23 @@ def test_prepare_weights_synthetic_cli(tmp_path):
     assert r.returncode == 0, r.stderr
     files = sorted(os.listdir(tmp_path / "m"))
     assert "model.layers.0.safetensors" in files and "lm_head.safetensors" in files and "config.json" in files
+
+
+def test_main_synthetic_and_max_token_len(tmp_path):
+    """--synthetic PRESET (no checkpoint files) and --max_token_len truncation."""
+    from flexible_llm_sharding_amd.config import preset
+    from flexible_llm_sharding_amd.utils.synthetic import synthetic_prompts
+    cfg = preset("tiny")
+    prompts = synthetic_prompts(3, 40, 2, 6, cfg.vocab_size, seed=2)
+    pp = tmp_path / "prompts.pkl"
+    pickle.dump(prompts, open(pp, "wb"))
+    out = tmp_path / "scores.pkl"
+    mj = tmp_path / "m.json"
+    _run(["--synthetic", "tiny", "--prompt_pickle", str(pp), "--output_file", str(out),
+          "--max_token_len", "16", "--metrics_json", str(mj)], str(tmp_path))
+    scores = pickle.load(open(out, "rb"))
+    assert [s.shape for s in scores] == [(2, 1, cfg.vocab_size)] * 3
+    import json
+    m = json.load(open(mj))
+    # prefix truncated to 16 tokens (BOS included), each suffix to 16 (after BOS drop): 3 x (16 + 2 x 6)
+    assert m["stats"]["tokens"] == 3 * (16 + 2 * 6)

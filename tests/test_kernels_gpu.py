@@ -253,3 +253,13 @@ def test_gemm_variants_all_epilogues(ops, ref, var):
         torch.cuda.synchronize()
     finally:
         ops.k.fls_gemm_set_variant(9)
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 32000, 1024), (5, 1000, 8192), (16, 33, 96), (7, 100, 160)])
+def test_gemv_skinny(ops, M, N, K):
+    x = rnd(M, K, seed=41)
+    w = rnd(N, K, scale=0.05, seed=42)
+    y = ops.gemv_skinny(x, w)
+    torch.cuda.synchronize()
+    assert rel_err(y, x.float() @ w.float().t()) < 2e-3
+    assert ops.linear(x, w).shape == (M, N)          # linear() routes M <= 16 here
