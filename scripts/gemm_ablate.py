@@ -12,7 +12,11 @@ from flexible_llm_sharding_amd import _native  # noqa: E402
 
 NAMES = {0: "full", 1: "no_dma", 2: "no_lds_read", 3: "mfma_only", 4: "no_mfma", 5: "lds_read_only",
          6: "dma_only", 10: "v4_full", 11: "v4_no_dma", 14: "v4_no_mfma",
-         20: "v1_groupN_full", 26: "v1_groupN_dma_only"}
+         20: "v1_groupN_full", 26: "v1_groupN_dma_only",
+         40: "v10_full", 41: "v10_no_dma", 42: "v10_no_lds_read", 43: "v10_mfma_only",
+         45: "v10_no_dma_no_sync", 47: "v10_mfma_only_no_sync"}
+if os.environ.get("ABL_ONLY"):
+    NAMES = {k: v for k, v in NAMES.items() if k >= int(os.environ["ABL_ONLY"])}
 
 
 def main():
