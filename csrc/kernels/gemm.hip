@@ -1387,7 +1387,12 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_v9(const half_t* __restrict__ 
 // ph3 XA(t+3).  Requires an even number of K-tiles.
 
 // ABL (ablation, main loop only): bit0 = no LDS-DMA, bit1 = no fragment ds_reads, bit2 = no waits/barriers
-template <int EPI, int ABL = 0>
+// SCHED: placement of a phase's 8 ds_reads / 4 LDS-DMA ops among its 32 MFMAs
+//   0: reads after MFMAs 0,2,..,14; DMA after 17,20,23,26 (default)
+//   1: DMA first (after 0,2,4,6), reads after 8,10,..,22
+//   2: spread: reads after 0,4,..,28; DMA after 2,10,18,26
+//   3: alternate from the start: read/DMA after 0..11 (r r d r r d ...), rest bare
+template <int EPI, int ABL = 0, int SCHED = 0>
 __global__ __launch_bounds__(256, 1) void gemm_nt_v10(const half_t* __restrict__ A, const half_t* __restrict__ W,
                                                     half_t* __restrict__ C, int M, int N, int K, int lda, int ldw,
                                                     int ldc, Epi ep) {
@@ -1483,15 +1488,26 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_v10(const half_t* __restrict__
     _Pragma("unroll") for (int i_ = 0; i_ < 32; ++i_) {                                           \
       const int s_ = i_ >> 4, u_ = (xh) * 4 + ((i_ >> 2) & 3), t_ = (wh) * 4 + (i_ & 3);          \
       mfma_acc_inplace_ordered(acc[u_][t_], wf[t_][s_], xf[u_][s_]);                              \
-      if (!(ABL & 2) && i_ < 16 && (i_ & 1) == 0) {                                               \
-        const int f_ = (rh) * 4 + (i_ >> 2), k_ = (i_ >> 1) & 1;                                  \
+      constexpr int rsl_[4][32] = {                                                               \
+        {0,-1,1,-1,2,-1,3,-1,4,-1,5,-1,6,-1,7,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1},  \
+        {-1,-1,-1,-1,-1,-1,-1,-1,0,-1,1,-1,2,-1,3,-1,4,-1,5,-1,6,-1,7,-1,-1,-1,-1,-1,-1,-1,-1,-1},  \
+        {0,-1,-1,-1,1,-1,-1,-1,2,-1,-1,-1,3,-1,-1,-1,4,-1,-1,-1,5,-1,-1,-1,6,-1,-1,-1,7,-1,-1,-1},  \
+        {0,1,-1,2,3,-1,4,5,-1,6,7,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1}}; \
+      constexpr int dsl_[4][32] = {                                                               \
+        {-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,0,-1,-1,1,-1,-1,2,-1,-1,3,-1,-1,-1,-1,-1},\
+        {0,-1,1,-1,2,-1,3,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1},\
+        {-1,-1,0,-1,-1,-1,-1,-1,-1,-1,1,-1,-1,-1,-1,-1,-1,-1,2,-1,-1,-1,-1,-1,-1,-1,3,-1,-1,-1,-1,-1},\
+        {-1,-1,0,-1,-1,1,-1,-1,2,-1,-1,3,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1,-1}};\
+      const int rj_ = rsl_[SCHED][i_], dj_ = dsl_[SCHED][i_];                                     \
+      if (!(ABL & 2) && rj_ >= 0) {                                                               \
+        const int f_ = (rh) * 4 + (rj_ >> 1), k_ = rj_ & 1;                                       \
         if (RX)                                                                                   \
           xf[f_][k_] = *(const half8*)(smem + (rbuf) * v9::BUF + xrow + f_ * 2048 + (k_ ? c1 : c0)); \
         else                                                                                      \
           wf[f_][k_] = *(const half8*)(smem + (rbuf) * v9::BUF + wrow + f_ * 2048 + (k_ ? c1 : c0)); \
       }                                                                                           \
-      if (!(ABL & 1) && i_ >= 17 && i_ <= 26 && (i_ - 17) % 3 == 0) {                             \
-        const int p_ = (i_ - 17) / 3;                                                             \
+      if (!(ABL & 1) && dj_ >= 0) {                                                               \
+        const int p_ = dj_;                                                                       \
         if (DX)                                                                                   \
           glds16(Ab + (size_t)(dk0) * 2 + xo[(dhb) * 4 + p_],                                     \
                  smem + (dbuf) * v9::BUF + (prow[p_] + (dhb) * 64) * 128);                        \
@@ -1556,12 +1572,220 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_v10(const half_t* __restrict__
   }
 }
 
+// ------------------------------------------------------------------ v11
+// v10 with the LDS-DMA issued as `buffer_load_dwordx4 ... offen lds` from a
+// buffer resource: every piece of an operand uses the SAME per-lane VGPR
+// offset (row-in-piece x ld + swizzled chunk) and a wave-uniform SGPR offset
+// (piece row base x ld + k), so the DMA costs no per-piece vector address
+// registers or VALU; rows past M read as zero (buffer range check) instead of
+// being clamped.  Schedule identical to v10.
+
+// v9 with ONE barrier per two phases (64 MFMAs): the register read-ahead stays
+// one phase deep (registers are private, they need no barrier); only the
+// shared-LDS hazards are synchronised, at super-phase (SP) granularity:
+//   SP0 of tile t: DMA XA(t+2) + W-first(t+2)    SP1 of tile t: DMA W-second(t+2) + XB(t+2)
+// (tile t's data is read in SPs 2t-1 and 2t, so each region is refilled in the
+// SP after its last reads, and every half-tile is read 3 SPs after issue:
+// `vmcnt(16)` = 2 SPs x 2 half-tiles x 4 ops stay in flight at each barrier).
+// Original v9 notes follow.
+//
+// v6's geometry (4 waves = one per SIMD, 128x128 outputs per wave in 256
+// AGPR accumulators: 2/3 of the LDS fragment reads per FLOP of the 8-wave
+// kernels) with v8's read-ahead schedule, and the LDS reads and DMA
+// interleaved INTO the MFMA stream (one wave per SIMD: nothing else would
+// fill the matrix pipe while they issue).  Per phase (one 64x64 quadrant x
+// K=64 = 32 MFMAs):
+//   32 MFMA || {8 ds_read_b128 of a fragment half for a later phase, then one
+//   half-tile of LDS-DMA (4 per lane)}  ->  lgkmcnt(0), vmcnt(24)  ->  s_barrier
+// Quadrant order alternates with tile parity exactly as in v8.  Reads issued
+// in phase P complete before barrier P+1, so their region is refilled in
+// phase P+1; each half-tile is read 7 phases after it is issued (6 younger
+// half-tiles = 24 LDS-DMA ops stay in flight across every barrier).
+// Half-tile issue in tile t: ph0 W-first(t+2), ph1 W-second(t+2), ph2 XB(t+2),
+// ph3 XA(t+3).  Requires an even number of K-tiles.
+
+// ABL (ablation, main loop only): bit0 = no LDS-DMA, bit1 = no fragment ds_reads, bit2 = no waits/barriers
+template <int EPI, int ABL = 0>
+__global__ __launch_bounds__(256, 1) void gemm_nt_v11(const half_t* __restrict__ A, const half_t* __restrict__ W,
+                                                    half_t* __restrict__ C, int M, int N, int K, int lda, int ldw,
+                                                    int ldc, Epi ep) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  const int nwg = gridDim.x;
+  int bid = blockIdx.x;
+  {
+    const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7, loc = bid >> 3;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+  }
+  const int tiles_m = (M + BM - 1) / BM;
+  const int tiles_n = N / BN;
+  constexpr int GROUP_M = 8;
+  const int group = bid / (GROUP_M * tiles_n);
+  const int first_m = group * GROUP_M;
+  const int gsz = min(tiles_m - first_m, GROUP_M);
+  const int in_g = bid - group * GROUP_M * tiles_n;
+  const int tm = first_m + in_g % gsz;
+  const int tn = in_g / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // staging: a half-tile = 16 pieces of 8 rows x 128 B, rows {(j>>3)*128 + (j&7)*8} (+64 for the B half);
+  // wave w moves pieces 4w .. 4w+3
+  const int lr = lane >> 3;
+  const int lc = (lane & 7) ^ lr;
+  int prow[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int j = 4 * wave + i;
+    prow[i] = (j >> 3) * 128 + (j & 7) * 8;
+  }
+  // buffer resources: X = whole matrix (rows >= M fall outside num_records -> 0), W = this block's 256 rows
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, M * lda * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)(W + (size_t)n0 * ldw), (short)0,
+                                                                       BN * ldw * 2, 0x00020000);
+  const unsigned xv = (unsigned)(lr * lda + lc * 8) * 2u;      // per-lane, shared by every X piece
+  const unsigned wv = (unsigned)(lr * ldw + lc * 8) * 2u;      // per-lane, shared by every W piece
+  unsigned xs[4], ws[4];                                       // wave-uniform piece bases (bytes)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    xs[i] = (unsigned)((m0 + prow[i]) * lda) * 2u;
+    ws[i] = (unsigned)(prow[i] * ldw) * 2u;
+  }
+  const unsigned xhb = (unsigned)(64 * lda) * 2u, whb = (unsigned)(64 * ldw) * 2u;
+#define V11_BLD(rsrc, lds, voff, soff)                                                            \
+  __builtin_amdgcn_raw_ptr_buffer_load_lds((rsrc), (LDS_AS void*)(lds), 16, (voff), (soff), 0, 0)
+#define V11_X(buf, hb, k0)                                                                        \
+  _Pragma("unroll") for (int i_ = 0; i_ < 4; ++i_)                                                \
+    V11_BLD(xr, smem + (buf) * v9::BUF + (prow[i_] + (hb) * 64) * 128, xv,                        \
+            xs[i_] + (hb) * xhb + (unsigned)(k0) * 2u);
+#define V11_W(buf, hb, k0)                                                                        \
+  _Pragma("unroll") for (int i_ = 0; i_ < 4; ++i_)                                                \
+    V11_BLD(wr, smem + (buf) * v9::BUF + v9::WIMG + (prow[i_] + (hb) * 64) * 128, wv,             \
+            ws[i_] + (hb) * whb + (unsigned)(k0) * 2u);
+
+  const int wm = wave >> 1, wn = wave & 1;
+  const int fr = lane & 15, grp = lane >> 4;
+  const int sw = fr & 7;
+  const int c0 = ((0 + grp) ^ sw) << 4;
+  const int c1 = ((4 + grp) ^ sw) << 4;
+  const int xrow = (wm * 128 + fr) * 128;
+  const int wrow = v9::WIMG + (wn * 128 + fr) * 128;
+
+  floatx4 acc[8][8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc[u][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  half8 xf[8][2], wf[8][2];
+#define V11_FENCE_ACC()                                                                            \
+  _Pragma("unroll") for (int u_ = 0; u_ < 8; ++u_)                                                \
+  _Pragma("unroll") for (int t_ = 0; t_ < 8; ++t_) asm volatile("" : "+a"(acc[u_][t_]));
+  // zero-init (VALU AGPR writes) must not sit right before the first asm MFMA reading them
+  V11_FENCE_ACC();
+  asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+
+#define V11_RX(buf, h)                                                                             \
+  _Pragma("unroll") for (int u_ = (h) * 4; u_ < (h) * 4 + 4; ++u_) {                              \
+    xf[u_][0] = *(const half8*)(smem + (buf) * v9::BUF + xrow + u_ * 2048 + c0);                  \
+    xf[u_][1] = *(const half8*)(smem + (buf) * v9::BUF + xrow + u_ * 2048 + c1);                  \
+  }
+#define V11_RW(buf, h)                                                                             \
+  _Pragma("unroll") for (int t_ = (h) * 4; t_ < (h) * 4 + 4; ++t_) {                              \
+    wf[t_][0] = *(const half8*)(smem + (buf) * v9::BUF + wrow + t_ * 2048 + c0);                  \
+    wf[t_][1] = *(const half8*)(smem + (buf) * v9::BUF + wrow + t_ * 2048 + c1);                  \
+  }
+  // one phase: reads for a later phase, one half-tile of DMA, 32 MFMAs (interleaved), waits, barrier
+// one phase: 32 MFMAs (k-step outer, 4x4 tiles of the quadrant) with, in issue order,
+// one ds_read after each of the first 16 even-numbered MFMAs (the 8 reads of the half
+// needed later) and the half-tile's 4 LDS-DMA ops after MFMAs 17, 20, 23, 26;
+// then lgkmcnt(0) + counted vmcnt + barrier.  RX: 1 = read an X half, 0 = a W half.
+#define V11_PHASE(xh, wh, RX, rbuf, rh, DX, dbuf, dhb, dk0, SYNC)                                        \
+  {                                                                                               \
+    _Pragma("unroll") for (int i_ = 0; i_ < 32; ++i_) {                                           \
+      const int s_ = i_ >> 4, u_ = (xh) * 4 + ((i_ >> 2) & 3), t_ = (wh) * 4 + (i_ & 3);          \
+      mfma_acc_inplace_ordered(acc[u_][t_], wf[t_][s_], xf[u_][s_]);                              \
+      if (!(ABL & 2) && i_ < 16 && (i_ & 1) == 0) {                                               \
+        const int f_ = (rh) * 4 + (i_ >> 2), k_ = (i_ >> 1) & 1;                                  \
+        if (RX)                                                                                   \
+          xf[f_][k_] = *(const half8*)(smem + (rbuf) * v9::BUF + xrow + f_ * 2048 + (k_ ? c1 : c0)); \
+        else                                                                                      \
+          wf[f_][k_] = *(const half8*)(smem + (rbuf) * v9::BUF + wrow + f_ * 2048 + (k_ ? c1 : c0)); \
+      }                                                                                           \
+      if (!(ABL & 1) && i_ >= 17 && i_ <= 26 && (i_ - 17) % 3 == 0) {                             \
+        const int p_ = (i_ - 17) / 3;                                                             \
+        if (DX)                                                                                   \
+          V11_BLD(xr, smem + (dbuf) * v9::BUF + (prow[p_] + (dhb) * 64) * 128, xv,                \
+                  xs[p_] + (dhb) * xhb + (unsigned)(dk0) * 2u);                                   \
+        else                                                                                      \
+          V11_BLD(wr, smem + (dbuf) * v9::BUF + v9::WIMG + (prow[p_] + (dhb) * 64) * 128, wv,     \
+                  ws[p_] + (dhb) * whb + (unsigned)(dk0) * 2u);                                   \
+      }                                                                                           \
+    }                                                                                             \
+    if (SYNC && !(ABL & 4)) {                                                                     \
+      __builtin_amdgcn_s_waitcnt(0xC07F);                 /* lgkmcnt(0) */                        \
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");                                           \
+      __builtin_amdgcn_s_barrier();                                                               \
+    }                                                                                             \
+  }
+
+  const int nk = K / BK;                       // even (host-checked)
+  const int kc1 = min(1, nk - 1) * BK;
+  // prologue = virtual SPs -4..-1: [XA0 WA0] [WB0 XB0] [XA1 WB1] [WA1 XB1]
+  V11_X(0, 0, 0); V11_W(0, 0, 0); V11_W(0, 1, 0); V11_X(0, 1, 0);
+  V11_X(1, 0, kc1); V11_W(1, 1, kc1); V11_W(1, 0, kc1); V11_X(1, 1, kc1);
+  asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  V11_RX(0, 0); V11_RW(0, 0);                  // SP -1's reads: x0(0), w0(0)
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int kt = 0; kt < nk; kt += 2) {
+    const int ka = min(kt + 2, nk - 1) * BK;   // tile kt+2 -> buf 0
+    const int kb = min(kt + 3, nk - 1) * BK;   // tile kt+3 -> buf 1
+    // even tile kt (buf 0; W-first = WA, W-second = WB)
+    V11_PHASE(0, 0, 0, 0, 1, 1, 0, 0, ka, 0);  // read w1(kt)   ; DMA XA(kt+2)
+    V11_PHASE(0, 1, 1, 0, 1, 0, 0, 0, ka, 1);  // read x1(kt)   ; DMA WA(kt+2)   | sync
+    V11_PHASE(1, 1, 1, 1, 0, 0, 0, 1, ka, 0);  // read x0(kt+1) ; DMA WB(kt+2)
+    V11_PHASE(1, 0, 0, 1, 1, 1, 0, 1, ka, 1);  // read w1(kt+1) ; DMA XB(kt+2)   | sync
+    // odd tile kt+1 (buf 1; W-first = WB, W-second = WA)
+    V11_PHASE(0, 1, 0, 1, 0, 1, 1, 0, kb, 0);  // read w0(kt+1) ; DMA XA(kt+3)
+    V11_PHASE(0, 0, 1, 1, 1, 0, 1, 1, kb, 1);  // read x1(kt+1) ; DMA WB(kt+3)   | sync
+    V11_PHASE(1, 0, 1, 0, 0, 0, 1, 0, kb, 0);  // read x0(kt+2) ; DMA WA(kt+3)
+    V11_PHASE(1, 1, 0, 0, 0, 1, 1, 1, kb, 1);  // read w0(kt+2) ; DMA XB(kt+3)   | sync
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // the accumulators were written by inline-asm MFMAs the hazard recognizer cannot see:
+  // the nops give the last ones their passes, and the tied empty asms (ordered after the
+  // nops, being volatile too) make every later AGPR read depend on them
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  V11_FENCE_ACC();
+#undef V11_FENCE_ACC
+#undef V11_PHASE
+#undef V11_RW
+#undef V11_RX
+#undef V11_W
+#undef V11_X
+#undef V11_BLD
+
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int m = m0 + wm * 128 + u * 16 + fr;
+    if (m < M) {
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+        store_pair<EPI>(C, ldc, m, n0 + wn * 128 + p * 32, grp, acc[u][2 * p], acc[u][2 * p + 1], ep);
+    }
+  }
+}
+
 int g_variant = -1;   // -1: from env FLS_GEMM_VARIANT (default 3)
 
 int variant() {
   if (g_variant < 0) {
     const char* e = getenv("FLS_GEMM_VARIANT");
-    g_variant = e ? atoi(e) : 9;
+    g_variant = e ? atoi(e) : 10;
   }
   return g_variant;
 }
@@ -1573,11 +1797,19 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
   const bool fast = (N % BN == 0) && (K % BK == 0) && (lda % 8 == 0) && (ldw % 8 == 0) && M > 0;
   // v8/v9 need an even K-tile count (2-tile unrolled body), v9 32-bit X offsets; else v3
   const bool even_k = (K / BK) % 2 == 0;
-  if (((var == 9 || var == 10) && !(even_k && (size_t)M * lda * 2 < (1ull << 32))) || (var == 8 && !even_k))
+  if (((var == 9 || var == 10 || var == 11) && !(even_k && (size_t)M * lda * 2 < (1ull << 32))) || (var == 8 && !even_k))
     var = 3;
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
   const bool fast4 = fast && (K % (2 * v4::BK4) == 0);
-  if (var == 10 && fast) {
+  if (var == 11 && fast) {
+    static bool attr11 = false;
+    if (!attr11) {
+      (void)hipFuncSetAttribute((const void*)gemm_nt_v11<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                2 * v9::BUF);
+      attr11 = true;
+    }
+    hipLaunchKernelGGL(gemm_nt_v11<EPI>, dim3(tiles), dim3(256), 2 * v9::BUF, s, A, W, C, M, N, K, lda, ldw, ldc, ep);
+  } else if (var == 10 && fast) {
     static bool attr10 = false;
     if (!attr10) {
       (void)hipFuncSetAttribute((const void*)gemm_nt_v10<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1701,6 +1933,22 @@ extern "C" int fls_gemm_ablate(int abl, const void* A, const void* W, void* C, i
     break;
     FLS_ABL10_CASE(0) FLS_ABL10_CASE(1) FLS_ABL10_CASE(2) FLS_ABL10_CASE(3) FLS_ABL10_CASE(5) FLS_ABL10_CASE(7)
 #undef FLS_ABL10_CASE
+#define FLS_SCHED10_CASE(X)                                                                                  \
+  case 60 + X:                                                                                               \
+    if ((K / BK) % 2) return -2;                                                                             \
+    (void)hipFuncSetAttribute((const void*)gemm_nt_v10<0, 0, X>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                              2 * v9::BUF);                                                                  \
+    hipLaunchKernelGGL((gemm_nt_v10<0, 0, X>), dim3(tiles), dim3(256), 2 * v9::BUF, (hipStream_t)s, a, w, c, M, N, \
+                       K, K, K, N, ep);                                                                      \
+    break;
+    FLS_SCHED10_CASE(0) FLS_SCHED10_CASE(1) FLS_SCHED10_CASE(2) FLS_SCHED10_CASE(3)
+#undef FLS_SCHED10_CASE
+    case 50:
+      if ((K / BK) % 2) return -2;
+      (void)hipFuncSetAttribute((const void*)gemm_nt_v11<0, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * v9::BUF);
+      hipLaunchKernelGGL((gemm_nt_v11<0, 0>), dim3(tiles), dim3(256), 2 * v9::BUF, (hipStream_t)s, a, w, c, M, N, K,
+                         K, K, N, ep);
+      break;
     default: return -3;
   }
 #undef FLS_ABL4_CASE
