@@ -153,7 +153,8 @@ def main(argv=None):
                    "layer_num_per_shard": a.lnps, "storage_location": a.storage,
                    "parallelism": (f"pp{world}-roundrobin" if mode == "mp" else
                                    (f"dp{world}-allgather-weights" if dp else "single")),
-                   "resident": a.resident, "token_budget": a.token_budget},
+                   "resident": a.resident, "token_budget": a.token_budget,
+                   "gemm_backend": os.environ.get("FLS_GEMM_BACKEND", "hip") if dev.type == "cuda" else "torch"},
     }
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -6,11 +6,14 @@ allocated through PyTorch's caching allocator.  There is deliberately no
 fallback: a missing library raises (see ``_native.kernels``).
 
 Projection GEMMs: ``FLS_GEMM_BACKEND`` selects
-  * ``hip``       — our fused MFMA kernels (RoPE / SwiGLU / residual epilogues in registers);
+  * ``hip``       — (default) our fused MFMA kernels (RoPE / SwiGLU / residual epilogues in
+                    registers; ``gemm_nt_v10``, see profiles/r1_gemm_study);
   * ``hipblaslt`` — the plain GEMM on hipBLASLt (residual via beta=1) followed by our
                     stand-alone RoPE / SwiGLU epilogue kernels;
-  * ``auto``      — (default) per (op, N, K, M-bucket) the faster of the two, timed once on
-                    first use (scratch outputs, so in-place ops are not applied twice).
+  * ``auto``      — per (op, N, K, M-bucket) the faster of the two, timed once on first use
+                    (scratch outputs, so in-place ops are not applied twice).
+On the 70B bench ``auto`` is ~1.4% faster end to end but needs the unfused [M, 2I] SwiGLU
+intermediate (peak HBM 6.8 GB vs 4.9 GB), so the hand-written path is the default.
 Both paths are numerically checked against each other in tests/test_kernels_gpu.py.
 Measured trade-off on 70B shapes: profiles/r1_gemm_ablation/README.md.
 """
@@ -48,7 +51,7 @@ class HipOps:
 
     def __init__(self):
         self.k = _native.kernels()
-        self.backend = os.environ.get("FLS_GEMM_BACKEND", "auto")
+        self.backend = os.environ.get("FLS_GEMM_BACKEND", "hip")
         if self.backend not in ("auto", "hip", "hipblaslt"):
             raise ValueError(f"FLS_GEMM_BACKEND={self.backend!r}")
         self.choice = {}          # (op, N, K, M-bucket) -> "hip" | "hipblaslt"

@@ -67,6 +67,27 @@ def child():
         torch.cuda.synchronize()
         res.setdefault("gemm_with_copy_ms", []).append(e0.elapsed_time(e1) / gemm_iters)
         res.setdefault("copy_with_gemm_ms", []).append(c0.elapsed_time(c1))
+    # bandwidth-bound kernel next to the streams: rmsnorm over [16128, 8192]
+    xr = torch.randn(16128, 8192, device=dev).half()
+    wn = torch.randn(8192, device=dev).half()
+    hd = alloc_host(nb)
+
+    def norms():
+        for _ in range(20):
+            ops.rmsnorm(xr, wn, 1e-5)
+
+    norms(); torch.cuda.synchronize()
+    for rep in range(3):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(); norms(); e1.record(); torch.cuda.synchronize()
+        res.setdefault("rmsnorm_alone_ms", []).append(e0.elapsed_time(e1) / 20)
+        copy()
+        e0.record(); norms(); e1.record(); torch.cuda.synchronize()
+        res.setdefault("rmsnorm_with_h2d_ms", []).append(e0.elapsed_time(e1) / 20)
+        with torch.cuda.stream(side):
+            hd.copy_(d, non_blocking=True)
+        e0.record(); norms(); e1.record(); torch.cuda.synchronize()
+        res.setdefault("rmsnorm_with_d2h_ms", []).append(e0.elapsed_time(e1) / 20)
     out = {k: round(min(v), 3) for k, v in res.items()}
     out["copy_GBps_alone"] = round(nb / out["copy_alone_ms"] / 1e6, 1)
     print("RESULT " + json.dumps(out), flush=True)
