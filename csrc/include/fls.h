@@ -47,7 +47,7 @@ enum { FLS_EPI_NONE = 0, FLS_EPI_RESID = 1, FLS_EPI_SWIGLU = 2, FLS_EPI_ROPE = 3
 //           head_dim) with pos[m] and fp32 tables cos/sin [maxpos, head_dim/2]
 int fls_gemm(const void* A, const void* W, void* C, const void* R, int M, int N, int K,
              int lda, int ldw, int ldc, int ldr, int epi, const int* pos, const float* cos_t,
-             const float* sin_t, int rope_cols, int head_dim, fls_stream_t s);
+             const float* sin_t, int rope_cols, int head_dim, const void* bias, fls_stream_t s);
 // shared-prefix / varlen flash attention over packed work items (int32 x8)
 int fls_gemm_set_variant(int v);
 int fls_gemm_ablate(int abl, const void* A, const void* W, void* C, int M, int N, int K, fls_stream_t s);

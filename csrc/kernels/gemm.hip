@@ -44,6 +44,7 @@ struct Epi {
   const float* sin_t;
   int rope_cols;
   int head_dim;
+  const half_t* bias;   // optional per-output-column bias (Qwen2 q/k/v, Llama attention_bias), added first
 };
 
 // Store one pair of 16-column subtiles (cols n_first + 4*grp + r and +16)
@@ -62,6 +63,12 @@ __device__ __forceinline__ void store_pair(half_t* __restrict__ C, int ldc, int 
     return;
   } else {
     floatx4 a = acc_a, b = acc_b;
+    if (ep.bias) {
+      const half4 ba = *(const half4*)(ep.bias + c0);
+      const half4 bb = *(const half4*)(ep.bias + c0 + 16);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { a[r] += (float)ba[r]; b[r] += (float)bb[r]; }
+    }
     if constexpr (EPI == FLS_EPI_ROPE) {
       if (n_first < ep.rope_cols) {
         const int hd = ep.head_dim, half_hd = hd >> 1;
@@ -73,7 +80,7 @@ __device__ __forceinline__ void store_pair(half_t* __restrict__ C, int ldc, int 
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float cs = cr[r], sn = sr[r];
-          const float x1 = acc_a[r], x2 = acc_b[r];
+          const float x1 = a[r], x2 = b[r];
           a[r] = x1 * cs - x2 * sn;
           b[r] = x2 * cs + x1 * sn;
         }
@@ -279,6 +286,7 @@ __global__ __launch_bounds__(256) void gemm_nt_generic(const half_t* __restrict_
             const int n = nf + h * 16 + 4 * grp + r;
             if (n < N) {
               float v = h ? acc[u][2 * p + 1][r] : acc[u][2 * p][r];
+              if (ep.bias) v += (float)ep.bias[n];
               if constexpr (EPI == FLS_EPI_RESID) v += (float)ep.R[(size_t)m * ep.ldr + n];
               C[(size_t)m * ldc + n] = (half_t)v;
             }
@@ -1883,13 +1891,13 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
 
 }  // namespace
 
-extern "C" int fls_kernels_version(void) { return 2; }
+extern "C" int fls_kernels_version(void) { return 3; }
 
 // microbenchmark-only entry: v1 main loop with parts removed (results are garbage)
 extern "C" int fls_gemm_ablate(int abl, const void* A, const void* W, void* C, int M, int N, int K,
                                fls_stream_t s) {
   if (N % BN || K % BK) return -2;
-  Epi ep{nullptr, 0, nullptr, nullptr, nullptr, 0, 0};
+  Epi ep{nullptr, 0, nullptr, nullptr, nullptr, 0, 0, nullptr};
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
   auto a = (const half_t*)A;
   auto w = (const half_t*)W;
@@ -1966,11 +1974,12 @@ extern "C" int fls_gemm_set_variant(int v) {
 
 extern "C" int fls_gemm(const void* A, const void* W, void* C, const void* R, int M, int N, int K, int lda, int ldw,
                         int ldc, int ldr, int epi, const int* pos, const float* cos_t, const float* sin_t,
-                        int rope_cols, int head_dim, fls_stream_t s) {
+                        int rope_cols, int head_dim, const void* bias, fls_stream_t s) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
+  if (bias && epi == FLS_EPI_SWIGLU) return -4;
   if ((epi == FLS_EPI_SWIGLU || epi == FLS_EPI_ROPE) && (N % 32)) return -2;
   if (epi == FLS_EPI_ROPE && (head_dim % 32 || rope_cols % 32)) return -3;
-  Epi ep{(const half_t*)R, ldr, pos, cos_t, sin_t, rope_cols, head_dim};
+  Epi ep{(const half_t*)R, ldr, pos, cos_t, sin_t, rope_cols, head_dim, (const half_t*)bias};
   auto a = (const half_t*)A;
   auto w = (const half_t*)W;
   auto c = (half_t*)C;

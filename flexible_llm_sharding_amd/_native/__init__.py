@@ -48,11 +48,17 @@ def _load_runtime():
     return lib
 
 
+KERNELS_ABI = 3   # bumped whenever a C signature in csrc/include/fls.h changes
+
+
 def _load_kernels():
     lib = ctypes.CDLL(_KERNELS)
     _bind(lib, "fls_kernels_version", c_int)
+    if lib.fls_kernels_version() != KERNELS_ABI:
+        raise RuntimeError(f"{_KERNELS} is a stale build (ABI {lib.fls_kernels_version()} != {KERNELS_ABI}); "
+                           "rebuild with python -m flexible_llm_sharding_amd._native.build")
     _bind(lib, "fls_gemm", c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
-          c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p)
+          c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p)
     _bind(lib, "fls_gemm_set_variant", c_int, c_int)
     _bind(lib, "fls_gemm_ablate", c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p)
     _bind(lib, "fls_attention", c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,

@@ -28,6 +28,9 @@ class ModelConfig:
     rope_theta: float = 10000.0
     max_position_embeddings: int = 4096
     tie_word_embeddings: bool = False
+    attention_bias: bool = False        # q/k/v projection biases (Qwen2; Llama attention_bias)
+    o_proj_bias: bool = False           # o_proj bias (Llama attention_bias=True)
+    sliding_window: Optional[int] = None  # Mistral; must cover the token cap (checked by the runner)
     bos_token_id: int = 1
     eos_token_id: int = 2
     torch_dtype: str = "float16"
@@ -64,7 +67,8 @@ class ModelConfig:
 
     def decoder_layer_params(self) -> int:
         h, i = self.hidden_size, self.intermediate_size
-        return h * self.qkv_size + h * h + 3 * h * i + 2 * h
+        n = h * self.qkv_size + h * h + 3 * h * i + 2 * h
+        return n + (self.qkv_size if self.attention_bias else 0) + (h if self.o_proj_bias else 0)
 
     def total_params(self) -> int:
         emb = self.vocab_size * self.hidden_size
@@ -91,6 +95,24 @@ class ModelConfig:
         rs = d.get("rope_scaling")
         if rs:
             raise NotImplementedError(f"rope_scaling={rs} is not supported (Llama-2 has none)")
+        mt = d.get("model_type", "llama")
+        if mt not in SUPPORTED_MODEL_TYPES:
+            raise NotImplementedError(f"model_type={mt!r}: supported are {sorted(SUPPORTED_MODEL_TYPES)}")
+        if d.get("mlp_bias"):
+            raise NotImplementedError("mlp_bias=True is not supported")
+        hdim = d.get("head_dim")
+        if hdim is not None and hdim != d.get("hidden_size", cls.hidden_size) // d.get(
+                "num_attention_heads", cls.num_attention_heads):
+            raise NotImplementedError(f"head_dim={hdim} != hidden_size / num_attention_heads")
+        if d.get("hidden_act", "silu") != "silu":
+            raise NotImplementedError(f"hidden_act={d.get('hidden_act')!r} (SwiGLU/silu only)")
+        if mt == "qwen2":
+            # HF Qwen2Attention: q/k/v Linear with bias, o_proj without
+            kw["attention_bias"], kw["o_proj_bias"] = True, False
+        elif d.get("attention_bias"):
+            kw["attention_bias"], kw["o_proj_bias"] = True, True
+        if not d.get("use_sliding_window", mt == "mistral"):
+            kw.pop("sliding_window", None)
         if isinstance(kw.get("eos_token_id"), list):
             kw["eos_token_id"] = kw["eos_token_id"][0]
         cfg = cls(**kw)
@@ -114,6 +136,11 @@ class ModelConfig:
             json.dump(d, f, indent=2)
 
 
+# Llama-structured causal LMs (model.embed_tokens / model.layers.N / model.norm / lm_head with
+# q/k/v/o + gate/up/down + two RMSNorms per layer) -- what the reference's AutoModelForCausalLM
+# path (utils.py:101-115) runs in practice.
+SUPPORTED_MODEL_TYPES = {"llama", "mistral", "qwen2"}
+
 # Standard HF configs (computed sizes in SURVEY.md §2.3).
 PRESETS = {
     "llama2-7b": dict(hidden_size=4096, intermediate_size=11008, num_attention_heads=32,
@@ -122,10 +149,21 @@ PRESETS = {
                        num_key_value_heads=40, num_hidden_layers=40),
     "llama2-70b": dict(hidden_size=8192, intermediate_size=28672, num_attention_heads=64,
                        num_key_value_heads=8, num_hidden_layers=80),
+    "mistral-7b": dict(hidden_size=4096, intermediate_size=14336, num_attention_heads=32,
+                       num_key_value_heads=8, num_hidden_layers=32, rope_theta=1e6,
+                       model_type="mistral", architectures=["MistralForCausalLM"]),
+    "qwen2-7b": dict(hidden_size=3584, intermediate_size=18944, num_attention_heads=28,
+                     num_key_value_heads=4, num_hidden_layers=28, vocab_size=152064, rope_theta=1e6,
+                     rms_norm_eps=1e-6, attention_bias=True, model_type="qwen2",
+                     architectures=["Qwen2ForCausalLM"]),
     # tiny configs for tests (GQA 2:1, head_dim 64)
     "tiny": dict(hidden_size=256, intermediate_size=512, num_attention_heads=4,
                  num_key_value_heads=2, num_hidden_layers=2, vocab_size=512,
                  max_position_embeddings=4096),
+    "tiny-qwen2": dict(hidden_size=256, intermediate_size=512, num_attention_heads=4,
+                       num_key_value_heads=2, num_hidden_layers=2, vocab_size=512, rope_theta=1e6,
+                       rms_norm_eps=1e-6, attention_bias=True, model_type="qwen2",
+                       architectures=["Qwen2ForCausalLM"]),
     "small": dict(hidden_size=1024, intermediate_size=2816, num_attention_heads=8,
                   num_key_value_heads=2, num_hidden_layers=4, vocab_size=32000),
 }

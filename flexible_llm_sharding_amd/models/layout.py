@@ -14,6 +14,8 @@ Decoder layer packing (fp16, every tensor 256-byte aligned)::
     wo    [H, Hq]          o_proj
     wgu   [2I, H]          gate/up interleaved in blocks of 16 rows
     wdown [H, I]           down_proj
+    bqkv  [Hq+2Hkv]        q|k|v biases, permuted like wqkv rows (Qwen2 / attention_bias only)
+    bo    [H]              o_proj bias (Llama attention_bias only)
 
 *RoPE pair permutation* — HF Llama rotates (d, d + hd/2) pairs
 (``rotate_half``).  Per head we reorder rows as ``[0:16], [hd/2:hd/2+16],
@@ -104,6 +106,10 @@ def layer_layout(cfg: ModelConfig, kind: str, elem_size: int = 2) -> LayerLayout
     elif kind == "decoder":
         specs = [("ln1", (H,)), ("ln2", (H,)), ("wqkv", (cfg.qkv_size, H)),
                  ("wo", (H, cfg.q_size)), ("wgu", (2 * I, H)), ("wdown", (H, I))]
+        if cfg.attention_bias:
+            specs.append(("bqkv", (cfg.qkv_size,)))
+        if cfg.o_proj_bias:
+            specs.append(("bo", (H,)))
     else:
         raise ValueError(kind)
     slots, off = [], 0
@@ -182,11 +188,16 @@ def hf_param_names(cfg: ModelConfig, layer_name: str) -> List[str]:
     if kind == "head":
         return ["lm_head.weight"]
     p = layer_name
-    return [f"{p}.self_attn.q_proj.weight", f"{p}.self_attn.k_proj.weight",
-            f"{p}.self_attn.v_proj.weight", f"{p}.self_attn.o_proj.weight",
-            f"{p}.mlp.gate_proj.weight", f"{p}.mlp.up_proj.weight",
-            f"{p}.mlp.down_proj.weight", f"{p}.input_layernorm.weight",
-            f"{p}.post_attention_layernorm.weight"]
+    names = [f"{p}.self_attn.q_proj.weight", f"{p}.self_attn.k_proj.weight",
+             f"{p}.self_attn.v_proj.weight", f"{p}.self_attn.o_proj.weight",
+             f"{p}.mlp.gate_proj.weight", f"{p}.mlp.up_proj.weight",
+             f"{p}.mlp.down_proj.weight", f"{p}.input_layernorm.weight",
+             f"{p}.post_attention_layernorm.weight"]
+    if cfg.attention_bias:
+        names += [f"{p}.self_attn.{n}_proj.bias" for n in ("q", "k", "v")]
+    if cfg.o_proj_bias:
+        names.append(f"{p}.self_attn.o_proj.bias")
+    return names
 
 
 def pack_layer(cfg: ModelConfig, layer_name: str, sd: Dict[str, torch.Tensor],
@@ -234,6 +245,12 @@ def pack_layer(cfg: ModelConfig, layer_name: str, sd: Dict[str, torch.Tensor],
         views["wdown"].copy_(get(f"{p}.mlp.down_proj.weight"))
         views["ln1"].copy_(get(f"{p}.input_layernorm.weight"))
         views["ln2"].copy_(get(f"{p}.post_attention_layernorm.weight"))
+        if cfg.attention_bias:
+            bq = permute_heads_rows(get(f"{p}.self_attn.q_proj.bias")[:, None], cfg.num_attention_heads, hd)
+            bk = permute_heads_rows(get(f"{p}.self_attn.k_proj.bias")[:, None], cfg.num_key_value_heads, hd)
+            views["bqkv"].copy_(torch.cat([bq[:, 0], bk[:, 0], get(f"{p}.self_attn.v_proj.bias")], 0))
+        if cfg.o_proj_bias:
+            views["bo"].copy_(get(f"{p}.self_attn.o_proj.bias"))
     return out
 
 
@@ -254,7 +271,17 @@ def unpack_layer(cfg: ModelConfig, layer_name: str, buf: torch.Tensor,
     qs, ks = cfg.q_size, cfg.kv_size
     wqkv = v["wqkv"]
     g, u = deinterleave_gate_up(v["wgu"])
+    out = {}
+    if cfg.attention_bias:
+        b = v["bqkv"][:, None]
+        out[f"{p}.self_attn.q_proj.bias"] = unpermute_heads_rows(b[:qs], cfg.num_attention_heads, hd)[:, 0].clone()
+        out[f"{p}.self_attn.k_proj.bias"] = unpermute_heads_rows(b[qs:qs + ks], cfg.num_key_value_heads,
+                                                                  hd)[:, 0].clone()
+        out[f"{p}.self_attn.v_proj.bias"] = v["bqkv"][qs + ks:].clone()
+    if cfg.o_proj_bias:
+        out[f"{p}.self_attn.o_proj.bias"] = v["bo"].clone()
     return {
+        **out,
         f"{p}.self_attn.q_proj.weight": unpermute_heads_rows(wqkv[:qs], cfg.num_attention_heads, hd).clone(),
         f"{p}.self_attn.k_proj.weight": unpermute_heads_rows(wqkv[qs:qs + ks], cfg.num_key_value_heads, hd).clone(),
         f"{p}.self_attn.v_proj.weight": wqkv[qs + ks:].clone(),

@@ -65,12 +65,12 @@ def run_decoder(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, b
     eps = cfg.rms_norm_eps
     h = ops.rmsnorm(x, W["ln1"], eps)
     qkv = ops.qkv_rope(h, W["wqkv"], meta["positions"], ctx.cos, ctx.sin,
-                       cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim)
+                       cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim, bias=W.get("bqkv"))
     del h
     attn_arg = meta["work"] if getattr(ops, "uses_work_items", False) else batch.segments
     a = ops.attention(qkv, attn_arg, cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim)
     del qkv
-    x = ops.linear_residual(a, W["wo"], x)
+    x = ops.linear_residual(a, W["wo"], x, bias=W.get("bo"))
     del a
     T = x.shape[0]
     step = max(1, ctx.mlp_chunk)

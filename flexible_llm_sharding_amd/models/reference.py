@@ -38,10 +38,11 @@ def _block(x, sd, p, cfg, pos, cos, sin, mask, past_kv=None):
     B, T, H = x.shape
     nh, nkv, hd = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
     g = lambda n: sd[f"{p}.{n}"].float()
+    b = lambda n: sd[f"{p}.{n}"].float() if f"{p}.{n}" in sd else 0.0    # Qwen2 / attention_bias
     h = _rms(x, g("input_layernorm.weight"), cfg.rms_norm_eps)
-    q = (h @ g("self_attn.q_proj.weight").t()).view(B, T, nh, hd).transpose(1, 2)
-    k = (h @ g("self_attn.k_proj.weight").t()).view(B, T, nkv, hd).transpose(1, 2)
-    v = (h @ g("self_attn.v_proj.weight").t()).view(B, T, nkv, hd).transpose(1, 2)
+    q = (h @ g("self_attn.q_proj.weight").t() + b("self_attn.q_proj.bias")).view(B, T, nh, hd).transpose(1, 2)
+    k = (h @ g("self_attn.k_proj.weight").t() + b("self_attn.k_proj.bias")).view(B, T, nkv, hd).transpose(1, 2)
+    v = (h @ g("self_attn.v_proj.weight").t() + b("self_attn.v_proj.bias")).view(B, T, nkv, hd).transpose(1, 2)
     q, k = _rope(q, pos, cos, sin), _rope(k, pos, cos, sin)
     if past_kv is not None:
         k = torch.cat([past_kv[0], k], 2)
@@ -55,7 +56,7 @@ def _block(x, sd, p, cfg, pos, cos, sin, mask, past_kv=None):
         s = s + mask
     a = torch.softmax(s, -1) @ vv
     a = a.transpose(1, 2).reshape(B, T, nh * hd)
-    x = x + a @ g("self_attn.o_proj.weight").t()
+    x = x + a @ g("self_attn.o_proj.weight").t() + b("self_attn.o_proj.bias")
     h = _rms(x, g("post_attention_layernorm.weight"), cfg.rms_norm_eps)
     m = F.silu(h @ g("mlp.gate_proj.weight").t()) * (h @ g("mlp.up_proj.weight").t())
     x = x + m @ g("mlp.down_proj.weight").t()

@@ -90,7 +90,7 @@ class HipOps:
     # ---------------------------------------------------------------- GEMM
     def gemm(self, x: torch.Tensor, w: torch.Tensor, epi: int = EPI_NONE, out: torch.Tensor = None,
              resid: torch.Tensor = None, positions=None, cos=None, sin=None, rope_cols: int = 0,
-             head_dim: int = 0) -> torch.Tensor:
+             head_dim: int = 0, bias: torch.Tensor = None) -> torch.Tensor:
         _f16(x, "x")
         _f16(w, "w")
         M, K = x.shape
@@ -101,12 +101,16 @@ class HipOps:
         if out is None:
             out = torch.empty(M, ncols, dtype=torch.float16, device=x.device)
         R = resid if resid is not None else out
+        if bias is not None:
+            _f16(bias, "bias")
+            if bias.numel() != N or not bias.is_contiguous():
+                raise ValueError(f"bias must be a contiguous [{N}] vector")
         rc = self.k.fls_gemm(x.data_ptr(), w.data_ptr(), out.data_ptr(), R.data_ptr(), M, N, K,
                              x.stride(0), w.stride(0), out.stride(0), R.stride(0), epi,
                              positions.data_ptr() if positions is not None else None,
                              cos.data_ptr() if cos is not None else None,
                              sin.data_ptr() if sin is not None else None,
-                             rope_cols, head_dim, _stream())
+                             rope_cols, head_dim, bias.data_ptr() if bias is not None else None, _stream())
         _chk(rc, "fls_gemm")
         return out
 
@@ -127,13 +131,15 @@ class HipOps:
         return self._pick("linear", x, w, lambda: self.gemm(x, w), lambda: torch.matmul(x, w.t()),
                           lambda: self.gemm(x, w), lambda: torch.matmul(x, w.t()))
 
-    def linear_residual(self, x, w, resid):
+    def linear_residual(self, x, w, resid, bias=None):
         _f16(resid, "resid")
 
         def hip():
-            return self.gemm(x, w, EPI_RESID, out=resid, resid=resid)
+            return self.gemm(x, w, EPI_RESID, out=resid, resid=resid, bias=bias)
 
         def blt():
+            if bias is not None:
+                resid.add_(bias)
             return resid.addmm_(x, w.t())
 
         scratch = [None]
@@ -141,7 +147,7 @@ class HipOps:
         def s_hip():
             if scratch[0] is None:
                 scratch[0] = torch.empty_like(resid)
-            return self.gemm(x, w, EPI_RESID, out=scratch[0], resid=resid)
+            return self.gemm(x, w, EPI_RESID, out=scratch[0], resid=resid, bias=bias)
 
         def s_blt():
             if scratch[0] is None:
@@ -163,17 +169,17 @@ class HipOps:
 
         return self._pick("swiglu", x, wgu, hip, blt, hip, blt)
 
-    def qkv_rope(self, x, wqkv, positions, cos, sin, n_q_heads, n_kv_heads, head_dim):
+    def qkv_rope(self, x, wqkv, positions, cos, sin, n_q_heads, n_kv_heads, head_dim, bias=None):
         if positions.dtype != torch.int32:
             raise TypeError("positions must be int32")
         rope_cols = (n_q_heads + n_kv_heads) * head_dim
 
         def hip():
             return self.gemm(x, wqkv, EPI_ROPE, positions=positions, cos=cos, sin=sin,
-                             rope_cols=rope_cols, head_dim=head_dim)
+                             rope_cols=rope_cols, head_dim=head_dim, bias=bias)
 
         def blt():
-            y = torch.matmul(x, wqkv.t())
+            y = torch.matmul(x, wqkv.t()) if bias is None else torch.addmm(bias, x, wqkv.t())
             _chk(self.k.fls_rope_inplace(y.data_ptr(), positions.data_ptr(), cos.data_ptr(), sin.data_ptr(),
                                          y.shape[0], y.stride(0), rope_cols, head_dim, _stream()),
                  "fls_rope_inplace")

@@ -39,8 +39,11 @@ class TorchOps:
     def linear(self, x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
         return (self._c(x) @ self._c(w).t()).to(x.dtype)
 
-    def linear_residual(self, x: torch.Tensor, w: torch.Tensor, resid: torch.Tensor) -> torch.Tensor:
+    def linear_residual(self, x: torch.Tensor, w: torch.Tensor, resid: torch.Tensor,
+                        bias: torch.Tensor = None) -> torch.Tensor:
         y = self._c(x) @ self._c(w).t()
+        if bias is not None:
+            y = y + self._c(bias)
         return (self._c(resid) + y).to(resid.dtype)
 
     def swiglu_up(self, x: torch.Tensor, wgu: torch.Tensor) -> torch.Tensor:
@@ -52,8 +55,10 @@ class TorchOps:
 
     def qkv_rope(self, x: torch.Tensor, wqkv: torch.Tensor, positions: torch.Tensor,
                  cos: torch.Tensor, sin: torch.Tensor, n_q_heads: int, n_kv_heads: int,
-                 head_dim: int) -> torch.Tensor:
+                 head_dim: int, bias: torch.Tensor = None) -> torch.Tensor:
         y = self._c(x) @ self._c(wqkv).t()
+        if bias is not None:
+            y = y + self._c(bias)
         qk_cols = (n_q_heads + n_kv_heads) * head_dim
         T = y.shape[0]
         qk = y[:, :qk_cols].reshape(T, n_q_heads + n_kv_heads, head_dim // (2 * PAIR_BLOCK), 2, PAIR_BLOCK)
@@ -131,4 +136,6 @@ def fill_params(slot_name: str, std: float):
         return 1.0, 0.1
     if slot_name == "embed":
         return 0.0, 1.0
+    if slot_name in ("bqkv", "bo"):
+        return 0.0, 10 * std
     return 0.0, std

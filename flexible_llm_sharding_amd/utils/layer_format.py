@@ -74,6 +74,7 @@ def split_into_layers(src_dir: str, out_dir: str, verbose: bool = True) -> List[
     layer_params: Dict[str, List[str]] = defaultdict(list)
     for p in wmap:
         layer_params[layer_of_param(p)].append(p)
+    tied = "lm_head" not in layer_params and "model.embed_tokens.weight" in wmap and _tied(src_dir)
     # deterministic order: by the (sorted) source shards each layer needs
     shard_order = {s: i for i, s in enumerate(sorted(set(wmap.values())))}
     layers = sorted(layer_params, key=lambda l: (max(shard_order[wmap[p]] for p in layer_params[l]), l))
@@ -103,7 +104,20 @@ def split_into_layers(src_dir: str, out_dir: str, verbose: bool = True) -> List[
         assert len(sd) == len(layer_params[l]), f"Should have {len(layer_params[l])} keys for {l}"
         save_file(sd, layer_file(out_dir, l))
         written.append(l)
+        if tied and l == "model.embed_tokens":
+            # tie_word_embeddings checkpoints store no lm_head: give the head its own layer file so
+            # the per-layer format stays complete (the reference would fail to open lm_head here)
+            save_file({"lm_head.weight": sd["model.embed_tokens.weight"].clone()}, layer_file(out_dir, "lm_head"))
+            written.append("lm_head")
         for s in need:
             if last_use.get(s) == l:
                 cache.pop(s, None)
     return written
+
+
+def _tied(src_dir: str) -> bool:
+    try:
+        with open(os.path.join(src_dir, "config.json")) as f:
+            return bool(json.load(f).get("tie_word_embeddings", False))
+    except (OSError, ValueError):
+        return False

@@ -41,7 +41,15 @@ def synthetic_layer_state_dict(cfg: ModelConfig, layer_name: str, seed: int = 0,
     if layer_name == "lm_head":
         return {"lm_head.weight": rnd(V, H)}
     p = layer_name
+    bias = {}
+    if cfg.attention_bias:
+        bias.update({f"{p}.self_attn.q_proj.bias": rnd(cfg.q_size) * 10,
+                     f"{p}.self_attn.k_proj.bias": rnd(cfg.kv_size) * 10,
+                     f"{p}.self_attn.v_proj.bias": rnd(cfg.kv_size) * 10})
+    if cfg.o_proj_bias:
+        bias[f"{p}.self_attn.o_proj.bias"] = rnd(H) * 10
     return {
+        **bias,
         f"{p}.self_attn.q_proj.weight": rnd(cfg.q_size, H),
         f"{p}.self_attn.k_proj.weight": rnd(cfg.kv_size, H),
         f"{p}.self_attn.v_proj.weight": rnd(cfg.kv_size, H),

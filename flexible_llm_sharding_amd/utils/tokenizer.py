@@ -18,6 +18,7 @@ Llama tokenizer directory.
 """
 from __future__ import annotations
 
+import json
 import os
 import string
 from dataclasses import dataclass
@@ -60,8 +61,19 @@ def write_synthetic_tokenizer(model_path: str, vocab_size: int = 32000) -> None:
 
 def load_tokenizer(model_path: str):
     """AutoTokenizer with the reference's pad/padding settings (utils.py:102-104)."""
-    from transformers import AutoTokenizer
-    tok = AutoTokenizer.from_pretrained(model_path)
+    from transformers import AutoTokenizer, PreTrainedTokenizerFast
+    cls_name = None
+    try:
+        with open(os.path.join(model_path, "tokenizer_config.json")) as f:
+            cls_name = json.load(f).get("tokenizer_class")
+    except (OSError, ValueError):
+        pass
+    if cls_name in ("PreTrainedTokenizerFast", "TokenizersBackend"):
+        # an explicit generic fast tokenizer (e.g. ours): do not let AutoTokenizer substitute the
+        # model_type's own class from config.json
+        tok = PreTrainedTokenizerFast.from_pretrained(model_path)
+    else:
+        tok = AutoTokenizer.from_pretrained(model_path)
     tok.pad_token = tok.eos_token
     tok.padding_side = "right"
     return tok

@@ -147,3 +147,66 @@ def test_checkpoint_resume_after_fault(ctx, tmp_path, monkeypatch):
         ck.commit(k, [0], torch.float32)
     assert ck.available() == [2, 3]
     assert torch.equal(ck.load(3)[0], torch.ones(2, 3))
+
+
+def _hf_family_case(tmp_path, family):
+    """tiny random checkpoint of another Llama-structured family + its HF model."""
+    transformers = pytest.importorskip("transformers")
+    from flexible_llm_sharding_amd.config import preset
+    from flexible_llm_sharding_amd.utils.synthetic import write_synthetic_checkpoint
+    from flexible_llm_sharding_amd.utils.tokenizer import write_synthetic_tokenizer
+    if family == "qwen2":
+        cfg = preset("tiny-qwen2")
+        hf_cfg = transformers.Qwen2Config(
+            hidden_size=cfg.hidden_size, intermediate_size=cfg.intermediate_size,
+            num_attention_heads=cfg.num_attention_heads, num_key_value_heads=cfg.num_key_value_heads,
+            num_hidden_layers=cfg.num_hidden_layers, vocab_size=cfg.vocab_size, rms_norm_eps=cfg.rms_norm_eps,
+            rope_theta=cfg.rope_theta, max_position_embeddings=cfg.max_position_embeddings,
+            tie_word_embeddings=False, use_sliding_window=False)
+        model = transformers.Qwen2ForCausalLM(hf_cfg)
+    else:
+        cfg = preset("tiny", model_type="mistral", architectures=["MistralForCausalLM"], rope_theta=1e6,
+                     sliding_window=4096)
+        hf_cfg = transformers.MistralConfig(
+            hidden_size=cfg.hidden_size, intermediate_size=cfg.intermediate_size,
+            num_attention_heads=cfg.num_attention_heads, num_key_value_heads=cfg.num_key_value_heads,
+            num_hidden_layers=cfg.num_hidden_layers, vocab_size=cfg.vocab_size, rms_norm_eps=cfg.rms_norm_eps,
+            rope_theta=cfg.rope_theta, max_position_embeddings=cfg.max_position_embeddings,
+            tie_word_embeddings=False, sliding_window=4096)
+        model = transformers.MistralForCausalLM(hf_cfg)
+    path = str(tmp_path / family)
+    write_synthetic_checkpoint(cfg, path, seed=5, std=0.05)
+    write_synthetic_tokenizer(path, cfg.vocab_size)
+    sd = load_full_state_dict(cfg, path)
+    missing, unexpected = model.float().eval().load_state_dict({k: v.float() for k, v in sd.items()}, strict=False)
+    assert not unexpected and all("rotary" in m for m in missing), (missing, unexpected)
+    return path, cfg, sd, model
+
+
+@pytest.mark.parametrize("family", ["qwen2", "mistral"])
+def test_other_llama_families_match_hf(tmp_path, family):
+    """Qwen2 (q/k/v biases, rope_theta 1e6) and Mistral == HF transformers in causal mode,
+    and == the fp32 oracle in the reference's bidirectional-prefix mode."""
+    from flexible_llm_sharding_amd.config import ModelConfig
+    path, cfg, sd, model = _hf_family_case(tmp_path, family)
+    assert ModelConfig.from_pretrained(path).attention_bias == (family == "qwen2")
+    tok = load_tokenizer(path)
+    prompts = synthetic_prompts(3, 20, 2, 5, cfg.vocab_size, seed=9, vary=True)
+    out = ShardedRunner(cfg, FileLayerSource(cfg, path), "cpu", tok, prefix_attention="causal")(prompts)
+    for (prefix, sufs), o in zip(prompts, out):
+        tp = tokenize_prompt(tok, prefix, sufs)
+        for j, s in enumerate(tp.suffixes):
+            with torch.no_grad():
+                logits = model(torch.tensor([tp.prefix + s])).logits[0, -1].float()
+            assert np.abs(o[j, 0].astype(np.float32) - torch.softmax(logits, -1).numpy()).max() < 2e-3
+    bid = ShardedRunner(cfg, FileLayerSource(cfg, path), "cpu", tok, layer_num_per_shard=2)(prompts)
+    for o, rf in zip(bid, reference_scores(cfg, sd, tok, prompts)):
+        assert np.abs(o.astype(np.float32) - rf).max() < 1e-4
+
+
+def test_unsupported_configs_rejected():
+    from flexible_llm_sharding_amd.config import ModelConfig
+    for bad in ({"model_type": "gemma"}, {"mlp_bias": True}, {"hidden_act": "gelu"},
+                {"hidden_size": 256, "num_attention_heads": 4, "head_dim": 128}):
+        with pytest.raises(NotImplementedError):
+            ModelConfig.from_dict(bad)

@@ -58,3 +58,19 @@ def test_resident_repeat_calls(setup):
     assert r.prefetcher.bytes_h2d == h2d_first          # no re-streaming when resident
     for x, y in zip(a, b):
         assert np.array_equal(x, y)
+
+
+def test_qwen2_family_on_gpu(tmp_path):
+    """Qwen2-structured model (q/k/v bias in the fused RoPE epilogue) vs the fp32 oracle."""
+    from flexible_llm_sharding_amd.config import preset
+    from flexible_llm_sharding_amd.utils.synthetic import write_synthetic_checkpoint
+    cfg = preset("tiny-qwen2")
+    path = str(tmp_path / "q2")
+    write_synthetic_checkpoint(cfg, path, seed=3, std=0.05)
+    tok = load_tokenizer(path)
+    prompts = synthetic_prompts(4, 70, 3, 12, cfg.vocab_size, seed=5, vary=True)
+    ref = reference_scores(cfg, load_full_state_dict(cfg, path), tok, prompts)
+    r = ShardedRunner(cfg, HostStore.from_model_path(cfg, path), "cuda:0", tok, layer_num_per_shard=2)
+    for o, rf in zip(r(prompts), ref):
+        assert np.abs(o.astype(np.float32) - rf).max() < 2e-3
+    r.close()

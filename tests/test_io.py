@@ -90,10 +90,10 @@ def test_layer_of_param():
     assert layer_of_param("lm_head.weight") == "lm_head"
 
 
-def _hf_checkpoint(tmp_path, fmt):
+def _hf_checkpoint(tmp_path, fmt, name="tiny", tied=False):
     from flexible_llm_sharding_amd.utils.synthetic import synthetic_layer_state_dict
     from flexible_llm_sharding_amd.utils.tokenizer import write_synthetic_tokenizer
-    cfg = preset("tiny")
+    cfg = preset(name, tie_word_embeddings=tied)
     d = tmp_path / f"hf_{fmt}"
     d.mkdir()
     cfg.save(str(d))
@@ -101,6 +101,8 @@ def _hf_checkpoint(tmp_path, fmt):
     sd = {}
     for n in cfg.layer_names():
         sd.update(synthetic_layer_state_dict(cfg, n, seed=2))
+    if tied:
+        del sd["lm_head.weight"]             # HF tied checkpoints store no lm_head
     names = sorted(sd)
     halves = [names[: len(names) // 2], names[len(names) // 2:]]
     wmap = {}
@@ -130,3 +132,20 @@ def test_split_into_layers(tmp_path, fmt):
         for k, v in got.items():
             assert layer_of_param(k) == n
             assert torch.equal(v, sd[k])
+
+
+def test_split_tied_qwen2_checkpoint(tmp_path):
+    """Qwen2 (q/k/v biases) with tie_word_embeddings: the converter materialises lm_head,
+    and the packed layer round-trips biases through the RoPE row permutation."""
+    from flexible_llm_sharding_amd.models.layout import pack_layer, unpack_layer
+    cfg, src, sd = _hf_checkpoint(tmp_path, "safetensors", name="tiny-qwen2", tied=True)
+    out = tmp_path / "layers_tied"
+    written = split_into_layers(str(src), str(out), verbose=False)
+    assert sorted(written) == sorted(cfg.layer_names())
+    head = load_file(str(out / "lm_head.safetensors"))["lm_head.weight"]
+    assert torch.equal(head, sd["model.embed_tokens.weight"])
+    layer = load_file(str(out / "model.layers.1.safetensors"))
+    assert "model.layers.1.self_attn.q_proj.bias" in layer
+    back = unpack_layer(cfg, "model.layers.1", pack_layer(cfg, "model.layers.1", layer))
+    for k, v in layer.items():
+        assert torch.equal(back[k], v), k

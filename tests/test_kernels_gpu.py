@@ -263,3 +263,30 @@ def test_gemv_skinny(ops, M, N, K):
     torch.cuda.synchronize()
     assert rel_err(y, x.float() @ w.float().t()) < 2e-3
     assert ops.linear(x, w).shape == (M, N)          # linear() routes M <= 16 here
+
+
+@pytest.mark.parametrize("var", [3, 10])
+def test_gemm_bias_epilogues(ops, ref, var):
+    """Per-column bias ahead of RoPE (Qwen2 q/k/v) and ahead of the residual add (o_proj)."""
+    from flexible_llm_sharding_amd.config import ModelConfig
+    from flexible_llm_sharding_amd.models.llama import rope_tables
+    M, H, nh, nkv, hd = 300, 512, 4, 2, 128
+    ops.k.fls_gemm_set_variant(var)
+    try:
+        x = rnd(M, H, seed=51)
+        wqkv = rnd((nh + 2 * nkv) * hd, H, scale=0.05, seed=52)
+        b = rnd((nh + 2 * nkv) * hd, scale=0.5, seed=53)
+        pos = torch.randint(0, 4000, (M,), dtype=torch.int32, device=DEV)
+        cfg = ModelConfig(hidden_size=nh * hd, num_attention_heads=nh, num_key_value_heads=nkv)
+        cos, sin = rope_tables(cfg, 4096)
+        y = ops.qkv_rope(x, wqkv, pos, cos.to(DEV), sin.to(DEV), nh, nkv, hd, bias=b)
+        r = ref.qkv_rope(x.float().cpu(), wqkv.float().cpu(), pos.cpu(), cos, sin, nh, nkv, hd, bias=b.float().cpu())
+        assert rel_err(y.cpu(), r) < 3e-3
+        wo = rnd(H, H, scale=0.05, seed=54)
+        bo = rnd(H, scale=0.5, seed=55)
+        r0 = rnd(M, H, seed=56)
+        out = ops.linear_residual(x, wo, r0.clone(), bias=bo)
+        assert rel_err(out, r0.float() + x.float() @ wo.float().t() + bo.float()) < 2e-3
+        torch.cuda.synchronize()
+    finally:
+        ops.k.fls_gemm_set_variant(10)
