@@ -49,13 +49,15 @@ struct Epi {
 
 // Store one pair of 16-column subtiles (cols n_first + 4*grp + r and +16)
 // for output row m.  acc_a: first subtile, acc_b: second (its partner).
+// n_first: first column of the 32-column block (gate|up or rotation-pair block);
+// off: the lane's 4-column group inside its first 16 columns (acc_b is 16 columns on).
 template <int EPI>
-__device__ __forceinline__ void store_pair(half_t* __restrict__ C, int ldc, int m, int n_first, int grp,
-                                           const floatx4& acc_a, const floatx4& acc_b, const Epi& ep) {
-  const int c0 = n_first + 4 * grp;
+__device__ __forceinline__ void store_pair_off(half_t* __restrict__ C, int ldc, int m, int n_first, int off,
+                                               const floatx4& acc_a, const floatx4& acc_b, const Epi& ep) {
+  const int c0 = n_first + off;
   if constexpr (EPI == FLS_EPI_SWIGLU) {
     // pair = (gate, up) of intermediate columns [n_first/2, n_first/2 + 16)
-    const int oc = n_first / 2 + 4 * grp;
+    const int oc = n_first / 2 + off;
     half4 o;
 #pragma unroll
     for (int r = 0; r < 4; ++r) o[r] = (half_t)(silu(acc_a[r]) * acc_b[r]);
@@ -98,6 +100,12 @@ __device__ __forceinline__ void store_pair(half_t* __restrict__ C, int ldc, int 
     *(half4*)(C + (size_t)m * ldc + c0) = oa;
     *(half4*)(C + (size_t)m * ldc + c0 + 16) = ob;
   }
+}
+
+template <int EPI>
+__device__ __forceinline__ void store_pair(half_t* __restrict__ C, int ldc, int m, int n_first, int grp,
+                                           const floatx4& acc_a, const floatx4& acc_b, const Epi& ep) {
+  store_pair_off<EPI>(C, ldc, m, n_first, 4 * grp, acc_a, acc_b, ep);
 }
 
 // ABL (ablation, microbenchmarks only): bit0 = no LDS-DMA in the K loop,
@@ -1788,6 +1796,179 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_v11(const half_t* __restrict__
   }
 }
 
+// ------------------------------------------------------------------ v12
+// v10's schedule on v_mfma_f32_32x32x16_f16: the wave's 128x128 quadrant is
+// 4 x 4 blocks of 32x32 (16 floatx16 = 256 AGPRs), a phase = one 64x64 quadrant
+// x K=64 = 16 MFMAs (same matrix-pipe time as v10's 32 16x16x32 ones, half the
+// instructions).  A fragment half = 2 blocks x 4 k-steps = 8 half8, read one
+// phase ahead exactly as in v10; the 32x32 layout puts a lane's 4-row groups
+// 8 apart, so RoPE / SwiGLU partners (16 apart) are element groups g, g+2 of
+// the same lane.
+template <int EPI, int ABL = 0>
+__global__ __launch_bounds__(256, 1) void gemm_nt_v12(const half_t* __restrict__ A, const half_t* __restrict__ W,
+                                                     half_t* __restrict__ C, int M, int N, int K, int lda, int ldw,
+                                                     int ldc, Epi ep) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  const int nwg = gridDim.x;
+  int bid = blockIdx.x;
+  {
+    const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7, loc = bid >> 3;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+  }
+  const int tiles_m = (M + BM - 1) / BM;
+  const int tiles_n = N / BN;
+  constexpr int GROUP_M = 8;
+  const int group = bid / (GROUP_M * tiles_n);
+  const int first_m = group * GROUP_M;
+  const int gsz = min(tiles_m - first_m, GROUP_M);
+  const int in_g = bid - group * GROUP_M * tiles_n;
+  const int tm = first_m + in_g % gsz;
+  const int tn = in_g / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // staging: identical to v10 (half-tiles XA/XB = X rows {0-63,128-191}/{64-127,192-255}, WA/WB likewise)
+  const int lr = lane >> 3;
+  const int lc = (lane & 7) ^ lr;
+  int prow[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int j = 4 * wave + i;
+    prow[i] = (j >> 3) * 128 + (j & 7) * 8;
+  }
+  unsigned xo[8], wo[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    xo[i] = (unsigned)(min(m0 + prow[i] + lr, M - 1) * lda + lc * 8) * 2u;
+    xo[4 + i] = (unsigned)(min(m0 + prow[i] + 64 + lr, M - 1) * lda + lc * 8) * 2u;
+    wo[i] = (unsigned)((prow[i] + lr) * ldw + lc * 8) * 2u;
+  }
+  const char* Ab = (const char*)A;
+  const char* Wb = (const char*)(W + (size_t)n0 * ldw);
+  const size_t wb_off = (size_t)64 * ldw * 2;
+#define V12_X(buf, hb, k0)                                                                        \
+  _Pragma("unroll") for (int i_ = 0; i_ < 4; ++i_)                                                \
+    glds16(Ab + (size_t)(k0) * 2 + xo[(hb) * 4 + i_], smem + (buf) * v9::BUF + (prow[i_] + (hb) * 64) * 128);
+#define V12_W(buf, hb, k0)                                                                        \
+  _Pragma("unroll") for (int i_ = 0; i_ < 4; ++i_)                                                \
+    glds16(Wb + (hb) * wb_off + (size_t)(k0) * 2 + wo[i_],                                        \
+           smem + (buf) * v9::BUF + v9::WIMG + (prow[i_] + (hb) * 64) * 128);
+
+  // fragments: lane reads row (lane & 31) of a 32-row block, 16-B chunk 2s + (lane >> 5)
+  const int wm = wave >> 1, wn = wave & 1;
+  const int r32 = lane & 31, hi = lane >> 5, sw = lane & 7;
+  const int xrow = (wm * 128 + r32) * 128;
+  const int wrow = v9::WIMG + (wn * 128 + r32) * 128;
+  int ch[4];
+#pragma unroll
+  for (int st = 0; st < 4; ++st) ch[st] = ((2 * st + hi) ^ sw) << 4;
+
+  floatx16 acc[4][4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[u][t][e] = 0.f;
+  half8 xf[4][4], wf[4][4];           // [32-row block][k-step]
+#define V12_FENCE_ACC()                                                                           \
+  _Pragma("unroll") for (int u_ = 0; u_ < 4; ++u_)                                                \
+  _Pragma("unroll") for (int t_ = 0; t_ < 4; ++t_) asm volatile("" : "+a"(acc[u_][t_]));
+  V12_FENCE_ACC();
+  asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+
+#define V12_RX(buf, h)                                                                            \
+  _Pragma("unroll") for (int j_ = 0; j_ < 8; ++j_)                                                \
+    xf[(h) * 2 + (j_ >> 2)][j_ & 3] =                                                             \
+        *(const half8*)(smem + (buf) * v9::BUF + xrow + ((h) * 2 + (j_ >> 2)) * 4096 + ch[j_ & 3]);
+#define V12_RW(buf, h)                                                                            \
+  _Pragma("unroll") for (int j_ = 0; j_ < 8; ++j_)                                                \
+    wf[(h) * 2 + (j_ >> 2)][j_ & 3] =                                                             \
+        *(const half8*)(smem + (buf) * v9::BUF + wrow + ((h) * 2 + (j_ >> 2)) * 4096 + ch[j_ & 3]);
+  // phase: 16 MFMAs (k-step outer); one read after each of MFMAs 0..7; DMA after 8, 10, 12, 14
+#define V12_PHASE(xh, wh, RX, rbuf, rh, DX, dbuf, dhb, dk0, SYNC)                                  \
+  {                                                                                               \
+    _Pragma("unroll") for (int i_ = 0; i_ < 16; ++i_) {                                           \
+      const int s_ = i_ >> 2, u_ = (xh) * 2 + ((i_ >> 1) & 1), t_ = (wh) * 2 + (i_ & 1);          \
+      mfma32_acc_inplace_ordered(acc[u_][t_], wf[t_][s_], xf[u_][s_]);                            \
+      if (!(ABL & 2) && i_ < 8) {                                                                 \
+        const int b_ = (rh) * 2 + (i_ >> 2), k_ = i_ & 3;                                         \
+        if (RX)                                                                                   \
+          xf[b_][k_] = *(const half8*)(smem + (rbuf) * v9::BUF + xrow + b_ * 4096 + ch[k_]);      \
+        else                                                                                      \
+          wf[b_][k_] = *(const half8*)(smem + (rbuf) * v9::BUF + wrow + b_ * 4096 + ch[k_]);      \
+      }                                                                                           \
+      if (!(ABL & 1) && i_ >= 8 && (i_ & 1) == 0) {                                               \
+        const int p_ = (i_ - 8) >> 1;                                                             \
+        if (DX)                                                                                   \
+          glds16(Ab + (size_t)(dk0) * 2 + xo[(dhb) * 4 + p_],                                     \
+                 smem + (dbuf) * v9::BUF + (prow[p_] + (dhb) * 64) * 128);                        \
+        else                                                                                      \
+          glds16(Wb + (dhb) * wb_off + (size_t)(dk0) * 2 + wo[p_],                                \
+                 smem + (dbuf) * v9::BUF + v9::WIMG + (prow[p_] + (dhb) * 64) * 128);             \
+      }                                                                                           \
+    }                                                                                             \
+    if (SYNC) {                                                                                   \
+      __builtin_amdgcn_s_waitcnt(0xC07F);                                                         \
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");                                           \
+      __builtin_amdgcn_s_barrier();                                                               \
+    }                                                                                             \
+  }
+
+  const int nk = K / BK;
+  const int kc1 = min(1, nk - 1) * BK;
+  V12_X(0, 0, 0); V12_W(0, 0, 0); V12_W(0, 1, 0); V12_X(0, 1, 0);
+  V12_X(1, 0, kc1); V12_W(1, 1, kc1); V12_W(1, 0, kc1); V12_X(1, 1, kc1);
+  asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  V12_RX(0, 0); V12_RW(0, 0);
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int kt = 0; kt < nk; kt += 2) {
+    const int ka = min(kt + 2, nk - 1) * BK;
+    const int kb = min(kt + 3, nk - 1) * BK;
+    V12_PHASE(0, 0, 0, 0, 1, 1, 0, 0, ka, 0);
+    V12_PHASE(0, 1, 1, 0, 1, 0, 0, 0, ka, 1);
+    V12_PHASE(1, 1, 1, 1, 0, 0, 0, 1, ka, 0);
+    V12_PHASE(1, 0, 0, 1, 1, 1, 0, 1, ka, 1);
+    V12_PHASE(0, 1, 0, 1, 0, 1, 1, 0, kb, 0);
+    V12_PHASE(0, 0, 1, 1, 1, 0, 1, 1, kb, 1);
+    V12_PHASE(1, 0, 1, 0, 0, 0, 1, 0, kb, 0);
+    V12_PHASE(1, 1, 0, 0, 0, 1, 1, 1, kb, 1);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  V12_FENCE_ACC();
+#undef V12_FENCE_ACC
+#undef V12_PHASE
+#undef V12_RW
+#undef V12_RX
+#undef V12_W
+#undef V12_X
+
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int m = m0 + wm * 128 + u * 32 + r32;
+    if (m < M) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int nb = n0 + wn * 128 + t * 32;
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+          const floatx4 a = {acc[u][t][4 * g], acc[u][t][4 * g + 1], acc[u][t][4 * g + 2], acc[u][t][4 * g + 3]};
+          const floatx4 c = {acc[u][t][4 * g + 8], acc[u][t][4 * g + 9], acc[u][t][4 * g + 10],
+                             acc[u][t][4 * g + 11]};
+          store_pair_off<EPI>(C, ldc, m, nb, 8 * g + 4 * hi, a, c, ep);
+        }
+      }
+    }
+  }
+}
+
 int g_variant = -1;   // -1: from env FLS_GEMM_VARIANT (default 3)
 
 int variant() {
@@ -1805,11 +1986,19 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
   const bool fast = (N % BN == 0) && (K % BK == 0) && (lda % 8 == 0) && (ldw % 8 == 0) && M > 0;
   // v8/v9 need an even K-tile count (2-tile unrolled body), v9 32-bit X offsets; else v3
   const bool even_k = (K / BK) % 2 == 0;
-  if (((var == 9 || var == 10 || var == 11) && !(even_k && (size_t)M * lda * 2 < (1ull << 32))) || (var == 8 && !even_k))
+  if (((var == 9 || var == 10 || var == 11 || var == 12) && !(even_k && (size_t)M * lda * 2 < (1ull << 32))) || (var == 8 && !even_k))
     var = 3;
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
   const bool fast4 = fast && (K % (2 * v4::BK4) == 0);
-  if (var == 11 && fast) {
+  if (var == 12 && fast) {
+    static bool attr12 = false;
+    if (!attr12) {
+      (void)hipFuncSetAttribute((const void*)gemm_nt_v12<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                2 * v9::BUF);
+      attr12 = true;
+    }
+    hipLaunchKernelGGL(gemm_nt_v12<EPI>, dim3(tiles), dim3(256), 2 * v9::BUF, s, A, W, C, M, N, K, lda, ldw, ldc, ep);
+  } else if (var == 11 && fast) {
     static bool attr11 = false;
     if (!attr11) {
       (void)hipFuncSetAttribute((const void*)gemm_nt_v11<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1951,6 +2140,19 @@ extern "C" int fls_gemm_ablate(int abl, const void* A, const void* W, void* C, i
     break;
     FLS_SCHED10_CASE(0) FLS_SCHED10_CASE(1) FLS_SCHED10_CASE(2) FLS_SCHED10_CASE(3)
 #undef FLS_SCHED10_CASE
+    case 70:
+    case 71:
+      if ((K / BK) % 2) return -2;
+      if (abl == 70) {
+        (void)hipFuncSetAttribute((const void*)gemm_nt_v12<0, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * v9::BUF);
+        hipLaunchKernelGGL((gemm_nt_v12<0, 0>), dim3(tiles), dim3(256), 2 * v9::BUF, (hipStream_t)s, a, w, c, M, N, K,
+                           K, K, N, ep);
+      } else {
+        (void)hipFuncSetAttribute((const void*)gemm_nt_v12<0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * v9::BUF);
+        hipLaunchKernelGGL((gemm_nt_v12<0, 1>), dim3(tiles), dim3(256), 2 * v9::BUF, (hipStream_t)s, a, w, c, M, N, K,
+                           K, K, N, ep);
+      }
+      break;
     case 50:
       if ((K / BK) % 2) return -2;
       (void)hipFuncSetAttribute((const void*)gemm_nt_v11<0, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * v9::BUF);

@@ -50,6 +50,8 @@ def build_source(args, cfg: ModelConfig, comm: Comm, device: torch.device):
     src = FileLayerSource(cfg, args.model_path)
     if args.weight_cache == "disk":
         return src
+    if args.weight_cache == "packed":
+        return open_packed_source(args, cfg, comm, mine)
     return HostStore.from_source(src, pinned=device.type == "cuda", names=mine)
 
 
@@ -71,6 +73,18 @@ def build_runner(args, cfg: ModelConfig, device, comm: Comm, tok) -> ShardedRunn
                          resume_dir=getattr(args, "resume_dir", None),
                          checkpoint_every=getattr(args, "checkpoint_every", 0),
                          max_token_len=getattr(args, "max_token_len", None) or MAX_TOKEN_LEN)
+
+
+def open_packed_source(args, cfg: ModelConfig, comm: Comm, names):
+    """Build (rank 0, once) and open the packed-layer cache."""
+    from .runtime.packed import PackedFileSource, build_packed_cache
+    cache = args.packed_dir or os.path.join(args.model_path, ".fls_packed")
+    if comm.rank == 0:
+        n = build_packed_cache(FileLayerSource(cfg, args.model_path), cache, verbose=args.verbose)
+        if n and args.verbose:
+            print(f"[packed cache] wrote {n} layers to {cache}")
+    comm.barrier()
+    return PackedFileSource(cfg, cache, names=names)
 
 
 def load_model_meta(args):

@@ -50,6 +50,16 @@ class SlicedHostStore(HostStore):
     def from_source(cls, src: LayerSource, rank: int, world: int, pinned: bool = True,
                     names: Optional[Sequence[str]] = None) -> "SlicedHostStore":
         st = cls(src.cfg, rank, world, src.dtype, pinned, names)
+        if hasattr(src, "read_range_into"):
+            # packed images on disk: read only this rank's byte slice of each layer
+            for n in st.names:
+                nb, c = st.nbytes(n), st.chunk_bytes(n)
+                buf = hostmem.alloc_host(c, pinned=pinned)
+                lo, hi = rank * c, min(nb, (rank + 1) * c)
+                if hi > lo:
+                    src.read_range_into(n, buf, lo, hi)
+                st.buffers[n] = buf
+            return st
         full = None
         for n in st.names:
             nb = st.nbytes(n)
@@ -144,8 +154,11 @@ def build_dp_sharded_runner(args, cfg, device, comm: Comm, tok, store: Optional[
     if store is None and getattr(args, "synthetic", None):
         store = SlicedHostStore.synthetic(cfg, device, comm.rank, comm.world, pinned=device.type == "cuda")
     elif store is None:
-        store = SlicedHostStore.from_source(FileLayerSource(cfg, args.model_path), comm.rank, comm.world,
-                                            pinned=device.type == "cuda")
+        src = FileLayerSource(cfg, args.model_path)
+        if getattr(args, "weight_cache", "host") == "packed":
+            from ..api import open_packed_source
+            src = open_packed_source(args, cfg, comm, None)
+        store = SlicedHostStore.from_source(src, comm.rank, comm.world, pinned=device.type == "cuda")
     names = cfg.layer_names()
     plan = make_plan(len(names), args.layer_num_per_shard, comm.world, comm.rank, True)
     shards = [s for s in plan.my_shards if len(s)]

@@ -44,8 +44,12 @@ def build_parser() -> argparse.ArgumentParser:
                    help="prefix self-attention: reference-compatible bidirectional (default) or causal")
     p.add_argument("--resident", type=str2bool, nargs="?", const=True, default=False,
                    help="keep every shard resident in HBM after first load (288 GB fits 70B)")
-    p.add_argument("--weight_cache", choices=["host", "disk"], default="host",
-                   help="host: pinned-RAM layer cache read once; disk: re-read layer files every pass")
+    p.add_argument("--weight_cache", choices=["host", "disk", "packed"], default="host",
+                   help="host: pack every layer once into pinned host RAM (fastest, needs ~model-size RAM); "
+                        "disk: re-read + re-pack the per-layer safetensors every pass (reference behaviour); "
+                        "packed: stream pre-packed layer images from --packed_dir (built on first use)")
+    p.add_argument("--packed_dir", type=str, default=None,
+                   help="packed-layer cache directory (default: <model_path>/.fls_packed)")
     p.add_argument("--dp_weight_shard", type=str2bool, nargs="?", const=True, default=True,
                    help="data parallel: scatter-load 1/G of each layer per GPU + RCCL all-gather")
     p.add_argument("--token_budget", type=int, default=16384, help="max tokens per packed micro-batch")

@@ -3,6 +3,8 @@
 
     python prepare_weights.py <hf_dir> <new_file_dir>
     python prepare_weights.py --synthetic llama2-7b <new_file_dir> [--seed 0]
+    add --packed to also write the packed-layer cache (<new_file_dir>/.fls_packed) used by
+    ``main.py --weight_cache packed``
 """
 import argparse
 import sys
@@ -20,14 +22,23 @@ def main(argv=None):
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--std", type=float, default=0.02)
     ap.add_argument("--num_hidden_layers", type=int, default=None)
+    ap.add_argument("--packed", action="store_true", help="also build the packed-layer cache")
     a = ap.parse_args(argv)
     if a.synthetic:
         from flexible_llm_sharding_amd.config import preset
         from flexible_llm_sharding_amd.utils.synthetic import write_synthetic_checkpoint
         kw = {} if a.num_hidden_layers is None else {"num_hidden_layers": a.num_hidden_layers}
         write_synthetic_checkpoint(preset(a.bin_dir, **kw), a.new_file_dir, seed=a.seed, std=a.std)
-        return 0
-    split_into_layers(a.bin_dir, a.new_file_dir)
+    else:
+        split_into_layers(a.bin_dir, a.new_file_dir)
+    if a.packed:
+        import os
+        from flexible_llm_sharding_amd.config import ModelConfig
+        from flexible_llm_sharding_amd.runtime.packed import build_packed_cache
+        from flexible_llm_sharding_amd.runtime.weights import FileLayerSource
+        cfg = ModelConfig.from_pretrained(a.new_file_dir)
+        build_packed_cache(FileLayerSource(cfg, a.new_file_dir), os.path.join(a.new_file_dir, ".fls_packed"),
+                           verbose=True)
     return 0
 
 

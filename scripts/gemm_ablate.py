@@ -15,7 +15,8 @@ NAMES = {0: "full", 1: "no_dma", 2: "no_lds_read", 3: "mfma_only", 4: "no_mfma",
          20: "v1_groupN_full", 26: "v1_groupN_dma_only",
          40: "v10_full", 41: "v10_no_dma", 42: "v10_no_lds_read", 43: "v10_mfma_only",
          45: "v10_no_dma_no_sync", 47: "v10_mfma_only_no_sync", 50: "v11_full",
-         60: "v10_sched0", 61: "v10_sched1_dma_first", 62: "v10_sched2_spread", 63: "v10_sched3_front"}
+         60: "v10_sched0", 61: "v10_sched1_dma_first", 62: "v10_sched2_spread", 63: "v10_sched3_front",
+         70: "v12_full", 71: "v12_no_dma"}
 if os.environ.get("ABL_ONLY"):
     NAMES = {k: v for k, v in NAMES.items() if k >= int(os.environ["ABL_ONLY"])}
 

@@ -59,7 +59,7 @@ def main():
         row = {"op": name, "M": m, "N": N, "K": K}
         # correctness of each variant vs hipBLASLt (plain epilogue)
         ref = torch.matmul(x, w.t()).float()
-        for var in (9, 10, 11):
+        for var in (10, 12):
             ops.k.fls_gemm_set_variant(var)
             y = ops.gemm(x, w)
             err = ((y.float() - ref).norm() / ref.norm()).item()

@@ -121,3 +121,20 @@ def test_main_synthetic_and_max_token_len(tmp_path):
     m = json.load(open(mj))
     # prefix truncated to 16 tokens (BOS included), each suffix to 16 (after BOS drop): 3 x (16 + 2 x 6)
     assert m["stats"]["tokens"] == 3 * (16 + 2 * 6)
+
+
+def test_main_weight_cache_modes_agree(tiny_model, tmp_path):
+    """host / disk / packed weight caches give identical scores (packed cache built on first use)."""
+    from flexible_llm_sharding_amd.utils.synthetic import synthetic_prompts
+    path, cfg = tiny_model
+    pp = tmp_path / "prompts.pkl"
+    pickle.dump(synthetic_prompts(3, 12, 2, 4, cfg.vocab_size, seed=3), open(pp, "wb"))
+    outs = {}
+    for mode in ("host", "disk", "packed"):
+        out = tmp_path / f"s_{mode}.pkl"
+        _run(["--model_path", path, "--prompt_pickle", str(pp), "--output_file", str(out),
+              "--weight_cache", mode, "--packed_dir", str(tmp_path / "pk")], str(tmp_path))
+        outs[mode] = pickle.load(open(out, "rb"))
+    for a, b, c in zip(outs["host"], outs["disk"], outs["packed"]):
+        assert np.array_equal(a, b) and np.array_equal(a, c)
+    assert len(os.listdir(tmp_path / "pk")) == len(cfg.layer_names())

@@ -149,3 +149,48 @@ def test_split_tied_qwen2_checkpoint(tmp_path):
     back = unpack_layer(cfg, "model.layers.1", pack_layer(cfg, "model.layers.1", layer))
     for k, v in layer.items():
         assert torch.equal(back[k], v), k
+
+
+def test_packed_cache_source(tiny_model, tmp_path):
+    """--weight_cache packed: images equal the in-RAM packing, stale caches are rebuilt,
+    and a rank's byte slice can be read on its own."""
+    from flexible_llm_sharding_amd.runtime.packed import PackedFileSource, build_packed_cache, packed_path
+    from flexible_llm_sharding_amd.runtime.weights import FileLayerSource
+    path, cfg = tiny_model
+    src = FileLayerSource(cfg, path)
+    cache = str(tmp_path / "pk")
+    assert build_packed_cache(src, cache) == len(cfg.layer_names())
+    assert build_packed_cache(src, cache) == 0                      # up to date
+    pk = PackedFileSource(cfg, cache)
+    for n in cfg.layer_names():
+        a = torch.zeros(src.nbytes(n), dtype=torch.uint8)
+        b = torch.zeros(src.nbytes(n), dtype=torch.uint8)
+        src.read_into(n, a)
+        pk.read_into(n, b)
+        assert torch.equal(a, b), n
+        part = torch.zeros(100, dtype=torch.uint8)
+        pk.read_range_into(n, part, 300, 400)
+        assert torch.equal(part, a[300:400])
+    # a cache written for another config is stale -> refused, then rebuilt
+    other = preset("tiny", rms_norm_eps=1e-6)
+    with pytest.raises(FileNotFoundError):
+        PackedFileSource(other, cache)
+    with open(packed_path(cache, "lm_head"), "r+b") as f:
+        f.write(b"garbage!")
+    assert build_packed_cache(src, cache) == 1
+
+
+def test_dp_slices_from_packed_cache(tiny_model, tmp_path):
+    from flexible_llm_sharding_amd.parallel.data_parallel import SlicedHostStore
+    from flexible_llm_sharding_amd.runtime.packed import PackedFileSource, build_packed_cache
+    from flexible_llm_sharding_amd.runtime.weights import FileLayerSource
+    path, cfg = tiny_model
+    src = FileLayerSource(cfg, path)
+    build_packed_cache(src, str(tmp_path / "pk"))
+    for rank in range(3):
+        a = SlicedHostStore.from_source(src, rank, 3, pinned=False)
+        b = SlicedHostStore.from_source(PackedFileSource(cfg, str(tmp_path / "pk")), rank, 3, pinned=False)
+        for n in cfg.layer_names():
+            nb, c = a.nbytes(n), a.chunk_bytes(n)
+            valid = max(0, min(nb, (rank + 1) * c) - rank * c)
+            assert torch.equal(a.buffers[n][:valid], b.buffers[n][:valid]), (rank, n)

@@ -225,7 +225,7 @@ def test_gemm_autotune_choice():
     assert rel_err(y, x.float() @ w.float().t()) < 2e-3
 
 
-@pytest.mark.parametrize("var", [1, 3, 6, 7, 8, 9, 10, 11])
+@pytest.mark.parametrize("var", [1, 3, 6, 7, 8, 9, 10, 11, 12])
 def test_gemm_variants_all_epilogues(ops, ref, var):
     """Every main-loop variant (v1 8-wave, v3 ping-pong, v6 one-wave-per-SIMD, v7 counted-vmcnt phases)
     against fp32 references, with all four epilogues and a ragged M."""
@@ -265,7 +265,7 @@ def test_gemv_skinny(ops, M, N, K):
     assert ops.linear(x, w).shape == (M, N)          # linear() routes M <= 16 here
 
 
-@pytest.mark.parametrize("var", [3, 10])
+@pytest.mark.parametrize("var", [3, 10, 12])
 def test_gemm_bias_epilogues(ops, ref, var):
     """Per-column bias ahead of RoPE (Qwen2 q/k/v) and ahead of the residual add (o_proj)."""
     from flexible_llm_sharding_amd.config import ModelConfig
