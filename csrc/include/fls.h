@@ -51,6 +51,7 @@ int fls_gemm(const void* A, const void* W, void* C, const void* R, int M, int N,
 // shared-prefix / varlen flash attention over packed work items (int32 x8)
 int fls_gemm_set_variant(int v);
 int fls_gemm_ablate(int abl, const void* A, const void* W, void* C, int M, int N, int K, fls_stream_t s);
+int fls_attn_set_variant(int v);   // 1 = 16 rows/wave; 2 = 32 rows/wave + staged prefetch; 3 = 2 + double-buffered LDS (default)
 int fls_attention(const void* qkv, void* out, const int* work, int n_items, int n_q_heads,
                   int n_kv_heads, int head_dim, int ld_qkv, int ld_out, float scale, fls_stream_t s);
 int fls_rmsnorm(const void* x, const void* w, void* y, const int* row_idx, int rows, int H,

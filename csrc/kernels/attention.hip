@@ -125,20 +125,26 @@ __global__ __launch_bounds__(256 * HPB) void attn_fwd(const half_t* __restrict__
       }
       // ---- scale, mask, online softmax (query = lane's fr row)
       float mx = -INFINITY;
+      // key k0 + 16t + 4grp + r is visible iff 16t + r <= rel (one compare per score)
+      const int rel = (causal ? min(klen - 1, qi) : klen - 1) - k0 - grp * 4;
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int key = k0 + t * 16 + grp * 4 + r;
-          const bool vis = key < klen && (!causal || key <= qi);
-          const float v = vis ? sc[t][r] * scale_log2 : -INFINITY;
+          const float v = (t * 16 + r <= rel) ? sc[t][r] * scale_log2 : -INFINITY;
           sc[t][r] = v;
           mx = fmaxf(mx, v);
         }
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float m_new = fmaxf(m_run, mx);
-      const float alpha = fast_exp2(m_run - m_new);
+      // rescale only when some row's max grew (alpha == 1 exactly otherwise)
+      if (!__all(m_new == m_run)) {
+        const float alpha = fast_exp2(m_run - m_new);
+        l_run *= alpha;
+#pragma unroll
+        for (int u = 0; u < NU; ++u) o[u] *= alpha;
+      }
       m_run = m_new;
       float psum = 0.f;
       half8 pf[2];
@@ -150,9 +156,7 @@ __global__ __launch_bounds__(256 * HPB) void attn_fwd(const half_t* __restrict__
           psum += p;
           pf[t >> 1][(t & 1) * 4 + r] = (half_t)p;
         }
-      l_run = l_run * alpha + psum;
-#pragma unroll
-      for (int u = 0; u < NU; ++u) o[u] *= alpha;
+      l_run += psum;
 
       // ---- O^T += V^T P^T ; V^T fragment via two transposed 4x16 reads
       const int q4 = (lane & 15) >> 2, p4 = lane & 3;
@@ -187,7 +191,227 @@ __global__ __launch_bounds__(256 * HPB) void attn_fwd(const half_t* __restrict__
   }
 }
 
+// ------------------------------------------------------------------- v2
+// LDS-read intensity is what bounds attn_fwd: every wave re-reads the whole
+// 64-key K and V tile (32 KB) from LDS for only 16 query rows (32 MFMAs), so
+// the LDS pipe needs ~2x the MFMA time.  v2 gives each wave 32 query rows
+// (two 16-row groups sharing every K / V^T fragment it reads: 64 MFMAs per
+// 32 KB) with 2 waves per query head and HPB heads of one KV group per block,
+// and overlaps the global->LDS staging with compute: tile t+1's K/V rows are
+// loaded into registers before tile t's MFMAs and written to LDS after the
+// barrier that retires tile t's reads (guide T14, write-after-barrier).
+// The key tiles of both ranges (prefix, own suffix) form one flat sequence so
+// the prefetch crosses the range boundary.  DB = true (variant 3, default)
+// double-buffers the LDS tile: tile t+1 is written into the other buffer right
+// after tile t's MFMAs and tile t+2's loads are issued, one barrier per tile.
+// Masking is one integer compare per score against a per-lane visibility
+// bound, and the O / l rescale is skipped when no row's running max grew
+// (alpha would be exactly 1).
+// Measured (profiles/r1_attention): 1024-token prefix + 5x64 suffixes, 70B
+// heads: v1 598 -> v3 727 TFLOP/s; 4096-token prefix: 683 -> 870.
+template <int HD, int HPB, bool DB>
+__global__ __launch_bounds__(128 * HPB, 2) void attn_fwd_v2(const half_t* __restrict__ qkv, half_t* __restrict__ out,
+                                                       const int* __restrict__ work, int nh, int nkv, int ld_qkv,
+                                                       int ld_out, float scale_log2) {
+  constexpr int NT_ = 128 * HPB;
+  constexpr int NS = HD / 32;               // k-steps of QK^T
+  constexpr int NU = HD / 16;               // 16-wide d subtiles of O
+  constexpr int CH = HD / 8;                // 16-byte chunks per K/V row
+  constexpr int PER = KT * CH / NT_;        // chunks per thread per operand
+  static_assert(PER >= 1 && (KT * CH) % NT_ == 0, "tile / block mismatch");
+  constexpr int TILE_BYTES = 2 * KT * HD * 2;         // K + V
+  __shared__ __attribute__((aligned(16))) char smem[(DB ? 2 : 1) * TILE_BYTES];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int h = blockIdx.y * HPB + (wave >> 1);
+  const int g = h / (nh / nkv);             // same for every head of the block (HPB | group)
+  const int rbase = (wave & 1) * 32;        // this wave's first query row of the item
+
+  const int* wi = work + blockIdx.x * 8;
+  const int q_start = wi[0], q_len = wi[1], q_off = wi[2];
+  const int r_start0 = wi[3], r_len0 = wi[4], r_causal0 = wi[5];
+  const int r_start1 = wi[6], r_len1 = wi[7];
+  const int kend0 = r_len0 <= 0 ? 0 : (r_causal0 ? min(r_len0, q_off + q_len) : r_len0);
+  const int kend1 = r_len1 <= 0 ? 0 : min(r_len1, q_off + q_len);
+  const int n0 = (kend0 + KT - 1) / KT;
+  const int ntiles = n0 + (kend1 + KT - 1) / KT;
+
+  const int fr = lane & 15, grp = lane >> 4;
+  const int q_col = h * HD;
+  const int k_col = nh * HD + g * HD;
+  const int v_col = (nh + nkv) * HD + g * HD;
+
+  half8 qf[2][NS];
+  int qi[2];
+#pragma unroll
+  for (int qg = 0; qg < 2; ++qg) {
+    const int qrow = rbase + qg * 16 + fr;
+    const half_t* qp = qkv + (size_t)(q_start + min(qrow, q_len - 1)) * ld_qkv + q_col + grp * 8;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) qf[qg][s] = *(const half8*)(qp + s * 32);
+    qi[qg] = q_off + qrow;
+  }
+
+  floatx4 o[2][NU];
+#pragma unroll
+  for (int qg = 0; qg < 2; ++qg)
+#pragma unroll
+    for (int u = 0; u < NU; ++u) o[qg][u] = floatx4{0.f, 0.f, 0.f, 0.f};
+  float m_run[2] = {-1e30f, -1e30f};
+  float l_run[2] = {0.f, 0.f};
+
+  half8 pk[PER], pv[PER];
+  auto load_tile = [&](int t) {
+    const bool r1 = t >= n0;
+    const int k0 = (r1 ? t - n0 : t) * KT;
+    const int klen = r1 ? r_len1 : r_len0;
+    const int kb = r1 ? r_start1 : r_start0;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = tid + i * NT_;
+      const int row = c / CH, ch = c % CH;
+      const half_t* src = qkv + (size_t)(kb + min(k0 + row, klen - 1)) * ld_qkv;
+      pk[i] = *(const half8*)(src + k_col + ch * 8);
+      pv[i] = *(const half8*)(src + v_col + ch * 8);
+    }
+  };
+  auto store_tile = [&](int buf) {
+    char* Ks = smem + buf * TILE_BYTES;
+    char* Vs = Ks + KT * HD * 2;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = tid + i * NT_;
+      const int row = c / CH, ch = c % CH;
+      *(half8*)(Ks + Lds<HD>::k_off(row, ch)) = pk[i];
+      *(half8*)(Vs + Lds<HD>::v_off(row, ch)) = pv[i];
+    }
+  };
+
+  if (ntiles > 0) {
+    load_tile(0);
+    store_tile(0);
+    if (DB && ntiles > 1) load_tile(1);
+  }
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    const bool r1 = t >= n0;
+    const int k0 = (r1 ? t - n0 : t) * KT;
+    const int klen = r1 ? r_len1 : r_len0;
+    const bool causal = r1 || r_causal0;
+    const char* Ks = smem + (DB ? (t & 1) : 0) * TILE_BYTES;
+    const char* Vs = Ks + KT * HD * 2;
+    if (!DB && t + 1 < ntiles) load_tile(t + 1);     // in flight under this tile's MFMAs
+
+    // ---- S^T = K Q^T for both 16-row query groups (each K fragment read once)
+    floatx4 sc[2][4];
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt) {
+      sc[0][tt] = floatx4{0.f, 0.f, 0.f, 0.f};
+      sc[1][tt] = floatx4{0.f, 0.f, 0.f, 0.f};
+      const int krow = tt * 16 + fr;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        const half8 kf = *(const half8*)(Ks + Lds<HD>::k_off(krow, s * 4 + grp));
+        sc[0][tt] = mfma16x16x32(kf, qf[0][s], sc[0][tt]);
+        sc[1][tt] = mfma16x16x32(kf, qf[1][s], sc[1][tt]);
+      }
+    }
+    // ---- scale, mask, online softmax per query group
+    half8 pf[2][2];
+#pragma unroll
+    for (int qg = 0; qg < 2; ++qg) {
+      float mx = -INFINITY;
+      const int rel = (causal ? min(klen - 1, qi[qg]) : klen - 1) - k0 - grp * 4;
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = (tt * 16 + r <= rel) ? sc[qg][tt][r] * scale_log2 : -INFINITY;
+          sc[qg][tt][r] = v;
+          mx = fmaxf(mx, v);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float m_new = fmaxf(m_run[qg], mx);
+      if (!__all(m_new == m_run[qg])) {
+        const float alpha = fast_exp2(m_run[qg] - m_new);
+        l_run[qg] *= alpha;
+#pragma unroll
+        for (int u = 0; u < NU; ++u) o[qg][u] *= alpha;
+      }
+      m_run[qg] = m_new;
+      float psum = 0.f;
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = fast_exp2(sc[qg][tt][r] - m_new);
+          psum += p;
+          pf[qg][tt >> 1][(tt & 1) * 4 + r] = (half_t)p;
+        }
+      l_run[qg] += psum;
+    }
+    // ---- O^T += V^T P^T (each V^T fragment read once for both groups)
+    const int q4 = (lane & 15) >> 2, p4 = lane & 3;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int row_a = ks * 32 + grp * 4 + q4;
+      const int row_b = row_a + 16;
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        const int ch = u * 2 + (p4 >> 1);
+        const half4 va = ds_read_tr16(Vs + Lds<HD>::v_off(row_a, ch) + (p4 & 1) * 8);
+        const half4 vb = ds_read_tr16(Vs + Lds<HD>::v_off(row_b, ch) + (p4 & 1) * 8);
+        const half8 vf = {va[0], va[1], va[2], va[3], vb[0], vb[1], vb[2], vb[3]};
+        o[0][u] = mfma16x16x32(vf, pf[0][ks], o[0][u]);
+        o[1][u] = mfma16x16x32(vf, pf[1][ks], o[1][u]);
+      }
+    }
+    if (DB) {
+      // the other buffer's last readers (tile t-1) all passed the previous barrier
+      if (t + 1 < ntiles) {
+        store_tile((t + 1) & 1);
+        if (t + 2 < ntiles) load_tile(t + 2);   // in flight under tile t+1's MFMAs
+      }
+      __syncthreads();
+    } else if (t + 1 < ntiles) {
+      __syncthreads();          // every wave is done reading tile t
+      store_tile(0);
+      __syncthreads();
+    }
+  }
+  // ---- normalise and store
+#pragma unroll
+  for (int qg = 0; qg < 2; ++qg) {
+    float l = l_run[qg];
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const int qrow = rbase + qg * 16 + fr;
+    if (qrow < q_len) {
+      const float inv = 1.f / l;
+      half_t* op = out + (size_t)(q_start + qrow) * ld_out + h * HD + grp * 4;
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        half4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = (half_t)(o[qg][u][r] * inv);
+        *(half4*)(op + u * 16) = v;
+      }
+    }
+  }
+}
+
+int g_attn_variant = 3;
+
 }  // namespace
+
+extern "C" int fls_attn_set_variant(int v) {
+  if (v < 1 || v > 3) return -1;
+  g_attn_variant = v;
+  return 0;
+}
 
 extern "C" int fls_attention(const void* qkv, void* out, const int* work, int n_items, int n_q_heads,
                              int n_kv_heads, int head_dim, int ld_qkv, int ld_out, float scale, fls_stream_t s) {
@@ -196,6 +420,30 @@ extern "C" int fls_attention(const void* qkv, void* out, const int* work, int n_
   const float scale_log2 = scale * 1.4426950408889634f;
   auto st = (hipStream_t)s;
   const int group = n_q_heads / n_kv_heads;
+  if (g_attn_variant >= 2 && group % 2 == 0 && (head_dim == 64 || head_dim == 128)) {
+    const int hpb = group % 4 == 0 ? 4 : 2;
+    const bool db = g_attn_variant == 3;
+    dim3 grid2(n_items, n_q_heads / hpb);
+#define FLS_ATTN2_LAUNCH(HD_, HPB_)                                                                       \
+  do {                                                                                                    \
+    if (db)                                                                                               \
+      hipLaunchKernelGGL((attn_fwd_v2<HD_, HPB_, true>), grid2, dim3(128 * HPB_), 0, st,                   \
+                         (const half_t*)qkv, (half_t*)out, work, n_q_heads, n_kv_heads, ld_qkv, ld_out,    \
+                         scale_log2);                                                                     \
+    else                                                                                                  \
+      hipLaunchKernelGGL((attn_fwd_v2<HD_, HPB_, false>), grid2, dim3(128 * HPB_), 0, st,                  \
+                         (const half_t*)qkv, (half_t*)out, work, n_q_heads, n_kv_heads, ld_qkv, ld_out,    \
+                         scale_log2);                                                                     \
+  } while (0)
+    if (head_dim == 128) {
+      if (hpb == 4) FLS_ATTN2_LAUNCH(128, 4); else FLS_ATTN2_LAUNCH(128, 2);
+    } else {
+      if (hpb == 4) FLS_ATTN2_LAUNCH(64, 4); else FLS_ATTN2_LAUNCH(64, 2);
+    }
+#undef FLS_ATTN2_LAUNCH
+    FLS_CHECK_LAUNCH();
+    return 0;
+  }
   const bool two = (group % 2) == 0;        // pair up query heads of one KV group
   dim3 grid(n_items, two ? n_q_heads / 2 : n_q_heads);
 #define FLS_ATTN_LAUNCH(HD_, HPB_)                                                                          \

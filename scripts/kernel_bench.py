@@ -88,14 +88,29 @@ def main():
     b = pack_prompts(tps, list(range(12)), "bidirectional")
     meta = b.device_tensors(dev)
     qkv = torch.randn(b.num_tokens, (nh + 2 * nkv) * hd, device=dev).half()
-    t = timeit(lambda: ops.attention(qkv, meta["work"], nh, nkv, hd), a.iters)
     from flexible_llm_sharding_amd.models.llama import layer_flops
     from flexible_llm_sharding_amd.config import preset
     cfg = preset("llama2-70b")
-    att_fl = layer_flops(cfg, b) - 2.0 * b.num_tokens * cfg.decoder_layer_params()
-    row = {"op": "attention_shared_prefix", "tokens": b.num_tokens, "ours_ms": t * 1e3, "ours_tflops": att_fl / t / 1e12}
-    res.append(row)
-    print(json.dumps(row), flush=True)
+    cases = [("p1024_s5x64", b, meta, qkv)]
+    tps4 = [TokenizedPrompt(list(range(4096)), [list(range(64))] * 5, 64, [63] * 5) for _ in range(3)]
+    b4 = pack_prompts(tps4, list(range(3)), "bidirectional")
+    cases.append(("p4096_s5x64", b4, b4.device_tensors(dev),
+                  torch.randn(b4.num_tokens, (nh + 2 * nkv) * hd, device=dev).half()))
+    for cname, bb, mm, qq in cases:
+        att_fl = layer_flops(cfg, bb) - 2.0 * bb.num_tokens * cfg.decoder_layer_params()
+        row = {"op": "attention_shared_prefix", "case": cname, "tokens": bb.num_tokens}
+        ts = {1: [], 2: [], 3: []}
+        for _ in range(3):                       # interleaved rounds (guide §5.4 rule 24)
+            for var in (1, 2, 3):
+                ops.k.fls_attn_set_variant(var)
+                ts[var].append(timeit(lambda: ops.attention(qq, mm["work"], nh, nkv, hd), a.iters))
+        ops.k.fls_attn_set_variant(3)
+        for var in (1, 2, 3):
+            t = sorted(ts[var])[1]
+            row[f"v{var}_ms"] = t * 1e3
+            row[f"v{var}_tflops"] = att_fl / t / 1e12
+        res.append(row)
+        print(json.dumps(row), flush=True)
     x = torch.randn(M, H, device=dev).half()
     wln = torch.randn(H, device=dev).half()
     t = timeit(lambda: ops.rmsnorm(x, wln, 1e-5), a.iters)

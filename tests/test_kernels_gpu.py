@@ -115,10 +115,17 @@ def _attn_case(nh, nkv, hd, prompts, prefix_attention, seed=0):
     return b, qkv
 
 
-@pytest.mark.parametrize("nh,nkv,hd", [(4, 2, 64), (8, 1, 128), (2, 2, 128)])
+@pytest.fixture(params=[1, 2, 3], ids=["attn_v1", "attn_v2", "attn_v2db"])
+def attn_variant(request, ops):
+    assert ops.k.fls_attn_set_variant(request.param) == 0
+    yield request.param
+    ops.k.fls_attn_set_variant(3)
+
+
+@pytest.mark.parametrize("nh,nkv,hd", [(4, 2, 64), (8, 1, 128), (2, 2, 128), (16, 2, 128), (12, 2, 64)])
 @pytest.mark.parametrize("mode", ["bidirectional", "causal"])
-def test_attention_shared_prefix(ops, ref, nh, nkv, hd, mode):
-    prompts = [(70, [5, 64, 1]), (1, [3]), (130, [65, 17, 129])]
+def test_attention_shared_prefix(ops, ref, attn_variant, nh, nkv, hd, mode):
+    prompts = [(70, [5, 64, 1]), (1, [3]), (130, [65, 17, 129]), (200, [33, 64])]
     b, qkv = _attn_case(nh, nkv, hd, prompts, mode)
     meta = b.device_tensors(DEV)
     y = ops.attention(qkv.to(DEV), meta["work"], nh, nkv, hd)
@@ -127,7 +134,7 @@ def test_attention_shared_prefix(ops, ref, nh, nkv, hd, mode):
     assert rel_err(y.cpu(), r) < 5e-3
 
 
-def test_attention_softmax_spike(ops, ref):
+def test_attention_softmax_spike(ops, ref, attn_variant):
     # force the online-softmax rescale path: one huge key late in the sequence
     nh, nkv, hd = 2, 1, 128
     b, qkv = _attn_case(nh, nkv, hd, [(200, [40])], "bidirectional", seed=3)
