@@ -52,6 +52,7 @@ def main(argv=None):
     ap.add_argument("--mode", default="auto", choices=["auto", "mp", "dp"])
     ap.add_argument("--token-budget", type=int, default=16384)
     ap.add_argument("--resident", action="store_true")
+    ap.add_argument("--hip-graphs", action="store_true", help="with --resident: whole-forward HIP graph replay")
     ap.add_argument("--prefix-attention", default="bidirectional")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--json-out", default=None)
@@ -111,7 +112,7 @@ def main(argv=None):
     runner = ShardedRunner(cfg, store, dev, tok, layer_num_per_shard=a.lnps, storage_location=a.storage,
                            disk_folder=f"/tmp/fls_bench_spill_{rank}", prefix_attention=a.prefix_attention,
                            token_budget=a.token_budget, resident=a.resident, comm=comm, data_parallel=dp,
-                           prefetcher=pf)
+                           prefetcher=pf, hip_graphs=a.hip_graphs)
     if not a.cpu:
         torch.cuda.reset_peak_memory_stats(dev)
 
@@ -153,7 +154,7 @@ def main(argv=None):
                    "layer_num_per_shard": a.lnps, "storage_location": a.storage,
                    "parallelism": (f"pp{world}-roundrobin" if mode == "mp" else
                                    (f"dp{world}-allgather-weights" if dp else "single")),
-                   "resident": a.resident, "token_budget": a.token_budget,
+                   "resident": a.resident, "hip_graphs": bool(runner.hip_graphs), "token_budget": a.token_budget,
                    "gemm_backend": os.environ.get("FLS_GEMM_BACKEND", "hip") if dev.type == "cuda" else "torch"},
     }
     if rank == 0:

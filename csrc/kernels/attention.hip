@@ -62,6 +62,7 @@ __global__ __launch_bounds__(256 * HPB) void attn_fwd(const half_t* __restrict__
 
   const int* wi = work + blockIdx.x * 8;
   const int q_start = wi[0], q_len = wi[1], q_off = wi[2];
+  if (q_len <= 0) return;                   // padding item (bucketed graph replays); block-uniform
   const int r_start[2] = {wi[3], wi[6]};
   const int r_len[2] = {wi[4], wi[7]};
   const int r_causal[2] = {wi[5], 1};
@@ -231,6 +232,7 @@ __global__ __launch_bounds__(128 * HPB, 2) void attn_fwd_v2(const half_t* __rest
 
   const int* wi = work + blockIdx.x * 8;
   const int q_start = wi[0], q_len = wi[1], q_off = wi[2];
+  if (q_len <= 0) return;                   // padding item (bucketed graph replays); block-uniform
   const int r_start0 = wi[3], r_len0 = wi[4], r_causal0 = wi[5];
   const int r_start1 = wi[6], r_len1 = wi[7];
   const int kend0 = r_len0 <= 0 ? 0 : (r_causal0 ? min(r_len0, q_off + q_len) : r_len0);

@@ -72,7 +72,8 @@ def build_runner(args, cfg: ModelConfig, device, comm: Comm, tok) -> ShardedRunn
                          act_dtype=act, verbose=args.verbose,
                          resume_dir=getattr(args, "resume_dir", None),
                          checkpoint_every=getattr(args, "checkpoint_every", 0),
-                         max_token_len=getattr(args, "max_token_len", None) or MAX_TOKEN_LEN)
+                         max_token_len=getattr(args, "max_token_len", None) or MAX_TOKEN_LEN,
+                         hip_graphs=getattr(args, "hip_graphs", False))
 
 
 def open_packed_source(args, cfg: ModelConfig, comm: Comm, names):

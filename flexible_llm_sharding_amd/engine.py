@@ -64,7 +64,7 @@ class ShardedRunner:
                  act_dtype: Optional[torch.dtype] = None, n_slots: int = 2,
                  mlp_chunk: int = 16384, prefetcher: Optional[ShardPrefetcher] = None,
                  verbose: bool = False, resume_dir: Optional[str] = None, checkpoint_every: int = 0,
-                 max_token_len: int = MAX_TOKEN_LEN):
+                 max_token_len: int = MAX_TOKEN_LEN, hip_graphs: bool = False):
         self.cfg = cfg
         self.src = source
         self.dev = torch.device(device)
@@ -107,6 +107,12 @@ class ShardedRunner:
         self.h2d_stream = torch.cuda.Stream(self.dev) if self.cuda else None
         self.d2h_stream = torch.cuda.Stream(self.dev) if self.cuda else None
         self._store: Optional[ActivationStore] = None
+        # whole-forward HIP graphs: only when every shard is local AND resident (fixed weight pointers)
+        self.hip_graphs = bool(hip_graphs and self.cuda and resident and self.plan.mode != "mp"
+                               and not resume_dir)
+        self._graphs = None
+        self._n_decoders = sum(1 for n in self.names if layer_kind(n) == "decoder")
+        self._W_all: Dict[str, Dict[str, torch.Tensor]] = {}
 
     # ----------------------------------------------------------- helpers
     def tokenize(self, prompts) -> List[TokenizedPrompt]:
@@ -161,6 +167,8 @@ class ShardedRunner:
         n = len(tps)
         groups = split_microbatches(tps, self.token_budget)
         batches = [pack_prompts([tps[i] for i in g], g, self.prefix_attention) for g in groups]
+        if self.hip_graphs:
+            return self._run_graphed(tps, batches, t_start)
         metas = [b.device_tensors(self.dev) for b in batches]   # all uploads before any compute
         store = self._get_store()
         store.bytes_d2h = store.bytes_h2d = 0
@@ -301,6 +309,60 @@ class ShardedRunner:
             print(f"{self.dev} rank{comm.rank}: loaded {n_layers} layers in {pf.wait_seconds:.2f}s "
                   f"(exposed weight wait); {len(self.my_shards)} shards, {len(batches)} micro-batches, "
                   f"{self.stats['tokens']:.0f} tokens in {wall:.2f}s")
+        return outputs
+
+    # ------------------------------------------------------ HIP graphs
+    def _forward_all(self, meta: dict, batch: PackedBatch) -> torch.Tensor:
+        """embed -> every layer -> norm -> head on resident weights (captured by GraphedForward)."""
+        state = None
+        for name in self.names:
+            state = run_layer(self.ctx, name, self._W_all[name], state, batch, meta)
+        return state
+
+    def _run_graphed(self, tps, batches, t_start: float) -> List[Optional[np.ndarray]]:
+        """Resident-weights path: one graph replay per micro-batch (runtime/graphs.py).
+
+        Activations never leave HBM (there is no shard boundary inside the
+        graph), so ``storage_location`` has nothing to park.
+        """
+        from .runtime.graphs import GraphedForward
+        pf = self.prefetcher
+        if not self._W_all:
+            for k in range(len(self.my_shards)):
+                self._W_all.update(pf.acquire(k))
+        if self._graphs is None:
+            self._graphs = GraphedForward(self.dev, self._forward_all)
+        outputs: List[Optional[np.ndarray]] = [None] * len(tps)
+        flops = 0.0
+        pending = []
+        store = self._get_store()
+        for batch in batches:
+            probs = self._graphs.run(batch)
+            nbytes = probs.numel() * probs.element_size()
+            pool_buf = store.host_buffer(nbytes)
+            host = pool_buf[:nbytes].view(probs.dtype).view(probs.shape)
+            host.copy_(probs, non_blocking=True)     # same stream: ordered before the next replay
+            pending.append((batch, host, pool_buf))
+            flops += self._n_decoders * layer_flops(self.cfg, batch)
+        torch.cuda.synchronize(self.dev)
+        for batch, host, pool_buf in pending:
+            probs = host.numpy()
+            r = 0
+            for j, pid in enumerate(batch.prompt_ids):
+                ns = batch.n_suffix[j]
+                outputs[pid] = np.expand_dims(probs[r:r + ns].astype(np.float16, copy=True), axis=1)
+                r += ns
+            store.recycle_host(pool_buf)
+        wall = time.perf_counter() - t_start
+        self.stats = {
+            "wall_s": wall, "compute_launch_s": wall,
+            "tokens": float(sum(b.num_tokens for b in batches)),
+            "padded_tokens": float(sum(b.padded_tokens for b in batches)),
+            "decoder_flops": flops, "micro_batches": float(len(batches)),
+            "weight_wait_s": pf.wait_seconds, "weight_h2d_bytes": 0.0,
+            "act_d2h_bytes": 0.0, "act_h2d_bytes": 0.0, "resumed_from_shard": 0.0,
+            "graph_captures": float(self._graphs.captures), "graph_replays": float(self._graphs.replays),
+        }
         return outputs
 
     # ------------------------------------------------- progress / resume

@@ -174,4 +174,5 @@ def build_dp_sharded_runner(args, cfg, device, comm: Comm, tok, store: Optional[
                          act_dtype=act, prefetcher=pf, verbose=getattr(args, "verbose", False),
                          resume_dir=getattr(args, "resume_dir", None),
                          checkpoint_every=getattr(args, "checkpoint_every", 0),
-                         max_token_len=getattr(args, "max_token_len", None) or MAX_TOKEN_LEN)
+                         max_token_len=getattr(args, "max_token_len", None) or MAX_TOKEN_LEN,
+                         hip_graphs=getattr(args, "hip_graphs", False))

@@ -1,0 +1,121 @@
+"""HIP-graph replay of the whole per-micro-batch forward (resident weights).
+
+The reference dispatches every op of every layer from Python, one prompt at a
+time (``/root/reference/utils.py:239-291``).  With small batches (a few short
+prompts, or the ``--num_gen_token`` loop that re-runs the full model once per
+generated token, ``main.py:65-90``) the GPU work per layer is a few tens of
+microseconds and host-side dispatch dominates.
+
+When every shard of this rank is resident in HBM the weight pointers never
+change, so embed -> all decoder layers -> final norm -> LM head + softmax of one
+micro-batch is captured ONCE as a HIP graph (``torch.cuda.CUDAGraph`` is
+hipGraph on ROCm) and replayed with a single launch.  Batch shapes are
+bucketed so replays are reused across calls and generation steps:
+
+* tokens -> multiple of ``TOKEN_BUCKET`` (the GEMM M tile; padded rows compute
+  garbage that no valid row ever reads: GEMM / RMSNorm rows are independent and
+  no attention work item covers them),
+* attention work items -> multiple of ``WORK_BUCKET`` (padding items have
+  ``q_len = 0``; the kernels return before touching memory),
+* scored rows -> multiple of ``SCORE_BUCKET`` (padding gathers row 0; ignored).
+
+The metadata of a new batch is copied into the graph's static input tensors
+before the replay; the probabilities come out of its static output tensor.
+All graphs share one memory pool and are replayed in order on one stream, so
+intermediates are shared between them.
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+from typing import Callable, Dict, Tuple
+
+import numpy as np
+import torch
+
+from .batch import WORK_ITEM_FIELDS, PackedBatch
+
+TOKEN_BUCKET = 256
+WORK_BUCKET = 32
+SCORE_BUCKET = 16
+
+
+def _ceil(n: int, m: int) -> int:
+    return max(m, (n + m - 1) // m * m)
+
+
+def bucket_key(batch: PackedBatch) -> Tuple[int, int, int]:
+    return (_ceil(batch.num_tokens, TOKEN_BUCKET), _ceil(batch.work.shape[0], WORK_BUCKET),
+            _ceil(batch.n_scored, SCORE_BUCKET))
+
+
+def padded_meta(batch: PackedBatch, key) -> Dict[str, np.ndarray]:
+    T, W, S = key
+    ids = np.zeros(T, np.int32)
+    ids[:batch.num_tokens] = batch.ids
+    pos = np.zeros(T, np.int32)
+    pos[:batch.num_tokens] = batch.positions
+    work = np.zeros((W, WORK_ITEM_FIELDS), np.int32)
+    work[:batch.work.shape[0]] = batch.work
+    last = np.zeros(S, np.int32)
+    last[:batch.n_scored] = batch.last_idx
+    return {"ids": ids, "positions": pos, "work": work, "last_idx": last}
+
+
+class _Graph:
+    def __init__(self, meta: Dict[str, torch.Tensor]):
+        self.meta = meta                     # static device inputs
+        self.graph = torch.cuda.CUDAGraph()
+        self.out: torch.Tensor = None        # static device output [S, V]
+        self.replays = 0
+
+
+class GraphedForward:
+    """LRU cache of captured whole-model forwards, keyed by the bucketed shape.
+
+    ``forward(meta, batch) -> probs`` must run embed..head for one micro-batch
+    on the current stream using only ``meta`` (device tensors) and resident
+    weights; it is called eagerly once (warm-up) and then under capture.
+    """
+
+    def __init__(self, device, forward: Callable, max_graphs: int = 8):
+        self.dev = torch.device(device)
+        self.forward = forward
+        self.max_graphs = max_graphs
+        self.pool = torch.cuda.graph_pool_handle()
+        self.graphs: "OrderedDict[tuple, _Graph]" = OrderedDict()
+        self.captures = 0
+        self.replays = 0
+
+    def _capture(self, key, batch: PackedBatch) -> _Graph:
+        host = padded_meta(batch, key)
+        meta = {k: torch.from_numpy(v).to(self.dev) for k, v in host.items()}
+        g = _Graph(meta)
+        s = torch.cuda.Stream(self.dev)
+        s.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(s):
+            self.forward(meta, batch)                       # warm-up (lazy inits, autotune)
+        torch.cuda.current_stream(self.dev).wait_stream(s)
+        torch.cuda.synchronize(self.dev)
+        with torch.cuda.graph(g.graph, pool=self.pool, stream=s):
+            g.out = self.forward(meta, batch)
+        torch.cuda.synchronize(self.dev)
+        self.captures += 1
+        return g
+
+    def run(self, batch: PackedBatch) -> torch.Tensor:
+        """Replay (capturing on first sight of the bucket); returns [n_scored, V] on the device."""
+        key = bucket_key(batch)
+        g = self.graphs.get(key)
+        if g is None:
+            if len(self.graphs) >= self.max_graphs:
+                self.graphs.popitem(last=False)
+            g = self._capture(key, batch)
+            self.graphs[key] = g
+        else:
+            self.graphs.move_to_end(key)
+            for k, v in padded_meta(batch, key).items():
+                g.meta[k].copy_(torch.from_numpy(v), non_blocking=False)
+        g.graph.replay()
+        g.replays += 1
+        self.replays += 1
+        return g.out[:batch.n_scored]

@@ -42,6 +42,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--num_gpus", type=int, default=None, help="GPUs to use (default: all visible; 0 = CPU)")
     p.add_argument("--prefix_attention", choices=["bidirectional", "causal"], default="bidirectional",
                    help="prefix self-attention: reference-compatible bidirectional (default) or causal")
+    p.add_argument("--hip_graphs", type=str2bool, nargs="?", const=True, default=False,
+                   help="with --resident: capture each micro-batch's whole forward as one HIP graph and "
+                        "replay it (shape-bucketed; removes per-op host dispatch for small batches)")
     p.add_argument("--resident", type=str2bool, nargs="?", const=True, default=False,
                    help="keep every shard resident in HBM after first load (288 GB fits 70B)")
     p.add_argument("--weight_cache", choices=["host", "disk", "packed"], default="host",
