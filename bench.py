@@ -123,9 +123,10 @@ def main(argv=None):
     comm.barrier()
     sync()
     t_start = time.perf_counter()
+    outs = None
     for i in range(a.steps):
         ts = time.perf_counter()
-        runner(prompts)
+        outs = runner(prompts)
         log(rank, f"[bench] step {i}: {time.perf_counter() - ts:.2f}s  stats={json.dumps({k: round(v, 3) for k, v in runner.stats.items()})}")
     sync()
     comm.barrier()
@@ -138,6 +139,10 @@ def main(argv=None):
         tok_step = comm.all_reduce_sum(tok_step)
         padded_step = comm.all_reduce_sum(padded_step)
     peak = comm.all_reduce_max(0.0 if a.cpu else float(torch.cuda.max_memory_allocated(dev)))
+    # every score this rank produced must be a finite probability (guards the timed path's numerics)
+    import numpy as np
+    finite = all(np.isfinite(o.astype(np.float32)).all() for o in (outs or []) if o is not None)
+    finite = comm.all_reduce_min(1.0 if finite else 0.0) >= 1.0
     ms = elapsed / a.steps * 1000.0
     value = tok_step * a.steps / elapsed
     out = {
@@ -145,7 +150,7 @@ def main(argv=None):
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms, 2), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "fp32-cpu-rehearsal" if a.cpu else "fp16",
         "data": "synthetic prompts (synthetic tokenizer) + random-init Llama-2-70B weights in pinned host RAM",
-        "peak_gpu_mem_gb": round(peak / 1e9, 3),
+        "peak_gpu_mem_gb": round(peak / 1e9, 3), "scores_finite": finite,
         "config": {"model": a.model if a.num_layers is None else f"{a.model}-L{a.num_layers}",
                    "global_batch": n_prompts * (world if dp else 1),
                    "seq_len": a.prefix_len + a.suffix_len,

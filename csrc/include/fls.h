@@ -52,8 +52,10 @@ int fls_gemm(const void* A, const void* W, void* C, const void* R, int M, int N,
 int fls_gemm_set_variant(int v);
 int fls_gemm_ablate(int abl, const void* A, const void* W, void* C, int M, int N, int K, fls_stream_t s);
 int fls_attn_set_variant(int v);   // 1 = 16 rows/wave; 2 = 32 rows/wave + staged prefetch; 3 = 2 + double-buffered LDS (default)
+// kv0 (optional, [P, 2*n_kv*hd] K then V, row stride ld_kv0): range 0 of every work item indexes it
 int fls_attention(const void* qkv, void* out, const int* work, int n_items, int n_q_heads,
-                  int n_kv_heads, int head_dim, int ld_qkv, int ld_out, float scale, fls_stream_t s);
+                  int n_kv_heads, int head_dim, int ld_qkv, int ld_out, float scale, const void* kv0,
+                  int ld_kv0, fls_stream_t s);
 int fls_rmsnorm(const void* x, const void* w, void* y, const int* row_idx, int rows, int H,
                 int ldx, int ldy, float eps, fls_stream_t s);
 int fls_embed(const int* ids, const void* table, void* out, int T, int H, int V, fls_stream_t s);

@@ -46,7 +46,8 @@ struct Lds {
 template <int HD, int HPB>
 __global__ __launch_bounds__(256 * HPB) void attn_fwd(const half_t* __restrict__ qkv, half_t* __restrict__ out,
                                                     const int* __restrict__ work, int nh, int nkv, int ld_qkv,
-                                                    int ld_out, float scale_log2) {
+                                                    int ld_out, float scale_log2, const half_t* __restrict__ kv0,
+                                                    int ld_kv0) {
   constexpr int NS = HD / 32;     // k-steps of the QK^T product
   constexpr int NU = HD / 16;     // 16-wide d subtiles of O
   __shared__ __attribute__((aligned(16))) char smem[2 * KT * HD * 2];
@@ -94,6 +95,12 @@ __global__ __launch_bounds__(256 * HPB) void attn_fwd(const half_t* __restrict__
     if (klen <= 0) continue;
     const int kbase = r_start[rg];
     const bool causal = r_causal[rg] != 0;
+    // range 0 may live in the prefix K/V cache ([P, 2 * nkv * HD], K then V)
+    const bool from_cache = rg == 0 && kv0 != nullptr;
+    const half_t* kvb = from_cache ? kv0 : qkv;
+    const int ldk = from_cache ? ld_kv0 : ld_qkv;
+    const int kc = from_cache ? g * HD : k_col;
+    const int vc = from_cache ? (nkv + g) * HD : v_col;
     // keys needed by the last valid query of this block
     const int kend = causal ? min(klen, q_off + q_len) : klen;
     for (int k0 = 0; k0 < kend; k0 += KT) {
@@ -104,9 +111,9 @@ __global__ __launch_bounds__(256 * HPB) void attn_fwd(const half_t* __restrict__
       for (int c = tid; c < CHUNKS; c += NT_) {
         const int row = c / (HD / 8), ch = c % (HD / 8);
         const int key = min(k0 + row, klen - 1);
-        const half_t* src = qkv + (size_t)(kbase + key) * ld_qkv;
-        const half8 kv = *(const half8*)(src + k_col + ch * 8);
-        const half8 vv = *(const half8*)(src + v_col + ch * 8);
+        const half_t* src = kvb + (size_t)(kbase + key) * ldk;
+        const half8 kv = *(const half8*)(src + kc + ch * 8);
+        const half8 vv = *(const half8*)(src + vc + ch * 8);
         *(half8*)(Ks + Lds<HD>::k_off(row, ch)) = kv;
         *(half8*)(Vs + Lds<HD>::v_off(row, ch)) = vv;
       }
@@ -213,7 +220,8 @@ __global__ __launch_bounds__(256 * HPB) void attn_fwd(const half_t* __restrict__
 template <int HD, int HPB, bool DB>
 __global__ __launch_bounds__(128 * HPB, 2) void attn_fwd_v2(const half_t* __restrict__ qkv, half_t* __restrict__ out,
                                                        const int* __restrict__ work, int nh, int nkv, int ld_qkv,
-                                                       int ld_out, float scale_log2) {
+                                                       int ld_out, float scale_log2,
+                                                       const half_t* __restrict__ kv0, int ld_kv0) {
   constexpr int NT_ = 128 * HPB;
   constexpr int NS = HD / 32;               // k-steps of QK^T
   constexpr int NU = HD / 16;               // 16-wide d subtiles of O
@@ -270,13 +278,19 @@ __global__ __launch_bounds__(128 * HPB, 2) void attn_fwd_v2(const half_t* __rest
     const int k0 = (r1 ? t - n0 : t) * KT;
     const int klen = r1 ? r_len1 : r_len0;
     const int kb = r1 ? r_start1 : r_start0;
+    // range 0 may live in the prefix K/V cache ([P, 2 * nkv * HD], K then V)
+    const bool from_cache = !r1 && kv0 != nullptr;
+    const half_t* kvb = from_cache ? kv0 : qkv;
+    const int ldk = from_cache ? ld_kv0 : ld_qkv;
+    const int kc = from_cache ? g * HD : k_col;
+    const int vc = from_cache ? (nkv + g) * HD : v_col;
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int c = tid + i * NT_;
       const int row = c / CH, ch = c % CH;
-      const half_t* src = qkv + (size_t)(kb + min(k0 + row, klen - 1)) * ld_qkv;
-      pk[i] = *(const half8*)(src + k_col + ch * 8);
-      pv[i] = *(const half8*)(src + v_col + ch * 8);
+      const half_t* src = kvb + (size_t)(kb + min(k0 + row, klen - 1)) * ldk;
+      pk[i] = *(const half8*)(src + kc + ch * 8);
+      pv[i] = *(const half8*)(src + vc + ch * 8);
     }
   };
   auto store_tile = [&](int buf) {
@@ -416,7 +430,8 @@ extern "C" int fls_attn_set_variant(int v) {
 }
 
 extern "C" int fls_attention(const void* qkv, void* out, const int* work, int n_items, int n_q_heads,
-                             int n_kv_heads, int head_dim, int ld_qkv, int ld_out, float scale, fls_stream_t s) {
+                             int n_kv_heads, int head_dim, int ld_qkv, int ld_out, float scale, const void* kv0,
+                             int ld_kv0, fls_stream_t s) {
   if (n_items <= 0) return 0;
   if (n_q_heads % n_kv_heads) return -2;
   const float scale_log2 = scale * 1.4426950408889634f;
@@ -431,11 +446,11 @@ extern "C" int fls_attention(const void* qkv, void* out, const int* work, int n_
     if (db)                                                                                               \
       hipLaunchKernelGGL((attn_fwd_v2<HD_, HPB_, true>), grid2, dim3(128 * HPB_), 0, st,                   \
                          (const half_t*)qkv, (half_t*)out, work, n_q_heads, n_kv_heads, ld_qkv, ld_out,    \
-                         scale_log2);                                                                     \
+                         scale_log2, (const half_t*)kv0, ld_kv0);                                                                     \
     else                                                                                                  \
       hipLaunchKernelGGL((attn_fwd_v2<HD_, HPB_, false>), grid2, dim3(128 * HPB_), 0, st,                  \
                          (const half_t*)qkv, (half_t*)out, work, n_q_heads, n_kv_heads, ld_qkv, ld_out,    \
-                         scale_log2);                                                                     \
+                         scale_log2, (const half_t*)kv0, ld_kv0);                                                                     \
   } while (0)
     if (head_dim == 128) {
       if (hpb == 4) FLS_ATTN2_LAUNCH(128, 4); else FLS_ATTN2_LAUNCH(128, 2);
@@ -450,7 +465,7 @@ extern "C" int fls_attention(const void* qkv, void* out, const int* work, int n_
   dim3 grid(n_items, two ? n_q_heads / 2 : n_q_heads);
 #define FLS_ATTN_LAUNCH(HD_, HPB_)                                                                          \
   hipLaunchKernelGGL((attn_fwd<HD_, HPB_>), grid, dim3(256 * HPB_), 0, st, (const half_t*)qkv, (half_t*)out, \
-                     work, n_q_heads, n_kv_heads, ld_qkv, ld_out, scale_log2)
+                     work, n_q_heads, n_kv_heads, ld_qkv, ld_out, scale_log2, (const half_t*)kv0, ld_kv0)
   switch (head_dim) {
     case 64:
       if (two) FLS_ATTN_LAUNCH(64, 2); else FLS_ATTN_LAUNCH(64, 1);

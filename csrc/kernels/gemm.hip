@@ -2080,7 +2080,7 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
 
 }  // namespace
 
-extern "C" int fls_kernels_version(void) { return 4; }
+extern "C" int fls_kernels_version(void) { return 5; }
 
 // microbenchmark-only entry: v1 main loop with parts removed (results are garbage)
 extern "C" int fls_gemm_ablate(int abl, const void* A, const void* W, void* C, int M, int N, int K,

@@ -73,7 +73,9 @@ def build_runner(args, cfg: ModelConfig, device, comm: Comm, tok) -> ShardedRunn
                          resume_dir=getattr(args, "resume_dir", None),
                          checkpoint_every=getattr(args, "checkpoint_every", 0),
                          max_token_len=getattr(args, "max_token_len", None) or MAX_TOKEN_LEN,
-                         hip_graphs=getattr(args, "hip_graphs", False))
+                         hip_graphs=getattr(args, "hip_graphs", False),
+                         prefix_kv_cache=getattr(args, "prefix_kv_cache", False),
+                         prefix_cache_entries=getattr(args, "prefix_cache_entries", 8))
 
 
 def open_packed_source(args, cfg: ModelConfig, comm: Comm, names):

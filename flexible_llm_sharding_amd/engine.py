@@ -64,7 +64,8 @@ class ShardedRunner:
                  act_dtype: Optional[torch.dtype] = None, n_slots: int = 2,
                  mlp_chunk: int = 16384, prefetcher: Optional[ShardPrefetcher] = None,
                  verbose: bool = False, resume_dir: Optional[str] = None, checkpoint_every: int = 0,
-                 max_token_len: int = MAX_TOKEN_LEN, hip_graphs: bool = False):
+                 max_token_len: int = MAX_TOKEN_LEN, hip_graphs: bool = False,
+                 prefix_kv_cache: bool = False, prefix_cache_entries: int = 8):
         self.cfg = cfg
         self.src = source
         self.dev = torch.device(device)
@@ -111,6 +112,12 @@ class ShardedRunner:
         self.hip_graphs = bool(hip_graphs and self.cuda and resident and self.plan.mode != "mp"
                                and not resume_dir)
         self._graphs = None
+        # prefix K/V reuse across calls (generation steps): runtime/prefix_cache.py
+        self.prefix_cache = None
+        if prefix_kv_cache and not self.hip_graphs and not resume_dir:
+            from .runtime.prefix_cache import PrefixKVCache
+            self.prefix_cache = PrefixKVCache(2 * cfg.num_key_value_heads * cfg.head_dim, self.dev,
+                                              self.act_dtype, prefix_cache_entries)
         self._n_decoders = sum(1 for n in self.names if layer_kind(n) == "decoder")
         self._W_all: Dict[str, Dict[str, torch.Tensor]] = {}
 
@@ -165,10 +172,46 @@ class ShardedRunner:
     def run_tokenized(self, tps: Sequence[TokenizedPrompt]) -> List[Optional[np.ndarray]]:
         t_start = time.perf_counter()
         n = len(tps)
-        groups = split_microbatches(tps, self.token_budget)
-        batches = [pack_prompts([tps[i] for i in g], g, self.prefix_attention) for g in groups]
+        entry, cached = self._prefix_entry(tps)
+        groups = split_microbatches(tps, self.token_budget, suffix_only=cached)
+        batches = [pack_prompts([tps[i] for i in g], g, self.prefix_attention,
+                                prefix_offsets=[entry.offsets[i] for i in g] if entry is not None else None,
+                                kv_cached=cached) for g in groups]
         if self.hip_graphs:
             return self._run_graphed(tps, batches, t_start)
+        self.ctx.prefix_entry = entry
+        try:
+            outputs = self._run_batches(tps, batches, t_start)
+        except BaseException:
+            if entry is not None and not cached:
+                self.prefix_cache.drop(entry)
+            raise
+        finally:
+            self.ctx.prefix_entry = None
+        if entry is not None:
+            entry.complete = True
+            if cached:
+                self.prefix_cache.hits += 1
+            else:
+                self.prefix_cache.misses += 1
+        self.stats["prefix_cached"] = float(cached)
+        return outputs
+
+    def _prefix_entry(self, tps):
+        """-> (PrefixEntry or None, cached?).  Model-parallel ranks agree (identical packing)."""
+        pc = self.prefix_cache
+        if pc is None:
+            return None, False
+        e = pc.lookup(tps)
+        have = 1.0 if e is not None else 0.0
+        if self.plan.mode == "mp" and self.comm.active:
+            have = self.comm.all_reduce_min(have)
+        if have >= 1.0:
+            return e, True
+        return pc.begin(tps), False
+
+    def _run_batches(self, tps, batches, t_start: float) -> List[Optional[np.ndarray]]:
+        n = len(tps)
         metas = [b.device_tensors(self.dev) for b in batches]   # all uploads before any compute
         store = self._get_store()
         store.bytes_d2h = store.bytes_h2d = 0

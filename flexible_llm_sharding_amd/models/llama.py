@@ -53,6 +53,7 @@ class ExecContext:
     cos: torch.Tensor
     sin: torch.Tensor
     mlp_chunk: int = 16384       # rows per gate/up + down chunk (bounds the [T, I] buffer)
+    prefix_entry: Optional[object] = None   # runtime.prefix_cache.PrefixEntry of the current call
 
 
 def run_embed(ctx: ExecContext, W: Dict[str, torch.Tensor], meta: dict) -> torch.Tensor:
@@ -60,15 +61,24 @@ def run_embed(ctx: ExecContext, W: Dict[str, torch.Tensor], meta: dict) -> torch
 
 
 def run_decoder(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, batch,
-                meta: dict) -> torch.Tensor:
+                meta: dict, layer_name: str = "") -> torch.Tensor:
     cfg, ops = ctx.cfg, ctx.ops
     eps = cfg.rms_norm_eps
     h = ops.rmsnorm(x, W["ln1"], eps)
     qkv = ops.qkv_rope(h, W["wqkv"], meta["positions"], ctx.cos, ctx.sin,
                        cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim, bias=W.get("bqkv"))
     del h
+    kv0 = None
+    pe = ctx.prefix_entry
+    if pe is not None:
+        qs, kv = cfg.q_size, 2 * cfg.num_key_value_heads * cfg.head_dim
+        if batch.kv_cached:                  # prefix K/V of every prompt from the cache
+            kv0 = pe.buffer(layer_name)
+        elif "pfx_src" in meta:              # full pass: keep the prefix rows' post-RoPE K/V
+            pe.buffer(layer_name, create=True).index_copy_(
+                0, meta["pfx_dst"], qkv[:, qs:qs + kv].index_select(0, meta["pfx_src"]))
     attn_arg = meta["work"] if getattr(ops, "uses_work_items", False) else batch.segments
-    a = ops.attention(qkv, attn_arg, cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim)
+    a = ops.attention(qkv, attn_arg, cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim, kv0=kv0)
     del qkv
     x = ops.linear_residual(a, W["wo"], x, bias=W.get("bo"))
     del a
@@ -103,7 +113,7 @@ def run_layer(ctx: ExecContext, layer_name: str, W: Dict[str, torch.Tensor],
     if kind == "embed":
         return run_embed(ctx, W, meta)
     if kind == "decoder":
-        return run_decoder(ctx, W, state, batch, meta)
+        return run_decoder(ctx, W, state, batch, meta, layer_name)
     if kind == "norm":
         return run_norm(ctx, W, state, meta)
     return run_head(ctx, W, state)

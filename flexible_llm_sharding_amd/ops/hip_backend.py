@@ -188,15 +188,21 @@ class HipOps:
         return self._pick("qkv_rope", x, wqkv, hip, blt, hip, blt)
 
     # ----------------------------------------------------------- attention
-    def attention(self, qkv, work, n_q_heads, n_kv_heads, head_dim):
+    def attention(self, qkv, work, n_q_heads, n_kv_heads, head_dim, kv0=None):
+        """kv0 ([P, 2 * n_kv * hd], K then V): range 0 of every work item reads these rows (prefix cache)."""
         _f16(qkv, "qkv")
         if work.dtype != torch.int32 or not work.is_cuda:
             raise TypeError("work items must be an int32 CUDA tensor")
+        if kv0 is not None:
+            _f16(kv0, "kv0")
+            if kv0.shape[1] != 2 * n_kv_heads * head_dim:
+                raise ValueError(f"kv0 must be [P, {2 * n_kv_heads * head_dim}], got {tuple(kv0.shape)}")
         T = qkv.shape[0]
         out = torch.empty(T, n_q_heads * head_dim, dtype=torch.float16, device=qkv.device)
         rc = self.k.fls_attention(qkv.data_ptr(), out.data_ptr(), work.data_ptr(), work.shape[0],
                                   n_q_heads, n_kv_heads, head_dim, qkv.stride(0), out.stride(0),
-                                  head_dim ** -0.5, _stream())
+                                  head_dim ** -0.5, kv0.data_ptr() if kv0 is not None else None,
+                                  kv0.stride(0) if kv0 is not None else 0, _stream())
         _chk(rc, "fls_attention")
         return out
 

@@ -73,28 +73,36 @@ class TorchOps:
         return torch.cat([qk_out, y[:, qk_cols:]], dim=1).to(x.dtype)
 
     def attention(self, qkv: torch.Tensor, segments, n_q_heads: int, n_kv_heads: int,
-                  head_dim: int) -> torch.Tensor:
-        """Shared-prefix attention over packed segments (see runtime.batch)."""
+                  head_dim: int, kv0: torch.Tensor = None) -> torch.Tensor:
+        """Shared-prefix attention over packed segments (see runtime.batch).
+
+        ``kv0`` ([P, 2 * n_kv * hd], K then V): range 0 of every segment indexes
+        these rows instead of the packed QKV (prefix K/V cache)."""
         T = qkv.shape[0]
         qs = n_q_heads * head_dim
         ks = n_kv_heads * head_dim
         q_all = qkv[:, :qs].view(T, n_q_heads, head_dim)
         k_all = qkv[:, qs:qs + ks].view(T, n_kv_heads, head_dim)
         v_all = qkv[:, qs + ks:qs + 2 * ks].view(T, n_kv_heads, head_dim)
+        if kv0 is not None:
+            k0_all = kv0[:, :ks].reshape(-1, n_kv_heads, head_dim)
+            v0_all = kv0[:, ks:2 * ks].reshape(-1, n_kv_heads, head_dim)
+        else:
+            k0_all, v0_all = k_all, v_all
         out = torch.empty(T, qs, dtype=qkv.dtype, device=qkv.device)
         rep = n_q_heads // n_kv_heads
         scale = head_dim ** -0.5
         dev = qkv.device
         for sg in segments:
             q = self._c(q_all[sg.q_start:sg.q_start + sg.q_len])                # [q, nh, d]
-            kr = [(sg.r0_start, sg.r0_len, sg.r0_causal)]
+            kr = [(sg.r0_start, sg.r0_len, sg.r0_causal, k0_all, v0_all)]
             if sg.r1_len:
-                kr.append((sg.r1_start, sg.r1_len, 1))
+                kr.append((sg.r1_start, sg.r1_len, 1, k_all, v_all))
             ks_, vs_, masks = [], [], []
             qi = torch.arange(sg.q_len, device=dev)
-            for st, ln, causal in kr:
-                ks_.append(k_all[st:st + ln])
-                vs_.append(v_all[st:st + ln])
+            for st, ln, causal, kk, vv in kr:
+                ks_.append(kk[st:st + ln])
+                vs_.append(vv[st:st + ln])
                 kj = torch.arange(ln, device=dev)
                 m = torch.ones(sg.q_len, ln, dtype=torch.bool, device=dev)
                 if causal:

@@ -101,6 +101,13 @@ class Comm:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
+    def all_reduce_min(self, x: float) -> float:
+        if not self.active:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=self.device if self.backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return float(t.item())
+
     def all_reduce_sum(self, x: float) -> float:
         if not self.active:
             return x

@@ -175,4 +175,6 @@ def build_dp_sharded_runner(args, cfg, device, comm: Comm, tok, store: Optional[
                          resume_dir=getattr(args, "resume_dir", None),
                          checkpoint_every=getattr(args, "checkpoint_every", 0),
                          max_token_len=getattr(args, "max_token_len", None) or MAX_TOKEN_LEN,
-                         hip_graphs=getattr(args, "hip_graphs", False))
+                         hip_graphs=getattr(args, "hip_graphs", False),
+                         prefix_kv_cache=getattr(args, "prefix_kv_cache", False),
+                         prefix_cache_entries=getattr(args, "prefix_cache_entries", 8))

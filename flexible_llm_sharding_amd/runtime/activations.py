@@ -222,16 +222,22 @@ class ActivationStore:
         else:
             host = e.host
         nbytes = int(np.prod(e.shape)) * torch.empty((), dtype=e.dtype).element_size()
-        out = torch.empty(e.shape, dtype=e.dtype, device=self.dev)
+        cur = torch.cuda.current_stream(self.dev)
         if e.event is not None:
             self.h2d.wait_event(e.event)     # D2H finished before reading the host copy back
         with torch.cuda.stream(self.h2d):
+            # Allocate ON the H2D stream: a block from the compute stream's pool may
+            # still be in use by compute kernels queued before its Python-side free,
+            # and this copy does not wait for them (it overlaps the previous
+            # micro-batch's compute).  record_stream below keeps the block from being
+            # reused until the compute stream's consumers are done.
+            out = torch.empty(e.shape, dtype=e.dtype, device=self.dev)
             out.copy_(host[:nbytes].view(e.dtype).view(e.shape), non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(self.h2d)
         self.bytes_h2d += nbytes
-        torch.cuda.current_stream(self.dev).wait_event(ev)
-        out.record_stream(torch.cuda.current_stream(self.dev))
+        cur.wait_event(ev)
+        out.record_stream(cur)
         if pop:
             # host buffer is reusable once the H2D has completed (checked lazily)
             with self.lock:

@@ -21,7 +21,7 @@ causal mask they cannot influence it.
 from __future__ import annotations
 
 from dataclasses import dataclass, field
-from typing import List, Sequence
+from typing import List, Optional, Sequence
 
 import numpy as np
 import torch
@@ -55,6 +55,9 @@ class PackedBatch:
     num_tokens: int
     padded_tokens: int                    # reference-equivalent token count
     max_pos: int
+    kv_cached: bool = False               # prefixes come from a PrefixEntry (range 0 rows index it)
+    pfx_src: Optional[np.ndarray] = None  # capture: packed rows of every prefix token ...
+    pfx_dst: Optional[np.ndarray] = None  # ... and their rows in the prefix K/V cache
     _dev: dict = field(default_factory=dict, repr=False)
 
     @property
@@ -73,25 +76,45 @@ class PackedBatch:
                 "work": torch.from_numpy(self.work).to(d, non_blocking=nb),
                 "last_idx": torch.from_numpy(self.last_idx).to(d, non_blocking=nb),
             }
+            if self.pfx_src is not None:
+                self._dev[key]["pfx_src"] = torch.from_numpy(self.pfx_src).to(d, non_blocking=nb)
+                self._dev[key]["pfx_dst"] = torch.from_numpy(self.pfx_dst).to(d, non_blocking=nb)
         return self._dev[key]
 
 
 def pack_prompts(tps: Sequence[TokenizedPrompt], prompt_ids: Sequence[int],
-                 prefix_attention: str = "bidirectional") -> PackedBatch:
+                 prefix_attention: str = "bidirectional", prefix_offsets: Optional[Sequence[int]] = None,
+                 kv_cached: bool = False) -> PackedBatch:
+    """Pack prompts into one token matrix + attention work items.
+
+    ``prefix_offsets`` (rows of each prompt's prefix in a PrefixEntry) turns on
+    prefix K/V reuse: with ``kv_cached`` the prefixes are NOT packed (only the
+    suffix tokens are computed; range 0 of each suffix item indexes the cache),
+    otherwise the batch records which packed rows to copy into the cache.
+    """
     if prefix_attention not in ("bidirectional", "causal"):
         raise ValueError(prefix_attention)
+    if kv_cached and prefix_offsets is None:
+        raise ValueError("kv_cached needs prefix_offsets")
     pcausal = 1 if prefix_attention == "causal" else 0
     ids, pos, segs, last, nsuf = [], [], [], [], []
+    src, dst = [], []
     t = 0
     padded = 0
     max_pos = 0
-    for tp in tps:
+    for j, tp in enumerate(tps):
         Lp = len(tp.prefix)
-        p0 = t
-        ids.extend(tp.prefix)
-        pos.extend(range(Lp))
-        segs.append(Segment(p0, Lp, p0, Lp, pcausal, 0, 0))
-        t += Lp
+        if kv_cached:
+            p0 = prefix_offsets[j]
+        else:
+            p0 = t
+            ids.extend(tp.prefix)
+            pos.extend(range(Lp))
+            segs.append(Segment(p0, Lp, p0, Lp, pcausal, 0, 0))
+            if prefix_offsets is not None:
+                src.extend(range(t, t + Lp))
+                dst.extend(range(prefix_offsets[j], prefix_offsets[j] + Lp))
+            t += Lp
         for s in tp.suffixes:
             n = len(s)
             s0 = t
@@ -113,16 +136,19 @@ def pack_prompts(tps: Sequence[TokenizedPrompt], prompt_ids: Sequence[int],
         ids=np.asarray(ids, dtype=np.int32), positions=np.asarray(pos, dtype=np.int32),
         segments=segs, work=np.asarray(work, dtype=np.int32).reshape(-1, WORK_ITEM_FIELDS),
         last_idx=np.asarray(last, dtype=np.int32), num_tokens=t, padded_tokens=padded,
-        max_pos=max_pos)
+        max_pos=max_pos, kv_cached=kv_cached,
+        pfx_src=np.asarray(src, dtype=np.int64) if (prefix_offsets is not None and not kv_cached) else None,
+        pfx_dst=np.asarray(dst, dtype=np.int64) if (prefix_offsets is not None and not kv_cached) else None)
 
 
 def split_microbatches(tps: Sequence[TokenizedPrompt], token_budget: int,
-                       max_prompts: int = 0) -> List[List[int]]:
+                       max_prompts: int = 0, suffix_only: bool = False) -> List[List[int]]:
     """Group consecutive prompts so each micro-batch holds <= token_budget tokens
-    (a single oversized prompt still forms its own micro-batch)."""
+    (a single oversized prompt still forms its own micro-batch).  ``suffix_only``
+    counts only suffix tokens (prefixes served from the prefix K/V cache)."""
     groups, cur, cur_t = [], [], 0
     for i, tp in enumerate(tps):
-        n = tp.num_tokens
+        n = tp.num_tokens - (len(tp.prefix) if suffix_only else 0)
         if cur and (cur_t + n > token_budget or (max_prompts and len(cur) >= max_prompts)):
             groups.append(cur)
             cur, cur_t = [], 0

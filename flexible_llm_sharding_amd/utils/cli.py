@@ -45,6 +45,11 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--hip_graphs", type=str2bool, nargs="?", const=True, default=False,
                    help="with --resident: capture each micro-batch's whole forward as one HIP graph and "
                         "replay it (shape-bucketed; removes per-op host dispatch for small batches)")
+    p.add_argument("--prefix_kv_cache", type=str2bool, nargs="?", const=True, default=False,
+                   help="keep every prompt's prefix K/V per layer in HBM and reuse it in later calls on the same "
+                        "prefixes (each --num_gen_token step then computes only the suffix tokens; exact)")
+    p.add_argument("--prefix_cache_entries", type=int, default=8,
+                   help="prefix K/V cache: calls (prompt batches) kept, LRU")
     p.add_argument("--resident", type=str2bool, nargs="?", const=True, default=False,
                    help="keep every shard resident in HBM after first load (288 GB fits 70B)")
     p.add_argument("--weight_cache", choices=["host", "disk", "packed"], default="host",

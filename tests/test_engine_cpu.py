@@ -210,3 +210,55 @@ def test_unsupported_configs_rejected():
                 {"hidden_size": 256, "num_attention_heads": 4, "head_dim": 128}):
         with pytest.raises(NotImplementedError):
             ModelConfig.from_dict(bad)
+
+
+@pytest.mark.parametrize("num_batch_calls", [1, 2])
+def test_prefix_kv_cache_generation_exact(tiny_model, num_batch_calls):
+    """--prefix_kv_cache: later calls on the same prefixes compute only suffix tokens, same scores."""
+    from flexible_llm_sharding_amd.api import generation_loop
+    from flexible_llm_sharding_amd.engine import ShardedRunner
+    from flexible_llm_sharding_amd.parallel.comm import Comm
+    from flexible_llm_sharding_amd.runtime.weights import HostStore
+    from flexible_llm_sharding_amd.utils.synthetic import synthetic_prompts
+    from flexible_llm_sharding_amd.utils.tokenizer import load_tokenizer
+    import argparse
+    path, cfg = tiny_model
+    tok = load_tokenizer(path)
+    prompts = synthetic_prompts(5, 60, 3, 6, cfg.vocab_size, seed=21, vary=True)
+    src = HostStore.from_model_path(cfg, path, pinned=False)
+    args = argparse.Namespace(num_gen_token=3, data_parallel=False, num_batch=num_batch_calls)
+    plain = ShardedRunner(cfg, src, "cpu", tok, layer_num_per_shard=2, token_budget=150)
+    cached = ShardedRunner(cfg, src, "cpu", tok, layer_num_per_shard=2, token_budget=150, prefix_kv_cache=True)
+    s0, u0 = generation_loop(args, plain, Comm(), tok, prompts)
+    s1, u1 = generation_loop(args, cached, Comm(), tok, prompts)
+    assert u0 == u1
+    for a, b in zip(s0, s1):
+        assert a.shape == b.shape
+        assert np.abs(a.astype(np.float32) - b.astype(np.float32)).max() < 1e-5
+    pc = cached.prefix_cache
+    assert pc.misses == num_batch_calls and pc.hits == 2 * num_batch_calls
+    assert cached.stats["prefix_cached"] == 1.0
+    # the cached pass computed only the suffix tokens of the last call's prompts
+    from flexible_llm_sharding_amd.api import batch_ranges
+    b0, b1 = batch_ranges(len(prompts), num_batch_calls)[-1]
+    n_prefix = sum(len(tp.prefix) for tp in plain.tokenize(prompts[b0:b1]))
+    assert cached.stats["tokens"] == plain.stats["tokens"] - n_prefix
+
+
+def test_prefix_cache_invalidated_by_new_prefix(tiny_model):
+    from flexible_llm_sharding_amd.engine import ShardedRunner
+    from flexible_llm_sharding_amd.runtime.weights import HostStore
+    from flexible_llm_sharding_amd.utils.synthetic import synthetic_prompts
+    from flexible_llm_sharding_amd.utils.tokenizer import load_tokenizer
+    path, cfg = tiny_model
+    tok = load_tokenizer(path)
+    src = HostStore.from_model_path(cfg, path, pinned=False)
+    r = ShardedRunner(cfg, src, "cpu", tok, prefix_kv_cache=True)
+    ref = ShardedRunner(cfg, src, "cpu", tok)
+    p1 = synthetic_prompts(2, 30, 2, 4, cfg.vocab_size, seed=1)
+    p2 = synthetic_prompts(2, 30, 2, 4, cfg.vocab_size, seed=2)
+    for ps in (p1, p2, p1):
+        out = r(ps)
+        for a, b in zip(out, ref(ps)):
+            assert np.abs(a.astype(np.float32) - b.astype(np.float32)).max() < 1e-5
+    assert r.prefix_cache.hits == 1 and r.prefix_cache.misses == 2

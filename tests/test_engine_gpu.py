@@ -98,3 +98,50 @@ def test_hip_graph_replay_matches_eager(setup):
         assert np.abs(o.astype(np.float32) - rf).max() < 2e-3
     eager.close()
     g.close()
+
+
+def test_prefix_kv_cache_on_gpu(setup):
+    """Second call on the same prefixes: suffix tokens only, prefix K/V read from the HBM cache."""
+    path, cfg, tok, prompts, ref = setup
+    src = HostStore.from_model_path(cfg, path)
+    r = ShardedRunner(cfg, src, "cuda:0", tok, layer_num_per_shard=2, storage_location="cpu", token_budget=200,
+                      prefix_kv_cache=True)
+    a = r(prompts)
+    full_tokens = r.stats["tokens"]
+    b = r(prompts)
+    assert r.stats["prefix_cached"] == 1.0 and r.stats["tokens"] < full_tokens
+    for x, y, rf in zip(a, b, ref):
+        assert np.abs(x.astype(np.float32) - y.astype(np.float32)).max() < 1e-3
+        assert np.abs(y.astype(np.float32) - rf).max() < 2e-3
+    r.close()
+
+
+@pytest.fixture(scope="module")
+def mid_model():
+    """Llama-2-7B shapes, 4 layers, random-init in pinned host memory (large enough for copies to race compute)."""
+    from flexible_llm_sharding_amd.config import preset
+    from flexible_llm_sharding_amd.utils.tokenizer import write_synthetic_tokenizer
+    import tempfile
+    cfg = preset("llama2-7b", num_hidden_layers=4)
+    store = HostStore.synthetic(cfg, torch.device("cuda", 0), seed=3)
+    d = tempfile.mkdtemp(prefix="fls_tok_")
+    write_synthetic_tokenizer(d, cfg.vocab_size)
+    prompts = synthetic_prompts(12, 1024, 5, 64, cfg.vocab_size, seed=4)
+    return cfg, store, load_tokenizer(d), prompts
+
+
+@pytest.mark.parametrize("storage", ["cpu", "disk"])
+def test_activation_store_no_race_large_batches(mid_model, tmp_path, storage):
+    """storage cpu/disk (async D2H/H2D overlapping compute, >= 3 micro-batches) must equal storage gpu bitwise."""
+    cfg, store, tok, prompts = mid_model
+    ref = ShardedRunner(cfg, store, "cuda:0", tok, layer_num_per_shard=1, storage_location="gpu", token_budget=4096)
+    want = ref(prompts)
+    ref.close()
+    r = ShardedRunner(cfg, store, "cuda:0", tok, layer_num_per_shard=1, storage_location=storage,
+                      disk_folder=str(tmp_path / "spill"), token_budget=4096)
+    got = r(prompts)
+    assert r.stats["micro_batches"] >= 3 and r.stats["act_h2d_bytes"] > 0
+    for a, b in zip(want, got):
+        assert np.isfinite(a.astype(np.float32)).all()
+        assert np.array_equal(a, b)
+    r.close()

@@ -1,6 +1,7 @@
 """HIP kernel numerics vs plain-PyTorch fp32 references (run on an MI355X)."""
 import math
 
+import numpy as np
 import pytest
 import torch
 
@@ -130,6 +131,33 @@ def test_attention_shared_prefix(ops, ref, attn_variant, nh, nkv, hd, mode):
     meta = b.device_tensors(DEV)
     y = ops.attention(qkv.to(DEV), meta["work"], nh, nkv, hd)
     r = ref.attention(qkv.float(), b.segments, nh, nkv, hd)
+    torch.cuda.synchronize()
+    assert rel_err(y.cpu(), r) < 5e-3
+
+
+@pytest.mark.parametrize("nh,nkv,hd", [(8, 1, 128), (2, 2, 128), (4, 2, 64)])
+def test_attention_prefix_from_cache(ops, ref, attn_variant, nh, nkv, hd):
+    """Range 0 read from a separate prefix K/V tensor (prefix cache) == the full packed pass."""
+    from flexible_llm_sharding_amd.runtime.batch import pack_prompts
+    from flexible_llm_sharding_amd.utils.tokenizer import TokenizedPrompt
+    prompts = [(70, [5, 64, 1]), (130, [65, 17]), (9, [3, 40])]
+    tps = [TokenizedPrompt(list(range(lp)), [list(range(l)) for l in ls], max(ls), [l - 1 for l in ls])
+           for lp, ls in prompts]
+    offs, t = [], 0
+    for lp, _ in prompts:
+        offs.append(t)
+        t += lp
+    full = pack_prompts(tps, [0, 1, 2], "bidirectional", prefix_offsets=offs)
+    g = torch.Generator().manual_seed(5)
+    qkv = torch.randn(full.num_tokens, (nh + 2 * nkv) * hd, generator=g).half()
+    qs, kv = nh * hd, 2 * nkv * hd
+    cache = torch.zeros(t, kv, dtype=torch.float16)
+    cache[torch.from_numpy(full.pfx_dst)] = qkv[torch.from_numpy(full.pfx_src), qs:qs + kv]
+    cached = pack_prompts(tps, [0, 1, 2], "bidirectional", prefix_offsets=offs, kv_cached=True)
+    keep = np.setdiff1d(np.arange(full.num_tokens), full.pfx_src)       # suffix rows, in packed order
+    qkv_s = qkv[torch.from_numpy(keep)].contiguous()
+    y = ops.attention(qkv_s.to(DEV), cached.device_tensors(DEV)["work"], nh, nkv, hd, kv0=cache.to(DEV))
+    r = ref.attention(qkv.float(), full.segments, nh, nkv, hd)[torch.from_numpy(keep)]
     torch.cuda.synchronize()
     assert rel_err(y.cpu(), r) < 5e-3
 
