@@ -131,6 +131,10 @@ def main(argv=None):
     sync()
     comm.barrier()
     elapsed = time.perf_counter() - t_start
+    if not a.cpu:
+        ms_ = torch.cuda.memory_stats(dev)
+        log(rank, f"[bench] allocator: device mallocs {ms_.get('num_device_alloc')}, "
+                  f"retries {ms_.get('num_alloc_retries')}, reserved {ms_.get('reserved_bytes.all.peak', 0) / 1e9:.2f} GB")
     elapsed = comm.all_reduce_max(elapsed)
 
     tok_step = runner.stats["tokens"]
@@ -139,6 +143,7 @@ def main(argv=None):
         tok_step = comm.all_reduce_sum(tok_step)
         padded_step = comm.all_reduce_sum(padded_step)
     peak = comm.all_reduce_max(0.0 if a.cpu else float(torch.cuda.max_memory_allocated(dev)))
+    peak_res = comm.all_reduce_max(0.0 if a.cpu else float(torch.cuda.max_memory_reserved(dev)))
     # every score this rank produced must be a finite probability (guards the timed path's numerics)
     import numpy as np
     finite = all(np.isfinite(o.astype(np.float32)).all() for o in (outs or []) if o is not None)
@@ -150,7 +155,8 @@ def main(argv=None):
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms, 2), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "fp32-cpu-rehearsal" if a.cpu else "fp16",
         "data": "synthetic prompts (synthetic tokenizer) + random-init Llama-2-70B weights in pinned host RAM",
-        "peak_gpu_mem_gb": round(peak / 1e9, 3), "scores_finite": finite,
+        "peak_gpu_mem_gb": round(peak / 1e9, 3), "peak_gpu_reserved_gb": round(peak_res / 1e9, 3),
+        "scores_finite": finite,
         "config": {"model": a.model if a.num_layers is None else f"{a.model}-L{a.num_layers}",
                    "global_batch": n_prompts * (world if dp else 1),
                    "seq_len": a.prefix_len + a.suffix_len,

@@ -231,6 +231,7 @@ class ShardedRunner:
                 store.put(b, t.to(self.dev))
             items = [it for it in items if it[0] >= k0]
         carry = {}                     # micro-batch -> device activation kept across a shard boundary
+        shard_ev: List = []            # end-of-shard events on the compute stream (host run-ahead bound)
         recvs = {}
         recv_src = None
         recv_next = 0
@@ -250,6 +251,7 @@ class ShardedRunner:
                 if cur_k >= 0:
                     pf.release(cur_k)
                     sends = [(t, w) for (t, w) in sends if not w.is_completed()]   # bound memory
+                    self._throttle(shard_ev)
                 with trace.range(f"shard{k}:acquire"):
                     W = pf.acquire(k)
                 with trace.range(f"shard{k + 1}:prefetch"):
@@ -345,6 +347,9 @@ class ShardedRunner:
             "weight_wait_s": pf.wait_seconds, "weight_h2d_bytes": float(pf.bytes_h2d - h2d0),
             "act_d2h_bytes": float(store.bytes_d2h), "act_h2d_bytes": float(store.bytes_h2d),
             "resumed_from_shard": float(k0),
+            # GPU-side: compute stream stalled on the weight / activation copy streams
+            "weight_stall_gpu_s": pf.take_stall_seconds() if self.cuda else 0.0,
+            "act_stall_gpu_s": store.take_stall_seconds() if self.cuda else 0.0,
         }
         if self.verbose:
             # utils.py:304 prints "loaded N layers in Ts" per device
@@ -353,6 +358,24 @@ class ShardedRunner:
                   f"(exposed weight wait); {len(self.my_shards)} shards, {len(batches)} micro-batches, "
                   f"{self.stats['tokens']:.0f} tokens in {wall:.2f}s")
         return outputs
+
+    def _throttle(self, shard_ev: List) -> None:
+        """Bound how far the host runs ahead of the GPU to ``RUNAHEAD_SHARDS`` shards.
+
+        Nothing else stops Python from queueing the whole pass: every activation
+        buffer that crosses streams (H2D landing buffers, D2H sources) is then
+        held by the caching allocator until the GPU catches up, which costs a
+        hipMalloc per micro-batch and tens of GB of reserved HBM.  Two shards of
+        queued work are far more than the copy streams need to overlap."""
+        if not self.cuda:
+            return
+        e = torch.cuda.Event()
+        e.record(torch.cuda.current_stream(self.dev))
+        shard_ev.append(e)
+        while len(shard_ev) > self.RUNAHEAD_SHARDS:
+            shard_ev.pop(0).synchronize()
+
+    RUNAHEAD_SHARDS = 2
 
     # ------------------------------------------------------ HIP graphs
     def _forward_all(self, meta: dict, batch: PackedBatch) -> torch.Tensor:

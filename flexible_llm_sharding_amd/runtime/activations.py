@@ -74,6 +74,7 @@ class ActivationStore:
         self._recycle: List[Tuple[torch.Tensor, torch.cuda.Event]] = []
         self.bytes_d2h = 0
         self.bytes_h2d = 0
+        self._stall_ev: List[Tuple[torch.cuda.Event, torch.cuda.Event]] = []   # compute-stream waits on H2D
         self.lock = threading.Lock()
 
     # ------------------------------------------------------------- pool
@@ -236,7 +237,11 @@ class ActivationStore:
             ev = torch.cuda.Event()
             ev.record(self.h2d)
         self.bytes_h2d += nbytes
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(cur)
         cur.wait_event(ev)
+        e1.record(cur)
+        self._stall_ev.append((e0, e1))
         out.record_stream(cur)
         if pop:
             # host buffer is reusable once the H2D has completed (checked lazily)
@@ -248,6 +253,13 @@ class ActivationStore:
                 except OSError:
                     pass
         return out
+
+    def take_stall_seconds(self) -> float:
+        """GPU time the compute stream spent waiting for activation H2D since the last call
+        (events must have completed: call after a synchronize)."""
+        t = sum(a.elapsed_time(b) for a, b in self._stall_ev) / 1e3
+        self._stall_ev = []
+        return t
 
     def _drop(self, e: _Entry) -> None:
         if e.write_fut is not None:

@@ -65,6 +65,7 @@ class ShardPrefetcher:
         # stats
         self.bytes_h2d = 0
         self.wait_seconds = 0.0
+        self._stall_ev: List[Tuple[torch.cuda.Event, torch.cuda.Event]] = []
         self.load_seconds = 0.0
         self.lock = threading.Lock()
 
@@ -168,11 +169,23 @@ class ShardPrefetcher:
             for w in ev:
                 w.wait()
         elif ev is not None:
-            torch.cuda.current_stream(self.dev).wait_event(ev)
+            cur = torch.cuda.current_stream(self.dev)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(cur)
+            cur.wait_event(ev)
+            e1.record(cur)
+            self._stall_ev.append((e0, e1))
         if self.resident:
             self._loaded_resident.add(k)
         self.wait_seconds += time.perf_counter() - t0
         return views
+
+    def take_stall_seconds(self) -> float:
+        """GPU time the compute stream spent waiting for weight H2D since the last call
+        (after a synchronize)."""
+        t = sum(a.elapsed_time(b) for a, b in self._stall_ev) / 1e3
+        self._stall_ev = []
+        return t
 
     def release(self, k: int) -> None:
         if self.resident:
