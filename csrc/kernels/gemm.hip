@@ -304,6 +304,118 @@ __global__ __launch_bounds__(256) void gemm_nt_generic(const half_t* __restrict_
   }
 }
 
+// ------------------------------------------------------------------ mid-M
+// For small / medium M (a few prompts, generation steps, LM heads with > 16
+// scored rows) the 256x256 tiles leave most of the 256 CUs idle (7B QKV at
+// M = 416: 96 blocks).  gemm_nt_mid uses 64 (M) x 128 (N) x 64 tiles: 4 waves
+// in a 2 x 2 grid, each 32 x 64 outputs (2 x 4 MFMA 16x16x32 tiles, 32 fp32
+// accumulators), operands staged by LDS-DMA (16 B per lane, XOR chunk swizzle
+// on the source address) into a 3-deep ring with one counted vmcnt + raw
+// barrier per K-tile; XCD-aware order puts every M tile of one N tile on the
+// same XCD so each weight tile comes from HBM once and from L2 after that.
+// Same C^T fragment orientation and epilogues as the main kernels.
+namespace mid {
+constexpr int BMm = 64, BNm = 128, BKm = 64, NTm = 256, NSTAGE = 3;
+constexpr int STAGE = (BMm + BNm) * BKm * 2;     // 24 KiB: A rows 0..63 then W rows 0..127
+constexpr int GROUPS = (BMm + BNm) / 8;          // 8-row (1 KiB) LDS-DMA groups per stage
+constexpr int PER_WAVE = GROUPS / 4;             // 6 LDS-DMA per wave per stage
+}  // namespace mid
+
+template <int EPI>
+__global__ __launch_bounds__(mid::NTm) void gemm_nt_mid(const half_t* __restrict__ A, const half_t* __restrict__ W,
+                                                     half_t* __restrict__ C, int M, int N, int K, int lda, int ldw,
+                                                     int ldc, Epi ep) {
+  using namespace mid;
+  extern __shared__ __attribute__((aligned(16))) char lds_mid[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fr = lane & 15, grp = lane >> 4;
+  const int mt = (M + BMm - 1) / BMm, ntn = N / BNm;
+  // XCD-aware bijective remap: logical tiles [xcd*q .. ) run on one XCD, M fastest
+  int bid = blockIdx.x;
+  {
+    const int nwg = mt * ntn;
+    const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7, loc = bid >> 3;
+    if (nwg >= 8) bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+  }
+  const int m0 = (bid % mt) * BMm;
+  const int n0 = (bid / mt) * BNm;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nk = K / BKm;
+
+  // this lane's LDS-DMA sources: group g = wave + 4*i covers tile rows 8*g .. 8*g+7
+  const half_t* src[PER_WAVE];
+  const int sub = lane >> 3;                       // row inside the 8-row group
+  const int kc = ((lane & 7) ^ sub) * 8;           // source chunk pre-swizzled (read XORs it back)
+#pragma unroll
+  for (int i = 0; i < PER_WAVE; ++i) {
+    const int g = wave + 4 * i;
+    if (g < BMm / 8) {
+      const int m = min(m0 + g * 8 + sub, M - 1);
+      src[i] = A + (size_t)m * lda + kc;
+    } else {
+      const int n = n0 + (g - BMm / 8) * 8 + sub;
+      src[i] = W + (size_t)n * ldw + kc;
+    }
+  }
+  auto stage = [&](int kt) {
+    char* base = lds_mid + (kt % NSTAGE) * STAGE;
+#pragma unroll
+    for (int i = 0; i < PER_WAVE; ++i) glds16(src[i] + (size_t)kt * BKm, base + (wave + 4 * i) * 1024);
+  };
+
+  floatx4 acc[2][4];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[u][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  stage(0);
+  if (nk > 1) stage(1);
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 2 < nk) {
+      stage(kt + 2);
+      asm volatile("s_waitcnt vmcnt(12)" ::: "memory");   // tiles kt+1, kt+2 stay in flight
+    } else if (kt + 1 < nk) {
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();                          // every wave's part of tile kt landed
+    const char* Xs = lds_mid + (kt % NSTAGE) * STAGE;
+    const char* Ws = Xs + BMm * BKm * 2;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int c = ks * 4 + grp;                          // logical 16-byte chunk of this lane
+      half8 xf[2], wf[4];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int r = wm * 32 + u * 16 + fr;
+        xf[u] = *(const half8*)(Xs + r * 128 + ((c ^ (r & 7)) << 4));
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int r = wn * 64 + t * 16 + fr;
+        wf[t] = *(const half8*)(Ws + r * 128 + ((c ^ (r & 7)) << 4));
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[u][t] = mfma16x16x32(wf[t], xf[u], acc[u][t]);
+    }
+    // WAR: stage(kt + 3) (next iteration) overwrites this buffer; all reads are done
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int m = m0 + wm * 32 + u * 16 + fr;
+    if (m >= M) continue;
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+      store_pair<EPI>(C, ldc, m, n0 + wn * 64 + p * 32, grp, acc[u][2 * p], acc[u][2 * p + 1], ep);
+  }
+}
+
 // ------------------------------------------------------------------ v3
 // Ping-pong: the 8 waves form two groups (waves 0-3 / 4-7; the hardware puts
 // one wave of each group on every SIMD).  Group 1 runs one barrier-slot
@@ -1979,9 +2091,38 @@ int variant() {
   return g_variant;
 }
 
+int g_mid = -1;   // mid-M kernel: -1 = from FLS_GEMM_MID (default on), 0 = off, 1 = on
+
+bool mid_enabled() {
+  if (g_mid < 0) {
+    const char* e = getenv("FLS_GEMM_MID");
+    g_mid = e ? (atoi(e) != 0) : 1;
+  }
+  return g_mid != 0;
+}
+
 template <int EPI>
 int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int lda, int ldw, int ldc,
            const Epi& ep, hipStream_t s) {
+  // Too few 256x256 tiles for 256 CUs -> 64x128 tiles.  Measured crossover
+  // (profiles/r1_gemm_mid): the mid kernel wins below ~128 main tiles, and at
+  // M <= 64 (3/4 of every 256-row tile wasted) up to 512; above that its lower
+  // L2 reuse (43 vs 128 FLOP per staged byte) costs more than the idle CUs.
+  const size_t tiles256 = (size_t)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  if (mid_enabled() && N % mid::BNm == 0 && K % mid::BKm == 0 && lda % 8 == 0 && ldw % 8 == 0 &&
+      (tiles256 < 128 || (M <= 64 && tiles256 < 512))) {
+    static bool attr_mid = false;
+    if (!attr_mid) {
+      (void)hipFuncSetAttribute((const void*)gemm_nt_mid<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                mid::NSTAGE * mid::STAGE);
+      attr_mid = true;
+    }
+    const int blocks = ((M + mid::BMm - 1) / mid::BMm) * (N / mid::BNm);
+    hipLaunchKernelGGL(gemm_nt_mid<EPI>, dim3(blocks), dim3(mid::NTm), mid::NSTAGE * mid::STAGE, s, A, W, C, M, N,
+                       K, lda, ldw, ldc, ep);
+    FLS_CHECK_LAUNCH();
+    return 0;
+  }
   int var = variant();
   const bool fast = (N % BN == 0) && (K % BK == 0) && (lda % 8 == 0) && (ldw % 8 == 0) && M > 0;
   // v8/v9 need an even K-tile count (2-tile unrolled body), v9 32-bit X offsets; else v3
@@ -2081,6 +2222,12 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
 }  // namespace
 
 extern "C" int fls_kernels_version(void) { return 5; }
+
+// A/B switch for the mid-M kernel (tests / microbenchmarks)
+extern "C" int fls_gemm_set_mid(int on) {
+  g_mid = on ? 1 : 0;
+  return 0;
+}
 
 // microbenchmark-only entry: v1 main loop with parts removed (results are garbage)
 extern "C" int fls_gemm_ablate(int abl, const void* A, const void* W, void* C, int M, int N, int K,

@@ -260,6 +260,44 @@ def test_gemm_autotune_choice():
     assert rel_err(y, x.float() @ w.float().t()) < 2e-3
 
 
+@pytest.mark.parametrize("M", [1, 17, 64, 100, 416, 517, 1000])
+def test_gemm_mid_all_epilogues(ops, ref, M):
+    """64x128-tile mid-M kernel (chosen when 256x256 tiles cannot fill the chip) vs fp32 references."""
+    from flexible_llm_sharding_amd.config import ModelConfig
+    from flexible_llm_sharding_amd.models.llama import rope_tables
+    H, I, nh, nkv, hd = 512, 768, 4, 2, 128
+    x = rnd(M, H, seed=41)
+    w = rnd(H, H, scale=0.05, seed=42)
+    assert rel_err(ops.gemm(x, w), x.float() @ w.float().t()) < 2e-3
+    r0 = rnd(M, H, seed=43)
+    out = ops.gemm(x, w, EPI_RESID, out=r0.clone(), resid=r0.clone())
+    assert rel_err(out, r0.float() + x.float() @ w.float().t()) < 2e-3
+    wgu = rnd(2 * I, H, scale=0.05, seed=44)
+    assert rel_err(ops.gemm(x, wgu, EPI_SWIGLU).cpu(), ref.swiglu_up(x.float().cpu(), wgu.float().cpu())) < 3e-3
+    wqkv = rnd((nh + 2 * nkv) * hd, H, scale=0.05, seed=45)
+    pos = torch.randint(0, 4000, (M,), dtype=torch.int32, device=DEV)
+    cfg = ModelConfig(hidden_size=nh * hd, num_attention_heads=nh, num_key_value_heads=nkv)
+    cos, sin = rope_tables(cfg, 4096)
+    y = ops.gemm(x, wqkv, EPI_ROPE, positions=pos, cos=cos.to(DEV), sin=sin.to(DEV),
+                 rope_cols=(nh + nkv) * hd, head_dim=hd)
+    r = ref.qkv_rope(x.float().cpu(), wqkv.float().cpu(), pos.cpu(), cos, sin, nh, nkv, hd)
+    assert rel_err(y.cpu(), r) < 3e-3
+    # bias epilogue (Qwen2) and exactness of the fragment orientation
+    b = rnd(H, scale=0.5, seed=46)
+    yb = ops.gemm(x, w, bias=b)
+    assert rel_err(yb, x.float() @ w.float().t() + b.float()) < 2e-3
+    torch.cuda.synchronize()
+
+
+def test_gemm_mid_asymmetric_exact(ops):
+    M, N, K = 100, 256, 128
+    x = torch.eye(M, K, dtype=torch.float16, device=DEV)
+    w = (torch.arange(N * K, device=DEV).reshape(N, K) % 17).to(torch.float16)
+    y = ops.gemm(x, w)
+    torch.cuda.synchronize()
+    assert torch.equal(y, w.t().contiguous()[:M])
+
+
 @pytest.mark.parametrize("var", [1, 3, 6, 7, 8, 9, 10, 11, 12])
 def test_gemm_variants_all_epilogues(ops, ref, var):
     """Every main-loop variant (v1 8-wave, v3 ping-pong, v6 one-wave-per-SIMD, v7 counted-vmcnt phases)
@@ -268,6 +306,7 @@ def test_gemm_variants_all_epilogues(ops, ref, var):
     from flexible_llm_sharding_amd.models.llama import rope_tables
     M, H, I, nh, nkv, hd = 517, 512, 768, 4, 2, 128
     ops.k.fls_gemm_set_variant(var)
+    ops.k.fls_gemm_set_mid(0)           # these shapes would otherwise take the 64x128 mid-M kernel
     try:
         x = rnd(M, H, seed=31)
         w = rnd(H, H, scale=0.05, seed=32)
@@ -288,6 +327,7 @@ def test_gemm_variants_all_epilogues(ops, ref, var):
         torch.cuda.synchronize()
     finally:
         ops.k.fls_gemm_set_variant(10)
+        ops.k.fls_gemm_set_mid(1)
 
 
 @pytest.mark.parametrize("M,N,K", [(1, 32000, 1024), (5, 1000, 8192), (16, 33, 96), (7, 100, 160)])
