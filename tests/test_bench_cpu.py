@@ -1,0 +1,54 @@
+"""The driver's bench contract, rehearsed on CPU/gloo: ``bench.py`` under
+``torch.distributed.run`` (one rank per device) prints ONE JSON line on rank 0
+with the whole-job aggregate."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _bench(world, extra, tmp_path):
+    args = ["--gpus", str(world), "--steps", "2", "--warmup", "1", "--cpu", "--model", "tiny",
+            "--prompts-per-gpu", "3", "--prefix-len", "24", "--suffix-len", "4"] + extra
+    if world > 1:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+               "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py")] + args
+    else:
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py")] + args
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("world,mode", [(1, "auto"), (2, "auto"), (2, "mp"), (3, "auto")])
+def test_bench_contract(tmp_path, world, mode):
+    out = _bench(world, ["--mode", mode], tmp_path)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in out
+    assert out["n_gpus"] == world and out["steps"] == 2 and out["warmup"] == 1
+    assert out["scores_finite"] is True and out["value"] > 0
+    tok = out["config"]["tokens_per_step"]
+    # value is the whole-job aggregate: tokens per step (summed over ranks) / seconds per step
+    assert abs(out["value"] - tok / (out["ms_per_step"] / 1e3)) / out["value"] < 0.02
+    if world > 1:
+        want = "pp" if mode == "mp" else "dp"
+        assert out["config"]["parallelism"].startswith(want)
+    # weak scaling: per-rank work fixed, global batch grows with the rank count
+    assert out["config"]["global_batch"] == 3 * world
