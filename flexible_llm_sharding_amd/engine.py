@@ -231,6 +231,7 @@ class ShardedRunner:
                 store.put(b, t.to(self.dev))
             items = [it for it in items if it[0] >= k0]
         carry = {}                     # micro-batch -> device activation kept across a shard boundary
+        pos = {it: i for i, it in enumerate(items)}
         shard_ev: List = []            # end-of-shard events on the compute stream (host run-ahead bound)
         recvs = {}
         recv_src = None
@@ -311,8 +312,10 @@ class ShardedRunner:
             elif dst_rank != comm.rank:
                 st = state.contiguous()
                 sends.append((st, comm.isend(st, dst_rank)))
-            elif nxt is not None and nxt[0] == k + 1 and nxt[1] == b and self.storage != "gpu":
-                carry[b] = state           # boundary micro-batch stays in HBM (zigzag)
+            elif self.storage != "gpu" and pos.get((k + 1, b), len(items)) - idx <= self.CARRY_WINDOW:
+                # re-used within CARRY_WINDOW micro-batch computes (the zigzag boundary micro-batch
+                # and its neighbour): a PCIe round trip would only add traffic, keep it in HBM
+                carry[b] = state
             else:
                 store.put(b, state)
             del state
@@ -376,6 +379,9 @@ class ShardedRunner:
             shard_ev.pop(0).synchronize()
 
     RUNAHEAD_SHARDS = 2
+    # an activation consumed again within this many micro-batch computes stays in HBM
+    # (zigzag: the boundary micro-batch is next, its neighbour 3 computes later)
+    CARRY_WINDOW = 3
 
     # ------------------------------------------------------ HIP graphs
     def _forward_all(self, meta: dict, batch: PackedBatch) -> torch.Tensor:
