@@ -146,7 +146,7 @@ class HostStore(LayerSource):
         st = cls(cfg, torch.float16, pinned, names)
         dev = torch.device(device)
         ops = get_ops(dev)
-        maxb = max(st.nbytes(n) for n in st.names)
+        maxb = max((st.nbytes(n) for n in st.names), default=0)   # an MP rank may own no layers
         stage = torch.empty(maxb, dtype=torch.uint8, device=dev)
         for li, n in enumerate(st.names):
             if progress is not None and li % 10 == 0:
