@@ -31,6 +31,9 @@ class ModelConfig:
     attention_bias: bool = False        # q/k/v projection biases (Qwen2; Llama attention_bias)
     o_proj_bias: bool = False           # o_proj bias (Llama attention_bias=True)
     sliding_window: Optional[int] = None  # Mistral; must cover the token cap (checked by the runner)
+    # RoPE frequency scaling (HF ``rope_scaling`` / v5 ``rope_parameters``): linear, llama3, yarn
+    rope_scaling: Optional[dict] = None
+    explicit_head_dim: Optional[int] = None   # HF ``head_dim`` when != hidden / heads (Mistral-Nemo)
     bos_token_id: int = 1
     eos_token_id: int = 2
     torch_dtype: str = "float16"
@@ -40,7 +43,7 @@ class ModelConfig:
     # ------------------------------------------------------------------ derived
     @property
     def head_dim(self) -> int:
-        return self.hidden_size // self.num_attention_heads
+        return self.explicit_head_dim or self.hidden_size // self.num_attention_heads
 
     @property
     def q_size(self) -> int:
@@ -76,12 +79,20 @@ class ModelConfig:
         return emb + head + self.hidden_size + self.num_hidden_layers * self.decoder_layer_params()
 
     def validate(self) -> None:
-        if self.hidden_size % self.num_attention_heads:
+        if self.explicit_head_dim is None and self.hidden_size % self.num_attention_heads:
             raise ValueError("hidden_size must be divisible by num_attention_heads")
         if self.num_attention_heads % self.num_key_value_heads:
             raise ValueError("num_attention_heads must be a multiple of num_key_value_heads")
         if self.head_dim % 32:
             raise ValueError("head_dim must be a multiple of 32 (RoPE pair blocks of 16)")
+        rs = self.rope_scaling
+        if rs:
+            kind = rs.get("rope_type", rs.get("type"))
+            if kind not in ROPE_SCALING_TYPES:
+                raise NotImplementedError(f"rope_scaling type {kind!r}: supported are {sorted(ROPE_SCALING_TYPES)}"
+                                          " (dynamic NTK depends on each call's length: not supported)")
+            if float(rs.get("factor") or 1.0) <= 0:
+                raise ValueError(f"rope_scaling factor must be > 0: {rs}")
 
     # ---------------------------------------------------------------------- io
     @classmethod
@@ -92,18 +103,24 @@ class ModelConfig:
                 kw[f] = d[f]
         if "num_key_value_heads" not in d or d.get("num_key_value_heads") is None:
             kw["num_key_value_heads"] = d.get("num_attention_heads", cls.num_attention_heads)
-        rs = d.get("rope_scaling")
-        if rs:
-            raise NotImplementedError(f"rope_scaling={rs} is not supported (Llama-2 has none)")
+        rp = d.get("rope_parameters")          # transformers v5 form: {"rope_type", "rope_theta", ...}
+        if isinstance(rp, dict):
+            if "rope_theta" in rp:
+                kw["rope_theta"] = rp["rope_theta"]
+            if rp.get("rope_type", "default") != "default":
+                kw["rope_scaling"] = {k: v for k, v in rp.items() if k != "rope_theta"}
+        rs = kw.get("rope_scaling")
+        if rs and rs.get("rope_type", rs.get("type")) == "default":
+            kw.pop("rope_scaling")
         mt = d.get("model_type", "llama")
         if mt not in SUPPORTED_MODEL_TYPES:
             raise NotImplementedError(f"model_type={mt!r}: supported are {sorted(SUPPORTED_MODEL_TYPES)}")
         if d.get("mlp_bias"):
             raise NotImplementedError("mlp_bias=True is not supported")
         hdim = d.get("head_dim")
-        if hdim is not None and hdim != d.get("hidden_size", cls.hidden_size) // d.get(
-                "num_attention_heads", cls.num_attention_heads):
-            raise NotImplementedError(f"head_dim={hdim} != hidden_size / num_attention_heads")
+        if hdim is not None and hdim * d.get("num_attention_heads", cls.num_attention_heads) != d.get(
+                "hidden_size", cls.hidden_size):
+            kw["explicit_head_dim"] = int(hdim)
         if d.get("hidden_act", "silu") != "silu":
             raise NotImplementedError(f"hidden_act={d.get('hidden_act')!r} (SwiGLU/silu only)")
         if mt == "qwen2":
@@ -132,6 +149,7 @@ class ModelConfig:
     def save(self, model_path: str) -> None:
         os.makedirs(model_path, exist_ok=True)
         d = asdict(self)
+        d["head_dim"] = self.head_dim           # HF key (also read back by from_dict)
         with open(os.path.join(model_path, "config.json"), "w") as f:
             json.dump(d, f, indent=2)
 
@@ -140,6 +158,8 @@ class ModelConfig:
 # q/k/v/o + gate/up/down + two RMSNorms per layer) -- what the reference's AutoModelForCausalLM
 # path (utils.py:101-115) runs in practice.
 SUPPORTED_MODEL_TYPES = {"llama", "mistral", "qwen2"}
+# static RoPE scalings: they only change the cos/sin tables (models/llama.py rope_inv_freq)
+ROPE_SCALING_TYPES = {"linear", "llama3", "yarn"}
 
 # Standard HF configs (computed sizes in SURVEY.md §2.3).
 PRESETS = {
@@ -164,6 +184,12 @@ PRESETS = {
                        num_key_value_heads=2, num_hidden_layers=2, vocab_size=512, rope_theta=1e6,
                        rms_norm_eps=1e-6, attention_bias=True, model_type="qwen2",
                        architectures=["Qwen2ForCausalLM"]),
+    # Llama-3.1 geometry (GQA 8:1, 128k vocab, llama3 RoPE scaling)
+    "llama3.1-8b": dict(hidden_size=4096, intermediate_size=14336, num_attention_heads=32,
+                        num_key_value_heads=8, num_hidden_layers=32, vocab_size=128256, rope_theta=500000.0,
+                        max_position_embeddings=131072, bos_token_id=128000, eos_token_id=128001,
+                        rope_scaling={"rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0,
+                                      "high_freq_factor": 4.0, "original_max_position_embeddings": 8192}),
     "small": dict(hidden_size=1024, intermediate_size=2816, num_attention_heads=8,
                   num_key_value_heads=2, num_hidden_layers=4, vocab_size=32000),
 }

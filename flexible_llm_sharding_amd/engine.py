@@ -87,6 +87,8 @@ class ShardedRunner:
         self.L = len(self.names)
         self.plan: ShardPlan = make_plan(self.L, layer_num_per_shard, self.comm.world, self.comm.rank,
                                          data_parallel)
+        if self.cuda and cfg.head_dim not in (64, 128):
+            raise NotImplementedError(f"head_dim={cfg.head_dim}: the HIP attention kernels serve 64 and 128")
         self.act_dtype = act_dtype or (torch.float16 if self.cuda else torch.float32)
         self.ops = get_ops(self.dev)
         cos, sin = rope_tables(cfg, max(cfg.max_position_embeddings, max_token_len),

@@ -26,6 +26,60 @@ from ..config import ModelConfig, MAX_TOKEN_LEN
 from .layout import layer_kind
 
 
+def rope_inv_freq(cfg: ModelConfig):
+    """-> (inverse frequencies [hd/2] fp32, cos/sin scale) for the config's RoPE.
+
+    Static scalings only change the tables, so the fused RoPE epilogue of the
+    QKV GEMM serves all of them: ``linear`` (positions / factor), ``llama3``
+    (Llama-3.1: long wavelengths / factor, a smooth ramp between) and ``yarn``
+    (NTK-by-parts ramp between interpolated and extrapolated frequencies, cos/sin
+    scaled by the attention factor) — the formulas of HF ``modeling_rope_utils``.
+    """
+    hd = cfg.head_dim
+    base = float(cfg.rope_theta)
+    inv = 1.0 / (base ** (torch.arange(0, hd, 2, dtype=torch.int64).float() / hd))
+    rs = cfg.rope_scaling
+    if not rs:
+        return inv, 1.0
+    kind = rs.get("rope_type", rs.get("type"))
+    factor = float(rs.get("factor") or 1.0)
+    if kind == "linear":
+        return inv / factor, 1.0
+    orig = float(rs.get("original_max_position_embeddings") or cfg.max_position_embeddings)
+    if kind == "llama3":
+        lo_f, hi_f = float(rs.get("low_freq_factor", 1.0)), float(rs.get("high_freq_factor", 4.0))
+        wavelen = 2 * math.pi / inv
+        out = torch.where(wavelen > orig / lo_f, inv / factor, inv)
+        smooth = (orig / wavelen - lo_f) / (hi_f - lo_f)
+        smoothed = (1 - smooth) * out / factor + smooth * out
+        medium = (wavelen >= orig / hi_f) & (wavelen <= orig / lo_f)
+        return torch.where(medium, smoothed, out), 1.0
+    if kind == "yarn":
+        if rs.get("factor") is None:
+            factor = cfg.max_position_embeddings / orig
+
+        def mscale(scale, m=1.0):
+            return 1.0 if scale <= 1 else 0.1 * m * math.log(scale) + 1.0
+        att = rs.get("attention_factor")
+        if att is None:
+            m, m_all = rs.get("mscale"), rs.get("mscale_all_dim")
+            att = (mscale(factor, m) / mscale(factor, m_all)) if (m and m_all) else mscale(factor)
+        beta_fast, beta_slow = float(rs.get("beta_fast") or 32), float(rs.get("beta_slow") or 1)
+
+        def corr_dim(n_rot):
+            return (hd * math.log(orig / (n_rot * 2 * math.pi))) / (2 * math.log(base))
+        lo, hi = corr_dim(beta_fast), corr_dim(beta_slow)
+        if rs.get("truncate", True):
+            lo, hi = math.floor(lo), math.ceil(hi)
+        lo, hi = max(lo, 0), min(hi, hd - 1)
+        if lo == hi:
+            hi += 0.001
+        ramp = ((torch.arange(hd // 2, dtype=torch.float32) - lo) / (hi - lo)).clamp(0, 1)
+        extrap = 1 - ramp
+        return (inv / factor) * (1 - extrap) + inv * extrap, float(att)
+    raise NotImplementedError(f"rope_scaling {rs}")
+
+
 def rope_tables(cfg: ModelConfig, max_pos: int = MAX_TOKEN_LEN, table_dtype=torch.float16,
                 device="cpu"):
     """cos/sin [max_pos, hd/2] in fp32 holding ``table_dtype``-rounded values.
@@ -34,11 +88,10 @@ def rope_tables(cfg: ModelConfig, max_pos: int = MAX_TOKEN_LEN, table_dtype=torc
     casts every buffer to fp16 (``utils.py:118-119``); rotate-half uses
     ``emb = cat(freqs, freqs)`` so only hd/2 distinct frequencies exist.
     """
-    hd = cfg.head_dim
-    inv_freq = 1.0 / (cfg.rope_theta ** (torch.arange(0, hd, 2, dtype=torch.int64).float() / hd))
+    inv_freq, att = rope_inv_freq(cfg)
     t = torch.arange(max(max_pos, 1), dtype=torch.float32)
     freqs = torch.outer(t, inv_freq)
-    cos, sin = freqs.cos(), freqs.sin()
+    cos, sin = freqs.cos() * att, freqs.sin() * att
     if table_dtype is not None and table_dtype != torch.float32:
         cos, sin = cos.to(table_dtype).float(), sin.to(table_dtype).float()
     return cos.contiguous().to(device), sin.contiguous().to(device)

@@ -149,6 +149,19 @@ def test_checkpoint_resume_after_fault(ctx, tmp_path, monkeypatch):
     assert torch.equal(ck.load(3)[0], torch.ones(2, 3))
 
 
+# Llama checkpoints whose RoPE tables or head geometry differ from Llama-2 (Llama-3.1's llama3
+# scaling, linear and YaRN scaling, an explicit head_dim with nh*hd != hidden as in Mistral-Nemo)
+LLAMA_VARIANTS = {
+    "llama3_rope": dict(rope_theta=500000.0, rope_scaling={
+        "rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0, "high_freq_factor": 4.0,
+        "original_max_position_embeddings": 64}),
+    "linear_rope": dict(rope_scaling={"rope_type": "linear", "factor": 4.0}),
+    "yarn_rope": dict(rope_theta=1e6, rope_scaling={"rope_type": "yarn", "factor": 4.0,
+                                                    "original_max_position_embeddings": 1024}),
+    "head_dim_32": dict(explicit_head_dim=32),
+}
+
+
 def _hf_family_case(tmp_path, family):
     """tiny random checkpoint of another Llama-structured family + its HF model."""
     transformers = pytest.importorskip("transformers")
@@ -164,6 +177,16 @@ def _hf_family_case(tmp_path, family):
             rope_theta=cfg.rope_theta, max_position_embeddings=cfg.max_position_embeddings,
             tie_word_embeddings=False, use_sliding_window=False)
         model = transformers.Qwen2ForCausalLM(hf_cfg)
+    elif family in LLAMA_VARIANTS:
+        over = dict(LLAMA_VARIANTS[family])
+        cfg = preset("tiny", **over)
+        hf_cfg = transformers.LlamaConfig(
+            hidden_size=cfg.hidden_size, intermediate_size=cfg.intermediate_size,
+            num_attention_heads=cfg.num_attention_heads, num_key_value_heads=cfg.num_key_value_heads,
+            num_hidden_layers=cfg.num_hidden_layers, vocab_size=cfg.vocab_size, rms_norm_eps=cfg.rms_norm_eps,
+            rope_theta=cfg.rope_theta, max_position_embeddings=cfg.max_position_embeddings,
+            tie_word_embeddings=False, rope_scaling=cfg.rope_scaling, head_dim=cfg.head_dim)
+        model = transformers.LlamaForCausalLM(hf_cfg)
     else:
         cfg = preset("tiny", model_type="mistral", architectures=["MistralForCausalLM"], rope_theta=1e6,
                      sliding_window=4096)
@@ -183,7 +206,7 @@ def _hf_family_case(tmp_path, family):
     return path, cfg, sd, model
 
 
-@pytest.mark.parametrize("family", ["qwen2", "mistral"])
+@pytest.mark.parametrize("family", ["qwen2", "mistral"] + sorted(LLAMA_VARIANTS))
 def test_other_llama_families_match_hf(tmp_path, family):
     """Qwen2 (q/k/v biases, rope_theta 1e6) and Mistral == HF transformers in causal mode,
     and == the fp32 oracle in the reference's bidirectional-prefix mode."""
@@ -207,9 +230,25 @@ def test_other_llama_families_match_hf(tmp_path, family):
 def test_unsupported_configs_rejected():
     from flexible_llm_sharding_amd.config import ModelConfig
     for bad in ({"model_type": "gemma"}, {"mlp_bias": True}, {"hidden_act": "gelu"},
-                {"hidden_size": 256, "num_attention_heads": 4, "head_dim": 128}):
+                {"rope_scaling": {"rope_type": "dynamic", "factor": 2.0}},
+                {"rope_parameters": {"rope_type": "longrope", "rope_theta": 1e4}}):
         with pytest.raises(NotImplementedError):
             ModelConfig.from_dict(bad)
+
+
+def test_config_rope_and_head_dim_forms(tmp_path):
+    """HF v4 (rope_theta + rope_scaling) and v5 (rope_parameters) config forms; explicit head_dim
+    survives save/load."""
+    from flexible_llm_sharding_amd.config import ModelConfig
+    v4 = ModelConfig.from_dict({"rope_theta": 5e5, "rope_scaling": {"rope_type": "llama3", "factor": 8.0}})
+    v5 = ModelConfig.from_dict({"rope_parameters": {"rope_type": "llama3", "factor": 8.0, "rope_theta": 5e5}})
+    assert v4.rope_theta == v5.rope_theta == 5e5 and v4.rope_scaling == v5.rope_scaling
+    assert ModelConfig.from_dict({"rope_parameters": {"rope_type": "default", "rope_theta": 1e6}}).rope_scaling is None
+    c = ModelConfig.from_dict({"hidden_size": 256, "num_attention_heads": 4, "num_key_value_heads": 2,
+                               "head_dim": 32})
+    assert c.head_dim == 32 and c.q_size == 128
+    c.save(str(tmp_path))
+    assert ModelConfig.from_pretrained(str(tmp_path)) == c
 
 
 @pytest.mark.parametrize("num_batch_calls", [1, 2])

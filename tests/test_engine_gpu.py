@@ -76,6 +76,32 @@ def test_qwen2_family_on_gpu(tmp_path):
     r.close()
 
 
+@pytest.mark.parametrize("variant", ["llama3_rope", "yarn_rope", "head_dim_explicit"])
+def test_llama_variants_on_gpu(tmp_path, variant):
+    """Llama-3.1 / YaRN RoPE tables and an explicit head_dim (nh*hd != hidden) through the HIP kernels."""
+    from flexible_llm_sharding_amd.config import preset
+    from flexible_llm_sharding_amd.utils.synthetic import write_synthetic_checkpoint
+    over = {
+        "llama3_rope": dict(rope_theta=500000.0, rope_scaling={
+            "rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0, "high_freq_factor": 4.0,
+            "original_max_position_embeddings": 64}),
+        "yarn_rope": dict(rope_theta=1e6, rope_scaling={"rope_type": "yarn", "factor": 4.0,
+                                                        "original_max_position_embeddings": 64}),
+        # 8 heads x 64 = 512 query columns on a 256-wide residual stream
+        "head_dim_explicit": dict(num_attention_heads=8, num_key_value_heads=2, explicit_head_dim=64),
+    }[variant]
+    cfg = preset("tiny", **over)
+    path = str(tmp_path / variant)
+    write_synthetic_checkpoint(cfg, path, seed=4, std=0.05)
+    tok = load_tokenizer(path)
+    prompts = synthetic_prompts(4, 90, 3, 12, cfg.vocab_size, seed=6, vary=True)
+    ref = reference_scores(cfg, load_full_state_dict(cfg, path), tok, prompts)
+    r = ShardedRunner(cfg, HostStore.from_model_path(cfg, path), "cuda:0", tok, layer_num_per_shard=2)
+    for o, rf in zip(r(prompts), ref):
+        assert np.abs(o.astype(np.float32) - rf).max() < 2e-3
+    r.close()
+
+
 def test_hip_graph_replay_matches_eager(setup):
     """--resident --hip_graphs: whole-forward graph capture + shape-bucketed replay."""
     path, cfg, tok, prompts, ref = setup
