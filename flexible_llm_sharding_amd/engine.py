@@ -122,6 +122,7 @@ class ShardedRunner:
                                               self.act_dtype, prefix_cache_entries)
         self._n_decoders = sum(1 for n in self.names if layer_kind(n) == "decoder")
         self._W_all: Dict[str, Dict[str, torch.Tensor]] = {}
+        self._h2d0: Optional[int] = None     # prefetcher byte count at the start of the next call
 
     # ----------------------------------------------------------- helpers
     def tokenize(self, prompts) -> List[TokenizedPrompt]:
@@ -144,6 +145,12 @@ class ShardedRunner:
     # ------------------------------------------------------------- main
     def __call__(self, prompts) -> List[np.ndarray]:
         """Reference API: list of (prefix, suffixes) -> list of [n_s, 1, V] fp16 arrays."""
+        if self.my_shards and not self.resume_dir and not self.hip_graphs:
+            # the first shards' weights do not depend on the prompts: their H2D overlaps tokenization
+            if self._h2d0 is None:
+                self._h2d0 = self.prefetcher.bytes_h2d
+            for k in range(min(self.prefetcher.n_slots, len(self.my_shards))):
+                self.prefetcher.prefetch(k)
         return self.run_tokenized(self.tokenize(prompts))
 
     def _get_store(self) -> ActivationStore:
@@ -225,7 +232,10 @@ class ShardedRunner:
         flops = 0.0
         compute_s = 0.0
         sends = []
-        h2d0 = pf.bytes_h2d
+        # weight bytes of this call: counted from its early prefetch (or the previous call's
+        # speculative one), not from the first acquire
+        h2d0 = pf.bytes_h2d if self._h2d0 is None else self._h2d0
+        self._h2d0 = None
         items = self.schedule(len(batches))
         ck, k0 = self._open_checkpoint(tps)
         if k0 > 0:
@@ -321,14 +331,25 @@ class ShardedRunner:
             else:
                 store.put(b, state)
             del state
+        h2d_end = pf.bytes_h2d
         if cur_k >= 0:
             pf.release(cur_k)
+            if self._speculative_prefetch():
+                self._h2d0 = h2d_end
+                # every slot is free again: the next call's first shards stream in under this
+                # call's tail (lm_head, D2H of the scores) and the next tokenization
+                for k in range(min(pf.n_slots, len(self.my_shards))):
+                    pf.prefetch(k)
         if recvs:
             raise RuntimeError("unconsumed receives")
         for t, w in sends:
             w.wait()
         if self.cuda:
-            torch.cuda.synchronize(self.dev)
+            # the compute and activation streams, not the whole device: the weight copy stream
+            # may already be streaming the next call's first shards (speculative prefetch)
+            torch.cuda.current_stream(self.dev).synchronize()
+            self.h2d_stream.synchronize()
+            self.d2h_stream.synchronize()
         for batch, host, ev, pool_buf in out_pending:
             probs = host.numpy()
             r = 0
@@ -349,7 +370,7 @@ class ShardedRunner:
             "tokens": float(sum(b.num_tokens for b in batches)),
             "padded_tokens": float(sum(b.padded_tokens for b in batches)),
             "decoder_flops": flops, "micro_batches": float(len(batches)),
-            "weight_wait_s": pf.wait_seconds, "weight_h2d_bytes": float(pf.bytes_h2d - h2d0),
+            "weight_wait_s": pf.wait_seconds, "weight_h2d_bytes": float(h2d_end - h2d0),
             "act_d2h_bytes": float(store.bytes_d2h), "act_h2d_bytes": float(store.bytes_h2d),
             "resumed_from_shard": float(k0),
             # GPU-side: compute stream stalled on the weight / activation copy streams
@@ -363,6 +384,22 @@ class ShardedRunner:
                   f"(exposed weight wait); {len(self.my_shards)} shards, {len(batches)} micro-batches, "
                   f"{self.stats['tokens']:.0f} tokens in {wall:.2f}s")
         return outputs
+
+    def _speculative_prefetch(self) -> bool:
+        """Prefetch the next call's first shards at the end of a call?  Off by default: measured
+        on one MI355X (profiles/r1_host_path) it is neutral on 70B lnps=1 and costs 2% on 7B
+        lnps=8 (the tail's copies compete with the last shard's compute), while the prefetch
+        at the start of ``__call__`` already overlaps tokenization.  ``FLS_SPECULATIVE_PREFETCH=1``
+        turns it on.  Never when resuming (the next call may start elsewhere), resident
+        (nothing to load) or with the data-parallel all-gather prefetcher (no collectives
+        left in flight after a call)."""
+        import os
+        from .parallel.data_parallel import AllGatherPrefetcher
+        pf = self.prefetcher
+        if os.environ.get("FLS_SPECULATIVE_PREFETCH", "0") != "1":
+            return False
+        return (self.cuda and not self.resume_dir and not pf.resident
+                and not isinstance(pf, AllGatherPrefetcher))
 
     def _throttle(self, shard_ev: List) -> None:
         """Bound how far the host runs ahead of the GPU to ``RUNAHEAD_SHARDS`` shards.

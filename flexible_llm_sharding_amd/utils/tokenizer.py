@@ -105,9 +105,13 @@ def tokenize_prompt(tok, prefix: str, suffixes: Sequence[str],
     p = tok(prefix, return_attention_mask=False, truncation=True, max_length=max_len)["input_ids"]
     s = tok(list(suffixes), return_attention_mask=False, truncation=True, max_length=max_len,
             padding=True)["input_ids"]
+    return _assemble(p, s, tok.pad_token_id)
+
+
+def _assemble(p, s, pad) -> TokenizedPrompt:
+    """prefix ids + the right-padded suffix batch -> TokenizedPrompt (utils.py:250-259)."""
     rows = [list(r[1:]) for r in s]
     Ls = len(rows[0]) if rows else 0
-    pad = tok.pad_token_id
     eos, real = [], []
     for r in rows:
         e = sum(1 for t in r if t != pad) - 1
@@ -122,4 +126,23 @@ def tokenize_prompt(tok, prefix: str, suffixes: Sequence[str],
 
 def tokenize_prompts(tok, prompts: Sequence[Tuple[str, Sequence[str]]],
                      max_len: int = MAX_TOKEN_LEN) -> List[TokenizedPrompt]:
-    return [tokenize_prompt(tok, pre, suf, max_len) for pre, suf in prompts]
+    """All prompts in two batched tokenizer calls (the fast tokenizer encodes a batch on
+    all cores; per-prompt calls cost ~75 ms per 32 x 1k-token prompts, inside every pass).
+    Each prompt's suffix batch is then right-padded to its own longest suffix exactly as
+    ``tok(suffixes, padding=True)`` does, so the result equals :func:`tokenize_prompt`."""
+    if not prompts:
+        return []
+    pre = tok([p for p, _ in prompts], return_attention_mask=False, truncation=True,
+              max_length=max_len)["input_ids"]
+    flat = [x for _, sufs in prompts for x in sufs]
+    enc = tok(flat, return_attention_mask=False, truncation=True, max_length=max_len)["input_ids"] if flat else []
+    pad = tok.pad_token_id
+    right = getattr(tok, "padding_side", "right") == "right"
+    out, j = [], 0
+    for (p, sufs), ids in zip(prompts, pre):
+        rows = enc[j:j + len(sufs)]
+        j += len(sufs)
+        L = max((len(r) for r in rows), default=0)
+        padded = [list(r) + [pad] * (L - len(r)) if right else [pad] * (L - len(r)) + list(r) for r in rows]
+        out.append(_assemble(ids, padded, pad))
+    return out

@@ -31,6 +31,18 @@ def test_tokenize_contract(ctx):
     assert tp.padded_tokens == 4 + 3 * 3
 
 
+def test_batched_tokenize_equals_per_prompt(ctx):
+    """tokenize_prompts (two batched tokenizer calls) == tokenize_prompt per prompt, incl. truncation,
+    suffixes of different lengths and empty suffix strings."""
+    from flexible_llm_sharding_amd.utils.tokenizer import tokenize_prompts
+    path, cfg, tok, prompts, sd = ctx
+    extra = [("wd we wf", ("wg wh", "", "wj wk wl wm")), ("wa " * 50, ("wb",))]
+    for max_len in (4096, 16):
+        got = tokenize_prompts(tok, list(prompts) + extra, max_len)
+        want = [tokenize_prompt(tok, p, s, max_len) for p, s in list(prompts) + extra]
+        assert [vars(g) for g in got] == [vars(w) for w in want]
+
+
 def test_microbatch_split():
     from flexible_llm_sharding_amd.utils.tokenizer import TokenizedPrompt
     tps = [TokenizedPrompt([1] * 10, [[1] * 5], 5, [4]) for _ in range(7)]   # 15 tokens each
