@@ -171,3 +171,36 @@ def test_activation_store_no_race_large_batches(mid_model, tmp_path, storage):
         assert np.isfinite(a.astype(np.float32)).all()
         assert np.array_equal(a, b)
     r.close()
+
+
+def test_dp_allgather_prefetcher_over_rccl(setup, tmp_path):
+    """The data-parallel weight path on real RCCL: a one-rank `nccl` process group, each layer
+    H2D'd as a byte slice and completed in HBM by `all_gather_into_tensor` on RCCL's stream
+    (async work handles, copy-stream -> RCCL-stream -> compute-stream ordering), vs the oracle."""
+    import socket
+    import torch.distributed as dist
+    from flexible_llm_sharding_amd.parallel.comm import Comm
+    from flexible_llm_sharding_amd.parallel.data_parallel import AllGatherPrefetcher, SlicedHostStore
+    path, cfg, tok, prompts, ref = setup
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dev = torch.device("cuda", 0)
+    store = dist.TCPStore("127.0.0.1", port, 1, True)
+    dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=dev)
+    try:
+        comm = Comm(0, 1, dev, "nccl")
+        src = SlicedHostStore.from_source(FileLayerSource(cfg, path), 0, 1)
+        names = cfg.layer_names()
+        from flexible_llm_sharding_amd.parallel.planner import make_plan
+        plan = make_plan(len(names), 2, 1, 0, True)
+        pf = AllGatherPrefetcher(src, names, [sh for sh in plan.my_shards if len(sh)], dev, comm)
+        r = ShardedRunner(cfg, src, dev, tok, layer_num_per_shard=2, storage_location="cpu",
+                          token_budget=200, comm=comm, data_parallel=True, prefetcher=pf)
+        for _ in range(2):                       # second call: slots recycled behind RCCL writes
+            for o, rf in zip(r(prompts), ref):
+                assert np.abs(o.astype(np.float32) - rf).max() < 2e-3
+        r.close()
+    finally:
+        dist.destroy_process_group()
