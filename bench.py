@@ -53,6 +53,8 @@ def main(argv=None):
     ap.add_argument("--token-budget", type=int, default=16384)
     ap.add_argument("--resident", action="store_true")
     ap.add_argument("--hip-graphs", action="store_true", help="with --resident: whole-forward HIP graph replay")
+    ap.add_argument("--no-prune-last", action="store_true",
+                    help="compute every row in the last decoder layer (A/B of the scored-rows-only layer)")
     ap.add_argument("--prefix-attention", default="bidirectional")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--json-out", default=None)
@@ -112,7 +114,7 @@ def main(argv=None):
     runner = ShardedRunner(cfg, store, dev, tok, layer_num_per_shard=a.lnps, storage_location=a.storage,
                            disk_folder=f"/tmp/fls_bench_spill_{rank}", prefix_attention=a.prefix_attention,
                            token_budget=a.token_budget, resident=a.resident, comm=comm, data_parallel=dp,
-                           prefetcher=pf, hip_graphs=a.hip_graphs)
+                           prefetcher=pf, hip_graphs=a.hip_graphs, prune_last_layer=not a.no_prune_last)
     if not a.cpu:
         torch.cuda.reset_peak_memory_stats(dev)
 

@@ -65,7 +65,8 @@ class ShardedRunner:
                  mlp_chunk: int = 16384, prefetcher: Optional[ShardPrefetcher] = None,
                  verbose: bool = False, resume_dir: Optional[str] = None, checkpoint_every: int = 0,
                  max_token_len: int = MAX_TOKEN_LEN, hip_graphs: bool = False,
-                 prefix_kv_cache: bool = False, prefix_cache_entries: int = 8):
+                 prefix_kv_cache: bool = False, prefix_cache_entries: int = 8,
+                 prune_last_layer: bool = True):
         self.cfg = cfg
         self.src = source
         self.dev = torch.device(device)
@@ -94,6 +95,9 @@ class ShardedRunner:
         cos, sin = rope_tables(cfg, max(cfg.max_position_embeddings, max_token_len),
                                torch.float16, self.dev)
         self.ctx = ExecContext(cfg, self.ops, self.dev, self.act_dtype, cos, sin, mlp_chunk)
+        decs = [n for n in self.names if layer_kind(n) == "decoder"]
+        self.ctx.prune_last = bool(prune_last_layer and decs)
+        self.ctx.last_decoder = decs[-1] if decs else ""
         my = [s for s in self.plan.my_shards if len(s)]
         self.my_shards = my
         self.prefetcher = prefetcher or ShardPrefetcher(source, self.names, my, self.dev,
@@ -136,6 +140,8 @@ class ShardedRunner:
     def _state_shape(self, layer_idx: int, batch: PackedBatch):
         """Shape of the activation produced by ``layer_idx`` (utils.py:281-286)."""
         kind = layer_kind(self.names[layer_idx])
+        if kind == "decoder" and self.ctx.prune_last and self.names[layer_idx] == self.ctx.last_decoder:
+            return (batch.n_scored, self.cfg.hidden_size)
         if kind in ("embed", "decoder"):
             return (batch.num_tokens, self.cfg.hidden_size)
         if kind == "norm":
@@ -312,7 +318,7 @@ class ShardedRunner:
                     name = self.names[li]
                     state = run_layer(self.ctx, name, W[name], state, batch, meta)
                     if layer_kind(name) == "decoder":
-                        flops += layer_flops(self.cfg, batch)
+                        flops += layer_flops(self.cfg, batch, self._pruned(name))
             compute_s += time.perf_counter() - tc
             if pbar is not None:
                 pbar.update(1)
@@ -385,6 +391,9 @@ class ShardedRunner:
                   f"{self.stats['tokens']:.0f} tokens in {wall:.2f}s")
         return outputs
 
+    def _pruned(self, name: str) -> bool:
+        return self.ctx.prune_last and name == self.ctx.last_decoder
+
     def _speculative_prefetch(self) -> bool:
         """Prefetch the next call's first shards at the end of a call?  Off by default: measured
         on one MI355X (profiles/r1_host_path) it is neutral on 70B lnps=1 and costs 2% on 7B
@@ -454,7 +463,8 @@ class ShardedRunner:
             host = pool_buf[:nbytes].view(probs.dtype).view(probs.shape)
             host.copy_(probs, non_blocking=True)     # same stream: ordered before the next replay
             pending.append((batch, host, pool_buf))
-            flops += self._n_decoders * layer_flops(self.cfg, batch)
+            flops += sum(layer_flops(self.cfg, batch, self._pruned(n)) for n in self.names
+                         if layer_kind(n) == "decoder")
         torch.cuda.synchronize(self.dev)
         for batch, host, pool_buf in pending:
             probs = host.numpy()
@@ -505,7 +515,8 @@ class ShardedRunner:
         fp = run_fingerprint(self.cfg, [tp.prefix + [t for s in tp.suffixes for t in s] + [-1] for tp in tps],
                              lnps=self.lnps, budget=self.token_budget, attn=self.prefix_attention,
                              world=self.comm.world, rank=self.comm.rank, dp=self.data_parallel,
-                             dtype=str(self.act_dtype), every=self.checkpoint_every)
+                             dtype=str(self.act_dtype), every=self.checkpoint_every,
+                             prune=self.ctx.prune_last)
         ck = RunCheckpoint(self.resume_dir, fp, self.comm.rank)
         have = set(ck.available())
         if self.comm.world > 1:

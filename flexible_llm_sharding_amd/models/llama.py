@@ -107,6 +107,10 @@ class ExecContext:
     sin: torch.Tensor
     mlp_chunk: int = 16384       # rows per gate/up + down chunk (bounds the [T, I] buffer)
     prefix_entry: Optional[object] = None   # runtime.prefix_cache.PrefixEntry of the current call
+    # the last decoder layer computes only the scored rows (its K/V still cover every token):
+    # nothing downstream reads the other rows (final norm gathers the scored rows, utils.py:284-286)
+    prune_last: bool = True
+    last_decoder: str = ""
 
 
 def run_embed(ctx: ExecContext, W: Dict[str, torch.Tensor], meta: dict) -> torch.Tensor:
@@ -115,7 +119,12 @@ def run_embed(ctx: ExecContext, W: Dict[str, torch.Tensor], meta: dict) -> torch
 
 def run_decoder(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, batch,
                 meta: dict, layer_name: str = "") -> torch.Tensor:
+    """One pre-norm decoder block on the packed rows.  With ``prune`` (the last decoder
+    layer) Q/attention/O/MLP run only for the scored rows and the result is
+    [n_scored, H]: K/V are still projected for every token (the scored rows attend to
+    the whole prefix and their own suffix)."""
     cfg, ops = ctx.cfg, ctx.ops
+    prune = ctx.prune_last and layer_name == ctx.last_decoder
     eps = cfg.rms_norm_eps
     h = ops.rmsnorm(x, W["ln1"], eps)
     qkv = ops.qkv_rope(h, W["wqkv"], meta["positions"], ctx.cos, ctx.sin,
@@ -130,9 +139,17 @@ def run_decoder(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, b
         elif "pfx_src" in meta:              # full pass: keep the prefix rows' post-RoPE K/V
             pe.buffer(layer_name, create=True).index_copy_(
                 0, meta["pfx_dst"], qkv[:, qs:qs + kv].index_select(0, meta["pfx_src"]))
-    attn_arg = meta["work"] if getattr(ops, "uses_work_items", False) else batch.segments
+    work_items = getattr(ops, "uses_work_items", False)
+    if prune:
+        attn_arg = meta["work_last"] if work_items else batch.last_segments
+    else:
+        attn_arg = meta["work"] if work_items else batch.segments
     a = ops.attention(qkv, attn_arg, cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim, kv0=kv0)
     del qkv
+    if prune:
+        idx = meta["last_idx"]
+        a = a.index_select(0, idx)
+        x = x.index_select(0, idx)
     x = ops.linear_residual(a, W["wo"], x, bias=W.get("bo"))
     del a
     T = x.shape[0]
@@ -153,6 +170,8 @@ def run_decoder(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, b
 
 
 def run_norm(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, meta: dict) -> torch.Tensor:
+    if ctx.prune_last and ctx.last_decoder:
+        return ctx.ops.rmsnorm(x, W["norm"], ctx.cfg.rms_norm_eps)    # rows already gathered
     return ctx.ops.gather_rmsnorm(x, meta["last_idx"], W["norm"], ctx.cfg.rms_norm_eps)
 
 
@@ -172,13 +191,21 @@ def run_layer(ctx: ExecContext, layer_name: str, W: Dict[str, torch.Tensor],
     return run_head(ctx, W, state)
 
 
-def layer_flops(cfg: ModelConfig, batch) -> float:
-    """Approximate forward FLOPs of one decoder layer on ``batch`` (GEMMs + attention)."""
+def layer_flops(cfg: ModelConfig, batch, pruned: bool = False) -> float:
+    """Approximate forward FLOPs of one decoder layer on ``batch`` (GEMMs + attention);
+    ``pruned``: the last decoder layer (K/V for every token, the rest for scored rows)."""
     T = batch.num_tokens
-    gemm = 2.0 * T * cfg.decoder_layer_params()
+    if pruned:
+        S = batch.n_scored
+        kv = 2 * cfg.kv_size * cfg.hidden_size
+        gemm = 2.0 * (T * kv + S * (cfg.decoder_layer_params() - kv))
+        segs = batch.last_segments
+    else:
+        gemm = 2.0 * T * cfg.decoder_layer_params()
+        segs = batch.segments
     att = 0.0
-    for sg in batch.segments:
+    for sg in segs:
         keys = sg.r0_len if not sg.r0_causal else (sg.q_len + 1) / 2.0
-        keys += (sg.r1_len + 1) / 2.0 if sg.r1_len else 0.0
+        keys += sg.q_off + (sg.q_len + 1) / 2.0 if sg.r1_len else 0.0
         att += 4.0 * sg.q_len * keys * cfg.q_size
     return gemm + att

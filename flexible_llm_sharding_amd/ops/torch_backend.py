@@ -99,7 +99,7 @@ class TorchOps:
             if sg.r1_len:
                 kr.append((sg.r1_start, sg.r1_len, 1, k_all, v_all))
             ks_, vs_, masks = [], [], []
-            qi = torch.arange(sg.q_len, device=dev)
+            qi = torch.arange(sg.q_len, device=dev) + sg.q_off
             for st, ln, causal, kk, vv in kr:
                 ks_.append(kk[st:st + ln])
                 vs_.append(vv[st:st + ln])

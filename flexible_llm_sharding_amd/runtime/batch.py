@@ -41,6 +41,7 @@ class Segment:
     r0_causal: int
     r1_start: int
     r1_len: int          # r1 (own suffix) is always causal
+    q_off: int = 0       # index of the first query inside its segment (causal compare)
 
 
 @dataclass
@@ -52,6 +53,8 @@ class PackedBatch:
     segments: List[Segment]
     work: np.ndarray                      # [n_items, 8] int32
     last_idx: np.ndarray                  # [S_total] int32 rows scored
+    last_segments: List[Segment]          # one single-query segment per scored row (last layer)
+    work_last: np.ndarray                 # [S_total, 8] their work items
     num_tokens: int
     padded_tokens: int                    # reference-equivalent token count
     max_pos: int
@@ -75,6 +78,7 @@ class PackedBatch:
                 "positions": torch.from_numpy(self.positions).to(d, non_blocking=nb),
                 "work": torch.from_numpy(self.work).to(d, non_blocking=nb),
                 "last_idx": torch.from_numpy(self.last_idx).to(d, non_blocking=nb),
+                "work_last": torch.from_numpy(self.work_last).to(d, non_blocking=nb),
             }
             if self.pfx_src is not None:
                 self._dev[key]["pfx_src"] = torch.from_numpy(self.pfx_src).to(d, non_blocking=nb)
@@ -97,7 +101,7 @@ def pack_prompts(tps: Sequence[TokenizedPrompt], prompt_ids: Sequence[int],
     if kv_cached and prefix_offsets is None:
         raise ValueError("kv_cached needs prefix_offsets")
     pcausal = 1 if prefix_attention == "causal" else 0
-    ids, pos, segs, last, nsuf = [], [], [], [], []
+    ids, pos, segs, last, nsuf, lsegs = [], [], [], [], [], []
     src, dst = [], []
     t = 0
     padded = 0
@@ -122,23 +126,32 @@ def pack_prompts(tps: Sequence[TokenizedPrompt], prompt_ids: Sequence[int],
             pos.extend(range(Lp, Lp + n))
             segs.append(Segment(s0, n, p0, Lp, 0, s0, n))
             last.append(s0 + n - 1)
+            # the scored row alone, for a last decoder layer that computes only scored rows
+            lsegs.append(Segment(s0 + n - 1, 1, p0, Lp, 0, s0, n, q_off=n - 1))
             t += n
         max_pos = max(max_pos, Lp + max([len(s) for s in tp.suffixes] or [0]))
         nsuf.append(tp.n_suffix)
         padded += tp.padded_tokens
-    work = []
-    for sg in segs:
-        for off in range(0, sg.q_len, Q_BLOCK):
-            work.append((sg.q_start + off, min(Q_BLOCK, sg.q_len - off), off,
-                         sg.r0_start, sg.r0_len, sg.r0_causal, sg.r1_start, sg.r1_len))
+    work = _work_items(segs)
     return PackedBatch(
         prompt_ids=list(prompt_ids), n_suffix=nsuf,
         ids=np.asarray(ids, dtype=np.int32), positions=np.asarray(pos, dtype=np.int32),
-        segments=segs, work=np.asarray(work, dtype=np.int32).reshape(-1, WORK_ITEM_FIELDS),
-        last_idx=np.asarray(last, dtype=np.int32), num_tokens=t, padded_tokens=padded,
+        segments=segs, work=work,
+        last_idx=np.asarray(last, dtype=np.int32), last_segments=lsegs,
+        work_last=_work_items(lsegs), num_tokens=t, padded_tokens=padded,
         max_pos=max_pos, kv_cached=kv_cached,
         pfx_src=np.asarray(src, dtype=np.int64) if (prefix_offsets is not None and not kv_cached) else None,
         pfx_dst=np.asarray(dst, dtype=np.int64) if (prefix_offsets is not None and not kv_cached) else None)
+
+
+def _work_items(segs: Sequence[Segment]) -> np.ndarray:
+    """Segments -> [n_items, 8] int32 work items of at most Q_BLOCK queries."""
+    work = []
+    for sg in segs:
+        for off in range(0, sg.q_len, Q_BLOCK):
+            work.append((sg.q_start + off, min(Q_BLOCK, sg.q_len - off), sg.q_off + off,
+                         sg.r0_start, sg.r0_len, sg.r0_causal, sg.r1_start, sg.r1_len))
+    return np.asarray(work, dtype=np.int32).reshape(-1, WORK_ITEM_FIELDS)
 
 
 def split_microbatches(tps: Sequence[TokenizedPrompt], token_budget: int,

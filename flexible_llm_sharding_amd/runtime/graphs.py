@@ -17,7 +17,8 @@ bucketed so replays are reused across calls and generation steps:
   no attention work item covers them),
 * attention work items -> multiple of ``WORK_BUCKET`` (padding items have
   ``q_len = 0``; the kernels return before touching memory),
-* scored rows -> multiple of ``SCORE_BUCKET`` (padding gathers row 0; ignored).
+* scored rows -> multiple of ``SCORE_BUCKET`` (padding gathers row 0; ignored; the
+  last decoder layer's single-query work items are padded with ``q_len = 0``).
 
 The metadata of a new batch is copied into the graph's static input tensors
 before the replay; the probabilities come out of its static output tensor.
@@ -58,7 +59,9 @@ def padded_meta(batch: PackedBatch, key) -> Dict[str, np.ndarray]:
     work[:batch.work.shape[0]] = batch.work
     last = np.zeros(S, np.int32)
     last[:batch.n_scored] = batch.last_idx
-    return {"ids": ids, "positions": pos, "work": work, "last_idx": last}
+    wl = np.zeros((S, WORK_ITEM_FIELDS), np.int32)        # padding items: q_len 0
+    wl[:batch.work_last.shape[0]] = batch.work_last
+    return {"ids": ids, "positions": pos, "work": work, "last_idx": last, "work_last": wl}
 
 
 class _Graph:

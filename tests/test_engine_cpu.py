@@ -313,3 +313,18 @@ def test_prefix_cache_invalidated_by_new_prefix(tiny_model):
         for a, b in zip(out, ref(ps)):
             assert np.abs(a.astype(np.float32) - b.astype(np.float32)).max() < 1e-5
     assert r.prefix_cache.hits == 1 and r.prefix_cache.misses == 2
+
+
+@pytest.mark.parametrize("prefix_attention", ["bidirectional", "causal"])
+def test_last_layer_pruning_is_exact(ctx, prefix_attention):
+    """The last decoder layer computing only the scored rows (K/V for every token) gives the
+    full computation's scores and fewer FLOPs; the final norm then skips its gather."""
+    path, cfg, tok, prompts, sd = ctx
+    src = FileLayerSource(cfg, path)
+    full = ShardedRunner(cfg, src, "cpu", tok, prefix_attention=prefix_attention, token_budget=60,
+                         prune_last_layer=False)
+    pr = ShardedRunner(cfg, src, "cpu", tok, prefix_attention=prefix_attention, token_budget=60)
+    a, b = full(prompts), pr(prompts)
+    for x, y in zip(a, b):
+        assert np.abs(x.astype(np.float32) - y.astype(np.float32)).max() < 1e-5
+    assert pr.stats["decoder_flops"] < full.stats["decoder_flops"]
