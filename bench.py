@@ -50,6 +50,8 @@ def main(argv=None):
     ap.add_argument("--lnps", type=int, default=1)
     ap.add_argument("--storage", default="cpu", choices=["gpu", "cpu", "disk"])
     ap.add_argument("--mode", default="auto", choices=["auto", "mp", "dp"])
+    ap.add_argument("--stages", default="round_robin", choices=["round_robin", "contiguous"],
+                    help="--mode mp: shard k on GPU k mod N (reference) or one contiguous stage per GPU")
     ap.add_argument("--token-budget", type=int, default=16384)
     ap.add_argument("--resident", action="store_true")
     ap.add_argument("--hip-graphs", action="store_true", help="with --resident: whole-forward HIP graph replay")
@@ -88,7 +90,7 @@ def main(argv=None):
     kw = {} if a.num_layers is None else {"num_hidden_layers": a.num_layers}
     cfg = preset(a.model, **kw)
     names = cfg.layer_names()
-    plan = make_plan(len(names), a.lnps, world, rank, dp)
+    plan = make_plan(len(names), a.lnps, world, rank, dp, a.stages)
     mine = sorted({i for sh in plan.my_shards for i in sh})
     t0 = time.perf_counter()
     log(rank, f"[bench] generating {len(mine)} random-init {a.model} layers on {dev} -> pinned host ...")
@@ -114,7 +116,8 @@ def main(argv=None):
     runner = ShardedRunner(cfg, store, dev, tok, layer_num_per_shard=a.lnps, storage_location=a.storage,
                            disk_folder=f"/tmp/fls_bench_spill_{rank}", prefix_attention=a.prefix_attention,
                            token_budget=a.token_budget, resident=a.resident, comm=comm, data_parallel=dp,
-                           prefetcher=pf, hip_graphs=a.hip_graphs, prune_last_layer=not a.no_prune_last)
+                           prefetcher=pf, hip_graphs=a.hip_graphs, prune_last_layer=not a.no_prune_last,
+                           pipeline_stages=a.stages)
     if not a.cpu:
         torch.cuda.reset_peak_memory_stats(dev)
 
@@ -165,7 +168,7 @@ def main(argv=None):
                    "prefix_len": a.prefix_len, "n_suffix": a.n_suffix, "suffix_len": a.suffix_len,
                    "tokens_per_step": tok_step, "padded_tokens_per_step": padded_step,
                    "layer_num_per_shard": a.lnps, "storage_location": a.storage,
-                   "parallelism": (f"pp{world}-roundrobin" if mode == "mp" else
+                   "parallelism": (f"pp{world}-{a.stages.replace('_', '')}" if mode == "mp" else
                                    (f"dp{world}-allgather-weights" if dp else "single")),
                    "resident": a.resident, "hip_graphs": bool(runner.hip_graphs), "token_budget": a.token_budget,
                    "gemm_backend": os.environ.get("FLS_GEMM_BACKEND", "hip") if dev.type == "cuda" else "torch"},

@@ -43,7 +43,8 @@ def batch_ranges(n: int, num_batch: int):
 
 def build_source(args, cfg: ModelConfig, comm: Comm, device: torch.device):
     names = cfg.layer_names()
-    plan = make_plan(len(names), args.layer_num_per_shard, comm.world, comm.rank, args.data_parallel)
+    plan = make_plan(len(names), args.layer_num_per_shard, comm.world, comm.rank, args.data_parallel,
+                     getattr(args, "pipeline_stages", "round_robin"))
     mine = [names[i] for i in sorted({i for sh in plan.my_shards for i in sh})]
     if getattr(args, "synthetic", None):
         return HostStore.synthetic(cfg, device, seed=0, pinned=device.type == "cuda", names=mine)
@@ -75,7 +76,8 @@ def build_runner(args, cfg: ModelConfig, device, comm: Comm, tok) -> ShardedRunn
                          max_token_len=getattr(args, "max_token_len", None) or MAX_TOKEN_LEN,
                          hip_graphs=getattr(args, "hip_graphs", False),
                          prefix_kv_cache=getattr(args, "prefix_kv_cache", False),
-                         prefix_cache_entries=getattr(args, "prefix_cache_entries", 8))
+                         prefix_cache_entries=getattr(args, "prefix_cache_entries", 8),
+                         pipeline_stages=getattr(args, "pipeline_stages", "round_robin"))
 
 
 def open_packed_source(args, cfg: ModelConfig, comm: Comm, names):

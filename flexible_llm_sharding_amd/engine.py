@@ -66,7 +66,7 @@ class ShardedRunner:
                  verbose: bool = False, resume_dir: Optional[str] = None, checkpoint_every: int = 0,
                  max_token_len: int = MAX_TOKEN_LEN, hip_graphs: bool = False,
                  prefix_kv_cache: bool = False, prefix_cache_entries: int = 8,
-                 prune_last_layer: bool = True):
+                 prune_last_layer: bool = True, pipeline_stages: str = "round_robin"):
         self.cfg = cfg
         self.src = source
         self.dev = torch.device(device)
@@ -87,7 +87,7 @@ class ShardedRunner:
         self.names = cfg.layer_names()
         self.L = len(self.names)
         self.plan: ShardPlan = make_plan(self.L, layer_num_per_shard, self.comm.world, self.comm.rank,
-                                         data_parallel)
+                                         data_parallel, pipeline_stages)
         if self.cuda and cfg.head_dim not in (64, 128):
             raise NotImplementedError(f"head_dim={cfg.head_dim}: the HIP attention kernels serve 64 and 128")
         self.act_dtype = act_dtype or (torch.float16 if self.cuda else torch.float32)

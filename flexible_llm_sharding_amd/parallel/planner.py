@@ -10,8 +10,11 @@ Bit-compatible with the reference formulas in ``/root/reference/utils.py:143-157
 
 ``L`` is ``num_hidden_layers + 3`` (embed, decoders, final norm, lm_head).
 
-Beyond the reference we add ``contiguous_stage_plan`` — the MI355X-friendly
-alternative for resident pipelines where each GPU owns one contiguous slice.
+Beyond the reference, ``stages="contiguous"`` gives each GPU one contiguous
+slice of layers (``contiguous_stage_plan``), split into shards of <= lnps: a
+micro-batch then crosses xGMI G-1 times per pass instead of at every shard
+boundary (82 hand-offs for 70B lnps=1 over 8 GPUs) — the layout for resident
+pipelines, where each GPU keeps its whole stage in HBM.
 """
 from __future__ import annotations
 
@@ -70,13 +73,15 @@ class ShardPlan:
     world: int
     all_shards: Tuple[Tuple[int, ...], ...]   # global, in execution order
     my_shards: Tuple[Tuple[int, ...], ...]    # this rank, in execution order
+    owners: Tuple[int, ...] = ()              # mp: rank of every global shard (default k mod G)
+    stages: str = "round_robin"
 
     def owner_of_layer(self, layer_idx: int) -> int:
         if self.mode != "mp":
             return self.rank
         for k, sh in enumerate(self.all_shards):
             if layer_idx in sh:
-                return k % self.world
+                return self.owners[k] if self.owners else k % self.world
         raise KeyError(layer_idx)
 
     def next_nonempty_owner(self, layer_idx: int) -> int:
@@ -87,17 +92,33 @@ class ShardPlan:
         return self.owner_of_layer(layer_idx - 1)
 
 
+PIPELINE_STAGES = ("round_robin", "contiguous")
+
+
 def make_plan(num_layers: int, layer_num_per_shard: int, world: int, rank: int,
-              data_parallel: bool) -> ShardPlan:
+              data_parallel: bool, stages: str = "round_robin") -> ShardPlan:
+    if stages not in PIPELINE_STAGES:
+        raise ValueError(f"stages={stages!r}: choose from {PIPELINE_STAGES}")
     if world <= 1:
         sh = single_device_shards(num_layers, layer_num_per_shard)
         return ShardPlan("single", 0, 1, tuple(sh), tuple(sh))
     if data_parallel:
         sh = single_device_shards(num_layers, layer_num_per_shard)
         return ShardPlan("dp", rank, world, tuple(sh), tuple(sh))
+    if stages == "contiguous":
+        all_sh, owners = [], []
+        for r, block in enumerate(contiguous_stage_plan(num_layers, world)):
+            if not block:
+                continue
+            for sub in single_device_shards(len(block), layer_num_per_shard):
+                all_sh.append(tuple(block[i] for i in sub))
+                owners.append(r)
+        mine = [sh for sh, o in zip(all_sh, owners) if o == rank]
+        return ShardPlan("mp", rank, world, tuple(all_sh), tuple(mine), tuple(owners), stages)
     all_sh = model_parallel_all_shards(num_layers, layer_num_per_shard, world)
     mine = all_sh[rank::world]
-    return ShardPlan("mp", rank, world, tuple(all_sh), tuple(mine))
+    owners = tuple(k % world for k in range(len(all_sh)))
+    return ShardPlan("mp", rank, world, tuple(all_sh), tuple(mine), owners, stages)
 
 
 def shard_sizes(shards: Sequence[Sequence[int]]) -> List[int]:

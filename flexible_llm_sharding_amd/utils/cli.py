@@ -60,6 +60,8 @@ def build_parser() -> argparse.ArgumentParser:
                    help="packed-layer cache directory (default: <model_path>/.fls_packed)")
     p.add_argument("--dp_weight_shard", type=str2bool, nargs="?", const=True, default=True,
                    help="data parallel: scatter-load 1/G of each layer per GPU + RCCL all-gather")
+    p.add_argument("--pipeline_stages", choices=["round_robin", "contiguous"], default="round_robin",
+                   help="model parallel: shard k on GPU k mod G (reference) or one contiguous stage per GPU")
     p.add_argument("--token_budget", type=int, default=16384, help="max tokens per packed micro-batch")
     p.add_argument("--dtype", choices=["float16", "float32"], default=None,
                    help="activation dtype (default fp16 on GPU, fp32 on CPU)")

@@ -36,10 +36,12 @@ def _bench(world, extra, tmp_path):
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("world,mode", [(1, "auto"), (2, "auto"), (2, "mp"), (3, "auto"), (6, "mp")])
-def test_bench_contract(tmp_path, world, mode):
+@pytest.mark.parametrize("world,mode,stages", [(1, "auto", "round_robin"), (2, "auto", "round_robin"),
+                                               (2, "mp", "round_robin"), (3, "auto", "round_robin"),
+                                               (6, "mp", "round_robin"), (3, "mp", "contiguous")])
+def test_bench_contract(tmp_path, world, mode, stages):
     # world 6 on the 5-layer tiny model: the MP shard padding leaves rank 5 with no layers
-    out = _bench(world, ["--mode", mode], tmp_path)
+    out = _bench(world, ["--mode", mode, "--stages", stages], tmp_path)
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
               "scaling", "vs_baseline", "dtype", "data", "config"):
         assert k in out

@@ -23,7 +23,8 @@ def _port():
     return p
 
 
-def _worker(rank, world, port, path, prompts, lnps, dp, storage, out_dir, budget, pkv=False):
+def _worker(rank, world, port, path, prompts, lnps, dp, storage, out_dir, budget, pkv=False,
+            stages="round_robin"):
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
                        "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
     torch.set_num_threads(1)
@@ -37,7 +38,11 @@ def _worker(rank, world, port, path, prompts, lnps, dp, storage, out_dir, budget
     tok = load_tokenizer(path)
     r = ShardedRunner(cfg, FileLayerSource(cfg, path), "cpu", tok, layer_num_per_shard=lnps,
                       storage_location=storage, disk_folder=os.path.join(out_dir, f"spill{rank}"),
-                      comm=comm, data_parallel=dp, token_budget=budget, prefix_kv_cache=pkv)
+                      comm=comm, data_parallel=dp, token_budget=budget, prefix_kv_cache=pkv,
+                      pipeline_stages=stages)
+    if stages == "contiguous" and not dp:
+        flat = [i for sh in r.my_shards for i in sh]
+        assert flat == list(range(flat[0], flat[0] + len(flat)))          # one contiguous stage
     if dp:
         idx = np.array_split(np.arange(len(prompts)), world)[rank]
         mine = [prompts[i] for i in idx]
@@ -72,11 +77,13 @@ def single(tiny_model):
     return path, prompts, out
 
 
-@pytest.mark.parametrize("world,lnps,storage,budget", [(2, 1, "cpu", 40), (3, 1, "gpu", 30), (2, 2, "disk", 1000),
-                                                       (4, 1, "cpu", 60)])
-def test_model_parallel_pipeline(single, tmp_path, world, lnps, storage, budget):
+@pytest.mark.parametrize("world,lnps,storage,budget,stages", [
+    (2, 1, "cpu", 40, "round_robin"), (3, 1, "gpu", 30, "round_robin"), (2, 2, "disk", 1000, "round_robin"),
+    (4, 1, "cpu", 60, "round_robin"), (2, 1, "cpu", 40, "contiguous"), (3, 2, "gpu", 30, "contiguous")])
+def test_model_parallel_pipeline(single, tmp_path, world, lnps, storage, budget, stages):
     path, prompts, ref = single
-    mp.start_processes(_worker, args=(world, _port(), path, prompts, lnps, False, storage, str(tmp_path), budget),
+    mp.start_processes(_worker, args=(world, _port(), path, prompts, lnps, False, storage, str(tmp_path), budget,
+                                      False, stages),
                        nprocs=world, start_method="spawn", join=True)
     allv = pickle.load(open(tmp_path / "out.pkl", "rb"))
     owner = [v for v in allv if v and v[0] is not None]

@@ -68,3 +68,18 @@ def test_plan_modes():
 def test_invalid():
     with pytest.raises(ValueError):
         single_device_shards(10, 0)
+
+
+def test_contiguous_stages():
+    """--pipeline_stages contiguous: one contiguous block per rank, split into shards of <= lnps."""
+    for L, lnps, G in [(83, 1, 8), (83, 3, 8), (5, 2, 3), (35, 8, 4)]:
+        plans = [make_plan(L, lnps, G, r, False, "contiguous") for r in range(G)]
+        assert [i for sh in plans[0].all_shards for i in sh] == list(range(L))
+        for r, p in enumerate(plans):
+            flat = [i for sh in p.my_shards for i in sh]
+            assert flat == list(range(flat[0], flat[0] + len(flat)))
+            assert all(len(sh) <= lnps for sh in p.my_shards)
+            assert all(p.owner_of_layer(i) == r for i in flat)
+        # hand-offs between ranks: G - 1 per pass
+        owners = [plans[0].owner_of_layer(i) for i in range(L)]
+        assert sum(a != b for a, b in zip(owners, owners[1:])) == G - 1
