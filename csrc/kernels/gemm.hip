@@ -1520,7 +1520,9 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_v9(const half_t* __restrict__ 
 //   1: DMA first (after 0,2,4,6), reads after 8,10,..,22
 //   2: spread: reads after 0,4,..,28; DMA after 2,10,18,26
 //   3: alternate from the start: read/DMA after 0..11 (r r d r r d ...), rest bare
-template <int EPI, int ABL = 0, int SCHED = 0>
+// GM: tile order — consecutive blocks walk GM M-tiles per N-tile (grouped column-major);
+// negative GM groups -GM N-tiles per M-tile instead (microbenchmark variants, 80+ in fls_gemm_ablate)
+template <int EPI, int ABL = 0, int SCHED = 0, int GM = 8>
 __global__ __launch_bounds__(256, 1) void gemm_nt_v10(const half_t* __restrict__ A, const half_t* __restrict__ W,
                                                     half_t* __restrict__ C, int M, int N, int K, int lda, int ldw,
                                                     int ldc, Epi ep) {
@@ -1537,13 +1539,24 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_v10(const half_t* __restrict__
   }
   const int tiles_m = (M + BM - 1) / BM;
   const int tiles_n = N / BN;
-  constexpr int GROUP_M = 8;
-  const int group = bid / (GROUP_M * tiles_n);
-  const int first_m = group * GROUP_M;
-  const int gsz = min(tiles_m - first_m, GROUP_M);
-  const int in_g = bid - group * GROUP_M * tiles_n;
-  const int tm = first_m + in_g % gsz;
-  const int tn = in_g / gsz;
+  int tm, tn;
+  if (GM > 0) {
+    constexpr int GROUP_M = GM > 0 ? GM : 1;
+    const int group = bid / (GROUP_M * tiles_n);
+    const int first_m = group * GROUP_M;
+    const int gsz = min(tiles_m - first_m, GROUP_M);
+    const int in_g = bid - group * GROUP_M * tiles_n;
+    tm = first_m + in_g % gsz;
+    tn = in_g / gsz;
+  } else {
+    constexpr int GROUP_N = GM < 0 ? -GM : 1;
+    const int group = bid / (GROUP_N * tiles_m);
+    const int first_n = group * GROUP_N;
+    const int gsz = min(tiles_n - first_n, GROUP_N);
+    const int in_g = bid - group * GROUP_N * tiles_m;
+    tn = first_n + in_g % gsz;
+    tm = in_g / gsz;
+  }
   const int m0 = tm * BM, n0 = tn * BN;
 
   // staging: a half-tile = 16 pieces of 8 rows x 128 B, rows {(j>>3)*128 + (j&7)*8} (+64 for the B half);
@@ -2082,6 +2095,7 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_v12(const half_t* __restrict__
 }
 
 int g_variant = -1;   // -1: from env FLS_GEMM_VARIANT (default 3)
+int g_v10_order = 0;  // 0: by shape (launch<EPI>), else a fixed GM (fls_gemm_set_order)
 
 int variant() {
   if (g_variant < 0) {
@@ -2150,11 +2164,32 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
   } else if (var == 10 && fast) {
     static bool attr10 = false;
     if (!attr10) {
-      (void)hipFuncSetAttribute((const void*)gemm_nt_v10<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
+      (void)hipFuncSetAttribute((const void*)gemm_nt_v10<EPI, 0, 0, 8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                2 * v9::BUF);
+      (void)hipFuncSetAttribute((const void*)gemm_nt_v10<EPI, 0, 0, -4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                2 * v9::BUF);
+      (void)hipFuncSetAttribute((const void*)gemm_nt_v10<EPI, 0, 0, -8>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 2 * v9::BUF);
       attr10 = true;
     }
-    hipLaunchKernelGGL(gemm_nt_v10<EPI>, dim3(tiles), dim3(256), 2 * v9::BUF, s, A, W, C, M, N, K, lda, ldw, ldc, ep);
+    // tile order (scripts/gemm_order.py, profiles/r1_gemm_order): with few N tiles (o / down / qkv
+    // projections, N <= 16384) walking M inside groups of N tiles beats the M-grouped order by ~3-4%;
+    // the wide gate/up GEMM (N = 57344) keeps 8 M tiles per group
+    static const int env_order = [] {
+      const char* e = getenv("FLS_GEMM_ORDER");      // A/B of whole runs: 8, -4, -8
+      return e ? atoi(e) : 0;
+    }();
+    int order = g_v10_order ? g_v10_order : env_order;
+    if (order == 0) order = (N / BN <= 64) ? (K >= 16384 ? -4 : -8) : 8;
+    if (order == -4)
+      hipLaunchKernelGGL((gemm_nt_v10<EPI, 0, 0, -4>), dim3(tiles), dim3(256), 2 * v9::BUF, s, A, W, C, M, N, K, lda,
+                         ldw, ldc, ep);
+    else if (order == -8)
+      hipLaunchKernelGGL((gemm_nt_v10<EPI, 0, 0, -8>), dim3(tiles), dim3(256), 2 * v9::BUF, s, A, W, C, M, N, K, lda,
+                         ldw, ldc, ep);
+    else
+      hipLaunchKernelGGL((gemm_nt_v10<EPI, 0, 0, 8>), dim3(tiles), dim3(256), 2 * v9::BUF, s, A, W, C, M, N, K, lda,
+                         ldw, ldc, ep);
   } else if (var == 9 && fast) {
     static bool attr9 = false;
     if (!attr9) {
@@ -2222,6 +2257,14 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
 }  // namespace
 
 extern "C" int fls_kernels_version(void) { return 5; }
+
+// v10 tile order: 0 = by shape (default), 8 = M-grouped, -4 / -8 = N-grouped (A/B, tests)
+extern "C" int fls_gemm_set_order(int order) {
+  if (order != 0 && order != 8 && order != -4 && order != -8) return -1;
+  const int old = g_v10_order;
+  g_v10_order = order;
+  return old;
+}
 
 // A/B switch for the mid-M kernel (tests / microbenchmarks)
 extern "C" int fls_gemm_set_mid(int on) {
@@ -2300,6 +2343,18 @@ extern "C" int fls_gemm_ablate(int abl, const void* A, const void* W, void* C, i
                            K, K, N, ep);
       }
       break;
+#define FLS_ORD10_CASE(X, G)                                                                                 \
+  case X:                                                                                                    \
+    if ((K / BK) % 2) return -2;                                                                             \
+    (void)hipFuncSetAttribute((const void*)gemm_nt_v10<0, 0, 0, G>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                              2 * v9::BUF);                                                                  \
+    hipLaunchKernelGGL((gemm_nt_v10<0, 0, 0, G>), dim3(tiles), dim3(256), 2 * v9::BUF, (hipStream_t)s, a, w, c, M, \
+                       N, K, K, K, N, ep);                                                                   \
+    break;
+    FLS_ORD10_CASE(80, 2) FLS_ORD10_CASE(81, 4) FLS_ORD10_CASE(82, 8) FLS_ORD10_CASE(83, 16)
+    FLS_ORD10_CASE(84, -4) FLS_ORD10_CASE(85, -8) FLS_ORD10_CASE(86, -16) FLS_ORD10_CASE(87, -2)
+    FLS_ORD10_CASE(88, 1) FLS_ORD10_CASE(89, 8)
+#undef FLS_ORD10_CASE
     case 50:
       if ((K / BK) % 2) return -2;
       (void)hipFuncSetAttribute((const void*)gemm_nt_v11<0, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * v9::BUF);

@@ -330,6 +330,31 @@ def test_gemm_variants_all_epilogues(ops, ref, var):
         ops.k.fls_gemm_set_mid(1)
 
 
+@pytest.mark.parametrize("order", [8, -4, -8])
+def test_gemm_v10_tile_orders(ops, ref, order):
+    """v10 tile orders (M-grouped / N-grouped) only permute which block computes which tile:
+    every epilogue gives the fp32 reference and the same bits as the default order."""
+    M, N, K = 1100, 1536, 1024            # 5 x 6 tiles: ragged last M tile, groups split unevenly
+    ops.k.fls_gemm_set_mid(0)
+    try:
+        x = rnd(M, K, seed=51)
+        w = rnd(N, K, scale=0.05, seed=52)
+        r0 = rnd(M, N, seed=53)
+        base = [ops.gemm(x, w), ops.gemm(x, w, EPI_RESID, out=r0.clone(), resid=r0.clone()),
+                ops.gemm(x, w, EPI_SWIGLU)]
+        assert ops.k.fls_gemm_set_order(order) == 0
+        got = [ops.gemm(x, w), ops.gemm(x, w, EPI_RESID, out=r0.clone(), resid=r0.clone()),
+               ops.gemm(x, w, EPI_SWIGLU)]
+        torch.cuda.synchronize()
+        for a, b in zip(base, got):
+            assert torch.equal(a, b)
+        assert rel_err(got[0], x.float() @ w.float().t()) < 2e-3
+        assert rel_err(got[2].cpu(), ref.swiglu_up(x.float().cpu(), w.float().cpu())) < 3e-3
+    finally:
+        ops.k.fls_gemm_set_order(0)
+        ops.k.fls_gemm_set_mid(1)
+
+
 @pytest.mark.parametrize("M,N,K", [(1, 32000, 1024), (5, 1000, 8192), (16, 33, 96), (7, 100, 160)])
 def test_gemv_skinny(ops, M, N, K):
     x = rnd(M, K, seed=41)
