@@ -420,8 +420,15 @@ __global__ __launch_bounds__(128 * HPB, 2) void attn_fwd_v2(const half_t* __rest
 }
 
 int g_attn_variant = 3;
+int g_attn_mha_v2 = 0;   // odd GQA groups (MHA) on the v2/v3 kernel with one head per block (A/B)
 
 }  // namespace
+
+extern "C" int fls_attn_set_mha_v2(int on) {
+  const int old = g_attn_mha_v2;
+  g_attn_mha_v2 = on ? 1 : 0;
+  return old;
+}
 
 extern "C" int fls_attn_set_variant(int v) {
   if (v < 1 || v > 3) return -1;
@@ -437,8 +444,10 @@ extern "C" int fls_attention(const void* qkv, void* out, const int* work, int n_
   const float scale_log2 = scale * 1.4426950408889634f;
   auto st = (hipStream_t)s;
   const int group = n_q_heads / n_kv_heads;
-  if (g_attn_variant >= 2 && group % 2 == 0 && (head_dim == 64 || head_dim == 128)) {
-    const int hpb = group % 4 == 0 ? 4 : 2;
+  if (g_attn_variant >= 2 && (head_dim == 64 || head_dim == 128) &&
+      (group % 2 == 0 || g_attn_mha_v2)) {
+    // HPB query heads of one KV group per block; odd groups (MHA: Llama-2-7B/13B) one head per block
+    const int hpb = group % 4 == 0 ? 4 : (group % 2 == 0 ? 2 : 1);
     const bool db = g_attn_variant == 3;
     dim3 grid2(n_items, n_q_heads / hpb);
 #define FLS_ATTN2_LAUNCH(HD_, HPB_)                                                                       \
@@ -453,9 +462,9 @@ extern "C" int fls_attention(const void* qkv, void* out, const int* work, int n_
                          scale_log2, (const half_t*)kv0, ld_kv0);                                                                     \
   } while (0)
     if (head_dim == 128) {
-      if (hpb == 4) FLS_ATTN2_LAUNCH(128, 4); else FLS_ATTN2_LAUNCH(128, 2);
+      if (hpb == 4) FLS_ATTN2_LAUNCH(128, 4); else if (hpb == 2) FLS_ATTN2_LAUNCH(128, 2); else FLS_ATTN2_LAUNCH(128, 1);
     } else {
-      if (hpb == 4) FLS_ATTN2_LAUNCH(64, 4); else FLS_ATTN2_LAUNCH(64, 2);
+      if (hpb == 4) FLS_ATTN2_LAUNCH(64, 4); else if (hpb == 2) FLS_ATTN2_LAUNCH(64, 2); else FLS_ATTN2_LAUNCH(64, 1);
     }
 #undef FLS_ATTN2_LAUNCH
     FLS_CHECK_LAUNCH();

@@ -62,6 +62,7 @@ def _load_kernels():
     _bind(lib, "fls_gemm_set_variant", c_int, c_int)
     _bind(lib, "fls_gemm_set_mid", c_int, c_int)
     _bind(lib, "fls_gemm_set_order", c_int, c_int)
+    _bind(lib, "fls_attn_set_mha_v2", c_int, c_int)
     _bind(lib, "fls_gemm_ablate", c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p)
     _bind(lib, "fls_attn_set_variant", c_int, c_int)
     _bind(lib, "fls_attention", c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
