@@ -108,6 +108,155 @@ __device__ __forceinline__ void store_pair(half_t* __restrict__ C, int ldc, int 
   store_pair_off<EPI>(C, ldc, m, n_first, 4 * grp, acc_a, acc_b, ep);
 }
 
+// Epilogue of a wave's 128 (M) x 128 (N) quadrant held as acc[8 row groups][8 subtiles] (v10).
+// store_pair issues each row's operand loads (residual rows, RoPE position + cos/sin) right
+// before that row's stores, and because R may alias C the compiler cannot hoist the next
+// row's loads above them: 8 dependent load -> store round trips per tile while the matrix
+// pipe idles (scripts/gemm_epi_cost.py: RoPE cost 8% of the 70B QKV GEMM, 15% at K = 4096).
+// Here row group u+1's loads are issued before row group u's stores (different rows, so
+// in-place R == C stays correct), the positions of all 8 row groups are loaded up front and
+// the per-column bias once.
+template <int EPI>
+__device__ __forceinline__ void epilogue_quadrant(half_t* __restrict__ C, int ldc, int M, int mrow0, int ncol0,
+                                                  int grp, floatx4 (&acc)[8][8], const Epi& ep) {
+  const int off = 4 * grp;
+  if constexpr (EPI == FLS_EPI_NONE || EPI == FLS_EPI_SWIGLU) {
+    if (EPI == FLS_EPI_SWIGLU || ep.bias == nullptr) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int m = mrow0 + u * 16;
+        if (m < M) {
+#pragma unroll
+          for (int p = 0; p < 4; ++p)
+            store_pair_off<EPI>(C, ldc, m, ncol0 + p * 32, off, acc[u][2 * p], acc[u][2 * p + 1], ep);
+        }
+      }
+      return;
+    }
+  }
+  // per-column bias (same for every row): once, kept as fp16
+  half4 ba[4], bb[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    if (ep.bias) {
+      ba[p] = *(const half4*)(ep.bias + ncol0 + p * 32 + off);
+      bb[p] = *(const half4*)(ep.bias + ncol0 + p * 32 + off + 16);
+    } else {
+      ba[p] = half4{0, 0, 0, 0};
+      bb[p] = half4{0, 0, 0, 0};
+    }
+  }
+  if constexpr (EPI == FLS_EPI_RESID) {
+    half4 ra[2][4], rb[2][4];
+    auto load = [&](int u, int sl) {
+      const int m = min(mrow0 + u * 16, M - 1);
+      const half_t* rp = ep.R + (size_t)m * ep.ldr + ncol0 + off;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        ra[sl][p] = *(const half4*)(rp + p * 32);
+        rb[sl][p] = *(const half4*)(rp + p * 32 + 16);
+      }
+    };
+    load(0, 0);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int sl = u & 1;
+      if (u + 1 < 8) load(u + 1, sl ^ 1);
+      // keep the loads exactly one row group ahead: the cos/sin tables (float) cannot alias C
+      // (half), so without a fence the compiler hoists all 8 rows' loads and spills
+      asm volatile("" ::: "memory");
+      const int m = mrow0 + u * 16;
+      if (m < M) {
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          half4 oa, ob;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            oa[r] = (half_t)(acc[u][2 * p][r] + (float)ba[p][r] + (float)ra[sl][p][r]);
+            ob[r] = (half_t)(acc[u][2 * p + 1][r] + (float)bb[p][r] + (float)rb[sl][p][r]);
+          }
+          half_t* cp = C + (size_t)m * ldc + ncol0 + p * 32 + off;
+          *(half4*)cp = oa;
+          *(half4*)(cp + 16) = ob;
+        }
+      }
+    }
+  } else if constexpr (EPI == FLS_EPI_ROPE) {
+    const int hd = ep.head_dim, half_hd = hd >> 1;
+    int pos[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) pos[u] = ep.pos[min(mrow0 + u * 16, M - 1)];
+    int f0[4];
+    bool rot[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int o = (ncol0 + p * 32 + off) % hd;
+      f0[p] = (o >> 5) * 16 + (o & 15);
+      rot[p] = ncol0 + p * 32 < ep.rope_cols;       // wave-uniform
+    }
+    floatx4 cs[2][4], sn[2][4];
+    auto load = [&](int u, int sl) {
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        if (rot[p]) {
+          cs[sl][p] = *(const floatx4*)(ep.cos_t + (size_t)pos[u] * half_hd + f0[p]);
+          sn[sl][p] = *(const floatx4*)(ep.sin_t + (size_t)pos[u] * half_hd + f0[p]);
+        }
+      }
+    };
+    load(0, 0);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int sl = u & 1;
+      if (u + 1 < 8) load(u + 1, sl ^ 1);
+      // keep the loads exactly one row group ahead: the cos/sin tables (float) cannot alias C
+      // (half), so without a fence the compiler hoists all 8 rows' loads and spills
+      asm volatile("" ::: "memory");
+      const int m = mrow0 + u * 16;
+      if (m < M) {
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          half4 oa, ob;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float x1 = acc[u][2 * p][r] + (float)ba[p][r], x2 = acc[u][2 * p + 1][r] + (float)bb[p][r];
+            if (rot[p]) {
+              const float c = cs[sl][p][r], sv = sn[sl][p][r];
+              const float y1 = x1 * c - x2 * sv, y2 = x2 * c + x1 * sv;
+              x1 = y1;
+              x2 = y2;
+            }
+            oa[r] = (half_t)x1;
+            ob[r] = (half_t)x2;
+          }
+          half_t* cp = C + (size_t)m * ldc + ncol0 + p * 32 + off;
+          *(half4*)cp = oa;
+          *(half4*)(cp + 16) = ob;
+        }
+      }
+    }
+  } else {   // NONE with bias
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int m = mrow0 + u * 16;
+      if (m < M) {
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          half4 oa, ob;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            oa[r] = (half_t)(acc[u][2 * p][r] + (float)ba[p][r]);
+            ob[r] = (half_t)(acc[u][2 * p + 1][r] + (float)bb[p][r]);
+          }
+          half_t* cp = C + (size_t)m * ldc + ncol0 + p * 32 + off;
+          *(half4*)cp = oa;
+          *(half4*)(cp + 16) = ob;
+        }
+      }
+    }
+  }
+}
+
 // ABL (ablation, microbenchmarks only): bit0 = no LDS-DMA in the K loop,
 // bit1 = no fragment ds_reads (stale registers), bit2 = no MFMAs.
 template <int EPI, int ABL = 0, int ORD = 0>
@@ -1702,15 +1851,7 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_v10(const half_t* __restrict__
 #undef V10_W
 #undef V10_X
 
-#pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    const int m = m0 + wm * 128 + u * 16 + fr;
-    if (m < M) {
-#pragma unroll
-      for (int p = 0; p < 4; ++p)
-        store_pair<EPI>(C, ldc, m, n0 + wn * 128 + p * 32, grp, acc[u][2 * p], acc[u][2 * p + 1], ep);
-    }
-  }
+  epilogue_quadrant<EPI>(C, ldc, M, m0 + wm * 128 + fr, n0 + wn * 128, grp, acc, ep);
 }
 
 // ------------------------------------------------------------------ v11
