@@ -58,7 +58,7 @@ int fls_attn_set_variant(int v);   // 1 = 16 rows/wave; 2 = 32 rows/wave + stage
 // kv0 (optional, [P, 2*n_kv*hd] K then V, row stride ld_kv0): range 0 of every work item indexes it
 int fls_attention(const void* qkv, void* out, const int* work, int n_items, int n_q_heads,
                   int n_kv_heads, int head_dim, int ld_qkv, int ld_out, float scale, const void* kv0,
-                  int ld_kv0, fls_stream_t s);
+                  int ld_kv0, int q_block, fls_stream_t s);   // q_block: rows per work item (64 or 128)
 int fls_rmsnorm(const void* x, const void* w, void* y, const int* row_idx, int rows, int H,
                 int ldx, int ldy, float eps, fls_stream_t s);
 int fls_embed(const int* ids, const void* table, void* out, int T, int H, int V, fls_stream_t s);

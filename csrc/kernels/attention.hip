@@ -217,12 +217,14 @@ __global__ __launch_bounds__(256 * HPB) void attn_fwd(const half_t* __restrict__
 // (alpha would be exactly 1).
 // Measured (profiles/r1_attention): 1024-token prefix + 5x64 suffixes, 70B
 // heads: v1 598 -> v3 727 TFLOP/s; 4096-token prefix: 683 -> 870.
-template <int HD, int HPB, bool DB>
-__global__ __launch_bounds__(128 * HPB, 2) void attn_fwd_v2(const half_t* __restrict__ qkv, half_t* __restrict__ out,
+// WPH: waves per query head (32 query rows each) = rows per work item / 32.  WPH = 4 (128-row
+// items) serves multi-head attention, where no other head shares the K/V tile: 4 waves read it.
+template <int HD, int HPB, bool DB, int WPH = 2>
+__global__ __launch_bounds__(64 * WPH * HPB, 2) void attn_fwd_v2(const half_t* __restrict__ qkv, half_t* __restrict__ out,
                                                        const int* __restrict__ work, int nh, int nkv, int ld_qkv,
                                                        int ld_out, float scale_log2,
                                                        const half_t* __restrict__ kv0, int ld_kv0) {
-  constexpr int NT_ = 128 * HPB;
+  constexpr int NT_ = 64 * WPH * HPB;
   constexpr int NS = HD / 32;               // k-steps of QK^T
   constexpr int NU = HD / 16;               // 16-wide d subtiles of O
   constexpr int CH = HD / 8;                // 16-byte chunks per K/V row
@@ -234,9 +236,9 @@ __global__ __launch_bounds__(128 * HPB, 2) void attn_fwd_v2(const half_t* __rest
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int h = blockIdx.y * HPB + (wave >> 1);
+  const int h = blockIdx.y * HPB + wave / WPH;
   const int g = h / (nh / nkv);             // same for every head of the block (HPB | group)
-  const int rbase = (wave & 1) * 32;        // this wave's first query row of the item
+  const int rbase = (wave % WPH) * 32;      // this wave's first query row of the item
 
   const int* wi = work + blockIdx.x * 8;
   const int q_start = wi[0], q_len = wi[1], q_off = wi[2];
@@ -438,12 +440,30 @@ extern "C" int fls_attn_set_variant(int v) {
 
 extern "C" int fls_attention(const void* qkv, void* out, const int* work, int n_items, int n_q_heads,
                              int n_kv_heads, int head_dim, int ld_qkv, int ld_out, float scale, const void* kv0,
-                             int ld_kv0, fls_stream_t s) {
+                             int ld_kv0, int q_block, fls_stream_t s) {
   if (n_items <= 0) return 0;
   if (n_q_heads % n_kv_heads) return -2;
   const float scale_log2 = scale * 1.4426950408889634f;
   auto st = (hipStream_t)s;
   const int group = n_q_heads / n_kv_heads;
+  if (q_block > 64) {
+    // 128-row work items (runtime/batch.py pack_prompts(q_block=128)): 4 waves per query head
+    if (q_block > 128 || (head_dim != 64 && head_dim != 128)) return -5;
+    const int hpb = group % 2 == 0 ? 2 : 1;
+    dim3 grid4(n_items, n_q_heads / hpb);
+#define FLS_ATTN4_LAUNCH(HD_, HPB_)                                                                       \
+  hipLaunchKernelGGL((attn_fwd_v2<HD_, HPB_, true, 4>), grid4, dim3(256 * HPB_), 0, st, (const half_t*)qkv, \
+                     (half_t*)out, work, n_q_heads, n_kv_heads, ld_qkv, ld_out, scale_log2,               \
+                     (const half_t*)kv0, ld_kv0)
+    if (head_dim == 128) {
+      if (hpb == 2) FLS_ATTN4_LAUNCH(128, 2); else FLS_ATTN4_LAUNCH(128, 1);
+    } else {
+      if (hpb == 2) FLS_ATTN4_LAUNCH(64, 2); else FLS_ATTN4_LAUNCH(64, 1);
+    }
+#undef FLS_ATTN4_LAUNCH
+    FLS_CHECK_LAUNCH();
+    return 0;
+  }
   if (g_attn_variant >= 2 && (head_dim == 64 || head_dim == 128) &&
       (group % 2 == 0 || g_attn_mha_v2)) {
     // HPB query heads of one KV group per block; odd groups (MHA: Llama-2-7B/13B) one head per block

@@ -2397,7 +2397,7 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
 
 }  // namespace
 
-extern "C" int fls_kernels_version(void) { return 5; }
+extern "C" int fls_kernels_version(void) { return 6; }
 
 // v10 tile order: 0 = by shape (default), 8 = M-grouped, -4 / -8 = N-grouped (A/B, tests)
 extern "C" int fls_gemm_set_order(int order) {

@@ -48,7 +48,7 @@ def _load_runtime():
     return lib
 
 
-KERNELS_ABI = 5   # bumped whenever a C signature in csrc/include/fls.h changes
+KERNELS_ABI = 6   # bumped whenever a C signature in csrc/include/fls.h changes
 
 
 def _load_kernels():
@@ -66,7 +66,7 @@ def _load_kernels():
     _bind(lib, "fls_gemm_ablate", c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p)
     _bind(lib, "fls_attn_set_variant", c_int, c_int)
     _bind(lib, "fls_attention", c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
-          c_int, c_int, c_float, c_void_p, c_int, c_void_p)
+          c_int, c_int, c_float, c_void_p, c_int, c_int, c_void_p)
     _bind(lib, "fls_rmsnorm", c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
           c_int, c_float, c_void_p)
     _bind(lib, "fls_embed", c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p)

@@ -38,7 +38,7 @@ from .ops import get_ops
 from .parallel.comm import Comm
 from .parallel.planner import ShardPlan, make_plan
 from .runtime.activations import ActivationStore
-from .runtime.batch import PackedBatch, pack_prompts, split_microbatches
+from .runtime.batch import Q_BLOCK, Q_BLOCK_MHA, PackedBatch, pack_prompts, split_microbatches
 from .runtime.prefetch import ShardPrefetcher
 from .runtime.weights import LayerSource
 from .utils import trace
@@ -91,6 +91,9 @@ class ShardedRunner:
         if self.cuda and cfg.head_dim not in (64, 128):
             raise NotImplementedError(f"head_dim={cfg.head_dim}: the HIP attention kernels serve 64 and 128")
         self.act_dtype = act_dtype or (torch.float16 if self.cuda else torch.float32)
+        # multi-head models (odd GQA group): 128-row attention items, 4 waves share each K/V tile
+        mha = (cfg.num_attention_heads // cfg.num_key_value_heads) % 2 == 1
+        self.q_block = Q_BLOCK_MHA if (self.cuda and mha) else Q_BLOCK
         self.ops = get_ops(self.dev)
         cos, sin = rope_tables(cfg, max(cfg.max_position_embeddings, max_token_len),
                                torch.float16, self.dev)
@@ -191,7 +194,7 @@ class ShardedRunner:
         groups = split_microbatches(tps, self.token_budget, suffix_only=cached)
         batches = [pack_prompts([tps[i] for i in g], g, self.prefix_attention,
                                 prefix_offsets=[entry.offsets[i] for i in g] if entry is not None else None,
-                                kv_cached=cached) for g in groups]
+                                kv_cached=cached, q_block=self.q_block) for g in groups]
         if self.hip_graphs:
             return self._run_graphed(tps, batches, t_start)
         self.ctx.prefix_entry = entry

@@ -144,7 +144,8 @@ def run_decoder(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, b
         attn_arg = meta["work_last"] if work_items else batch.last_segments
     else:
         attn_arg = meta["work"] if work_items else batch.segments
-    a = ops.attention(qkv, attn_arg, cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim, kv0=kv0)
+    a = ops.attention(qkv, attn_arg, cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim, kv0=kv0,
+                      q_block=batch.q_block)
     del qkv
     if prune:
         idx = meta["last_idx"]

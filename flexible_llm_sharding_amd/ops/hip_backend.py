@@ -188,7 +188,7 @@ class HipOps:
         return self._pick("qkv_rope", x, wqkv, hip, blt, hip, blt)
 
     # ----------------------------------------------------------- attention
-    def attention(self, qkv, work, n_q_heads, n_kv_heads, head_dim, kv0=None):
+    def attention(self, qkv, work, n_q_heads, n_kv_heads, head_dim, kv0=None, q_block: int = 64):
         """kv0 ([P, 2 * n_kv * hd], K then V): range 0 of every work item reads these rows (prefix cache)."""
         _f16(qkv, "qkv")
         if work.dtype != torch.int32 or not work.is_cuda:
@@ -202,7 +202,7 @@ class HipOps:
         rc = self.k.fls_attention(qkv.data_ptr(), out.data_ptr(), work.data_ptr(), work.shape[0],
                                   n_q_heads, n_kv_heads, head_dim, qkv.stride(0), out.stride(0),
                                   head_dim ** -0.5, kv0.data_ptr() if kv0 is not None else None,
-                                  kv0.stride(0) if kv0 is not None else 0, _stream())
+                                  kv0.stride(0) if kv0 is not None else 0, q_block, _stream())
         _chk(rc, "fls_attention")
         return out
 

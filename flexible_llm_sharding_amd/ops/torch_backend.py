@@ -73,7 +73,7 @@ class TorchOps:
         return torch.cat([qk_out, y[:, qk_cols:]], dim=1).to(x.dtype)
 
     def attention(self, qkv: torch.Tensor, segments, n_q_heads: int, n_kv_heads: int,
-                  head_dim: int, kv0: torch.Tensor = None) -> torch.Tensor:
+                  head_dim: int, kv0: torch.Tensor = None, q_block: int = 64) -> torch.Tensor:
         """Shared-prefix attention over packed segments (see runtime.batch).
 
         ``kv0`` ([P, 2 * n_kv * hd], K then V): range 0 of every segment indexes

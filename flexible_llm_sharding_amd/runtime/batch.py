@@ -29,6 +29,7 @@ import torch
 from ..utils.tokenizer import TokenizedPrompt
 
 Q_BLOCK = 64            # query rows per attention work item (kernel tile)
+Q_BLOCK_MHA = 128       # multi-head models: 4 waves of one query head share each staged K/V tile
 WORK_ITEM_FIELDS = 8    # q_start q_len q_off r0_start r0_len r0_causal r1_start r1_len
 
 
@@ -59,6 +60,7 @@ class PackedBatch:
     padded_tokens: int                    # reference-equivalent token count
     max_pos: int
     kv_cached: bool = False               # prefixes come from a PrefixEntry (range 0 rows index it)
+    q_block: int = Q_BLOCK                # query rows per work item
     pfx_src: Optional[np.ndarray] = None  # capture: packed rows of every prefix token ...
     pfx_dst: Optional[np.ndarray] = None  # ... and their rows in the prefix K/V cache
     _dev: dict = field(default_factory=dict, repr=False)
@@ -88,7 +90,7 @@ class PackedBatch:
 
 def pack_prompts(tps: Sequence[TokenizedPrompt], prompt_ids: Sequence[int],
                  prefix_attention: str = "bidirectional", prefix_offsets: Optional[Sequence[int]] = None,
-                 kv_cached: bool = False) -> PackedBatch:
+                 kv_cached: bool = False, q_block: int = Q_BLOCK) -> PackedBatch:
     """Pack prompts into one token matrix + attention work items.
 
     ``prefix_offsets`` (rows of each prompt's prefix in a PrefixEntry) turns on
@@ -132,24 +134,24 @@ def pack_prompts(tps: Sequence[TokenizedPrompt], prompt_ids: Sequence[int],
         max_pos = max(max_pos, Lp + max([len(s) for s in tp.suffixes] or [0]))
         nsuf.append(tp.n_suffix)
         padded += tp.padded_tokens
-    work = _work_items(segs)
+    work = _work_items(segs, q_block)
     return PackedBatch(
         prompt_ids=list(prompt_ids), n_suffix=nsuf,
         ids=np.asarray(ids, dtype=np.int32), positions=np.asarray(pos, dtype=np.int32),
         segments=segs, work=work,
         last_idx=np.asarray(last, dtype=np.int32), last_segments=lsegs,
         work_last=_work_items(lsegs), num_tokens=t, padded_tokens=padded,
-        max_pos=max_pos, kv_cached=kv_cached,
+        max_pos=max_pos, kv_cached=kv_cached, q_block=q_block,
         pfx_src=np.asarray(src, dtype=np.int64) if (prefix_offsets is not None and not kv_cached) else None,
         pfx_dst=np.asarray(dst, dtype=np.int64) if (prefix_offsets is not None and not kv_cached) else None)
 
 
-def _work_items(segs: Sequence[Segment]) -> np.ndarray:
-    """Segments -> [n_items, 8] int32 work items of at most Q_BLOCK queries."""
+def _work_items(segs: Sequence[Segment], q_block: int = Q_BLOCK) -> np.ndarray:
+    """Segments -> [n_items, 8] int32 work items of at most ``q_block`` queries."""
     work = []
     for sg in segs:
-        for off in range(0, sg.q_len, Q_BLOCK):
-            work.append((sg.q_start + off, min(Q_BLOCK, sg.q_len - off), sg.q_off + off,
+        for off in range(0, sg.q_len, q_block):
+            work.append((sg.q_start + off, min(q_block, sg.q_len - off), sg.q_off + off,
                          sg.r0_start, sg.r0_len, sg.r0_causal, sg.r1_start, sg.r1_len))
     return np.asarray(work, dtype=np.int32).reshape(-1, WORK_ITEM_FIELDS)
 

@@ -25,9 +25,11 @@ def main():
         tps = [TokenizedPrompt(list(range(plen)), [list(range(64))] * 5, 64, [63] * 5) for _ in range(n)]
         b = pack_prompts(tps, list(range(n)), "bidirectional")
         meta = b.device_tensors(dev)
+        b128 = pack_prompts(tps, list(range(n)), "bidirectional", q_block=128)
+        meta128 = b128.device_tensors(dev)
         qkv = torch.randn(b.num_tokens, (nh + 2 * nkv) * hd, device=dev).half()
         fl = layer_flops(cfg, b) - 2.0 * b.num_tokens * cfg.decoder_layer_params()
-        arms = {"v1": (1, 0), "v2_hpb1": (2, 1), "v3_hpb1_db": (3, 1)}
+        arms = {"v1": (1, 0), "v2_hpb1": (2, 1), "v3_hpb1_db": (3, 1), "q128_4waves": (3, 0)}
         ts = {k: [] for k in arms}
         ref = None
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
@@ -35,7 +37,9 @@ def main():
             for k, (var, mha) in arms.items():
                 ops.k.fls_attn_set_variant(var)
                 ops.k.fls_attn_set_mha_v2(mha)
-                o = ops.attention(qkv, meta["work"], nh, nkv, hd)
+                qb = 128 if k == "q128_4waves" else 64
+                wk = meta128["work"] if qb == 128 else meta["work"]
+                o = ops.attention(qkv, wk, nh, nkv, hd, q_block=qb)
                 if rnd == 0:
                     if ref is None:
                         ref = o.float()
@@ -43,7 +47,7 @@ def main():
                     assert err < 2e-2, (k, err)
                 ev[0].record()
                 for _ in range(5):
-                    ops.attention(qkv, meta["work"], nh, nkv, hd)
+                    ops.attention(qkv, wk, nh, nkv, hd, q_block=qb)
                 ev[1].record()
                 torch.cuda.synchronize()
                 ts[k].append(ev[0].elapsed_time(ev[1]) / 5)

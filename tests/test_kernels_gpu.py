@@ -103,17 +103,31 @@ def test_gemm_rope(ops, ref, nh, nkv, hd, M):
     assert rel_err(y.cpu(), r) < 3e-3
 
 
-def _attn_case(nh, nkv, hd, prompts, prefix_attention, seed=0):
+def _attn_case(nh, nkv, hd, prompts, prefix_attention, seed=0, q_block=64):
     from flexible_llm_sharding_amd.runtime.batch import pack_prompts
     from flexible_llm_sharding_amd.utils.tokenizer import TokenizedPrompt
     g = torch.Generator().manual_seed(seed)
     tps = []
     for lp, lens in prompts:
         tps.append(TokenizedPrompt(list(range(lp)), [list(range(l)) for l in lens], max(lens), [l - 1 for l in lens]))
-    b = pack_prompts(tps, list(range(len(tps))), prefix_attention)
+    b = pack_prompts(tps, list(range(len(tps))), prefix_attention, q_block=q_block)
     T = b.num_tokens
     qkv = (torch.randn(T, (nh + 2 * nkv) * hd, generator=g)).to(torch.float16)
     return b, qkv
+
+
+@pytest.mark.parametrize("nh,nkv,hd", [(4, 4, 128), (6, 2, 64), (4, 2, 128), (3, 3, 64)])
+@pytest.mark.parametrize("mode", ["bidirectional", "causal"])
+def test_attention_128_row_items(ops, ref, nh, nkv, hd, mode):
+    """128-row work items (multi-head models): 4 waves per query head share each K/V tile;
+    ragged segments (1..200 rows) cross the 128-row boundary."""
+    prompts = [(70, [5, 64, 1]), (1, [3]), (130, [65, 17, 129]), (200, [33, 64])]
+    b, qkv = _attn_case(nh, nkv, hd, prompts, mode, q_block=128)
+    assert int(b.work[:, 1].max()) == 128
+    y = ops.attention(qkv.to(DEV), b.device_tensors(DEV)["work"], nh, nkv, hd, q_block=128)
+    r = ref.attention(qkv.float(), b.segments, nh, nkv, hd)
+    torch.cuda.synchronize()
+    assert rel_err(y.cpu(), r) < 5e-3
 
 
 @pytest.fixture(params=[1, 2, 3], ids=["attn_v1", "attn_v2", "attn_v2db"])
