@@ -52,6 +52,7 @@ int fls_gemm(const void* A, const void* W, void* C, const void* R, int M, int N,
 int fls_gemm_set_variant(int v);
 int fls_gemm_set_order(int order);   // v10 tile order: 0 by shape, 8 M-grouped, -4/-8 N-grouped
 int fls_gemm_set_mid(int on);   // 64x128-tile kernel for small / medium M (default on)
+int fls_gemm_set_rope_persistent(int on);   // variant 10: RoPE GEMMs on the persistent v13 (default on)
 int fls_gemm_ablate(int abl, const void* A, const void* W, void* C, int M, int N, int K, fls_stream_t s);
 int fls_attn_set_mha_v2(int on);   // odd GQA groups (MHA) on the v2/v3 kernel, one head per block
 int fls_attn_set_variant(int v);   // 1 = 16 rows/wave; 2 = 32 rows/wave + staged prefetch; 3 = 2 + double-buffered LDS (default)

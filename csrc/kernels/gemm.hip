@@ -1854,6 +1854,211 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_v10(const half_t* __restrict__
   epilogue_quadrant<EPI>(C, ldc, M, m0 + wm * 128 + fr, n0 + wn * 128, grp, acc, ep);
 }
 
+// ------------------------------------------------------------------ v13
+// Persistent v10: the grid is one block per CU (multiple of 8, so virtual tile id
+// v = blockIdx.x + i * gridDim.x stays on the XCD that v10's remap assumes) and each
+// block walks its tiles in the same remapped / grouped order as v10.  With one
+// block per CU (256 AGPR accumulators, 128 KiB LDS) v10 leaves the CU idle while a
+// tile's epilogue stores drain and while the next block's first K-tiles are in flight
+// (the fixed per-tile cost of the K sweep, profiles/r1_gemm_study/k_sweep.log:
+// 3-5% of the 70B projections).  Here the next tile's 2-stage prologue DMA is issued
+// BEFORE the current tile's epilogue, so the HBM/L2 latency of the first K-tiles
+// overlaps the epilogue's loads and stores.  Main loop identical to v10 (SCHED 0).
+template <int EPI, int GM = 8>
+__global__ __launch_bounds__(256, 1) void gemm_nt_v13(const half_t* __restrict__ A, const half_t* __restrict__ W,
+                                                    half_t* __restrict__ C, int M, int N, int K, int lda, int ldw,
+                                                    int ldc, Epi ep) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  const int tiles_m = (M + BM - 1) / BM;
+  const int tiles_n = N / BN;
+  const int ntiles = tiles_m * tiles_n;
+  const int q8 = ntiles >> 3, r8 = ntiles & 7;
+  int m0, n0;
+#define V13_TILE(v)                                                                                 \
+  {                                                                                                 \
+    const int xcd_ = (v) & 7, loc_ = (v) >> 3;                                                      \
+    const int b_ = (xcd_ < r8 ? xcd_ * (q8 + 1) : r8 * (q8 + 1) + (xcd_ - r8) * q8) + loc_;         \
+    int tm_, tn_;                                                                                   \
+    if (GM > 0) {                                                                                   \
+      constexpr int GROUP_M = GM > 0 ? GM : 1;                                                      \
+      const int group_ = b_ / (GROUP_M * tiles_n);                                                  \
+      const int first_ = group_ * GROUP_M;                                                          \
+      const int gsz_ = min(tiles_m - first_, GROUP_M);                                              \
+      const int in_ = b_ - group_ * GROUP_M * tiles_n;                                              \
+      tm_ = first_ + in_ % gsz_;                                                                    \
+      tn_ = in_ / gsz_;                                                                             \
+    } else {                                                                                        \
+      constexpr int GROUP_N = GM < 0 ? -GM : 1;                                                     \
+      const int group_ = b_ / (GROUP_N * tiles_m);                                                  \
+      const int first_ = group_ * GROUP_N;                                                          \
+      const int gsz_ = min(tiles_n - first_, GROUP_N);                                              \
+      const int in_ = b_ - group_ * GROUP_N * tiles_m;                                              \
+      tn_ = first_ + in_ % gsz_;                                                                    \
+      tm_ = in_ / gsz_;                                                                             \
+    }                                                                                               \
+    m0 = tm_ * BM;                                                                                  \
+    n0 = tn_ * BN;                                                                                  \
+  }
+
+  const int lr = lane >> 3;
+  const int lc = (lane & 7) ^ lr;
+  int prow[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int j = 4 * wave + i;
+    prow[i] = (j >> 3) * 128 + (j & 7) * 8;
+  }
+  unsigned xo[8], wo[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) wo[i] = (unsigned)((prow[i] + lr) * ldw + lc * 8) * 2u;
+  const char* Ab = (const char*)A;
+  const char* Wb;
+  const size_t wb_off = (size_t)64 * ldw * 2;
+#define V13_SETUP()                                                                                 \
+  {                                                                                                 \
+    _Pragma("unroll") for (int i_ = 0; i_ < 4; ++i_) {                                              \
+      xo[i_] = (unsigned)(min(m0 + prow[i_] + lr, M - 1) * lda + lc * 8) * 2u;                      \
+      xo[4 + i_] = (unsigned)(min(m0 + prow[i_] + 64 + lr, M - 1) * lda + lc * 8) * 2u;             \
+    }                                                                                               \
+    Wb = (const char*)(W + (size_t)n0 * ldw);                                                       \
+  }
+#define V13_X(buf, hb, k0)                                                                         \
+  _Pragma("unroll") for (int i_ = 0; i_ < 4; ++i_)                                                \
+    glds16(Ab + (size_t)(k0) * 2 + xo[(hb) * 4 + i_], smem + (buf) * v9::BUF + (prow[i_] + (hb) * 64) * 128);
+#define V13_W(buf, hb, k0)                                                                         \
+  _Pragma("unroll") for (int i_ = 0; i_ < 4; ++i_)                                                \
+    glds16(Wb + (hb) * wb_off + (size_t)(k0) * 2 + wo[i_], smem + (buf) * v9::BUF + v9::WIMG + (prow[i_] + (hb) * 64) * 128);
+
+  const int wm = wave >> 1, wn = wave & 1;
+  const int fr = lane & 15, grp = lane >> 4;
+  const int sw = fr & 7;
+  const int c0 = ((0 + grp) ^ sw) << 4;
+  const int c1 = ((4 + grp) ^ sw) << 4;
+  const int xrow = (wm * 128 + fr) * 128;
+  const int wrow = v9::WIMG + (wn * 128 + fr) * 128;
+
+  floatx4 acc[8][8];
+  half8 xf[8][2], wf[8][2];
+#define V13_FENCE_ACC()                                                                            \
+  _Pragma("unroll") for (int u_ = 0; u_ < 8; ++u_)                                                \
+  _Pragma("unroll") for (int t_ = 0; t_ < 8; ++t_) asm volatile("" : "+a"(acc[u_][t_]));
+#define V13_RX(buf, h)                                                                             \
+  _Pragma("unroll") for (int u_ = (h) * 4; u_ < (h) * 4 + 4; ++u_) {                              \
+    xf[u_][0] = *(const half8*)(smem + (buf) * v9::BUF + xrow + u_ * 2048 + c0);                  \
+    xf[u_][1] = *(const half8*)(smem + (buf) * v9::BUF + xrow + u_ * 2048 + c1);                  \
+  }
+#define V13_RW(buf, h)                                                                             \
+  _Pragma("unroll") for (int t_ = (h) * 4; t_ < (h) * 4 + 4; ++t_) {                              \
+    wf[t_][0] = *(const half8*)(smem + (buf) * v9::BUF + wrow + t_ * 2048 + c0);                  \
+    wf[t_][1] = *(const half8*)(smem + (buf) * v9::BUF + wrow + t_ * 2048 + c1);                  \
+  }
+// v10's phase with SCHED 0 (reads after even MFMAs 0..14, DMA after MFMAs 17, 20, 23, 26)
+#define V13_PHASE(xh, wh, RX, rbuf, rh, DX, dbuf, dhb, dk0, SYNC)                                  \
+  {                                                                                               \
+    _Pragma("unroll") for (int i_ = 0; i_ < 32; ++i_) {                                           \
+      const int s_ = i_ >> 4, u_ = (xh) * 4 + ((i_ >> 2) & 3), t_ = (wh) * 4 + (i_ & 3);          \
+      mfma_acc_inplace_ordered(acc[u_][t_], wf[t_][s_], xf[u_][s_]);                              \
+      if (i_ < 16 && (i_ & 1) == 0) {                                                             \
+        const int rj_ = i_ >> 1;                                                                  \
+        const int f_ = (rh) * 4 + (rj_ >> 1), k_ = rj_ & 1;                                       \
+        if (RX)                                                                                   \
+          xf[f_][k_] = *(const half8*)(smem + (rbuf) * v9::BUF + xrow + f_ * 2048 + (k_ ? c1 : c0)); \
+        else                                                                                      \
+          wf[f_][k_] = *(const half8*)(smem + (rbuf) * v9::BUF + wrow + f_ * 2048 + (k_ ? c1 : c0)); \
+      }                                                                                           \
+      if (i_ >= 17 && i_ <= 26 && (i_ - 17) % 3 == 0) {                                           \
+        const int p_ = (i_ - 17) / 3;                                                             \
+        if (DX)                                                                                   \
+          glds16(Ab + (size_t)(dk0) * 2 + xo[(dhb) * 4 + p_],                                     \
+                 smem + (dbuf) * v9::BUF + (prow[p_] + (dhb) * 64) * 128);                        \
+        else                                                                                      \
+          glds16(Wb + (dhb) * wb_off + (size_t)(dk0) * 2 + wo[p_],                                \
+                 smem + (dbuf) * v9::BUF + v9::WIMG + (prow[p_] + (dhb) * 64) * 128);             \
+      }                                                                                           \
+    }                                                                                             \
+    if (SYNC) {                                                                                   \
+      __builtin_amdgcn_s_waitcnt(0xC07F);                 /* lgkmcnt(0) */                        \
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");                                           \
+      __builtin_amdgcn_s_barrier();                                                               \
+    }                                                                                             \
+  }
+
+  const int nk = K / BK;                       // even (host-checked)
+  const int kc1 = min(1, nk - 1) * BK;
+#define V13_PROLOGUE_DMA()                                                                         \
+  V13_X(0, 0, 0); V13_W(0, 0, 0); V13_W(0, 1, 0); V13_X(0, 1, 0);                                 \
+  V13_X(1, 0, kc1); V13_W(1, 1, kc1); V13_W(1, 0, kc1); V13_X(1, 1, kc1);
+
+  int v = blockIdx.x;
+  V13_TILE(v);
+  V13_SETUP();
+  V13_PROLOGUE_DMA();
+  bool first = true;
+  while (true) {
+    if (first) {
+      asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+    } else {
+      // the prologue DMA was issued before the previous tile's epilogue loads / stores:
+      // vmcnt cannot count it apart from them
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int t = 0; t < 8; ++t) acc[u][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    V13_FENCE_ACC();
+    V13_RX(0, 0); V13_RW(0, 0);                // SP -1's reads: x0(0), w0(0)
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // zero-init (VALU AGPR writes) must not sit right before the first asm MFMA reading them
+    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+    for (int kt = 0; kt < nk; kt += 2) {
+      const int ka = min(kt + 2, nk - 1) * BK;
+      const int kb = min(kt + 3, nk - 1) * BK;
+      V13_PHASE(0, 0, 0, 0, 1, 1, 0, 0, ka, 0);
+      V13_PHASE(0, 1, 1, 0, 1, 0, 0, 0, ka, 1);
+      V13_PHASE(1, 1, 1, 1, 0, 0, 0, 1, ka, 0);
+      V13_PHASE(1, 0, 0, 1, 1, 1, 0, 1, ka, 1);
+      V13_PHASE(0, 1, 0, 1, 0, 1, 1, 0, kb, 0);
+      V13_PHASE(0, 0, 1, 1, 1, 0, 1, 1, kb, 1);
+      V13_PHASE(1, 0, 1, 0, 0, 0, 1, 0, kb, 0);
+      V13_PHASE(1, 1, 0, 0, 0, 1, 1, 1, kb, 1);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+    V13_FENCE_ACC();
+    const int em0 = m0, en0 = n0;
+    v += gridDim.x;
+    const bool more = v < ntiles;              // block-uniform
+    if (more) {
+      // every wave's LDS reads (lgkmcnt(0) before the last phase's barrier) and DMA
+      // (vmcnt(0) above) of this tile are complete once all waves pass this barrier
+      __builtin_amdgcn_s_barrier();
+      V13_TILE(v);
+      V13_SETUP();
+      V13_PROLOGUE_DMA();
+    }
+    epilogue_quadrant<EPI>(C, ldc, M, em0 + wm * 128 + fr, en0 + wn * 128, grp, acc, ep);
+    if (!more) break;
+    first = false;
+  }
+#undef V13_PROLOGUE_DMA
+#undef V13_FENCE_ACC
+#undef V13_PHASE
+#undef V13_RW
+#undef V13_RX
+#undef V13_W
+#undef V13_X
+#undef V13_SETUP
+#undef V13_TILE
+}
+
 // ------------------------------------------------------------------ v11
 // v10 with the LDS-DMA issued as `buffer_load_dwordx4 ... offen lds` from a
 // buffer resource: every piece of an operand uses the SAME per-lane VGPR
@@ -2237,6 +2442,7 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_v12(const half_t* __restrict__
 
 int g_variant = -1;   // -1: from env FLS_GEMM_VARIANT (default 3)
 int g_v10_order = 0;  // 0: by shape (launch<EPI>), else a fixed GM (fls_gemm_set_order)
+int g_rope_persistent = 1;  // variant 10: QKV + RoPE GEMMs on the persistent v13 (fls_gemm_set_rope_persistent)
 
 int variant() {
   if (g_variant < 0) {
@@ -2279,10 +2485,15 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
     return 0;
   }
   int var = variant();
+  // the persistent v13 (bit-identical to v10) pays off only where the epilogue is heavy enough to
+  // hide the next tile's prologue under it: QKV + RoPE 2.23 -> 2.12 ms on the 70B shape, while the
+  // store-only / residual epilogues lose 1-2% to the vmcnt(0) that also waits for the previous
+  // tile's store acks (profiles/r1_gemm_persistent)
+  if (var == 10 && EPI == FLS_EPI_ROPE && g_rope_persistent) var = 13;
   const bool fast = (N % BN == 0) && (K % BK == 0) && (lda % 8 == 0) && (ldw % 8 == 0) && M > 0;
   // v8/v9 need an even K-tile count (2-tile unrolled body), v9 32-bit X offsets; else v3
   const bool even_k = (K / BK) % 2 == 0;
-  if (((var == 9 || var == 10 || var == 11 || var == 12) && !(even_k && (size_t)M * lda * 2 < (1ull << 32))) || (var == 8 && !even_k))
+  if (((var == 9 || var == 10 || var == 11 || var == 12 || var == 13) && !(even_k && (size_t)M * lda * 2 < (1ull << 32))) || (var == 8 && !even_k))
     var = 3;
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
   const bool fast4 = fast && (K % (2 * v4::BK4) == 0);
@@ -2302,6 +2513,34 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
       attr11 = true;
     }
     hipLaunchKernelGGL(gemm_nt_v11<EPI>, dim3(tiles), dim3(256), 2 * v9::BUF, s, A, W, C, M, N, K, lda, ldw, ldc, ep);
+  } else if (var == 13 && fast) {
+    static bool attr13 = false;
+    static int ncu = 256;
+    if (!attr13) {
+      (void)hipFuncSetAttribute((const void*)gemm_nt_v13<EPI, 8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                2 * v9::BUF);
+      (void)hipFuncSetAttribute((const void*)gemm_nt_v13<EPI, -4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                2 * v9::BUF);
+      (void)hipFuncSetAttribute((const void*)gemm_nt_v13<EPI, -8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                2 * v9::BUF);
+      int dev = 0, n = 0;
+      if (hipGetDevice(&dev) == hipSuccess &&
+          hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n >= 8)
+        ncu = n & ~7;                            // a multiple of 8: virtual tile ids keep their XCD
+      attr13 = true;
+    }
+    const int grid = tiles < ncu ? tiles : ncu;
+    int order = g_v10_order;
+    if (order == 0) order = (N / BN <= 64) ? (K >= 16384 ? -4 : -8) : 8;
+    if (order == -4)
+      hipLaunchKernelGGL((gemm_nt_v13<EPI, -4>), dim3(grid), dim3(256), 2 * v9::BUF, s, A, W, C, M, N, K, lda, ldw,
+                         ldc, ep);
+    else if (order == -8)
+      hipLaunchKernelGGL((gemm_nt_v13<EPI, -8>), dim3(grid), dim3(256), 2 * v9::BUF, s, A, W, C, M, N, K, lda, ldw,
+                         ldc, ep);
+    else
+      hipLaunchKernelGGL((gemm_nt_v13<EPI, 8>), dim3(grid), dim3(256), 2 * v9::BUF, s, A, W, C, M, N, K, lda, ldw,
+                         ldc, ep);
   } else if (var == 10 && fast) {
     static bool attr10 = false;
     if (!attr10) {
@@ -2397,13 +2636,20 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
 
 }  // namespace
 
-extern "C" int fls_kernels_version(void) { return 6; }
+extern "C" int fls_kernels_version(void) { return 7; }
 
 // v10 tile order: 0 = by shape (default), 8 = M-grouped, -4 / -8 = N-grouped (A/B, tests)
 extern "C" int fls_gemm_set_order(int order) {
   if (order != 0 && order != 8 && order != -4 && order != -8) return -1;
   const int old = g_v10_order;
   g_v10_order = order;
+  return old;
+}
+
+// A/B switch: variant 10's RoPE GEMMs on the persistent v13 kernel (1, default) or on v10 (0)
+extern "C" int fls_gemm_set_rope_persistent(int on) {
+  const int old = g_rope_persistent;
+  g_rope_persistent = on ? 1 : 0;
   return old;
 }
 

@@ -48,7 +48,7 @@ def _load_runtime():
     return lib
 
 
-KERNELS_ABI = 6   # bumped whenever a C signature in csrc/include/fls.h changes
+KERNELS_ABI = 7   # bumped whenever a C signature in csrc/include/fls.h changes
 
 
 def _load_kernels():
@@ -61,6 +61,7 @@ def _load_kernels():
           c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p)
     _bind(lib, "fls_gemm_set_variant", c_int, c_int)
     _bind(lib, "fls_gemm_set_mid", c_int, c_int)
+    _bind(lib, "fls_gemm_set_rope_persistent", c_int, c_int)
     _bind(lib, "fls_gemm_set_order", c_int, c_int)
     _bind(lib, "fls_attn_set_mha_v2", c_int, c_int)
     _bind(lib, "fls_gemm_ablate", c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p)
