@@ -38,9 +38,11 @@ def _bench(world, extra, tmp_path):
 
 @pytest.mark.parametrize("world,mode,stages", [(1, "auto", "round_robin"), (2, "auto", "round_robin"),
                                                (2, "mp", "round_robin"), (3, "auto", "round_robin"),
-                                               (6, "mp", "round_robin"), (3, "mp", "contiguous")])
+                                               (6, "mp", "round_robin"), (3, "mp", "contiguous"),
+                                               (8, "auto", "round_robin")])
 def test_bench_contract(tmp_path, world, mode, stages):
-    # world 6 on the 5-layer tiny model: the MP shard padding leaves rank 5 with no layers
+    # world 6 on the 5-layer tiny model: the MP shard padding leaves rank 5 with no layers;
+    # world 8 DP = the driver's 8-GPU scaling point (every layer scatter-loaded 1/8 per rank + all-gather)
     out = _bench(world, ["--mode", mode, "--stages", stages], tmp_path)
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
               "scaling", "vs_baseline", "dtype", "data", "config"):
