@@ -159,7 +159,8 @@ def main(argv=None):
         "metric": METRIC, "value": round(value, 2), "unit": "tokens/s", "n_gpus": world,
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms, 2), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "fp32-cpu-rehearsal" if a.cpu else "fp16",
-        "data": "synthetic prompts (synthetic tokenizer) + random-init Llama-2-70B weights in pinned host RAM",
+        "data": f"synthetic prompts (synthetic tokenizer) + random-init {a.model} weights in "
+                f"{'HBM (resident)' if a.resident else 'pinned host RAM'}",
         "peak_gpu_mem_gb": round(peak / 1e9, 3), "peak_gpu_reserved_gb": round(peak_res / 1e9, 3),
         "scores_finite": finite,
         "config": {"model": a.model if a.num_layers is None else f"{a.model}-L{a.num_layers}",
