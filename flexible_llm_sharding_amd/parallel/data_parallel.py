@@ -94,19 +94,10 @@ class AllGatherPrefetcher(ShardPrefetcher):
         self.store = store
         super().__init__(store, layer_names, shards, device, n_slots=n_slots, resident=resident)
         self._pool = None                     # slices are host-resident: no loader thread
-        self._chunks: Dict[tuple, torch.Tensor] = {}
 
     def shard_bytes(self, k: int) -> int:
         G = self.comm.world
         return sum(_align(self.store.chunk_bytes(self.names[i]) * G) for i in self.shards[k])
-
-    def _chunk_buf(self, s: int, j: int, nbytes: int) -> torch.Tensor:
-        key = (s, j)
-        b = self._chunks.get(key)
-        if b is None or b.numel() < nbytes:
-            b = torch.empty(nbytes, dtype=torch.uint8, device=self.dev)
-            self._chunks[key] = b
-        return b
 
     def _load(self, k: int):
         t0 = time.perf_counter()
@@ -125,9 +116,11 @@ class AllGatherPrefetcher(ShardPrefetcher):
                 nb = self.store.nbytes(name)
                 c = self.store.chunk_bytes(name)
                 region = slot[off:off + c * G]
-                cb = self._chunk_buf(s, j, c)[:c]
-                cb.copy_(self.store.buffers[name][:c], non_blocking=self.cuda)
-                w = self.comm.all_gather_into(region, cb, async_op=self.cuda)
+                # in-place all-gather: this rank's slice is H2D'd straight into its own place in the
+                # slot (RCCL's sendbuff == recvbuff + rank * count form), so no staging buffer in HBM
+                mine = region[self.comm.rank * c:(self.comm.rank + 1) * c]
+                mine.copy_(self.store.buffers[name][:c], non_blocking=self.cuda)
+                w = self.comm.all_gather_into(region, mine, async_op=self.cuda)
                 if self.cuda:
                     works.append(w)
                 views[name] = self.store.layout(name).views(region[:nb], self.dtype)
