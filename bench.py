@@ -1,15 +1,23 @@
 """Benchmark: tokens/s + peak GPU memory of sharded Llama-2-70B scoring (lnps=1).
 
 Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1
-launched by ``torch.distributed.run`` (one rank per GPU, RCCL).  One *step*
-is one full pass of the sharded model over a batch of synthetic
-(prefix, 5 suffixes) prompts — the reference's ``ShardedLlama.__call__``
-(``/root/reference/utils.py:133-305``): every layer's weights streamed from
-pinned host RAM into HBM (layer_num_per_shard=1, double-buffered), every
-prompt scored, fp16 probabilities copied back to the host.  Weights are
-random-init Llama-2-70B generated on the GPU and parked in pinned host
-memory before timing (no network, no checkpoint); prompts are synthetic text
-tokenized inside the timed step by a synthetic tokenizer.
+launched by ``torch.distributed.run`` (one rank per GPU, RCCL), or, without a
+launcher, this script starts the N rank processes itself (before touching any
+GPU) and waits for them.  One *step* is one full pass of the sharded model
+over a batch of synthetic (prefix, 5 suffixes) prompts — the reference's
+``ShardedLlama.__call__`` (``/root/reference/utils.py:133-305``): every
+layer's weights streamed into HBM (layer_num_per_shard=1, double-buffered),
+every prompt scored, fp16 probabilities copied back to the host.  Prompts are
+synthetic text tokenized inside the timed step by a synthetic tokenizer;
+weights are random-init Llama-2-70B (no network, no checkpoint):
+
+* ``--weights host`` (default): generated on the GPU and parked in pinned host
+  RAM before timing (138 GB for 70B);
+* ``--weights stream``: written once as per-layer safetensors files
+  (``--ckpt-dir``; ``--unique-layers K`` hard-links decoder layers >= K to the
+  first K so 70B fits a small disk) and re-read from the files on every pass
+  through the native streamer's pinned chunk ring (~256 MB of pinned RAM) —
+  the reference's small-RAM mode.  ``--o-direct`` bypasses the page cache.
 
 Scaling is weak: each GPU adds ``--prompts-per-gpu`` prompts.  N>1 runs the
 data-parallel schedule (each GPU scores its own prompts; every layer is
@@ -17,16 +25,21 @@ scatter-loaded 1/N per GPU over its own PCIe link and re-assembled in HBM by
 an RCCL all-gather over xGMI), or with ``--mode mp`` the reference's default
 model-parallel schedule (shard k on GPU k mod N, RCCL send/recv of
 activations; each GPU streams only its own shards).
+
+Memory is reported as measured: ``peak_gpu_mem_gb`` (allocator high-water),
+``peak_device_used_gb`` (``hipMemGetInfo`` total - free sampled after every
+step: context, code objects, RCCL buffers and allocator slack included),
+``host_pinned_gb`` and ``host_peak_rss_gb``.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
-
-import torch
 
 METRIC = "tokens/sec + peak GPU mem, Llama-2-70B layer_num_per_shard=1 at 1/2/4/8 MI355X"
 
@@ -36,7 +49,7 @@ def log(rank, *a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def main(argv=None):
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -53,29 +66,86 @@ def main(argv=None):
     ap.add_argument("--stages", default="round_robin", choices=["round_robin", "contiguous"],
                     help="--mode mp: shard k on GPU k mod N (reference) or one contiguous stage per GPU")
     ap.add_argument("--token-budget", type=int, default=16384)
+    ap.add_argument("--max-vram-gb", type=float, default=None, help="size token budget / MLP chunk to this HBM cap")
     ap.add_argument("--resident", action="store_true")
     ap.add_argument("--hip-graphs", action="store_true", help="with --resident: whole-forward HIP graph replay")
     ap.add_argument("--no-prune-last", action="store_true",
                     help="compute every row in the last decoder layer (A/B of the scored-rows-only layer)")
     ap.add_argument("--prefix-attention", default="bidirectional")
+    ap.add_argument("--weights", default="host", choices=["host", "stream"])
+    ap.add_argument("--ckpt-dir", default=None, help="--weights stream: layer-file directory (written if absent)")
+    ap.add_argument("--ckpt-dtype", default="float16", choices=["float16", "bfloat16"])
+    ap.add_argument("--unique-layers", type=int, default=8)
+    ap.add_argument("--o-direct", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--cpu", action="store_true", help="CPU/gloo rehearsal of the same code path (tests only)")
-    a = ap.parse_args(argv)
+    return ap.parse_args(argv)
+
+
+def spawn_ranks(a, argv) -> int:
+    """--gpus N without a launcher: start N rank processes (children, no exec) and wait."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(a.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus),
+                   LOCAL_WORLD_SIZE=str(a.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    try:
+        for p in procs:
+            rc = max(rc, p.wait())
+            if rc:
+                break                     # one rank failed: stop the others (no hung collectives)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc
+
+
+def ensure_checkpoint(cfg, d: str, dtype: str, unique: int, rank: int, comm, progress) -> None:
+    """Write the synthetic per-layer checkpoint once (rank 0; a marker file makes it reusable)."""
+    import torch
+    from flexible_llm_sharding_amd.utils.synthetic import write_synthetic_checkpoint
+    marker = os.path.join(d, ".fls_bench_complete")
+    if rank == 0 and not os.path.exists(marker):
+        dev = "cpu" if not torch.cuda.is_available() else torch.device("cuda", torch.cuda.current_device())
+        write_synthetic_checkpoint(cfg, d, seed=0, dtype=getattr(torch, dtype), unique_layers=unique,
+                                   device=dev, progress=progress)
+        open(marker, "w").close()
+    comm.barrier()
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    a = parse(argv)
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn_ranks(a, argv)
+
+    import resource
+
+    import numpy as np
+    import torch
 
     from flexible_llm_sharding_amd.config import preset
     from flexible_llm_sharding_amd.engine import ShardedRunner
     from flexible_llm_sharding_amd.parallel.comm import Comm
     from flexible_llm_sharding_amd.parallel.data_parallel import AllGatherPrefetcher, SlicedHostStore
     from flexible_llm_sharding_amd.parallel.planner import make_plan
+    from flexible_llm_sharding_amd.runtime import hostmem
+    from flexible_llm_sharding_amd.runtime.stream import FileLayerSource
     from flexible_llm_sharding_amd.runtime.weights import HostStore
     from flexible_llm_sharding_amd.utils.synthetic import synthetic_prompts
     from flexible_llm_sharding_amd.utils.tokenizer import load_tokenizer, write_synthetic_tokenizer
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != a.gpus:
-        if a.gpus > 1:
-            raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch with torch.distributed.run")
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
     comm = Comm.from_env("cpu" if a.cpu else "cuda")
     rank = comm.rank
     if a.cpu:
@@ -93,15 +163,25 @@ def main(argv=None):
     plan = make_plan(len(names), a.lnps, world, rank, dp, a.stages)
     mine = sorted({i for sh in plan.my_shards for i in sh})
     t0 = time.perf_counter()
-    log(rank, f"[bench] generating {len(mine)} random-init {a.model} layers on {dev} -> pinned host ...")
-    prog = lambda i, n: log(rank, f"[bench]   layer {i}/{n} ({time.perf_counter() - t0:.0f}s)")  # noqa: E731
-    if dp:
-        # scatter-load: this rank keeps 1/G of every layer; layers re-assembled by RCCL all-gather
-        store = SlicedHostStore.synthetic(cfg, dev, rank, world, seed=a.seed, names=[names[i] for i in mine],
-                                          progress=prog)
+    prog = lambda i, n: log(rank, f"[bench]   layer {i}/{n} ({time.perf_counter() - t0:.0f}s)") if i % 10 == 0 else None  # noqa: E731
+    if a.weights == "stream":
+        ckpt = a.ckpt_dir or f"/tmp/fls_bench_ckpt_{a.model}{'' if a.num_layers is None else f'-L{a.num_layers}'}_{a.ckpt_dtype}_u{a.unique_layers}"
+        log(rank, f"[bench] per-layer checkpoint {ckpt} (unique decoder layers: {a.unique_layers}) ...")
+        ensure_checkpoint(cfg, ckpt, a.ckpt_dtype, a.unique_layers, rank, comm, prog)
+        store = FileLayerSource(cfg, ckpt, names=[names[i] for i in mine], direct=a.o_direct)
+        data_w = (f"random-init {a.model} weights as per-layer {a.ckpt_dtype} safetensors files "
+                  f"({a.unique_layers} distinct decoder layers, the rest hard links), streamed from the files "
+                  f"every pass ({'O_DIRECT' if a.o_direct else 'page cache'})")
     else:
-        store = HostStore.synthetic(cfg, dev, seed=a.seed, names=[names[i] for i in mine], progress=prog)
-    log(rank, f"[bench] host store {store.total_bytes / 1e9:.1f} GB in {time.perf_counter() - t0:.1f}s")
+        log(rank, f"[bench] generating {len(mine)} random-init {a.model} layers on {dev} -> pinned host ...")
+        if dp:
+            # scatter-load: this rank keeps 1/G of every layer; layers re-assembled by RCCL all-gather
+            store = SlicedHostStore.synthetic(cfg, dev, rank, world, seed=a.seed, names=[names[i] for i in mine],
+                                              progress=prog)
+        else:
+            store = HostStore.synthetic(cfg, dev, seed=a.seed, names=[names[i] for i in mine], progress=prog)
+        log(rank, f"[bench] host store {store.total_bytes / 1e9:.1f} GB in {time.perf_counter() - t0:.1f}s")
+        data_w = f"random-init {a.model} weights in {'HBM (resident)' if a.resident else 'pinned host RAM'}"
 
     tok_dir = f"/tmp/fls_bench_tok_{os.getpid()}"
     write_synthetic_tokenizer(tok_dir, cfg.vocab_size)
@@ -117,13 +197,24 @@ def main(argv=None):
                            disk_folder=f"/tmp/fls_bench_spill_{rank}", prefix_attention=a.prefix_attention,
                            token_budget=a.token_budget, resident=a.resident, comm=comm, data_parallel=dp,
                            prefetcher=pf, hip_graphs=a.hip_graphs, prune_last_layer=not a.no_prune_last,
-                           pipeline_stages=a.stages)
+                           pipeline_stages=a.stages, max_vram_gb=a.max_vram_gb)
+    if runner.vram_plan:
+        log(rank, f"[bench] --max-vram-gb {a.max_vram_gb}: {runner.vram_plan}")
+    dev_used_peak = 0.0
+
+    def sample_device():
+        nonlocal dev_used_peak
+        if not a.cpu:
+            free, total = torch.cuda.mem_get_info(dev)
+            dev_used_peak = max(dev_used_peak, float(total - free))
+
     if not a.cpu:
         torch.cuda.reset_peak_memory_stats(dev)
 
     for i in range(a.warmup):
         tw = time.perf_counter()
         runner(prompts)
+        sample_device()
         log(rank, f"[bench] warmup {i}: {time.perf_counter() - tw:.2f}s")
     comm.barrier()
     sync()
@@ -136,10 +227,13 @@ def main(argv=None):
     sync()
     comm.barrier()
     elapsed = time.perf_counter() - t_start
+    sample_device()
     if not a.cpu:
         ms_ = torch.cuda.memory_stats(dev)
         log(rank, f"[bench] allocator: device mallocs {ms_.get('num_device_alloc')}, "
                   f"retries {ms_.get('num_alloc_retries')}, reserved {ms_.get('reserved_bytes.all.peak', 0) / 1e9:.2f} GB")
+    if a.weights == "stream":
+        log(rank, f"[bench] streamer: {json.dumps({k: round(v, 3) for k, v in store.stats().items()})}")
     elapsed = comm.all_reduce_max(elapsed)
 
     tok_step = runner.stats["tokens"]
@@ -149,20 +243,30 @@ def main(argv=None):
         padded_step = comm.all_reduce_sum(padded_step)
     peak = comm.all_reduce_max(0.0 if a.cpu else float(torch.cuda.max_memory_allocated(dev)))
     peak_res = comm.all_reduce_max(0.0 if a.cpu else float(torch.cuda.max_memory_reserved(dev)))
+    dev_used_peak = comm.all_reduce_max(dev_used_peak)
+    pinned = hostmem.pinned_peak + (store.pinned_bytes() if a.weights == "stream" else 0)
+    pinned = comm.all_reduce_max(float(pinned))
+    rss = comm.all_reduce_max(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss * 1024.0)
     # every score this rank produced must be a finite probability (guards the timed path's numerics)
-    import numpy as np
     finite = all(np.isfinite(o.astype(np.float32)).all() for o in (outs or []) if o is not None)
     finite = comm.all_reduce_min(1.0 if finite else 0.0) >= 1.0
+    # which ranks / devices took part (the process group the collectives actually ran on)
+    import torch.distributed as dist
+    pg_world = dist.get_world_size() if dist.is_initialized() else 1
+    devices = comm.all_gather_object(str(dev) if a.cpu else f"{dev}:{torch.cuda.get_device_properties(dev).name}")
     ms = elapsed / a.steps * 1000.0
     value = tok_step * a.steps / elapsed
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "tokens/s", "n_gpus": world,
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms, 2), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "fp32-cpu-rehearsal" if a.cpu else "fp16",
-        "data": f"synthetic prompts (synthetic tokenizer) + random-init {a.model} weights in "
-                f"{'HBM (resident)' if a.resident else 'pinned host RAM'}",
+        "data": f"synthetic prompts (synthetic tokenizer) + {data_w}",
         "peak_gpu_mem_gb": round(peak / 1e9, 3), "peak_gpu_reserved_gb": round(peak_res / 1e9, 3),
+        "peak_device_used_gb": round(dev_used_peak / 1e9, 3),
+        "host_pinned_gb": round(pinned / 1e9, 3), "host_peak_rss_gb": round(rss / 1e9, 3),
         "scores_finite": finite,
+        "world": world, "process_group_ranks": pg_world,
+        "backend": comm.backend or ("none" if world == 1 else "?"), "rank_devices": devices,
         "config": {"model": a.model if a.num_layers is None else f"{a.model}-L{a.num_layers}",
                    "global_batch": n_prompts * (world if dp else 1),
                    "seq_len": a.prefix_len + a.suffix_len,
@@ -171,8 +275,9 @@ def main(argv=None):
                    "layer_num_per_shard": a.lnps, "storage_location": a.storage,
                    "parallelism": (f"pp{world}-{a.stages.replace('_', '')}" if mode == "mp" else
                                    (f"dp{world}-allgather-weights" if dp else "single")),
-                   "resident": a.resident, "hip_graphs": bool(runner.hip_graphs), "token_budget": a.token_budget,
-                   "gemm_backend": os.environ.get("FLS_GEMM_BACKEND", "hip") if dev.type == "cuda" else "torch"},
+                   "weights": a.weights, "resident": a.resident, "hip_graphs": bool(runner.hip_graphs),
+                   "token_budget": runner.token_budget, "mlp_chunk": runner.mlp_chunk,
+                   "max_vram_gb": a.max_vram_gb},
     }
     if rank == 0:
         print(json.dumps(out), flush=True)

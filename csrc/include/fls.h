@@ -36,24 +36,42 @@ uint64_t fls_st_data_offset(void* h);
 void  fls_st_close(void* h);
 int   fls_mem_info(uint64_t* free_b, uint64_t* total_b);
 
+// weight streamer: file byte ranges -> pinned chunk ring -> HBM (runtime/stream.py)
+typedef struct {
+  uint64_t file_off;   // byte offset in the file
+  uint64_t nbytes;     // bytes in the file
+  uint64_t dst_off;    // byte offset in the destination (HBM slot / host buffer)
+  int32_t kind;        // 0 raw copy, 1 fp32 in the file -> fp16 (nbytes / 2 written)
+  int32_t pad;
+} fls_piece_t;
+void*   fls_streamer_create(int device, uint64_t chunk_bytes, int n_chunks, int io_threads, int direct);
+uint64_t fls_streamer_pinned_bytes(void* h);
+int64_t fls_streamer_load(void* h, const char* path, const fls_piece_t* pieces, int n, void* dst_dev,
+                          fls_stream_t stream);
+int64_t fls_stream_read_host(const char* path, const fls_piece_t* pieces, int n, void* dst, int io_threads);
+int     fls_streamer_stats(void* h, double* read_s, double* wait_s, uint64_t* read_bytes, uint64_t* h2d_bytes,
+                           int* direct_fallbacks);
+void    fls_streamer_destroy(void* h);
+void    fls_f32_to_f16(const float* src, uint16_t* dst, uint64_t n);
+
 // ----------------------------------------------------------------- kernels
 int fls_kernels_version(void);
 // epilogue codes for fls_gemm
 enum { FLS_EPI_NONE = 0, FLS_EPI_RESID = 1, FLS_EPI_SWIGLU = 2, FLS_EPI_ROPE = 3 };
 // C[M, N'] = epi(A[M,K] . W[N,K]^T).  fp16 in / fp32 accumulate / fp16 out.
 //   RESID : C = acc + R (R may alias C)
-//   SWIGLU: W rows gate/up interleaved per 16; C has N/2 columns = silu(g)*u
-//   ROPE  : columns < rope_cols are rotated (RoPE-pair-permuted heads of
-//           head_dim) with pos[m] and fp32 tables cos/sin [maxpos, head_dim/2]
+//   SWIGLU: W = [gate (N/2 rows); up (N/2 rows)]; C has N/2 columns = silu(g)*u
+//   ROPE  : columns < rope_cols are rotated (HF rotate-half, natural head-dim
+//           order, head_dim 64 or 128) with pos[m] and fp32 tables cos/sin
+//           [maxpos, head_dim/2]
 int fls_gemm(const void* A, const void* W, void* C, const void* R, int M, int N, int K,
              int lda, int ldw, int ldc, int ldr, int epi, const int* pos, const float* cos_t,
              const float* sin_t, int rope_cols, int head_dim, const void* bias, fls_stream_t s);
-// shared-prefix / varlen flash attention over packed work items (int32 x8)
-int fls_gemm_set_variant(int v);
-int fls_gemm_set_order(int order);   // v10 tile order: 0 by shape, 8 M-grouped, -4/-8 N-grouped
+int fls_gemm_set_variant(int v);     // 10 (default) or 13 (every epilogue on the persistent kernel)
+int fls_gemm_set_order(int order);   // tile order: 0 by shape, 8 M-grouped, -4/-8 N-grouped
 int fls_gemm_set_mid(int on);   // 64x128-tile kernel for small / medium M (default on)
-int fls_gemm_set_rope_persistent(int on);   // variant 10: RoPE GEMMs on the persistent v13 (default on)
-int fls_gemm_ablate(int abl, const void* A, const void* W, void* C, int M, int N, int K, fls_stream_t s);
+int fls_gemm_set_rope_persistent(int on);   // RoPE GEMMs on the persistent v13 (default on)
+// shared-prefix / varlen flash attention over packed work items (int32 x8)
 int fls_attn_set_mha_v2(int on);   // odd GQA groups (MHA) on the v2/v3 kernel, one head per block
 int fls_attn_set_variant(int v);   // 1 = 16 rows/wave; 2 = 32 rows/wave + staged prefetch; 3 = 2 + double-buffered LDS (default)
 // kv0 (optional, [P, 2*n_kv*hd] K then V, row stride ld_kv0): range 0 of every work item indexes it
@@ -64,9 +82,8 @@ int fls_rmsnorm(const void* x, const void* w, void* y, const int* row_idx, int r
                 int ldx, int ldy, float eps, fls_stream_t s);
 int fls_embed(const int* ids, const void* table, void* out, int T, int H, int V, fls_stream_t s);
 int fls_softmax_rows(const void* logits, void* probs, int rows, int V, fls_stream_t s);
-int fls_rope_inplace(void* y, const int* pos, const float* cos_t, const float* sin_t, int M, int ld,
-                     int rope_cols, int head_dim, fls_stream_t s);
-int fls_swiglu(const void* y, void* out, int M, int I, int ldy, int ldo, fls_stream_t s);
+// dst = fp16(src): src_dtype 1 = bf16 (in place allowed), 2 = fp32 (no overlap)
+int fls_cast_f16(void* dst, const void* src, int src_dtype, uint64_t n, fls_stream_t s);
 // C[M,N] = X[M,K] W[N,K]^T for M <= 16 (skinny LM head); K % 32 == 0
 int fls_gemv_skinny(const void* x, const void* w, void* c, int M, int N, int K, int ldx, int ldw, int ldc,
                     fls_stream_t s);

@@ -1,5 +1,6 @@
 // Memory-bound kernels (gfx950): RMSNorm (optionally row-gathered), token
-// embedding gather, vocab softmax, synthetic weight fill.
+// embedding gather, vocab softmax, synthetic weight fill, weight dtype casts,
+// skinny-M GEMV.
 // All loads/stores are 16-byte vectors (guide G13: scalar fp16 loads cost
 // ~2x); one 256-thread block per row; fp32 statistics.
 #include "common.h"
@@ -170,59 +171,50 @@ __global__ __launch_bounds__(256) void fill_random_kernel(half_t* __restrict__ d
 }
 
 
-// ---------------------------------------------------------------- epilogues
-// Stand-alone versions of the GEMM epilogues, for when the projection itself
-// runs as a plain library GEMM (hipBLASLt): RoPE on the pair-permuted q/k
-// columns in place, and SwiGLU over 16-column interleaved gate/up blocks.
-// 8 columns (16 B) per thread, fp32 math.
-__global__ __launch_bounds__(256) void rope_inplace_kernel(half_t* __restrict__ y, const int* __restrict__ pos,
-                                                         const float* __restrict__ cos_t,
-                                                         const float* __restrict__ sin_t, int M, int ld,
-                                                         int rope_cols, int head_dim) {
-  // work item = (row, 32-column pair block, 8-column quarter of its first half)
-  const int per_row = (rope_cols / 32) * 2;
-  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= (long long)M * per_row) return;
-  const int m = (int)(idx / per_row);
-  const int r = (int)(idx % per_row);
-  const int blk = r >> 1, q = r & 1;          // pair block, 8-col quarter (0/1) inside 16
-  const int c1 = blk * 32 + q * 8;            // first-half columns c1..c1+7, partner +16
-  const int o = c1 % head_dim;
-  const int f0 = (o >> 5) * 16 + (o & 15);
-  const int p = pos[m];
-  const float* cr = cos_t + (size_t)p * (head_dim >> 1) + f0;
-  const float* sr = sin_t + (size_t)p * (head_dim >> 1) + f0;
-  half_t* row = y + (size_t)m * ld;
-  half8 a = *(half8*)(row + c1);
-  half8 b = *(half8*)(row + c1 + 16);
-  half8 oa, ob;
+// ---------------------------------------------------------------- dtype casts
+// Weights stream from the checkpoint as raw bytes (runtime/stream.py); bf16 / fp32
+// tensors are converted to the fp16 compute dtype on the copy stream once their DMA
+// has landed (the reference casts in set_module_tensor_to_device, utils.py:130).
+// Round-to-nearest-even, overflow to +-inf: torch's .to(float16).  bf16 -> fp16 may
+// run in place (same element size: every thread reads, then rewrites, its own 8
+// elements).  8 elements (16 B of output) per thread.
+template <int SRC, bool VEC>   // SRC 1 = bf16, 2 = fp32; VEC: 16-byte aligned pointers
+__global__ __launch_bounds__(256) void cast_f16_kernel(half_t* dst, const void* src, uint64_t n) {
+  const uint64_t base = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (base >= n) return;
+  float f[8];
+  const int cnt = (VEC && base + 8 <= n) ? 8 : (int)min((uint64_t)8, n - base);
+  if constexpr (SRC == 1) {
+    const uint16_t* s = (const uint16_t*)src + base;
+    if (VEC && cnt == 8) {
+      const uint4 v = *(const uint4*)s;
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const float cs = cr[j], sn = sr[j], x1 = (float)a[j], x2 = (float)b[j];
-    oa[j] = (half_t)(x1 * cs - x2 * sn);
-    ob[j] = (half_t)(x2 * cs + x1 * sn);
+      for (int j = 0; j < 4; ++j) {
+        f[2 * j] = __uint_as_float(w[j] << 16);
+        f[2 * j + 1] = __uint_as_float(w[j] & 0xFFFF0000u);
+      }
+    } else {
+      for (int j = 0; j < cnt; ++j) f[j] = __uint_as_float((uint32_t)s[j] << 16);
+    }
+  } else {
+    const float* s = (const float*)src + base;
+    if (VEC && cnt == 8) {
+      const float4 a = *(const float4*)s, b = *(const float4*)(s + 4);
+      f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+    } else {
+      for (int j = 0; j < cnt; ++j) f[j] = s[j];
+    }
   }
-  *(half8*)(row + c1) = oa;
-  *(half8*)(row + c1 + 16) = ob;
-}
-
-__global__ __launch_bounds__(256) void swiglu_kernel(const half_t* __restrict__ y, half_t* __restrict__ out, int M,
-                                                   int I, int ldy, int ldo) {
-  const int per_row = I / 8;
-  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= (long long)M * per_row) return;
-  const int m = (int)(idx / per_row);
-  const int c = (int)(idx % per_row) * 8;      // output columns c..c+7
-  const int blk = c >> 4, in = c & 15;
-  const half_t* row = y + (size_t)m * ldy + blk * 32 + in;
-  const half8 g = *(const half8*)row;
-  const half8 u = *(const half8*)(row + 16);
-  half8 o;
+  if (VEC && cnt == 8) {
+    half8 o;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) o[j] = (half_t)(silu((float)g[j]) * (float)u[j]);
-  *(half8*)(out + (size_t)m * ldo + c) = o;
+    for (int j = 0; j < 8; ++j) o[j] = (half_t)f[j];
+    *(half8*)(dst + base) = o;
+  } else {
+    for (int j = 0; j < cnt; ++j) dst[base + j] = (half_t)f[j];
+  }
 }
-
 
 // ---------------------------------------------------------------- skinny GEMV
 // C[M, N] = X[M, K] . W[N, K]^T for M <= 16 (LM head of a small batch, K12):
@@ -322,23 +314,23 @@ extern "C" int fls_fill_random(void* dst, uint64_t n_elems, uint64_t seed, float
   return 0;
 }
 
-extern "C" int fls_rope_inplace(void* y, const int* pos, const float* cos_t, const float* sin_t, int M, int ld,
-                                int rope_cols, int head_dim, fls_stream_t s) {
-  if (M <= 0 || rope_cols <= 0) return 0;
-  if (rope_cols % 32 || head_dim % 32 || ld % 8) return -2;
-  const long long items = (long long)M * (rope_cols / 32) * 2;
-  hipLaunchKernelGGL(rope_inplace_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, (hipStream_t)s,
-                     (half_t*)y, pos, cos_t, sin_t, M, ld, rope_cols, head_dim);
-  FLS_CHECK_LAUNCH();
-  return 0;
-}
-
-extern "C" int fls_swiglu(const void* y, void* out, int M, int I, int ldy, int ldo, fls_stream_t s) {
-  if (M <= 0 || I <= 0) return 0;
-  if (I % 16 || ldy % 8 || ldo % 8) return -2;
-  const long long items = (long long)M * (I / 8);
-  hipLaunchKernelGGL(swiglu_kernel, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, (hipStream_t)s,
-                     (const half_t*)y, (half_t*)out, M, I, ldy, ldo);
+// dst[i] = fp16(src[i]) for src_dtype 1 = bf16 (dst may equal src), 2 = fp32 (no overlap)
+extern "C" int fls_cast_f16(void* dst, const void* src, int src_dtype, uint64_t n, fls_stream_t s) {
+  if (n == 0) return 0;
+  if (src_dtype == 2 && (const char*)dst < (const char*)src + 4 * n && (const char*)src < (const char*)dst + 2 * n)
+    return -3;
+  if (src_dtype == 1 && dst != src && (const char*)dst < (const char*)src + 2 * n &&
+      (const char*)src < (const char*)dst + 2 * n)
+    return -3;
+  const bool vec = ((((uintptr_t)dst | (uintptr_t)src) & 15) == 0);
+  const uint64_t blocks = ((n + 7) / 8 + 255) / 256;
+  auto st = (hipStream_t)s;
+  const dim3 g((unsigned)blocks), b(256);
+  if (src_dtype == 1 && vec) hipLaunchKernelGGL((cast_f16_kernel<1, true>), g, b, 0, st, (half_t*)dst, src, n);
+  else if (src_dtype == 1) hipLaunchKernelGGL((cast_f16_kernel<1, false>), g, b, 0, st, (half_t*)dst, src, n);
+  else if (src_dtype == 2 && vec) hipLaunchKernelGGL((cast_f16_kernel<2, true>), g, b, 0, st, (half_t*)dst, src, n);
+  else if (src_dtype == 2) hipLaunchKernelGGL((cast_f16_kernel<2, false>), g, b, 0, st, (half_t*)dst, src, n);
+  else return -1;
   FLS_CHECK_LAUNCH();
   return 0;
 }

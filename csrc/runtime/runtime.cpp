@@ -9,7 +9,12 @@
 //   activation spill files (reference: np.save, utils.py:171-177);
 // * a block gather used to repack weights into the HBM-native layout;
 // * a safetensors header index (8-byte length + JSON) with a small JSON
-//   scanner specialised for the format.
+//   scanner specialised for the format;
+// * the weight streamer: per-layer file byte ranges -> a ring of pinned chunk
+//   buffers (persistent pread pool, optional O_DIRECT) -> hipMemcpyAsync of
+//   every tensor piece straight to its place in the HBM weight slot, on the
+//   caller's copy stream (reference: read + deserialize + per-tensor pageable
+//   H2D, utils.py:121-131).
 //
 // Built with g++ against libamdhip64 (host code only).
 #include "fls.h"
@@ -19,6 +24,10 @@
 #include <algorithm>
 #include <atomic>
 #include <cerrno>
+#include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -34,7 +43,8 @@ extern "C" int fls_rt_version(void) { return 1; }
 extern "C" void* fls_pinned_alloc(uint64_t bytes) {
   void* p = nullptr;
   if (bytes == 0) bytes = 1;
-  hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault);
+  // portable: the same pinned block may feed H2D copies of any device of the process
+  hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocPortable);
   if (e != hipSuccess) { (void)hipGetLastError(); return nullptr; }
   return p;
 }
@@ -290,3 +300,334 @@ extern "C" int fls_st_info(void* h, int i, char* name, int name_cap, char* dtype
 }
 
 extern "C" void fls_st_close(void* h) { delete (StFile*)h; }
+
+// ------------------------------------------------------------- streamer
+namespace {
+
+// fp32 -> fp16 bits, round to nearest even, overflow -> inf, NaN kept (torch .to(float16))
+inline uint16_t f32_to_f16_bits(float f) {
+  uint32_t x;
+  std::memcpy(&x, &f, 4);
+  const uint32_t sign = (x >> 16) & 0x8000u;
+  const uint32_t ax = x & 0x7FFFFFFFu;
+  if (ax >= 0x7F800000u) return (uint16_t)(sign | 0x7C00u | (ax > 0x7F800000u ? 0x200u : 0u));
+  if (ax >= 0x477FF000u) return (uint16_t)(sign | 0x7C00u);          // rounds past 65504 -> inf
+  if (ax < 0x38800000u) {                                            // fp16 subnormal or zero
+    if (ax < 0x33000000u) return (uint16_t)sign;                     // < 2^-25: rounds to 0
+    const uint32_t m = (ax & 0x7FFFFFu) | 0x800000u;
+    const int shift = 126 - (int)(ax >> 23);                         // 14 .. 24
+    const uint32_t r = m >> shift, rem = m & ((1u << shift) - 1), half = 1u << (shift - 1);
+    return (uint16_t)(sign | (r + (rem > half || (rem == half && (r & 1)))));
+  }
+  const uint32_t r = ((ax - 0x38000000u) >> 13), rem = ax & 0x1FFFu;
+  return (uint16_t)(sign | (r + (rem > 0x1000u || (rem == 0x1000u && (r & 1)))));
+}
+
+// persistent worker pool for parallel pread granules
+class IoPool {
+ public:
+  explicit IoPool(int n) {
+    for (int i = 0; i < std::max(1, n); ++i) ts_.emplace_back([this] { loop(); });
+  }
+  ~IoPool() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : ts_) t.join();
+  }
+  // run f(0..n-1) on the pool, return when all are done
+  void run(int64_t n, const std::function<void(int64_t)>& f) {
+    if (n <= 0) return;
+    std::unique_lock<std::mutex> g(m_);
+    job_ = &f;
+    n_ = n;
+    next_ = 0;
+    done_ = 0;
+    ++gen_;
+    cv_.notify_all();
+    done_cv_.wait(g, [&] { return done_ == n_; });
+    job_ = nullptr;
+  }
+  int size() const { return (int)ts_.size(); }
+
+ private:
+  void loop() {
+    uint64_t seen = 0;
+    std::unique_lock<std::mutex> g(m_);
+    for (;;) {
+      cv_.wait(g, [&] { return stop_ || (gen_ != seen && job_ && next_ < n_); });
+      if (stop_) return;
+      while (job_ && next_ < n_) {
+        const int64_t i = next_++;
+        const std::function<void(int64_t)>* f = job_;
+        g.unlock();
+        (*f)(i);
+        g.lock();
+        if (++done_ == n_) done_cv_.notify_all();
+      }
+      seen = gen_;
+    }
+  }
+  std::vector<std::thread> ts_;
+  std::mutex m_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(int64_t)>* job_ = nullptr;
+  int64_t n_ = 0, next_ = 0, done_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
+struct Slot {
+  char* buf = nullptr;
+  hipEvent_t ev = nullptr;
+  bool pending = false;
+};
+
+struct Streamer {
+  int device = 0;
+  uint64_t chunk = 0;
+  int direct = 0;
+  std::vector<Slot> slots;
+  size_t next = 0;
+  IoPool* pool = nullptr;
+  // stats
+  double read_s = 0, wait_s = 0;
+  uint64_t read_bytes = 0, h2d_bytes = 0;
+  int direct_fallbacks = 0;
+};
+
+struct SubPiece {
+  uint64_t file_off, nbytes, dst_off;
+  int kind;
+};
+
+constexpr uint64_t kAlign = 4096;
+constexpr uint64_t kGranule = 8ull << 20;   // pread granule per pool task
+
+// read [lo, hi) of fd into buf (buf corresponds to file offset lo); returns 0 or -errno
+int64_t pool_read(IoPool* pool, int fd, uint64_t lo, uint64_t hi, char* buf, uint64_t need_hi) {
+  const uint64_t bytes = hi - lo;
+  const int64_t n = (int64_t)((bytes + kGranule - 1) / kGranule);
+  std::atomic<int64_t> err{0};
+  pool->run(n, [&](int64_t c) {
+    const uint64_t a = (uint64_t)c * kGranule, len = std::min<uint64_t>(kGranule, bytes - a);
+    uint64_t done = 0;
+    while (done < len) {
+      ssize_t r = pread(fd, buf + a + done, len - done, lo + a + done);
+      if (r < 0) {
+        if (errno == EINTR) continue;
+        err.store(-errno);
+        return;
+      }
+      if (r == 0) {   // EOF: fine past the bytes we need (O_DIRECT rounds the range up)
+        if (lo + a + done < need_hi) err.store(-EIO);
+        return;
+      }
+      done += (uint64_t)r;
+    }
+  });
+  return err.load();
+}
+
+}  // namespace
+
+extern "C" void* fls_streamer_create(int device, uint64_t chunk_bytes, int n_chunks, int io_threads, int direct) {
+  if (chunk_bytes < (1u << 20) || n_chunks < 1) return nullptr;
+  if (hipSetDevice(device) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
+  auto* st = new Streamer();
+  st->device = device;
+  st->chunk = (chunk_bytes + kAlign - 1) / kAlign * kAlign;
+  st->direct = direct;
+  st->slots.resize(n_chunks);
+  for (auto& sl : st->slots) {
+    void* p = nullptr;
+    // + 2 alignment pages: an O_DIRECT read rounds the range out on both sides
+    if (hipHostMalloc(&p, st->chunk + 2 * kAlign, hipHostMallocPortable) != hipSuccess ||
+        hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming) != hipSuccess) {
+      (void)hipGetLastError();
+      if (p) (void)hipHostFree(p);
+      for (auto& s2 : st->slots) {
+        if (s2.buf) (void)hipHostFree(s2.buf);
+        if (s2.ev) (void)hipEventDestroy(s2.ev);
+      }
+      delete st;
+      return nullptr;
+    }
+    sl.buf = (char*)p;
+  }
+  st->pool = new IoPool(std::max(1, io_threads));
+  return st;
+}
+
+extern "C" uint64_t fls_streamer_pinned_bytes(void* h) {
+  auto* st = (Streamer*)h;
+  return st ? (uint64_t)st->slots.size() * (st->chunk + 2 * kAlign) : 0;
+}
+
+// Stream `n` pieces of `path` (sorted by file_off) to dst_dev + piece.dst_off on `stream`.
+// kind 0: raw bytes; kind 1: fp32 source converted to fp16 on the host (nbytes fp32 bytes in
+// the file, nbytes / 2 bytes written).  Returns the file bytes read, or < 0 on error.  Returns
+// once every copy is ENQUEUED; the caller records its own completion event on `stream`.
+extern "C" int64_t fls_streamer_load(void* h, const char* path, const fls_piece_t* pieces, int n, void* dst_dev,
+                                     fls_stream_t stream) {
+  auto* st = (Streamer*)h;
+  if (!st || n < 0) return -EINVAL;
+  if (n == 0) return 0;
+  if (hipSetDevice(st->device) != hipSuccess) { (void)hipGetLastError(); return -ENODEV; }
+  // split pieces so that every chunk (with O_DIRECT slack) fits a ring slot
+  const uint64_t maxp = st->chunk;
+  std::vector<SubPiece> sub;
+  for (int i = 0; i < n; ++i) {
+    const fls_piece_t& p = pieces[i];
+    if (i && p.file_off < pieces[i - 1].file_off) return -EINVAL;
+    if (p.kind != 0 && p.kind != 1) return -EINVAL;
+    uint64_t a = 0;
+    while (a < p.nbytes) {
+      const uint64_t len = std::min<uint64_t>(maxp, p.nbytes - a);   // maxp % 4096 == 0: fp32 elements stay whole
+      sub.push_back({p.file_off + a, len, p.dst_off + (p.kind == 1 ? a / 2 : a), (int)p.kind});
+      a += len;
+    }
+  }
+  int flags = O_RDONLY | O_CLOEXEC;
+  int fd = -1;
+  bool direct = st->direct != 0;
+  if (direct) {
+    fd = open(path, flags | O_DIRECT);
+    if (fd < 0) { direct = false; ++st->direct_fallbacks; }
+  }
+  if (fd < 0) fd = open(path, flags);
+  if (fd < 0) return -errno;
+  if (!direct) posix_fadvise(fd, 0, 0, POSIX_FADV_SEQUENTIAL);
+  int64_t total = 0;
+  size_t i = 0;
+  while (i < sub.size()) {
+    // chunk = consecutive sub-pieces whose file span fits the slot (small gaps are read through)
+    const uint64_t lo = sub[i].file_off;
+    size_t j = i + 1;
+    uint64_t hi = sub[i].file_off + sub[i].nbytes;
+    while (j < sub.size() && sub[j].file_off >= hi && sub[j].file_off - hi <= (1u << 20) &&
+           sub[j].file_off + sub[j].nbytes - lo <= maxp) {
+      hi = sub[j].file_off + sub[j].nbytes;
+      ++j;
+    }
+    Slot& sl = st->slots[st->next++ % st->slots.size()];
+    auto t0 = std::chrono::steady_clock::now();
+    if (sl.pending) {
+      if (hipEventSynchronize(sl.ev) != hipSuccess) { close(fd); (void)hipGetLastError(); return -EIO; }
+      sl.pending = false;
+    }
+    auto t1 = std::chrono::steady_clock::now();
+    uint64_t rlo = lo, rhi = hi;
+    if (direct) {
+      rlo = lo / kAlign * kAlign;
+      rhi = (hi + kAlign - 1) / kAlign * kAlign;
+    }
+    int64_t r = pool_read(st->pool, fd, rlo, rhi, sl.buf, hi);
+    if (r == -EINVAL && direct) {
+      // the file system refused O_DIRECT for this range: buffered from here on
+      close(fd);
+      fd = open(path, flags);
+      if (fd < 0) return -errno;
+      direct = false;
+      ++st->direct_fallbacks;
+      rlo = lo;
+      rhi = hi;
+      r = pool_read(st->pool, fd, rlo, rhi, sl.buf, hi);
+    }
+    if (r < 0) { close(fd); return r; }
+    auto t2 = std::chrono::steady_clock::now();
+    st->wait_s += std::chrono::duration<double>(t1 - t0).count();
+    st->read_s += std::chrono::duration<double>(t2 - t1).count();
+    st->read_bytes += hi - lo;
+    total += (int64_t)(hi - lo);
+    for (size_t k = i; k < j; ++k) {
+      char* src = sl.buf + (sub[k].file_off - rlo);
+      uint64_t len = sub[k].nbytes;
+      if (sub[k].kind == 1) {   // fp32 -> fp16 in place (write index <= read index: forward is safe)
+        const uint64_t cnt = len / 4;
+        const float* fs = (const float*)src;
+        uint16_t* hs = (uint16_t*)src;
+        for (uint64_t e = 0; e < cnt; ++e) {
+          float v;
+          std::memcpy(&v, fs + e, 4);
+          hs[e] = f32_to_f16_bits(v);
+        }
+        len = cnt * 2;
+      }
+      if (hipMemcpyAsync((char*)dst_dev + sub[k].dst_off, src, len, hipMemcpyHostToDevice, (hipStream_t)stream) !=
+          hipSuccess) {
+        close(fd);
+        (void)hipGetLastError();
+        return -EIO;
+      }
+      st->h2d_bytes += len;
+    }
+    if (hipEventRecord(sl.ev, (hipStream_t)stream) != hipSuccess) { close(fd); (void)hipGetLastError(); return -EIO; }
+    sl.pending = true;
+    i = j;
+  }
+  close(fd);
+  return total;
+}
+
+// host-only variant (no GPU): the same piece plan read into a host buffer (CPU runs / tests)
+extern "C" int64_t fls_stream_read_host(const char* path, const fls_piece_t* pieces, int n, void* dst,
+                                        int io_threads) {
+  int fd = open(path, O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return -errno;
+  int64_t total = 0;
+  for (int i = 0; i < n; ++i) {
+    const fls_piece_t& p = pieces[i];
+    char* d = (char*)dst + p.dst_off;
+    if (p.kind == 0) {
+      int64_t r = parallel_io(fd, p.file_off, p.nbytes, d, io_threads, false);
+      if (r < 0) { close(fd); return r; }
+    } else {
+      std::vector<char> tmp(p.nbytes);
+      int64_t r = parallel_io(fd, p.file_off, p.nbytes, tmp.data(), io_threads, false);
+      if (r < 0) { close(fd); return r; }
+      const uint64_t cnt = p.nbytes / 4;
+      for (uint64_t e = 0; e < cnt; ++e) {
+        float v;
+        std::memcpy(&v, tmp.data() + 4 * e, 4);
+        const uint16_t b = f32_to_f16_bits(v);
+        std::memcpy(d + 2 * e, &b, 2);
+      }
+    }
+    total += (int64_t)p.nbytes;
+  }
+  close(fd);
+  return total;
+}
+
+extern "C" int fls_streamer_stats(void* h, double* read_s, double* wait_s, uint64_t* read_bytes,
+                                  uint64_t* h2d_bytes, int* direct_fallbacks) {
+  auto* st = (Streamer*)h;
+  if (!st) return -1;
+  *read_s = st->read_s;
+  *wait_s = st->wait_s;
+  *read_bytes = st->read_bytes;
+  *h2d_bytes = st->h2d_bytes;
+  *direct_fallbacks = st->direct_fallbacks;
+  return 0;
+}
+
+extern "C" void fls_streamer_destroy(void* h) {
+  auto* st = (Streamer*)h;
+  if (!st) return;
+  (void)hipSetDevice(st->device);
+  for (auto& sl : st->slots) {
+    if (sl.pending) (void)hipEventSynchronize(sl.ev);
+    (void)hipEventDestroy(sl.ev);
+    (void)hipHostFree(sl.buf);
+  }
+  delete st->pool;
+  delete st;
+}
+
+// host-only f32 -> f16 conversion with the streamer's rounding (tests)
+extern "C" void fls_f32_to_f16(const float* src, uint16_t* dst, uint64_t n) {
+  for (uint64_t i = 0; i < n; ++i) dst[i] = f32_to_f16_bits(src[i]);
+}

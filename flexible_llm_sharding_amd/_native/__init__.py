@@ -45,10 +45,23 @@ def _load_runtime():
     _bind(lib, "fls_st_data_offset", c_uint64, c_void_p)
     _bind(lib, "fls_st_close", None, c_void_p)
     _bind(lib, "fls_mem_info", c_int, c_void_p, c_void_p)
+    _bind(lib, "fls_streamer_create", c_void_p, c_int, c_uint64, c_int, c_int, c_int)
+    _bind(lib, "fls_streamer_pinned_bytes", c_uint64, c_void_p)
+    _bind(lib, "fls_streamer_load", c_int64, c_void_p, c_char_p, c_void_p, c_int, c_void_p, c_void_p)
+    _bind(lib, "fls_stream_read_host", c_int64, c_char_p, c_void_p, c_int, c_void_p, c_int)
+    _bind(lib, "fls_streamer_stats", c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p)
+    _bind(lib, "fls_streamer_destroy", None, c_void_p)
+    _bind(lib, "fls_f32_to_f16", None, c_void_p, c_void_p, c_uint64)
     return lib
 
 
-KERNELS_ABI = 7   # bumped whenever a C signature in csrc/include/fls.h changes
+class Piece(ctypes.Structure):
+    """fls_piece_t (csrc/include/fls.h)."""
+    _fields_ = [("file_off", ctypes.c_uint64), ("nbytes", ctypes.c_uint64), ("dst_off", ctypes.c_uint64),
+                ("kind", ctypes.c_int32), ("pad", ctypes.c_int32)]
+
+
+KERNELS_ABI = 8   # bumped whenever a C signature in csrc/include/fls.h changes
 
 
 def _load_kernels():
@@ -64,7 +77,6 @@ def _load_kernels():
     _bind(lib, "fls_gemm_set_rope_persistent", c_int, c_int)
     _bind(lib, "fls_gemm_set_order", c_int, c_int)
     _bind(lib, "fls_attn_set_mha_v2", c_int, c_int)
-    _bind(lib, "fls_gemm_ablate", c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p)
     _bind(lib, "fls_attn_set_variant", c_int, c_int)
     _bind(lib, "fls_attention", c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
           c_int, c_int, c_float, c_void_p, c_int, c_int, c_void_p)
@@ -72,9 +84,7 @@ def _load_kernels():
           c_int, c_float, c_void_p)
     _bind(lib, "fls_embed", c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p)
     _bind(lib, "fls_softmax_rows", c_int, c_void_p, c_void_p, c_int, c_int, c_void_p)
-    _bind(lib, "fls_rope_inplace", c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
-          c_void_p)
-    _bind(lib, "fls_swiglu", c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p)
+    _bind(lib, "fls_cast_f16", c_int, c_void_p, c_void_p, c_int, c_uint64, c_void_p)
     _bind(lib, "fls_gemv_skinny", c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
           c_void_p)
     _bind(lib, "fls_fill_random", c_int, c_void_p, c_uint64, c_uint64, c_float, c_float, c_void_p)

@@ -30,7 +30,8 @@ from .config import MAX_TOKEN_LEN, ModelConfig
 from .engine import ShardedRunner
 from .parallel.comm import Comm
 from .parallel.planner import make_plan
-from .runtime.weights import FileLayerSource, HostStore
+from .runtime.stream import FileLayerSource
+from .runtime.weights import HostStore
 from .utils.cli import parse_args
 from .utils.tokenizer import load_tokenizer
 
@@ -41,6 +42,41 @@ def batch_ranges(n: int, num_batch: int):
     return list(zip([0] + ends[:-1], ends))
 
 
+def resolve_weight_cache(args, cfg: ModelConfig, comm: Comm, names: Sequence[str], sliced: bool) -> str:
+    """``--weight_cache`` -> ``host`` or ``stream``.
+
+    ``auto`` pins the packed layers in host RAM only when they fit the host budget
+    (``--host_mem_gb``, default 80% of MemAvailable shared by this node's ranks), and
+    otherwise streams them from the layer files every pass — the reference's small-RAM mode
+    (README: 70B with >= 8 GB RAM).  ``disk`` is the reference-named alias of ``stream``.
+    An explicit ``host`` that cannot fit is rejected instead of being OOM-killed mid-load
+    (e.g. ``--dp_weight_shard false`` would pin the whole model once per rank)."""
+    from .models.layout import layer_kind, layer_layout
+    from .runtime.stream import host_ram_available
+    from .runtime.weights import shard_chunk_bytes
+    mode = getattr(args, "weight_cache", "auto")
+    if getattr(args, "synthetic", None):
+        return "host"                  # generated in host RAM; there are no files to stream
+    if mode in ("disk", "stream"):
+        return "stream"
+    need = 0
+    for n in names:
+        nb = layer_layout(cfg, layer_kind(n)).nbytes
+        need += shard_chunk_bytes(nb, comm.world) if sliced else nb
+    local = int(os.environ.get("LOCAL_WORLD_SIZE", comm.world))
+    if getattr(args, "host_mem_gb", None):
+        budget = int(args.host_mem_gb * 1e9) // max(1, local)
+    else:
+        budget = int(0.8 * host_ram_available()) // max(1, local)
+    fits = budget <= 0 or need <= budget            # unknown RAM size: trust the user
+    if mode == "host":
+        if not fits:
+            raise SystemExit(f"--weight_cache host needs {need / 1e9:.1f} GB of pinned RAM per rank, the budget "
+                             f"is {budget / 1e9:.1f} GB: use --weight_cache stream (or auto)")
+        return "host"
+    return "host" if fits else "stream"
+
+
 def build_source(args, cfg: ModelConfig, comm: Comm, device: torch.device):
     names = cfg.layer_names()
     plan = make_plan(len(names), args.layer_num_per_shard, comm.world, comm.rank, args.data_parallel,
@@ -48,11 +84,9 @@ def build_source(args, cfg: ModelConfig, comm: Comm, device: torch.device):
     mine = [names[i] for i in sorted({i for sh in plan.my_shards for i in sh})]
     if getattr(args, "synthetic", None):
         return HostStore.synthetic(cfg, device, seed=0, pinned=device.type == "cuda", names=mine)
-    src = FileLayerSource(cfg, args.model_path)
-    if args.weight_cache == "disk":
+    src = FileLayerSource(cfg, args.model_path, names=mine, direct=getattr(args, "o_direct", False))
+    if resolve_weight_cache(args, cfg, comm, mine, sliced=False) == "stream":
         return src
-    if args.weight_cache == "packed":
-        return open_packed_source(args, cfg, comm, mine)
     return HostStore.from_source(src, pinned=device.type == "cuda", names=mine)
 
 
@@ -60,7 +94,8 @@ def build_runner(args, cfg: ModelConfig, device, comm: Comm, tok) -> ShardedRunn
     device = torch.device(device)
     if args.data_parallel and comm.world > 1 and args.dp_weight_shard:
         from .parallel.data_parallel import build_dp_sharded_runner
-        return build_dp_sharded_runner(args, cfg, device, comm, tok)
+        wc = resolve_weight_cache(args, cfg, comm, cfg.layer_names(), sliced=True)
+        return build_dp_sharded_runner(args, cfg, device, comm, tok, weight_cache=wc)
     src = build_source(args, cfg, comm, device)
     act = None
     if args.dtype:
@@ -77,19 +112,8 @@ def build_runner(args, cfg: ModelConfig, device, comm: Comm, tok) -> ShardedRunn
                          hip_graphs=getattr(args, "hip_graphs", False),
                          prefix_kv_cache=getattr(args, "prefix_kv_cache", False),
                          prefix_cache_entries=getattr(args, "prefix_cache_entries", 8),
-                         pipeline_stages=getattr(args, "pipeline_stages", "round_robin"))
-
-
-def open_packed_source(args, cfg: ModelConfig, comm: Comm, names):
-    """Build (rank 0, once) and open the packed-layer cache."""
-    from .runtime.packed import PackedFileSource, build_packed_cache
-    cache = args.packed_dir or os.path.join(args.model_path, ".fls_packed")
-    if comm.rank == 0:
-        n = build_packed_cache(FileLayerSource(cfg, args.model_path), cache, verbose=args.verbose)
-        if n and args.verbose:
-            print(f"[packed cache] wrote {n} layers to {cache}")
-    comm.barrier()
-    return PackedFileSource(cfg, cache, names=names)
+                         pipeline_stages=getattr(args, "pipeline_stages", "round_robin"),
+                         max_vram_gb=getattr(args, "max_vram_gb", None))
 
 
 def load_model_meta(args):
@@ -111,9 +135,14 @@ def run_all(args, runner: ShardedRunner, comm: Comm, prompts: Sequence) -> List[
         mine = [prompts[i] for i in idx]
     else:
         mine = list(prompts)
+    if not prompts:
+        return []
+    # data parallel with all-gathered weights: every rank runs num_batch passes, even over an
+    # empty slice, so the weight collectives line up across ranks
+    collective = getattr(runner.prefetcher, "collective", False)
     outs: List[np.ndarray] = []
     for b0, b1 in batch_ranges(len(mine), args.num_batch):
-        if b1 > b0:
+        if b1 > b0 or collective:
             outs += runner(mine[b0:b1])
     if comm.world == 1:
         return outs

@@ -67,7 +67,8 @@ class ShardedRunner:
                  verbose: bool = False, resume_dir: Optional[str] = None, checkpoint_every: int = 0,
                  max_token_len: int = MAX_TOKEN_LEN, hip_graphs: bool = False,
                  prefix_kv_cache: bool = False, prefix_cache_entries: int = 8,
-                 prune_last_layer: bool = True, pipeline_stages: str = "round_robin"):
+                 prune_last_layer: bool = True, pipeline_stages: str = "round_robin",
+                 max_vram_gb: Optional[float] = None):
         self.cfg = cfg
         self.src = source
         self.dev = torch.device(device)
@@ -78,7 +79,15 @@ class ShardedRunner:
         self.disk_folder = disk_folder
         self.max_act = max_activation_in_cpu
         self.prefix_attention = prefix_attention
+        self.vram_plan = None
+        if max_vram_gb:
+            # size the micro-batch and the MLP chunk to the HBM cap (runtime/memplan.py)
+            from .runtime.memplan import plan_for_vram
+            token_budget, mlp_chunk, est = plan_for_vram(cfg, int(max_vram_gb * 1e9), layer_num_per_shard,
+                                                         n_slots, token_budget, mlp_chunk)
+            self.vram_plan = {"token_budget": token_budget, "mlp_chunk": mlp_chunk, "estimated_peak_bytes": est}
         self.token_budget = token_budget
+        self.mlp_chunk = mlp_chunk
         self.comm = comm or Comm(0, 1, self.dev)
         self.data_parallel = data_parallel
         self.verbose = verbose
@@ -252,6 +261,13 @@ class ShardedRunner:
         h2d0 = pf.bytes_h2d if self._h2d0 is None else self._h2d0
         self._h2d0 = None
         items = self.schedule(len(batches))
+        if not items and self.my_shards and getattr(pf, "collective", False):
+            # a data-parallel rank with no prompts in this call still joins every shard's weight
+            # all-gather, so all ranks issue the same collective sequence
+            for k in range(len(self.my_shards)):
+                pf.acquire(k)
+                pf.prefetch(k + 1)
+                pf.release(k)
         ck, k0 = self._open_checkpoint(tps)
         if k0 > 0:
             for b, t in ck.load(k0).items():
@@ -375,6 +391,8 @@ class ShardedRunner:
             if pool_buf is not None:
                 store.recycle_host(pool_buf)
         store.clear()
+        store.trim()                   # pinned pool follows this call's shapes
+        wait_s = pf.take_wait_seconds()
         if pbar is not None:
             pbar.close()
         if ck is not None:
@@ -385,7 +403,7 @@ class ShardedRunner:
             "tokens": float(sum(b.num_tokens for b in batches)),
             "padded_tokens": float(sum(b.padded_tokens for b in batches)),
             "decoder_flops": flops, "micro_batches": float(len(batches)),
-            "weight_wait_s": pf.wait_seconds, "weight_h2d_bytes": float(h2d_end - h2d0),
+            "weight_wait_s": wait_s, "weight_h2d_bytes": float(h2d_end - h2d0),
             "act_d2h_bytes": float(store.bytes_d2h), "act_h2d_bytes": float(store.bytes_h2d),
             "resumed_from_shard": float(k0),
             # GPU-side: compute stream stalled on the weight / activation copy streams
@@ -395,7 +413,7 @@ class ShardedRunner:
         if self.verbose:
             # utils.py:304 prints "loaded N layers in Ts" per device
             n_layers = sum(len(s) for s in self.my_shards[k0:])
-            print(f"{self.dev} rank{comm.rank}: loaded {n_layers} layers in {pf.wait_seconds:.2f}s "
+            print(f"{self.dev} rank{comm.rank}: loaded {n_layers} layers in {wait_s:.2f}s "
                   f"(exposed weight wait); {len(self.my_shards)} shards, {len(batches)} micro-batches, "
                   f"{self.stats['tokens']:.0f} tokens in {wall:.2f}s")
         return outputs
@@ -489,7 +507,7 @@ class ShardedRunner:
             "tokens": float(sum(b.num_tokens for b in batches)),
             "padded_tokens": float(sum(b.padded_tokens for b in batches)),
             "decoder_flops": flops, "micro_batches": float(len(batches)),
-            "weight_wait_s": pf.wait_seconds, "weight_h2d_bytes": 0.0,
+            "weight_wait_s": pf.take_wait_seconds(), "weight_h2d_bytes": 0.0,
             "act_d2h_bytes": 0.0, "act_h2d_bytes": 0.0, "resumed_from_shard": 0.0,
             "graph_captures": float(self._graphs.captures), "graph_replays": float(self._graphs.replays),
         }
@@ -558,6 +576,8 @@ class ShardedRunner:
 
     def close(self):
         self.prefetcher.close()
+        if hasattr(self.src, "close"):
+            self.src.close()           # the streaming source's pinned ring
         if self._store is not None:
             self._store.close()
             self._store = None

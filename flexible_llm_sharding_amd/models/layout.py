@@ -1,32 +1,33 @@
-"""Packed per-layer weight layout — the HBM-native format the kernels consume.
+"""Packed per-layer weight layout — the HBM image the kernels consume.
 
 The reference keeps HF modules and installs each parameter separately with
-``set_module_tensor_to_device`` (``/root/reference/utils.py:128-130``).  We
-instead pack each layer into ONE contiguous buffer so that a shard moves
-host->HBM as a single large ``hipMemcpyAsync`` and every kernel gets raw
-pointers at fixed offsets.
+``set_module_tensor_to_device`` (``/root/reference/utils.py:128-130``).  Here
+each layer is ONE contiguous buffer (a weight slot), so a shard moves to HBM
+as large DMAs and every kernel gets raw pointers at fixed offsets.
 
-Decoder layer packing (fp16, every tensor 256-byte aligned)::
+Decoder layer image (fp16, every slot 256-byte aligned)::
 
     ln1   [H]              input_layernorm.weight
     ln2   [H]              post_attention_layernorm.weight
-    wqkv  [Hq+2Hkv, H]     q|k|v projections, q and k rows RoPE-pair permuted
+    wqkv  [Hq+2Hkv, H]     q_proj | k_proj | v_proj   (rows concatenated)
     wo    [H, Hq]          o_proj
-    wgu   [2I, H]          gate/up interleaved in blocks of 16 rows
+    wgu   [2I, H]          gate_proj | up_proj        (rows concatenated)
     wdown [H, I]           down_proj
-    bqkv  [Hq+2Hkv]        q|k|v biases, permuted like wqkv rows (Qwen2 / attention_bias only)
+    bqkv  [Hq+2Hkv]        q|k|v biases (Qwen2 / attention_bias only)
     bo    [H]              o_proj bias (Llama attention_bias only)
 
-*RoPE pair permutation* — HF Llama rotates (d, d + hd/2) pairs
-(``rotate_half``).  Per head we reorder rows as ``[0:16], [hd/2:hd/2+16],
-[16:32], [hd/2+16:hd/2+32], ...`` so the MFMA GEMM epilogue finds each
-rotation partner in the neighbouring 16-column subtile of the same lane and
-can apply RoPE in registers.  Q and K stay in this permuted head-dim order all
-the way into attention (QK^T is invariant to a common permutation of d).
+Every checkpoint tensor keeps its own row order and byte image: a slot is a
+plain concatenation of whole tensors.  The two places where the fused kernels
+need partners side by side are handled inside the GEMM, not by permuting
+weights: the RoPE epilogue finds the rotate-half partner ``d + hd/2`` of a
+head's column ``d`` in the same lane (``csrc/kernels/gemm.hip``), and the
+SwiGLU GEMM's W-tile loader reads gate and up rows interleaved per 16 from the
+two stacked blocks.  So a layer file streams to HBM as raw DMA of its tensors
+(:mod:`..runtime.stream`), with at most an in-place dtype cast on the GPU.
 
-*Gate/up interleave* — rows ``[g0:16], [u0:16], [g16:32], [u16:32] ...`` so
-the SwiGLU epilogue reads gate and up of the same intermediate column from two
-accumulator subtiles held by the same lane.
+:func:`placements` is the single description of where each checkpoint tensor
+lands; the host cache, the streamer, data-parallel slices, ``pack_layer`` and
+``unpack_layer`` all derive from it.
 """
 from __future__ import annotations
 
@@ -38,7 +39,6 @@ import torch
 from ..config import ModelConfig
 
 ALIGN_BYTES = 256
-PAIR_BLOCK = 16
 
 
 def _align(n_bytes: int) -> int:
@@ -122,82 +122,68 @@ def layer_layout(cfg: ModelConfig, kind: str, elem_size: int = 2) -> LayerLayout
     return LayerLayout(kind, tuple(slots), off, elem_size)
 
 
-# ----------------------------------------------------------------- permutations
-def rope_row_perm(head_dim: int) -> List[int]:
-    """Row order inside one head: packed row i takes HF row perm[i]."""
-    half = head_dim // 2
-    assert half % PAIR_BLOCK == 0, "head_dim/2 must be a multiple of 16"
-    perm = []
-    for j in range(half // PAIR_BLOCK):
-        perm += list(range(PAIR_BLOCK * j, PAIR_BLOCK * (j + 1)))
-        perm += list(range(half + PAIR_BLOCK * j, half + PAIR_BLOCK * (j + 1)))
-    return perm
+@dataclass(frozen=True)
+class Placement:
+    """Checkpoint tensor ``hf_name`` occupies ``numel`` elements of ``elem_size`` bytes at byte
+    ``offset`` of the image."""
+    hf_name: str
+    offset: int
+    numel: int
+    shape: Tuple[int, ...]
+    elem_size: int = 2
+
+    @property
+    def nbytes(self) -> int:
+        return self.elem_size * self.numel
 
 
-def permute_heads_rows(w: torch.Tensor, n_heads: int, head_dim: int) -> torch.Tensor:
-    perm = torch.tensor(rope_row_perm(head_dim), dtype=torch.long)
-    w3 = w.reshape(n_heads, head_dim, -1)
-    return w3[:, perm, :].reshape(w.shape)
+def placements(cfg: ModelConfig, layer_name: str, elem_size: int = 2) -> List[Placement]:
+    """Where every checkpoint tensor of ``layer_name`` lands in the packed image."""
+    kind = layer_kind(layer_name)
+    lay = layer_layout(cfg, kind, elem_size)
+    es = elem_size
+    H, I = cfg.hidden_size, cfg.intermediate_size
+    if kind == "embed":
+        return [Placement("model.embed_tokens.weight", 0, cfg.vocab_size * H, (cfg.vocab_size, H), es)]
+    if kind == "head":
+        return [Placement("lm_head.weight", 0, cfg.vocab_size * H, (cfg.vocab_size, H), es)]
+    if kind == "norm":
+        return [Placement("model.norm.weight", 0, H, (H,), es)]
+    p = layer_name
+    qs, ks = cfg.q_size, cfg.kv_size
+    o = {s.name: s.offset for s in lay.slots}
+    out = [
+        Placement(f"{p}.input_layernorm.weight", o["ln1"], H, (H,), es),
+        Placement(f"{p}.post_attention_layernorm.weight", o["ln2"], H, (H,), es),
+        Placement(f"{p}.self_attn.q_proj.weight", o["wqkv"], qs * H, (qs, H), es),
+        Placement(f"{p}.self_attn.k_proj.weight", o["wqkv"] + es * qs * H, ks * H, (ks, H), es),
+        Placement(f"{p}.self_attn.v_proj.weight", o["wqkv"] + es * (qs + ks) * H, ks * H, (ks, H), es),
+        Placement(f"{p}.self_attn.o_proj.weight", o["wo"], H * qs, (H, qs), es),
+        Placement(f"{p}.mlp.gate_proj.weight", o["wgu"], I * H, (I, H), es),
+        Placement(f"{p}.mlp.up_proj.weight", o["wgu"] + es * I * H, I * H, (I, H), es),
+        Placement(f"{p}.mlp.down_proj.weight", o["wdown"], H * I, (H, I), es),
+    ]
+    if cfg.attention_bias:
+        out += [Placement(f"{p}.self_attn.q_proj.bias", o["bqkv"], qs, (qs,), es),
+                Placement(f"{p}.self_attn.k_proj.bias", o["bqkv"] + es * qs, ks, (ks,), es),
+                Placement(f"{p}.self_attn.v_proj.bias", o["bqkv"] + es * (qs + ks), ks, (ks,), es)]
+    if cfg.o_proj_bias:
+        out.append(Placement(f"{p}.self_attn.o_proj.bias", o["bo"], H, (H,), es))
+    return out
 
 
-def unpermute_heads_rows(w: torch.Tensor, n_heads: int, head_dim: int) -> torch.Tensor:
-    perm = torch.tensor(rope_row_perm(head_dim), dtype=torch.long)
-    inv = torch.empty_like(perm)
-    inv[perm] = torch.arange(perm.numel())
-    w3 = w.reshape(n_heads, head_dim, -1)
-    return w3[:, inv, :].reshape(w.shape)
-
-
-def permute_head_cols(x: torch.Tensor, n_heads: int, head_dim: int) -> torch.Tensor:
-    """Apply the rope head-dim permutation to activations [..., n_heads*head_dim]."""
-    perm = torch.tensor(rope_row_perm(head_dim), dtype=torch.long, device=x.device)
-    shp = x.shape
-    return x.reshape(*shp[:-1], n_heads, head_dim)[..., perm].reshape(shp)
-
-
-def unpermute_head_cols(x: torch.Tensor, n_heads: int, head_dim: int) -> torch.Tensor:
-    perm = torch.tensor(rope_row_perm(head_dim), dtype=torch.long)
-    inv = torch.empty_like(perm)
-    inv[perm] = torch.arange(perm.numel())
-    inv = inv.to(x.device)
-    shp = x.shape
-    return x.reshape(*shp[:-1], n_heads, head_dim)[..., inv].reshape(shp)
-
-
-def interleave_gate_up(gate: torch.Tensor, up: torch.Tensor) -> torch.Tensor:
-    I, H = gate.shape
-    assert I % PAIR_BLOCK == 0, "intermediate_size must be a multiple of 16"
-    g = gate.reshape(I // PAIR_BLOCK, PAIR_BLOCK, H)
-    u = up.reshape(I // PAIR_BLOCK, PAIR_BLOCK, H)
-    return torch.stack([g, u], dim=1).reshape(2 * I, H)
-
-
-def deinterleave_gate_up(wgu: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
-    I2, H = wgu.shape
-    w = wgu.reshape(I2 // (2 * PAIR_BLOCK), 2, PAIR_BLOCK, H)
-    return w[:, 0].reshape(I2 // 2, H), w[:, 1].reshape(I2 // 2, H)
+def source_key(cfg: ModelConfig, layer_name: str, hf_name: str, available) -> str:
+    """Checkpoint key that feeds ``hf_name`` (tied LM head: the embedding table)."""
+    if hf_name in available:
+        return hf_name
+    if hf_name == "lm_head.weight" and cfg.tie_word_embeddings and "model.embed_tokens.weight" in available:
+        return "model.embed_tokens.weight"
+    raise KeyError(f"{layer_name}: missing tensor {hf_name}")
 
 
 # ------------------------------------------------------------------- packing
 def hf_param_names(cfg: ModelConfig, layer_name: str) -> List[str]:
-    kind = layer_kind(layer_name)
-    if kind == "embed":
-        return ["model.embed_tokens.weight"]
-    if kind == "norm":
-        return ["model.norm.weight"]
-    if kind == "head":
-        return ["lm_head.weight"]
-    p = layer_name
-    names = [f"{p}.self_attn.q_proj.weight", f"{p}.self_attn.k_proj.weight",
-             f"{p}.self_attn.v_proj.weight", f"{p}.self_attn.o_proj.weight",
-             f"{p}.mlp.gate_proj.weight", f"{p}.mlp.up_proj.weight",
-             f"{p}.mlp.down_proj.weight", f"{p}.input_layernorm.weight",
-             f"{p}.post_attention_layernorm.weight"]
-    if cfg.attention_bias:
-        names += [f"{p}.self_attn.{n}_proj.bias" for n in ("q", "k", "v")]
-    if cfg.o_proj_bias:
-        names.append(f"{p}.self_attn.o_proj.bias")
-    return names
+    return [pl.hf_name for pl in placements(cfg, layer_name)]
 
 
 def pack_layer(cfg: ModelConfig, layer_name: str, sd: Dict[str, torch.Tensor],
@@ -206,92 +192,35 @@ def pack_layer(cfg: ModelConfig, layer_name: str, sd: Dict[str, torch.Tensor],
 
     ``sd`` keys are full HF names (the per-layer file format of
     ``prepare_weights.py:40-43``).  ``int8`` is rejected like the reference
-    (``utils.py:129``).  Other float dtypes are cast to ``dtype`` (``utils.py:130``).
+    (``utils.py:129``); other float dtypes are cast to ``dtype`` (``utils.py:130``).
     """
     kind = layer_kind(layer_name)
     es = torch.empty((), dtype=dtype).element_size()
     lay = layer_layout(cfg, kind, es)
-    for k, v in sd.items():
+    for v in sd.values():
         if v.dtype == torch.int8:
             raise AssertionError("int8 not supported (need to add fp16_statistics)")
     if out is None:
         out = torch.zeros(lay.nbytes, dtype=torch.uint8)
-    views = lay.views(out, dtype)
-
-    def get(name):
-        if name not in sd:
-            raise KeyError(f"{layer_name}: missing tensor {name}")
-        return sd[name].to(dtype)
-
-    if kind == "embed":
-        views["embed"].copy_(get("model.embed_tokens.weight"))
-    elif kind == "norm":
-        views["norm"].copy_(get("model.norm.weight"))
-    elif kind == "head":
-        key = "lm_head.weight"
-        if key not in sd and cfg.tie_word_embeddings and "model.embed_tokens.weight" in sd:
-            key = "model.embed_tokens.weight"
-        views["head"].copy_(sd[key].to(dtype))
-    else:
-        p = layer_name
-        hd = cfg.head_dim
-        q = permute_heads_rows(get(f"{p}.self_attn.q_proj.weight"), cfg.num_attention_heads, hd)
-        k = permute_heads_rows(get(f"{p}.self_attn.k_proj.weight"), cfg.num_key_value_heads, hd)
-        v = get(f"{p}.self_attn.v_proj.weight")
-        views["wqkv"].copy_(torch.cat([q, k, v], 0))
-        views["wo"].copy_(get(f"{p}.self_attn.o_proj.weight"))
-        views["wgu"].copy_(interleave_gate_up(get(f"{p}.mlp.gate_proj.weight"),
-                                              get(f"{p}.mlp.up_proj.weight")))
-        views["wdown"].copy_(get(f"{p}.mlp.down_proj.weight"))
-        views["ln1"].copy_(get(f"{p}.input_layernorm.weight"))
-        views["ln2"].copy_(get(f"{p}.post_attention_layernorm.weight"))
-        if cfg.attention_bias:
-            bq = permute_heads_rows(get(f"{p}.self_attn.q_proj.bias")[:, None], cfg.num_attention_heads, hd)
-            bk = permute_heads_rows(get(f"{p}.self_attn.k_proj.bias")[:, None], cfg.num_key_value_heads, hd)
-            views["bqkv"].copy_(torch.cat([bq[:, 0], bk[:, 0], get(f"{p}.self_attn.v_proj.bias")], 0))
-        if cfg.o_proj_bias:
-            views["bo"].copy_(get(f"{p}.self_attn.o_proj.bias"))
+    b = out.view(torch.uint8)
+    for pl in placements(cfg, layer_name, es):
+        key = source_key(cfg, layer_name, pl.hf_name, sd)
+        t = sd[key]
+        if tuple(t.shape) != pl.shape:
+            raise ValueError(f"{layer_name}: {key} has shape {tuple(t.shape)}, config expects {pl.shape}")
+        b[pl.offset:pl.offset + pl.nbytes].view(dtype).copy_(t.reshape(-1).to(dtype))
     return out
 
 
 def unpack_layer(cfg: ModelConfig, layer_name: str, buf: torch.Tensor,
                  dtype: torch.dtype = torch.float16) -> Dict[str, torch.Tensor]:
-    """Inverse of :func:`pack_layer` (HF names, HF row order)."""
-    kind = layer_kind(layer_name)
+    """Inverse of :func:`pack_layer` (HF names and shapes)."""
     es = torch.empty((), dtype=dtype).element_size()
-    v = layer_layout(cfg, kind, es).views(buf, dtype)
-    if kind == "embed":
-        return {"model.embed_tokens.weight": v["embed"].clone()}
-    if kind == "norm":
-        return {"model.norm.weight": v["norm"].clone()}
-    if kind == "head":
-        return {"lm_head.weight": v["head"].clone()}
-    p = layer_name
-    hd = cfg.head_dim
-    qs, ks = cfg.q_size, cfg.kv_size
-    wqkv = v["wqkv"]
-    g, u = deinterleave_gate_up(v["wgu"])
+    b = buf.view(torch.uint8)
     out = {}
-    if cfg.attention_bias:
-        b = v["bqkv"][:, None]
-        out[f"{p}.self_attn.q_proj.bias"] = unpermute_heads_rows(b[:qs], cfg.num_attention_heads, hd)[:, 0].clone()
-        out[f"{p}.self_attn.k_proj.bias"] = unpermute_heads_rows(b[qs:qs + ks], cfg.num_key_value_heads,
-                                                                  hd)[:, 0].clone()
-        out[f"{p}.self_attn.v_proj.bias"] = v["bqkv"][qs + ks:].clone()
-    if cfg.o_proj_bias:
-        out[f"{p}.self_attn.o_proj.bias"] = v["bo"].clone()
-    return {
-        **out,
-        f"{p}.self_attn.q_proj.weight": unpermute_heads_rows(wqkv[:qs], cfg.num_attention_heads, hd).clone(),
-        f"{p}.self_attn.k_proj.weight": unpermute_heads_rows(wqkv[qs:qs + ks], cfg.num_key_value_heads, hd).clone(),
-        f"{p}.self_attn.v_proj.weight": wqkv[qs + ks:].clone(),
-        f"{p}.self_attn.o_proj.weight": v["wo"].clone(),
-        f"{p}.mlp.gate_proj.weight": g.clone(),
-        f"{p}.mlp.up_proj.weight": u.clone(),
-        f"{p}.mlp.down_proj.weight": v["wdown"].clone(),
-        f"{p}.input_layernorm.weight": v["ln1"].clone(),
-        f"{p}.post_attention_layernorm.weight": v["ln2"].clone(),
-    }
+    for pl in placements(cfg, layer_name, es):
+        out[pl.hf_name] = b[pl.offset:pl.offset + pl.nbytes].view(dtype).view(pl.shape).clone()
+    return out
 
 
 def max_layer_bytes(cfg: ModelConfig, elem_size: int = 2) -> int:

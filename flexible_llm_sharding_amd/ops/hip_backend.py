@@ -3,23 +3,14 @@
 Kernels run on the caller's current HIP stream (``torch.cuda.current_stream``)
 so they compose with the copy/comm streams of the runtime; outputs are
 allocated through PyTorch's caching allocator.  There is deliberately no
-fallback: a missing library raises (see ``_native.kernels``).
+fallback and no second GEMM backend: a missing library raises (see
+``_native.kernels``).
 
-Projection GEMMs: ``FLS_GEMM_BACKEND`` selects
-  * ``hip``       — (default) our fused MFMA kernels (RoPE / SwiGLU / residual epilogues in
-                    registers; ``gemm_nt_v10``, see profiles/r1_gemm_study);
-  * ``hipblaslt`` — the plain GEMM on hipBLASLt (residual via beta=1) followed by our
-                    stand-alone RoPE / SwiGLU epilogue kernels;
-  * ``auto``      — per (op, N, K, M-bucket) the faster of the two, timed once on first use
-                    (scratch outputs, so in-place ops are not applied twice).
-On the 70B bench ``auto`` is ~1.4% faster end to end but needs the unfused [M, 2I] SwiGLU
-intermediate (peak HBM 6.8 GB vs 4.9 GB), so the hand-written path is the default.
-Both paths are numerically checked against each other in tests/test_kernels_gpu.py.
-Measured trade-off on 70B shapes: profiles/r1_gemm_ablation/README.md.
+Projection GEMMs are the fused MFMA kernels of ``csrc/kernels/gemm.hip``:
+RoPE / SwiGLU / residual / bias epilogues in registers, on the checkpoint's
+own weight layout (``wqkv = [q; k; v]``, ``wgu = [gate; up]``).
 """
 from __future__ import annotations
-
-import os
 
 import torch
 
@@ -27,6 +18,7 @@ from .. import _native
 from .torch_backend import fill_params
 
 EPI_NONE, EPI_RESID, EPI_SWIGLU, EPI_ROPE = 0, 1, 2, 3
+CAST_BF16, CAST_F32 = 1, 2
 
 
 def _stream():
@@ -51,41 +43,6 @@ class HipOps:
 
     def __init__(self):
         self.k = _native.kernels()
-        self.backend = os.environ.get("FLS_GEMM_BACKEND", "hip")
-        if self.backend not in ("auto", "hip", "hipblaslt"):
-            raise ValueError(f"FLS_GEMM_BACKEND={self.backend!r}")
-        self.choice = {}          # (op, N, K, M-bucket) -> "hip" | "hipblaslt"
-        self.timings = {}
-
-    # ------------------------------------------------------- backend choice
-    def _pick(self, op, x, w, run_hip, run_blt, scratch_hip, scratch_blt):
-        if self.backend == "hip":
-            return run_hip()
-        if self.backend == "hipblaslt":
-            return run_blt()
-        M = x.shape[0]
-        key = (op, w.shape[0], w.shape[1], max(M, 1).bit_length())
-        ch = self.choice.get(key)
-        if ch is None:
-            ch = self._tune(key, scratch_hip, scratch_blt)
-        return run_hip() if ch == "hip" else run_blt()
-
-    def _tune(self, key, f_hip, f_blt, reps: int = 3):
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-        f_hip(); f_blt()                      # warm (kernel load / heuristics)
-        ev[0].record()
-        for _ in range(reps):
-            f_hip()
-        ev[1].record()
-        for _ in range(reps):
-            f_blt()
-        ev[2].record()
-        ev[2].synchronize()
-        th, tb = ev[0].elapsed_time(ev[1]) / reps, ev[1].elapsed_time(ev[2]) / reps
-        ch = "hip" if th <= tb else "hipblaslt"
-        self.choice[key] = ch
-        self.timings[key] = {"hip_ms": th, "hipblaslt_ms": tb, "choice": ch}
-        return ch
 
     # ---------------------------------------------------------------- GEMM
     def gemm(self, x: torch.Tensor, w: torch.Tensor, epi: int = EPI_NONE, out: torch.Tensor = None,
@@ -126,66 +83,25 @@ class HipOps:
         return out
 
     def linear(self, x, w):
-        if x.shape[0] <= 16 and x.shape[1] % 32 == 0 and self.backend != "hipblaslt":
+        if x.shape[0] <= 16 and x.shape[1] % 32 == 0:
             return self.gemv_skinny(x, w)
-        return self._pick("linear", x, w, lambda: self.gemm(x, w), lambda: torch.matmul(x, w.t()),
-                          lambda: self.gemm(x, w), lambda: torch.matmul(x, w.t()))
+        return self.gemm(x, w)
 
     def linear_residual(self, x, w, resid, bias=None):
+        """resid += x @ w^T (+ bias), in place."""
         _f16(resid, "resid")
-
-        def hip():
-            return self.gemm(x, w, EPI_RESID, out=resid, resid=resid, bias=bias)
-
-        def blt():
-            if bias is not None:
-                resid.add_(bias)
-            return resid.addmm_(x, w.t())
-
-        scratch = [None]
-
-        def s_hip():
-            if scratch[0] is None:
-                scratch[0] = torch.empty_like(resid)
-            return self.gemm(x, w, EPI_RESID, out=scratch[0], resid=resid, bias=bias)
-
-        def s_blt():
-            if scratch[0] is None:
-                scratch[0] = torch.empty_like(resid)
-            return torch.addmm(resid, x, w.t(), out=scratch[0])
-
-        return self._pick("resid", x, w, hip, blt, s_hip, s_blt)
+        return self.gemm(x, w, EPI_RESID, out=resid, resid=resid, bias=bias)
 
     def swiglu_up(self, x, wgu):
-        def hip():
-            return self.gemm(x, wgu, EPI_SWIGLU)
-
-        def blt():
-            y = torch.matmul(x, wgu.t())
-            out = torch.empty(y.shape[0], y.shape[1] // 2, dtype=torch.float16, device=y.device)
-            _chk(self.k.fls_swiglu(y.data_ptr(), out.data_ptr(), y.shape[0], y.shape[1] // 2, y.stride(0),
-                                   out.stride(0), _stream()), "fls_swiglu")
-            return out
-
-        return self._pick("swiglu", x, wgu, hip, blt, hip, blt)
+        """silu(x @ gate^T) * (x @ up^T) with wgu = [gate; up]."""
+        return self.gemm(x, wgu, EPI_SWIGLU)
 
     def qkv_rope(self, x, wqkv, positions, cos, sin, n_q_heads, n_kv_heads, head_dim, bias=None):
         if positions.dtype != torch.int32:
             raise TypeError("positions must be int32")
         rope_cols = (n_q_heads + n_kv_heads) * head_dim
-
-        def hip():
-            return self.gemm(x, wqkv, EPI_ROPE, positions=positions, cos=cos, sin=sin,
-                             rope_cols=rope_cols, head_dim=head_dim, bias=bias)
-
-        def blt():
-            y = torch.matmul(x, wqkv.t()) if bias is None else torch.addmm(bias, x, wqkv.t())
-            _chk(self.k.fls_rope_inplace(y.data_ptr(), positions.data_ptr(), cos.data_ptr(), sin.data_ptr(),
-                                         y.shape[0], y.stride(0), rope_cols, head_dim, _stream()),
-                 "fls_rope_inplace")
-            return y
-
-        return self._pick("qkv_rope", x, wqkv, hip, blt, hip, blt)
+        return self.gemm(x, wqkv, EPI_ROPE, positions=positions, cos=cos, sin=sin,
+                         rope_cols=rope_cols, head_dim=head_dim, bias=bias)
 
     # ----------------------------------------------------------- attention
     def attention(self, qkv, work, n_q_heads, n_kv_heads, head_dim, kv0=None, q_block: int = 64):
@@ -243,6 +159,11 @@ class HipOps:
 
     def lm_head_softmax(self, h, w):
         return self.softmax(self.linear(h, w))
+
+    def cast_f16(self, dst: torch.Tensor, src: torch.Tensor, src_code: int) -> None:
+        """dst (fp16 bytes) = fp16(src bytes of bf16 (code 1; may be in place) or fp32 (code 2))."""
+        n = dst.numel() * dst.element_size() // 2
+        _chk(self.k.fls_cast_f16(dst.data_ptr(), src.data_ptr(), src_code, n, _stream()), "fls_cast_f16")
 
     def fill_layer_random(self, buf: torch.Tensor, layout, seed: int, std: float = 0.02) -> None:
         views = layout.views(buf, torch.float16)

@@ -3,16 +3,14 @@
 Semantics follow the HF Llama block the reference drives
 (``/root/reference/utils.py:266-290``): RMSNorm with fp32
 statistics, RoPE rotate-half with fp16-rounded cos/sin tables, softmax in
-fp32, SwiGLU MLP.  Activations use the packed-weight conventions of
-:mod:`..models.layout` (RoPE-pair-permuted q/k head dims, 16-row gate/up
-interleave) so this backend is a drop-in oracle for the HIP kernels.
+fp32, SwiGLU MLP.  Weights are the packed images of :mod:`..models.layout`
+(checkpoint row order: ``wqkv = [q; k; v]``, ``wgu = [gate; up]``), exactly
+what the HIP kernels consume, so this backend is a drop-in oracle for them.
 """
 from __future__ import annotations
 
 import torch
 import torch.nn.functional as F
-
-from ..models.layout import PAIR_BLOCK
 
 
 class TorchOps:
@@ -47,11 +45,9 @@ class TorchOps:
         return (self._c(resid) + y).to(resid.dtype)
 
     def swiglu_up(self, x: torch.Tensor, wgu: torch.Tensor) -> torch.Tensor:
-        y = self._c(x) @ self._c(wgu).t()                     # [T, 2I] interleaved
-        T, I2 = y.shape
-        y = y.view(T, I2 // (2 * PAIR_BLOCK), 2, PAIR_BLOCK)
-        g, u = y[:, :, 0, :], y[:, :, 1, :]
-        return (F.silu(g) * u).reshape(T, I2 // 2).to(x.dtype)
+        y = self._c(x) @ self._c(wgu).t()                     # [T, 2I] = [gate | up]
+        I = y.shape[1] // 2
+        return (F.silu(y[:, :I]) * y[:, I:]).to(x.dtype)
 
     def qkv_rope(self, x: torch.Tensor, wqkv: torch.Tensor, positions: torch.Tensor,
                  cos: torch.Tensor, sin: torch.Tensor, n_q_heads: int, n_kv_heads: int,
@@ -61,15 +57,14 @@ class TorchOps:
             y = y + self._c(bias)
         qk_cols = (n_q_heads + n_kv_heads) * head_dim
         T = y.shape[0]
-        qk = y[:, :qk_cols].reshape(T, n_q_heads + n_kv_heads, head_dim // (2 * PAIR_BLOCK), 2, PAIR_BLOCK)
-        c = cos.index_select(0, positions.long()).to(self.cdt)   # [T, hd/2]
-        s = sin.index_select(0, positions.long()).to(self.cdt)
-        c = c.reshape(T, 1, head_dim // (2 * PAIR_BLOCK), PAIR_BLOCK)
-        s = s.reshape(T, 1, head_dim // (2 * PAIR_BLOCK), PAIR_BLOCK)
-        x1, x2 = qk[:, :, :, 0, :], qk[:, :, :, 1, :]
+        half = head_dim // 2
+        qk = y[:, :qk_cols].reshape(T, n_q_heads + n_kv_heads, 2, half)   # HF rotate_half halves
+        c = cos.index_select(0, positions.long()).to(self.cdt).reshape(T, 1, half)   # [T, 1, hd/2]
+        s = sin.index_select(0, positions.long()).to(self.cdt).reshape(T, 1, half)
+        x1, x2 = qk[:, :, 0, :], qk[:, :, 1, :]
         o1 = x1 * c - x2 * s
         o2 = x2 * c + x1 * s
-        qk_out = torch.stack([o1, o2], dim=3).reshape(T, qk_cols)
+        qk_out = torch.stack([o1, o2], dim=2).reshape(T, qk_cols)
         return torch.cat([qk_out, y[:, qk_cols:]], dim=1).to(x.dtype)
 
     def attention(self, qkv: torch.Tensor, segments, n_q_heads: int, n_kv_heads: int,

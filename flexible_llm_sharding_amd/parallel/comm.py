@@ -25,10 +25,12 @@ import torch.distributed as dist
 class Comm:
     """Thin wrapper; ``world == 1`` works without an initialised process group."""
 
-    def __init__(self, rank: int = 0, world: int = 1, device=None, backend: Optional[str] = None):
+    def __init__(self, rank: int = 0, world: int = 1, device=None, backend: Optional[str] = None,
+                 group=None):
         self.rank, self.world = rank, world
         self.device = torch.device(device) if device is not None else torch.device("cpu")
         self.backend = backend
+        self.group = group          # None: the default process group
 
     @property
     def active(self) -> bool:
@@ -56,6 +58,17 @@ class Comm:
                 kw["device_id"] = dev
             dist.init_process_group(**kw)
         return cls(rank, world, dev, backend)
+
+    def dup(self) -> "Comm":
+        """A Comm on a fresh communicator over the same ranks (collective: every rank calls it).
+
+        The data-parallel weight all-gathers run on their own communicator, issued by the
+        loader thread, so they never interleave with the main thread's collectives on the
+        default group (each communicator sees the same op sequence on every rank)."""
+        if not self.active:
+            return Comm(self.rank, self.world, self.device, self.backend)
+        return Comm(self.rank, self.world, self.device, self.backend,
+                    group=dist.new_group(ranks=list(range(self.world))))
 
     # -------------------------------------------------------------- p2p
     def setup_p2p_edges(self, edges) -> None:
@@ -92,7 +105,7 @@ class Comm:
                 dist.barrier()
 
     def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False):
-        return dist.all_gather_into_tensor(out, inp, async_op=async_op)
+        return dist.all_gather_into_tensor(out, inp, group=self.group, async_op=async_op)
 
     def all_reduce_max(self, x: float) -> float:
         if not self.active:

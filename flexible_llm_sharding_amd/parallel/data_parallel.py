@@ -5,14 +5,24 @@ of the current layer shared by every GPU thread; each GPU then copies the
 whole layer over its own PCIe link (G x the host traffic) and the GPUs move
 in lock-step under a Condition/Lock pair (ABBA order).
 
-MI355X design: each rank keeps only ITS 1/G byte-slice of every packed layer
-in pinned host memory (138/G GB for 70B), DMAs that slice into HBM over its
-own PCIe link, and the full layer is re-assembled in the HBM weight slot by
-``all_gather_into_tensor`` — RCCL over the fully connected xGMI fabric
-(7 links per GPU) — on the copy side of the double buffer, so shard k+1's
-H2D + all-gather overlap shard k's compute.  Per layer and GPU the PCIe
-traffic drops G-fold; every rank issues the same collectives in the same
-order (no P2P ordering hazards, no polling).  Prompts are split with
+MI355X design: each rank owns only ITS 1/G byte-slice of every packed layer
+and DMAs that slice into HBM over its own PCIe link; the full layer is
+re-assembled in the HBM weight slot by ``all_gather_into_tensor`` — RCCL over
+the fully connected xGMI fabric (7 links per GPU) — on the copy side of the
+double buffer, so shard k+1's H2D + all-gather overlap shard k's compute.
+The slice comes from either
+
+* pinned host RAM (:class:`SlicedHostStore`, ``--weight_cache host``: 138/G GB
+  per rank for 70B, each rank reading only its byte ranges of the layer files
+  once at start-up), or
+* the layer files on every pass (:class:`~..runtime.stream.FileLayerSource`,
+  ``--weight_cache stream``): each rank streams only its 1/G byte range, so
+  every file is read from disk once per pass for all GPUs — the reference's
+  shared host cache without the host copy.
+
+Per layer and GPU the PCIe (and disk) traffic drops G-fold; every rank issues
+the same collectives in the same order (no P2P ordering hazards, no polling),
+including ranks whose prompt slice is empty.  Prompts are split with
 ``np.array_split`` like ``main.py:69-70``; scores are gathered to rank 0.
 """
 from __future__ import annotations
@@ -49,28 +59,14 @@ class SlicedHostStore(HostStore):
     @classmethod
     def from_source(cls, src: LayerSource, rank: int, world: int, pinned: bool = True,
                     names: Optional[Sequence[str]] = None) -> "SlicedHostStore":
+        """Read only this rank's byte slice of every layer (``read_range_into``)."""
         st = cls(src.cfg, rank, world, src.dtype, pinned, names)
-        if hasattr(src, "read_range_into"):
-            # packed images on disk: read only this rank's byte slice of each layer
-            for n in st.names:
-                nb, c = st.nbytes(n), st.chunk_bytes(n)
-                buf = hostmem.alloc_host(c, pinned=pinned)
-                lo, hi = rank * c, min(nb, (rank + 1) * c)
-                if hi > lo:
-                    src.read_range_into(n, buf, lo, hi)
-                st.buffers[n] = buf
-            return st
-        full = None
         for n in st.names:
-            nb = st.nbytes(n)
-            if full is None or full.numel() < nb:
-                full = torch.empty(max(nb, max(st.nbytes(x) for x in st.names)), dtype=torch.uint8)
-            src.read_into(n, full)
-            c = st.chunk_bytes(n)
+            nb, c = st.nbytes(n), st.chunk_bytes(n)
             buf = hostmem.alloc_host(c, pinned=pinned)
             lo, hi = rank * c, min(nb, (rank + 1) * c)
             if hi > lo:
-                buf[:hi - lo].copy_(full[lo:hi])
+                src.read_range_into(n, buf, lo, hi)
             st.buffers[n] = buf
         return st
 
@@ -86,48 +82,73 @@ class SlicedHostStore(HostStore):
 
 class AllGatherPrefetcher(ShardPrefetcher):
     """Shard prefetcher whose H2D moves only this rank's slice; the layer is
-    completed in HBM with one all-gather per layer over xGMI."""
+    completed in HBM with one all-gather per layer over xGMI.
 
-    def __init__(self, store: SlicedHostStore, layer_names, shards, device, comm: Comm,
+    ``store`` is a :class:`SlicedHostStore` (slices pinned in host RAM) or a
+    streaming :class:`~..runtime.stream.FileLayerSource` (slices read from the
+    layer files every pass by a loader thread, bf16 cast after the gather)."""
+
+    collective = True      # every rank must acquire every shard (engine: empty prompt slices too)
+
+    def __init__(self, store: LayerSource, layer_names, shards, device, comm: Comm,
                  n_slots: int = 2, resident: bool = False):
-        self.comm = comm
+        self.comm = comm.dup()               # own communicator: gathers come from the loader thread
         self.store = store
+        self.streaming = not isinstance(store, SlicedHostStore)
         super().__init__(store, layer_names, shards, device, n_slots=n_slots, resident=resident)
-        self._pool = None                     # slices are host-resident: no loader thread
+        if not self.streaming:
+            self._pool = None                 # slices are host-resident: no loader thread
+        self.bytes_read = 0                   # file bytes this rank read (streaming)
+
+    def chunk_bytes(self, name: str) -> int:
+        return shard_chunk_bytes(self.store.nbytes(name), self.comm.world)
 
     def shard_bytes(self, k: int) -> int:
         G = self.comm.world
-        return sum(_align(self.store.chunk_bytes(self.names[i]) * G) for i in self.shards[k])
+        return sum(_align(self.chunk_bytes(self.names[i]) * G) for i in self.shards[k])
 
     def _load(self, k: int):
         t0 = time.perf_counter()
         s = self.slot_of(k)
         slot = self._slot(s)
-        G = self.comm.world
+        G, r = self.comm.world, self.comm.rank
         views: Dict[str, Dict[str, torch.Tensor]] = {}
-        works: List = []
         ctx = torch.cuda.stream(self.copy_stream) if self.cuda else _nullctx()
+        ev = None
         with ctx:
             if self.cuda and self._free_ev[s] is not None:
                 self.copy_stream.wait_event(self._free_ev[s])
             off = 0
-            for j, i in enumerate(self.shards[k]):
+            for i in self.shards[k]:
                 name = self.names[i]
                 nb = self.store.nbytes(name)
-                c = self.store.chunk_bytes(name)
+                c = self.chunk_bytes(name)
                 region = slot[off:off + c * G]
-                # in-place all-gather: this rank's slice is H2D'd straight into its own place in the
+                # in-place all-gather: this rank's slice lands straight in its own place in the
                 # slot (RCCL's sendbuff == recvbuff + rank * count form), so no staging buffer in HBM
-                mine = region[self.comm.rank * c:(self.comm.rank + 1) * c]
-                mine.copy_(self.store.buffers[name][:c], non_blocking=self.cuda)
+                mine = region[r * c:(r + 1) * c]
+                lo, hi = r * c, min(nb, (r + 1) * c)
+                if not self.streaming:
+                    mine.copy_(self.store.buffers[name][:c], non_blocking=self.cuda)
+                elif hi > lo and self.cuda:
+                    self.bytes_read += self.store.stream_into(name, mine, self.copy_stream, lo, hi, cast=False)
+                elif hi > lo:
+                    before = self.store.read_bytes
+                    self.store.read_range_into(name, mine, lo, hi)
+                    self.bytes_read += self.store.read_bytes - before
                 w = self.comm.all_gather_into(region, mine, async_op=self.cuda)
                 if self.cuda:
-                    works.append(w)
+                    w.wait()                  # the copy stream waits for the gather, not the host
+                if self.streaming and self.cuda:
+                    self.store.cast_on_gpu(name, region)
                 views[name] = self.store.layout(name).views(region[:nb], self.dtype)
                 off += _align(c * G)
-                self.bytes_h2d += c
+                self.bytes_h2d += max(0, hi - lo)
+            if self.cuda:
+                ev = torch.cuda.Event()
+                ev.record(self.copy_stream)
         self.load_seconds += time.perf_counter() - t0
-        return works, views, s
+        return ev, views, s
 
 
 class _nullctx:
@@ -138,20 +159,21 @@ class _nullctx:
         return False
 
 
-def build_dp_sharded_runner(args, cfg, device, comm: Comm, tok, store: Optional[SlicedHostStore] = None):
+def build_dp_sharded_runner(args, cfg, device, comm: Comm, tok, store: Optional[LayerSource] = None,
+                            weight_cache: str = "host"):
+    """Data-parallel runner with scatter-loaded weights: ``weight_cache`` ``host`` pins this
+    rank's slices (read once), ``stream`` re-reads them from the layer files every pass."""
     from ..config import MAX_TOKEN_LEN
     from ..engine import ShardedRunner
-    from ..runtime.weights import FileLayerSource
+    from ..runtime.stream import FileLayerSource
     from .planner import make_plan
     device = torch.device(device)
     if store is None and getattr(args, "synthetic", None):
         store = SlicedHostStore.synthetic(cfg, device, comm.rank, comm.world, pinned=device.type == "cuda")
     elif store is None:
-        src = FileLayerSource(cfg, args.model_path)
-        if getattr(args, "weight_cache", "host") == "packed":
-            from ..api import open_packed_source
-            src = open_packed_source(args, cfg, comm, None)
-        store = SlicedHostStore.from_source(src, comm.rank, comm.world, pinned=device.type == "cuda")
+        src = FileLayerSource(cfg, args.model_path, direct=getattr(args, "o_direct", False))
+        store = src if weight_cache == "stream" else SlicedHostStore.from_source(
+            src, comm.rank, comm.world, pinned=device.type == "cuda")
     names = cfg.layer_names()
     plan = make_plan(len(names), args.layer_num_per_shard, comm.world, comm.rank, True)
     shards = [s for s in plan.my_shards if len(s)]
@@ -170,4 +192,5 @@ def build_dp_sharded_runner(args, cfg, device, comm: Comm, tok, store: Optional[
                          max_token_len=getattr(args, "max_token_len", None) or MAX_TOKEN_LEN,
                          hip_graphs=getattr(args, "hip_graphs", False),
                          prefix_kv_cache=getattr(args, "prefix_kv_cache", False),
-                         prefix_cache_entries=getattr(args, "prefix_cache_entries", 8))
+                         prefix_cache_entries=getattr(args, "prefix_cache_entries", 8),
+                         max_vram_gb=getattr(args, "max_vram_gb", None))

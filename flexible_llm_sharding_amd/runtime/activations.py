@@ -15,7 +15,10 @@ Here the store keys whole micro-batches and reuses the copy engine:
   fp16 after a standard header) with the native ``pwrite`` engine; a reader
   thread ``pread``s it back into pinned memory ahead of use.
 
-Pinned buffers are pooled by size so the steady state allocates nothing.
+Pinned buffers are pooled in 1 MiB size buckets so the steady state allocates
+nothing; :meth:`ActivationStore.trim` (end of every call) frees the buckets the
+call did not use, so the pool tracks the current shapes instead of growing with
+every new batch / generation-step shape (``--num_batch`` still bounds RAM).
 """
 from __future__ import annotations
 
@@ -72,13 +75,17 @@ class ActivationStore:
         self._io = ThreadPoolExecutor(2, thread_name_prefix="fls-spill") if mode == "disk" else None
         self._inflight: Dict[object, Tuple[Future, None]] = {}
         self._recycle: List[Tuple[torch.Tensor, torch.cuda.Event]] = []
+        self._used_keys = set()           # pool buckets handed out since the last trim()
         self.bytes_d2h = 0
         self.bytes_h2d = 0
         self._stall_ev: List[Tuple[torch.cuda.Event, torch.cuda.Event]] = []   # compute-stream waits on H2D
         self.lock = threading.Lock()
 
     # ------------------------------------------------------------- pool
+    BUCKET = 1 << 20
+
     def _get_host(self, nbytes: int) -> torch.Tensor:
+        key = (max(1, nbytes) + self.BUCKET - 1) // self.BUCKET * self.BUCKET
         with self.lock:
             keep = []
             for h, ev in self._recycle:
@@ -87,18 +94,36 @@ class ActivationStore:
                 else:
                     keep.append((h, ev))
             self._recycle = keep
-            lst = self._pool.get(nbytes)
+            self._used_keys.add(key)
+            lst = self._pool.get(key)
             if lst:
                 return lst.pop()
-        return hostmem.alloc_host(nbytes, pinned=self.cuda)
+        return hostmem.alloc_host(key, pinned=self.cuda)
+
+    def pooled_bytes(self) -> int:
+        with self.lock:
+            return sum(k * len(v) for k, v in self._pool.items())
+
+    def trim(self) -> None:
+        """Free pooled buffers of sizes not used since the last trim (call between calls, when
+        every buffer is back in the pool)."""
+        with self.lock:
+            for h, ev in self._recycle:
+                ev.synchronize()
+                self._pool[h.numel()].append(h)
+            self._recycle = []
+            for k in list(self._pool):
+                if k not in self._used_keys:
+                    del self._pool[k]
+            self._used_keys = set()
 
     def _put_host(self, buf: torch.Tensor) -> None:
         with self.lock:
             self._pool[buf.numel()].append(buf)
 
     def host_buffer(self, nbytes: int) -> torch.Tensor:
-        """A pooled pinned buffer (rounded up to 1 MiB buckets) for other D2H users."""
-        return self._get_host((nbytes + (1 << 20) - 1) >> 20 << 20)
+        """A pooled pinned buffer (rounded up to a 1 MiB bucket) for other D2H users."""
+        return self._get_host(nbytes)
 
     def recycle_host(self, buf: torch.Tensor) -> None:
         """Return a buffer obtained from :meth:`host_buffer` to the pool."""
@@ -137,7 +162,7 @@ class ActivationStore:
         cur = torch.cuda.current_stream(self.dev)
         self.d2h.wait_stream(cur)
         with torch.cuda.stream(self.d2h):
-            host.view(t.dtype).view(e.shape).copy_(t, non_blocking=True)
+            host[:nbytes].view(t.dtype).view(e.shape).copy_(t, non_blocking=True)
             t.record_stream(self.d2h)
             ev = torch.cuda.Event()
             ev.record(self.d2h)

@@ -20,18 +20,31 @@ from ..utils import safetensors_io
 
 _IO_THREADS = int(os.environ.get("FLS_IO_THREADS", "8"))
 
+# pinned bytes currently held / high-water mark (alloc_host blocks; the streamer's ring is
+# reported by runtime.stream separately)
+pinned_live = 0
+pinned_peak = 0
+
+
+def _count(n: int) -> None:
+    global pinned_live, pinned_peak
+    pinned_live += n
+    pinned_peak = max(pinned_peak, pinned_live)
+
 
 class _PinnedOwner:
-    __slots__ = ("ptr", "lib", "__weakref__")
+    __slots__ = ("ptr", "lib", "n", "__weakref__")
 
-    def __init__(self, ptr, lib):
-        self.ptr, self.lib = ptr, lib
+    def __init__(self, ptr, lib, n):
+        self.ptr, self.lib, self.n = ptr, lib, n
+        _count(n)
 
     def __del__(self):
         try:
             if self.ptr:
                 self.lib.fls_pinned_free(self.ptr)
                 self.ptr = None
+                _count(-self.n)
         except Exception:
             pass
 
@@ -58,7 +71,7 @@ def alloc_host(nbytes: int, pinned: bool = True) -> torch.Tensor:
             if ptr:
                 arr_t = type("PinnedBlock", (ctypes.c_uint8 * n,), {})
                 arr = arr_t.from_address(ptr)
-                arr.owner = _PinnedOwner(ptr, rt)
+                arr.owner = _PinnedOwner(ptr, rt, n)
                 return torch.frombuffer(arr, dtype=torch.uint8)[:nbytes]
         return torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
     return torch.empty(nbytes, dtype=torch.uint8)

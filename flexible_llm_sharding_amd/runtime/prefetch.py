@@ -10,8 +10,9 @@ once; no per-shard free).  Shard ``k+1`` is copied into the other slot on a
 dedicated copy stream while shard ``k`` computes; the compute stream waits on
 a per-shard *ready* event, and the copy stream waits on the slot's *free*
 event recorded when the compute stream finished with its previous occupant.
-File-backed sources are read by a loader thread into two pinned staging
-buffers so disk reads, PCIe DMA and compute all overlap.
+File-backed sources (:class:`~.stream.FileLayerSource`) are streamed by a
+loader thread through the native streamer's pinned chunk ring straight into
+the slot, so disk reads, PCIe DMA and compute all overlap.
 
 ``resident=True`` gives every shard its own slot and never evicts (the whole
 model stays in the 288 GB HBM — BASELINE config 5).
@@ -123,7 +124,9 @@ class ShardPrefetcher:
                 nb = self.src.nbytes(name)
                 dst = slot[off:off + nb]
                 hb = self.src.host_buffer(name)
-                if hb is None:
+                if hb is None and hasattr(self.src, "stream_into"):
+                    self.src.stream_into(name, dst, self.copy_stream)
+                elif hb is None:
                     stage, si = self._stage_buf(nb)
                     self.src.read_into(name, stage)
                     dst.copy_(stage[:nb], non_blocking=True)
@@ -179,6 +182,11 @@ class ShardPrefetcher:
             self._loaded_resident.add(k)
         self.wait_seconds += time.perf_counter() - t0
         return views
+
+    def take_wait_seconds(self) -> float:
+        """Host time spent in :meth:`acquire` waiting for loads since the last call."""
+        t, self.wait_seconds = self.wait_seconds, 0.0
+        return t
 
     def take_stall_seconds(self) -> float:
         """GPU time the compute stream spent waiting for weight H2D since the last call

@@ -6,32 +6,28 @@ whole from disk, deserialized to CPU tensors and copied parameter by parameter
 (pageable, synchronous) to the GPU; the whole thing repeats for every batch,
 generation step and GPU.
 
-Here a source yields the *packed* layer (see :mod:`..models.layout`):
+Here a source yields the *packed* layer image (see :mod:`..models.layout`):
 
-* :class:`FileLayerSource` — per-layer safetensors files, read with the native
-  multi-threaded ``pread`` engine (or Python ``readinto``) and packed on the
-  host; used when host RAM is scarce (``--weight_cache disk``).
+* :class:`~.stream.FileLayerSource` — per-layer safetensors files streamed
+  every pass (file byte ranges -> pinned chunk ring -> HBM DMA, no CPU work);
+  the reference's small-RAM mode (``--weight_cache stream``).
 * :class:`HostStore` — every packed layer resident in pinned host memory
-  (read once), so each shard H2D is one DMA at PCIe line rate; default when
-  RAM allows.  Also built directly from synthetic random-init weights
-  (generated on the GPU and copied down) for the 70B benchmark.
+  (read once), so each shard H2D is one DMA at PCIe line rate
+  (``--weight_cache host``).  Also built directly from synthetic random-init
+  weights (generated on the GPU and copied down) for the 70B benchmark.
 * ``shard_fraction`` (data-parallel scatter-load): a rank keeps only its
   1/G byte-slice of every layer; the full layer is re-assembled in HBM with an
   RCCL all-gather over xGMI (:mod:`..parallel.data_parallel`).
 """
 from __future__ import annotations
 
-import os
 import threading
-import time
 from typing import Dict, List, Optional, Sequence
 
 import torch
 
 from ..config import ModelConfig
-from ..models.layout import LayerLayout, layer_kind, layer_layout, pack_layer
-from ..utils.layer_format import layer_file
-from ..utils.safetensors_io import load_file, read_header
+from ..models.layout import LayerLayout, layer_kind, layer_layout
 from . import hostmem
 
 
@@ -51,26 +47,6 @@ class LayerSource:
 
     def read_into(self, name: str, dst: torch.Tensor) -> None:
         raise NotImplementedError
-
-
-class FileLayerSource(LayerSource):
-    """Per-layer safetensors files in ``model_path`` (format of prepare_weights.py)."""
-
-    def __init__(self, cfg: ModelConfig, model_path: str, dtype=torch.float16):
-        self.cfg, self.model_path, self.dtype = cfg, model_path, dtype
-        missing = [n for n in cfg.layer_names() if not os.path.exists(layer_file(model_path, n))]
-        if missing:
-            raise FileNotFoundError(f"{model_path}: missing layer files {missing[:4]}...")
-        self.read_seconds = 0.0
-        self.read_bytes = 0
-
-    def read_into(self, name: str, dst: torch.Tensor) -> None:
-        t0 = time.perf_counter()
-        path = layer_file(self.model_path, name)
-        sd = hostmem.read_safetensors(path)
-        self.read_bytes += sum(v.numel() * v.element_size() for v in sd.values())
-        pack_layer(self.cfg, name, sd, self.dtype, out=dst[:self.nbytes(name)])
-        self.read_seconds += time.perf_counter() - t0
 
 
 class HostStore(LayerSource):
@@ -130,7 +106,8 @@ class HostStore(LayerSource):
     @classmethod
     def from_model_path(cls, cfg: ModelConfig, model_path: str, dtype=torch.float16,
                         pinned: bool = True, threads: int = 4) -> "HostStore":
-        return cls.from_source(FileLayerSource(cfg, model_path, dtype), pinned, threads)
+        from .stream import FileLayerSource
+        return cls.from_source(FileLayerSource(cfg, model_path, dtype=dtype), pinned, threads)
 
     @classmethod
     def synthetic(cls, cfg: ModelConfig, device: torch.device, seed: int = 0, std: float = 0.02,

@@ -52,17 +52,22 @@ def build_parser() -> argparse.ArgumentParser:
                    help="prefix K/V cache: calls (prompt batches) kept, LRU")
     p.add_argument("--resident", type=str2bool, nargs="?", const=True, default=False,
                    help="keep every shard resident in HBM after first load (288 GB fits 70B)")
-    p.add_argument("--weight_cache", choices=["host", "disk", "packed"], default="host",
-                   help="host: pack every layer once into pinned host RAM (fastest, needs ~model-size RAM); "
-                        "disk: re-read + re-pack the per-layer safetensors every pass (reference behaviour); "
-                        "packed: stream pre-packed layer images from --packed_dir (built on first use)")
-    p.add_argument("--packed_dir", type=str, default=None,
-                   help="packed-layer cache directory (default: <model_path>/.fls_packed)")
+    p.add_argument("--weight_cache", choices=["auto", "host", "stream", "disk"], default="auto",
+                   help="host: read every layer once into pinned host RAM (needs ~model-size RAM); "
+                        "stream (alias disk, the reference behaviour): re-read the per-layer safetensors every "
+                        "pass through a small pinned chunk ring (~256 MB of RAM) straight into HBM; "
+                        "auto: host if it fits --host_mem_gb, else stream")
+    p.add_argument("--host_mem_gb", type=float, default=None,
+                   help="host RAM budget for --weight_cache auto / host (default: 80%% of MemAvailable)")
+    p.add_argument("--o_direct", type=str2bool, nargs="?", const=True, default=False,
+                   help="stream layer files with O_DIRECT (bypass the page cache)")
     p.add_argument("--dp_weight_shard", type=str2bool, nargs="?", const=True, default=True,
                    help="data parallel: scatter-load 1/G of each layer per GPU + RCCL all-gather")
     p.add_argument("--pipeline_stages", choices=["round_robin", "contiguous"], default="round_robin",
                    help="model parallel: shard k on GPU k mod G (reference) or one contiguous stage per GPU")
     p.add_argument("--token_budget", type=int, default=16384, help="max tokens per packed micro-batch")
+    p.add_argument("--max_vram_gb", type=float, default=None,
+                   help="HBM cap per GPU: sizes --token_budget and the MLP chunk to fit (reference: 70B in 6 GB)")
     p.add_argument("--dtype", choices=["float16", "float32"], default=None,
                    help="activation dtype (default fp16 on GPU, fp32 on CPU)")
     p.add_argument("--verbose", type=str2bool, nargs="?", const=True, default=False)

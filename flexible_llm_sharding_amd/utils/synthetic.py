@@ -23,19 +23,19 @@ from .tokenizer import synthetic_word, write_synthetic_tokenizer
 
 
 def synthetic_layer_state_dict(cfg: ModelConfig, layer_name: str, seed: int = 0,
-                               std: float = 0.02, dtype=torch.float16) -> Dict[str, torch.Tensor]:
+                               std: float = 0.02, dtype=torch.float16, device="cpu") -> Dict[str, torch.Tensor]:
     idx = cfg.layer_names().index(layer_name)
-    g = torch.Generator().manual_seed(seed * 1000003 + idx)
+    g = torch.Generator(device=device).manual_seed(seed * 1000003 + idx)
     H, I, V = cfg.hidden_size, cfg.intermediate_size, cfg.vocab_size
 
     def rnd(*shape):
-        return (torch.randn(*shape, generator=g) * std).to(dtype)
+        return (torch.randn(*shape, generator=g, device=device) * std).to(dtype)
 
     def norm_w(n):
-        return (1.0 + 0.1 * torch.randn(n, generator=g)).to(dtype)
+        return (1.0 + 0.1 * torch.randn(n, generator=g, device=device)).to(dtype)
 
     if layer_name == "model.embed_tokens":
-        return {"model.embed_tokens.weight": (torch.randn(V, H, generator=g) * 1.0).to(dtype)}
+        return {"model.embed_tokens.weight": (torch.randn(V, H, generator=g, device=device) * 1.0).to(dtype)}
     if layer_name == "model.norm":
         return {"model.norm.weight": norm_w(H)}
     if layer_name == "lm_head":
@@ -63,13 +63,29 @@ def synthetic_layer_state_dict(cfg: ModelConfig, layer_name: str, seed: int = 0,
 
 
 def write_synthetic_checkpoint(cfg: ModelConfig, out_dir: str, seed: int = 0,
-                               std: float = 0.02, dtype=torch.float16) -> None:
+                               std: float = 0.02, dtype=torch.float16, unique_layers: int = 0,
+                               device="cpu", progress=None) -> None:
+    """``unique_layers`` > 0: only the first K decoder layers get their own random weights;
+    decoder layer i >= K is a hard link to layer i % K (a 138 GB 70B checkpoint in ~K x 1.7 GB of
+    disk for streaming benchmarks — the reads are per file, as for a real checkpoint)."""
     os.makedirs(out_dir, exist_ok=True)
     cfg.save(out_dir)
     write_synthetic_tokenizer(out_dir, cfg.vocab_size)
-    for name in cfg.layer_names():
-        sd = synthetic_layer_state_dict(cfg, name, seed, std, dtype)
-        save_file(sd, layer_file(out_dir, name))
+    names = cfg.layer_names()
+    for li, name in enumerate(names):
+        if progress is not None:
+            progress(li, len(names))
+        path = layer_file(out_dir, name)
+        if unique_layers and name.startswith("model.layers."):
+            i = int(name.split(".")[2])
+            if i >= unique_layers:
+                src = layer_file(out_dir, f"model.layers.{i % unique_layers}")
+                if os.path.exists(path):
+                    os.remove(path)
+                os.link(src, path)
+                continue
+        sd = synthetic_layer_state_dict(cfg, name, seed, std, dtype, device)
+        save_file(sd, path)
 
 
 def load_full_state_dict(cfg: ModelConfig, model_path: str) -> Dict[str, torch.Tensor]:

@@ -2,9 +2,8 @@
 ``prepare_weights.py``), or write a synthetic random-init model directory.
 
     python prepare_weights.py <hf_dir> <new_file_dir>
-    python prepare_weights.py --synthetic llama2-7b <new_file_dir> [--seed 0]
-    add --packed to also write the packed-layer cache (<new_file_dir>/.fls_packed) used by
-    ``main.py --weight_cache packed``
+    python prepare_weights.py --synthetic llama2-7b <new_file_dir> [--seed 0] [--dtype bfloat16]
+                              [--unique_layers K]   (decoder layers >= K hard-link to layer i % K)
 """
 import argparse
 import sys
@@ -22,23 +21,20 @@ def main(argv=None):
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--std", type=float, default=0.02)
     ap.add_argument("--num_hidden_layers", type=int, default=None)
-    ap.add_argument("--packed", action="store_true", help="also build the packed-layer cache")
+    ap.add_argument("--dtype", choices=["float16", "bfloat16", "float32"], default="float16",
+                    help="--synthetic: checkpoint dtype")
+    ap.add_argument("--unique_layers", type=int, default=0,
+                    help="--synthetic: write K distinct decoder layers, hard-link the rest (disk-limited boxes)")
     a = ap.parse_args(argv)
     if a.synthetic:
+        import torch
         from flexible_llm_sharding_amd.config import preset
         from flexible_llm_sharding_amd.utils.synthetic import write_synthetic_checkpoint
         kw = {} if a.num_hidden_layers is None else {"num_hidden_layers": a.num_hidden_layers}
-        write_synthetic_checkpoint(preset(a.bin_dir, **kw), a.new_file_dir, seed=a.seed, std=a.std)
+        write_synthetic_checkpoint(preset(a.bin_dir, **kw), a.new_file_dir, seed=a.seed, std=a.std,
+                                   dtype=getattr(torch, a.dtype), unique_layers=a.unique_layers)
     else:
         split_into_layers(a.bin_dir, a.new_file_dir)
-    if a.packed:
-        import os
-        from flexible_llm_sharding_amd.config import ModelConfig
-        from flexible_llm_sharding_amd.runtime.packed import build_packed_cache
-        from flexible_llm_sharding_amd.runtime.weights import FileLayerSource
-        cfg = ModelConfig.from_pretrained(a.new_file_dir)
-        build_packed_cache(FileLayerSource(cfg, a.new_file_dir), os.path.join(a.new_file_dir, ".fls_packed"),
-                           verbose=True)
     return 0
 
 

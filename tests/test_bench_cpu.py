@@ -20,10 +20,10 @@ def _port():
     return p
 
 
-def _bench(world, extra, tmp_path):
+def _bench(world, extra, tmp_path, launcher=True):
     args = ["--gpus", str(world), "--steps", "2", "--warmup", "1", "--cpu", "--model", "tiny",
             "--prompts-per-gpu", "3", "--prefix-len", "24", "--suffix-len", "4"] + extra
-    if world > 1:
+    if world > 1 and launcher:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
                "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py")] + args
     else:
@@ -57,3 +57,23 @@ def test_bench_contract(tmp_path, world, mode, stages):
         assert out["config"]["parallelism"].startswith(want)
     # weak scaling: per-rank work fixed, global batch grows with the rank count
     assert out["config"]["global_batch"] == 3 * world
+
+
+def test_bench_spawns_its_own_ranks(tmp_path):
+    """`bench.py --gpus 3` with no torchrun environment starts the 3 rank processes itself
+    and rank 0 prints one JSON line for the whole job; the JSON names the process group size."""
+    out = _bench(3, [], tmp_path, launcher=False)
+    assert out["n_gpus"] == 3 and out["world"] == 3 and out["process_group_ranks"] == 3
+    assert len(out["rank_devices"]) == 3 and out["backend"] == "gloo"
+    assert out["config"]["parallelism"].startswith("dp3") and out["scores_finite"] is True
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_bench_stream_weights(tmp_path, world):
+    """--weights stream: per-layer files written once, re-read every pass (DP: each rank its 1/G
+    slice + all-gather); the JSON reports the host pinned / RSS footprint."""
+    out = _bench(world, ["--weights", "stream", "--unique-layers", "1", "--ckpt-dir", str(tmp_path / "ck")],
+                 tmp_path, launcher=False)
+    assert out["config"]["weights"] == "stream" and out["scores_finite"] is True
+    assert "host_pinned_gb" in out and "host_peak_rss_gb" in out
+    assert os.path.exists(tmp_path / "ck" / "model.layers.1.safetensors")

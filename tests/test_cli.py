@@ -72,7 +72,7 @@ def test_main_end_to_end(tiny_model, tmp_path, storage, lnps, nb):
 def test_generation_is_greedy_rerun(tiny_model, tmp_path):
     """Step t's scores equal a fresh scoring of the prompts extended by steps < t (main.py:85-90)."""
     from flexible_llm_sharding_amd.engine import ShardedRunner
-    from flexible_llm_sharding_amd.runtime.weights import FileLayerSource
+    from flexible_llm_sharding_amd.runtime.stream import FileLayerSource
     from flexible_llm_sharding_amd.utils.synthetic import synthetic_prompts
     from flexible_llm_sharding_amd.utils.tokenizer import load_tokenizer
     path, cfg = tiny_model
@@ -124,17 +124,37 @@ def test_main_synthetic_and_max_token_len(tmp_path):
 
 
 def test_main_weight_cache_modes_agree(tiny_model, tmp_path):
-    """host / disk / packed weight caches give identical scores (packed cache built on first use)."""
+    """host / stream / disk (alias) / auto weight caches give identical scores; auto with a host
+    budget below the model size streams."""
     from flexible_llm_sharding_amd.utils.synthetic import synthetic_prompts
     path, cfg = tiny_model
     pp = tmp_path / "prompts.pkl"
     pickle.dump(synthetic_prompts(3, 12, 2, 4, cfg.vocab_size, seed=3), open(pp, "wb"))
     outs = {}
-    for mode in ("host", "disk", "packed"):
+    for mode, extra in (("host", []), ("stream", []), ("disk", []), ("auto", ["--host_mem_gb", "0.0001"])):
         out = tmp_path / f"s_{mode}.pkl"
         _run(["--model_path", path, "--prompt_pickle", str(pp), "--output_file", str(out),
-              "--weight_cache", mode, "--packed_dir", str(tmp_path / "pk")], str(tmp_path))
+              "--weight_cache", mode] + extra, str(tmp_path))
         outs[mode] = pickle.load(open(out, "rb"))
-    for a, b, c in zip(outs["host"], outs["disk"], outs["packed"]):
-        assert np.array_equal(a, b) and np.array_equal(a, c)
-    assert len(os.listdir(tmp_path / "pk")) == len(cfg.layer_names())
+    for m in ("stream", "disk", "auto"):
+        for a, b in zip(outs["host"], outs[m]):
+            assert np.array_equal(a, b), m
+
+
+def test_weight_cache_resolution(tiny_model):
+    """auto -> host when the packed model fits the host budget, else stream; an explicit host that
+    cannot fit is refused up front; disk is the reference-named alias of stream."""
+    import types
+    from flexible_llm_sharding_amd.api import resolve_weight_cache
+    from flexible_llm_sharding_amd.parallel.comm import Comm
+    path, cfg = tiny_model
+    names = cfg.layer_names()
+    comm = Comm(0, 1)
+
+    def args(mode, gb):
+        return types.SimpleNamespace(weight_cache=mode, host_mem_gb=gb, synthetic=None)
+    assert resolve_weight_cache(args("auto", 100.0), cfg, comm, names, sliced=False) == "host"
+    assert resolve_weight_cache(args("auto", 1e-4), cfg, comm, names, sliced=False) == "stream"
+    assert resolve_weight_cache(args("disk", 100.0), cfg, comm, names, sliced=False) == "stream"
+    with pytest.raises(SystemExit):
+        resolve_weight_cache(args("host", 1e-4), cfg, comm, names, sliced=False)

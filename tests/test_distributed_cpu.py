@@ -31,7 +31,7 @@ def _worker(rank, world, port, path, prompts, lnps, dp, storage, out_dir, budget
     from flexible_llm_sharding_amd.config import ModelConfig
     from flexible_llm_sharding_amd.engine import ShardedRunner
     from flexible_llm_sharding_amd.parallel.comm import Comm
-    from flexible_llm_sharding_amd.runtime.weights import FileLayerSource
+    from flexible_llm_sharding_amd.runtime.stream import FileLayerSource
     from flexible_llm_sharding_amd.utils.tokenizer import load_tokenizer
     comm = Comm.from_env("cpu", timeout_s=120)
     cfg = ModelConfig.from_pretrained(path)
@@ -68,7 +68,7 @@ def _worker(rank, world, port, path, prompts, lnps, dp, storage, out_dir, budget
 @pytest.fixture(scope="module")
 def single(tiny_model):
     from flexible_llm_sharding_amd.engine import ShardedRunner
-    from flexible_llm_sharding_amd.runtime.weights import FileLayerSource
+    from flexible_llm_sharding_amd.runtime.stream import FileLayerSource
     from flexible_llm_sharding_amd.utils.synthetic import synthetic_prompts
     from flexible_llm_sharding_amd.utils.tokenizer import load_tokenizer
     path, cfg = tiny_model

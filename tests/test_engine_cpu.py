@@ -8,7 +8,8 @@ import torch
 from flexible_llm_sharding_amd.engine import ShardedRunner
 from flexible_llm_sharding_amd.models.reference import reference_scores
 from flexible_llm_sharding_amd.runtime.batch import pack_prompts, split_microbatches
-from flexible_llm_sharding_amd.runtime.weights import FileLayerSource, HostStore
+from flexible_llm_sharding_amd.runtime.stream import FileLayerSource
+from flexible_llm_sharding_amd.runtime.weights import HostStore
 from flexible_llm_sharding_amd.utils.synthetic import load_full_state_dict, synthetic_prompts
 from flexible_llm_sharding_amd.utils.tokenizer import load_tokenizer, tokenize_prompt
 

@@ -10,7 +10,8 @@ if not torch.cuda.is_available():
 
 from flexible_llm_sharding_amd.engine import ShardedRunner  # noqa: E402
 from flexible_llm_sharding_amd.models.reference import reference_scores  # noqa: E402
-from flexible_llm_sharding_amd.runtime.weights import FileLayerSource, HostStore  # noqa: E402
+from flexible_llm_sharding_amd.runtime.stream import FileLayerSource  # noqa: E402
+from flexible_llm_sharding_amd.runtime.weights import HostStore  # noqa: E402
 from flexible_llm_sharding_amd.utils.synthetic import load_full_state_dict, synthetic_prompts  # noqa: E402
 from flexible_llm_sharding_amd.utils.tokenizer import load_tokenizer  # noqa: E402
 from flexible_llm_sharding_amd import _native  # noqa: E402
@@ -28,7 +29,7 @@ def setup(tiny_model):
 
 @pytest.mark.parametrize("storage", ["gpu", "cpu", "disk"])
 @pytest.mark.parametrize("lnps", [1, 3])
-@pytest.mark.parametrize("cache", ["host", "disk"])
+@pytest.mark.parametrize("cache", ["host", "stream"])
 def test_engine_matches_oracle(setup, tmp_path, storage, lnps, cache):
     path, cfg, tok, prompts, ref = setup
     src = FileLayerSource(cfg, path)
@@ -45,6 +46,34 @@ def test_engine_matches_oracle(setup, tmp_path, storage, lnps, cache):
         assert err < 2e-3, err
         # same argmax on confidently-separated rows
         assert (np.argmax(o, -1) == np.argmax(rf, -1)).mean() > 0.8
+    r.close()
+
+
+@pytest.mark.parametrize("dtype", ["bfloat16", "float32"])
+@pytest.mark.parametrize("direct", [False, True])
+def test_stream_cast_checkpoints(tmp_path, dtype, direct):
+    """--weight_cache stream from bf16 / fp32 checkpoints: bf16 converted in place in HBM by the
+    cast kernel on the copy stream, fp32 on the host in the pinned chunk; O_DIRECT reads (or the
+    buffered fallback where the file system refuses them); tiny chunk ring so pieces split and
+    the ring wraps many times.  Scores == the host-cache path bitwise, and close to the oracle."""
+    from flexible_llm_sharding_amd.config import preset
+    from flexible_llm_sharding_amd.utils.synthetic import write_synthetic_checkpoint
+    cfg = preset("tiny-qwen2")
+    path = str(tmp_path / dtype)
+    write_synthetic_checkpoint(cfg, path, seed=8, std=0.05, dtype=getattr(torch, dtype))
+    tok = load_tokenizer(path)
+    prompts = synthetic_prompts(4, 70, 3, 12, cfg.vocab_size, seed=9, vary=True)
+    ref = reference_scores(cfg, load_full_state_dict(cfg, path), tok, prompts)
+    src = FileLayerSource(cfg, path, chunk_mb=1, n_chunks=2, direct=direct)
+    r = ShardedRunner(cfg, src, "cuda:0", tok, layer_num_per_shard=1)
+    got = r(prompts)
+    got2 = r(prompts)
+    host = ShardedRunner(cfg, HostStore.from_model_path(cfg, path), "cuda:0", tok, layer_num_per_shard=1)(prompts)
+    assert src.pinned_bytes() <= 2 * ((1 << 20) + 8192)
+    assert src.stats()["h2d_bytes"] > 0
+    for a, b, c, rf in zip(got, got2, host, ref):
+        assert np.array_equal(a, b) and np.array_equal(a, c)
+        assert np.abs(a.astype(np.float32) - rf).max() < 2e-3
     r.close()
 
 
@@ -173,10 +202,12 @@ def test_activation_store_no_race_large_batches(mid_model, tmp_path, storage):
     r.close()
 
 
-def test_dp_allgather_prefetcher_over_rccl(setup, tmp_path):
+@pytest.mark.parametrize("streaming", [False, True])
+def test_dp_allgather_prefetcher_over_rccl(setup, tmp_path, streaming):
     """The data-parallel weight path on real RCCL: a one-rank `nccl` process group, each layer
-    H2D'd as a byte slice and completed in HBM by `all_gather_into_tensor` on RCCL's stream
-    (async work handles, copy-stream -> RCCL-stream -> compute-stream ordering), vs the oracle."""
+    H2D'd (from pinned slices, or streamed from the layer file) as a byte slice and completed in
+    HBM by `all_gather_into_tensor` on its own communicator (copy-stream -> RCCL-stream -> copy-
+    stream -> compute-stream ordering), vs the oracle."""
     import socket
     import torch.distributed as dist
     from flexible_llm_sharding_amd.parallel.comm import Comm
@@ -191,7 +222,7 @@ def test_dp_allgather_prefetcher_over_rccl(setup, tmp_path):
     dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=dev)
     try:
         comm = Comm(0, 1, dev, "nccl")
-        src = SlicedHostStore.from_source(FileLayerSource(cfg, path), 0, 1)
+        src = FileLayerSource(cfg, path) if streaming else SlicedHostStore.from_source(FileLayerSource(cfg, path), 0, 1)
         names = cfg.layer_names()
         from flexible_llm_sharding_amd.parallel.planner import make_plan
         plan = make_plan(len(names), 2, 1, 0, True)

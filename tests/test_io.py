@@ -151,46 +151,76 @@ def test_split_tied_qwen2_checkpoint(tmp_path):
         assert torch.equal(back[k], v), k
 
 
-def test_packed_cache_source(tiny_model, tmp_path):
-    """--weight_cache packed: images equal the in-RAM packing, stale caches are rebuilt,
-    and a rank's byte slice can be read on its own."""
-    from flexible_llm_sharding_amd.runtime.packed import PackedFileSource, build_packed_cache, packed_path
-    from flexible_llm_sharding_amd.runtime.weights import FileLayerSource
-    path, cfg = tiny_model
-    src = FileLayerSource(cfg, path)
-    cache = str(tmp_path / "pk")
-    assert build_packed_cache(src, cache) == len(cfg.layer_names())
-    assert build_packed_cache(src, cache) == 0                      # up to date
-    pk = PackedFileSource(cfg, cache)
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16, torch.float32])
+def test_file_source_reads_checkpoint_bytes(tmp_path, dtype):
+    """The streaming source builds each packed image from file byte ranges only: equal to
+    pack_layer of the loaded state dict for fp16 / bf16 / fp32 checkpoints, and any byte range
+    [lo, hi) (a data-parallel rank's slice) reads only the file bytes it covers."""
+    from flexible_llm_sharding_amd.runtime.stream import FileLayerSource
+    from flexible_llm_sharding_amd.utils.synthetic import load_full_state_dict, write_synthetic_checkpoint
+    from flexible_llm_sharding_amd.models.layout import pack_layer
+    cfg = preset("tiny-qwen2")
+    d = str(tmp_path / "ck")
+    write_synthetic_checkpoint(cfg, d, seed=4, dtype=dtype)
+    sd = load_full_state_dict(cfg, d)
+    src = FileLayerSource(cfg, d)
     for n in cfg.layer_names():
-        a = torch.zeros(src.nbytes(n), dtype=torch.uint8)
-        b = torch.zeros(src.nbytes(n), dtype=torch.uint8)
-        src.read_into(n, a)
-        pk.read_into(n, b)
-        assert torch.equal(a, b), n
-        part = torch.zeros(100, dtype=torch.uint8)
-        pk.read_range_into(n, part, 300, 400)
-        assert torch.equal(part, a[300:400])
-    # a cache written for another config is stale -> refused, then rebuilt
-    other = preset("tiny", rms_norm_eps=1e-6)
-    with pytest.raises(FileNotFoundError):
-        PackedFileSource(other, cache)
-    with open(packed_path(cache, "lm_head"), "r+b") as f:
-        f.write(b"garbage!")
-    assert build_packed_cache(src, cache) == 1
+        nb = src.nbytes(n)
+        full = torch.zeros(nb, dtype=torch.uint8)
+        src.read_into(n, full)
+        assert torch.equal(full, pack_layer(cfg, n, sd)), n
+        for G in (2, 3):
+            c = (nb + G - 1) // G // 2 * 2 + 2
+            for r in range(G):
+                lo, hi = min(nb, r * c), min(nb, (r + 1) * c)
+                part = torch.zeros(max(1, hi - lo), dtype=torch.uint8)
+                before = src.read_bytes
+                src.read_range_into(n, part, lo, hi)
+                assert torch.equal(part[:hi - lo], full[lo:hi]), (n, G, r)
+                # file bytes read == the tensor bytes this range covers (x 2 for fp32), not the file
+                want = sum(max(0, min(hi, r.img_off + 2 * r.numel) - max(lo, r.img_off)) * r.src_es // 2
+                           for r in src.plan(n).runs)
+                assert src.read_bytes - before == want
 
 
-def test_dp_slices_from_packed_cache(tiny_model, tmp_path):
+def test_f32_to_f16_rounding_matches_torch():
+    """The streamer's host fp32 -> fp16 conversion == torch .to(float16) (RNE, subnormals, inf, nan)."""
+    import ctypes
+    import numpy as np
+    from flexible_llm_sharding_amd import _native
+    rt = _native.runtime_or_none()
+    if rt is None:
+        pytest.skip("native runtime not built")
+    vals = torch.cat([torch.randn(10000) * 3, torch.randn(1000) * 1e-5, torch.randn(1000) * 1e-8,
+                      torch.tensor([65504., 65519.9, 65520., 1e6, -1e6, 0., -0., 2 ** -24, 2 ** -25, 3 * 2 ** -26,
+                                    float("inf"), float("-inf"), 5.960464477539063e-08, 6.103515625e-05,
+                                    6.097555160522461e-05, 1.0009765625, 1.00048828125, 1.00146484375])])
+    src = vals.float().contiguous()
+    out = torch.empty(src.numel(), dtype=torch.int16)
+    rt.fls_f32_to_f16(src.data_ptr(), out.data_ptr(), src.numel())
+    assert torch.equal(out.view(torch.float16), src.to(torch.float16))
+    nan = torch.tensor([float("nan")])
+    rt.fls_f32_to_f16(nan.data_ptr(), out.data_ptr(), 1)
+    assert torch.isnan(out[:1].view(torch.float16)).all()
+
+
+def test_dp_slices_read_only_their_range(tiny_model):
+    """SlicedHostStore.from_source: rank r's slices == bytes [r*c, (r+1)*c) of the full images,
+    and the G ranks together read each layer file's tensor bytes exactly once."""
     from flexible_llm_sharding_amd.parallel.data_parallel import SlicedHostStore
-    from flexible_llm_sharding_amd.runtime.packed import PackedFileSource, build_packed_cache
-    from flexible_llm_sharding_amd.runtime.weights import FileLayerSource
+    from flexible_llm_sharding_amd.runtime.stream import FileLayerSource
     path, cfg = tiny_model
-    src = FileLayerSource(cfg, path)
-    build_packed_cache(src, str(tmp_path / "pk"))
-    for rank in range(3):
-        a = SlicedHostStore.from_source(src, rank, 3, pinned=False)
-        b = SlicedHostStore.from_source(PackedFileSource(cfg, str(tmp_path / "pk")), rank, 3, pinned=False)
+    full_src = FileLayerSource(cfg, path)
+    G = 3
+    total = 0
+    for rank in range(G):
+        src = FileLayerSource(cfg, path)
+        st = SlicedHostStore.from_source(src, rank, G, pinned=False)
+        total += src.read_bytes
         for n in cfg.layer_names():
-            nb, c = a.nbytes(n), a.chunk_bytes(n)
+            nb, c = st.nbytes(n), st.chunk_bytes(n)
+            full = torch.zeros(nb, dtype=torch.uint8)
+            full_src.read_into(n, full)
             valid = max(0, min(nb, (rank + 1) * c) - rank * c)
-            assert torch.equal(a.buffers[n][:valid], b.buffers[n][:valid]), (rank, n)
+            assert torch.equal(st.buffers[n][:valid], full[rank * c:rank * c + valid]), (rank, n)
+    assert total == sum(full_src.plan(n).file_bytes for n in cfg.layer_names())

@@ -5,8 +5,6 @@ import numpy as np
 import pytest
 import torch
 
-from flexible_llm_sharding_amd.models.layout import PAIR_BLOCK
-
 pytestmark = pytest.mark.gpu
 
 if not torch.cuda.is_available():
@@ -22,7 +20,6 @@ DEV = torch.device("cuda", 0)
 @pytest.fixture(scope="module")
 def ops():
     o = HipOps()
-    o.backend = "hip"          # exercise the hand-written fused kernels (hipBLASLt path: test_gemm_backends_agree)
     assert _native.loaded_libraries().get("k"), "libfls_kernels.so not loaded"
     return o
 
@@ -238,42 +235,6 @@ def test_fill_random(ops):
     assert abs(f.mean().item()) < 0.01 and abs(f.std().item() - 1) < 0.01
 
 
-@pytest.mark.parametrize("M", [300, 2048])
-def test_gemm_backends_agree(M):
-    """Fused-epilogue MFMA kernels vs hipBLASLt + stand-alone epilogue kernels."""
-    from flexible_llm_sharding_amd.config import ModelConfig
-    from flexible_llm_sharding_amd.models.llama import rope_tables
-    a, b = HipOps(), HipOps()
-    a.backend, b.backend = "hip", "hipblaslt"
-    H, I, nh, nkv, hd = 512, 768, 4, 2, 128
-    x = rnd(M, H, seed=21)
-    wqkv = rnd((nh + 2 * nkv) * hd, H, scale=0.05, seed=22)
-    wgu = rnd(2 * I, H, scale=0.05, seed=23)
-    wd = rnd(H, I, scale=0.05, seed=24)
-    pos = torch.randint(0, 4000, (M,), dtype=torch.int32, device=DEV)
-    cfg = ModelConfig(hidden_size=nh * hd, num_attention_heads=nh, num_key_value_heads=nkv)
-    cos, sin = (t.to(DEV) for t in rope_tables(cfg, 4096))
-    q1 = a.qkv_rope(x, wqkv, pos, cos, sin, nh, nkv, hd)
-    q2 = b.qkv_rope(x, wqkv, pos, cos, sin, nh, nkv, hd)
-    s1, s2 = a.swiglu_up(x, wgu), b.swiglu_up(x, wgu)
-    r0 = rnd(M, H, seed=25)
-    r1 = a.linear_residual(s1, wd, r0.clone())
-    r2 = b.linear_residual(s1, wd, r0.clone())
-    torch.cuda.synchronize()
-    assert rel_err(q1, q2) < 2e-3 and rel_err(s1, s2) < 3e-3 and rel_err(r1, r2) < 2e-3
-
-
-def test_gemm_autotune_choice():
-    o = HipOps()
-    o.backend = "auto"
-    x = rnd(1024, 1024, seed=26)
-    w = rnd(2048, 1024, scale=0.05, seed=27)
-    y = o.linear(x, w)
-    torch.cuda.synchronize()
-    assert len(o.choice) == 1 and list(o.timings.values())[0]["choice"] in ("hip", "hipblaslt")
-    assert rel_err(y, x.float() @ w.float().t()) < 2e-3
-
-
 @pytest.mark.parametrize("M", [1, 17, 64, 100, 416, 517, 1000])
 def test_gemm_mid_all_epilogues(ops, ref, M):
     """64x128-tile mid-M kernel (chosen when 256x256 tiles cannot fill the chip) vs fp32 references."""
@@ -312,10 +273,10 @@ def test_gemm_mid_asymmetric_exact(ops):
     assert torch.equal(y, w.t().contiguous()[:M])
 
 
-@pytest.mark.parametrize("var", [1, 3, 6, 7, 8, 9, 10, 11, 12, 13])
+@pytest.mark.parametrize("var", [10, 13])
 def test_gemm_variants_all_epilogues(ops, ref, var):
-    """Every main-loop variant (v1 8-wave, v3 ping-pong, v6 one-wave-per-SIMD, v7 counted-vmcnt phases)
-    against fp32 references, with all four epilogues and a ragged M."""
+    """The main kernel (v10) and its persistent form (v13) against fp32 references, with all four
+    epilogues and a ragged M."""
     from flexible_llm_sharding_amd.config import ModelConfig
     from flexible_llm_sharding_amd.models.llama import rope_tables
     M, H, I, nh, nkv, hd = 517, 512, 768, 4, 2, 128
@@ -423,7 +384,7 @@ def test_gemv_skinny(ops, M, N, K):
     assert ops.linear(x, w).shape == (M, N)          # linear() routes M <= 16 here
 
 
-@pytest.mark.parametrize("var", [3, 10, 12, 13])
+@pytest.mark.parametrize("var", [10, 13])
 def test_gemm_bias_epilogues(ops, ref, var):
     """Per-column bias ahead of RoPE (Qwen2 q/k/v) and ahead of the residual add (o_proj)."""
     from flexible_llm_sharding_amd.config import ModelConfig

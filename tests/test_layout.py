@@ -1,22 +1,14 @@
-"""Packed HBM layout: pack/unpack round trip, RoPE pair permutation, gate/up interleave."""
+"""Packed HBM layout: placements, pack/unpack round trip, natural-order RoPE / SwiGLU oracle."""
+import pytest
 import torch
+import torch.nn.functional as F
 
 from flexible_llm_sharding_amd.config import preset
-from flexible_llm_sharding_amd.models.layout import (deinterleave_gate_up, interleave_gate_up, layer_layout,
-                                                     pack_layer, permute_head_cols, rope_row_perm,
-                                                     unpack_layer, unpermute_head_cols)
+from flexible_llm_sharding_amd.models.layout import layer_layout, pack_layer, placements, unpack_layer
 from flexible_llm_sharding_amd.models.llama import rope_tables
 from flexible_llm_sharding_amd.models.reference import _rope
 from flexible_llm_sharding_amd.ops.torch_backend import TorchOps
 from flexible_llm_sharding_amd.utils.synthetic import synthetic_layer_state_dict
-
-
-def test_rope_perm_is_permutation():
-    for hd in (64, 128):
-        p = rope_row_perm(hd)
-        assert sorted(p) == list(range(hd))
-        # blocks of 16 alternate first half / second half
-        assert p[:16] == list(range(16)) and p[16:32] == list(range(hd // 2, hd // 2 + 16))
 
 
 def test_pack_roundtrip():
@@ -32,6 +24,25 @@ def test_pack_roundtrip():
             assert torch.equal(back[k], sd[k]), k
 
 
+@pytest.mark.parametrize("model", ["tiny", "tiny-qwen2", "llama2-70b"])
+def test_placements_tile_the_slots(model):
+    """Every checkpoint tensor lands inside its slot, tensors never overlap, and the stacked
+    slots (wqkv = q|k|v, wgu = gate|up) are exactly filled — no permutation, no gaps."""
+    cfg = preset(model)
+    name = "model.layers.0"
+    lay = layer_layout(cfg, "decoder")
+    pls = sorted(placements(cfg, name), key=lambda p: p.offset)
+    for a, b in zip(pls, pls[1:]):
+        assert a.offset + a.nbytes <= b.offset
+    for slot, parts in (("wqkv", ("q_proj.weight", "k_proj.weight", "v_proj.weight")),
+                        ("wgu", ("gate_proj.weight", "up_proj.weight"))):
+        s = lay.slot(slot)
+        ps = [p for p in pls if any(p.hf_name.endswith(x) for x in parts)]
+        assert ps[0].offset == s.offset
+        assert sum(p.nbytes for p in ps) == 2 * s.numel
+    assert all(s.offset % 256 == 0 for s in lay.slots)
+
+
 def test_layout_alignment():
     cfg = preset("llama2-70b")
     lay = layer_layout(cfg, "decoder")
@@ -39,16 +50,8 @@ def test_layout_alignment():
     assert abs(lay.nbytes - 1.711e9) / 1.711e9 < 0.01
 
 
-def test_interleave_roundtrip():
-    g, u = torch.randn(64, 8), torch.randn(64, 8)
-    w = interleave_gate_up(g, u)
-    assert torch.equal(w[16:32], u[:16])
-    g2, u2 = deinterleave_gate_up(w)
-    assert torch.equal(g, g2) and torch.equal(u, u2)
-
-
-def test_rope_on_permuted_layout_equals_hf_rope():
-    """qkv_rope on packed (permuted) weights == HF rotate-half RoPE on HF-layout q/k, permuted."""
+def test_qkv_rope_oracle_equals_hf_rope():
+    """qkv_rope on the packed [q; k; v] weight == HF rotate-half RoPE on HF q/k, v untouched."""
     cfg = preset("tiny")
     nh, nkv, hd = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
     name = "model.layers.0"
@@ -65,19 +68,25 @@ def test_rope_on_permuted_layout_equals_hf_rope():
     qh = _rope(q.view(1, T, nh, hd).transpose(1, 2), pos.long()[None], cos, sin).transpose(1, 2).reshape(T, -1)
     kh = _rope(k.view(1, T, nkv, hd).transpose(1, 2), pos.long()[None], cos, sin).transpose(1, 2).reshape(T, -1)
     qs, ks = nh * hd, nkv * hd
-    assert torch.allclose(unpermute_head_cols(y[:, :qs], nh, hd), qh, atol=1e-4)
-    assert torch.allclose(unpermute_head_cols(y[:, qs:qs + ks], nkv, hd), kh, atol=1e-4)
-    assert torch.allclose(permute_head_cols(qh, nh, hd), y[:, :qs], atol=1e-4)
+    assert torch.allclose(y[:, :qs], qh, atol=1e-4)
+    assert torch.allclose(y[:, qs:qs + ks], kh, atol=1e-4)
     v = x @ sd[f"{name}.self_attn.v_proj.weight"].t()
     assert torch.allclose(y[:, qs + ks:], v, atol=1e-4)
+
+
+def test_swiglu_oracle_on_stacked_gate_up():
+    cfg = preset("tiny")
+    name = "model.layers.1"
+    sd = synthetic_layer_state_dict(cfg, name, seed=6, dtype=torch.float32)
+    W = layer_layout(cfg, "decoder", 4).views(pack_layer(cfg, name, sd, dtype=torch.float32), torch.float32)
+    x = torch.randn(7, cfg.hidden_size)
+    y = TorchOps().swiglu_up(x, W["wgu"])
+    ref = F.silu(x @ sd[f"{name}.mlp.gate_proj.weight"].t()) * (x @ sd[f"{name}.mlp.up_proj.weight"].t())
+    assert torch.allclose(y, ref, atol=1e-5)
 
 
 def test_int8_rejected():
     cfg = preset("tiny")
     sd = {"model.norm.weight": torch.ones(cfg.hidden_size, dtype=torch.int8)}
-    try:
+    with pytest.raises(AssertionError, match="int8"):
         pack_layer(cfg, "model.norm", sd)
-    except AssertionError as e:
-        assert "int8" in str(e)
-    else:
-        raise AssertionError("int8 accepted")
