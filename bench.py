@@ -112,7 +112,9 @@ def ensure_checkpoint(cfg, d: str, dtype: str, unique: int, rank: int, comm, pro
     """Write the synthetic per-layer checkpoint once (rank 0; a marker file makes it reusable)."""
     import torch
     from flexible_llm_sharding_amd.utils.synthetic import write_synthetic_checkpoint
-    marker = os.path.join(d, ".fls_bench_complete")
+    import hashlib
+    tag = hashlib.sha1(json.dumps([cfg.to_dict(), dtype, unique], sort_keys=True, default=str).encode()).hexdigest()[:12]
+    marker = os.path.join(d, f".fls_bench_complete_{tag}")
     if rank == 0 and not os.path.exists(marker):
         dev = "cpu" if not torch.cuda.is_available() else torch.device("cuda", torch.cuda.current_device())
         write_synthetic_checkpoint(cfg, d, seed=0, dtype=getattr(torch, dtype), unique_layers=unique,
@@ -126,6 +128,11 @@ def main(argv=None):
     a = parse(argv)
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return spawn_ranks(a, argv)
+    if a.max_vram_gb and not a.cpu:
+        # a VRAM cap: let the caching allocator grow segments in place instead of keeping one
+        # rounded block per size class and stream (set before the first HIP allocation)
+        for k in ("PYTORCH_HIP_ALLOC_CONF", "PYTORCH_CUDA_ALLOC_CONF"):
+            os.environ.setdefault(k, "expandable_segments:True")
 
     import resource
 
@@ -183,6 +190,8 @@ def main(argv=None):
         log(rank, f"[bench] host store {store.total_bytes / 1e9:.1f} GB in {time.perf_counter() - t0:.1f}s")
         data_w = f"random-init {a.model} weights in {'HBM (resident)' if a.resident else 'pinned host RAM'}"
 
+    if not a.cpu:
+        torch.cuda.empty_cache()     # set-up only: the weight generator's staging blocks are not part of a pass
     tok_dir = f"/tmp/fls_bench_tok_{os.getpid()}"
     write_synthetic_tokenizer(tok_dir, cfg.vocab_size)
     tok = load_tokenizer(tok_dir)
@@ -241,8 +250,10 @@ def main(argv=None):
     if dp:
         tok_step = comm.all_reduce_sum(tok_step)
         padded_step = comm.all_reduce_sum(padded_step)
-    peak = comm.all_reduce_max(0.0 if a.cpu else float(torch.cuda.max_memory_allocated(dev)))
-    peak_res = comm.all_reduce_max(0.0 if a.cpu else float(torch.cuda.max_memory_reserved(dev)))
+    # weight slots are exact-size hipMalloc blocks outside the caching allocator: add them back
+    slots = 0.0 if a.cpu else float(runner.prefetcher.hbm_bytes())
+    peak = comm.all_reduce_max(0.0 if a.cpu else float(torch.cuda.max_memory_allocated(dev)) + slots)
+    peak_res = comm.all_reduce_max(0.0 if a.cpu else float(torch.cuda.max_memory_reserved(dev)) + slots)
     dev_used_peak = comm.all_reduce_max(dev_used_peak)
     pinned = hostmem.pinned_peak + (store.pinned_bytes() if a.weights == "stream" else 0)
     pinned = comm.all_reduce_max(float(pinned))

@@ -35,6 +35,8 @@ int   fls_st_info(void* h, int i, char* name, int name_cap, char* dtype, int dty
 uint64_t fls_st_data_offset(void* h);
 void  fls_st_close(void* h);
 int   fls_mem_info(uint64_t* free_b, uint64_t* total_b);
+void* fls_device_alloc(int device, uint64_t bytes);        // hipMalloc (outside the torch allocator)
+int   fls_device_free(int device, void* p);
 
 // weight streamer: file byte ranges -> pinned chunk ring -> HBM (runtime/stream.py)
 typedef struct {

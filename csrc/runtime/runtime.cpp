@@ -70,6 +70,23 @@ extern "C" int fls_memcpy_async(void* dst, const void* src, uint64_t bytes, int 
   return hipMemcpyAsync(dst, src, bytes, k, (hipStream_t)s) == hipSuccess ? 0 : -1;
 }
 
+// exact-size device allocations outside PyTorch's caching allocator (weight slots: allocated
+// once per run, never split or cached per stream)
+extern "C" void* fls_device_alloc(int device, uint64_t bytes) {
+  void* p = nullptr;
+  if (hipSetDevice(device) != hipSuccess || hipMalloc(&p, bytes ? bytes : 1) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return p;
+}
+
+extern "C" int fls_device_free(int device, void* p) {
+  if (!p) return 0;
+  (void)hipSetDevice(device);
+  return hipFree(p) == hipSuccess ? 0 : -1;
+}
+
 extern "C" int fls_mem_info(uint64_t* free_b, uint64_t* total_b) {
   size_t f = 0, t = 0;
   if (hipMemGetInfo(&f, &t) != hipSuccess) return -1;

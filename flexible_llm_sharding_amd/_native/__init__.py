@@ -45,6 +45,8 @@ def _load_runtime():
     _bind(lib, "fls_st_data_offset", c_uint64, c_void_p)
     _bind(lib, "fls_st_close", None, c_void_p)
     _bind(lib, "fls_mem_info", c_int, c_void_p, c_void_p)
+    _bind(lib, "fls_device_alloc", c_void_p, c_int, c_uint64)
+    _bind(lib, "fls_device_free", c_int, c_int, c_void_p)
     _bind(lib, "fls_streamer_create", c_void_p, c_int, c_uint64, c_int, c_int, c_int)
     _bind(lib, "fls_streamer_pinned_bytes", c_uint64, c_void_p)
     _bind(lib, "fls_streamer_load", c_int64, c_void_p, c_char_p, c_void_p, c_int, c_void_p, c_void_p)

@@ -120,6 +120,11 @@ class ShardedRunner:
         self.my_shards = my
         self.prefetcher = prefetcher or ShardPrefetcher(source, self.names, my, self.dev,
                                                         n_slots=n_slots, resident=resident)
+        if self.vram_plan is not None and self.cuda:
+            # the weight slots are raw hipMalloc blocks: the allocator gets the rest of the cap
+            from .runtime.memplan import cap_allocator
+            slots = self.prefetcher.planned_hbm_bytes()
+            self.vram_plan["allocator_limit_bytes"] = cap_allocator(self.dev, int(max_vram_gb * 1e9), slots)
         self.stats: Dict[str, float] = {}
         if self.plan.mode == "mp" and self.comm.active:
             edges = []
@@ -136,6 +141,9 @@ class ShardedRunner:
         self.hip_graphs = bool(hip_graphs and self.cuda and resident and self.plan.mode != "mp"
                                and not resume_dir)
         self._graphs = None
+        if self.cuda and not self.hip_graphs:
+            from .models.llama import Workspace
+            self.ctx.ws = Workspace(self.dev, self.act_dtype)   # fixed scratch buffers (VRAM plan)
         # prefix K/V reuse across calls (generation steps): runtime/prefix_cache.py
         self.prefix_cache = None
         if prefix_kv_cache and not self.hip_graphs and not resume_dir:

@@ -97,6 +97,47 @@ def rope_tables(cfg: ModelConfig, max_pos: int = MAX_TOKEN_LEN, table_dtype=torc
     return cos.contiguous().to(device), sin.contiguous().to(device)
 
 
+class Workspace:
+    """One scratch arena reused by every decoder layer: the attention phase carves
+    [normed input | QKV | attention output] out of it, the MLP phase (where those are dead)
+    [normed chunk | SwiGLU chunk].  It is sized once, at the largest micro-batch seen, so the
+    caching allocator sees one fixed block instead of four fresh, differently sized
+    allocations per layer and micro-batch, and the two phases share the same bytes
+    (profiles/r2_vram).  Every user runs on the compute stream, so carving the same bytes in
+    the next phase / layer is ordered after their last reader."""
+
+    def __init__(self, device, dtype):
+        self.device, self.dtype = device, dtype
+        self.buf: Optional[torch.Tensor] = None
+        self.pos = 0
+
+    def reset(self) -> None:
+        self.pos = 0
+
+    def take(self, rows: int, cols: int) -> torch.Tensor:
+        n = rows * cols
+        n_al = (n + 127) // 128 * 128            # 256-byte aligned views
+        if self.buf is None or self.pos + n_al > self.buf.numel():
+            if self.pos:
+                raise RuntimeError("workspace phase outgrew its arena; reserve() the phase first")
+            self.buf = None
+            self.buf = torch.empty(n_al, dtype=self.dtype, device=self.device)
+        v = self.buf[self.pos:self.pos + n].view(rows, cols)
+        self.pos += n_al
+        return v
+
+    def reserve(self, *shapes) -> None:
+        """Grow the arena (between phases) to hold ``shapes`` = [(rows, cols), ...] at once."""
+        need = sum((r * c + 127) // 128 * 128 for r, c in shapes)
+        if self.buf is None or self.buf.numel() < need:
+            self.buf = None
+            self.buf = torch.empty(need, dtype=self.dtype, device=self.device)
+        self.pos = 0
+
+    def nbytes(self) -> int:
+        return 0 if self.buf is None else self.buf.numel() * self.buf.element_size()
+
+
 @dataclass
 class ExecContext:
     cfg: ModelConfig
@@ -111,6 +152,15 @@ class ExecContext:
     # nothing downstream reads the other rows (final norm gathers the scored rows, utils.py:284-286)
     prune_last: bool = True
     last_decoder: str = ""
+    ws: Optional[Workspace] = None          # scratch arena (None: fresh allocations, e.g. graph capture)
+
+    def phase(self, *shapes) -> None:
+        """Start a workspace phase that will carve ``shapes`` (rows, cols) in order."""
+        if self.ws is not None:
+            self.ws.reserve(*shapes)
+
+    def scratch(self, rows: int, cols: int) -> Optional[torch.Tensor]:
+        return self.ws.take(rows, cols) if self.ws is not None else None
 
 
 def run_embed(ctx: ExecContext, W: Dict[str, torch.Tensor], meta: dict) -> torch.Tensor:
@@ -126,9 +176,12 @@ def run_decoder(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, b
     cfg, ops = ctx.cfg, ctx.ops
     prune = ctx.prune_last and layer_name == ctx.last_decoder
     eps = cfg.rms_norm_eps
-    h = ops.rmsnorm(x, W["ln1"], eps)
+    T0 = x.shape[0]
+    ctx.phase((T0, cfg.hidden_size), (T0, cfg.qkv_size), (T0, cfg.q_size))
+    h = ops.rmsnorm(x, W["ln1"], eps, out=ctx.scratch(T0, cfg.hidden_size))
     qkv = ops.qkv_rope(h, W["wqkv"], meta["positions"], ctx.cos, ctx.sin,
-                       cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim, bias=W.get("bqkv"))
+                       cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim, bias=W.get("bqkv"),
+                       out=ctx.scratch(T0, cfg.qkv_size))
     del h
     kv0 = None
     pe = ctx.prefix_entry
@@ -145,7 +198,7 @@ def run_decoder(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, b
     else:
         attn_arg = meta["work"] if work_items else batch.segments
     a = ops.attention(qkv, attn_arg, cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim, kv0=kv0,
-                      q_block=batch.q_block)
+                      q_block=batch.q_block, out=ctx.scratch(T0, cfg.q_size))
     del qkv
     if prune:
         idx = meta["last_idx"]
@@ -155,16 +208,20 @@ def run_decoder(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, b
     del a
     T = x.shape[0]
     step = max(1, ctx.mlp_chunk)
+    I, H = cfg.intermediate_size, cfg.hidden_size
     if T <= step:
-        h = ops.rmsnorm(x, W["ln2"], eps)
-        m = ops.swiglu_up(h, W["wgu"])
+        ctx.phase((T, H), (T, I))               # the attention-phase bytes are dead: reuse them
+        h = ops.rmsnorm(x, W["ln2"], eps, out=ctx.scratch(T, H))
+        m = ops.swiglu_up(h, W["wgu"], out=ctx.scratch(T, I))
         del h
         x = ops.linear_residual(m, W["wdown"], x)
     else:
         for s in range(0, T, step):
             xs = x[s:s + step]
-            h = ops.rmsnorm(xs, W["ln2"], eps)
-            m = ops.swiglu_up(h, W["wgu"])
+            n = xs.shape[0]
+            ctx.phase((n, H), (n, I))
+            h = ops.rmsnorm(xs, W["ln2"], eps, out=ctx.scratch(n, H))
+            m = ops.swiglu_up(h, W["wgu"], out=ctx.scratch(n, I))
             del h
             x[s:s + step] = ops.linear_residual(m, W["wdown"], xs)
     return x

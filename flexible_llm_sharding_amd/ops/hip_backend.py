@@ -92,19 +92,19 @@ class HipOps:
         _f16(resid, "resid")
         return self.gemm(x, w, EPI_RESID, out=resid, resid=resid, bias=bias)
 
-    def swiglu_up(self, x, wgu):
+    def swiglu_up(self, x, wgu, out=None):
         """silu(x @ gate^T) * (x @ up^T) with wgu = [gate; up]."""
-        return self.gemm(x, wgu, EPI_SWIGLU)
+        return self.gemm(x, wgu, EPI_SWIGLU, out=out)
 
-    def qkv_rope(self, x, wqkv, positions, cos, sin, n_q_heads, n_kv_heads, head_dim, bias=None):
+    def qkv_rope(self, x, wqkv, positions, cos, sin, n_q_heads, n_kv_heads, head_dim, bias=None, out=None):
         if positions.dtype != torch.int32:
             raise TypeError("positions must be int32")
         rope_cols = (n_q_heads + n_kv_heads) * head_dim
-        return self.gemm(x, wqkv, EPI_ROPE, positions=positions, cos=cos, sin=sin,
+        return self.gemm(x, wqkv, EPI_ROPE, out=out, positions=positions, cos=cos, sin=sin,
                          rope_cols=rope_cols, head_dim=head_dim, bias=bias)
 
     # ----------------------------------------------------------- attention
-    def attention(self, qkv, work, n_q_heads, n_kv_heads, head_dim, kv0=None, q_block: int = 64):
+    def attention(self, qkv, work, n_q_heads, n_kv_heads, head_dim, kv0=None, q_block: int = 64, out=None):
         """kv0 ([P, 2 * n_kv * hd], K then V): range 0 of every work item reads these rows (prefix cache)."""
         _f16(qkv, "qkv")
         if work.dtype != torch.int32 or not work.is_cuda:
@@ -114,7 +114,8 @@ class HipOps:
             if kv0.shape[1] != 2 * n_kv_heads * head_dim:
                 raise ValueError(f"kv0 must be [P, {2 * n_kv_heads * head_dim}], got {tuple(kv0.shape)}")
         T = qkv.shape[0]
-        out = torch.empty(T, n_q_heads * head_dim, dtype=torch.float16, device=qkv.device)
+        if out is None:
+            out = torch.empty(T, n_q_heads * head_dim, dtype=torch.float16, device=qkv.device)
         rc = self.k.fls_attention(qkv.data_ptr(), out.data_ptr(), work.data_ptr(), work.shape[0],
                                   n_q_heads, n_kv_heads, head_dim, qkv.stride(0), out.stride(0),
                                   head_dim ** -0.5, kv0.data_ptr() if kv0 is not None else None,
@@ -123,12 +124,12 @@ class HipOps:
         return out
 
     # ------------------------------------------------------- elementwise
-    def rmsnorm(self, x, w, eps, row_idx=None):
+    def rmsnorm(self, x, w, eps, row_idx=None, out=None):
         _f16(x, "x")
         _f16(w, "w")
         rows = row_idx.shape[0] if row_idx is not None else x.shape[0]
         H = x.shape[1]
-        y = torch.empty(rows, H, dtype=torch.float16, device=x.device)
+        y = out if out is not None else torch.empty(rows, H, dtype=torch.float16, device=x.device)
         rc = self.k.fls_rmsnorm(x.data_ptr(), w.data_ptr(), y.data_ptr(),
                                 row_idx.data_ptr() if row_idx is not None else None,
                                 rows, H, x.stride(0), y.stride(0), float(eps), _stream())

@@ -27,7 +27,7 @@ class TorchOps:
     def embed(self, ids: torch.Tensor, table: torch.Tensor, out_dtype) -> torch.Tensor:
         return table.index_select(0, ids.long()).to(out_dtype)
 
-    def rmsnorm(self, x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
+    def rmsnorm(self, x: torch.Tensor, w: torch.Tensor, eps: float, out=None) -> torch.Tensor:
         # LlamaRMSNorm: fp32 variance, normalise, cast back, scale by weight.
         xf = x.float()
         var = xf.pow(2).mean(-1, keepdim=True)
@@ -44,14 +44,14 @@ class TorchOps:
             y = y + self._c(bias)
         return (self._c(resid) + y).to(resid.dtype)
 
-    def swiglu_up(self, x: torch.Tensor, wgu: torch.Tensor) -> torch.Tensor:
+    def swiglu_up(self, x: torch.Tensor, wgu: torch.Tensor, out=None) -> torch.Tensor:
         y = self._c(x) @ self._c(wgu).t()                     # [T, 2I] = [gate | up]
         I = y.shape[1] // 2
         return (F.silu(y[:, :I]) * y[:, I:]).to(x.dtype)
 
     def qkv_rope(self, x: torch.Tensor, wqkv: torch.Tensor, positions: torch.Tensor,
                  cos: torch.Tensor, sin: torch.Tensor, n_q_heads: int, n_kv_heads: int,
-                 head_dim: int, bias: torch.Tensor = None) -> torch.Tensor:
+                 head_dim: int, bias: torch.Tensor = None, out=None) -> torch.Tensor:
         y = self._c(x) @ self._c(wqkv).t()
         if bias is not None:
             y = y + self._c(bias)
@@ -68,7 +68,7 @@ class TorchOps:
         return torch.cat([qk_out, y[:, qk_cols:]], dim=1).to(x.dtype)
 
     def attention(self, qkv: torch.Tensor, segments, n_q_heads: int, n_kv_heads: int,
-                  head_dim: int, kv0: torch.Tensor = None, q_block: int = 64) -> torch.Tensor:
+                  head_dim: int, kv0: torch.Tensor = None, q_block: int = 64, out=None) -> torch.Tensor:
         """Shared-prefix attention over packed segments (see runtime.batch).
 
         ``kv0`` ([P, 2 * n_kv * hd], K then V): range 0 of every segment indexes

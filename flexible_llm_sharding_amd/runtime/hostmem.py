@@ -77,6 +77,40 @@ def alloc_host(nbytes: int, pinned: bool = True) -> torch.Tensor:
     return torch.empty(nbytes, dtype=torch.uint8)
 
 
+class _DeviceBlock:
+    """A raw hipMalloc block exposed to torch through ``__cuda_array_interface__`` (zero copy;
+    the tensor keeps this object alive, ``hipFree`` when the last view dies)."""
+
+    def __init__(self, ptr: int, nbytes: int, device: int, lib):
+        self.ptr, self.nbytes, self.device, self.lib = ptr, nbytes, device, lib
+        self.__cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (ptr, False),
+                                         "version": 3, "strides": None}
+
+    def __del__(self):
+        try:
+            if self.ptr:
+                self.lib.fls_device_free(self.device, self.ptr)
+                self.ptr = None
+        except Exception:
+            pass
+
+
+def alloc_device(nbytes: int, device: torch.device) -> torch.Tensor:
+    """uint8 device tensor of exactly ``nbytes`` allocated outside PyTorch's caching allocator
+    (weight slots: one allocation per run, so they never fragment the per-stream pools the
+    activations use).  Falls back to ``torch.empty`` if the native runtime is unavailable."""
+    dev = torch.device(device)
+    rt = _native.runtime_or_none()
+    if rt is not None and dev.type == "cuda":
+        idx = dev.index if dev.index is not None else torch.cuda.current_device()
+        ptr = rt.fls_device_alloc(idx, max(1, nbytes))
+        if not ptr:
+            raise torch.cuda.OutOfMemoryError(f"hipMalloc of {nbytes / 1e9:.2f} GB failed on {dev}")
+        t = torch.as_tensor(_DeviceBlock(ptr, max(1, nbytes), idx, rt), device=dev)
+        return t[:nbytes]
+    return torch.empty(nbytes, dtype=torch.uint8, device=dev)
+
+
 def pread_into(path: str, offset: int, nbytes: int, dst: torch.Tensor) -> None:
     """Read ``nbytes`` at ``offset`` of ``path`` into a contiguous CPU tensor."""
     assert dst.device.type == "cpu" and dst.is_contiguous()

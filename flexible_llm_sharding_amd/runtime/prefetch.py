@@ -79,8 +79,16 @@ class ShardPrefetcher:
 
     def _slot(self, s: int) -> torch.Tensor:
         if self._slots[s] is None:
-            self._slots[s] = torch.empty(max(1, self._slot_sizes[s]), dtype=torch.uint8, device=self.dev)
+            # exact-size hipMalloc outside the caching allocator: the slots live for the whole run,
+            # and a slot first touched by the loader thread would otherwise sit in the copy
+            # stream's private pool
+            self._slots[s] = hostmem.alloc_device(max(1, self._slot_sizes[s]), self.dev) if self.cuda else \
+                torch.empty(max(1, self._slot_sizes[s]), dtype=torch.uint8, device=self.dev)
         return self._slots[s]
+
+    def planned_hbm_bytes(self) -> int:
+        """Bytes of every weight slot once allocated (they are allocated on first use)."""
+        return sum(self._slot_sizes)
 
     def hbm_bytes(self) -> int:
         return sum(t.numel() for t in self._slots if t is not None)
