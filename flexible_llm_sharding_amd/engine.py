@@ -37,6 +37,7 @@ from .models.layout import layer_kind
 from .models.llama import ExecContext, layer_flops, rope_tables, run_layer
 from .ops import get_ops
 from .parallel.comm import Comm
+from .parallel.pipeline import rx_key
 from .parallel.planner import ShardPlan, make_plan
 from .runtime.activations import ActivationStore
 from .runtime.batch import Q_BLOCK, Q_BLOCK_MHA, PackedBatch, pack_prompts, split_microbatches
@@ -264,6 +265,7 @@ class ShardedRunner:
         flops = 0.0
         compute_s = 0.0
         sends = []
+        rx_err = None
         # weight bytes of this call: counted from its early prefetch (or the previous call's
         # speculative one), not from the first acquire
         h2d0 = pf.bytes_h2d if self._h2d0 is None else self._h2d0
@@ -276,100 +278,102 @@ class ShardedRunner:
                 pf.acquire(k)
                 pf.prefetch(k + 1)
                 pf.release(k)
-        ck, k0 = self._open_checkpoint(tps)
-        if k0 > 0:
-            for b, t in ck.load(k0).items():
+        ck, k0, ck_loaded = self._open_checkpoint(tps)
+        if k0 > 0 or ck_loaded:
+            for b, t in ck_loaded.items():
                 store.put(b, t.to(self.dev))
             items = [it for it in items if it[0] >= k0]
         carry = {}                     # micro-batch -> device activation kept across a shard boundary
         pos = {it: i for i, it in enumerate(items)}
         shard_ev: List = []            # end-of-shard events on the compute stream (host run-ahead bound)
-        recvs = {}
-        recv_src = None
-        recv_next = 0
+        rx = self._start_receiver(items, batches, k0, bool(ck_loaded)) if mp and comm.active else None
         cur_k = -1
         W = None
+        from_rx = False
         if self.my_shards and items:
             pf.prefetch(items[0][0])
         pbar = self._progress(len(items))
-        for idx, (k, b) in enumerate(items):
-            shard = self.my_shards[k]
-            first, last = shard[0], shard[-1]
-            if k != cur_k:
-                if ck is not None and cur_k >= 0 and self._ckpt_due(cur_k):
-                    ck.commit(cur_k + 1, range(len(batches)), self.act_dtype)
-                if self._fault is not None and k == self._fault:
-                    raise RuntimeError(f"FLS_FAULT injected on rank {comm.rank} at shard {k}")
-                if cur_k >= 0:
-                    pf.release(cur_k)
-                    sends = [(t, w) for (t, w) in sends if not w.is_completed()]   # bound memory
-                    self._throttle(shard_ev)
-                with trace.range(f"shard{k}:acquire"):
-                    W = pf.acquire(k)
-                with trace.range(f"shard{k + 1}:prefetch"):
-                    pf.prefetch(k + 1)
-                cur_k = k
-                src_rank = self._owner(first - 1) if (mp and first > 0) else comm.rank
-                dst_rank = self._owner(last + 1) if (mp and last + 1 < self.L) else comm.rank
-                recv_next = 0
-                recv_src = src_rank if (first > 0 and src_rank != comm.rank) else None
+        try:
+            for idx, (k, b) in enumerate(items):
+                shard = self.my_shards[k]
+                first, last = shard[0], shard[-1]
+                if k != cur_k:
+                    if ck is not None and cur_k >= 0 and self._ckpt_due(cur_k):
+                        ck.commit(self._ckpt_key(cur_k), range(len(batches)), self.act_dtype)
+                    if self._fault is not None and k == self._fault:
+                        raise RuntimeError(f"FLS_FAULT injected on rank {comm.rank} at shard {k}")
+                    if cur_k >= 0:
+                        pf.release(cur_k)
+                        self._throttle(shard_ev)
+                    with trace.range(f"shard{k}:acquire"):
+                        W = pf.acquire(k)
+                    with trace.range(f"shard{k + 1}:prefetch"):
+                        pf.prefetch(k + 1)
+                    cur_k = k
+                    src_rank = self._owner(first - 1) if (mp and first > 0) else comm.rank
+                    dst_rank = self._owner(last + 1) if (mp and last + 1 < self.L) else comm.rank
+                    # a stage whose input comes from another rank reads the receiver thread's store,
+                    # except the shard a model-parallel resume restarts at (inputs from the checkpoint)
+                    from_rx = rx is not None and first > 0 and src_rank != comm.rank and not (
+                        ck_loaded and k == k0)
 
-            def post_recvs(upto):
-                # receives are posted in the sender's order, at most `window` ahead: the
-                # reference's max_activation_in_cpu back-pressure (utils.py:179-180) — a
-                # producer blocks (on its own RCCL stream, not the host) until we post
-                nonlocal recv_next
-                while recv_next < min(upto, len(batches)):
-                    bb = recv_next
-                    buf = torch.empty(self._state_shape(first - 1, batches[bb]), dtype=self.act_dtype,
-                                      device=self.dev)
-                    recvs[bb] = (buf, comm.irecv(buf, recv_src))
-                    recv_next += 1
-
-            batch, meta = batches[b], metas[b]
-            if first == 0:
-                state = None
-            elif recv_src is not None:
-                post_recvs(b + self.recv_window(len(tps), len(batches)))
-                buf, work = recvs.pop(b)
-                work.wait()
-                state = buf
-            elif b in carry:
-                state = carry.pop(b)
-            else:
-                state = store.get(b)
-            # one-ahead activation prefetch (crosses shard boundaries)
-            if idx + 1 < len(items):
-                k2, b2 = items[idx + 1]
-                if self.my_shards[k2][0] > 0 and k2 == k:
-                    store.prefetch(b2)
-                elif k2 != k and idx + 2 < len(items):
-                    store.prefetch(items[idx + 2][1])
-            tc = time.perf_counter()
-            with trace.range(f"shard{k}:mb{b}:compute"):
-                for li in shard:
-                    name = self.names[li]
-                    state = run_layer(self.ctx, name, W[name], state, batch, meta)
-                    if layer_kind(name) == "decoder":
-                        flops += layer_flops(self.cfg, batch, self._pruned(name))
-            compute_s += time.perf_counter() - tc
-            if pbar is not None:
-                pbar.update(1)
-            if ck is not None and self._ckpt_due(k):
-                ck.save_state(k + 1, b, state)
-            nxt = items[idx + 1] if idx + 1 < len(items) else None
-            if last == self.L - 1:
-                out_pending.append(self._start_output_copy(batch, state))
-            elif dst_rank != comm.rank:
-                st = state.contiguous()
-                sends.append((st, comm.isend(st, dst_rank)))
-            elif self.storage != "gpu" and pos.get((k + 1, b), len(items)) - idx <= self.CARRY_WINDOW:
-                # re-used within CARRY_WINDOW micro-batch computes (the zigzag boundary micro-batch
-                # and its neighbour): a PCIe round trip would only add traffic, keep it in HBM
-                carry[b] = state
-            else:
-                store.put(b, state)
-            del state
+                batch, meta = batches[b], metas[b]
+                if first == 0:
+                    state = None
+                elif from_rx:
+                    state = rx.get(rx_key(k, b))
+                    if b + 1 < len(batches):
+                        rx.prefetch(rx_key(k, b + 1))
+                elif b in carry:
+                    state = carry.pop(b)
+                else:
+                    state = store.get(b)
+                if ck is not None and mp and self._ckpt_due(k) and state is not None:
+                    ck.save_state(self._ckpt_key(k), b, state)     # model parallel: a stage's inputs
+                # one-ahead activation prefetch (crosses shard boundaries)
+                if idx + 1 < len(items):
+                    k2, b2 = items[idx + 1]
+                    if self.my_shards[k2][0] > 0 and k2 == k:
+                        store.prefetch(b2)
+                    elif k2 != k and idx + 2 < len(items):
+                        store.prefetch(items[idx + 2][1])
+                tc = time.perf_counter()
+                with trace.range(f"shard{k}:mb{b}:compute"):
+                    for li in shard:
+                        name = self.names[li]
+                        state = run_layer(self.ctx, name, W[name], state, batch, meta)
+                        if layer_kind(name) == "decoder":
+                            flops += layer_flops(self.cfg, batch, self._pruned(name))
+                compute_s += time.perf_counter() - tc
+                if pbar is not None:
+                    pbar.update(1)
+                if ck is not None and not mp and self._ckpt_due(k):
+                    ck.save_state(self._ckpt_key(k), b, state)     # single / DP: a shard's outputs
+                if last == self.L - 1:
+                    out_pending.append(self._start_output_copy(batch, state))
+                elif dst_rank != comm.rank:
+                    st = state.contiguous()
+                    sends.append((st, comm.isend(st, dst_rank)))
+                elif self.storage != "gpu" and pos.get((k + 1, b), len(items)) - idx <= self.CARRY_WINDOW:
+                    # re-used within CARRY_WINDOW micro-batch computes (the zigzag boundary micro-batch
+                    # and its neighbour): a PCIe round trip would only add traffic, keep it in HBM
+                    carry[b] = state
+                else:
+                    store.put(b, state)
+                del state
+                # pending sends are retired per micro-batch: the consumer's receiver thread drains them
+                sends = [(t, w) for (t, w) in sends if not w.is_completed()]
+            if ck is not None and mp and cur_k >= 0 and self._ckpt_due(cur_k):
+                ck.commit(self._ckpt_key(cur_k), range(len(batches)), self.act_dtype)
+        finally:
+            if rx is not None:
+                rx_err = None
+                try:
+                    rx.close()
+                except BaseException as e:  # noqa: BLE001
+                    rx_err = e
+        if rx is not None and rx_err is not None:
+            raise rx_err
         h2d_end = pf.bytes_h2d
         if cur_k >= 0:
             pf.release(cur_k)
@@ -379,8 +383,6 @@ class ShardedRunner:
                 # call's tail (lm_head, D2H of the scores) and the next tokenization
                 for k in range(min(pf.n_slots, len(self.my_shards))):
                     pf.prefetch(k)
-        if recvs:
-            raise RuntimeError("unconsumed receives")
         for t, w in sends:
             w.wait()
         if self.cuda:
@@ -533,39 +535,76 @@ class ShardedRunner:
         return tqdm(total=total, desc=f"{self.dev} shard x micro-batch", unit="step")
 
     def _ckpt_due(self, k: int) -> bool:
-        """Checkpoint after shard k (index into my_shards)?  Never after the shard with lm_head."""
+        """Checkpoint at shard k (index into my_shards)?
+
+        Single / data parallel: after shard k, its outputs (never after the lm_head shard).
+        Model parallel: the inputs of shard k, every ``every`` global shards (a stage boundary
+        the consumer holds, so a restart needs no in-flight pipeline state)."""
         e = self.checkpoint_every
-        return (e > 0 and (k + 1) % e == 0 and k + 1 < len(self.my_shards)
+        if e <= 0:
+            return False
+        if self.plan.mode == "mp":
+            g = self.plan.all_shards.index(self.my_shards[k])
+            return g > 0 and g % e == 0 and self.my_shards[k][0] > 0
+        return ((k + 1) % e == 0 and k + 1 < len(self.my_shards)
                 and self.my_shards[k][-1] < self.L - 1)
 
+    def _ckpt_key(self, k: int) -> int:
+        """Checkpoint key: next local shard (single / DP) or the stage's first layer (MP)."""
+        return self.my_shards[k][0] if self.plan.mode == "mp" else k + 1
+
     def _open_checkpoint(self, tps):
-        """-> (RunCheckpoint or None, first shard to run).  DP ranks agree on a common shard."""
+        """-> (RunCheckpoint or None, first local shard to run, states to start from).
+
+        Data-parallel ranks agree on a shard they all hold.  Model-parallel ranks agree on the
+        latest stage boundary whose consumer holds its inputs: every rank skips the shards
+        before it, the consumer restarts from the checkpointed inputs, the others as usual."""
         if not self.resume_dir or not self.my_shards:
-            return None, 0
-        if self.plan.mode == "mp":
-            if self.verbose:
-                print("--resume_dir: ignored in model-parallel mode (in-flight pipeline state)")
-            return None, 0
+            return None, 0, {}
         from .runtime.checkpoint import RunCheckpoint, run_fingerprint
         fp = run_fingerprint(self.cfg, [tp.prefix + [t for s in tp.suffixes for t in s] + [-1] for tp in tps],
                              lnps=self.lnps, budget=self.token_budget, attn=self.prefix_attention,
                              world=self.comm.world, rank=self.comm.rank, dp=self.data_parallel,
                              dtype=str(self.act_dtype), every=self.checkpoint_every,
-                             prune=self.ctx.prune_last)
+                             prune=self.ctx.prune_last, stages=self.plan.stages)
         ck = RunCheckpoint(self.resume_dir, fp, self.comm.rank)
         have = set(ck.available())
+        if self.plan.mode == "mp":
+            allsets = self.comm.all_gather_object(sorted(have)) if self.comm.world > 1 else [sorted(have)]
+            usable = [L for r, keys in enumerate(allsets) for L in keys if self.plan.owner_of_layer(L) == r]
+            Lc = max(usable) if usable else 0
+            if Lc == 0:
+                return ck, 0, {}
+            k0 = next((k for k, sh in enumerate(self.my_shards) if sh[0] >= Lc), len(self.my_shards))
+            loaded = ck.load(Lc) if k0 < len(self.my_shards) and self.my_shards[k0][0] == Lc else {}
+            if self.verbose:
+                print(f"rank{self.comm.rank}: resuming at layer {Lc} (local shard {k0}) from {ck.dir}")
+            return ck, k0, loaded
         if self.comm.world > 1:
             for other in self.comm.all_gather_object(sorted(have)):
                 have &= set(other)
         k0 = max(have) if have else 0
         if k0 and self.verbose:
             print(f"rank{self.comm.rank}: resuming at shard {k0} from {ck.dir}")
-        return ck, k0
+        return ck, k0, (ck.load(k0) if k0 else {})
 
-    def recv_window(self, n_prompts: int, n_batches: int) -> int:
-        """Micro-batches a pipeline stage may have received but not consumed."""
-        per_mb = max(1.0, n_prompts / max(1, n_batches))
-        return max(2, int(self.max_act // per_mb))
+    def _start_receiver(self, items, batches, k0: int, resumed: bool):
+        """Receiver thread for every (shard, micro-batch) this rank gets from another rank."""
+        from .parallel.pipeline import StageReceiver
+        jobs, seen = [], set()
+        for k, b in items:
+            sh = self.my_shards[k]
+            if sh[0] == 0 or (resumed and k == k0):
+                continue
+            src = self._owner(sh[0] - 1)
+            if src == self.comm.rank:
+                continue
+            jobs.append((rx_key(k, b), src, self._state_shape(sh[0] - 1, batches[b])))
+            seen.add(k)
+        if not jobs:
+            return None
+        return StageReceiver(self.comm, self.dev, self.act_dtype, self.storage, self.disk_folder,
+                             str(self.comm.rank), jobs)
 
     def _start_output_copy(self, batch: PackedBatch, probs: torch.Tensor):
         if not self.cuda:

@@ -140,14 +140,16 @@ class ActivationStore:
 
     # -------------------------------------------------------------- put
     def put(self, key, t: torch.Tensor) -> None:
-        old = self._e.pop(key, None)
+        with self.lock:
+            old = self._e.pop(key, None)
         if old is not None:
             self._drop(old)
         e = _Entry()
         e.shape, e.dtype = tuple(t.shape), t.dtype
         if self.mode == "gpu":
             e.dev = t
-            self._e[key] = e
+            with self.lock:
+                self._e[key] = e
             return
         nbytes = t.numel() * t.element_size()
         if not self.cuda:
@@ -156,7 +158,8 @@ class ActivationStore:
             else:
                 e.path = self.path_for(key)
                 self._write_npy(e.path, t.contiguous(), e.shape, e.dtype)
-            self._e[key] = e
+            with self.lock:
+                self._e[key] = e
             return
         host = self._get_host(nbytes)
         cur = torch.cuda.current_stream(self.dev)
@@ -178,7 +181,8 @@ class ActivationStore:
                 self._put_host(ent.host)
                 ent.host = None
             e.write_fut = self._io.submit(_write)
-        self._e[key] = e
+        with self.lock:
+            self._e[key] = e
 
     def _write_npy(self, path: str, t: torch.Tensor, shape, dtype) -> None:
         hdr = _npy_header(shape, dtype)
@@ -207,9 +211,10 @@ class ActivationStore:
     # -------------------------------------------------------------- get
     def prefetch(self, key) -> None:
         """Start bringing ``key`` back to the device (no-op for gpu mode)."""
-        if self.mode == "gpu" or key in self._inflight or key not in self._e:
-            return
-        e = self._e[key]
+        with self.lock:
+            if self.mode == "gpu" or key in self._inflight or key not in self._e:
+                return
+            e = self._e[key]
         if not self.cuda:
             return
         if self.mode == "disk":
@@ -225,7 +230,8 @@ class ActivationStore:
             self._inflight[key] = (None, None)
 
     def get(self, key, pop: bool = True) -> torch.Tensor:
-        e = self._e.pop(key) if pop else self._e[key]
+        with self.lock:
+            e = self._e.pop(key) if pop else self._e[key]
         if self.mode == "gpu":
             return e.dev
         if not self.cuda:

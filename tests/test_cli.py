@@ -158,3 +158,49 @@ def test_weight_cache_resolution(tiny_model):
     assert resolve_weight_cache(args("disk", 100.0), cfg, comm, names, sliced=False) == "stream"
     with pytest.raises(SystemExit):
         resolve_weight_cache(args("host", 1e-4), cfg, comm, names, sliced=False)
+
+
+def _torchrun(world, args, cwd):
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "main.py")] + args
+    r = subprocess.run(cmd, cwd=cwd, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return r
+
+
+@pytest.mark.parametrize("n_prompts,num_batch,weight_cache", [(3, 2, "host"), (1, 1, "host"), (3, 2, "stream"),
+                                                               (0, 1, "host")])
+def test_main_data_parallel_uneven_slices(tiny_model, tmp_path, n_prompts, num_batch, weight_cache):
+    """DP with scatter-loaded weights and prompt slices of different sizes (3 prompts / 2 ranks with
+    2 batches: rank 1 has an empty batch; 1 prompt: rank 1 has none; 0 prompts): every rank still
+    runs num_batch passes, so the weight all-gathers stay matched, and the scores equal
+    a one-process run."""
+    from flexible_llm_sharding_amd.utils.synthetic import synthetic_prompts
+    path, cfg = tiny_model
+    prompts = synthetic_prompts(n_prompts, 14, 2, 4, cfg.vocab_size, seed=8, vary=True)
+    pp = tmp_path / "prompts.pkl"
+    pickle.dump(prompts, open(pp, "wb"))
+    common = ["--model_path", path, "--prompt_pickle", str(pp), "--num_batch", str(num_batch),
+              "--weight_cache", weight_cache]
+    _torchrun(2, common + ["--output_file", str(tmp_path / "dp.pkl"), "--data_parallel"], str(tmp_path))
+    _run(common + ["--output_file", str(tmp_path / "one.pkl")], str(tmp_path))
+    dp, one = pickle.load(open(tmp_path / "dp.pkl", "rb")), pickle.load(open(tmp_path / "one.pkl", "rb"))
+    assert len(dp) == len(one) == n_prompts
+    for a, b in zip(dp, one):
+        assert np.abs(a.astype(np.float32) - b.astype(np.float32)).max() < 1e-5
+
+
+def test_main_model_parallel_no_prompts(tiny_model, tmp_path):
+    """MP with an empty prompt list returns an empty score list."""
+    path, cfg = tiny_model
+    pp = tmp_path / "prompts.pkl"
+    pickle.dump([], open(pp, "wb"))
+    _torchrun(2, ["--model_path", path, "--prompt_pickle", str(pp), "--output_file", str(tmp_path / "o.pkl")],
+              str(tmp_path))
+    assert pickle.load(open(tmp_path / "o.pkl", "rb")) == []

@@ -189,3 +189,70 @@ def test_prefix_kv_cache_distributed(single, tmp_path, world, dp):
     assert len(got) == len(ref)
     for a, b in zip(got, ref):
         assert _close(a, b)
+
+
+def _mp_resume_worker(rank, world, port, path, prompts, out_dir, resume_dir, fault, storage):
+    if fault:
+        os.environ["FLS_FAULT"] = fault
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    torch.set_num_threads(1)
+    from flexible_llm_sharding_amd.config import ModelConfig
+    from flexible_llm_sharding_amd.engine import ShardedRunner
+    from flexible_llm_sharding_amd.parallel.comm import Comm
+    from flexible_llm_sharding_amd.runtime.stream import FileLayerSource
+    from flexible_llm_sharding_amd.utils.tokenizer import load_tokenizer
+    comm = Comm.from_env("cpu", timeout_s=60)
+    cfg = ModelConfig.from_pretrained(path)
+    r = ShardedRunner(cfg, FileLayerSource(cfg, path), "cpu", load_tokenizer(path), layer_num_per_shard=1,
+                      storage_location=storage, disk_folder=os.path.join(out_dir, f"spill{rank}"), comm=comm,
+                      token_budget=40, resume_dir=resume_dir, checkpoint_every=2)
+    outs = r(prompts)
+    allv = comm.gather_object(outs, dst=0)
+    resumed = comm.gather_object(r.stats["resumed_from_shard"], dst=0)
+    if rank == 0:
+        with open(os.path.join(out_dir, "out.pkl"), "wb") as f:
+            pickle.dump(allv, f)
+        with open(os.path.join(out_dir, "resumed.pkl"), "wb") as f:
+            pickle.dump(resumed, f)
+    comm.destroy()
+
+
+@pytest.fixture(scope="module")
+def deeper(tmp_path_factory):
+    """6 decoder layers: a 2-rank round-robin pipeline has 5 shards per rank."""
+    from flexible_llm_sharding_amd.config import preset
+    from flexible_llm_sharding_amd.engine import ShardedRunner
+    from flexible_llm_sharding_amd.runtime.stream import FileLayerSource
+    from flexible_llm_sharding_amd.utils.synthetic import synthetic_prompts, write_synthetic_checkpoint
+    from flexible_llm_sharding_amd.utils.tokenizer import load_tokenizer
+    cfg = preset("tiny", num_hidden_layers=6)
+    path = str(tmp_path_factory.mktemp("deep"))
+    write_synthetic_checkpoint(cfg, path, seed=2, std=0.05)
+    prompts = synthetic_prompts(7, 25, 3, 6, cfg.vocab_size, seed=22, vary=True)
+    out = ShardedRunner(cfg, FileLayerSource(cfg, path), "cpu", load_tokenizer(path))(prompts)
+    return path, prompts, out
+
+
+@pytest.mark.parametrize("storage", ["cpu", "disk"])
+def test_model_parallel_resume_after_rank_fault(deeper, tmp_path, storage):
+    """MP + --resume_dir: each stage checkpoints its inputs every 2 global shards; rank 1 dies
+    entering its 4th shard; the relaunch restarts every rank at the latest stage boundary whose
+    consumer holds its inputs (rank 0 resumes mid-pipeline, rank 1 after it) and matches a clean run.
+    Received activations drain through the receiver thread into the chosen storage."""
+    path, prompts, ref = deeper
+    ck = str(tmp_path / "ck")
+    with pytest.raises(Exception):
+        mp.start_processes(_mp_resume_worker, args=(2, _port(), path, prompts, str(tmp_path), ck, "1:3", storage),
+                           nprocs=2, start_method="spawn", join=True)
+    assert any(n.startswith("step") for n in os.listdir(os.path.join(ck, "rank0")))
+    mp.start_processes(_mp_resume_worker, args=(2, _port(), path, prompts, str(tmp_path), ck, "", storage),
+                       nprocs=2, start_method="spawn", join=True)
+    resumed = pickle.load(open(tmp_path / "resumed.pkl", "rb"))
+    assert resumed[0] >= 2 and resumed[1] >= 2          # layer 4 or 6 boundary: both ranks skip shards
+    allv = pickle.load(open(tmp_path / "out.pkl", "rb"))
+    owner = [v for v in allv if v and v[0] is not None]
+    assert len(owner) == 1
+    for a, b in zip(owner[0], ref):
+        assert _close(a, b)
+    assert not os.path.exists(ck) or not os.listdir(ck)   # cleared once the run completes
