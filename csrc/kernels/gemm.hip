@@ -41,6 +41,7 @@
 #include "fls.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace {
 
@@ -134,17 +135,42 @@ __device__ __forceinline__ void store_rope_pair(half_t* __restrict__ C, int ldc,
   *(half4*)(C + (size_t)m * ldc + cb) = ob;
 }
 
+// 16-byte stores of a pair of neighbouring 16-column subtiles (columns c .. c+31 of one row).
+// Lanes of row group g (lane >> 4) hold columns 4g..4g+3 of both subtiles; one v_permlane16_swap
+// per dword exchanges the odd groups' first-subtile halves with the even groups' second-subtile
+// halves, after which every lane owns 8 consecutive columns: g0 -> c+0, g2 -> c+8, g1 -> c+16,
+// g3 -> c+24.  Half the store instructions, and each 16-lane group writes whole 64-B segments.
+// Every lane must execute the swap (partners share the row, so a row guard belongs on the store).
+__device__ __forceinline__ uint4 wide_pair(half4 oa, half4 ob) {
+  const uint2 a = __builtin_bit_cast(uint2, oa), b = __builtin_bit_cast(uint2, ob);
+  const auto r0 = __builtin_amdgcn_permlane16_swap(a.x, b.x, false, false);
+  const auto r1 = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
+  return uint4{r0[0], r1[0], r0[1], r1[1]};
+}
+__device__ __forceinline__ int wide_off(int g) { return (g & 1) * 16 + (g >> 1) * 8; }
+
+// Inverse of wide_pair on a 16-byte row chunk loaded at wide_off (the swap is an involution):
+// returns this lane's 4 columns of the first and of the second subtile.
+__device__ __forceinline__ void unwide_pair(uint4 v, half4& a, half4& b) {
+  const auto r0 = __builtin_amdgcn_permlane16_swap(v.x, v.z, false, false);
+  const auto r1 = __builtin_amdgcn_permlane16_swap(v.y, v.w, false, false);
+  a = __builtin_bit_cast(half4, uint2{r0[0], r1[0]});
+  b = __builtin_bit_cast(half4, uint2{r0[1], r1[1]});
+}
+
 // RoPE epilogue of a v10/v13 wave quadrant (128 rows x 128 columns = whole heads).
 // HD 128: one head per wave, pairs (q, q+4); HD 64: two heads, pairs (q', q'+2),
-// q' in {0, 1, 4, 5}.  Row group u+1's cos/sin loads are issued before row group
-// u's stores (the tables cannot alias C, so a fence keeps the compiler from
-// hoisting all 8 rows' loads and spilling).
+// q' in {0, 1, 4, 5}.  Neighbouring subtiles (q, q+1), q even, leave as 16-byte stores
+// (wide_pair).  Row group u+1's cos/sin loads are issued before row group u's stores (the
+// tables cannot alias C, so a fence keeps the compiler from hoisting all 8 rows' loads and
+// spilling).
 template <int HD>
 __device__ __forceinline__ void epilogue_rope(half_t* __restrict__ C, int ldc, int M, int mrow0, int ncol0, int grp,
                                               floatx4 (&acc)[8][8], const Epi& ep) {
   constexpr int HS = HD / 32;
   constexpr int HALF = HD / 2;
   const int off = 4 * grp;
+  const int woff = wide_off(grp);
   int pos[8];
 #pragma unroll
   for (int u = 0; u < 8; ++u) pos[u] = ep.pos[min(mrow0 + u * 16, M - 1)];
@@ -182,130 +208,122 @@ __device__ __forceinline__ void epilogue_rope(half_t* __restrict__ C, int ldc, i
     if (u + 1 < 8) load(u + 1, sl ^ 1);
     asm volatile("" ::: "memory");
     const int m = mrow0 + u * 16;
-    if (m < M) {
+    half4 oa[4], ob[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int ta = HD == 128 ? q : (q & 1) + (q >> 1) * 4;
-        half4 oa, ob;
+    for (int q = 0; q < 4; ++q) {
+      const int ta = HD == 128 ? q : (q & 1) + (q >> 1) * 4;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float x1 = acc[u][ta][r] + (float)ba[q][r], x2 = acc[u][ta + HS][r] + (float)bb[q][r];
-          if (rot[q]) {
-            const float c = cs[sl][q][r], sv = sn[sl][q][r];
-            const float y1 = x1 * c - x2 * sv, y2 = x2 * c + x1 * sv;
-            x1 = y1;
-            x2 = y2;
-          }
-          oa[r] = (half_t)x1;
-          ob[r] = (half_t)x2;
+      for (int r = 0; r < 4; ++r) {
+        float x1 = acc[u][ta][r] + (float)ba[q][r], x2 = acc[u][ta + HS][r] + (float)bb[q][r];
+        if (rot[q]) {
+          const float c = cs[sl][q][r], sv = sn[sl][q][r];
+          const float y1 = x1 * c - x2 * sv, y2 = x2 * c + x1 * sv;
+          x1 = y1;
+          x2 = y2;
         }
-        half_t* cp = C + (size_t)m * ldc + ncol0 + ta * 16 + off;
-        *(half4*)cp = oa;
-        *(half4*)(cp + HALF) = ob;
+        oa[q][r] = (half_t)x1;
+        ob[q][r] = (half_t)x2;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q += 2) {
+      const int ta = HD == 128 ? q : (q & 1) + (q >> 1) * 4;
+      const uint4 va = wide_pair(oa[q], oa[q + 1]);
+      const uint4 vb = wide_pair(ob[q], ob[q + 1]);
+      half_t* cp = C + (size_t)m * ldc + ncol0 + ta * 16 + woff;
+      if (m < M) {
+        *(uint4*)cp = va;
+        *(uint4*)(cp + HALF) = vb;
       }
     }
   }
 }
 
-template <int EPI>
-__device__ __forceinline__ void epilogue_plain(half_t* __restrict__ C, int ldc, int M, int mrow0, int ncol0,
-                                               int grp, floatx4 (&acc)[8][8], const Epi& ep);
-
-// Epilogue of a wave's 128 (M) x 128 (N) quadrant held as acc[8 row groups][8 subtiles] (v10/v13).
-// Row group u+1's operand loads (residual rows) are issued before row group u's stores
-// (different rows, so in-place R == C stays correct); the per-column bias is loaded once.
+// Epilogue of a wave's 128 (M) x 128 (N) quadrant held as acc[8 row groups][8 subtiles] (v10/v13),
+// 16-byte stores throughout (wide_pair).  Row group u+1's operand loads (residual rows) are issued
+// before row group u's stores (different rows, so in-place R == C stays correct); the per-column
+// bias is loaded once.
 template <int EPI>
 __device__ __forceinline__ void epilogue_quadrant(half_t* __restrict__ C, int ldc, int M, int mrow0, int ncol0,
                                                   int grp, floatx4 (&acc)[8][8], const Epi& ep) {
   if constexpr (EPI == FLS_EPI_ROPE) {
     epilogue_rope<128>(C, ldc, M, mrow0, ncol0, grp, acc, ep);
+    return;
   } else if constexpr (EPI == EPI_ROPE64) {
     epilogue_rope<64>(C, ldc, M, mrow0, ncol0, grp, acc, ep);
+    return;
   } else {
-    epilogue_plain<EPI>(C, ldc, M, mrow0, ncol0, grp, acc, ep);
-  }
-}
-
-template <int EPI>
-__device__ __forceinline__ void epilogue_plain(half_t* __restrict__ C, int ldc, int M, int mrow0, int ncol0,
-                                               int grp, floatx4 (&acc)[8][8], const Epi& ep) {
-  const int off = 4 * grp;
-  if constexpr (EPI == FLS_EPI_NONE || EPI == FLS_EPI_SWIGLU) {
-    if (EPI == FLS_EPI_SWIGLU || ep.bias == nullptr) {
+    const int off = 4 * grp;
+    const int woff = wide_off(grp);
+    if constexpr (EPI == FLS_EPI_SWIGLU) {
+      // pair p -> intermediate columns [ncol0/2 + 16p, +16); pairs (p, p+1) share one 16-B store
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int m = mrow0 + u * 16;
-        if (m < M) {
+        half4 o[4];
 #pragma unroll
-          for (int p = 0; p < 4; ++p)
-            store_pair_off<EPI>(C, ldc, m, ncol0 + p * 32, off, acc[u][2 * p], acc[u][2 * p + 1], ep);
+        for (int p = 0; p < 4; ++p)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[p][r] = (half_t)(silu(acc[u][2 * p][r]) * acc[u][2 * p + 1][r]);
+#pragma unroll
+        for (int p = 0; p < 4; p += 2) {
+          const uint4 v = wide_pair(o[p], o[p + 1]);
+          if (m < M) *(uint4*)(C + (size_t)m * ldc + ncol0 / 2 + p * 16 + woff) = v;
         }
       }
       return;
-    }
-  }
-  half4 ba[4], bb[4];
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    if (ep.bias) {
-      ba[p] = *(const half4*)(ep.bias + ncol0 + p * 32 + off);
-      bb[p] = *(const half4*)(ep.bias + ncol0 + p * 32 + off + 16);
     } else {
-      ba[p] = half4{0, 0, 0, 0};
-      bb[p] = half4{0, 0, 0, 0};
-    }
-  }
-  if constexpr (EPI == FLS_EPI_RESID) {
-    half4 ra[2][4], rb[2][4];
-    auto load = [&](int u, int sl) {
-      const int m = min(mrow0 + u * 16, M - 1);
-      const half_t* rp = ep.R + (size_t)m * ep.ldr + ncol0 + off;
+      half4 ba[4], bb[4];
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
-        ra[sl][p] = *(const half4*)(rp + p * 32);
-        rb[sl][p] = *(const half4*)(rp + p * 32 + 16);
-      }
-    };
-    load(0, 0);
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int sl = u & 1;
-      if (u + 1 < 8) load(u + 1, sl ^ 1);
-      asm volatile("" ::: "memory");
-      const int m = mrow0 + u * 16;
-      if (m < M) {
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-          half4 oa, ob;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            oa[r] = (half_t)(acc[u][2 * p][r] + (float)ba[p][r] + (float)ra[sl][p][r]);
-            ob[r] = (half_t)(acc[u][2 * p + 1][r] + (float)bb[p][r] + (float)rb[sl][p][r]);
-          }
-          half_t* cp = C + (size_t)m * ldc + ncol0 + p * 32 + off;
-          *(half4*)cp = oa;
-          *(half4*)(cp + 16) = ob;
+        if (ep.bias) {
+          ba[p] = *(const half4*)(ep.bias + ncol0 + p * 32 + off);
+          bb[p] = *(const half4*)(ep.bias + ncol0 + p * 32 + off + 16);
+        } else {
+          ba[p] = half4{0, 0, 0, 0};
+          bb[p] = half4{0, 0, 0, 0};
         }
       }
-    }
-  } else {   // NONE with bias
+      uint4 rw[2][4];
+      auto load = [&](int u, int sl) {
+        if constexpr (EPI == FLS_EPI_RESID) {
+          const int m = min(mrow0 + u * 16, M - 1);
+          const half_t* rp = ep.R + (size_t)m * ep.ldr + ncol0 + woff;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int m = mrow0 + u * 16;
-      if (m < M) {
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-          half4 oa, ob;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            oa[r] = (half_t)(acc[u][2 * p][r] + (float)ba[p][r]);
-            ob[r] = (half_t)(acc[u][2 * p + 1][r] + (float)bb[p][r]);
-          }
-          half_t* cp = C + (size_t)m * ldc + ncol0 + p * 32 + off;
-          *(half4*)cp = oa;
-          *(half4*)(cp + 16) = ob;
+          for (int p = 0; p < 4; ++p) rw[sl][p] = *(const uint4*)(rp + p * 32);
         }
-      }
+      };
+      auto body = [&](auto has_bias) {
+        load(0, 0);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int sl = u & 1;
+          if (u + 1 < 8) load(u + 1, sl ^ 1);
+          asm volatile("" ::: "memory");
+          const int m = mrow0 + u * 16;
+#pragma unroll
+          for (int p = 0; p < 4; ++p) {
+            floatx4 a = acc[u][2 * p], b = acc[u][2 * p + 1];
+            if constexpr (decltype(has_bias)::value) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) { a[r] += (float)ba[p][r]; b[r] += (float)bb[p][r]; }
+            }
+            if constexpr (EPI == FLS_EPI_RESID) {
+              half4 ra, rb;
+              unwide_pair(rw[sl][p], ra, rb);
+#pragma unroll
+              for (int r = 0; r < 4; ++r) { a[r] += (float)ra[r]; b[r] += (float)rb[r]; }
+            }
+            half4 oa, ob;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) { oa[r] = (half_t)a[r]; ob[r] = (half_t)b[r]; }
+            const uint4 v = wide_pair(oa, ob);
+            if (m < M) *(uint4*)(C + (size_t)m * ldc + ncol0 + p * 32 + woff) = v;
+          }
+        }
+      };
+      if (ep.bias) body(std::true_type{});
+      else body(std::false_type{});
     }
   }
 }
