@@ -63,6 +63,7 @@ struct Epi {
   int head_dim;
   const half_t* bias;   // optional per-output-column bias (Qwen2 q/k/v, Llama attention_bias), added first
   int gu_rows;          // SWIGLU: I (rows of gate = rows of up)
+  int order;            // v10/v13 tile order (tile_of), set by the launcher
 };
 
 // SWIGLU logical row l (gate/up interleaved per 16 rows) -> physical row of [gate; up]
@@ -549,8 +550,6 @@ __global__ __launch_bounds__(mid::NTm) void gemm_nt_mid(const half_t* __restrict
 // ds_read_b128 after each of the first 16 even-numbered MFMAs (the 8 reads of the half
 // needed later) and the half-tile's 4 LDS-DMA ops after MFMAs 17, 20, 23, 26; then
 // lgkmcnt(0) + counted vmcnt + raw barrier.  Requires an even number of K-tiles.
-// GM: tile order — consecutive blocks walk GM M-tiles per N-tile (grouped column-major);
-// negative GM groups -GM N-tiles per M-tile instead.
 //
 // W-operand source addresses are per 8-row piece, so the SWIGLU loader can map the
 // logical (gate/up interleaved) tile rows onto the stacked [gate; up] weight.
@@ -561,7 +560,30 @@ __global__ __launch_bounds__(mid::NTm) void gemm_nt_mid(const half_t* __restrict
   (EPI == FLS_EPI_SWIGLU ? Wb + (size_t)(k0) * 2 + wo[(hb) * 4 + (i)]                             \
                          : Wb + (hb) * wb_off + (size_t)(k0) * 2 + wo[(i)])
 
-template <int EPI, int GM = 8>
+// Virtual tile id -> (tm, tn).  order > 0: groups of `order` M tiles walked M-fastest along N;
+// order < 0: groups of -order N tiles walked N-fastest along M.  With the XCD-aware remap
+// (virtual ids [x*q, (x+1)*q) run on XCD x) a group of tiles/8 makes each XCD own one chunk of
+// the grouped dimension's operand, which stays in its L2 / the MALL, while all XCDs walk the
+// other operand in step (profiles/r2_gemm).
+__device__ __forceinline__ int2 tile_of(int b, int tiles_m, int tiles_n, int order) {
+  const bool by_m = order > 0;
+  const int g = by_m ? order : -order;
+  const int along = by_m ? tiles_n : tiles_m;     // tiles walked per group member
+  const int total = by_m ? tiles_m : tiles_n;     // tiles of the grouped dimension
+  const int group = b / (g * along);
+  const int first = group * g;
+  const int gsz = min(total - first, g);
+  const int in_g = b - group * g * along;
+  const int grouped = first + in_g % gsz, walked = in_g / gsz;
+  return by_m ? int2{grouped, walked} : int2{walked, grouped};   // (tm, tn)
+}
+
+// raw buffer descriptor over [base, base + 4 GiB): the launcher guarantees every offset fits 32 bits
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, -1, 0x00020000);
+}
+
+template <int EPI>
 __global__ __launch_bounds__(256, 1) void gemm_nt_v10(const half_t* __restrict__ A, const half_t* __restrict__ W,
                                                     half_t* __restrict__ C, int M, int N, int K, int lda, int ldw,
                                                     int ldc, Epi ep) {
@@ -578,24 +600,8 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_v10(const half_t* __restrict__
   }
   const int tiles_m = (M + BM - 1) / BM;
   const int tiles_n = N / BN;
-  int tm, tn;
-  if (GM > 0) {
-    constexpr int GROUP_M = GM > 0 ? GM : 1;
-    const int group = bid / (GROUP_M * tiles_n);
-    const int first_m = group * GROUP_M;
-    const int gsz = min(tiles_m - first_m, GROUP_M);
-    const int in_g = bid - group * GROUP_M * tiles_n;
-    tm = first_m + in_g % gsz;
-    tn = in_g / gsz;
-  } else {
-    constexpr int GROUP_N = GM < 0 ? -GM : 1;
-    const int group = bid / (GROUP_N * tiles_m);
-    const int first_n = group * GROUP_N;
-    const int gsz = min(tiles_n - first_n, GROUP_N);
-    const int in_g = bid - group * GROUP_N * tiles_m;
-    tn = first_n + in_g % gsz;
-    tm = in_g / gsz;
-  }
+  const int2 tmn = tile_of(bid, tiles_m, tiles_n, ep.order);
+  const int tm = tmn.x, tn = tmn.y;
   const int m0 = tm * BM, n0 = tn * BN;
 
   // staging: a half-tile = 16 pieces of 8 rows x 128 B, rows {(j>>3)*128 + (j&7)*8} (+64 for the B half);
@@ -628,12 +634,22 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_v10(const half_t* __restrict__
   }
   const char* Ab = (const char*)A;
   const char* Wb = (const char*)(W + (size_t)(EPI == FLS_EPI_SWIGLU ? n0 / 2 : n0) * ldw);
+  const __amdgpu_buffer_rsrc_t rA = make_rsrc(Ab);
+  const __amdgpu_buffer_rsrc_t rW = make_rsrc(Wb);
+// LDS-DMA of one 1 KiB piece: buffer_load ... lds with the per-lane 32-bit offset and the K (and
+// half-tile) step in soffset (0.5-1% over the global_load_lds form, profiles/r2_gemm)
+#define V10_DMA_X(k0, idx, dst)                                                                    \
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (LDS_AS void*)(dst), 16, xo[idx], (k0) * 2, 0, 0)
+#define V10_DMA_W(hb, i, k0, dst)                                                                  \
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (LDS_AS void*)(dst), 16,                             \
+      EPI == FLS_EPI_SWIGLU ? wo[(hb) * 4 + (i)] : wo[(i)],                                         \
+      (EPI == FLS_EPI_SWIGLU ? 0u : (unsigned)((hb) * wb_off)) + (k0) * 2, 0, 0)
 #define V10_X(buf, hb, k0)                                                                         \
   _Pragma("unroll") for (int i_ = 0; i_ < 4; ++i_)                                                \
-    glds16(Ab + (size_t)(k0) * 2 + xo[(hb) * 4 + i_], smem + (buf) * BUF + (prow[i_] + (hb) * 64) * 128);
+    V10_DMA_X(k0, (hb) * 4 + i_, smem + (buf) * BUF + (prow[i_] + (hb) * 64) * 128);
 #define V10_W(buf, hb, k0)                                                                         \
   _Pragma("unroll") for (int i_ = 0; i_ < 4; ++i_)                                                \
-    glds16(FLS_W_SRC(hb, i_, k0), smem + (buf) * BUF + WIMG + (prow[i_] + (hb) * 64) * 128);
+    V10_DMA_W(hb, i_, k0, smem + (buf) * BUF + WIMG + (prow[i_] + (hb) * 64) * 128);
 
   const int wm = wave >> 1, wn = wave & 1;
   const int fr = lane & 15, grp = lane >> 4;
@@ -686,11 +702,9 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_v10(const half_t* __restrict__
       if (i_ >= 17 && i_ <= 26 && (i_ - 17) % 3 == 0) {                                           \
         const int p_ = (i_ - 17) / 3;                                                             \
         if (DX)                                                                                   \
-          glds16(Ab + (size_t)(dk0) * 2 + xo[(dhb) * 4 + p_],                                     \
-                 smem + (dbuf) * BUF + (prow[p_] + (dhb) * 64) * 128);                            \
+          V10_DMA_X(dk0, (dhb) * 4 + p_, smem + (dbuf) * BUF + (prow[p_] + (dhb) * 64) * 128);    \
         else                                                                                      \
-          glds16(FLS_W_SRC(dhb, p_, dk0),                                                         \
-                 smem + (dbuf) * BUF + WIMG + (prow[p_] + (dhb) * 64) * 128);                     \
+          V10_DMA_W(dhb, p_, dk0, smem + (dbuf) * BUF + WIMG + (prow[p_] + (dhb) * 64) * 128);    \
       }                                                                                           \
     }                                                                                             \
     if (SYNC) {                                                                                   \
@@ -736,6 +750,8 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_v10(const half_t* __restrict__
 #undef V10_RX
 #undef V10_W
 #undef V10_X
+#undef V10_DMA_X
+#undef V10_DMA_W
 
   epilogue_quadrant<EPI>(C, ldc, M, m0 + wm * 128 + fr, n0 + wn * 128, grp, acc, ep);
 }
@@ -749,7 +765,7 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_v10(const half_t* __restrict__
 // Here the next tile's 2-stage prologue DMA is issued BEFORE the current tile's
 // epilogue, so the HBM/L2 latency of the first K-tiles overlaps the epilogue's loads
 // and stores.  Main loop identical to v10 (the same V10_PHASE body).
-template <int EPI, int GM = 8>
+template <int EPI>
 __global__ __launch_bounds__(256, 1) void gemm_nt_v13(const half_t* __restrict__ A, const half_t* __restrict__ W,
                                                     half_t* __restrict__ C, int M, int N, int K, int lda, int ldw,
                                                     int ldc, Epi ep) {
@@ -767,24 +783,8 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_v13(const half_t* __restrict__
   {                                                                                                 \
     const int xcd_ = (v) & 7, loc_ = (v) >> 3;                                                      \
     const int b_ = (xcd_ < r8 ? xcd_ * (q8 + 1) : r8 * (q8 + 1) + (xcd_ - r8) * q8) + loc_;         \
-    int tm_, tn_;                                                                                   \
-    if (GM > 0) {                                                                                   \
-      constexpr int GROUP_M = GM > 0 ? GM : 1;                                                      \
-      const int group_ = b_ / (GROUP_M * tiles_n);                                                  \
-      const int first_ = group_ * GROUP_M;                                                          \
-      const int gsz_ = min(tiles_m - first_, GROUP_M);                                              \
-      const int in_ = b_ - group_ * GROUP_M * tiles_n;                                              \
-      tm_ = first_ + in_ % gsz_;                                                                    \
-      tn_ = in_ / gsz_;                                                                             \
-    } else {                                                                                        \
-      constexpr int GROUP_N = GM < 0 ? -GM : 1;                                                     \
-      const int group_ = b_ / (GROUP_N * tiles_m);                                                  \
-      const int first_ = group_ * GROUP_N;                                                          \
-      const int gsz_ = min(tiles_n - first_, GROUP_N);                                              \
-      const int in_ = b_ - group_ * GROUP_N * tiles_m;                                              \
-      tn_ = first_ + in_ % gsz_;                                                                    \
-      tm_ = in_ / gsz_;                                                                             \
-    }                                                                                               \
+    const int2 tmn_ = tile_of(b_, tiles_m, tiles_n, ep.order);                                      \
+    const int tm_ = tmn_.x, tn_ = tmn_.y;                                                           \
     m0 = tm_ * BM;                                                                                  \
     n0 = tn_ * BN;                                                                                  \
   }
@@ -813,6 +813,8 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_v13(const half_t* __restrict__
   }
   const char* Ab = (const char*)A;
   const char* Wb;
+  const __amdgpu_buffer_rsrc_t rA = make_rsrc(Ab);
+  __amdgpu_buffer_rsrc_t rW;
 #define V13_SETUP()                                                                                 \
   {                                                                                                 \
     _Pragma("unroll") for (int i_ = 0; i_ < 4; ++i_) {                                              \
@@ -820,7 +822,14 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_v13(const half_t* __restrict__
       xo[4 + i_] = (unsigned)(min(m0 + prow[i_] + 64 + lr, M - 1) * lda + lc * 8) * 2u;             \
     }                                                                                               \
     Wb = (const char*)(W + (size_t)(EPI == FLS_EPI_SWIGLU ? n0 / 2 : n0) * ldw);                    \
+    rW = make_rsrc(Wb);                                                                             \
   }
+#define V10_DMA_X(k0, idx, dst)                                                                    \
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (LDS_AS void*)(dst), 16, xo[idx], (k0) * 2, 0, 0)
+#define V10_DMA_W(hb, i, k0, dst)                                                                  \
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rW, (LDS_AS void*)(dst), 16,                             \
+      EPI == FLS_EPI_SWIGLU ? wo[(hb) * 4 + (i)] : wo[(i)],                                         \
+      (EPI == FLS_EPI_SWIGLU ? 0u : (unsigned)((hb) * wb_off)) + (k0) * 2, 0, 0)
 #define V10_X(buf, hb, k0)                                                                         \
   _Pragma("unroll") for (int i_ = 0; i_ < 4; ++i_)                                                \
     glds16(Ab + (size_t)(k0) * 2 + xo[(hb) * 4 + i_], smem + (buf) * BUF + (prow[i_] + (hb) * 64) * 128);
@@ -920,25 +929,26 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_v13(const half_t* __restrict__
 #undef V10_RX
 #undef V10_W
 #undef V10_X
+#undef V10_DMA_X
+#undef V10_DMA_W
 #undef V13_SETUP
 #undef V13_TILE
 }
 #undef FLS_W_SRC
 
 int g_variant = 10;          // 10: v10 (RoPE on v13 when g_rope_persistent); 13: every epilogue on v13
-int g_order = 0;             // 0: by shape, else a fixed GM (fls_gemm_set_order)
+int g_order = 0;             // 0: by shape, else a fixed signed group size (fls_gemm_set_order)
 int g_rope_persistent = 1;   // QKV + RoPE GEMMs on the persistent v13 (fls_gemm_set_rope_persistent)
 int g_mid = 1;               // mid-M kernel on (fls_gemm_set_mid)
 
-template <int EPI, int GM>
+template <int EPI>
 void launch_main(bool persistent, int tiles, const half_t* A, const half_t* W, half_t* C, int M, int N, int K,
                  int lda, int ldw, int ldc, const Epi& ep, hipStream_t s) {
   if (persistent) {
     static bool attr = false;
     static int ncu = 256;
     if (!attr) {
-      (void)hipFuncSetAttribute((const void*)gemm_nt_v13<EPI, GM>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                2 * BUF);
+      (void)hipFuncSetAttribute((const void*)gemm_nt_v13<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BUF);
       int dev = 0, n = 0;
       if (hipGetDevice(&dev) == hipSuccess &&
           hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n >= 8)
@@ -946,18 +956,34 @@ void launch_main(bool persistent, int tiles, const half_t* A, const half_t* W, h
       attr = true;
     }
     const int grid = tiles < ncu ? tiles : ncu;
-    hipLaunchKernelGGL((gemm_nt_v13<EPI, GM>), dim3(grid), dim3(256), 2 * BUF, s, A, W, C, M, N, K, lda, ldw, ldc,
-                       ep);
+    hipLaunchKernelGGL((gemm_nt_v13<EPI>), dim3(grid), dim3(256), 2 * BUF, s, A, W, C, M, N, K, lda, ldw, ldc, ep);
   } else {
     static bool attr = false;
     if (!attr) {
-      (void)hipFuncSetAttribute((const void*)gemm_nt_v10<EPI, GM>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                2 * BUF);
+      (void)hipFuncSetAttribute((const void*)gemm_nt_v10<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BUF);
       attr = true;
     }
-    hipLaunchKernelGGL((gemm_nt_v10<EPI, GM>), dim3(tiles), dim3(256), 2 * BUF, s, A, W, C, M, N, K, lda, ldw, ldc,
-                       ep);
+    hipLaunchKernelGGL((gemm_nt_v10<EPI>), dim3(tiles), dim3(256), 2 * BUF, s, A, W, C, M, N, K, lda, ldw, ldc, ep);
   }
+}
+
+// Default tile order (profiles/r2_gemm/README.md).  Groups of g tiles of one dimension are walked
+// along the other; the XCD remap gives XCD x the virtual ids [x*q, (x+1)*q), q = tiles / 8.
+//  * 4 <= g <= 8 keeps an XCD's 32 concurrent tiles a compact g x 32/g block (11-12 operand panels
+//    per K-step in its L2);
+//  * g dividing tiles/8 along the grouped dimension gives every XCD whole groups, so all XCDs walk
+//    the other operand in step and the MALL serves each of its panels to all 8 (N-grouped: the
+//    activations; each XCD keeps its own chunk of the weight).
+// Measured on the 70B shapes at 14k rows: N-grouped -4 (O, down, gate/up) and -5 (QKV) beat
+// round 1's fixed orders by 0.5-2.5% and the M-grouped lock-step order 7 by 1-2%.
+int auto_order(int tiles_m, int tiles_n) {
+  if (tiles_n % 8 == 0)
+    for (int g = 4; g <= 8; ++g)
+      if ((tiles_n / 8) % g == 0) return -g;
+  if (tiles_m % 8 == 0)
+    for (int g = 4; g <= 8; ++g)
+      if ((tiles_m / 8) % g == 0) return g;
+  return -4;
 }
 
 template <int EPI>
@@ -968,7 +994,11 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
   // 32-bit per-lane DMA offsets (X rows; SWIGLU up-block rows)
   const bool offs32 = (size_t)M * lda * 2 < (1ull << 32) &&
                       (EPI != FLS_EPI_SWIGLU || (size_t)(N / 2 + BN) * ldw * 2 < (1ull << 32));
-  const bool main_ok = N % BN == 0 && K % BK == 0 && (K / BK) % 2 == 0 && lda % 8 == 0 && ldw % 8 == 0 && offs32;
+  // the v10/v13 epilogues store (and load the residual) 16 B per lane
+  const bool wide_ok = ldc % 8 == 0 && ((uintptr_t)C & 15) == 0 &&
+                       (EPI != FLS_EPI_RESID || (ep.ldr % 8 == 0 && ((uintptr_t)ep.R & 15) == 0));
+  const bool main_ok = N % BN == 0 && K % BK == 0 && (K / BK) % 2 == 0 && lda % 8 == 0 && ldw % 8 == 0 && offs32 &&
+                       wide_ok;
   // Too few 256x256 tiles for 256 CUs -> 64x128 tiles.  Measured crossover (profiles/r1_gemm_mid):
   // the mid kernel wins below ~128 main tiles, and at M <= 64 (3/4 of every 256-row tile wasted)
   // up to 512; above that its lower L2 reuse (43 vs 128 FLOP per staged byte) costs more than the
@@ -998,14 +1028,12 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
   // tile's store acks (profiles/r1_gemm_persistent)
   const bool persistent = g_variant == 13 || (is_rope(EPI) && g_rope_persistent);
   const int tiles = (int)tiles256;
-  // tile order (profiles/r1_gemm_order): with few N tiles (o / down / qkv projections,
-  // N <= 16384) walking M inside groups of N tiles beats the M-grouped order by ~3-4%;
-  // the wide gate/up GEMM (N = 57344) keeps 8 M tiles per group
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = N / BN;
   int order = g_order;
-  if (order == 0) order = (N / BN <= 64) ? (K >= 16384 ? -4 : -8) : 8;
-  if (order == -4) launch_main<EPI, -4>(persistent, tiles, A, W, C, M, N, K, lda, ldw, ldc, ep, s);
-  else if (order == -8) launch_main<EPI, -8>(persistent, tiles, A, W, C, M, N, K, lda, ldw, ldc, ep, s);
-  else launch_main<EPI, 8>(persistent, tiles, A, W, C, M, N, K, lda, ldw, ldc, ep, s);
+  if (order == 0) order = auto_order(tiles_m, tiles_n);
+  Epi e = ep;
+  e.order = order;
+  launch_main<EPI>(persistent, tiles, A, W, C, M, N, K, lda, ldw, ldc, e, s);
   FLS_CHECK_LAUNCH();
   return 0;
 }
@@ -1014,9 +1042,8 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
 
 extern "C" int fls_kernels_version(void) { return 8; }
 
-// tile order: 0 = by shape (default), 8 = M-grouped, -4 / -8 = N-grouped (A/B, tests)
+// tile order: 0 = by shape (default); g > 0: groups of g M tiles; g < 0: groups of -g N tiles (A/B, tests)
 extern "C" int fls_gemm_set_order(int order) {
-  if (order != 0 && order != 8 && order != -4 && order != -8) return -1;
   const int old = g_order;
   g_order = order;
   return old;
@@ -1053,7 +1080,7 @@ extern "C" int fls_gemm(const void* A, const void* W, void* C, const void* R, in
   if ((epi == FLS_EPI_SWIGLU || epi == FLS_EPI_ROPE) && (N % 32)) return -2;
   if (epi == FLS_EPI_ROPE && ((head_dim != 64 && head_dim != 128) || rope_cols % head_dim || N % head_dim))
     return -3;
-  Epi ep{(const half_t*)R, ldr, pos, cos_t, sin_t, rope_cols, head_dim, (const half_t*)bias, N / 2};
+  Epi ep{(const half_t*)R, ldr, pos, cos_t, sin_t, rope_cols, head_dim, (const half_t*)bias, N / 2, 0};
   auto a = (const half_t*)A;
   auto w = (const half_t*)W;
   auto c = (half_t*)C;

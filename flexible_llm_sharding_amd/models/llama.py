@@ -167,6 +167,29 @@ def run_embed(ctx: ExecContext, W: Dict[str, torch.Tensor], meta: dict) -> torch
     return ctx.ops.embed(meta["ids"], W["embed"], ctx.act_dtype)
 
 
+def _pruned_qkv(ctx: ExecContext, W: Dict[str, torch.Tensor], h: torch.Tensor, meta: dict, T0: int) -> torch.Tensor:
+    """QKV of the pruned last decoder layer: K/V (+ RoPE on K) for every row, Q (+ RoPE) only for
+    the scored rows, scattered into the Q columns of those rows.  The other rows' Q columns are
+    left unwritten: the last layer's attention work items (``work_last``) query only scored rows.
+    Q is q_size / qkv_size of the projection (80% for Llama-2-70B)."""
+    cfg, ops = ctx.cfg, ctx.ops
+    qs, nq, nkv, hd = cfg.q_size, cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
+    qkv = ctx.scratch(T0, cfg.qkv_size)
+    if qkv is None:
+        qkv = torch.empty(T0, cfg.qkv_size, dtype=h.dtype, device=h.device)
+    w, b = W["wqkv"], W.get("bqkv")
+    kv_view = qkv[:, qs:]
+    kv = ops.qkv_rope(h, w[qs:], meta["positions"], ctx.cos, ctx.sin, 0, nkv, hd,
+                      bias=b[qs:] if b is not None else None, out=kv_view)
+    if kv.data_ptr() != kv_view.data_ptr():
+        kv_view.copy_(kv)
+    idx = meta["last_idx"]
+    q = ops.qkv_rope(h.index_select(0, idx), w[:qs], meta["positions"].index_select(0, idx), ctx.cos, ctx.sin,
+                     nq, 0, hd, bias=b[:qs] if b is not None else None)
+    qkv[:, :qs].index_copy_(0, idx if idx.dtype == torch.int64 else idx.long(), q)
+    return qkv
+
+
 def run_decoder(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, batch,
                 meta: dict, layer_name: str = "") -> torch.Tensor:
     """One pre-norm decoder block on the packed rows.  With ``prune`` (the last decoder
@@ -179,9 +202,12 @@ def run_decoder(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, b
     T0 = x.shape[0]
     ctx.phase((T0, cfg.hidden_size), (T0, cfg.qkv_size), (T0, cfg.q_size))
     h = ops.rmsnorm(x, W["ln1"], eps, out=ctx.scratch(T0, cfg.hidden_size))
-    qkv = ops.qkv_rope(h, W["wqkv"], meta["positions"], ctx.cos, ctx.sin,
-                       cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim, bias=W.get("bqkv"),
-                       out=ctx.scratch(T0, cfg.qkv_size))
+    if prune:
+        qkv = _pruned_qkv(ctx, W, h, meta, T0)
+    else:
+        qkv = ops.qkv_rope(h, W["wqkv"], meta["positions"], ctx.cos, ctx.sin,
+                           cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim, bias=W.get("bqkv"),
+                           out=ctx.scratch(T0, cfg.qkv_size))
     del h
     kv0 = None
     pe = ctx.prefix_entry

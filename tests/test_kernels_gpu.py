@@ -305,9 +305,9 @@ def test_gemm_variants_all_epilogues(ops, ref, var):
         ops.k.fls_gemm_set_mid(1)
 
 
-@pytest.mark.parametrize("order", [8, -4, -8])
+@pytest.mark.parametrize("order", [8, -4, -8, 1, -1, 2, 3, -5])
 def test_gemm_v10_tile_orders(ops, ref, order):
-    """v10 tile orders (M-grouped / N-grouped) only permute which block computes which tile:
+    """v10 tile orders (groups of M tiles / of N tiles, any size) only permute which block computes which tile:
     every epilogue gives the fp32 reference and the same bits as the default order."""
     M, N, K = 1100, 1536, 1024            # 5 x 6 tiles: ragged last M tile, groups split unevenly
     ops.k.fls_gemm_set_mid(0)
@@ -330,7 +330,7 @@ def test_gemm_v10_tile_orders(ops, ref, order):
         ops.k.fls_gemm_set_mid(1)
 
 
-@pytest.mark.parametrize("order", [8, -8])
+@pytest.mark.parametrize("order", [8, -8, 5, -3])
 def test_gemm_v13_persistent_matches_v10(ops, ref, order):
     """v13 (persistent v10: one block per CU walks several tiles, the next tile's prologue DMA
     issued before this tile's epilogue) computes every tile exactly as v10 does: same bits for
