@@ -69,10 +69,8 @@ enum { FLS_EPI_NONE = 0, FLS_EPI_RESID = 1, FLS_EPI_SWIGLU = 2, FLS_EPI_ROPE = 3
 int fls_gemm(const void* A, const void* W, void* C, const void* R, int M, int N, int K,
              int lda, int ldw, int ldc, int ldr, int epi, const int* pos, const float* cos_t,
              const float* sin_t, int rope_cols, int head_dim, const void* bias, fls_stream_t s);
-int fls_gemm_set_variant(int v);     // 10 (default) or 13 (every epilogue on the persistent kernel)
 int fls_gemm_set_order(int order);   // tile order: 0 by shape, 8 M-grouped, -4/-8 N-grouped
 int fls_gemm_set_mid(int on);   // 64x128-tile kernel for small / medium M (default on)
-int fls_gemm_set_rope_persistent(int on);   // RoPE GEMMs on the persistent v13 (default on)
 // shared-prefix / varlen flash attention over packed work items (int32 x8)
 int fls_attn_set_mha_v2(int on);   // odd GQA groups (MHA) on the v2/v3 kernel, one head per block
 int fls_attn_set_variant(int v);   // 1 = 16 rows/wave; 2 = 32 rows/wave + staged prefetch; 3 = 2 + double-buffered LDS (default)

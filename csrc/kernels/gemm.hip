@@ -12,13 +12,11 @@
 //   * gemm_nt_v10 — 256 x 256 x 64 tile, 4 waves (one per SIMD), each wave
 //     128 x 128 outputs in 256 AGPR accumulators (v_mfma_f32_16x16x32_f16: holds
 //     a higher clock than 32x32x16 on random data, guide §5.4 r28).  Operands
-//     staged global -> LDS by global_load_lds_dwordx4 (LDS-DMA) with the XOR
+//     staged global -> LDS by buffer_load_dwordx4 ... lds (LDS-DMA) with the XOR
 //     chunk swizzle on the per-lane SOURCE address (guide T2 / rule 21), three
 //     half-tile super-phases in flight, one counted vmcnt + raw s_barrier per
 //     two phases, LDS fragment reads and DMA interleaved into the MFMA stream.
 //     XCD-aware bijective block remap + grouped tile order (guide T1).
-//   * gemm_nt_v13 — persistent v10 (one block per CU walks its tiles; the next
-//     tile's prologue DMA is issued under this tile's epilogue).  Bit-identical.
 //   * gemm_nt_mid — 64 x 128 x 64 tiles, 3-deep LDS-DMA ring, for M too small
 //     to fill 256 CUs with 256 x 256 tiles, and for odd K-tile counts (v10's
 //     body is unrolled over two K-tiles).
@@ -26,7 +24,8 @@
 //
 // The MFMA computes C^T tiles (A operand = W fragment, B operand = X fragment)
 // so each lane holds 4 consecutive output columns of one row in each 16-column
-// subtile: 8-byte stores, and the epilogue partners live in the same lane:
+// subtile (v10 pairs neighbouring subtiles into 16-byte stores with one
+// v_permlane16_swap), and the epilogue partners live in the same lane:
 //   RESID : C = acc (+ bias) + R          (R may alias C: in-place residual)
 //   SWIGLU: W = [gate (I rows); up (I rows)] (HF gate_proj / up_proj stacked);
 //           the W-tile loader reads logical rows interleaved per 16 (gate rows
@@ -47,7 +46,7 @@ namespace {
 
 constexpr int BM = 256, BN = 256, BK = 64;
 // internal epilogue code: RoPE with head_dim 64 (FLS_EPI_ROPE inside this file means head_dim 128);
-// a compile-time head dim keeps the v10/v13 RoPE epilogue free of spills
+// a compile-time head dim keeps the v10 RoPE epilogue free of spills
 constexpr int EPI_ROPE64 = 4;
 constexpr bool is_rope(int epi) { return epi == FLS_EPI_ROPE || epi == EPI_ROPE64; }
 constexpr int BUF = 65536;    // one K-tile stage: X image (32 KiB) then W image (32 KiB)
@@ -63,7 +62,7 @@ struct Epi {
   int head_dim;
   const half_t* bias;   // optional per-output-column bias (Qwen2 q/k/v, Llama attention_bias), added first
   int gu_rows;          // SWIGLU: I (rows of gate = rows of up)
-  int order;            // v10/v13 tile order (tile_of), set by the launcher
+  int order;            // v10 tile order (tile_of), set by the launcher
 };
 
 // SWIGLU logical row l (gate/up interleaved per 16 rows) -> physical row of [gate; up]
@@ -159,7 +158,7 @@ __device__ __forceinline__ void unwide_pair(uint4 v, half4& a, half4& b) {
   b = __builtin_bit_cast(half4, uint2{r0[1], r1[1]});
 }
 
-// RoPE epilogue of a v10/v13 wave quadrant (128 rows x 128 columns = whole heads).
+// RoPE epilogue of a v10 wave quadrant (128 rows x 128 columns = whole heads).
 // HD 128: one head per wave, pairs (q, q+4); HD 64: two heads, pairs (q', q'+2),
 // q' in {0, 1, 4, 5}.  Neighbouring subtiles (q, q+1), q even, leave as 16-byte stores
 // (wide_pair).  Row group u+1's cos/sin loads are issued before row group u's stores (the
@@ -240,7 +239,7 @@ __device__ __forceinline__ void epilogue_rope(half_t* __restrict__ C, int ldc, i
   }
 }
 
-// Epilogue of a wave's 128 (M) x 128 (N) quadrant held as acc[8 row groups][8 subtiles] (v10/v13),
+// Epilogue of a wave's 128 (M) x 128 (N) quadrant held as acc[8 row groups][8 subtiles] (v10),
 // 16-byte stores throughout (wide_pair).  Row group u+1's operand loads (residual rows) are issued
 // before row group u's stores (different rows, so in-place R == C stays correct); the per-column
 // bias is loaded once.
@@ -554,12 +553,6 @@ __global__ __launch_bounds__(mid::NTm) void gemm_nt_mid(const half_t* __restrict
 // W-operand source addresses are per 8-row piece, so the SWIGLU loader can map the
 // logical (gate/up interleaved) tile rows onto the stacked [gate; up] weight.
 
-// W-tile DMA source of piece i of half-tile hb at K offset k0 (the non-SWIGLU form keeps the
-// half-tile step in the scalar base: saddr + voffset addressing, no per-lane adds)
-#define FLS_W_SRC(hb, i, k0)                                                                      \
-  (EPI == FLS_EPI_SWIGLU ? Wb + (size_t)(k0) * 2 + wo[(hb) * 4 + (i)]                             \
-                         : Wb + (hb) * wb_off + (size_t)(k0) * 2 + wo[(i)])
-
 // Virtual tile id -> (tm, tn).  order > 0: groups of `order` M tiles walked M-fastest along N;
 // order < 0: groups of -order N tiles walked N-fastest along M.  With the XCD-aware remap
 // (virtual ids [x*q, (x+1)*q) run on XCD x) a group of tiles/8 makes each XCD own one chunk of
@@ -761,218 +754,20 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_v10(const half_t* __restrict__
   epilogue_quadrant<EPI>(C, ldc, M, m0 + wm * 128 + fr, n0 + wn * 128, grp, acc, ep);
 }
 
-// ------------------------------------------------------------------ v13
-// Persistent v10: the grid is one block per CU (multiple of 8, so virtual tile id
-// v = blockIdx.x + i * gridDim.x stays on the XCD that v10's remap assumes) and each
-// block walks its tiles in the same remapped / grouped order as v10.  With one
-// block per CU (256 AGPR accumulators, 128 KiB LDS) v10 leaves the CU idle while a
-// tile's epilogue stores drain and while the next block's first K-tiles are in flight.
-// Here the next tile's 2-stage prologue DMA is issued BEFORE the current tile's
-// epilogue, so the HBM/L2 latency of the first K-tiles overlaps the epilogue's loads
-// and stores.  Main loop identical to v10 (the same V10_PHASE body).
-template <int EPI>
-__global__ __launch_bounds__(256, 1) void gemm_nt_v13(const half_t* __restrict__ A, const half_t* __restrict__ W,
-                                                    half_t* __restrict__ C, int M, int N, int K, int lda, int ldw,
-                                                    int ldc, Epi ep) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-
-  const int tiles_m = (M + BM - 1) / BM;
-  const int tiles_n = N / BN;
-  const int ntiles = tiles_m * tiles_n;
-  const int q8 = ntiles >> 3, r8 = ntiles & 7;
-  int m0, n0;
-#define V13_TILE(v)                                                                                 \
-  {                                                                                                 \
-    const int xcd_ = (v) & 7, loc_ = (v) >> 3;                                                      \
-    const int b_ = (xcd_ < r8 ? xcd_ * (q8 + 1) : r8 * (q8 + 1) + (xcd_ - r8) * q8) + loc_;         \
-    const int2 tmn_ = tile_of(b_, tiles_m, tiles_n, ep.order);                                      \
-    const int tm_ = tmn_.x, tn_ = tmn_.y;                                                           \
-    m0 = tm_ * BM;                                                                                  \
-    n0 = tn_ * BN;                                                                                  \
-  }
-
-  const int lr = lane >> 3;
-  const int lc = (lane & 7) ^ lr;
-  int prow[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int j = 4 * wave + i;
-    prow[i] = (j >> 3) * 128 + (j & 7) * 8;
-  }
-  unsigned xo[8], wo[8];
-  const size_t wb_off = (size_t)64 * ldw * 2;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    if constexpr (EPI == FLS_EPI_SWIGLU) {
-#pragma unroll
-      for (int hb = 0; hb < 2; ++hb) {
-        const int l = prow[i] + hb * 64;
-        wo[hb * 4 + i] = (unsigned)((((l >> 4) & 1) * ep.gu_rows + (l >> 5) * 16 + (l & 15) + lr) * ldw + lc * 8) * 2u;
-      }
-    } else {
-      wo[i] = (unsigned)((prow[i] + lr) * ldw + lc * 8) * 2u;
-    }
-  }
-  const char* Ab = (const char*)A;
-  const char* Wb;
-  const __amdgpu_buffer_rsrc_t rA = make_rsrc(Ab);
-  const __amdgpu_buffer_rsrc_t rZ = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(Ab), (short)0, 0, 0x00020000);
-  __amdgpu_buffer_rsrc_t rW;
-#define V13_SETUP()                                                                                 \
-  {                                                                                                 \
-    _Pragma("unroll") for (int i_ = 0; i_ < 4; ++i_) {                                              \
-      xo[i_] = (unsigned)(min(m0 + prow[i_] + lr, M - 1) * lda + lc * 8) * 2u;                      \
-      xo[4 + i_] = (unsigned)(min(m0 + prow[i_] + 64 + lr, M - 1) * lda + lc * 8) * 2u;             \
-    }                                                                                               \
-    Wb = (const char*)(W + (size_t)(EPI == FLS_EPI_SWIGLU ? n0 / 2 : n0) * ldw);                    \
-    rW = make_rsrc(Wb);                                                                             \
-  }
-#define V10_DMA_X(rs, k0, idx, dst)                                                                \
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_AS void*)(dst), 16, xo[idx], (k0) * 2, 0, 0)
-#define V10_DMA_W(rs, hb, i, k0, dst)                                                              \
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (LDS_AS void*)(dst), 16,                             \
-      EPI == FLS_EPI_SWIGLU ? wo[(hb) * 4 + (i)] : wo[(i)],                                         \
-      (EPI == FLS_EPI_SWIGLU ? 0u : (unsigned)((hb) * wb_off)) + (k0) * 2, 0, 0)
-#define V10_X(buf, hb, k0)                                                                         \
-  _Pragma("unroll") for (int i_ = 0; i_ < 4; ++i_)                                                \
-    glds16(Ab + (size_t)(k0) * 2 + xo[(hb) * 4 + i_], smem + (buf) * BUF + (prow[i_] + (hb) * 64) * 128);
-#define V10_W(buf, hb, k0)                                                                         \
-  _Pragma("unroll") for (int i_ = 0; i_ < 4; ++i_)                                                \
-    glds16(FLS_W_SRC(hb, i_, k0), smem + (buf) * BUF + WIMG + (prow[i_] + (hb) * 64) * 128);
-
-  const int wm = wave >> 1, wn = wave & 1;
-  const int fr = lane & 15, grp = lane >> 4;
-  const int sw = fr & 7;
-  const int c0 = ((0 + grp) ^ sw) << 4;
-  const int c1 = ((4 + grp) ^ sw) << 4;
-  const int xrow = (wm * 128 + fr) * 128;
-  const int wrow = WIMG + (wn * 128 + fr) * 128;
-
-  floatx4 acc[8][8];
-  half8 xf[8][2], wf[8][2];
-#define V13_FENCE_ACC()                                                                            \
-  _Pragma("unroll") for (int u_ = 0; u_ < 8; ++u_)                                                \
-  _Pragma("unroll") for (int t_ = 0; t_ < 8; ++t_) asm volatile("" : "+a"(acc[u_][t_]));
-#define V10_RX(buf, h)                                                                             \
-  _Pragma("unroll") for (int u_ = (h) * 4; u_ < (h) * 4 + 4; ++u_) {                              \
-    xf[u_][0] = *(const half8*)(smem + (buf) * BUF + xrow + u_ * 2048 + c0);                      \
-    xf[u_][1] = *(const half8*)(smem + (buf) * BUF + xrow + u_ * 2048 + c1);                      \
-  }
-#define V10_RW(buf, h)                                                                             \
-  _Pragma("unroll") for (int t_ = (h) * 4; t_ < (h) * 4 + 4; ++t_) {                              \
-    wf[t_][0] = *(const half8*)(smem + (buf) * BUF + wrow + t_ * 2048 + c0);                      \
-    wf[t_][1] = *(const half8*)(smem + (buf) * BUF + wrow + t_ * 2048 + c1);                      \
-  }
-
-  const int nk = K / BK;                       // even (host-checked)
-  const int kc1 = min(1, nk - 1) * BK;
-#define V13_PROLOGUE_DMA()                                                                         \
-  V10_X(0, 0, 0); V10_W(0, 0, 0); V10_W(0, 1, 0); V10_X(0, 1, 0);                                 \
-  V10_X(1, 0, kc1); V10_W(1, 1, kc1); V10_W(1, 0, kc1); V10_X(1, 1, kc1);
-
-  int v = blockIdx.x;
-  V13_TILE(v);
-  V13_SETUP();
-  V13_PROLOGUE_DMA();
-  bool first = true;
-  while (true) {
-    if (first) {
-      asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-    } else {
-      // the prologue DMA was issued before the previous tile's epilogue loads / stores:
-      // vmcnt cannot count it apart from them
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-#pragma unroll
-    for (int u = 0; u < 8; ++u)
-#pragma unroll
-      for (int t = 0; t < 8; ++t) acc[u][t] = floatx4{0.f, 0.f, 0.f, 0.f};
-    V13_FENCE_ACC();
-    V10_RX(0, 0); V10_RW(0, 0);                // SP -1's reads: x0(0), w0(0)
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    // zero-init (VALU AGPR writes) must not sit right before the first asm MFMA reading them
-    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
-    for (int kt = 0; kt < nk; kt += 2) {
-      const int ka = min(kt + 2, nk - 1) * BK;
-      const int kb = min(kt + 3, nk - 1) * BK;
-      const __amdgpu_buffer_rsrc_t rXka = kt + 2 < nk ? rA : rZ, rWka = kt + 2 < nk ? rW : rZ;
-      const __amdgpu_buffer_rsrc_t rXkb = kt + 3 < nk ? rA : rZ, rWkb = kt + 3 < nk ? rW : rZ;
-      V10_PHASE(0, 0, 0, 0, 1, 1, 0, 0, ka, 0);
-      V10_PHASE(0, 1, 1, 0, 1, 0, 0, 0, ka, 1);
-      V10_PHASE(1, 1, 1, 1, 0, 0, 0, 1, ka, 0);
-      V10_PHASE(1, 0, 0, 1, 1, 1, 0, 1, ka, 1);
-      V10_PHASE(0, 1, 0, 1, 0, 1, 1, 0, kb, 0);
-      V10_PHASE(0, 0, 1, 1, 1, 0, 1, 1, kb, 1);
-      V10_PHASE(1, 0, 1, 0, 0, 0, 1, 0, kb, 0);
-      V10_PHASE(1, 1, 0, 0, 0, 1, 1, 1, kb, 1);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-    V13_FENCE_ACC();
-    const int em0 = m0, en0 = n0;
-    v += gridDim.x;
-    const bool more = v < ntiles;              // block-uniform
-    if (more) {
-      // every wave's LDS reads (lgkmcnt(0) before the last phase's barrier) and DMA
-      // (vmcnt(0) above) of this tile are complete once all waves pass this barrier
-      __builtin_amdgcn_s_barrier();
-      V13_TILE(v);
-      V13_SETUP();
-      V13_PROLOGUE_DMA();
-    }
-    epilogue_quadrant<EPI>(C, ldc, M, em0 + wm * 128 + fr, en0 + wn * 128, grp, acc, ep);
-    if (!more) break;
-    first = false;
-  }
-#undef V13_PROLOGUE_DMA
-#undef V13_FENCE_ACC
 #undef V10_PHASE
-#undef V10_RW
-#undef V10_RX
-#undef V10_W
-#undef V10_X
-#undef V10_DMA_X
-#undef V10_DMA_W
-#undef V13_SETUP
-#undef V13_TILE
-}
-#undef FLS_W_SRC
 
-int g_variant = 10;          // 10: v10 (RoPE on v13 when g_rope_persistent); 13: every epilogue on v13
 int g_order = 0;             // 0: by shape, else a fixed signed group size (fls_gemm_set_order)
-int g_rope_persistent = 1;   // QKV + RoPE GEMMs on the persistent v13 (fls_gemm_set_rope_persistent)
 int g_mid = 1;               // mid-M kernel on (fls_gemm_set_mid)
 
 template <int EPI>
-void launch_main(bool persistent, int tiles, const half_t* A, const half_t* W, half_t* C, int M, int N, int K,
-                 int lda, int ldw, int ldc, const Epi& ep, hipStream_t s) {
-  if (persistent) {
-    static bool attr = false;
-    static int ncu = 256;
-    if (!attr) {
-      (void)hipFuncSetAttribute((const void*)gemm_nt_v13<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BUF);
-      int dev = 0, n = 0;
-      if (hipGetDevice(&dev) == hipSuccess &&
-          hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n >= 8)
-        ncu = n & ~7;                            // a multiple of 8: virtual tile ids keep their XCD
-      attr = true;
-    }
-    const int grid = tiles < ncu ? tiles : ncu;
-    hipLaunchKernelGGL((gemm_nt_v13<EPI>), dim3(grid), dim3(256), 2 * BUF, s, A, W, C, M, N, K, lda, ldw, ldc, ep);
-  } else {
-    static bool attr = false;
-    if (!attr) {
-      (void)hipFuncSetAttribute((const void*)gemm_nt_v10<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BUF);
-      attr = true;
-    }
-    hipLaunchKernelGGL((gemm_nt_v10<EPI>), dim3(tiles), dim3(256), 2 * BUF, s, A, W, C, M, N, K, lda, ldw, ldc, ep);
+void launch_main(int tiles, const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int lda, int ldw,
+                 int ldc, const Epi& ep, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_nt_v10<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * BUF);
+    attr = true;
   }
+  hipLaunchKernelGGL((gemm_nt_v10<EPI>), dim3(tiles), dim3(256), 2 * BUF, s, A, W, C, M, N, K, lda, ldw, ldc, ep);
 }
 
 // Default tile order (profiles/r2_gemm/README.md).  Groups of g tiles of one dimension are walked
@@ -1002,7 +797,7 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
   // 32-bit per-lane DMA offsets (X rows; SWIGLU up-block rows)
   const bool offs32 = (size_t)M * lda * 2 < (1ull << 32) &&
                       (EPI != FLS_EPI_SWIGLU || (size_t)(N / 2 + BN) * ldw * 2 < (1ull << 32));
-  // the v10/v13 epilogues store (and load the residual) 16 B per lane
+  // the v10 epilogues store (and load the residual) 16 B per lane
   const bool wide_ok = ldc % 8 == 0 && ((uintptr_t)C & 15) == 0 &&
                        (EPI != FLS_EPI_RESID || (ep.ldr % 8 == 0 && ((uintptr_t)ep.R & 15) == 0));
   const bool main_ok = N % BN == 0 && K % BK == 0 && (K / BK) % 2 == 0 && lda % 8 == 0 && ldw % 8 == 0 && offs32 &&
@@ -1030,25 +825,23 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
     FLS_CHECK_LAUNCH();
     return 0;
   }
-  // The persistent v13 (bit-identical to v10) pays off only where the epilogue is heavy enough to
-  // hide the next tile's prologue under it: QKV + RoPE 2.23 -> 2.12 ms on the 70B shape, while the
-  // store-only / residual epilogues lose 1-2% to the vmcnt(0) that also waits for the previous
-  // tile's store acks (profiles/r1_gemm_persistent)
-  const bool persistent = g_variant == 13 || (is_rope(EPI) && g_rope_persistent);
+  // One block per tile, dispatched by the hardware as CUs free up.  A persistent form (one block
+  // per CU walking its tiles, the next tile's prologue DMA under this tile's epilogue) measured
+  // 1.1-3.9% slower on every 70B / 7B shape once the tile order was XCD-aware (profiles/r2_gemm).
   const int tiles = (int)tiles256;
   const int tiles_m = (M + BM - 1) / BM, tiles_n = N / BN;
   int order = g_order;
   if (order == 0) order = auto_order(tiles_m, tiles_n);
   Epi e = ep;
   e.order = order;
-  launch_main<EPI>(persistent, tiles, A, W, C, M, N, K, lda, ldw, ldc, e, s);
+  launch_main<EPI>(tiles, A, W, C, M, N, K, lda, ldw, ldc, e, s);
   FLS_CHECK_LAUNCH();
   return 0;
 }
 
 }  // namespace
 
-extern "C" int fls_kernels_version(void) { return 8; }
+extern "C" int fls_kernels_version(void) { return 9; }
 
 // tile order: 0 = by shape (default); g > 0: groups of g M tiles; g < 0: groups of -g N tiles (A/B, tests)
 extern "C" int fls_gemm_set_order(int order) {
@@ -1057,26 +850,10 @@ extern "C" int fls_gemm_set_order(int order) {
   return old;
 }
 
-// RoPE GEMMs on the persistent v13 kernel (1, default) or on v10 (0): with RCCL kernels co-running
-// (multi-GPU) a persistent block displaced by an RCCL block would run its whole tile list late
-extern "C" int fls_gemm_set_rope_persistent(int on) {
-  const int old = g_rope_persistent;
-  g_rope_persistent = on ? 1 : 0;
-  return old;
-}
-
 // mid-M kernel for small grids on (1, default) or off (0; tests)
 extern "C" int fls_gemm_set_mid(int on) {
   const int old = g_mid;
   g_mid = on ? 1 : 0;
-  return old;
-}
-
-// main-kernel variant: 10 (v10, RoPE on v13 per fls_gemm_set_rope_persistent) or 13 (all on v13)
-extern "C" int fls_gemm_set_variant(int v) {
-  if (v != 10 && v != 13) return -1;
-  const int old = g_variant;
-  g_variant = v;
   return old;
 }
 

@@ -106,11 +106,6 @@ class ShardedRunner:
         mha = (cfg.num_attention_heads // cfg.num_key_value_heads) % 2 == 1
         self.q_block = Q_BLOCK_MHA if (self.cuda and mha) else Q_BLOCK
         self.ops = get_ops(self.dev)
-        if self.cuda and self.comm.world > 1 and not (data_parallel and resident) and hasattr(self.ops, "k"):
-            # RCCL all-gather / send-recv kernels co-run with compute here. The persistent RoPE GEMM (v13)
-            # runs one block per CU, so a block displaced by an RCCL block would run its whole tile list
-            # after the rest: the QKV GEMMs go to the non-persistent v10 instead (bit-identical results).
-            self.ops.k.fls_gemm_set_rope_persistent(int(os.environ.get("FLS_ROPE_PERSISTENT", "0")))
         cos, sin = rope_tables(cfg, max(cfg.max_position_embeddings, max_token_len),
                                torch.float16, self.dev)
         self.ctx = ExecContext(cfg, self.ops, self.dev, self.act_dtype, cos, sin, mlp_chunk)

@@ -1,4 +1,6 @@
-"""Run one GEMM shape for profiling (rocprofv3 --pmc): python scripts/gemm_one.py VARIANT [M N K] [iters]"""
+"""Run one GEMM shape for profiling (rocprofv3 --pmc): python scripts/gemm_one.py WHICH [M N K] [iters]
+
+WHICH >= 0: the hand-written v10 kernel; < 0: hipBLASLt (torch.matmul) for comparison."""
 import os
 import sys
 
@@ -14,8 +16,6 @@ def main():
     iters = int(sys.argv[5]) if len(sys.argv) >= 6 else 10
     dev = torch.device("cuda", 0)
     ops = HipOps()
-    if var >= 0:
-        ops.k.fls_gemm_set_variant(var)
     x = (torch.rand(M, K, device=dev) * 2 - 1).half()
     w = ((torch.rand(N, K, device=dev) * 2 - 1) * 0.02).half()
     out = torch.empty(M, N, dtype=torch.float16, device=dev)

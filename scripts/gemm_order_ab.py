@@ -1,4 +1,4 @@
-"""A/B of v10/v13 tile orders on the 70B projection GEMMs with their fused epilogues
+"""A/B of v10 tile orders on the 70B projection GEMMs with their fused epilogues
 (interleaved rounds, median of 3).   python scripts/gemm_order_ab.py [--m 14336] [--orders 0,-8,8,-4]
 
 order 0 = the launcher's default (each XCD owns 1/8 of the smaller tile dimension);
