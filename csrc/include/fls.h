@@ -71,13 +71,15 @@ int fls_gemm(const void* A, const void* W, void* C, const void* R, int M, int N,
              const float* sin_t, int rope_cols, int head_dim, const void* bias, fls_stream_t s);
 int fls_gemm_set_order(int order);   // tile order: 0 by shape, 8 M-grouped, -4/-8 N-grouped
 int fls_gemm_set_mid(int on);   // 64x128-tile kernel for small / medium M (default on)
-// shared-prefix / varlen flash attention over packed work items (int32 x8)
-int fls_attn_set_mha_v2(int on);   // odd GQA groups (MHA) on the v2/v3 kernel, one head per block
-int fls_attn_set_variant(int v);   // 1 = 16 rows/wave; 2 = 32 rows/wave + staged prefetch; 3 = 2 + double-buffered LDS (default)
-// kv0 (optional, [P, 2*n_kv*hd] K then V, row stride ld_kv0): range 0 of every work item indexes it
+// shared-prefix / varlen flash attention over packed work items (int32 x8:
+// q_start q_len q_off r0_start r0_len r0_causal r1_start r1_len).
+// kv0 (optional, [P, 2*n_kv*hd] K then V, row stride ld_kv0): range 0 of every work item indexes it.
+// seg_lo (optional, [T] int32): first packed row of the suffix holding each row; range-1 key j is
+// visible to query row i iff seg_lo[i] <= j <= i, so an item may hold several suffixes of a prompt
+// (null: one suffix per item).  q_block: rows per work item (64 or 128).
 int fls_attention(const void* qkv, void* out, const int* work, int n_items, int n_q_heads,
                   int n_kv_heads, int head_dim, int ld_qkv, int ld_out, float scale, const void* kv0,
-                  int ld_kv0, int q_block, fls_stream_t s);   // q_block: rows per work item (64 or 128)
+                  int ld_kv0, const int* seg_lo, int q_block, fls_stream_t s);
 int fls_rmsnorm(const void* x, const void* w, void* y, const int* row_idx, int rows, int H,
                 int ldx, int ldy, float eps, fls_stream_t s);
 int fls_embed(const int* ids, const void* table, void* out, int T, int H, int V, fls_stream_t s);

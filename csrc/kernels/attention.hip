@@ -5,31 +5,44 @@
 // repeat_kv'd to every query head — materialised n_s * (nh/nkv) times — and a
 // [1, nh, Lp, Lp] fp32 probability matrix.
 //
-// Here K/V are read IN PLACE from the packed QKV activation: a work item is
-// a block of <= 64 query rows of one segment plus up to two key ranges
-//   range 0: the prompt's prefix (bidirectional, or causal for prefix queries
-//            in --prefix_attention causal),
-//   range 1: the suffix's own tokens, causal (key j visible to query i iff j <= i),
-// so every suffix of a prompt reads the single shared prefix K/V, GQA-native
-// (query head h uses kv head h / (nh/nkv)).
+// Here K/V are read IN PLACE from the packed QKV activation.  A work item
+// (runtime/batch.py) is a block of <= q_block query rows plus up to two key ranges
+//   range 0: the prompt's shared prefix (bidirectional, or causal for prefix
+//            queries in --prefix_attention causal),
+//   range 1: suffix rows, causal and block-diagonal: key j is visible to query
+//            row i iff seg_lo[i] <= j <= i (packed rows; seg_lo = first row of
+//            the suffix holding row i),
+// so one item can hold several suffixes of one prompt and they all read the
+// prompt's single prefix K/V in the same pass (GQA-native: query head h uses
+// kv head h / (nh/nkv)).  Without seg_lo an item's range 1 is one suffix.
 //
-// Structure (4 waves x 16 query rows; K/V tiles of 64 keys in LDS):
+// Block: HPB query heads of one KV group x WPH waves of 32 query rows each
+// (q_block = 32 * WPH); every K/V tile staged in LDS feeds HPB * WPH waves.
 //   * S^T = K . Q^T with v_mfma_f32_16x16x32_f16 (A = K fragment from LDS,
-//     B = Q fragment in registers), so each lane owns ONE query row's scores:
-//     the online-softmax max/sum needs only 2 cross-lane xor steps and the
-//     P fragment for the next MFMA is lane-local (no LDS round trip);
-//   * O^T += V^T . P^T: the V^T operand comes from ds_read_b64_tr_b16
-//     (hardware transpose read, guide T10) of a row-major, XOR-swizzled V
-//     tile; O^T keeps the query on the lane too, so rescaling by
-//     exp2(m_old - m_new) is lane-local;
-//   * K tile XOR-swizzled per 16-byte chunk for conflict-free ds_read_b128.
+//     B = Q fragment in registers): each lane owns one query row's 16 scores
+//     of a 64-key tile, so the row max is in-lane + two permlane swaps and the
+//     P fragment of the next MFMA is lane-local;
+//   * O^T += V^T . P^T with V^T from ds_read_b64_tr_b16 (hardware transpose
+//     read) of a row-major, XOR-swizzled V tile; K tile XOR-swizzled per
+//     16-byte chunk for conflict-free ds_read_b128;
+//   * K/V tiles register-staged (32-bit buffer loads issued one tile ahead,
+//     written to the other LDS buffer after the tile's MFMAs): one barrier per
+//     tile (guide T14);
+//   * softmax VALU work kept off the MFMA critical path: raw scores (the scale
+//     folds into one FMA per score before the exp), masking only on boundary
+//     tiles (wave-uniform branch), max3 chains without canonicalisation, and a
+//     deferred rescale (guide T13): O and l are rescaled only when a row's max
+//     grows by more than 2^8, otherwise P is taken against the old max
+//     (P <= 256: exact range in fp16; O and l accumulate in fp32).
+// Measured (profiles/r2_attn): 70B heads, 1k prefix + 5 x 64 suffixes 828
+// TFLOP/s (round-1 kernel 728), 4k prefix 992 (880).
 #include "common.h"
 #include "fls.h"
 
 namespace {
 
-constexpr int KT = 64;       // keys per tile
-constexpr int QB = 64;       // query rows per work item (4 waves x 16)
+constexpr int KT = 64;                 // keys per tile
+constexpr float DEFER_LOG2 = 8.0f;     // deferred-rescale threshold (log2 units)
 
 template <int HD>
 struct Lds {
@@ -41,189 +54,41 @@ struct Lds {
   __device__ static int v_off(int row, int ch) { return row * ROW + ((ch ^ ((row & (NCH / 2 - 1)) << 1)) << 4); }
 };
 
-// HPB query heads of the same KV group per block (GQA): waves 4*j .. 4*j+3
-// serve head h0 + j, so every K/V tile staged in LDS feeds 4*HPB waves.
-template <int HD, int HPB>
-__global__ __launch_bounds__(256 * HPB) void attn_fwd(const half_t* __restrict__ qkv, half_t* __restrict__ out,
-                                                    const int* __restrict__ work, int nh, int nkv, int ld_qkv,
-                                                    int ld_out, float scale_log2, const half_t* __restrict__ kv0,
-                                                    int ld_kv0) {
-  constexpr int NS = HD / 32;     // k-steps of the QK^T product
-  constexpr int NU = HD / 16;     // 16-wide d subtiles of O
-  __shared__ __attribute__((aligned(16))) char smem[2 * KT * HD * 2];
-  char* Ks = smem;
-  char* Vs = smem + KT * HD * 2;
-
-  constexpr int NT_ = 256 * HPB;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = (tid >> 6) & 3;          // row group inside the 64-row item
-  const int h = blockIdx.y * HPB + (tid >> 8);
-  const int g = h / (nh / nkv);
-
-  const int* wi = work + blockIdx.x * 8;
-  const int q_start = wi[0], q_len = wi[1], q_off = wi[2];
-  if (q_len <= 0) return;                   // padding item (bucketed graph replays); block-uniform
-  const int r_start[2] = {wi[3], wi[6]};
-  const int r_len[2] = {wi[4], wi[7]};
-  const int r_causal[2] = {wi[5], 1};
-
-  const int fr = lane & 15, grp = lane >> 4;
-  const int q_col = h * HD;
-  const int k_col = nh * HD + g * HD;
-  const int v_col = (nh + nkv) * HD + g * HD;
-
-  // Q fragments (B operand of S^T = K Q^T): lane holds Q[row fr][32s + 8grp .. +8]
-  const int qrow = wave * 16 + fr;
-  const int qrow_c = min(qrow, q_len - 1);
-  half8 qf[NS];
-  {
-    const half_t* qp = qkv + (size_t)(q_start + qrow_c) * ld_qkv + q_col + grp * 8;
-#pragma unroll
-    for (int s = 0; s < NS; ++s) qf[s] = *(const half8*)(qp + s * 32);
-  }
-  const int qi = q_off + qrow;   // query index within its segment (causal compare)
-
-  floatx4 o[NU];
-#pragma unroll
-  for (int u = 0; u < NU; ++u) o[u] = floatx4{0.f, 0.f, 0.f, 0.f};
-  float m_run = -1e30f;
-  float l_run = 0.f;
-
-  for (int rg = 0; rg < 2; ++rg) {
-    const int klen = r_len[rg];
-    if (klen <= 0) continue;
-    const int kbase = r_start[rg];
-    const bool causal = r_causal[rg] != 0;
-    // range 0 may live in the prefix K/V cache ([P, 2 * nkv * HD], K then V)
-    const bool from_cache = rg == 0 && kv0 != nullptr;
-    const half_t* kvb = from_cache ? kv0 : qkv;
-    const int ldk = from_cache ? ld_kv0 : ld_qkv;
-    const int kc = from_cache ? g * HD : k_col;
-    const int vc = from_cache ? (nkv + g) * HD : v_col;
-    // keys needed by the last valid query of this block
-    const int kend = causal ? min(klen, q_off + q_len) : klen;
-    for (int k0 = 0; k0 < kend; k0 += KT) {
-      __syncthreads();
-      // ---- stage K and V tiles (64 rows x HD) into LDS, 16 B per thread-chunk
-      constexpr int CHUNKS = KT * HD / 8;
-#pragma unroll
-      for (int c = tid; c < CHUNKS; c += NT_) {
-        const int row = c / (HD / 8), ch = c % (HD / 8);
-        const int key = min(k0 + row, klen - 1);
-        const half_t* src = kvb + (size_t)(kbase + key) * ldk;
-        const half8 kv = *(const half8*)(src + kc + ch * 8);
-        const half8 vv = *(const half8*)(src + vc + ch * 8);
-        *(half8*)(Ks + Lds<HD>::k_off(row, ch)) = kv;
-        *(half8*)(Vs + Lds<HD>::v_off(row, ch)) = vv;
-      }
-      __syncthreads();
-
-      // ---- S^T tile: 4 subtiles of 16 keys; lane holds keys 16t + 4grp + r of query fr
-      floatx4 sc[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        sc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-        const int krow = t * 16 + fr;
-#pragma unroll
-        for (int s = 0; s < NS; ++s) {
-          const half8 kf = *(const half8*)(Ks + Lds<HD>::k_off(krow, s * 4 + grp));
-          sc[t] = mfma16x16x32(kf, qf[s], sc[t]);
-        }
-      }
-      // ---- scale, mask, online softmax (query = lane's fr row)
-      float mx = -INFINITY;
-      // key k0 + 16t + 4grp + r is visible iff 16t + r <= rel (one compare per score)
-      const int rel = (causal ? min(klen - 1, qi) : klen - 1) - k0 - grp * 4;
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float v = (t * 16 + r <= rel) ? sc[t][r] * scale_log2 : -INFINITY;
-          sc[t][r] = v;
-          mx = fmaxf(mx, v);
-        }
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float m_new = fmaxf(m_run, mx);
-      // rescale only when some row's max grew (alpha == 1 exactly otherwise)
-      if (!__all(m_new == m_run)) {
-        const float alpha = fast_exp2(m_run - m_new);
-        l_run *= alpha;
-#pragma unroll
-        for (int u = 0; u < NU; ++u) o[u] *= alpha;
-      }
-      m_run = m_new;
-      float psum = 0.f;
-      half8 pf[2];
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float p = fast_exp2(sc[t][r] - m_new);
-          psum += p;
-          pf[t >> 1][(t & 1) * 4 + r] = (half_t)p;
-        }
-      l_run += psum;
-
-      // ---- O^T += V^T P^T ; V^T fragment via two transposed 4x16 reads
-      const int q4 = (lane & 15) >> 2, p4 = lane & 3;
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const int row_a = ks * 32 + grp * 4 + q4;
-        const int row_b = row_a + 16;
-#pragma unroll
-        for (int u = 0; u < NU; ++u) {
-          const int ch = u * 2 + (p4 >> 1);
-          const half4 va = ds_read_tr16(Vs + Lds<HD>::v_off(row_a, ch) + (p4 & 1) * 8);
-          const half4 vb = ds_read_tr16(Vs + Lds<HD>::v_off(row_b, ch) + (p4 & 1) * 8);
-          const half8 vf = {va[0], va[1], va[2], va[3], vb[0], vb[1], vb[2], vb[3]};
-          o[u] = mfma16x16x32(vf, pf[ks], o[u]);
-        }
-      }
-    }
-  }
-  // ---- normalise and store: lane holds O[q = fr][d = 16u + 4grp + r]
-  l_run += __shfl_xor(l_run, 16, 64);
-  l_run += __shfl_xor(l_run, 32, 64);
-  if (qrow < q_len) {
-    const float inv = 1.f / l_run;
-    half_t* op = out + (size_t)(q_start + qrow) * ld_out + h * HD + grp * 4;
-#pragma unroll
-    for (int u = 0; u < NU; ++u) {
-      half4 v;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = (half_t)(o[u][r] * inv);
-      *(half4*)(op + u * 16) = v;
-    }
-  }
+// max without the canonicalising v_max(x, x) the compiler puts in front of fmaxf on MFMA results
+// (guide: keep such ops single instructions); scores are never NaN here
+__device__ __forceinline__ float vmax3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float vmax(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
 }
 
-// ------------------------------------------------------------------- v2
-// LDS-read intensity is what bounds attn_fwd: every wave re-reads the whole
-// 64-key K and V tile (32 KB) from LDS for only 16 query rows (32 MFMAs), so
-// the LDS pipe needs ~2x the MFMA time.  v2 gives each wave 32 query rows
-// (two 16-row groups sharing every K / V^T fragment it reads: 64 MFMAs per
-// 32 KB) with 2 waves per query head and HPB heads of one KV group per block,
-// and overlaps the global->LDS staging with compute: tile t+1's K/V rows are
-// loaded into registers before tile t's MFMAs and written to LDS after the
-// barrier that retires tile t's reads (guide T14, write-after-barrier).
-// The key tiles of both ranges (prefix, own suffix) form one flat sequence so
-// the prefetch crosses the range boundary.  DB = true (variant 3, default)
-// double-buffers the LDS tile: tile t+1 is written into the other buffer right
-// after tile t's MFMAs and tile t+2's loads are issued, one barrier per tile.
-// Masking is one integer compare per score against a per-lane visibility
-// bound, and the O / l rescale is skipped when no row's running max grew
-// (alpha would be exactly 1).
-// Measured (profiles/r1_attention): 1024-token prefix + 5x64 suffixes, 70B
-// heads: v1 598 -> v3 727 TFLOP/s; 4096-token prefix: 683 -> 870.
-// WPH: waves per query head (32 query rows each) = rows per work item / 32.  WPH = 4 (128-row
-// items) serves multi-head attention, where no other head shares the K/V tile: 4 waves read it.
-template <int HD, int HPB, bool DB, int WPH = 2>
-__global__ __launch_bounds__(64 * WPH * HPB, 2) void attn_fwd_v2(const half_t* __restrict__ qkv, half_t* __restrict__ out,
-                                                       const int* __restrict__ work, int nh, int nkv, int ld_qkv,
-                                                       int ld_out, float scale_log2,
-                                                       const half_t* __restrict__ kv0, int ld_kv0) {
+// max over the 4 lane groups (lanes l, l^16, l^32, l^48) that hold one query row: VALU permlane
+// swaps, not ds_bpermute (the LDS pipe is busy with the K / V^T fragment reads)
+__device__ __forceinline__ float max_xor16_32(float v) {
+  auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = vmax(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return vmax(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+
+typedef float float2_ __attribute__((ext_vector_type(2)));
+typedef _Float16 half2_ __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ unsigned pack_h2(float a, float b) {
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(float2_{a, b}, half2_));
+}
+
+template <int HD, int HPB, int WPH>
+__global__ __launch_bounds__(64 * WPH * HPB, 2) void attn_fwd(const half_t* __restrict__ qkv, half_t* __restrict__ out,
+                                                    const int* __restrict__ work, const int* __restrict__ seg_lo,
+                                                    int nh, int nkv, int ld_qkv, int ld_out, float scale_log2,
+                                                    const half_t* __restrict__ kv0, int ld_kv0) {
   constexpr int NT_ = 64 * WPH * HPB;
   constexpr int NS = HD / 32;               // k-steps of QK^T
   constexpr int NU = HD / 16;               // 16-wide d subtiles of O
@@ -231,11 +96,11 @@ __global__ __launch_bounds__(64 * WPH * HPB, 2) void attn_fwd_v2(const half_t* _
   constexpr int PER = KT * CH / NT_;        // chunks per thread per operand
   static_assert(PER >= 1 && (KT * CH) % NT_ == 0, "tile / block mismatch");
   constexpr int TILE_BYTES = 2 * KT * HD * 2;         // K + V
-  __shared__ __attribute__((aligned(16))) char smem[(DB ? 2 : 1) * TILE_BYTES];
+  __shared__ __attribute__((aligned(16))) char smem[2 * TILE_BYTES];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform: h, g, descriptors in SGPRs
   const int h = blockIdx.y * HPB + wave / WPH;
   const int g = h / (nh / nkv);             // same for every head of the block (HPB | group)
   const int rbase = (wave % WPH) * 32;      // this wave's first query row of the item
@@ -251,48 +116,58 @@ __global__ __launch_bounds__(64 * WPH * HPB, 2) void attn_fwd_v2(const half_t* _
   const int ntiles = n0 + (kend1 + KT - 1) / KT;
 
   const int fr = lane & 15, grp = lane >> 4;
-  const int q_col = h * HD;
   const int k_col = nh * HD + g * HD;
   const int v_col = (nh + nkv) * HD + g * HD;
+  // one buffer descriptor per key range, based at the range's first row: 32-bit offsets
+  // (klen * ld * 2 bytes stays far below 4 GiB for any context this engine accepts)
+  const bool cache0 = kv0 != nullptr;                  // range 0 from the prefix K/V cache
+  const int ld0 = cache0 ? ld_kv0 : ld_qkv;
+  const int kc0 = cache0 ? g * HD : k_col, vc0 = cache0 ? (nkv + g) * HD : v_col;
+  const __amdgpu_buffer_rsrc_t rs0 = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<half_t*>((cache0 ? kv0 : qkv) + (size_t)r_start0 * ld0), (short)0, -1, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<half_t*>(qkv + (size_t)r_start1 * ld_qkv), (short)0, -1, 0x00020000);
 
   half8 qf[2][NS];
-  int qi[2];
+  int qi[2], lo[2];
 #pragma unroll
   for (int qg = 0; qg < 2; ++qg) {
     const int qrow = rbase + qg * 16 + fr;
-    const half_t* qp = qkv + (size_t)(q_start + min(qrow, q_len - 1)) * ld_qkv + q_col + grp * 8;
+    const int qr = q_start + min(qrow, q_len - 1);
+    const half_t* qp = qkv + (size_t)qr * ld_qkv + h * HD + grp * 8;
 #pragma unroll
     for (int s = 0; s < NS; ++s) qf[qg][s] = *(const half8*)(qp + s * 32);
-    qi[qg] = q_off + qrow;
+    qi[qg] = q_off + qrow;                  // range-1 index of this query row (causal upper bound)
+    lo[qg] = seg_lo && r_len1 > 0 ? seg_lo[qr] - r_start1 : 0;   // its suffix's first range-1 key
   }
+  // the wave's first query row bounds every causal compare from below: a tile is fully visible to
+  // the whole wave iff its last key is visible to that row (range 1 with several suffixes: masked)
+  const int qi_min = q_off + rbase;
+  const bool multi = seg_lo != nullptr;
 
   floatx4 o[2][NU];
 #pragma unroll
   for (int qg = 0; qg < 2; ++qg)
 #pragma unroll
     for (int u = 0; u < NU; ++u) o[qg][u] = floatx4{0.f, 0.f, 0.f, 0.f};
-  float m_run[2] = {-1e30f, -1e30f};
+  float m_run[2] = {-1e30f, -1e30f};        // raw-score domain
   float l_run[2] = {0.f, 0.f};
 
-  half8 pk[PER], pv[PER];
+  u32x4 pk[PER], pv[PER];
   auto load_tile = [&](int t) {
     const bool r1 = t >= n0;
     const int k0 = (r1 ? t - n0 : t) * KT;
     const int klen = r1 ? r_len1 : r_len0;
-    const int kb = r1 ? r_start1 : r_start0;
-    // range 0 may live in the prefix K/V cache ([P, 2 * nkv * HD], K then V)
-    const bool from_cache = !r1 && kv0 != nullptr;
-    const half_t* kvb = from_cache ? kv0 : qkv;
-    const int ldk = from_cache ? ld_kv0 : ld_qkv;
-    const int kc = from_cache ? g * HD : k_col;
-    const int vc = from_cache ? (nkv + g) * HD : v_col;
+    const int ldk = r1 ? ld_qkv : ld0;
+    const unsigned kc = (unsigned)(r1 ? k_col : kc0) * 2u, vc = (unsigned)(r1 ? v_col : vc0) * 2u;
+    const __amdgpu_buffer_rsrc_t r = r1 ? rs1 : rs0;
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int c = tid + i * NT_;
       const int row = c / CH, ch = c % CH;
-      const half_t* src = kvb + (size_t)(kb + min(k0 + row, klen - 1)) * ldk;
-      pk[i] = *(const half8*)(src + kc + ch * 8);
-      pv[i] = *(const half8*)(src + vc + ch * 8);
+      const unsigned off = (unsigned)(min(k0 + row, klen - 1) * ldk + ch * 8) * 2u;
+      pk[i] = __builtin_amdgcn_raw_buffer_load_b128(r, off, kc, 0);
+      pv[i] = __builtin_amdgcn_raw_buffer_load_b128(r, off, vc, 0);
     }
   };
   auto store_tile = [&](int buf) {
@@ -302,15 +177,15 @@ __global__ __launch_bounds__(64 * WPH * HPB, 2) void attn_fwd_v2(const half_t* _
     for (int i = 0; i < PER; ++i) {
       const int c = tid + i * NT_;
       const int row = c / CH, ch = c % CH;
-      *(half8*)(Ks + Lds<HD>::k_off(row, ch)) = pk[i];
-      *(half8*)(Vs + Lds<HD>::v_off(row, ch)) = pv[i];
+      *(u32x4*)(Ks + Lds<HD>::k_off(row, ch)) = pk[i];
+      *(u32x4*)(Vs + Lds<HD>::v_off(row, ch)) = pv[i];
     }
   };
 
   if (ntiles > 0) {
     load_tile(0);
     store_tile(0);
-    if (DB && ntiles > 1) load_tile(1);
+    if (ntiles > 1) load_tile(1);
   }
   __syncthreads();
   for (int t = 0; t < ntiles; ++t) {
@@ -318,9 +193,8 @@ __global__ __launch_bounds__(64 * WPH * HPB, 2) void attn_fwd_v2(const half_t* _
     const int k0 = (r1 ? t - n0 : t) * KT;
     const int klen = r1 ? r_len1 : r_len0;
     const bool causal = r1 || r_causal0;
-    const char* Ks = smem + (DB ? (t & 1) : 0) * TILE_BYTES;
+    const char* Ks = smem + (t & 1) * TILE_BYTES;
     const char* Vs = Ks + KT * HD * 2;
-    if (!DB && t + 1 < ntiles) load_tile(t + 1);     // in flight under this tile's MFMAs
 
     // ---- S^T = K Q^T for both 16-row query groups (each K fragment read once)
     floatx4 sc[2][4];
@@ -336,40 +210,63 @@ __global__ __launch_bounds__(64 * WPH * HPB, 2) void attn_fwd_v2(const half_t* _
         sc[1][tt] = mfma16x16x32(kf, qf[1][s], sc[1][tt]);
       }
     }
-    // ---- scale, mask, online softmax per query group
+    // ---- visibility: wave-uniform fast path when every key of the tile is visible to every row
+    const int vis_last = causal ? min(klen - 1, qi_min) : klen - 1;
+    if (k0 + KT - 1 > vis_last || (r1 && multi)) {
+      asm volatile("" ::: "memory");        // keep this a branch (not per-score selects on every tile)
+#pragma unroll
+      for (int qg = 0; qg < 2; ++qg) {
+        // key k0 + 16tt + 4grp + r is visible iff lo_rel <= 16tt + r <= hi_rel
+        const int hi_rel = (causal ? min(klen - 1, qi[qg]) : klen - 1) - k0 - grp * 4;
+        const int lo_rel = (r1 ? lo[qg] : 0) - k0 - grp * 4;
+#pragma unroll
+        for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (tt * 16 + r > hi_rel || tt * 16 + r < lo_rel) sc[qg][tt][r] = -INFINITY;
+      }
+    }
+    // ---- online softmax per query group
     half8 pf[2][2];
 #pragma unroll
     for (int qg = 0; qg < 2; ++qg) {
-      float mx = -INFINITY;
-      const int rel = (causal ? min(klen - 1, qi[qg]) : klen - 1) - k0 - grp * 4;
-#pragma unroll
-      for (int tt = 0; tt < 4; ++tt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float v = (tt * 16 + r <= rel) ? sc[qg][tt][r] * scale_log2 : -INFINITY;
-          sc[qg][tt][r] = v;
-          mx = fmaxf(mx, v);
-        }
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float m_new = fmaxf(m_run[qg], mx);
-      if (!__all(m_new == m_run[qg])) {
-        const float alpha = fast_exp2(m_run[qg] - m_new);
+      // 16 scores of this lane's query: two independent max3 chains, then across the lane groups
+      float ma = vmax3(sc[qg][0][0], sc[qg][0][1], sc[qg][0][2]);
+      float mb = vmax3(sc[qg][2][0], sc[qg][2][1], sc[qg][2][2]);
+      ma = vmax3(ma, sc[qg][0][3], sc[qg][1][0]);
+      mb = vmax3(mb, sc[qg][2][3], sc[qg][3][0]);
+      ma = vmax3(ma, sc[qg][1][1], sc[qg][1][2]);
+      mb = vmax3(mb, sc[qg][3][1], sc[qg][3][2]);
+      const float mx = max_xor16_32(vmax3(ma, sc[qg][1][3], vmax(mb, sc[qg][3][3])));
+      // deferred rescale: keep the old max unless some row of the wave grew past 2^DEFER_LOG2
+      // (the previous tile's P.V is complete: nothing at the old scale is pending)
+      if (!__all((mx - m_run[qg]) * scale_log2 <= DEFER_LOG2)) {
+        const float m_new = fmaxf(m_run[qg], mx);
+        const float alpha = fast_exp2((m_run[qg] - m_new) * scale_log2);
         l_run[qg] *= alpha;
 #pragma unroll
         for (int u = 0; u < NU; ++u) o[qg][u] *= alpha;
+        m_run[qg] = m_new;
       }
-      m_run[qg] = m_new;
+      const float mc = m_run[qg] * scale_log2;
       float psum = 0.f;
+      unsigned pw[8];
 #pragma unroll
-      for (int tt = 0; tt < 4; ++tt)
+      for (int tt = 0; tt < 4; ++tt) {
+        float p[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float p = fast_exp2(sc[qg][tt][r] - m_new);
-          psum += p;
-          pf[qg][tt >> 1][(tt & 1) * 4 + r] = (half_t)p;
+          p[r] = fast_exp2(__builtin_fmaf(sc[qg][tt][r], scale_log2, -mc));
+          psum += p[r];
         }
+        pw[tt * 2] = pack_h2(p[0], p[1]);
+        pw[tt * 2 + 1] = pack_h2(p[2], p[3]);
+      }
       l_run[qg] += psum;
+      // P^T fragment: element (tt & 1) * 4 + r of k-step tt >> 1 = key 16 tt + 4 grp + r
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        pf[qg][ks] = __builtin_bit_cast(half8, u32x4{pw[ks * 4], pw[ks * 4 + 1], pw[ks * 4 + 2], pw[ks * 4 + 3]});
     }
     // ---- O^T += V^T P^T (each V^T fragment read once for both groups)
     const int q4 = (lane & 15) >> 2, p4 = lane & 3;
@@ -387,18 +284,11 @@ __global__ __launch_bounds__(64 * WPH * HPB, 2) void attn_fwd_v2(const half_t* _
         o[1][u] = mfma16x16x32(vf, pf[1][ks], o[1][u]);
       }
     }
-    if (DB) {
-      // the other buffer's last readers (tile t-1) all passed the previous barrier
-      if (t + 1 < ntiles) {
-        store_tile((t + 1) & 1);
-        if (t + 2 < ntiles) load_tile(t + 2);   // in flight under tile t+1's MFMAs
-      }
-      __syncthreads();
-    } else if (t + 1 < ntiles) {
-      __syncthreads();          // every wave is done reading tile t
-      store_tile(0);
-      __syncthreads();
+    if (t + 1 < ntiles) {
+      store_tile((t + 1) & 1);               // the other buffer's readers (tile t-1) passed the last barrier
+      if (t + 2 < ntiles) load_tile(t + 2);  // in flight under tile t+1's MFMAs
     }
+    __syncthreads();
   }
   // ---- normalise and store
 #pragma unroll
@@ -421,91 +311,54 @@ __global__ __launch_bounds__(64 * WPH * HPB, 2) void attn_fwd_v2(const half_t* _
   }
 }
 
-int g_attn_variant = 3;
-int g_attn_mha_v2 = 0;   // odd GQA groups (MHA) on the v2/v3 kernel with one head per block (A/B)
-
-}  // namespace
-
-extern "C" int fls_attn_set_mha_v2(int on) {
-  const int old = g_attn_mha_v2;
-  g_attn_mha_v2 = on ? 1 : 0;
-  return old;
-}
-
-extern "C" int fls_attn_set_variant(int v) {
-  if (v < 1 || v > 3) return -1;
-  g_attn_variant = v;
-  return 0;
-}
-
-extern "C" int fls_attention(const void* qkv, void* out, const int* work, int n_items, int n_q_heads,
-                             int n_kv_heads, int head_dim, int ld_qkv, int ld_out, float scale, const void* kv0,
-                             int ld_kv0, int q_block, fls_stream_t s) {
-  if (n_items <= 0) return 0;
-  if (n_q_heads % n_kv_heads) return -2;
-  const float scale_log2 = scale * 1.4426950408889634f;
-  auto st = (hipStream_t)s;
-  const int group = n_q_heads / n_kv_heads;
-  if (q_block > 64) {
-    // 128-row work items (runtime/batch.py pack_prompts(q_block=128)): 4 waves per query head
-    if (q_block > 128 || (head_dim != 64 && head_dim != 128)) return -5;
-    const int hpb = group % 2 == 0 ? 2 : 1;
-    dim3 grid4(n_items, n_q_heads / hpb);
-#define FLS_ATTN4_LAUNCH(HD_, HPB_)                                                                       \
-  hipLaunchKernelGGL((attn_fwd_v2<HD_, HPB_, true, 4>), grid4, dim3(256 * HPB_), 0, st, (const half_t*)qkv, \
-                     (half_t*)out, work, n_q_heads, n_kv_heads, ld_qkv, ld_out, scale_log2,               \
-                     (const half_t*)kv0, ld_kv0)
-    if (head_dim == 128) {
-      if (hpb == 2) FLS_ATTN4_LAUNCH(128, 2); else FLS_ATTN4_LAUNCH(128, 1);
-    } else {
-      if (hpb == 2) FLS_ATTN4_LAUNCH(64, 2); else FLS_ATTN4_LAUNCH(64, 1);
-    }
-#undef FLS_ATTN4_LAUNCH
-    FLS_CHECK_LAUNCH();
-    return 0;
+template <int HD, int WPH>
+int launch(int hpb, dim3 grid, hipStream_t st, const half_t* qkv, half_t* out, const int* work, const int* seg_lo,
+           int nh, int nkv, int ld_qkv, int ld_out, float scale_log2, const half_t* kv0, int ld_kv0) {
+#define FLS_ATTN_LAUNCH(HPB_)                                                                                 \
+  hipLaunchKernelGGL((attn_fwd<HD, HPB_, WPH>), grid, dim3(64 * WPH * HPB_), 0, st, qkv, out, work, seg_lo, nh, \
+                     nkv, ld_qkv, ld_out, scale_log2, kv0, ld_kv0)
+  if constexpr (WPH == 2) {
+    if (hpb == 4) FLS_ATTN_LAUNCH(4);
+    else if (hpb == 2) FLS_ATTN_LAUNCH(2);
+    else FLS_ATTN_LAUNCH(1);
+  } else {
+    if (hpb == 2) FLS_ATTN_LAUNCH(2);
+    else FLS_ATTN_LAUNCH(1);
   }
-  if (g_attn_variant >= 2 && (head_dim == 64 || head_dim == 128) &&
-      (group % 2 == 0 || g_attn_mha_v2)) {
-    // HPB query heads of one KV group per block; odd groups (MHA: Llama-2-7B/13B) one head per block
-    const int hpb = group % 4 == 0 ? 4 : (group % 2 == 0 ? 2 : 1);
-    const bool db = g_attn_variant == 3;
-    dim3 grid2(n_items, n_q_heads / hpb);
-#define FLS_ATTN2_LAUNCH(HD_, HPB_)                                                                       \
-  do {                                                                                                    \
-    if (db)                                                                                               \
-      hipLaunchKernelGGL((attn_fwd_v2<HD_, HPB_, true>), grid2, dim3(128 * HPB_), 0, st,                   \
-                         (const half_t*)qkv, (half_t*)out, work, n_q_heads, n_kv_heads, ld_qkv, ld_out,    \
-                         scale_log2, (const half_t*)kv0, ld_kv0);                                                                     \
-    else                                                                                                  \
-      hipLaunchKernelGGL((attn_fwd_v2<HD_, HPB_, false>), grid2, dim3(128 * HPB_), 0, st,                  \
-                         (const half_t*)qkv, (half_t*)out, work, n_q_heads, n_kv_heads, ld_qkv, ld_out,    \
-                         scale_log2, (const half_t*)kv0, ld_kv0);                                                                     \
-  } while (0)
-    if (head_dim == 128) {
-      if (hpb == 4) FLS_ATTN2_LAUNCH(128, 4); else if (hpb == 2) FLS_ATTN2_LAUNCH(128, 2); else FLS_ATTN2_LAUNCH(128, 1);
-    } else {
-      if (hpb == 4) FLS_ATTN2_LAUNCH(64, 4); else if (hpb == 2) FLS_ATTN2_LAUNCH(64, 2); else FLS_ATTN2_LAUNCH(64, 1);
-    }
-#undef FLS_ATTN2_LAUNCH
-    FLS_CHECK_LAUNCH();
-    return 0;
-  }
-  const bool two = (group % 2) == 0;        // pair up query heads of one KV group
-  dim3 grid(n_items, two ? n_q_heads / 2 : n_q_heads);
-#define FLS_ATTN_LAUNCH(HD_, HPB_)                                                                          \
-  hipLaunchKernelGGL((attn_fwd<HD_, HPB_>), grid, dim3(256 * HPB_), 0, st, (const half_t*)qkv, (half_t*)out, \
-                     work, n_q_heads, n_kv_heads, ld_qkv, ld_out, scale_log2, (const half_t*)kv0, ld_kv0)
-  switch (head_dim) {
-    case 64:
-      if (two) FLS_ATTN_LAUNCH(64, 2); else FLS_ATTN_LAUNCH(64, 1);
-      break;
-    case 128:
-      if (two) FLS_ATTN_LAUNCH(128, 2); else FLS_ATTN_LAUNCH(128, 1);
-      break;
-    default:
-      return -3;
-  }
+
 #undef FLS_ATTN_LAUNCH
   FLS_CHECK_LAUNCH();
   return 0;
+}
+
+}  // namespace
+
+extern "C" int fls_attention(const void* qkv, void* out, const int* work, int n_items, int n_q_heads,
+                             int n_kv_heads, int head_dim, int ld_qkv, int ld_out, float scale, const void* kv0,
+                             int ld_kv0, const int* seg_lo, int q_block, fls_stream_t s) {
+  if (n_items <= 0) return 0;
+  if (n_q_heads % n_kv_heads) return -2;
+  if (head_dim != 64 && head_dim != 128) return -3;
+  if (q_block != 64 && q_block != 128) return -5;
+  const float scale_log2 = scale * 1.4426950408889634f;
+  auto st = (hipStream_t)s;
+  const int group = n_q_heads / n_kv_heads;
+  // heads of one KV group per block share every staged K/V tile: up to 4 (64-row items) or 2
+  // (128-row items, 4 waves per head) as the group allows, else 1 (multi-head attention)
+  int hpb = 1;
+  if (q_block == 64) hpb = group % 4 == 0 ? 4 : (group % 2 == 0 ? 2 : 1);
+  else hpb = group % 2 == 0 ? 2 : 1;
+  const dim3 grid(n_items, n_q_heads / hpb);
+  auto q = (const half_t*)qkv;
+  auto o = (half_t*)out;
+  auto k0 = (const half_t*)kv0;
+  if (q_block == 64)
+    return head_dim == 128 ? launch<128, 2>(hpb, grid, st, q, o, work, seg_lo, n_q_heads, n_kv_heads, ld_qkv, ld_out,
+                                            scale_log2, k0, ld_kv0)
+                           : launch<64, 2>(hpb, grid, st, q, o, work, seg_lo, n_q_heads, n_kv_heads, ld_qkv, ld_out,
+                                           scale_log2, k0, ld_kv0);
+  return head_dim == 128 ? launch<128, 4>(hpb, grid, st, q, o, work, seg_lo, n_q_heads, n_kv_heads, ld_qkv, ld_out,
+                                          scale_log2, k0, ld_kv0)
+                         : launch<64, 4>(hpb, grid, st, q, o, work, seg_lo, n_q_heads, n_kv_heads, ld_qkv, ld_out,
+                                         scale_log2, k0, ld_kv0);
 }

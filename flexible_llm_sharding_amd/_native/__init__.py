@@ -63,7 +63,7 @@ class Piece(ctypes.Structure):
                 ("kind", ctypes.c_int32), ("pad", ctypes.c_int32)]
 
 
-KERNELS_ABI = 9   # bumped whenever a C signature in csrc/include/fls.h changes
+KERNELS_ABI = 10   # bumped whenever a C signature in csrc/include/fls.h changes
 
 
 def _load_kernels():
@@ -76,10 +76,8 @@ def _load_kernels():
           c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p)
     _bind(lib, "fls_gemm_set_mid", c_int, c_int)
     _bind(lib, "fls_gemm_set_order", c_int, c_int)
-    _bind(lib, "fls_attn_set_mha_v2", c_int, c_int)
-    _bind(lib, "fls_attn_set_variant", c_int, c_int)
     _bind(lib, "fls_attention", c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
-          c_int, c_int, c_float, c_void_p, c_int, c_int, c_void_p)
+          c_int, c_int, c_float, c_void_p, c_int, c_void_p, c_int, c_void_p)
     _bind(lib, "fls_rmsnorm", c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
           c_int, c_float, c_void_p)
     _bind(lib, "fls_embed", c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p)

@@ -223,8 +223,10 @@ def run_decoder(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, b
         attn_arg = meta["work_last"] if work_items else batch.last_segments
     else:
         attn_arg = meta["work"] if work_items else batch.segments
+    # work items span several suffixes of a prompt: seg_lo makes their range 1 block-diagonal
+    kw = {"seg_lo": meta["seg_lo"]} if work_items else {}
     a = ops.attention(qkv, attn_arg, cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim, kv0=kv0,
-                      q_block=batch.q_block, out=ctx.scratch(T0, cfg.q_size))
+                      q_block=batch.q_block, out=ctx.scratch(T0, cfg.q_size), **kw)
     del qkv
     if prune:
         idx = meta["last_idx"]

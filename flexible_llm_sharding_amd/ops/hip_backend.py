@@ -104,8 +104,10 @@ class HipOps:
                          rope_cols=rope_cols, head_dim=head_dim, bias=bias)
 
     # ----------------------------------------------------------- attention
-    def attention(self, qkv, work, n_q_heads, n_kv_heads, head_dim, kv0=None, q_block: int = 64, out=None):
-        """kv0 ([P, 2 * n_kv * hd], K then V): range 0 of every work item reads these rows (prefix cache)."""
+    def attention(self, qkv, work, n_q_heads, n_kv_heads, head_dim, kv0=None, q_block: int = 64, out=None,
+                  seg_lo=None):
+        """kv0 ([P, 2 * n_kv * hd], K then V): range 0 of every work item reads these rows (prefix cache).
+        seg_lo ([T] int32, first row of each row's suffix): work items may span several suffixes."""
         _f16(qkv, "qkv")
         if work.dtype != torch.int32 or not work.is_cuda:
             raise TypeError("work items must be an int32 CUDA tensor")
@@ -114,12 +116,17 @@ class HipOps:
             if kv0.shape[1] != 2 * n_kv_heads * head_dim:
                 raise ValueError(f"kv0 must be [P, {2 * n_kv_heads * head_dim}], got {tuple(kv0.shape)}")
         T = qkv.shape[0]
+        # work items from runtime/batch.py span suffix boundaries: without seg_lo a query would see the
+        # other suffixes of its item, so it is required here (the C ABI's null form is one-suffix items)
+        if seg_lo is None or seg_lo.dtype != torch.int32 or not seg_lo.is_cuda or seg_lo.shape[0] < T:
+            raise TypeError("seg_lo (PackedBatch.seg_lo: int32 CUDA, one row per packed token) is required")
         if out is None:
             out = torch.empty(T, n_q_heads * head_dim, dtype=torch.float16, device=qkv.device)
         rc = self.k.fls_attention(qkv.data_ptr(), out.data_ptr(), work.data_ptr(), work.shape[0],
                                   n_q_heads, n_kv_heads, head_dim, qkv.stride(0), out.stride(0),
                                   head_dim ** -0.5, kv0.data_ptr() if kv0 is not None else None,
-                                  kv0.stride(0) if kv0 is not None else 0, q_block, _stream())
+                                  kv0.stride(0) if kv0 is not None else 0,
+                                  seg_lo.data_ptr() if seg_lo is not None else None, q_block, _stream())
         _chk(rc, "fls_attention")
         return out
 

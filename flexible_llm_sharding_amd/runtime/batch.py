@@ -15,6 +15,13 @@ projection is one large MFMA GEMM, and describe the attention structure with
   ``Lp .. Lp+len-1`` (``utils.py:275``); keys = the whole prefix (shared, read
   in place, never expanded) + the suffix itself causally (``utils.py:276``).
 
+A prompt's suffixes are packed back to back, and their work items cover those
+rows in ``q_block`` chunks regardless of suffix boundaries: an item's range 1
+spans every suffix it touches and ``seg_lo`` (first row of each row's suffix)
+makes it block-diagonal, so 5 suffixes of 10 tokens are one item over the
+shared prefix instead of 5 mostly empty ones (the reference's one-pass
+shared-prefix cascade, without a second pass to merge).
+
 Padding tokens after a suffix's scored position are never computed: under the
 causal mask they cannot influence it.
 """
@@ -53,6 +60,7 @@ class PackedBatch:
     positions: np.ndarray                 # [T] int32
     segments: List[Segment]
     work: np.ndarray                      # [n_items, 8] int32
+    seg_lo: np.ndarray                    # [T] int32: first packed row of each row's suffix (prefix rows: their own start)
     last_idx: np.ndarray                  # [S_total] int32 rows scored
     last_segments: List[Segment]          # one single-query segment per scored row (last layer)
     work_last: np.ndarray                 # [S_total, 8] their work items
@@ -79,6 +87,7 @@ class PackedBatch:
                 "ids": torch.from_numpy(self.ids).to(d, non_blocking=nb),
                 "positions": torch.from_numpy(self.positions).to(d, non_blocking=nb),
                 "work": torch.from_numpy(self.work).to(d, non_blocking=nb),
+                "seg_lo": torch.from_numpy(self.seg_lo).to(d, non_blocking=nb),
                 "last_idx": torch.from_numpy(self.last_idx).to(d, non_blocking=nb),
                 "work_last": torch.from_numpy(self.work_last).to(d, non_blocking=nb),
             }
@@ -104,6 +113,7 @@ def pack_prompts(tps: Sequence[TokenizedPrompt], prompt_ids: Sequence[int],
         raise ValueError("kv_cached needs prefix_offsets")
     pcausal = 1 if prefix_attention == "causal" else 0
     ids, pos, segs, last, nsuf, lsegs = [], [], [], [], [], []
+    seg_lo, work = [], []
     src, dst = [], []
     t = 0
     padded = 0
@@ -117,28 +127,38 @@ def pack_prompts(tps: Sequence[TokenizedPrompt], prompt_ids: Sequence[int],
             ids.extend(tp.prefix)
             pos.extend(range(Lp))
             segs.append(Segment(p0, Lp, p0, Lp, pcausal, 0, 0))
+            seg_lo.extend([p0] * Lp)
+            work.extend(_items(segs[-1], q_block))
             if prefix_offsets is not None:
                 src.extend(range(t, t + Lp))
                 dst.extend(range(prefix_offsets[j], prefix_offsets[j] + Lp))
             t += Lp
+        sfx0 = t
         for s in tp.suffixes:
             n = len(s)
             s0 = t
             ids.extend(s)
             pos.extend(range(Lp, Lp + n))
+            seg_lo.extend([s0] * n)
             segs.append(Segment(s0, n, p0, Lp, 0, s0, n))
             last.append(s0 + n - 1)
             # the scored row alone, for a last decoder layer that computes only scored rows
             lsegs.append(Segment(s0 + n - 1, 1, p0, Lp, 0, s0, n, q_off=n - 1))
             t += n
+        # the prompt's suffix rows [sfx0, t) in q_block chunks; range 1 of a chunk starts at the
+        # suffix holding its first row
+        for c0 in range(sfx0, t, q_block):
+            c1 = min(c0 + q_block, t)
+            r1 = seg_lo[c0]
+            work.append((c0, c1 - c0, c0 - r1, p0, Lp, 0, r1, c1 - r1))
         max_pos = max(max_pos, Lp + max([len(s) for s in tp.suffixes] or [0]))
         nsuf.append(tp.n_suffix)
         padded += tp.padded_tokens
-    work = _work_items(segs, q_block)
+    work = np.asarray(work, dtype=np.int32).reshape(-1, WORK_ITEM_FIELDS)
     return PackedBatch(
         prompt_ids=list(prompt_ids), n_suffix=nsuf,
         ids=np.asarray(ids, dtype=np.int32), positions=np.asarray(pos, dtype=np.int32),
-        segments=segs, work=work,
+        segments=segs, work=work, seg_lo=np.asarray(seg_lo, dtype=np.int32),
         last_idx=np.asarray(last, dtype=np.int32), last_segments=lsegs,
         work_last=_work_items(lsegs), num_tokens=t, padded_tokens=padded,
         max_pos=max_pos, kv_cached=kv_cached, q_block=q_block,
@@ -146,14 +166,33 @@ def pack_prompts(tps: Sequence[TokenizedPrompt], prompt_ids: Sequence[int],
         pfx_dst=np.asarray(dst, dtype=np.int64) if (prefix_offsets is not None and not kv_cached) else None)
 
 
+def _items(sg: Segment, q_block: int = Q_BLOCK) -> List[tuple]:
+    """One segment -> work items of at most ``q_block`` queries."""
+    return [(sg.q_start + off, min(q_block, sg.q_len - off), sg.q_off + off,
+             sg.r0_start, sg.r0_len, sg.r0_causal, sg.r1_start, sg.r1_len)
+            for off in range(0, sg.q_len, q_block)]
+
+
 def _work_items(segs: Sequence[Segment], q_block: int = Q_BLOCK) -> np.ndarray:
-    """Segments -> [n_items, 8] int32 work items of at most ``q_block`` queries."""
-    work = []
-    for sg in segs:
-        for off in range(0, sg.q_len, q_block):
-            work.append((sg.q_start + off, min(q_block, sg.q_len - off), sg.q_off + off,
-                         sg.r0_start, sg.r0_len, sg.r0_causal, sg.r1_start, sg.r1_len))
+    """Segments -> [n_items, 8] int32 work items of at most ``q_block`` queries (one segment each)."""
+    work = [it for sg in segs for it in _items(sg, q_block)]
     return np.asarray(work, dtype=np.int32).reshape(-1, WORK_ITEM_FIELDS)
+
+
+def visible_keys(work: np.ndarray, seg_lo: Optional[np.ndarray], row: int) -> List[tuple]:
+    """(range, first key row, last key row) visible to packed query ``row`` under the work items:
+    the semantics of the attention kernel (csrc/kernels/attention.hip), for host-side tests."""
+    for q_start, q_len, q_off, r0s, r0l, r0c, r1s, r1l in work.tolist():
+        if q_start <= row < q_start + q_len:
+            qi = q_off + row - q_start
+            out = []
+            if r0l > 0:
+                out.append((0, r0s, r0s + (min(r0l - 1, qi) if r0c else r0l - 1)))
+            if r1l > 0:
+                lo = (int(seg_lo[row]) - r1s) if seg_lo is not None else 0
+                out.append((1, r1s + lo, r1s + min(r1l - 1, qi)))
+            return out
+    return []
 
 
 def split_microbatches(tps: Sequence[TokenizedPrompt], token_budget: int,

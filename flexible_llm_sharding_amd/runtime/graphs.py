@@ -57,11 +57,13 @@ def padded_meta(batch: PackedBatch, key) -> Dict[str, np.ndarray]:
     pos[:batch.num_tokens] = batch.positions
     work = np.zeros((W, WORK_ITEM_FIELDS), np.int32)
     work[:batch.work.shape[0]] = batch.work
+    seg_lo = np.zeros(T, np.int32)                         # padding rows: never a query of any item
+    seg_lo[:batch.num_tokens] = batch.seg_lo
     last = np.zeros(S, np.int32)
     last[:batch.n_scored] = batch.last_idx
     wl = np.zeros((S, WORK_ITEM_FIELDS), np.int32)        # padding items: q_len 0
     wl[:batch.work_last.shape[0]] = batch.work_last
-    return {"ids": ids, "positions": pos, "work": work, "last_idx": last, "work_last": wl}
+    return {"ids": ids, "positions": pos, "work": work, "seg_lo": seg_lo, "last_idx": last, "work_last": wl}
 
 
 class _Graph:

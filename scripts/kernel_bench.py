@@ -94,16 +94,8 @@ def main():
     for cname, bb, mm, qq in cases:
         att_fl = layer_flops(cfg, bb) - 2.0 * bb.num_tokens * cfg.decoder_layer_params()
         row = {"op": "attention_shared_prefix", "case": cname, "tokens": bb.num_tokens}
-        ts = {1: [], 2: [], 3: []}
-        for _ in range(3):                       # interleaved rounds (guide §5.4 rule 24)
-            for var in (1, 2, 3):
-                ops.k.fls_attn_set_variant(var)
-                ts[var].append(timeit(lambda: ops.attention(qq, mm["work"], nh, nkv, hd), a.iters))
-        ops.k.fls_attn_set_variant(3)
-        for var in (1, 2, 3):
-            t = sorted(ts[var])[1]
-            row[f"v{var}_ms"] = t * 1e3
-            row[f"v{var}_tflops"] = att_fl / t / 1e12
+        t = timeit(lambda: ops.attention(qq, mm["work"], nh, nkv, hd, seg_lo=mm["seg_lo"]), a.iters)
+        row.update({"ours_ms": t * 1e3, "ours_tflops": att_fl / t / 1e12})
         res.append(row)
         print(json.dumps(row), flush=True)
     x = torch.randn(M, H, device=dev).half()

@@ -59,8 +59,43 @@ def test_pack_segments():
     assert b.num_tokens == 12
     assert b.positions.tolist() == [0, 1, 2, 3, 4, 3] * 2
     assert b.last_idx.tolist() == [4, 5, 10, 11]
-    assert b.work.shape == (6, 8)
-    assert b.work[1].tolist() == [3, 2, 0, 0, 3, 0, 3, 2]
+    # per prompt: one prefix item + one item over both suffixes (block-diagonal range 1)
+    assert b.work.shape == (4, 8)
+    assert b.work[1].tolist() == [3, 3, 0, 0, 3, 0, 3, 3]
+    assert b.seg_lo.tolist() == [0, 0, 0, 3, 3, 5, 6, 6, 6, 9, 9, 11]
+
+
+@pytest.mark.parametrize("q_block", [64, 128])
+@pytest.mark.parametrize("prefix_attention", ["bidirectional", "causal"])
+def test_work_items_cover_segments(q_block, prefix_attention):
+    """Every packed query row sees, through the work items + seg_lo (the attention kernel's
+    semantics), exactly the keys its segment defines: the whole prefix (or its causal part) and
+    its own suffix up to itself — with suffixes of many lengths sharing items."""
+    from flexible_llm_sharding_amd.runtime.batch import visible_keys
+    from flexible_llm_sharding_amd.utils.tokenizer import TokenizedPrompt
+    rng = np.random.default_rng(3)
+    tps = []
+    for lp, lens in [(70, [5, 64, 1, 3, 100]), (1, [3]), (130, [65, 17, 129, 2]), (200, [33, 64] * 4)]:
+        tps.append(TokenizedPrompt(list(range(lp)), [list(rng.integers(0, 9, l)) for l in lens], max(lens),
+                                   [l - 1 for l in lens]))
+    b = pack_prompts(tps, list(range(len(tps))), prefix_attention, q_block=q_block)
+    assert int(b.work[:, 1].max()) <= q_block
+    covered = np.zeros(b.num_tokens, np.int32)
+    for q_start, q_len, *_ in b.work.tolist():
+        covered[q_start:q_start + q_len] += 1
+    assert (covered == 1).all()                        # every row in exactly one item
+    for sg in b.segments:
+        for i in range(sg.q_len):
+            row = sg.q_start + i
+            want = []
+            if sg.r0_len:
+                qi = sg.q_off + i
+                want.append((0, sg.r0_start, sg.r0_start + (min(sg.r0_len - 1, qi) if sg.r0_causal else sg.r0_len - 1)))
+            if sg.r1_len:
+                want.append((1, sg.r1_start, sg.r1_start + i))
+            assert visible_keys(b.work, b.seg_lo, row) == want, (row, sg)
+    n_sfx_items = int((b.work[:, 7] > 0).sum())
+    assert n_sfx_items == sum(-(-sum(len(s) for s in tp.suffixes) // q_block) for tp in tps)
 
 
 @pytest.mark.parametrize("storage", ["gpu", "cpu", "disk"])

@@ -121,33 +121,27 @@ def test_attention_128_row_items(ops, ref, nh, nkv, hd, mode):
     prompts = [(70, [5, 64, 1]), (1, [3]), (130, [65, 17, 129]), (200, [33, 64])]
     b, qkv = _attn_case(nh, nkv, hd, prompts, mode, q_block=128)
     assert int(b.work[:, 1].max()) == 128
-    y = ops.attention(qkv.to(DEV), b.device_tensors(DEV)["work"], nh, nkv, hd, q_block=128)
+    meta = b.device_tensors(DEV)
+    y = ops.attention(qkv.to(DEV), meta["work"], nh, nkv, hd, q_block=128, seg_lo=meta["seg_lo"])
     r = ref.attention(qkv.float(), b.segments, nh, nkv, hd)
     torch.cuda.synchronize()
     assert rel_err(y.cpu(), r) < 5e-3
 
 
-@pytest.fixture(params=[1, 2, 3], ids=["attn_v1", "attn_v2", "attn_v2db"])
-def attn_variant(request, ops):
-    assert ops.k.fls_attn_set_variant(request.param) == 0
-    yield request.param
-    ops.k.fls_attn_set_variant(3)
-
-
 @pytest.mark.parametrize("nh,nkv,hd", [(4, 2, 64), (8, 1, 128), (2, 2, 128), (16, 2, 128), (12, 2, 64)])
 @pytest.mark.parametrize("mode", ["bidirectional", "causal"])
-def test_attention_shared_prefix(ops, ref, attn_variant, nh, nkv, hd, mode):
+def test_attention_shared_prefix(ops, ref, nh, nkv, hd, mode):
     prompts = [(70, [5, 64, 1]), (1, [3]), (130, [65, 17, 129]), (200, [33, 64])]
     b, qkv = _attn_case(nh, nkv, hd, prompts, mode)
     meta = b.device_tensors(DEV)
-    y = ops.attention(qkv.to(DEV), meta["work"], nh, nkv, hd)
+    y = ops.attention(qkv.to(DEV), meta["work"], nh, nkv, hd, seg_lo=meta["seg_lo"])
     r = ref.attention(qkv.float(), b.segments, nh, nkv, hd)
     torch.cuda.synchronize()
     assert rel_err(y.cpu(), r) < 5e-3
 
 
 @pytest.mark.parametrize("nh,nkv,hd", [(8, 1, 128), (2, 2, 128), (4, 2, 64)])
-def test_attention_prefix_from_cache(ops, ref, attn_variant, nh, nkv, hd):
+def test_attention_prefix_from_cache(ops, ref, nh, nkv, hd):
     """Range 0 read from a separate prefix K/V tensor (prefix cache) == the full packed pass."""
     from flexible_llm_sharding_amd.runtime.batch import pack_prompts
     from flexible_llm_sharding_amd.utils.tokenizer import TokenizedPrompt
@@ -167,13 +161,14 @@ def test_attention_prefix_from_cache(ops, ref, attn_variant, nh, nkv, hd):
     cached = pack_prompts(tps, [0, 1, 2], "bidirectional", prefix_offsets=offs, kv_cached=True)
     keep = np.setdiff1d(np.arange(full.num_tokens), full.pfx_src)       # suffix rows, in packed order
     qkv_s = qkv[torch.from_numpy(keep)].contiguous()
-    y = ops.attention(qkv_s.to(DEV), cached.device_tensors(DEV)["work"], nh, nkv, hd, kv0=cache.to(DEV))
+    cm = cached.device_tensors(DEV)
+    y = ops.attention(qkv_s.to(DEV), cm["work"], nh, nkv, hd, kv0=cache.to(DEV), seg_lo=cm["seg_lo"])
     r = ref.attention(qkv.float(), full.segments, nh, nkv, hd)[torch.from_numpy(keep)]
     torch.cuda.synchronize()
     assert rel_err(y.cpu(), r) < 5e-3
 
 
-def test_attention_softmax_spike(ops, ref, attn_variant):
+def test_attention_softmax_spike(ops, ref):
     # force the online-softmax rescale path: one huge key late in the sequence
     nh, nkv, hd = 2, 1, 128
     b, qkv = _attn_case(nh, nkv, hd, [(200, [40])], "bidirectional", seed=3)
@@ -181,7 +176,48 @@ def test_attention_softmax_spike(ops, ref, attn_variant):
     qkv[150, qs:qs + hd] = 8.0          # key 150 of the prefix
     qkv[:, :qs] = qkv[:, :qs].clamp(-1, 1) + 0.5
     meta = b.device_tensors(DEV)
-    y = ops.attention(qkv.to(DEV), meta["work"], nh, nkv, hd)
+    y = ops.attention(qkv.to(DEV), meta["work"], nh, nkv, hd, seg_lo=meta["seg_lo"])
+    r = ref.attention(qkv.float(), b.segments, nh, nkv, hd)
+    torch.cuda.synchronize()
+    assert torch.isfinite(y).all()
+    assert rel_err(y.cpu(), r) < 5e-3
+
+
+@pytest.mark.parametrize("q_block", [64, 128])
+@pytest.mark.parametrize("nh,nkv,hd", [(8, 2, 128), (4, 4, 128), (4, 2, 64)])
+def test_attention_multi_suffix_items(ops, ref, q_block, nh, nkv, hd):
+    """Work items holding several suffixes of one prompt (short suffixes, one crossing an item
+    boundary): block-diagonal range 1 via seg_lo; the same rows computed with one suffix per item
+    (runtime.batch._work_items) give the same result."""
+    from flexible_llm_sharding_amd.runtime.batch import _work_items
+    prompts = [(100, [3, 5, 1, 10, 7, 2, 60, 9]), (40, [30, 30, 30, 30, 30]), (1, [1, 2])]
+    b, qkv = _attn_case(nh, nkv, hd, prompts, "bidirectional", seed=21, q_block=q_block)
+    assert (b.work[:, 7] > b.work[:, 1]).any() or (b.work[:, 2] > 0).any()    # items span suffixes
+    meta = b.device_tensors(DEV)
+    q = qkv.to(DEV)
+    y = ops.attention(q, meta["work"], nh, nkv, hd, q_block=q_block, seg_lo=meta["seg_lo"])
+    single = torch.from_numpy(_work_items(b.segments, q_block)).to(DEV)
+    y1 = ops.attention(q, single, nh, nkv, hd, q_block=q_block, seg_lo=meta["seg_lo"])
+    r = ref.attention(qkv.float(), b.segments, nh, nkv, hd)
+    torch.cuda.synchronize()
+    assert rel_err(y.cpu(), r) < 5e-3
+    assert rel_err(y1.cpu(), r) < 5e-3
+
+
+@pytest.mark.parametrize("q_block", [64, 128])
+def test_attention_softmax_ramp(ops, ref, q_block):
+    """Scores that grow along the keys, tile after tile, by a little more or a little less than the
+    deferred-rescale threshold (2^8): v4 alternates between keeping the old running max (P up to
+    256) and rescaling O and l; both paths must agree with the fp32 reference."""
+    nh, nkv, hd = 4, 2 if q_block == 64 else 4, 128
+    b, qkv = _attn_case(nh, nkv, hd, [(600, [64, 40]), (300, [130])], "bidirectional", seed=9, q_block=q_block)
+    qs = nh * hd
+    T = qkv.shape[0]
+    ramp = torch.linspace(0.0, 6.0, T).unsqueeze(1)
+    qkv[:, :qs] = 0.25
+    qkv[:, qs:qs + nkv * hd] = ramp + 0.05 * qkv[:, qs:qs + nkv * hd]
+    meta = b.device_tensors(DEV)
+    y = ops.attention(qkv.to(DEV), meta["work"], nh, nkv, hd, q_block=q_block, seg_lo=meta["seg_lo"])
     r = ref.attention(qkv.float(), b.segments, nh, nkv, hd)
     torch.cuda.synchronize()
     assert torch.isfinite(y).all()
