@@ -16,6 +16,12 @@ the slot, so disk reads, PCIe DMA and compute all overlap.
 
 ``resident=True`` gives every shard its own slot and never evicts (the whole
 model stays in the 288 GB HBM — BASELINE config 5).
+
+Tiny shards (the final RMSNorm of a ``layer_num_per_shard=1`` plan: 16 KB) get a
+buffer of their own instead of a full slot, and the full-size shards alternate
+between the slots in their own order: the LM head then loads while the last
+decoder layer computes instead of after it (a 0.5 GB copy the GPU waited for
+at the end of every 70B pass, ``profiles/r2_trace``).
 """
 from __future__ import annotations
 
@@ -49,10 +55,24 @@ class ShardPrefetcher:
         sizes = [self.shard_bytes(k) for k in range(len(self.shards))]
         self.slot_bytes = max(sizes) if sizes else 0
         self.n_slots = max(1, len(self.shards)) if resident else max(1, min(n_slots, len(self.shards) or 1))
-        self._slots: List[Optional[torch.Tensor]] = [None] * self.n_slots
-        self._slot_sizes = ([sizes[k] for k in range(len(self.shards))] if resident else
-                            [self.slot_bytes] * self.n_slots)
-        self._free_ev: List[Optional[torch.cuda.Event]] = [None] * self.n_slots
+        if resident:
+            self._slot_sizes = list(sizes)
+            self._slot_map = list(range(len(self.shards)))
+        else:
+            # shards below 1/32 of a slot (and <= 64 MiB) own a small buffer; the others take the
+            # slots round-robin in their own order
+            tiny = min(self.slot_bytes // 32, 64 << 20)
+            self._slot_sizes = [self.slot_bytes] * self.n_slots
+            self._slot_map, big = [], 0
+            for k, nb in enumerate(sizes):
+                if nb <= tiny and len(self.shards) > self.n_slots:
+                    self._slot_map.append(len(self._slot_sizes))
+                    self._slot_sizes.append(nb)
+                else:
+                    self._slot_map.append(big % self.n_slots)
+                    big += 1
+        self._slots: List[Optional[torch.Tensor]] = [None] * len(self._slot_sizes)
+        self._free_ev: List[Optional[torch.cuda.Event]] = [None] * len(self._slot_sizes)
         self._pending: Dict[int, Future] = {}
         self._ready: Dict[int, Tuple[Optional[torch.cuda.Event], Dict[str, Dict[str, torch.Tensor]], int]] = {}
         self._loaded_resident = set()
@@ -75,7 +95,7 @@ class ShardPrefetcher:
         return sum(_align(self.src.nbytes(self.names[i])) for i in self.shards[k])
 
     def slot_of(self, k: int) -> int:
-        return k if self.resident else k % self.n_slots
+        return self._slot_map[k]
 
     def _slot(self, s: int) -> torch.Tensor:
         if self._slots[s] is None:

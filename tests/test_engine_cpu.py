@@ -364,3 +364,29 @@ def test_last_layer_pruning_is_exact(ctx, prefix_attention):
     for x, y in zip(a, b):
         assert np.abs(x.astype(np.float32) - y.astype(np.float32)).max() < 1e-5
     assert pr.stats["decoder_flops"] < full.stats["decoder_flops"]
+
+
+def test_prefetcher_slot_map_tiny_shards():
+    """lnps=1 on a Llama-2-70B-shaped plan: the final RMSNorm (16 KB) owns a small buffer, the
+    full-size shards alternate between the two slots in their own order, so the LM head's slot is
+    not the last decoder layer's (it loads while that layer computes)."""
+    from flexible_llm_sharding_amd.config import preset
+    from flexible_llm_sharding_amd.parallel.planner import make_plan
+    from flexible_llm_sharding_amd.runtime.prefetch import ShardPrefetcher
+    from flexible_llm_sharding_amd.runtime.weights import HostStore
+    cfg = preset("llama2-70b")
+    names = cfg.layer_names()
+    plan = make_plan(len(names), 1, 1, 0, False)
+    shards = [s for s in plan.my_shards if len(s)]
+    pf = ShardPrefetcher(HostStore(cfg, names=[]), names, shards, "cpu", n_slots=2)
+    k_norm, k_head, k_last = len(shards) - 2, len(shards) - 1, len(shards) - 3
+    assert pf.slot_of(k_norm) >= 2 and pf._slot_sizes[pf.slot_of(k_norm)] == pf.shard_bytes(k_norm)
+    assert {pf.slot_of(k) for k in range(len(shards)) if k != k_norm} == {0, 1}
+    assert pf.slot_of(k_head) != pf.slot_of(k_last)
+    assert pf.slot_of(0) != pf.slot_of(1)
+    assert pf.planned_hbm_bytes() == 2 * pf.slot_bytes + pf.shard_bytes(k_norm)
+    # lnps = 8: no tiny shard, plain alternation
+    plan8 = make_plan(len(names), 8, 1, 0, False)
+    sh8 = [s for s in plan8.my_shards if len(s)]
+    pf8 = ShardPrefetcher(HostStore(cfg, names=[]), names, sh8, "cpu", n_slots=2)
+    assert [pf8.slot_of(k) for k in range(len(sh8))] == [k % 2 for k in range(len(sh8))]
