@@ -65,7 +65,8 @@ def parse(argv=None):
     ap.add_argument("--mode", default="auto", choices=["auto", "mp", "dp"])
     ap.add_argument("--stages", default="round_robin", choices=["round_robin", "contiguous"],
                     help="--mode mp: shard k on GPU k mod N (reference) or one contiguous stage per GPU")
-    ap.add_argument("--token-budget", type=int, default=16384)
+    ap.add_argument("--token-budget", type=int, default=49152)
+    ap.add_argument("--mlp-chunk", type=int, default=16384, help="rows per SwiGLU MLP chunk")
     ap.add_argument("--max-vram-gb", type=float, default=None, help="size token budget / MLP chunk to this HBM cap")
     ap.add_argument("--resident", action="store_true")
     ap.add_argument("--hip-graphs", action="store_true", help="with --resident: whole-forward HIP graph replay")
@@ -204,7 +205,8 @@ def main(argv=None):
                                  resident=a.resident)
     runner = ShardedRunner(cfg, store, dev, tok, layer_num_per_shard=a.lnps, storage_location=a.storage,
                            disk_folder=f"/tmp/fls_bench_spill_{rank}", prefix_attention=a.prefix_attention,
-                           token_budget=a.token_budget, resident=a.resident, comm=comm, data_parallel=dp,
+                           token_budget=a.token_budget, mlp_chunk=a.mlp_chunk, resident=a.resident, comm=comm,
+                           data_parallel=dp,
                            prefetcher=pf, hip_graphs=a.hip_graphs, prune_last_layer=not a.no_prune_last,
                            pipeline_stages=a.stages, max_vram_gb=a.max_vram_gb)
     if runner.vram_plan:

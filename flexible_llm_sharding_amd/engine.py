@@ -46,6 +46,11 @@ from .runtime.weights import LayerSource
 from .utils import trace
 from .utils.tokenizer import TokenizedPrompt, tokenize_prompts
 
+# Default micro-batch: 48k packed tokens (the 70B bench's 43k-token pass is one micro-batch: fewer
+# GEMM tails and per-layer waits, +1.0-1.2% over 16k with 2 GB less device memory in use,
+# profiles/r2_budget_gen); the MLP keeps 16k-row chunks (one 43k chunk measured -1.5%).
+TOKEN_BUDGET = 49152
+
 
 def _parse_fault(rank: int):
     """FLS_FAULT="rank:shard" — fault injection for failure-handling tests."""
@@ -61,7 +66,7 @@ class ShardedRunner:
     def __init__(self, cfg: ModelConfig, source: LayerSource, device="cpu", tokenizer=None,
                  layer_num_per_shard: int = 1, storage_location: str = "cpu",
                  disk_folder: str = "./temp", max_activation_in_cpu: int = 100,
-                 prefix_attention: str = "bidirectional", token_budget: int = 16384,
+                 prefix_attention: str = "bidirectional", token_budget: int = TOKEN_BUDGET,
                  resident: bool = False, comm: Optional[Comm] = None, data_parallel: bool = False,
                  act_dtype: Optional[torch.dtype] = None, n_slots: int = 2,
                  mlp_chunk: int = 16384, prefetcher: Optional[ShardPrefetcher] = None,

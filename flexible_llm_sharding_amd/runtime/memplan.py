@@ -65,13 +65,13 @@ def weight_slot_bytes(cfg: ModelConfig, lnps: int, n_slots: int = 2) -> int:
 
 
 def plan_for_vram(cfg: ModelConfig, max_vram_bytes: int, lnps: int = 1, n_slots: int = 2,
-                  token_budget: int = 16384, mlp_chunk: int = 16384) -> Tuple[int, int, int]:
+                  token_budget: int = 49152, mlp_chunk: int = 16384) -> Tuple[int, int, int]:
     """-> (token_budget, mlp_chunk, estimated peak bytes), the largest pair <= the requested one
     that fits ``max_vram_bytes``; raises if even the smallest does not."""
     weights = weight_slot_bytes(cfg, lnps, n_slots)
     best = None
     # every GEMM wants a large M: prefer the pair with the largest smaller side, then the largest sum
-    for tb in (t for t in sorted({token_budget, 16384, 12288, 8192, 6144, 4096, 3072, 2048, 1024}) if t <= token_budget):
+    for tb in (t for t in sorted({token_budget, 49152, 32768, 24576, 16384, 12288, 8192, 6144, 4096, 3072, 2048, 1024}) if t <= token_budget):
         for mc in (m for m in sorted({mlp_chunk, 16384, 8192, 4096, 2048, 1024}) if m <= min(mlp_chunk, tb)):
             est = weights + activation_bytes(cfg, tb, mc) + DEVICE_OVERHEAD
             key = (min(tb, mc), tb + mc)

@@ -239,3 +239,12 @@ class ShardPrefetcher:
     def close(self):
         if self._pool is not None:
             self._pool.shutdown(wait=True)
+        if self.cuda:
+            torch.cuda.synchronize(self.dev)
+        # drop the HBM slots (and every view into them): a closed runner holds no weights
+        with self.lock:
+            self._pending.clear()
+            self._ready.clear()
+        self._loaded_resident.clear()
+        self._slots = [None] * len(self._slot_sizes)
+        self._free_ev = [None] * len(self._slot_sizes)

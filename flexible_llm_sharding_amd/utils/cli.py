@@ -65,7 +65,8 @@ def build_parser() -> argparse.ArgumentParser:
                    help="data parallel: scatter-load 1/G of each layer per GPU + RCCL all-gather")
     p.add_argument("--pipeline_stages", choices=["round_robin", "contiguous"], default="round_robin",
                    help="model parallel: shard k on GPU k mod G (reference) or one contiguous stage per GPU")
-    p.add_argument("--token_budget", type=int, default=16384, help="max tokens per packed micro-batch")
+    p.add_argument("--token_budget", type=int, default=49152,
+                   help="max tokens per packed micro-batch (MLP still runs in 16k-row chunks)")
     p.add_argument("--max_vram_gb", type=float, default=None,
                    help="HBM cap per GPU: sizes --token_budget and the MLP chunk to fit (reference: 70B in 6 GB)")
     p.add_argument("--dtype", choices=["float16", "float32"], default=None,

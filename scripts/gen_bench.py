@@ -8,6 +8,7 @@ bench.py (random-init weights in pinned host RAM, lnps=1 streaming).
     python scripts/gen_bench.py [--model llama2-70b] [--gen 4] [--prompts 32] [--json out.json]
 """
 import argparse
+import gc
 import json
 import os
 import sys
@@ -40,6 +41,9 @@ class _TimedRunner:
         self.tokens.append(self.r.stats["tokens"])
         return out
 
+    def __getattr__(self, name):          # run_all reads the runner's prefetcher / plan
+        return getattr(self.r, name)
+
 
 def main():
     ap = argparse.ArgumentParser()
@@ -48,6 +52,8 @@ def main():
     ap.add_argument("--prompts", type=int, default=32)
     ap.add_argument("--prefix-len", type=int, default=1024)
     ap.add_argument("--suffix-len", type=int, default=64)
+    ap.add_argument("--resident", action="store_true", help="weights resident in HBM (288 GB holds 70B)")
+    ap.add_argument("--token-budget", type=int, default=16384)
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -59,11 +65,12 @@ def main():
     prompts = synthetic_prompts(a.prompts, a.prefix_len, 5, a.suffix_len, cfg.vocab_size, seed=0)
     args = argparse.Namespace(num_gen_token=a.gen, data_parallel=False, num_batch=1)
     res = {"model": a.model, "prompts": a.prompts, "prefix_len": a.prefix_len, "suffix_len": a.suffix_len,
-           "num_gen_token": a.gen, "layer_num_per_shard": 1, "storage_location": "cpu"}
+           "num_gen_token": a.gen, "layer_num_per_shard": 1, "storage_location": "cpu",
+           "resident": a.resident, "token_budget": a.token_budget}
     scores = {}
     for name, pkv in (("rerun", False), ("prefix_kv_cache", True)):
         r = ShardedRunner(cfg, store, dev, tok, layer_num_per_shard=1, storage_location="cpu",
-                          prefix_kv_cache=pkv)
+                          prefix_kv_cache=pkv, resident=a.resident, token_budget=a.token_budget)
         tr = _TimedRunner(r)
         t = time.perf_counter()
         s, _ = generation_loop(args, tr, Comm(0, 1, dev), tok, prompts)
@@ -76,6 +83,9 @@ def main():
             res[name]["cache_gb"] = round(r.prefix_cache.nbytes / 1e9, 2)
         print(json.dumps({name: res[name]}), flush=True)
         r.close()
+        del r, tr
+        gc.collect()
+        torch.cuda.empty_cache()
         torch.cuda.reset_peak_memory_stats(dev)
     res["max_abs_diff"] = float(max(np.abs(x.astype(np.float32) - y.astype(np.float32)).max()
                                     for x, y in zip(scores["rerun"], scores["prefix_kv_cache"])))
