@@ -68,7 +68,7 @@ class ShardedRunner:
                  disk_folder: str = "./temp", max_activation_in_cpu: int = 100,
                  prefix_attention: str = "bidirectional", token_budget: int = TOKEN_BUDGET,
                  resident: bool = False, comm: Optional[Comm] = None, data_parallel: bool = False,
-                 act_dtype: Optional[torch.dtype] = None, n_slots: int = 2,
+                 act_dtype: Optional[torch.dtype] = None, n_slots: Optional[int] = None,
                  mlp_chunk: int = 16384, prefetcher: Optional[ShardPrefetcher] = None,
                  verbose: bool = False, resume_dir: Optional[str] = None, checkpoint_every: int = 0,
                  max_token_len: int = MAX_TOKEN_LEN, hip_graphs: bool = False,
@@ -86,6 +86,12 @@ class ShardedRunner:
         self.max_act = max_activation_in_cpu
         self.prefix_attention = prefix_attention
         self.vram_plan = None
+        if n_slots is None:
+            # double buffer.  A third slot (2 shards prefetched ahead, straight across call
+            # boundaries) cut the GPU's weight waits from 37 to 26 ms per 70B pass but not the pass
+            # time (the rest of the call-boundary idle is host work), for +1.7 GB of HBM
+            # (profiles/r2_slots): opt-in via n_slots / bench --slots
+            n_slots = 2
         if max_vram_gb:
             # size the micro-batch and the MLP chunk to the HBM cap (runtime/memplan.py)
             from .runtime.memplan import plan_for_vram
@@ -308,7 +314,7 @@ class ShardedRunner:
                     with trace.range(f"shard{k}:acquire"):
                         W = pf.acquire(k)
                     with trace.range(f"shard{k + 1}:prefetch"):
-                        pf.prefetch(k + 1)
+                        self._prefetch_ahead(k)
                     cur_k = k
                     src_rank = self._owner(first - 1) if (mp and first > 0) else comm.rank
                     dst_rank = self._owner(last + 1) if (mp and last + 1 < self.L) else comm.rank
@@ -377,12 +383,7 @@ class ShardedRunner:
         h2d_end = pf.bytes_h2d
         if cur_k >= 0:
             pf.release(cur_k)
-            if self._speculative_prefetch():
-                self._h2d0 = h2d_end
-                # every slot is free again: the next call's first shards stream in under this
-                # call's tail (lm_head, D2H of the scores) and the next tokenization
-                for k in range(min(pf.n_slots, len(self.my_shards))):
-                    pf.prefetch(k)
+        pf.epoch += 1                  # the next call's loads continue the slot round-robin
         for t, w in sends:
             w.wait()
         if self.cuda:
@@ -432,20 +433,37 @@ class ShardedRunner:
         return self.ctx.prune_last and name == self.ctx.last_decoder
 
     def _speculative_prefetch(self) -> bool:
-        """Prefetch the next call's first shards at the end of a call?  Off by default: measured
-        on one MI355X (profiles/r1_host_path) it is neutral on 70B lnps=1 and costs 2% on 7B
-        lnps=8 (the tail's copies compete with the last shard's compute), while the prefetch
-        at the start of ``__call__`` already overlaps tokenization.  ``FLS_SPECULATIVE_PREFETCH=1``
-        turns it on.  Never when resuming (the next call may start elsewhere), resident
-        (nothing to load) or with the data-parallel all-gather prefetcher (no collectives
-        left in flight after a call)."""
+        """Let the prefetch run on into the next call's first shards (same weights every call)?
+        On with 3+ slots: the next call's embedding and first layer then load under this call's
+        last layers, LM head and tokenization (GPU weight waits 37 -> 26 ms per 70B pass, pass time
+        unchanged: profiles/r2_slots).  With 2 slots the only free slot at the end of a call is
+        the last layer's; measured neutral (profiles/r1_host_path, profiles/r2_chunk_spec), off.
+        ``FLS_SPECULATIVE_PREFETCH=0/1`` overrides.  Never when resuming (the next call may start
+        elsewhere), resident (nothing to load), model parallel, or with the data-parallel
+        all-gather prefetcher (no collectives left in flight after a call)."""
         import os
         from .parallel.data_parallel import AllGatherPrefetcher
         pf = self.prefetcher
-        if os.environ.get("FLS_SPECULATIVE_PREFETCH", "0") != "1":
+        env = os.environ.get("FLS_SPECULATIVE_PREFETCH")
+        if env is not None and env != "1":
             return False
-        return (self.cuda and not self.resume_dir and not pf.resident
+        if env is None and pf.n_slots < 3:
+            return False
+        return (self.cuda and not self.resume_dir and not pf.resident and not self.hip_graphs
+                and not (self.plan.mode == "mp" and self.comm.active)
                 and not isinstance(pf, AllGatherPrefetcher))
+
+    def _prefetch_ahead(self, k: int) -> None:
+        """After acquiring shard k: start the next ``n_slots - 1`` loads (each lands in the slot of
+        a shard already released); past the last shard, the next call's first shards."""
+        pf = self.prefetcher
+        n = len(self.my_shards)
+        depth = 1 if pf.resident else max(1, pf.n_slots - 1)
+        for j in range(k + 1, k + 1 + depth):
+            if j < n:
+                pf.prefetch(j)
+            elif j - n < n and self._speculative_prefetch():
+                pf.prefetch(j - n, epoch=pf.epoch + 1)
 
     def _throttle(self, shard_ev: List) -> None:
         """Bound how far the host runs ahead of the GPU to ``RUNAHEAD_SHARDS`` shards.

@@ -107,9 +107,9 @@ class AllGatherPrefetcher(ShardPrefetcher):
         G = self.comm.world
         return sum(_align(self.chunk_bytes(self.names[i]) * G) for i in self.shards[k])
 
-    def _load(self, k: int):
+    def _load(self, k: int, epoch=None):
         t0 = time.perf_counter()
-        s = self.slot_of(k)
+        s = self.slot_of(k, epoch)
         slot = self._slot(s)
         G, r = self.comm.world, self.comm.rank
         views: Dict[str, Dict[str, torch.Tensor]] = {}

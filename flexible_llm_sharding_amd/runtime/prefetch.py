@@ -18,10 +18,14 @@ the slot, so disk reads, PCIe DMA and compute all overlap.
 model stays in the 288 GB HBM — BASELINE config 5).
 
 Tiny shards (the final RMSNorm of a ``layer_num_per_shard=1`` plan: 16 KB) get a
-buffer of their own instead of a full slot, and the full-size shards alternate
-between the slots in their own order: the LM head then loads while the last
+buffer of their own instead of a full slot, and the full-size shards take the
+slots round-robin in their own order: the LM head then loads while the last
 decoder layer computes instead of after it (a 0.5 GB copy the GPU waited for
-at the end of every 70B pass, ``profiles/r2_trace``).
+at the end of every 70B pass, ``profiles/r2_trace``).  The round-robin runs on
+across calls (``epoch``: call e's i-th full-size shard is the (e * n_big + i)-th
+load), so with ``n_slots`` slots the engine can prefetch ``n_slots - 1`` shards
+ahead straight across a call boundary: the slot a shard lands in was always
+last used ``n_slots`` loads earlier, by a shard that is already released.
 """
 from __future__ import annotations
 
@@ -64,13 +68,18 @@ class ShardPrefetcher:
             tiny = min(self.slot_bytes // 32, 64 << 20)
             self._slot_sizes = [self.slot_bytes] * self.n_slots
             self._slot_map, big = [], 0
+            self._big_idx: List[int] = []          # index among the full-size shards, -1: own buffer
             for k, nb in enumerate(sizes):
                 if nb <= tiny and len(self.shards) > self.n_slots:
                     self._slot_map.append(len(self._slot_sizes))
                     self._slot_sizes.append(nb)
+                    self._big_idx.append(-1)
                 else:
                     self._slot_map.append(big % self.n_slots)
+                    self._big_idx.append(big)
                     big += 1
+            self._n_big = big
+        self.epoch = 0                              # calls completed (rotates the slot round-robin)
         self._slots: List[Optional[torch.Tensor]] = [None] * len(self._slot_sizes)
         self._free_ev: List[Optional[torch.cuda.Event]] = [None] * len(self._slot_sizes)
         self._pending: Dict[int, Future] = {}
@@ -94,8 +103,11 @@ class ShardPrefetcher:
     def shard_bytes(self, k: int) -> int:
         return sum(_align(self.src.nbytes(self.names[i])) for i in self.shards[k])
 
-    def slot_of(self, k: int) -> int:
-        return self._slot_map[k]
+    def slot_of(self, k: int, epoch: Optional[int] = None) -> int:
+        if self.resident or self._big_idx[k] < 0:
+            return self._slot_map[k]
+        e = self.epoch if epoch is None else epoch
+        return (self._big_idx[k] + e * self._n_big) % self.n_slots
 
     def _slot(self, s: int) -> torch.Tensor:
         if self._slots[s] is None:
@@ -127,9 +139,9 @@ class ShardPrefetcher:
         return max(self.src.nbytes(n) for n in self.names)
 
     # -------------------------------------------------------------- load
-    def _load(self, k: int):
+    def _load(self, k: int, epoch: Optional[int] = None):
         t0 = time.perf_counter()
-        s = self.slot_of(k)
+        s = self.slot_of(k, epoch)
         views: Dict[str, Dict[str, torch.Tensor]] = {}
         if not self.cuda:
             for i in self.shards[k]:
@@ -170,7 +182,9 @@ class ShardPrefetcher:
         self.load_seconds += time.perf_counter() - t0
         return ev, views, s
 
-    def prefetch(self, k: int) -> None:
+    def prefetch(self, k: int, epoch: Optional[int] = None) -> None:
+        """Start loading shard ``k`` (of call ``epoch``: default the current one; the engine
+        passes ``epoch + 1`` for the next call's first shards)."""
         if k < 0 or k >= len(self.shards):
             return
         with self.lock:
@@ -179,9 +193,9 @@ class ShardPrefetcher:
             if self.resident and k in self._loaded_resident:
                 return
             if self._pool is not None:
-                self._pending[k] = self._pool.submit(self._load, k)
+                self._pending[k] = self._pool.submit(self._load, k, epoch)
                 return
-        r = self._load(k)
+        r = self._load(k, epoch)
         with self.lock:
             self._ready[k] = r
 

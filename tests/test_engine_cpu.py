@@ -390,3 +390,45 @@ def test_prefetcher_slot_map_tiny_shards():
     sh8 = [s for s in plan8.my_shards if len(s)]
     pf8 = ShardPrefetcher(HostStore(cfg, names=[]), names, sh8, "cpu", n_slots=2)
     assert [pf8.slot_of(k) for k in range(len(sh8))] == [k % 2 for k in range(len(sh8))]
+
+
+@pytest.mark.parametrize("lnps,n_slots", [(1, 3), (1, 2), (8, 3), (3, 4)])
+def test_prefetcher_slots_rotate_across_calls(lnps, n_slots):
+    """The engine prefetches n_slots - 1 shards ahead and, past the last shard, the next call's first
+    shards (epoch + 1).  Replaying that order over several calls: every load lands in a slot whose
+    previous occupant was already released, and two shards live at the same time never share one."""
+    from flexible_llm_sharding_amd.config import preset
+    from flexible_llm_sharding_amd.parallel.planner import make_plan
+    from flexible_llm_sharding_amd.runtime.prefetch import ShardPrefetcher
+    from flexible_llm_sharding_amd.runtime.weights import HostStore
+    cfg = preset("llama2-70b")
+    names = cfg.layer_names()
+    shards = [s for s in make_plan(len(names), lnps, 1, 0, False).my_shards if len(s)]
+    pf = ShardPrefetcher(HostStore(cfg, names=[]), names, shards, "cpu", n_slots=n_slots)
+    n, depth = len(shards), n_slots - 1
+    occupant = {}                 # slot -> (epoch, shard) loaded last
+    released, loaded = set(), set()
+
+    def load(e, k):
+        if (e, k) in loaded:
+            return
+        s = pf.slot_of(k, e)
+        prev = occupant.get(s)
+        assert prev is None or prev in released, (e, k, s, prev)
+        occupant[s] = (e, k)
+        loaded.add((e, k))
+
+    for e in range(4):
+        pf.epoch = e
+        for k in range(min(n_slots, n)):        # __call__: the first shards (no-op if already loaded)
+            load(e, k)
+        for k in range(n):
+            if k:
+                released.add((e, k - 1))
+            load(e, k)                          # acquire
+            for j in range(k + 1, k + 1 + depth):
+                if j < n:
+                    load(e, j)
+                elif j - n < n:
+                    load(e + 1, j - n)          # speculative: the next call's first shards
+        released.add((e, n - 1))
