@@ -70,6 +70,8 @@ def parse(argv=None):
     ap.add_argument("--slots", type=int, default=None, help="HBM weight slots (default 2; 3 prefetches across call boundaries)")
     ap.add_argument("--max-vram-gb", type=float, default=None, help="size token budget / MLP chunk to this HBM cap")
     ap.add_argument("--resident", action="store_true")
+    ap.add_argument("--hbm-cache-gb", type=float, default=0.0,
+                    help="keep this many GB of layers resident in HBM, stream the rest (not the headline config)")
     ap.add_argument("--hip-graphs", action="store_true", help="with --resident: whole-forward HIP graph replay")
     ap.add_argument("--no-prune-last", action="store_true",
                     help="compute every row in the last decoder layer (A/B of the scored-rows-only layer)")
@@ -207,7 +209,7 @@ def main(argv=None):
     runner = ShardedRunner(cfg, store, dev, tok, layer_num_per_shard=a.lnps, storage_location=a.storage,
                            disk_folder=f"/tmp/fls_bench_spill_{rank}", prefix_attention=a.prefix_attention,
                            token_budget=a.token_budget, mlp_chunk=a.mlp_chunk, resident=a.resident, comm=comm,
-                           data_parallel=dp, n_slots=a.slots,
+                           data_parallel=dp, n_slots=a.slots, hbm_cache_gb=a.hbm_cache_gb,
                            prefetcher=pf, hip_graphs=a.hip_graphs, prune_last_layer=not a.no_prune_last,
                            pipeline_stages=a.stages, max_vram_gb=a.max_vram_gb)
     if runner.vram_plan:
@@ -291,7 +293,7 @@ def main(argv=None):
                                    (f"dp{world}-allgather-weights" if dp else "single")),
                    "weights": a.weights, "resident": a.resident, "hip_graphs": bool(runner.hip_graphs),
                    "token_budget": runner.token_budget, "mlp_chunk": runner.mlp_chunk,
-                   "weight_slots": runner.prefetcher.n_slots,
+                   "weight_slots": runner.prefetcher.n_slots, "hbm_cache_gb": a.hbm_cache_gb,
                    "max_vram_gb": a.max_vram_gb},
     }
     if rank == 0:

@@ -110,6 +110,7 @@ def build_runner(args, cfg: ModelConfig, device, comm: Comm, tok) -> ShardedRunn
                          checkpoint_every=getattr(args, "checkpoint_every", 0),
                          max_token_len=getattr(args, "max_token_len", None) or MAX_TOKEN_LEN,
                          hip_graphs=getattr(args, "hip_graphs", False),
+                         hbm_cache_gb=getattr(args, "hbm_cache_gb", 0.0) or 0.0,
                          prefix_kv_cache=getattr(args, "prefix_kv_cache", False),
                          prefix_cache_entries=getattr(args, "prefix_cache_entries", 8),
                          pipeline_stages=getattr(args, "pipeline_stages", "round_robin"),

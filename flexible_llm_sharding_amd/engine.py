@@ -74,7 +74,7 @@ class ShardedRunner:
                  max_token_len: int = MAX_TOKEN_LEN, hip_graphs: bool = False,
                  prefix_kv_cache: bool = False, prefix_cache_entries: int = 8,
                  prune_last_layer: bool = True, pipeline_stages: str = "round_robin",
-                 max_vram_gb: Optional[float] = None):
+                 max_vram_gb: Optional[float] = None, hbm_cache_gb: float = 0.0):
         self.cfg = cfg
         self.src = source
         self.dev = torch.device(device)
@@ -125,8 +125,15 @@ class ShardedRunner:
         self.ctx.last_decoder = decs[-1] if decs else ""
         my = [s for s in self.plan.my_shards if len(s)]
         self.my_shards = my
+        keep = None
+        if hbm_cache_gb and prefetcher is None and not resident:
+            if max_vram_gb:
+                raise ValueError("--hbm_cache_gb and --max_vram_gb are exclusive (a cache needs HBM, a cap limits it)")
+            from .runtime.prefetch import choose_kept_shards
+            sizes = [sum(source.nbytes(self.names[i]) for i in sh) for sh in my]
+            keep = choose_kept_shards(sizes, int(hbm_cache_gb * 1e9))
         self.prefetcher = prefetcher or ShardPrefetcher(source, self.names, my, self.dev,
-                                                        n_slots=n_slots, resident=resident)
+                                                        n_slots=n_slots, resident=resident, keep=keep)
         if self.vram_plan is not None and self.cuda:
             # the weight slots are raw hipMalloc blocks: the allocator gets the rest of the cap
             from .runtime.memplan import cap_allocator
@@ -459,11 +466,18 @@ class ShardedRunner:
         pf = self.prefetcher
         n = len(self.my_shards)
         depth = 1 if pf.resident else max(1, pf.n_slots - 1)
-        for j in range(k + 1, k + 1 + depth):
+        issued, j = 0, k + 1
+        while issued < depth and j < k + 1 + n:
             if j < n:
-                pf.prefetch(j)
+                kk, ep = j, None
             elif j - n < n and self._speculative_prefetch():
-                pf.prefetch(j - n, epoch=pf.epoch + 1)
+                kk, ep = j - n, pf.epoch + 1
+            else:
+                break
+            if not pf.is_kept_loaded(kk):     # kept shards already in HBM do not count
+                pf.prefetch(kk, epoch=ep)
+                issued += 1
+            j += 1
 
     def _throttle(self, shard_ev: List) -> None:
         """Bound how far the host runs ahead of the GPU to ``RUNAHEAD_SHARDS`` shards.

@@ -15,7 +15,10 @@ loader thread through the native streamer's pinned chunk ring straight into
 the slot, so disk reads, PCIe DMA and compute all overlap.
 
 ``resident=True`` gives every shard its own slot and never evicts (the whole
-model stays in the 288 GB HBM — BASELINE config 5).
+model stays in the 288 GB HBM — BASELINE config 5).  ``keep`` does that for a
+subset (``--hbm_cache_gb``: as many shards as the budget holds, spread evenly
+over the pass by :func:`choose_kept_shards`), the rest keep streaming: each
+streamed load then has the kept shards' compute to hide under.
 
 Tiny shards (the final RMSNorm of a ``layer_num_per_shard=1`` plan: 16 KB) get a
 buffer of their own instead of a full slot, and the full-size shards take the
@@ -45,10 +48,28 @@ def _align(n: int) -> int:
     return (n + ALIGN_BYTES - 1) // ALIGN_BYTES * ALIGN_BYTES
 
 
+def choose_kept_shards(sizes: Sequence[int], budget: int) -> List[int]:
+    """Shards to keep resident under ``budget`` bytes, spread evenly over the pass (a kept
+    shard every ~total/budget shards), so the streamed loads between them stay evenly spaced."""
+    total = sum(sizes)
+    if budget <= 0 or total <= 0:
+        return []
+    if budget >= total:
+        return list(range(len(sizes)))
+    f, acc, left, keep = budget / total, 0.0, budget, []
+    for k, nb in enumerate(sizes):
+        acc += f
+        if acc >= 1.0 and nb <= left:
+            keep.append(k)
+            left -= nb
+            acc -= 1.0
+    return keep
+
+
 class ShardPrefetcher:
     def __init__(self, source: LayerSource, layer_names: Sequence[str],
                  shards: Sequence[Tuple[int, ...]], device, n_slots: int = 2,
-                 resident: bool = False, dtype=torch.float16):
+                 resident: bool = False, dtype=torch.float16, keep: Optional[Sequence[int]] = None):
         self.src = source
         self.names = list(layer_names)
         self.shards = [tuple(s) for s in shards]
@@ -56,8 +77,11 @@ class ShardPrefetcher:
         self.cuda = self.dev.type == "cuda"
         self.dtype = dtype
         self.resident = resident
+        # shards that stay in HBM after their first load (all of them when resident)
+        self._sticky = set(range(len(self.shards))) if resident else set(keep or ())
         sizes = [self.shard_bytes(k) for k in range(len(self.shards))]
-        self.slot_bytes = max(sizes) if sizes else 0
+        streamed = [nb for k, nb in enumerate(sizes) if k not in self._sticky]
+        self.slot_bytes = max(streamed or sizes) if sizes else 0
         self.n_slots = max(1, len(self.shards)) if resident else max(1, min(n_slots, len(self.shards) or 1))
         if resident:
             self._slot_sizes = list(sizes)
@@ -70,7 +94,7 @@ class ShardPrefetcher:
             self._slot_map, big = [], 0
             self._big_idx: List[int] = []          # index among the full-size shards, -1: own buffer
             for k, nb in enumerate(sizes):
-                if nb <= tiny and len(self.shards) > self.n_slots:
+                if k in self._sticky or (nb <= tiny and len(self.shards) > self.n_slots):
                     self._slot_map.append(len(self._slot_sizes))
                     self._slot_sizes.append(nb)
                     self._big_idx.append(-1)
@@ -190,7 +214,7 @@ class ShardPrefetcher:
         with self.lock:
             if k in self._ready or k in self._pending:
                 return
-            if self.resident and k in self._loaded_resident:
+            if k in self._sticky and k in self._loaded_resident:
                 return
             if self._pool is not None:
                 self._pending[k] = self._pool.submit(self._load, k, epoch)
@@ -220,10 +244,17 @@ class ShardPrefetcher:
             cur.wait_event(ev)
             e1.record(cur)
             self._stall_ev.append((e0, e1))
-        if self.resident:
+        if k in self._sticky:
             self._loaded_resident.add(k)
         self.wait_seconds += time.perf_counter() - t0
         return views
+
+    def is_kept_loaded(self, k: int) -> bool:
+        """Shard k stays in HBM and is already there (prefetching it is a no-op)."""
+        return k in self._sticky and k in self._loaded_resident
+
+    def kept_bytes(self) -> int:
+        return sum(self.shard_bytes(k) for k in self._sticky)
 
     def take_wait_seconds(self) -> float:
         """Host time spent in :meth:`acquire` waiting for loads since the last call."""
@@ -238,7 +269,7 @@ class ShardPrefetcher:
         return t
 
     def release(self, k: int) -> None:
-        if self.resident:
+        if k in self._sticky:
             return
         with self.lock:
             ent = self._ready.pop(k, None)

@@ -53,7 +53,8 @@ def main():
     ap.add_argument("--prefix-len", type=int, default=1024)
     ap.add_argument("--suffix-len", type=int, default=64)
     ap.add_argument("--resident", action="store_true", help="weights resident in HBM (288 GB holds 70B)")
-    ap.add_argument("--token-budget", type=int, default=16384)
+    ap.add_argument("--token-budget", type=int, default=49152)
+    ap.add_argument("--hbm-cache-gb", type=float, default=0.0, help="layers kept resident in HBM, the rest streamed")
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -66,11 +67,12 @@ def main():
     args = argparse.Namespace(num_gen_token=a.gen, data_parallel=False, num_batch=1)
     res = {"model": a.model, "prompts": a.prompts, "prefix_len": a.prefix_len, "suffix_len": a.suffix_len,
            "num_gen_token": a.gen, "layer_num_per_shard": 1, "storage_location": "cpu",
-           "resident": a.resident, "token_budget": a.token_budget}
+           "resident": a.resident, "token_budget": a.token_budget, "hbm_cache_gb": a.hbm_cache_gb}
     scores = {}
     for name, pkv in (("rerun", False), ("prefix_kv_cache", True)):
         r = ShardedRunner(cfg, store, dev, tok, layer_num_per_shard=1, storage_location="cpu",
-                          prefix_kv_cache=pkv, resident=a.resident, token_budget=a.token_budget)
+                          prefix_kv_cache=pkv, resident=a.resident, token_budget=a.token_budget,
+                          hbm_cache_gb=a.hbm_cache_gb)
         tr = _TimedRunner(r)
         t = time.perf_counter()
         s, _ = generation_loop(args, tr, Comm(0, 1, dev), tok, prompts)

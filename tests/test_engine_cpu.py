@@ -432,3 +432,37 @@ def test_prefetcher_slots_rotate_across_calls(lnps, n_slots):
                 elif j - n < n:
                     load(e + 1, j - n)          # speculative: the next call's first shards
         released.add((e, n - 1))
+
+
+def test_choose_kept_shards_spread_and_budget():
+    from flexible_llm_sharding_amd.runtime.prefetch import choose_kept_shards
+    sizes = [5] + [17] * 80 + [1, 5]                    # embed, 80 layers, norm, head (GB-ish units)
+    for budget in (0, 17, 100, 17 * 40, 1000, sum(sizes)):
+        keep = choose_kept_shards(sizes, budget)
+        assert sum(sizes[k] for k in keep) <= budget
+        assert keep == sorted(set(keep))
+    assert choose_kept_shards(sizes, sum(sizes)) == list(range(len(sizes)))
+    half = choose_kept_shards(sizes, sum(sizes) // 2)
+    gaps = np.diff(half)
+    assert len(half) >= 35 and gaps.max() <= 3         # kept shards interleave with streamed ones
+
+
+@pytest.mark.parametrize("frac", [0.5, 1.0])
+def test_hbm_cache_keeps_shards_and_matches(ctx, frac):
+    """--hbm_cache_gb: some (or all) shards stay loaded across calls, the rest stream; scores equal
+    the plain streaming run on every call, kept shards are never re-read."""
+    path, cfg, tok, prompts, sd = ctx
+    src = FileLayerSource(cfg, path)
+    gb = frac * sum(src.nbytes(n) for n in cfg.layer_names()) / 1e9
+    base = ShardedRunner(cfg, FileLayerSource(cfg, path), "cpu", tok, layer_num_per_shard=1, token_budget=60)
+    r = ShardedRunner(cfg, src, "cpu", tok, layer_num_per_shard=1, token_budget=60, hbm_cache_gb=gb)
+    pf = r.prefetcher
+    kept = sorted(pf._sticky)
+    assert kept and (frac < 1.0) == (len(kept) < len(r.my_shards))
+    want = base(prompts)
+    for _ in range(2):
+        got = r(prompts)
+        for a, b in zip(got, want):
+            assert np.array_equal(a, b)
+    assert all(pf.is_kept_loaded(k) for k in kept)
+    assert not any(pf.is_kept_loaded(k) for k in range(len(r.my_shards)) if k not in kept)

@@ -235,3 +235,29 @@ def test_dp_allgather_prefetcher_over_rccl(setup, tmp_path, streaming):
         r.close()
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("slots", [2, 3])
+def test_hbm_cache_and_slot_rotation(setup, slots):
+    """Half the shards kept in HBM (--hbm_cache_gb) and 2 or 3 rotating weight slots (3: prefetch
+    across call boundaries): three calls give the plain double-buffered run's scores bitwise, and
+    the kept shards are loaded once."""
+    path, cfg, tok, prompts, ref = setup
+    src = FileLayerSource(cfg, path)
+    gb = 0.5 * sum(src.nbytes(n) for n in cfg.layer_names()) / 1e9
+    base = ShardedRunner(cfg, FileLayerSource(cfg, path), "cuda:0", tok, layer_num_per_shard=1, token_budget=200)
+    want = base(prompts)
+    base.close()
+    r = ShardedRunner(cfg, src, "cuda:0", tok, layer_num_per_shard=1, token_budget=200, hbm_cache_gb=gb,
+                      n_slots=slots)
+    kept = sorted(r.prefetcher._sticky)
+    assert 0 < len(kept) < len(r.my_shards)
+    h2d = []
+    for _ in range(3):
+        got = r(prompts)
+        h2d.append(r.stats["weight_h2d_bytes"])
+        for a, b in zip(got, want):
+            assert np.array_equal(a, b)
+    kept_bytes = r.prefetcher.kept_bytes()
+    assert h2d[2] < sum(src.nbytes(n) for n in cfg.layer_names()) - 0.9 * kept_bytes
+    r.close()
