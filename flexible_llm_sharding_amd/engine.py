@@ -228,7 +228,7 @@ class ShardedRunner:
         t_start = time.perf_counter()
         n = len(tps)
         entry, cached = self._prefix_entry(tps)
-        groups = split_microbatches(tps, self.token_budget, suffix_only=cached)
+        groups = split_microbatches(tps, self.micro_budget(tps, cached), suffix_only=cached)
         batches = [pack_prompts([tps[i] for i in g], g, self.prefix_attention,
                                 prefix_offsets=[entry.offsets[i] for i in g] if entry is not None else None,
                                 kv_cached=cached, q_block=self.q_block) for g in groups]
@@ -251,6 +251,25 @@ class ShardedRunner:
                 self.prefix_cache.misses += 1
         self.stats["prefix_cached"] = float(cached)
         return outputs
+
+    # model parallel: micro-batches per pipeline stage wanted before the budget may shrink, and the
+    # smallest budget it shrinks to (GEMM efficiency falls off below ~8k rows)
+    MP_MICRO_PER_STAGE = 2
+    MP_MIN_BUDGET = 8192
+
+    def micro_budget(self, tps, cached: bool = False) -> int:
+        """Token budget of this call's micro-batches.  Model parallel: a rank computes its next
+        layer only when the previous stage hands over a micro-batch, so with fewer micro-batches
+        than stages every rank idles part of each round (utilisation ~ micro-batches / stages);
+        the budget then shrinks so that there are >= MP_MICRO_PER_STAGE x stages micro-batches
+        (not below MP_MIN_BUDGET tokens).  Every rank tokenizes the same prompts, so all ranks
+        derive the same split."""
+        b = self.token_budget
+        if self.plan.mode == "mp" and self.comm.world > 1:
+            total = sum(tp.num_tokens - (len(tp.prefix) if cached else 0) for tp in tps)
+            want = -(-total // (self.MP_MICRO_PER_STAGE * self.comm.world))
+            b = min(b, max(self.MP_MIN_BUDGET, want))
+        return b
 
     def _prefix_entry(self, tps):
         """-> (PrefixEntry or None, cached?).  Model-parallel ranks agree (identical packing)."""

@@ -466,3 +466,24 @@ def test_hbm_cache_keeps_shards_and_matches(ctx, frac):
             assert np.array_equal(a, b)
     assert all(pf.is_kept_loaded(k) for k in kept)
     assert not any(pf.is_kept_loaded(k) for k in range(len(r.my_shards)) if k not in kept)
+
+
+def test_mp_micro_budget_fills_pipeline():
+    """Model parallel: the per-call micro-batch budget shrinks so each of G stages sees >= 2
+    micro-batches (not below 8k tokens); single / data parallel keep --token_budget."""
+    from types import SimpleNamespace
+    from flexible_llm_sharding_amd.utils.tokenizer import TokenizedPrompt
+    tps = [TokenizedPrompt([1] * 1024, [[1] * 64] * 5, 64, [63] * 5) for _ in range(256)]   # 344k tokens
+    total = sum(tp.num_tokens for tp in tps)
+    for mode, world, want in (("mp", 8, -(-total // 16)), ("mp", 2, 49152), ("single", 1, 49152),
+                              ("dp", 8, 49152)):
+        r = SimpleNamespace(token_budget=49152, plan=SimpleNamespace(mode=mode), comm=SimpleNamespace(world=world),
+                            MP_MICRO_PER_STAGE=2, MP_MIN_BUDGET=8192)
+        b = ShardedRunner.micro_budget(r, tps)
+        assert b == want, (mode, world, b)
+        if mode == "mp":
+            assert len(split_microbatches(tps, b)) >= 2 * world
+    small = tps[:8]                                  # 10.8k tokens: the 8k floor wins
+    r = SimpleNamespace(token_budget=49152, plan=SimpleNamespace(mode="mp"), comm=SimpleNamespace(world=8),
+                        MP_MICRO_PER_STAGE=2, MP_MIN_BUDGET=8192)
+    assert ShardedRunner.micro_budget(r, small) == 8192
