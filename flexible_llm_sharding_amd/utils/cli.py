@@ -55,7 +55,7 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--hbm_cache_gb", type=float, default=0.0,
                    help="keep this many GB of shards resident in HBM after their first load, spread evenly "
                         "over the pass; the others stream every pass (generation steps with a partly "
-                        "cached model move fewer bytes over PCIe)")
+                        "cached model move fewer bytes over PCIe; single-GPU and model-parallel runs)")
     p.add_argument("--weight_cache", choices=["auto", "host", "stream", "disk"], default="auto",
                    help="host: read every layer once into pinned host RAM (needs ~model-size RAM); "
                         "stream (alias disk, the reference behaviour): re-read the per-layer safetensors every "
