@@ -87,11 +87,13 @@ class ShardedRunner:
         self.prefix_attention = prefix_attention
         self.vram_plan = None
         if n_slots is None:
-            # double buffer.  A third slot (2 shards prefetched ahead, straight across call
-            # boundaries) cut the GPU's weight waits from 37 to 26 ms per 70B pass but not the pass
-            # time (the rest of the call-boundary idle is host work), for +1.7 GB of HBM
-            # (profiles/r2_slots): opt-in via n_slots / bench --slots
-            n_slots = 2
+            # Multi-layer shards: three slots, so the next call's first shard (several layers, more
+            # than tokenization hides) streams in under this call's last shards: 7B lnps=8 +8%,
+            # 70B lnps=4 +1.6% (profiles/r2_slots7b).  lnps=1: the double buffer — the third slot
+            # only moved host-bound idle around on 70B (+1.7 GB of HBM for 0%, profiles/r2_slots).
+            # Under a VRAM cap, for resident weights or an external (data-parallel) prefetcher: 2.
+            n_slots = 3 if (self.cuda and layer_num_per_shard > 1 and not resident and not max_vram_gb
+                            and prefetcher is None) else 2
         if max_vram_gb:
             # size the micro-batch and the MLP chunk to the HBM cap (runtime/memplan.py)
             from .runtime.memplan import plan_for_vram
