@@ -94,6 +94,8 @@ def build_runner(args, cfg: ModelConfig, device, comm: Comm, tok) -> ShardedRunn
     device = torch.device(device)
     if args.data_parallel and comm.world > 1 and args.dp_weight_shard:
         from .parallel.data_parallel import build_dp_sharded_runner
+        if getattr(args, "hbm_cache_gb", 0.0):
+            print("--hbm_cache_gb is not used with the data-parallel all-gather weight path", file=sys.stderr)
         wc = resolve_weight_cache(args, cfg, comm, cfg.layer_names(), sliced=True)
         return build_dp_sharded_runner(args, cfg, device, comm, tok, weight_cache=wc)
     src = build_source(args, cfg, comm, device)
