@@ -199,7 +199,12 @@ class ShardedRunner:
                 self._h2d0 = self.prefetcher.bytes_h2d
             for k in range(min(self.prefetcher.n_slots, len(self.my_shards))):
                 self.prefetcher.prefetch(k)
-        return self.run_tokenized(self.tokenize(prompts))
+        t0 = time.perf_counter()
+        tps = self.tokenize(prompts)
+        t_tok = time.perf_counter() - t0
+        out = self.run_tokenized(tps)
+        self.stats["host_tokenize_s"] = t_tok
+        return out
 
     def _get_store(self) -> ActivationStore:
         if self._store is None:
@@ -234,6 +239,7 @@ class ShardedRunner:
         batches = [pack_prompts([tps[i] for i in g], g, self.prefix_attention,
                                 prefix_offsets=[entry.offsets[i] for i in g] if entry is not None else None,
                                 kv_cached=cached, q_block=self.q_block) for g in groups]
+        t_pack = time.perf_counter() - t_start
         if self.hip_graphs:
             return self._run_graphed(tps, batches, t_start)
         self.ctx.prefix_entry = entry
@@ -252,6 +258,7 @@ class ShardedRunner:
             else:
                 self.prefix_cache.misses += 1
         self.stats["prefix_cached"] = float(cached)
+        self.stats["host_pack_s"] = t_pack
         return outputs
 
     # model parallel: micro-batches per pipeline stage wanted before the budget may shrink, and the
