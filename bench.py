@@ -67,7 +67,7 @@ def parse(argv=None):
                     help="--mode mp: shard k on GPU k mod N (reference) or one contiguous stage per GPU")
     ap.add_argument("--token-budget", type=int, default=49152)
     ap.add_argument("--mlp-chunk", type=int, default=16384, help="rows per SwiGLU MLP chunk")
-    ap.add_argument("--slots", type=int, default=None, help="HBM weight slots (default: 3 for lnps > 1, else 2; 3 prefetches across call boundaries)")
+    ap.add_argument("--slots", type=int, default=None, help="HBM weight slots (default 3, 2 under --max-vram-gb; 3 prefetches across call boundaries)")
     ap.add_argument("--max-vram-gb", type=float, default=None, help="size token budget / MLP chunk to this HBM cap")
     ap.add_argument("--resident", action="store_true")
     ap.add_argument("--hbm-cache-gb", type=float, default=0.0,

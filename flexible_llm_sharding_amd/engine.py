@@ -87,13 +87,13 @@ class ShardedRunner:
         self.prefix_attention = prefix_attention
         self.vram_plan = None
         if n_slots is None:
-            # Multi-layer shards: three slots, so the next call's first shard (several layers, more
-            # than tokenization hides) streams in under this call's last shards: 7B lnps=8 +8%,
-            # 70B lnps=4 +1.6% (profiles/r2_slots7b).  lnps=1: the double buffer — the third slot
-            # only moved host-bound idle around on 70B (+1.7 GB of HBM for 0%, profiles/r2_slots).
-            # Under a VRAM cap, for resident weights or an external (data-parallel) prefetcher: 2.
-            n_slots = 3 if (self.cuda and layer_num_per_shard > 1 and not resident and not max_vram_gb
-                            and prefetcher is None) else 2
+            # Three rotating slots (the embedding / LM head in buffers of their own), so the next
+            # call's first layers stream in under this call's last ones and no pass waits for its
+            # weights at the call boundary: 70B lnps=1 +0.9% (36 -> 1 ms weight wait per pass,
+            # profiles/r2_slots_own), 7B lnps=8 +7.8%, 70B lnps=4 +1.6% (profiles/r2_slots7b), for
+            # +2.8 GB of HBM on 70B.  The double buffer under a VRAM cap (the 6 GB mode), for
+            # resident weights and for the external data-parallel prefetcher.
+            n_slots = 3 if (self.cuda and not resident and not max_vram_gb and prefetcher is None) else 2
         if max_vram_gb:
             # size the micro-batch and the MLP chunk to the HBM cap (runtime/memplan.py)
             from .runtime.memplan import plan_for_vram
@@ -469,10 +469,10 @@ class ShardedRunner:
 
     def _speculative_prefetch(self) -> bool:
         """Let the prefetch run on into the next call's first shards (same weights every call)?
-        On with 3+ slots: the next call's embedding and first layer then load under this call's
-        last layers, LM head and tokenization (GPU weight waits 37 -> 26 ms per 70B pass, pass time
-        unchanged: profiles/r2_slots).  With 2 slots the only free slot at the end of a call is
-        the last layer's; measured neutral (profiles/r1_host_path, profiles/r2_chunk_spec), off.
+        On with 3+ slots (the default): the next call's embedding and first layer then load under
+        this call's last layers (profiles/r2_slots_own, profiles/r2_slots7b).  With 2 slots the
+        only free slot at the end of a call is the last layer's; measured neutral
+        (profiles/r1_host_path, profiles/r2_chunk_spec), off.
         ``FLS_SPECULATIVE_PREFETCH=0/1`` overrides.  Never when resuming (the next call may start
         elsewhere), resident (nothing to load), model parallel, or with the data-parallel
         all-gather prefetcher (no collectives left in flight after a call)."""
@@ -489,8 +489,9 @@ class ShardedRunner:
                 and not isinstance(pf, AllGatherPrefetcher))
 
     def _prefetch_ahead(self, k: int) -> None:
-        """After acquiring shard k: start the next ``n_slots - 1`` loads (each lands in the slot of
-        a shard already released); past the last shard, the next call's first shards."""
+        """After acquiring shard k: start loads up to the ``n_slots - 1``-th next shard that uses the
+        rotating slots (each lands in the slot of a shard already released; shards with a buffer of
+        their own on the way load too); past the last shard, the next call's first shards."""
         pf = self.prefetcher
         n = len(self.my_shards)
         depth = 1 if pf.resident else max(1, pf.n_slots - 1)
@@ -502,9 +503,12 @@ class ShardedRunner:
                 kk, ep = j - n, pf.epoch + 1
             else:
                 break
-            if not pf.is_kept_loaded(kk):     # kept shards already in HBM do not count
+            if not pf.is_kept_loaded(kk):     # kept shards already in HBM load nothing
                 pf.prefetch(kk, epoch=ep)
-                issued += 1
+                # with 3+ slots own-buffer shards do not use up the lookahead (the double buffer
+                # keeps its one-shard lookahead: data-parallel ranks issue gathers in that order)
+                if pf.n_slots < 3 or pf.in_rotation(kk):
+                    issued += 1
             j += 1
 
     def _throttle(self, shard_ev: List) -> None:

@@ -88,8 +88,13 @@ class ShardPrefetcher:
             self._slot_map = list(range(len(self.shards)))
         else:
             # shards below 1/32 of a slot (and <= 64 MiB) own a small buffer; the others take the
-            # slots round-robin in their own order
+            # slots round-robin in their own order.  With 3+ slots, shards up to a third of a slot
+            # (70B lnps=1: the 0.5 GB embedding and LM head) own a buffer too, so the rotation holds
+            # only the big shards and the lookahead reaches the next call's first layer while the
+            # second-to-last one still computes (the last, pruned layer is too short to hide it)
             tiny = min(self.slot_bytes // 32, 64 << 20)
+            if self.n_slots >= 3:
+                tiny = self.slot_bytes // 3
             self._slot_sizes = [self.slot_bytes] * self.n_slots
             self._slot_map, big = [], 0
             self._big_idx: List[int] = []          # index among the full-size shards, -1: own buffer
@@ -248,6 +253,10 @@ class ShardPrefetcher:
             self._loaded_resident.add(k)
         self.wait_seconds += time.perf_counter() - t0
         return views
+
+    def in_rotation(self, k: int) -> bool:
+        """Shard k loads into the rotating slots (not a buffer of its own)."""
+        return not self.resident and self._big_idx[k] >= 0
 
     def is_kept_loaded(self, k: int) -> bool:
         """Shard k stays in HBM and is already there (prefetching it is a no-op)."""

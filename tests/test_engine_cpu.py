@@ -426,12 +426,15 @@ def test_prefetcher_slots_rotate_across_calls(lnps, n_slots):
             if k:
                 released.add((e, k - 1))
             load(e, k)                          # acquire
-            for j in range(k + 1, k + 1 + depth):
-                if j < n:
-                    load(e, j)
-                elif j - n < n:
-                    load(e + 1, j - n)          # speculative: the next call's first shards
+            issued, j = 0, k + 1                # ShardedRunner._prefetch_ahead
+            while issued < depth and j < k + 1 + n:
+                ee, kk = (e, j) if j < n else (e + 1, j - n)   # past the end: the next call's shards
+                load(ee, kk)
+                issued += n_slots < 3 or pf.in_rotation(kk)   # own buffers: free lookahead (3+ slots)
+                j += 1
         released.add((e, n - 1))
+    if n_slots >= 3 and lnps == 1:              # embedding and LM head own buffers: rotation = decoders
+        assert not pf.in_rotation(0) and not pf.in_rotation(n - 1) and pf.in_rotation(1)
 
 
 def test_choose_kept_shards_spread_and_budget():
