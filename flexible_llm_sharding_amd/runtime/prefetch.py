@@ -1,13 +1,14 @@
-"""Double-buffered shard prefetcher: host (pinned / file) -> HBM weight slots.
+"""Shard prefetcher: host (pinned / file) -> rotating HBM weight slots.
 
 Reference: each shard's layers are loaded synchronously before compute
 (``/root/reference/utils.py:230-233``) and unloaded to ``meta`` with
 ``empty_cache`` afterwards (``utils.py:299-302``) — compute and weight I/O
 never overlap.
 
-Here HBM holds ``n_slots`` fixed weight slots (2 = double buffer, allocated
-once; no per-shard free).  Shard ``k+1`` is copied into the other slot on a
-dedicated copy stream while shard ``k`` computes; the compute stream waits on
+Here HBM holds ``n_slots`` fixed weight slots (allocated once; no per-shard
+free; the engine uses 3, or 2 = a double buffer under a VRAM cap).  The next
+shards are copied into the other slots on a dedicated copy stream while shard
+``k`` computes; the compute stream waits on
 a per-shard *ready* event, and the copy stream waits on the slot's *free*
 event recorded when the compute stream finished with its previous occupant.
 File-backed sources (:class:`~.stream.FileLayerSource`) are streamed by a
