@@ -17,8 +17,10 @@ MI355X design of the same schedule:
   micro-batch's H2D overlapping the current one's compute;
 * model parallel (reference default for >1 GPU): shard k runs on rank
   k mod G exactly like ``utils.py:151-153``; hand-offs between ranks are
-  RCCL ``isend``/``irecv`` over xGMI with every receive posted at shard start
-  (no polling, no shared state), keyed by micro-batch.
+  RCCL ``isend``/``irecv`` over xGMI issued in a per-rank program fixed before
+  the pass (:func:`~.parallel.pipeline.build_programs`: no receive queued ahead
+  of work it depends on) into a bounded, runner-lifetime
+  :class:`~.parallel.pipeline.StageInbox` (no polling, no shared state).
 * data parallel: each rank runs all shards on its slice of prompts; weights
   can be scatter-loaded 1/G per rank and all-gathered over xGMI
   (:mod:`.parallel.data_parallel`).
@@ -37,7 +39,7 @@ from .models.layout import layer_kind
 from .models.llama import ExecContext, layer_flops, rope_tables, run_layer
 from .ops import get_ops
 from .parallel.comm import Comm
-from .parallel.pipeline import rx_key
+from .parallel.pipeline import StageInbox, build_programs, host_wait, rank_items, rx_key
 from .parallel.planner import ShardPlan, make_plan
 from .runtime.activations import ActivationStore
 from .runtime.batch import Q_BLOCK, Q_BLOCK_MHA, PackedBatch, pack_prompts, split_microbatches
@@ -74,7 +76,7 @@ class ShardedRunner:
                  max_token_len: int = MAX_TOKEN_LEN, hip_graphs: bool = False,
                  prefix_kv_cache: bool = False, prefix_cache_entries: int = 8,
                  prune_last_layer: bool = True, pipeline_stages: str = "round_robin",
-                 max_vram_gb: Optional[float] = None, hbm_cache_gb: float = 0.0):
+                 max_vram_gb: Optional[float] = None, hbm_cache_gb: float = 0.0, rx_window: int = 2):
         self.cfg = cfg
         self.src = source
         self.dev = torch.device(device)
@@ -83,7 +85,11 @@ class ShardedRunner:
         self.lnps = layer_num_per_shard
         self.storage = storage_location
         self.disk_folder = disk_folder
+        # model parallel: parked (early-received) activations per tier before the next slower one
+        # (utils.py:179-180's back-pressure bound, parallel/pipeline.py)
         self.max_act = max_activation_in_cpu
+        self.rx_window = rx_window
+        self.resident = resident
         self.prefix_attention = prefix_attention
         self.vram_plan = None
         if n_slots is None:
@@ -153,6 +159,8 @@ class ShardedRunner:
         self.h2d_stream = torch.cuda.Stream(self.dev) if self.cuda else None
         self.d2h_stream = torch.cuda.Stream(self.dev) if self.cuda else None
         self._store: Optional[ActivationStore] = None
+        self._inbox: Optional[StageInbox] = None
+        self._mp_start_layer = 0
         # whole-forward HIP graphs: only when every shard is local AND resident (fixed weight pointers)
         self.hip_graphs = bool(hip_graphs and self.cuda and resident and self.plan.mode != "mp"
                                and not resume_dir)
@@ -193,7 +201,7 @@ class ShardedRunner:
     # ------------------------------------------------------------- main
     def __call__(self, prompts) -> List[np.ndarray]:
         """Reference API: list of (prefix, suffixes) -> list of [n_s, 1, V] fp16 arrays."""
-        if self.my_shards and not self.resume_dir and not self.hip_graphs:
+        if self.my_shards and prompts and not self.resume_dir and not self.hip_graphs:
             # the first shards' weights do not depend on the prompts: their H2D overlaps tokenization
             if self._h2d0 is None:
                 self._h2d0 = self.prefetcher.bytes_h2d
@@ -206,6 +214,20 @@ class ShardedRunner:
         self.stats["host_tokenize_s"] = t_tok
         return out
 
+    def _get_inbox(self) -> StageInbox:
+        if self._inbox is None:
+            self._inbox = StageInbox(self.comm, self.dev, self.act_dtype, self.storage, self.disk_folder,
+                                     str(self.comm.rank), window=self.rx_window, max_parked=self.max_act,
+                                     h2d_stream=self.h2d_stream, d2h_stream=self.d2h_stream)
+        return self._inbox
+
+    def _mp_program(self, n_batches: int):
+        """This rank's hand-off program (every rank derives all ranks' plans: same result)."""
+        plans = {r: make_plan(self.L, self.lnps, self.comm.world, r, False, self.plan.stages)
+                 for r in range(self.comm.world)}
+        progs = build_programs(plans, n_batches, self._mb_major(), self._mp_start_layer)
+        return progs[self.comm.rank]
+
     def _get_store(self) -> ActivationStore:
         if self._store is None:
             self._store = ActivationStore(self.storage, self.dev, self.disk_folder,
@@ -213,16 +235,26 @@ class ShardedRunner:
                                           h2d_stream=self.h2d_stream, d2h_stream=self.d2h_stream)
         return self._store
 
+    def _mb_major(self) -> bool:
+        """Model parallel with contiguous stages held resident: micro-batch-major order (a
+        micro-batch runs through the whole stage and moves on), so stage r+1 starts after one
+        micro-batch instead of after stage r's whole pass.  Same on every rank (a global flag)."""
+        return self.plan.mode == "mp" and self.plan.stages == "contiguous" and self.resident
+
     def schedule(self, n_batches: int):
         """Flat (shard, micro-batch) order.
 
         Single-GPU / data-parallel runs visit micro-batches in zigzag order
         (0..n-1, then n-1..0, ...) so the micro-batch that ends shard k starts
         shard k+1 and its activation never leaves HBM; the model-parallel
-        pipeline keeps the natural order every rank's send/recv sequence
-        expects.
+        pipeline uses :func:`~.parallel.pipeline.rank_items` (shard-major, or
+        micro-batch-major for resident contiguous stages), the order
+        :func:`~.parallel.pipeline.build_programs` derives every rank's
+        send / receive program from.
         """
-        zig = self.plan.mode != "mp"
+        if self.plan.mode == "mp":
+            return rank_items(self.my_shards, n_batches, self._mb_major())
+        zig = True
         items = []
         for k in range(len(self.my_shards)):
             order = range(n_batches)
@@ -306,13 +338,13 @@ class ShardedRunner:
         flops = 0.0
         compute_s = 0.0
         sends = []
-        rx_err = None
         # weight bytes of this call: counted from its early prefetch (or the previous call's
         # speculative one), not from the first acquire
         h2d0 = pf.bytes_h2d if self._h2d0 is None else self._h2d0
         self._h2d0 = None
         items = self.schedule(len(batches))
-        if not items and self.my_shards and getattr(pf, "collective", False):
+        collective = getattr(pf, "collective", False)
+        if not items and self.my_shards and collective:
             # a data-parallel rank with no prompts in this call still joins every shard's weight
             # all-gather, so all ranks issue the same collective sequence
             for k in range(len(self.my_shards)):
@@ -327,10 +359,21 @@ class ShardedRunner:
         carry = {}                     # micro-batch -> device activation kept across a shard boundary
         pos = {it: i for i, it in enumerate(items)}
         shard_ev: List = []            # end-of-shard events on the compute stream (host run-ahead bound)
-        rx = self._start_receiver(items, batches, k0, bool(ck_loaded)) if mp and comm.active else None
+        prog = inbox = None
+        if mp and comm.active and items:
+            prog = self._mp_program(len(batches))
+            if list(prog.items) != list(items):
+                raise RuntimeError("model-parallel program does not match this rank's schedule")
+            inbox = self._get_inbox()
+            inbox.begin_call(max([self._rx_bytes(k, batches[b]) for (k, b), s in zip(items, prog.src)
+                                  if s is not None] or [0]))
         cur_k = -1
         W = None
-        from_rx = False
+        ok = False
+        # data parallel: the next shard's all-gather is enqueued after this shard's first compute
+        # (a collective kernel sharing a hardware queue with compute then sits behind it, never
+        # ahead of it); single GPU / model parallel: right after the acquire
+        prefetch_due = -1
         if self.my_shards and items:
             pf.prefetch(items[0][0])
         pbar = self._progress(len(items))
@@ -348,23 +391,26 @@ class ShardedRunner:
                         self._throttle(shard_ev)
                     with trace.range(f"shard{k}:acquire"):
                         W = pf.acquire(k)
-                    with trace.range(f"shard{k + 1}:prefetch"):
-                        self._prefetch_ahead(k)
                     cur_k = k
-                    src_rank = self._owner(first - 1) if (mp and first > 0) else comm.rank
+                    if collective:
+                        prefetch_due = k
+                    else:
+                        with trace.range(f"shard{k + 1}:prefetch"):
+                            self._prefetch_ahead(k)
                     dst_rank = self._owner(last + 1) if (mp and last + 1 < self.L) else comm.rank
-                    # a stage whose input comes from another rank reads the receiver thread's store,
-                    # except the shard a model-parallel resume restarts at (inputs from the checkpoint)
-                    from_rx = rx is not None and first > 0 and src_rank != comm.rank and not (
-                        ck_loaded and k == k0)
 
                 batch, meta = batches[b], metas[b]
+                if prog is not None:
+                    for c in prog.posts[idx]:         # receives due before this item (program order)
+                        kc, bc = items[c]
+                        inbox.post(rx_key(kc, bc), prog.src[c], self._state_shape(self.my_shards[kc][0] - 1,
+                                                                                  batches[bc]),
+                                   park=c in prog.parked)
+                from_rx = prog is not None and prog.src[idx] is not None
                 if first == 0:
                     state = None
                 elif from_rx:
-                    state = rx.get(rx_key(k, b))
-                    if b + 1 < len(batches):
-                        rx.prefetch(rx_key(k, b + 1))
+                    state = inbox.get(rx_key(k, b))
                 elif b in carry:
                     state = carry.pop(b)
                 else:
@@ -374,7 +420,10 @@ class ShardedRunner:
                 # one-ahead activation prefetch (crosses shard boundaries)
                 if idx + 1 < len(items):
                     k2, b2 = items[idx + 1]
-                    if self.my_shards[k2][0] > 0 and k2 == k:
+                    if prog is not None and prog.src[idx + 1] is not None:
+                        if idx + 1 in prog.parked:
+                            inbox.prefetch(rx_key(k2, b2))
+                    elif self.my_shards[k2][0] > 0 and k2 == k:
                         store.prefetch(b2)
                     elif k2 != k and idx + 2 < len(items):
                         store.prefetch(items[idx + 2][1])
@@ -386,15 +435,21 @@ class ShardedRunner:
                         if layer_kind(name) == "decoder":
                             flops += layer_flops(self.cfg, batch, self._pruned(name))
                 compute_s += time.perf_counter() - tc
+                if prefetch_due == k:
+                    prefetch_due = -1
+                    with trace.range(f"shard{k + 1}:prefetch"):
+                        self._prefetch_ahead(k)
                 if pbar is not None:
                     pbar.update(1)
                 if ck is not None and not mp and self._ckpt_due(k):
                     ck.save_state(self._ckpt_key(k), b, state)     # single / DP: a shard's outputs
+                send_w = None
                 if last == self.L - 1:
                     out_pending.append(self._start_output_copy(batch, state))
                 elif dst_rank != comm.rank:
                     st = state.contiguous()
-                    sends.append((st, comm.isend(st, dst_rank)))
+                    send_w = comm.isend(st, dst_rank)
+                    sends.append((st, send_w))
                 elif self.storage != "gpu" and pos.get((k + 1, b), len(items)) - idx <= self.CARRY_WINDOW:
                     # re-used within CARRY_WINDOW micro-batch computes (the zigzag boundary micro-batch
                     # and its neighbour): a PCIe round trip would only add traffic, keep it in HBM
@@ -402,23 +457,34 @@ class ShardedRunner:
                 else:
                     store.put(b, state)
                 del state
-                # pending sends are retired per micro-batch: the consumer's receiver thread drains them
+                if from_rx:
+                    inbox.release(rx_key(k, b), send_w)
+                # pending sends are retired per micro-batch (the consumer posts its receive at the
+                # point of use); at most SEND_WINDOW outputs stay alive waiting for their consumer
                 sends = [(t, w) for (t, w) in sends if not w.is_completed()]
+                while len(sends) > self.SEND_WINDOW:
+                    host_wait(sends.pop(0)[1], cuda=self.cuda)
             if ck is not None and mp and cur_k >= 0 and self._ckpt_due(cur_k):
                 ck.commit(self._ckpt_key(cur_k), range(len(batches)), self.act_dtype)
+            ok = True
         finally:
-            if rx is not None:
-                rx_err = None
-                try:
-                    rx.close()
-                except BaseException as e:  # noqa: BLE001
-                    rx_err = e
-        if rx is not None and rx_err is not None:
-            raise rx_err
+            if not ok:
+                # an aborted pass: the held shard is released and every loaded-but-unused shard
+                # forgotten, so a later call's loads never land on weights still waiting to be used
+                if cur_k >= 0:
+                    pf.release(cur_k)
+                    cur_k = -1
+                if not collective:
+                    pf.discard_loaded()
+                if inbox is not None:
+                    inbox.abort()
         h2d_end = pf.bytes_h2d
         if cur_k >= 0:
             pf.release(cur_k)
-        pf.epoch += 1                  # the next call's loads continue the slot round-robin
+        if items:
+            pf.epoch += 1              # the next call's loads continue the slot round-robin
+        elif not collective:
+            pf.discard_loaded()        # nothing ran: drop the early prefetch
         for t, w in sends:
             w.wait()
         if self.cuda:
@@ -427,6 +493,10 @@ class ShardedRunner:
             torch.cuda.current_stream(self.dev).synchronize()
             self.h2d_stream.synchronize()
             self.d2h_stream.synchronize()
+        rx_stats = {}
+        if inbox is not None:
+            inbox.end_call()
+            rx_stats = {f"rx_{k}": float(v) for k, v in inbox.stats.items()}
         for batch, host, ev, pool_buf in out_pending:
             probs = host.numpy()
             r = 0
@@ -456,6 +526,7 @@ class ShardedRunner:
             "weight_stall_gpu_s": pf.take_stall_seconds() if self.cuda else 0.0,
             "act_stall_gpu_s": store.take_stall_seconds() if self.cuda else 0.0,
         }
+        self.stats.update(rx_stats)
         if self.verbose:
             # utils.py:304 prints "loaded N layers in Ts" per device
             n_layers = sum(len(s) for s in self.my_shards[k0:])
@@ -463,6 +534,13 @@ class ShardedRunner:
                   f"(exposed weight wait); {len(self.my_shards)} shards, {len(batches)} micro-batches, "
                   f"{self.stats['tokens']:.0f} tokens in {wall:.2f}s")
         return outputs
+
+    # model parallel: outputs waiting for their consumer before the host waits for the oldest
+    SEND_WINDOW = 3
+
+    def _rx_bytes(self, k: int, batch: PackedBatch) -> int:
+        shape = self._state_shape(self.my_shards[k][0] - 1, batch)
+        return int(np.prod(shape)) * torch.empty((), dtype=self.act_dtype).element_size()
 
     def _pruned(self, name: str) -> bool:
         return self.ctx.prune_last and name == self.ctx.last_decoder
@@ -623,6 +701,7 @@ class ShardedRunner:
         Data-parallel ranks agree on a shard they all hold.  Model-parallel ranks agree on the
         latest stage boundary whose consumer holds its inputs: every rank skips the shards
         before it, the consumer restarts from the checkpointed inputs, the others as usual."""
+        self._mp_start_layer = 0
         if not self.resume_dir or not self.my_shards:
             return None, 0, {}
         from .runtime.checkpoint import RunCheckpoint, run_fingerprint
@@ -639,6 +718,7 @@ class ShardedRunner:
             Lc = max(usable) if usable else 0
             if Lc == 0:
                 return ck, 0, {}
+            self._mp_start_layer = Lc
             k0 = next((k for k, sh in enumerate(self.my_shards) if sh[0] >= Lc), len(self.my_shards))
             loaded = ck.load(Lc) if k0 < len(self.my_shards) and self.my_shards[k0][0] == Lc else {}
             if self.verbose:
@@ -651,24 +731,6 @@ class ShardedRunner:
         if k0 and self.verbose:
             print(f"rank{self.comm.rank}: resuming at shard {k0} from {ck.dir}")
         return ck, k0, (ck.load(k0) if k0 else {})
-
-    def _start_receiver(self, items, batches, k0: int, resumed: bool):
-        """Receiver thread for every (shard, micro-batch) this rank gets from another rank."""
-        from .parallel.pipeline import StageReceiver
-        jobs, seen = [], set()
-        for k, b in items:
-            sh = self.my_shards[k]
-            if sh[0] == 0 or (resumed and k == k0):
-                continue
-            src = self._owner(sh[0] - 1)
-            if src == self.comm.rank:
-                continue
-            jobs.append((rx_key(k, b), src, self._state_shape(sh[0] - 1, batches[b])))
-            seen.add(k)
-        if not jobs:
-            return None
-        return StageReceiver(self.comm, self.dev, self.act_dtype, self.storage, self.disk_folder,
-                             str(self.comm.rank), jobs)
 
     def _start_output_copy(self, batch: PackedBatch, probs: torch.Tensor):
         if not self.cuda:
@@ -686,6 +748,9 @@ class ShardedRunner:
         return batch, host, ev, pool_buf
 
     def close(self):
+        if self._inbox is not None:
+            self._inbox.close()
+            self._inbox = None
         self.prefetcher.close()
         if hasattr(self.src, "close"):
             self.src.close()           # the streaming source's pinned ring

@@ -157,3 +157,162 @@ class Comm:
     def destroy(self):
         if self.active and dist.is_initialized():
             dist.destroy_process_group()
+
+
+class LoopbackHub:
+    """Shared state of a :class:`LoopbackComm` world: ``world`` ranks as threads of one process.
+
+    Point-to-point messages are matched per directed edge in posting order (the RCCL / NCCL
+    rule) and transferred as soon as both sides are posted, whichever posts second issuing the
+    copy (CUDA: on the receive's posting stream, after the send's event — no host waits).
+    Every send / receive a rank posts is appended to ``log[rank]`` as
+    ``("send" | "recv", src, dst, seq)`` in submission order, which
+    :func:`~.pipeline.simulate_single_queue` can replay."""
+
+    def __init__(self, world: int, timeout_s: float = 300.0):
+        import threading
+        from collections import defaultdict
+        self.world = world
+        self.timeout_s = timeout_s
+        self.cv = threading.Condition()
+        self.sends = defaultdict(dict)           # (src, dst) -> seq -> _LoopOp (send side)
+        self.recvs = defaultdict(dict)           # (src, dst) -> seq -> _LoopOp (receive side)
+        self.n_send = defaultdict(int)
+        self.n_recv = defaultdict(int)
+        self.log: List[List[tuple]] = [[] for _ in range(world)]
+        self._coll: dict = {}
+        self._coll_round = [0] * world
+
+    def exchange(self, rank: int, obj: Any) -> List[Any]:
+        """All ranks deposit ``obj``; every rank gets the list (a blocking collective)."""
+        with self.cv:
+            rnd = self._coll_round[rank]
+            self._coll_round[rank] += 1
+            slot = self._coll.setdefault(rnd, {})
+            slot[rank] = obj
+            self.cv.notify_all()
+            if not self.cv.wait_for(lambda: len(slot) == self.world, timeout=self.timeout_s):
+                raise TimeoutError("loopback collective timed out")
+            return [slot[r] for r in range(self.world)]
+
+    def _transfer(self, snd: "_LoopOp", rcv: "_LoopOp") -> None:
+        """Both sides posted: copy (caller holds ``cv``)."""
+        if rcv.t.is_cuda:
+            s = rcv.stream
+            if snd.ev is not None:
+                s.wait_event(snd.ev)
+            with torch.cuda.stream(s):
+                rcv.t.copy_(snd.t, non_blocking=True)
+            snd.t.record_stream(s)
+            ev = torch.cuda.Event()
+            ev.record(s)
+            snd.done_ev = rcv.done_ev = ev
+        else:
+            rcv.t.copy_(snd.t)
+        snd.done = rcv.done = True
+        self.cv.notify_all()
+
+    def post(self, kind: str, edge, t: torch.Tensor) -> "_LoopWork":
+        op = _LoopOp(t)
+        with self.cv:
+            if kind == "send":
+                seq = self.n_send[edge]
+                self.n_send[edge] += 1
+                self.sends[edge][seq] = op
+                self.log[edge[0]].append(("send", edge[0], edge[1], seq))
+                peer = self.recvs[edge].pop(seq, None)
+                if peer is not None:
+                    self.sends[edge].pop(seq)
+                    self._transfer(op, peer)
+            else:
+                seq = self.n_recv[edge]
+                self.n_recv[edge] += 1
+                self.recvs[edge][seq] = op
+                self.log[edge[1]].append(("recv", edge[0], edge[1], seq))
+                peer = self.sends[edge].pop(seq, None)
+                if peer is not None:
+                    self.recvs[edge].pop(seq)
+                    self._transfer(peer, op)
+        return _LoopWork(self, op, f"{kind} {edge}#{seq}")
+
+
+class _LoopOp:
+    def __init__(self, t: torch.Tensor):
+        self.t = t
+        self.ev = None
+        self.stream = None
+        if t.is_cuda:
+            self.stream = torch.cuda.current_stream(t.device)
+            self.ev = torch.cuda.Event()
+            self.ev.record(self.stream)
+        self.done = False
+        self.done_ev = None
+
+
+class _LoopWork:
+    """Work of a loopback send / receive.  CUDA: ``wait()`` orders the CURRENT stream after the
+    transfer (the host only waits until the peer has posted); CPU: blocks until copied."""
+
+    def __init__(self, hub: LoopbackHub, op: _LoopOp, name: str):
+        self.hub, self.op, self.name = hub, op, name
+
+    def wait(self) -> bool:
+        hub, op = self.hub, self.op
+        with hub.cv:
+            if not hub.cv.wait_for(lambda: op.done, timeout=hub.timeout_s):
+                raise TimeoutError(f"loopback {self.name}: peer never posted")
+        if op.done_ev is not None:
+            torch.cuda.current_stream(op.t.device).wait_event(op.done_ev)
+        return True
+
+    def is_completed(self) -> bool:
+        op = self.op
+        if not op.done:
+            return False
+        return op.done_ev is None or op.done_ev.query()
+
+
+class LoopbackComm(Comm):
+    """``Comm`` for ``world`` ranks as threads of one process (tests / rehearsal): sends and
+    receives are device copies ordered by events (no RCCL), collectives go through the hub."""
+
+    def __init__(self, hub: LoopbackHub, rank: int, device=None):
+        super().__init__(rank, hub.world, device, "loopback")
+        self.hub = hub
+
+    def dup(self) -> "LoopbackComm":
+        raise NotImplementedError("loopback comm: one communicator per world")
+
+    def setup_p2p_edges(self, edges) -> None:
+        self._edge_groups = {}
+
+    def isend(self, t: torch.Tensor, dst: int):
+        return self.hub.post("send", (self.rank, dst), t)
+
+    def irecv(self, t: torch.Tensor, src: int):
+        return self.hub.post("recv", (src, self.rank), t)
+
+    def barrier(self):
+        self.hub.exchange(self.rank, None)
+
+    def all_reduce_max(self, x: float) -> float:
+        return max(self.hub.exchange(self.rank, x))
+
+    def all_reduce_min(self, x: float) -> float:
+        return min(self.hub.exchange(self.rank, x))
+
+    def all_reduce_sum(self, x: float) -> float:
+        return sum(self.hub.exchange(self.rank, x))
+
+    def broadcast_object(self, obj: Any, src: int = 0) -> Any:
+        return self.hub.exchange(self.rank, obj)[src]
+
+    def gather_object(self, obj: Any, dst: int = 0) -> Optional[List[Any]]:
+        allv = self.hub.exchange(self.rank, obj)
+        return allv if self.rank == dst else None
+
+    def all_gather_object(self, obj: Any) -> List[Any]:
+        return self.hub.exchange(self.rank, obj)
+
+    def destroy(self):
+        pass

@@ -40,7 +40,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 
-from ..models.layout import ALIGN_BYTES
+from ..models.layout import ALIGN_BYTES, layer_kind
 from . import hostmem
 from .weights import LayerSource
 
@@ -81,26 +81,35 @@ class ShardPrefetcher:
         # shards that stay in HBM after their first load (all of them when resident)
         self._sticky = set(range(len(self.shards))) if resident else set(keep or ())
         sizes = [self.shard_bytes(k) for k in range(len(self.shards))]
-        streamed = [nb for k, nb in enumerate(sizes) if k not in self._sticky]
+        n_rot_slots = max(1, min(n_slots, len(self.shards) or 1))
+        # shards that own a buffer instead of a rotating slot: kept (sticky) shards; with 3+ slots
+        # every shard without a decoder layer (70B lnps=1: the 0.5 GB embedding and LM head; for
+        # large-vocab models like Llama-3.1-8B they are the LARGEST shards), so the
+        # rotation holds only decoder shards and the lookahead reaches the next call's first layer
+        # while the second-to-last one still computes (the last, pruned layer is too short to hide
+        # it); below 3 slots only shards under 1/32 of a decoder shard (the final norm: 16 KB)
+        aux = [all(layer_kind(self.names[i]) != "decoder" for i in sh) for sh in self.shards]
+        dec = [nb for k, nb in enumerate(sizes) if k not in self._sticky and not aux[k]]
+        ref = max(dec) if dec else max([nb for k, nb in enumerate(sizes) if k not in self._sticky] or sizes or [0])
+        many = len(self.shards) > n_rot_slots
+        own = []
+        for k, nb in enumerate(sizes):
+            o = k in self._sticky
+            if not resident and not o and many:
+                o = (aux[k] and n_rot_slots >= 3) or nb <= min(ref // 32, 64 << 20)
+            own.append(o)
+        streamed = [nb for k, nb in enumerate(sizes) if not own[k]]
         self.slot_bytes = max(streamed or sizes) if sizes else 0
-        self.n_slots = max(1, len(self.shards)) if resident else max(1, min(n_slots, len(self.shards) or 1))
+        self.n_slots = max(1, len(self.shards)) if resident else n_rot_slots
         if resident:
             self._slot_sizes = list(sizes)
             self._slot_map = list(range(len(self.shards)))
         else:
-            # shards below 1/32 of a slot (and <= 64 MiB) own a small buffer; the others take the
-            # slots round-robin in their own order.  With 3+ slots, shards up to a third of a slot
-            # (70B lnps=1: the 0.5 GB embedding and LM head) own a buffer too, so the rotation holds
-            # only the big shards and the lookahead reaches the next call's first layer while the
-            # second-to-last one still computes (the last, pruned layer is too short to hide it)
-            tiny = min(self.slot_bytes // 32, 64 << 20)
-            if self.n_slots >= 3:
-                tiny = self.slot_bytes // 3
             self._slot_sizes = [self.slot_bytes] * self.n_slots
             self._slot_map, big = [], 0
-            self._big_idx: List[int] = []          # index among the full-size shards, -1: own buffer
+            self._big_idx: List[int] = []          # index among the rotating shards, -1: own buffer
             for k, nb in enumerate(sizes):
-                if k in self._sticky or (nb <= tiny and len(self.shards) > self.n_slots):
+                if own[k]:
                     self._slot_map.append(len(self._slot_sizes))
                     self._slot_sizes.append(nb)
                     self._big_idx.append(-1)
@@ -254,6 +263,25 @@ class ShardPrefetcher:
             self._loaded_resident.add(k)
         self.wait_seconds += time.perf_counter() - t0
         return views
+
+    def discard_loaded(self) -> None:
+        """Forget every loaded or loading shard that was never acquired (after an empty or aborted
+        pass).  Their slots are then free for any later load: nothing computes on them, and a
+        later copy into the same slot is ordered behind theirs on the copy stream.  Without this a
+        shard loaded at epoch e could be overwritten by a load of the next call's round-robin
+        before being used."""
+        with self.lock:
+            pend = list(self._pending.items())
+            self._pending.clear()
+        for _, f in pend:
+            try:
+                f.result()
+            except Exception:  # noqa: BLE001 - the load is being dropped anyway
+                pass
+        with self.lock:
+            for k in list(self._ready):
+                if k not in self._sticky:
+                    del self._ready[k]
 
     def in_rotation(self, k: int) -> bool:
         """Shard k loads into the rotating slots (not a buffer of its own)."""
