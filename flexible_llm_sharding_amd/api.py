@@ -90,14 +90,78 @@ def build_source(args, cfg: ModelConfig, comm: Comm, device: torch.device):
     return HostStore.from_source(src, pinned=device.type == "cuda", names=mine)
 
 
-def build_runner(args, cfg: ModelConfig, device, comm: Comm, tok) -> ShardedRunner:
+def repeated_passes(args) -> bool:
+    """The same weights stream more than once per run (reference: every generation step and every
+    batch re-streams the whole model, ``main.py:19-23,65-76``)."""
+    return getattr(args, "num_gen_token", 1) > 1 or getattr(args, "num_batch", 1) > 1
+
+
+def resolve_prefix_kv_cache(args) -> bool:
+    """``--prefix_kv_cache auto``: on for greedy generation (exact: later steps re-score the same
+    prefixes, runtime/prefix_cache.py)."""
+    v = getattr(args, "prefix_kv_cache", False)
+    if v == "auto":
+        return getattr(args, "num_gen_token", 1) > 1 and not getattr(args, "resume_dir", None)
+    return bool(v)
+
+
+def prefix_kv_bytes(cfg: ModelConfig, tok, prompts, n_decoders: int, elem: int = 2) -> int:
+    """HBM the prefix K/V cache needs for ``prompts`` (post-RoPE K and V of every prefix token,
+    every decoder layer this rank runs)."""
+    if tok is None or not prompts:
+        return 0
+    n = sum(len(tok(p[0]).input_ids) for p in prompts)
+    return n * 2 * cfg.num_key_value_heads * cfg.head_dim * elem * n_decoders
+
+
+def auto_hbm_cache_bytes(args, cfg: ModelConfig, device: torch.device, reserve: int = 0,
+                         n_slots: int = 3) -> int:
+    """Free HBM minus this run's activation plan (weight slots, one micro-batch's activations and
+    workspace, ``reserve`` — e.g. the prefix K/V cache — and a 4 GB margin)."""
+    if device.type != "cuda":
+        return 0
+    from .runtime.memplan import DEVICE_OVERHEAD, activation_bytes, weight_slot_bytes
+    free, _ = torch.cuda.mem_get_info(device)
+    need = (weight_slot_bytes(cfg, args.layer_num_per_shard, n_slots)
+            + activation_bytes(cfg, getattr(args, "token_budget", 49152), 16384)
+            + DEVICE_OVERHEAD + reserve + int(4e9))
+    return max(0, free - need)
+
+
+def resolve_hbm_cache_gb(args, cfg: ModelConfig, device: torch.device, reserve: int = 0) -> float:
+    """``--hbm_cache_gb auto``: repeated passes keep as many shards in HBM as fit (the 70B model
+    in full on one MI355X, so only the first pass crosses PCIe); a single pass caches nothing."""
+    v = getattr(args, "hbm_cache_gb", 0.0)
+    if v != "auto":
+        return float(v or 0.0)
+    if (device.type != "cuda" or not repeated_passes(args) or getattr(args, "resident", False)
+            or getattr(args, "max_vram_gb", None) or getattr(args, "resume_dir", None)):
+        return 0.0
+    return auto_hbm_cache_bytes(args, cfg, device, reserve) / 1e9
+
+
+def build_runner(args, cfg: ModelConfig, device, comm: Comm, tok, prompts=None) -> ShardedRunner:
     device = torch.device(device)
+    from .models.layout import layer_kind
+    pkv = resolve_prefix_kv_cache(args)
+    n_dec = sum(1 for n in cfg.layer_names() if layer_kind(n) == "decoder")
+    if not args.data_parallel and comm.world > 1:
+        n_dec = -(-n_dec // comm.world)
+    reserve = prefix_kv_bytes(cfg, tok, prompts, n_dec) if pkv else 0
     if args.data_parallel and comm.world > 1 and args.dp_weight_shard:
         from .parallel.data_parallel import build_dp_sharded_runner
-        if getattr(args, "hbm_cache_gb", 0.0):
+        hv = getattr(args, "hbm_cache_gb", 0.0)
+        if hv not in ("auto", 0, 0.0, None):
             print("--hbm_cache_gb is not used with the data-parallel all-gather weight path", file=sys.stderr)
+        if hv == "auto" and not args.resident and device.type == "cuda" and repeated_passes(args):
+            # repeated passes: gather every layer once and keep it (resident) when the model fits
+            from .models.layout import layer_layout
+            model = sum(layer_layout(cfg, layer_kind(n)).nbytes for n in cfg.layer_names())
+            if model <= auto_hbm_cache_bytes(args, cfg, device, reserve, n_slots=0):
+                args = copy.copy(args)
+                args.resident = True
         wc = resolve_weight_cache(args, cfg, comm, cfg.layer_names(), sliced=True)
-        return build_dp_sharded_runner(args, cfg, device, comm, tok, weight_cache=wc)
+        return build_dp_sharded_runner(args, cfg, device, comm, tok, weight_cache=wc, prefix_kv_cache=pkv)
     src = build_source(args, cfg, comm, device)
     act = None
     if args.dtype:
@@ -112,8 +176,8 @@ def build_runner(args, cfg: ModelConfig, device, comm: Comm, tok) -> ShardedRunn
                          checkpoint_every=getattr(args, "checkpoint_every", 0),
                          max_token_len=getattr(args, "max_token_len", None) or MAX_TOKEN_LEN,
                          hip_graphs=getattr(args, "hip_graphs", False),
-                         hbm_cache_gb=getattr(args, "hbm_cache_gb", 0.0) or 0.0,
-                         prefix_kv_cache=getattr(args, "prefix_kv_cache", False),
+                         hbm_cache_gb=resolve_hbm_cache_gb(args, cfg, device, reserve),
+                         prefix_kv_cache=pkv,
                          prefix_cache_entries=getattr(args, "prefix_cache_entries", 8),
                          pipeline_stages=getattr(args, "pipeline_stages", "round_robin"),
                          max_vram_gb=getattr(args, "max_vram_gb", None))
@@ -200,7 +264,7 @@ def run_rank(args, comm: Comm) -> Optional[dict]:
         original = pickle.load(f)      # the user's own prompt file (reference format)
     cfg, tok = load_model_meta(args)
     t0 = time.perf_counter()
-    runner = build_runner(args, cfg, device, comm, tok)
+    runner = build_runner(args, cfg, device, comm, tok, original)
     t_build = time.perf_counter() - t0
     t1 = time.perf_counter()
     scores, updated = generation_loop(args, runner, comm, tok, original)

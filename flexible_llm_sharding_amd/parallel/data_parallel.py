@@ -160,7 +160,7 @@ class _nullctx:
 
 
 def build_dp_sharded_runner(args, cfg, device, comm: Comm, tok, store: Optional[LayerSource] = None,
-                            weight_cache: str = "host"):
+                            weight_cache: str = "host", prefix_kv_cache: Optional[bool] = None):
     """Data-parallel runner with scatter-loaded weights: ``weight_cache`` ``host`` pins this
     rank's slices (read once), ``stream`` re-reads them from the layer files every pass."""
     from ..config import MAX_TOKEN_LEN
@@ -191,6 +191,7 @@ def build_dp_sharded_runner(args, cfg, device, comm: Comm, tok, store: Optional[
                          checkpoint_every=getattr(args, "checkpoint_every", 0),
                          max_token_len=getattr(args, "max_token_len", None) or MAX_TOKEN_LEN,
                          hip_graphs=getattr(args, "hip_graphs", False),
-                         prefix_kv_cache=getattr(args, "prefix_kv_cache", False),
+                         prefix_kv_cache=(prefix_kv_cache if prefix_kv_cache is not None
+                                          else getattr(args, "prefix_kv_cache", False) is True),
                          prefix_cache_entries=getattr(args, "prefix_cache_entries", 8),
                          max_vram_gb=getattr(args, "max_vram_gb", None))

@@ -21,6 +21,14 @@ def str2bool(v) -> bool:
     raise argparse.ArgumentTypeError(f"boolean expected, got {v!r}")
 
 
+def bool_or_auto(v):
+    return "auto" if str(v).strip().lower() == "auto" else str2bool(v)
+
+
+def gb_or_auto(v):
+    return "auto" if str(v).strip().lower() == "auto" else float(v)
+
+
 def build_parser() -> argparse.ArgumentParser:
     p = argparse.ArgumentParser(description="MI355X-native layer-sharded Llama scoring / generation")
     # ---- reference flags (main.py:31-46)
@@ -45,17 +53,21 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--hip_graphs", type=str2bool, nargs="?", const=True, default=False,
                    help="with --resident: capture each micro-batch's whole forward as one HIP graph and "
                         "replay it (shape-bucketed; removes per-op host dispatch for small batches)")
-    p.add_argument("--prefix_kv_cache", type=str2bool, nargs="?", const=True, default=False,
+    p.add_argument("--prefix_kv_cache", type=bool_or_auto, nargs="?", const=True, default="auto",
                    help="keep every prompt's prefix K/V per layer in HBM and reuse it in later calls on the same "
-                        "prefixes (each --num_gen_token step then computes only the suffix tokens; exact)")
+                        "prefixes (each --num_gen_token step then computes only the suffix tokens; exact). "
+                        "auto (default): on when --num_gen_token > 1")
     p.add_argument("--prefix_cache_entries", type=int, default=8,
                    help="prefix K/V cache: calls (prompt batches) kept, LRU")
     p.add_argument("--resident", type=str2bool, nargs="?", const=True, default=False,
                    help="keep every shard resident in HBM after first load (288 GB fits 70B)")
-    p.add_argument("--hbm_cache_gb", type=float, default=0.0,
+    p.add_argument("--hbm_cache_gb", type=gb_or_auto, default="auto",
                    help="keep this many GB of shards resident in HBM after their first load, spread evenly "
                         "over the pass; the others stream every pass (generation steps with a partly "
-                        "cached model move fewer bytes over PCIe; single-GPU and model-parallel runs)")
+                        "cached model move fewer bytes over PCIe).  auto (default): with repeated passes "
+                        "over the same weights (--num_gen_token > 1 or --num_batch > 1) the free HBM minus "
+                        "the activation plan (the whole 70B model on one 288 GB MI355X; data parallel: "
+                        "resident all-gathered layers when they fit), else 0")
     p.add_argument("--weight_cache", choices=["auto", "host", "stream", "disk"], default="auto",
                    help="host: read every layer once into pinned host RAM (needs ~model-size RAM); "
                         "stream (alias disk, the reference behaviour): re-read the per-layer safetensors every "
@@ -84,7 +96,7 @@ def build_parser() -> argparse.ArgumentParser:
                         "generated in pinned host RAM, plus a synthetic tokenizer; --model_path is not read")
     p.add_argument("--resume_dir", type=str, default=None,
                    help="checkpoint inter-shard activations here and resume a crashed run from them "
-                        "(single-GPU / data-parallel)")
+                        "(single-GPU, data-parallel and model-parallel)")
     p.add_argument("--checkpoint_every", type=int, default=8, help="shards between checkpoints (with --resume_dir)")
     p.add_argument("--profile", type=str2bool, nargs="?", const=True, default=False,
                    help="emit roctx ranges (shard load / micro-batch compute) for rocprofv3 --marker-trace")

@@ -204,3 +204,22 @@ def test_main_model_parallel_no_prompts(tiny_model, tmp_path):
     _torchrun(2, ["--model_path", path, "--prompt_pickle", str(pp), "--output_file", str(tmp_path / "o.pkl")],
               str(tmp_path))
     assert pickle.load(open(tmp_path / "o.pkl", "rb")) == []
+
+
+def test_repeated_pass_defaults():
+    """--prefix_kv_cache / --hbm_cache_gb default to auto: on for generation / repeated passes."""
+    from flexible_llm_sharding_amd.api import repeated_passes, resolve_hbm_cache_gb, resolve_prefix_kv_cache
+    from flexible_llm_sharding_amd.config import preset
+    import torch
+    base = ["--prompt_pickle", "p.pkl", "--output_file", "o.pkl"]
+    a = parse_args(base)
+    assert a.prefix_kv_cache == "auto" and a.hbm_cache_gb == "auto"
+    assert not repeated_passes(a) and not resolve_prefix_kv_cache(a)
+    g = parse_args(base + ["--num_gen_token", "4"])
+    assert repeated_passes(g) and resolve_prefix_kv_cache(g)
+    assert repeated_passes(parse_args(base + ["--num_batch", "2"]))
+    assert not resolve_prefix_kv_cache(parse_args(base + ["--num_gen_token", "4", "--prefix_kv_cache", "false"]))
+    assert parse_args(base + ["--hbm_cache_gb", "12.5"]).hbm_cache_gb == 12.5
+    cfg = preset("tiny")
+    assert resolve_hbm_cache_gb(g, cfg, torch.device("cpu")) == 0.0       # nothing to cache on a CPU run
+    assert resolve_hbm_cache_gb(parse_args(base + ["--hbm_cache_gb", "3"]), cfg, torch.device("cpu")) == 3.0
