@@ -47,6 +47,8 @@ typedef struct {
   int32_t pad;
 } fls_piece_t;
 void*   fls_streamer_create(int device, uint64_t chunk_bytes, int n_chunks, int io_threads, int direct);
+void*   fls_streamer_create_host(uint64_t chunk_bytes, int n_chunks, int io_threads, int direct, int copy_delay_us);
+int     fls_streamer_sync_host(void* h);
 uint64_t fls_streamer_pinned_bytes(void* h);
 int64_t fls_streamer_load(void* h, const char* path, const fls_piece_t* pieces, int n, void* dst_dev,
                           fls_stream_t stream);

@@ -26,6 +26,7 @@
 #include <cerrno>
 #include <chrono>
 #include <condition_variable>
+#include <deque>
 #include <functional>
 #include <mutex>
 #include <cstdio>
@@ -396,14 +397,145 @@ class IoPool {
   bool stop_ = false;
 };
 
+// The streamer's device side behind an interface: HIP in production; a host engine (malloc'd
+// ring, copies run by a worker thread in FIFO order, events signalled by that thread) so the
+// ring's slot reuse, the pread pool and the O_DIRECT fallback run under ASan / TSan without a
+// GPU (csrc/tests/test_runtime.cpp).  The host engine's copies READ the ring slot
+// asynchronously exactly as the DMA engine does, so reusing a slot before its event fired is a
+// data race TSan reports (and a wrong byte the test sees).
+struct CopyEngine {
+  virtual ~CopyEngine() = default;
+  virtual int set_device() = 0;
+  virtual void* alloc_host(uint64_t n) = 0;
+  virtual void free_host(void* p) = 0;
+  virtual void* event_create() = 0;
+  virtual void event_destroy(void* ev) = 0;
+  virtual int event_record(void* ev, void* stream) = 0;
+  virtual int event_sync(void* ev) = 0;
+  virtual int copy_async(void* dst, const void* src, uint64_t n, void* stream) = 0;
+};
+
+struct HipEngine final : CopyEngine {
+  int device;
+  explicit HipEngine(int d) : device(d) {}
+  int set_device() override {
+    if (hipSetDevice(device) != hipSuccess) { (void)hipGetLastError(); return -1; }
+    return 0;
+  }
+  void* alloc_host(uint64_t n) override {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, n, hipHostMallocPortable) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
+    return p;
+  }
+  void free_host(void* p) override { (void)hipHostFree(p); }
+  void* event_create() override {
+    hipEvent_t ev = nullptr;
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
+    return ev;
+  }
+  void event_destroy(void* ev) override { (void)hipEventDestroy((hipEvent_t)ev); }
+  int event_record(void* ev, void* stream) override {
+    if (hipEventRecord((hipEvent_t)ev, (hipStream_t)stream) != hipSuccess) { (void)hipGetLastError(); return -1; }
+    return 0;
+  }
+  int event_sync(void* ev) override {
+    if (hipEventSynchronize((hipEvent_t)ev) != hipSuccess) { (void)hipGetLastError(); return -1; }
+    return 0;
+  }
+  int copy_async(void* dst, const void* src, uint64_t n, void* stream) override {
+    if (hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, (hipStream_t)stream) != hipSuccess) {
+      (void)hipGetLastError();
+      return -1;
+    }
+    return 0;
+  }
+};
+
+struct HostEngine final : CopyEngine {
+  struct Ev {
+    uint64_t recorded = 0, done = 0;
+  };
+  struct Task {
+    void* dst;
+    const void* src;
+    uint64_t n;
+    Ev* ev;
+    uint64_t gen;
+  };
+  std::mutex m;
+  std::condition_variable cv, done_cv;
+  std::deque<Task> q;
+  bool busy = false;
+  bool stop = false;
+  int delay_us;
+  std::thread worker;
+  explicit HostEngine(int delay) : delay_us(delay) { worker = std::thread([this] { loop(); }); }
+  ~HostEngine() override {
+    {
+      std::lock_guard<std::mutex> g(m);
+      stop = true;
+    }
+    cv.notify_all();
+    worker.join();
+  }
+  void loop() {
+    std::unique_lock<std::mutex> g(m);
+    for (;;) {
+      cv.wait(g, [&] { return stop || !q.empty(); });
+      if (q.empty()) return;   // stop requested and nothing left
+      Task t = q.front();
+      q.pop_front();
+      busy = true;
+      g.unlock();
+      if (t.ev == nullptr) {
+        if (delay_us) std::this_thread::sleep_for(std::chrono::microseconds(delay_us));
+        std::memcpy(t.dst, t.src, t.n);           // the "DMA" reads the pinned slot now
+      }
+      g.lock();
+      busy = false;
+      if (t.ev) t.ev->done = t.gen;
+      done_cv.notify_all();
+    }
+  }
+  int set_device() override { return 0; }
+  void* alloc_host(uint64_t n) override { return std::malloc(n); }
+  void free_host(void* p) override { std::free(p); }
+  void* event_create() override { return new Ev(); }
+  void event_destroy(void* ev) override { delete (Ev*)ev; }
+  int event_record(void* ev, void*) override {
+    std::lock_guard<std::mutex> g(m);
+    Ev* e = (Ev*)ev;
+    q.push_back({nullptr, nullptr, 0, e, ++e->recorded});
+    cv.notify_all();
+    return 0;
+  }
+  int event_sync(void* ev) override {
+    std::unique_lock<std::mutex> g(m);
+    Ev* e = (Ev*)ev;
+    done_cv.wait(g, [&] { return e->done >= e->recorded; });
+    return 0;
+  }
+  int copy_async(void* dst, const void* src, uint64_t n, void*) override {
+    std::lock_guard<std::mutex> g(m);
+    q.push_back({dst, src, n, nullptr, 0});
+    cv.notify_all();
+    return 0;
+  }
+  void drain() {
+    std::unique_lock<std::mutex> g(m);
+    done_cv.wait(g, [&] { return q.empty() && !busy; });
+  }
+};
+
 struct Slot {
   char* buf = nullptr;
-  hipEvent_t ev = nullptr;
+  void* ev = nullptr;
   bool pending = false;
 };
 
 struct Streamer {
-  int device = 0;
+  CopyEngine* eng = nullptr;
+  bool host = false;
   uint64_t chunk = 0;
   int direct = 0;
   std::vector<Slot> slots;
@@ -450,32 +582,56 @@ int64_t pool_read(IoPool* pool, int fd, uint64_t lo, uint64_t hi, char* buf, uin
 
 }  // namespace
 
-extern "C" void* fls_streamer_create(int device, uint64_t chunk_bytes, int n_chunks, int io_threads, int direct) {
-  if (chunk_bytes < (1u << 20) || n_chunks < 1) return nullptr;
-  if (hipSetDevice(device) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
+static Streamer* streamer_new(CopyEngine* eng, bool host, uint64_t chunk_bytes, int n_chunks, int io_threads,
+                              int direct) {
+  if (chunk_bytes < (1u << 20) || n_chunks < 1 || eng->set_device() != 0) {
+    delete eng;
+    return nullptr;
+  }
   auto* st = new Streamer();
-  st->device = device;
+  st->eng = eng;
+  st->host = host;
   st->chunk = (chunk_bytes + kAlign - 1) / kAlign * kAlign;
   st->direct = direct;
   st->slots.resize(n_chunks);
   for (auto& sl : st->slots) {
-    void* p = nullptr;
     // + 2 alignment pages: an O_DIRECT read rounds the range out on both sides
-    if (hipHostMalloc(&p, st->chunk + 2 * kAlign, hipHostMallocPortable) != hipSuccess ||
-        hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming) != hipSuccess) {
-      (void)hipGetLastError();
-      if (p) (void)hipHostFree(p);
+    void* p = eng->alloc_host(st->chunk + 2 * kAlign);
+    void* ev = p ? eng->event_create() : nullptr;
+    if (!p || !ev) {
+      if (p) eng->free_host(p);
       for (auto& s2 : st->slots) {
-        if (s2.buf) (void)hipHostFree(s2.buf);
-        if (s2.ev) (void)hipEventDestroy(s2.ev);
+        if (s2.buf) eng->free_host(s2.buf);
+        if (s2.ev) eng->event_destroy(s2.ev);
       }
+      delete eng;
       delete st;
       return nullptr;
     }
     sl.buf = (char*)p;
+    sl.ev = ev;
   }
   st->pool = new IoPool(std::max(1, io_threads));
   return st;
+}
+
+extern "C" void* fls_streamer_create(int device, uint64_t chunk_bytes, int n_chunks, int io_threads, int direct) {
+  return streamer_new(new HipEngine(device), false, chunk_bytes, n_chunks, io_threads, direct);
+}
+
+// GPU-free streamer (tests, sanitizers): `dst_dev` of fls_streamer_load is a host pointer, copies
+// are done by a worker thread (each optionally delayed by copy_delay_us to widen race windows)
+extern "C" void* fls_streamer_create_host(uint64_t chunk_bytes, int n_chunks, int io_threads, int direct,
+                                          int copy_delay_us) {
+  return streamer_new(new HostEngine(copy_delay_us), true, chunk_bytes, n_chunks, io_threads, direct);
+}
+
+// host streamer: wait until every enqueued copy is done
+extern "C" int fls_streamer_sync_host(void* h) {
+  auto* st = (Streamer*)h;
+  if (!st || !st->host) return -1;
+  static_cast<HostEngine*>(st->eng)->drain();
+  return 0;
 }
 
 extern "C" uint64_t fls_streamer_pinned_bytes(void* h) {
@@ -492,7 +648,7 @@ extern "C" int64_t fls_streamer_load(void* h, const char* path, const fls_piece_
   auto* st = (Streamer*)h;
   if (!st || n < 0) return -EINVAL;
   if (n == 0) return 0;
-  if (hipSetDevice(st->device) != hipSuccess) { (void)hipGetLastError(); return -ENODEV; }
+  if (st->eng->set_device() != 0) return -ENODEV;
   // split pieces so that every chunk (with O_DIRECT slack) fits a ring slot
   const uint64_t maxp = st->chunk;
   std::vector<SubPiece> sub;
@@ -532,7 +688,7 @@ extern "C" int64_t fls_streamer_load(void* h, const char* path, const fls_piece_
     Slot& sl = st->slots[st->next++ % st->slots.size()];
     auto t0 = std::chrono::steady_clock::now();
     if (sl.pending) {
-      if (hipEventSynchronize(sl.ev) != hipSuccess) { close(fd); (void)hipGetLastError(); return -EIO; }
+      if (st->eng->event_sync(sl.ev) != 0) { close(fd); return -EIO; }
       sl.pending = false;
     }
     auto t1 = std::chrono::steady_clock::now();
@@ -573,15 +729,13 @@ extern "C" int64_t fls_streamer_load(void* h, const char* path, const fls_piece_
         }
         len = cnt * 2;
       }
-      if (hipMemcpyAsync((char*)dst_dev + sub[k].dst_off, src, len, hipMemcpyHostToDevice, (hipStream_t)stream) !=
-          hipSuccess) {
+      if (st->eng->copy_async((char*)dst_dev + sub[k].dst_off, src, len, stream) != 0) {
         close(fd);
-        (void)hipGetLastError();
         return -EIO;
       }
       st->h2d_bytes += len;
     }
-    if (hipEventRecord(sl.ev, (hipStream_t)stream) != hipSuccess) { close(fd); (void)hipGetLastError(); return -EIO; }
+    if (st->eng->event_record(sl.ev, stream) != 0) { close(fd); return -EIO; }
     sl.pending = true;
     i = j;
   }
@@ -634,13 +788,14 @@ extern "C" int fls_streamer_stats(void* h, double* read_s, double* wait_s, uint6
 extern "C" void fls_streamer_destroy(void* h) {
   auto* st = (Streamer*)h;
   if (!st) return;
-  (void)hipSetDevice(st->device);
+  (void)st->eng->set_device();
   for (auto& sl : st->slots) {
-    if (sl.pending) (void)hipEventSynchronize(sl.ev);
-    (void)hipEventDestroy(sl.ev);
-    (void)hipHostFree(sl.buf);
+    if (sl.pending) (void)st->eng->event_sync(sl.ev);
+    st->eng->event_destroy(sl.ev);
+    st->eng->free_host(sl.buf);
   }
   delete st->pool;
+  delete st->eng;
   delete st;
 }
 

@@ -1,7 +1,10 @@
 // Host-side unit test of the native runtime, built with AddressSanitizer +
 // UBSan (and separately ThreadSanitizer) by tests/test_sanitizers.py.
-// Exercises the multi-threaded pread/pwrite engine, the block gather and the
-// safetensors header index (incl. malformed headers) without a GPU.
+// Exercises the multi-threaded pread/pwrite engine, the block gather, the
+// safetensors header index (incl. malformed headers) and the weight streamer
+// (persistent pread pool + pinned chunk ring + asynchronous copies, on its
+// GPU-free host copy engine: ring wrap-around and slot reuse, O_DIRECT and its
+// buffered fallback, fp32 -> fp16 pieces, pieces split across chunks) without a GPU.
 #include <cassert>
 #include <cstdint>
 #include <cstdio>
@@ -94,6 +97,86 @@ int main(int argc, char** argv) {
   uint64_t huge = 1ull << 40;
   write_file(st, std::string(reinterpret_cast<const char*>(&huge), 8));
   CHECK(fls_st_open(st.c_str()) == nullptr);
+  // ---- weight streamer on the host copy engine
+  {
+    // a "layer file": 3 MiB header gap, then raw fp16 pieces and one fp32 piece, odd sizes
+    const uint64_t fsz = (26ull << 20) + 4096 * 3 + 777;
+    std::vector<uint8_t> fb(fsz);
+    for (uint64_t i = 0; i < fsz; ++i) fb[i] = (uint8_t)((i * 2246822519u) >> 11);
+    const std::string lf = dir + "/fls_rt_layer.bin";
+    CHECK(fls_pwrite_from(lf.c_str(), 0, fsz, fb.data(), 4, 1) == (int64_t)fsz);
+    // fp32 piece at [20 MiB, 20 MiB + 4 MiB): finite values so the f16 rounding is well defined
+    const uint64_t f32_off = 20ull << 20, f32_n = 4ull << 20;
+    for (uint64_t e = 0; e < f32_n / 4; ++e) {
+      float v = (float)((int)(e % 2001) - 1000) * 0.37f;
+      std::memcpy(fb.data() + f32_off + 4 * e, &v, 4);
+    }
+    CHECK(fls_pwrite_from(lf.c_str(), f32_off, f32_n, fb.data() + f32_off, 2, 0) == (int64_t)f32_n);
+    std::vector<fls_piece_t> pcs;
+    uint64_t dst = 0;
+    auto add = [&](uint64_t off, uint64_t n, int kind) {
+      fls_piece_t p{off, n, dst, kind, 0};
+      pcs.push_back(p);
+      dst += kind ? n / 2 : n;
+      dst = (dst + 255) / 256 * 256;
+    };
+    add(3ull << 20, (5ull << 20) + 123, 0);           // split over several 1 MiB chunks
+    add((8ull << 20) + 4096, 4096 * 3 + 5, 0);        // small piece, packed with the next (gap read through)
+    add((8ull << 20) + 4096 * 5, (11ull << 20) + 11, 0);
+    add(f32_off, f32_n, 1);                           // fp32 -> fp16 on the host
+    add(f32_off + f32_n + 64, fsz - (f32_off + f32_n + 64), 0);
+    std::vector<uint8_t> want(dst, 0);
+    for (const auto& p : pcs) {
+      if (p.kind == 0) {
+        std::memcpy(want.data() + p.dst_off, fb.data() + p.file_off, p.nbytes);
+      } else {
+        fls_f32_to_f16((const float*)(fb.data() + p.file_off), (uint16_t*)(want.data() + p.dst_off), p.nbytes / 4);
+      }
+    }
+    for (int direct = 0; direct < 2; ++direct) {
+      for (int chunks : {1, 2, 3}) {
+        // 1 MiB chunks, 4 pread threads; copies delayed so a premature slot reuse would overlap them
+        void* sh = fls_streamer_create_host(1u << 20, chunks, 4, direct, 50);
+        CHECK(sh != nullptr);
+        if (!sh) continue;
+        for (int rep = 0; rep < 3; ++rep) {          // the ring keeps rotating across loads
+          std::vector<uint8_t> got(dst, 0xCD);
+          const int64_t r = fls_streamer_load(sh, lf.c_str(), pcs.data(), (int)pcs.size(), got.data(), nullptr);
+          CHECK(r > 0);
+          CHECK(fls_streamer_sync_host(sh) == 0);
+          for (const auto& p : pcs) {
+            const uint64_t n = p.kind ? p.nbytes / 2 : p.nbytes;
+            CHECK(std::memcmp(got.data() + p.dst_off, want.data() + p.dst_off, n) == 0);
+          }
+        }
+        double rs, ws;
+        uint64_t rb, hb;
+        int fb_n = -1;
+        CHECK(fls_streamer_stats(sh, &rs, &ws, &rb, &hb, &fb_n) == 0);
+        CHECK(rb > 0 && hb > 0 && fb_n >= 0);
+        fls_streamer_destroy(sh);
+      }
+    }
+    // a larger chunk with several pread granules per chunk (8 MiB granules, 20 MiB chunk)
+    void* sh = fls_streamer_create_host(20u << 20, 2, 3, 0, 0);
+    CHECK(sh != nullptr);
+    if (sh) {
+      std::vector<uint8_t> got(dst, 0);
+      CHECK(fls_streamer_load(sh, lf.c_str(), pcs.data(), (int)pcs.size(), got.data(), nullptr) > 0);
+      CHECK(fls_streamer_sync_host(sh) == 0);
+      CHECK(std::memcmp(got.data(), want.data(), dst) == 0);
+      // unsorted pieces and bad kinds are rejected
+      fls_piece_t bad2[2] = {pcs[1], pcs[0]};
+      CHECK(fls_streamer_load(sh, lf.c_str(), bad2, 2, got.data(), nullptr) < 0);
+      fls_piece_t badk = pcs[0];
+      badk.kind = 7;
+      CHECK(fls_streamer_load(sh, lf.c_str(), &badk, 1, got.data(), nullptr) < 0);
+      CHECK(fls_streamer_load(sh, (dir + "/missing.bin").c_str(), pcs.data(), 1, got.data(), nullptr) < 0);
+      fls_streamer_destroy(sh);
+    }
+    CHECK(fls_streamer_create_host(1000, 2, 1, 0, 0) == nullptr);     // chunk below 1 MiB
+    std::remove(lf.c_str());
+  }
   std::remove(blob.c_str());
   std::remove(st.c_str());
   if (fails) {
