@@ -100,12 +100,17 @@ class ShardedRunner:
             # +2.8 GB of HBM on 70B.  The double buffer under a VRAM cap (the 6 GB mode), for
             # resident weights and for the external data-parallel prefetcher.
             n_slots = 3 if (self.cuda and not resident and not max_vram_gb and prefetcher is None) else 2
+        self._vram_cap = int(max_vram_gb * 1e9) if max_vram_gb else 0
+        self._plan_req = (token_budget, mlp_chunk, n_slots)
+        qkv_chunk = 0
         if max_vram_gb:
-            # size the micro-batch and the MLP chunk to the HBM cap (runtime/memplan.py)
+            # size the micro-batch and the QKV / MLP chunks to the HBM cap (runtime/memplan.py);
+            # re-planned per call once its token count is known (_plan_call)
             from .runtime.memplan import plan_for_vram
-            token_budget, mlp_chunk, est = plan_for_vram(cfg, int(max_vram_gb * 1e9), layer_num_per_shard,
-                                                         n_slots, token_budget, mlp_chunk)
-            self.vram_plan = {"token_budget": token_budget, "mlp_chunk": mlp_chunk, "estimated_peak_bytes": est}
+            token_budget, mlp_chunk, qkv_chunk, est = plan_for_vram(cfg, self._vram_cap, layer_num_per_shard,
+                                                                    n_slots, token_budget, mlp_chunk)
+            self.vram_plan = {"token_budget": token_budget, "mlp_chunk": mlp_chunk, "qkv_chunk": qkv_chunk,
+                              "estimated_peak_bytes": est}
         self.token_budget = token_budget
         self.mlp_chunk = mlp_chunk
         self.comm = comm or Comm(0, 1, self.dev)
@@ -127,7 +132,7 @@ class ShardedRunner:
         self.ops = get_ops(self.dev)
         cos, sin = rope_tables(cfg, max(cfg.max_position_embeddings, max_token_len),
                                torch.float16, self.dev)
-        self.ctx = ExecContext(cfg, self.ops, self.dev, self.act_dtype, cos, sin, mlp_chunk)
+        self.ctx = ExecContext(cfg, self.ops, self.dev, self.act_dtype, cos, sin, mlp_chunk, qkv_chunk=qkv_chunk)
         decs = [n for n in self.names if layer_kind(n) == "decoder"]
         self.ctx.prune_last = bool(prune_last_layer and decs)
         self.ctx.last_decoder = decs[-1] if decs else ""
@@ -267,6 +272,8 @@ class ShardedRunner:
         t_start = time.perf_counter()
         n = len(tps)
         entry, cached = self._prefix_entry(tps)
+        if self._vram_cap:
+            self._plan_call(tps, cached)
         groups = split_microbatches(tps, self.micro_budget(tps, cached), suffix_only=cached)
         batches = [pack_prompts([tps[i] for i in g], g, self.prefix_attention,
                                 prefix_offsets=[entry.offsets[i] for i in g] if entry is not None else None,
@@ -292,6 +299,19 @@ class ShardedRunner:
         self.stats["prefix_cached"] = float(cached)
         self.stats["host_pack_s"] = t_pack
         return outputs
+
+    def _plan_call(self, tps, cached: bool) -> None:
+        """--max_vram_gb: re-plan micro-batch and chunk sizes for this call's token count (one
+        micro-batch whenever the cap allows it: the hidden state then never leaves HBM)."""
+        from .runtime.memplan import plan_for_vram
+        total = sum(tp.num_tokens - (len(tp.prefix) if cached else 0) for tp in tps)
+        tb, mc, n_slots = self._plan_req
+        tb, mc, qc, est = plan_for_vram(self.cfg, self._vram_cap, self.lnps, self.prefetcher.n_slots, tb, mc,
+                                        total_tokens=max(1, total))
+        self.token_budget, self.mlp_chunk = tb, mc
+        self.ctx.mlp_chunk, self.ctx.qkv_chunk = mc, qc
+        self.vram_plan.update({"token_budget": tb, "mlp_chunk": mc, "qkv_chunk": qc, "estimated_peak_bytes": est,
+                               "call_tokens": total})
 
     # model parallel: micro-batches per pipeline stage wanted before the budget may shrink, and the
     # smallest budget it shrinks to (GEMM efficiency falls off below ~8k rows)

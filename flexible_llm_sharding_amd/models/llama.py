@@ -147,6 +147,7 @@ class ExecContext:
     cos: torch.Tensor
     sin: torch.Tensor
     mlp_chunk: int = 16384       # rows per gate/up + down chunk (bounds the [T, I] buffer)
+    qkv_chunk: int = 0           # rows per RMSNorm + QKV chunk (0: all rows; bounds the normed-input buffer)
     prefix_entry: Optional[object] = None   # runtime.prefix_cache.PrefixEntry of the current call
     # the last decoder layer computes only the scored rows (its K/V still cover every token):
     # nothing downstream reads the other rows (final norm gathers the scored rows, utils.py:284-286)
@@ -167,26 +168,57 @@ def run_embed(ctx: ExecContext, W: Dict[str, torch.Tensor], meta: dict) -> torch
     return ctx.ops.embed(meta["ids"], W["embed"], ctx.act_dtype)
 
 
-def _pruned_qkv(ctx: ExecContext, W: Dict[str, torch.Tensor], h: torch.Tensor, meta: dict, T0: int) -> torch.Tensor:
-    """QKV of the pruned last decoder layer: K/V (+ RoPE on K) for every row, Q (+ RoPE) only for
-    the scored rows, scattered into the Q columns of those rows.  The other rows' Q columns are
-    left unwritten: the last layer's attention work items (``work_last``) query only scored rows.
-    Q is q_size / qkv_size of the projection (80% for Llama-2-70B)."""
+def balanced_step(rows: int, limit: int, align: int = 256) -> int:
+    """Rows per chunk when ``rows`` are cut into the fewest chunks of <= ``limit`` rows, sized
+    evenly (GEMM tile rounds: 43,008 rows under a 16,384 limit -> 3 x 14,336, not 16k+16k+10k)."""
+    if limit <= 0 or rows <= limit:
+        return max(rows, 1)
+    n = -(-rows // limit)
+    step = -(-rows // n)
+    step = -(-step // align) * align
+    return min(step, limit) if step <= limit else limit
+
+
+def _attn_inputs(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, meta: dict,
+                 prune: bool) -> torch.Tensor:
+    """RMSNorm + QKV projection (+ RoPE, + bias) of every row into one [T, qkv] buffer, in row
+    chunks of ``ctx.qkv_chunk`` (only a chunk of normed rows is ever alive: the workspace holds
+    [normed chunk | QKV]).  ``prune`` (the last decoder layer): K/V (+ RoPE on K) for every row,
+    Q only for the scored rows, scattered into the Q columns of those rows — the other rows' Q
+    columns stay unwritten, the last layer's attention work items (``work_last``) query only
+    scored rows (Q is q_size / qkv_size of the projection: 80% for Llama-2-70B)."""
     cfg, ops = ctx.cfg, ctx.ops
-    qs, nq, nkv, hd = cfg.q_size, cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
-    qkv = ctx.scratch(T0, cfg.qkv_size)
+    H, Qn, qs = cfg.hidden_size, cfg.qkv_size, cfg.q_size
+    nq, nkv, hd = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
+    eps = cfg.rms_norm_eps
+    T0 = x.shape[0]
+    step = balanced_step(T0, ctx.qkv_chunk) if ctx.qkv_chunk else T0
+    ctx.phase((step, H), (T0, Qn))
+    hbuf = ctx.scratch(step, H)
+    qkv = ctx.scratch(T0, Qn)
     if qkv is None:
-        qkv = torch.empty(T0, cfg.qkv_size, dtype=h.dtype, device=h.device)
+        qkv = torch.empty(T0, Qn, dtype=x.dtype, device=x.device)
     w, b = W["wqkv"], W.get("bqkv")
-    kv_view = qkv[:, qs:]
-    kv = ops.qkv_rope(h, w[qs:], meta["positions"], ctx.cos, ctx.sin, 0, nkv, hd,
-                      bias=b[qs:] if b is not None else None, out=kv_view)
-    if kv.data_ptr() != kv_view.data_ptr():
-        kv_view.copy_(kv)
-    idx = meta["last_idx"]
-    q = ops.qkv_rope(h.index_select(0, idx), w[:qs], meta["positions"].index_select(0, idx), ctx.cos, ctx.sin,
-                     nq, 0, hd, bias=b[:qs] if b is not None else None)
-    qkv[:, :qs].index_copy_(0, idx if idx.dtype == torch.int64 else idx.long(), q)
+    pos = meta["positions"]
+    for s in range(0, T0, step):
+        e = min(T0, s + step)
+        h = ops.rmsnorm(x[s:e], W["ln1"], eps, out=hbuf[:e - s] if hbuf is not None else None)
+        if prune:
+            dst = qkv[s:e, qs:]
+            r = ops.qkv_rope(h, w[qs:], pos[s:e], ctx.cos, ctx.sin, 0, nkv, hd,
+                             bias=b[qs:] if b is not None else None, out=dst)
+        else:
+            dst = qkv[s:e]
+            r = ops.qkv_rope(h, w, pos[s:e], ctx.cos, ctx.sin, nq, nkv, hd, bias=b, out=dst)
+        if r.data_ptr() != dst.data_ptr():
+            dst.copy_(r)
+        del h
+    if prune:
+        idx = meta["last_idx"]
+        hq = ops.rmsnorm(x.index_select(0, idx), W["ln1"], eps)
+        q = ops.qkv_rope(hq, w[:qs], pos.index_select(0, idx), ctx.cos, ctx.sin, nq, 0, hd,
+                         bias=b[:qs] if b is not None else None)
+        qkv[:, :qs].index_copy_(0, idx if idx.dtype == torch.int64 else idx.long(), q)
     return qkv
 
 
@@ -195,20 +227,17 @@ def run_decoder(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, b
     """One pre-norm decoder block on the packed rows.  With ``prune`` (the last decoder
     layer) Q/attention/O/MLP run only for the scored rows and the result is
     [n_scored, H]: K/V are still projected for every token (the scored rows attend to
-    the whole prefix and their own suffix)."""
+    the whole prefix and their own suffix).
+
+    Activation memory per micro-batch of T rows: the hidden state x (updated in place by the
+    residual epilogues) plus one workspace arena holding [normed chunk | QKV] in the attention
+    phase — the attention output overwrites the Q columns it was computed from (each (row,
+    head) is read and written by one work item) and feeds the O projection as a strided view
+    — and [normed chunk | SwiGLU chunk] in the MLP phase."""
     cfg, ops = ctx.cfg, ctx.ops
     prune = ctx.prune_last and layer_name == ctx.last_decoder
     eps = cfg.rms_norm_eps
-    T0 = x.shape[0]
-    ctx.phase((T0, cfg.hidden_size), (T0, cfg.qkv_size), (T0, cfg.q_size))
-    h = ops.rmsnorm(x, W["ln1"], eps, out=ctx.scratch(T0, cfg.hidden_size))
-    if prune:
-        qkv = _pruned_qkv(ctx, W, h, meta, T0)
-    else:
-        qkv = ops.qkv_rope(h, W["wqkv"], meta["positions"], ctx.cos, ctx.sin,
-                           cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim, bias=W.get("bqkv"),
-                           out=ctx.scratch(T0, cfg.qkv_size))
-    del h
+    qkv = _attn_inputs(ctx, W, x, meta, prune)
     kv0 = None
     pe = ctx.prefix_entry
     if pe is not None:
@@ -226,7 +255,7 @@ def run_decoder(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, b
     # work items span several suffixes of a prompt: seg_lo makes their range 1 block-diagonal
     kw = {"seg_lo": meta["seg_lo"]} if work_items else {}
     a = ops.attention(qkv, attn_arg, cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim, kv0=kv0,
-                      q_block=batch.q_block, out=ctx.scratch(T0, cfg.q_size), **kw)
+                      q_block=batch.q_block, out=qkv[:, :cfg.q_size], **kw)
     del qkv
     if prune:
         idx = meta["last_idx"]
@@ -235,8 +264,8 @@ def run_decoder(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, b
     x = ops.linear_residual(a, W["wo"], x, bias=W.get("bo"))
     del a
     T = x.shape[0]
-    step = max(1, ctx.mlp_chunk)
     I, H = cfg.intermediate_size, cfg.hidden_size
+    step = balanced_step(T, max(1, ctx.mlp_chunk))
     if T <= step:
         ctx.phase((T, H), (T, I))               # the attention-phase bytes are dead: reuse them
         h = ops.rmsnorm(x, W["ln2"], eps, out=ctx.scratch(T, H))

@@ -5,20 +5,21 @@ at ``layer_num_per_shard=1`` (``/root/reference/README.md:2,31``).  Here the
 HBM in use is
 
     weight slots (2 x the largest shard: 2 x 1.71 GB for 70B, lnps=1)
-  + activations of one packed micro-batch (``token_budget`` tokens)
-  + the MLP chunk intermediate (``mlp_chunk`` rows x intermediate_size)
-  + states kept across shard boundaries / in flight on the copy streams
+  + one workspace arena (models/llama.py): [normed chunk (``qkv_chunk`` rows) | QKV of the
+    micro-batch] in the attention phase — the attention output overwrites Q in place — and
+    [normed chunk | SwiGLU chunk] (``mlp_chunk`` rows) in the MLP phase
+  + the hidden states alive: 1 when the whole call is one micro-batch (it never leaves HBM),
+    else the one being computed, the carry window and the copy-stream landing buffers
   + the HIP context, code objects and allocator slack,
 
-so a VRAM cap is met by sizing ``token_budget`` and ``mlp_chunk``:
-:func:`plan_for_vram` picks the largest (most MFMA-efficient) pair whose
-estimated peak fits.  The estimate is deliberately simple and conservative;
-``bench.py --max-vram-gb`` reports the measured ``hipMemGetInfo`` peak next
-to it (``profiles/r2_vram``).
+so a VRAM cap is met by sizing ``token_budget``, ``qkv_chunk`` and ``mlp_chunk``:
+:func:`plan_for_vram` picks, for the call's token count, the fewest micro-batches (one means
+no activation traffic over PCIe at all) and then the largest chunks whose estimated peak
+fits.  ``bench.py --max-vram-gb`` reports the measured ``hipMemGetInfo`` peak next to it.
 """
 from __future__ import annotations
 
-from typing import Tuple
+from typing import Optional, Tuple
 
 from ..config import ModelConfig
 from ..models.layout import layer_kind, layer_layout
@@ -29,17 +30,25 @@ DEVICE_OVERHEAD = int(0.75e9)
 # hidden states alive at once: the one being computed, the carry window (3, engine.CARRY_WINDOW)
 # and one H2D landing buffer
 STATES = 5
-# caching-allocator slack on the (few, reused) activation blocks
+# caching-allocator slack on the (few, reused) activation blocks; one micro-batch per call holds
+# exactly two large blocks (state + arena), rounded to 2 MB
 SLACK = 1.10
+SLACK_ONE = 1.02
+# the plan aims this far below the cap (the estimate is a model; hipMemGetInfo is the judge)
+CAP_MARGIN = 0.015
 
 
-def activation_bytes(cfg: ModelConfig, tokens: int, mlp_chunk: int, elem: int = 2) -> int:
-    """Peak activation bytes of one micro-batch of ``tokens`` rows: the fixed scratch buffers
-    (models.llama.Workspace: normed input, QKV, attention output, SwiGLU chunk) + live states."""
+def activation_bytes(cfg: ModelConfig, tokens: int, mlp_chunk: int, elem: int = 2, qkv_chunk: int = 0,
+                     states: int = STATES) -> int:
+    """Peak activation bytes of one micro-batch of ``tokens`` rows: the workspace arena
+    (models.llama: [normed chunk | QKV], then [normed chunk | SwiGLU chunk]) + live states."""
+    from ..models.llama import balanced_step
     H, I = cfg.hidden_size, cfg.intermediate_size
-    chunk = min(tokens, mlp_chunk)
-    scratch = max(tokens * (H + cfg.qkv_size + cfg.q_size), chunk * (H + I))   # one arena, two phases
-    return int(SLACK * elem * (scratch + STATES * tokens * H))
+    chunk = balanced_step(tokens, mlp_chunk)
+    qc = balanced_step(tokens, qkv_chunk) if qkv_chunk else tokens
+    scratch = max(qc * H + tokens * cfg.qkv_size, chunk * (H + I))   # one arena, two phases
+    slack = SLACK_ONE if states == 1 else SLACK
+    return int(slack * elem * (scratch + states * tokens * H))
 
 
 def cap_allocator(device, max_vram_bytes: int, other_device_bytes: int) -> int:
@@ -65,19 +74,32 @@ def weight_slot_bytes(cfg: ModelConfig, lnps: int, n_slots: int = 2) -> int:
 
 
 def plan_for_vram(cfg: ModelConfig, max_vram_bytes: int, lnps: int = 1, n_slots: int = 2,
-                  token_budget: int = 49152, mlp_chunk: int = 16384) -> Tuple[int, int, int]:
-    """-> (token_budget, mlp_chunk, estimated peak bytes), the largest pair <= the requested one
-    that fits ``max_vram_bytes``; raises if even the smallest does not."""
+                  token_budget: int = 49152, mlp_chunk: int = 16384,
+                  total_tokens: Optional[int] = None) -> Tuple[int, int, int, int]:
+    """-> (token_budget, mlp_chunk, qkv_chunk, estimated peak bytes) for a call of
+    ``total_tokens`` packed tokens (None: unknown, assume several micro-batches).  Preference:
+    fewest micro-batches (one keeps the hidden state in HBM for the whole pass: no activation
+    traffic over PCIe), then the largest smaller chunk, then the largest sum; raises if nothing
+    fits."""
     weights = weight_slot_bytes(cfg, lnps, n_slots)
+    target = int(max_vram_bytes * (1.0 - CAP_MARGIN))
     best = None
-    # every GEMM wants a large M: prefer the pair with the largest smaller side, then the largest sum
-    for tb in (t for t in sorted({token_budget, 49152, 32768, 24576, 16384, 12288, 8192, 6144, 4096, 3072, 2048, 1024}) if t <= token_budget):
-        for mc in (m for m in sorted({mlp_chunk, 16384, 8192, 4096, 2048, 1024}) if m <= min(mlp_chunk, tb)):
-            est = weights + activation_bytes(cfg, tb, mc) + DEVICE_OVERHEAD
-            key = (min(tb, mc), tb + mc)
-            if est <= max_vram_bytes and (best is None or key > best[3]):
-                best = (tb, mc, est, key)
+    budgets = sorted({token_budget, 49152, 32768, 24576, 16384, 12288, 8192, 6144, 4096, 3072, 2048, 1024})
+    chunks = sorted({mlp_chunk, 16384, 12288, 8192, 6144, 4096, 2048, 1024})
+    for tb in (t for t in budgets if t <= token_budget):
+        rows = min(tb, total_tokens) if total_tokens else tb
+        n_mb = -(-total_tokens // tb) if total_tokens else 2
+        states = 1 if n_mb == 1 else STATES
+        for mc in (m for m in chunks if m <= min(mlp_chunk, tb)):
+            for qc in sorted({0, 16384, 8192, 4096, 2048}):
+                if qc and qc >= rows:
+                    continue
+                est = weights + activation_bytes(cfg, rows, mc, qkv_chunk=qc, states=states) + DEVICE_OVERHEAD
+                qeff = qc or rows
+                key = (-n_mb, min(rows, mc, qeff), mc + qeff)
+                if est <= target and (best is None or key > best[4]):
+                    best = (tb, mc, qc, est, key)
     if best is None:
         raise ValueError(f"--max_vram_gb {max_vram_bytes / 1e9:.1f}: the weight slots alone need "
                          f"{(weights + DEVICE_OVERHEAD) / 1e9:.1f} GB")
-    return best[:3]
+    return best[:4]

@@ -490,3 +490,24 @@ def test_mp_micro_budget_fills_pipeline():
     r = SimpleNamespace(token_budget=49152, plan=SimpleNamespace(mode="mp"), comm=SimpleNamespace(world=8),
                         MP_MICRO_PER_STAGE=2, MP_MIN_BUDGET=8192)
     assert ShardedRunner.micro_budget(r, small) == 8192
+
+
+def test_chunked_qkv_and_mlp_rows_match(tiny_model):
+    """Row-chunked RMSNorm + QKV (the --max_vram_gb layout) and small MLP chunks give the same
+    scores as whole-micro-batch projections."""
+    from flexible_llm_sharding_amd.engine import ShardedRunner
+    from flexible_llm_sharding_amd.models.llama import balanced_step
+    from flexible_llm_sharding_amd.runtime.stream import FileLayerSource
+    from flexible_llm_sharding_amd.utils.synthetic import synthetic_prompts
+    from flexible_llm_sharding_amd.utils.tokenizer import load_tokenizer
+    path, cfg = tiny_model
+    tok = load_tokenizer(path)
+    prompts = synthetic_prompts(5, 30, 3, 6, cfg.vocab_size, seed=4, vary=True)
+    want = ShardedRunner(cfg, FileLayerSource(cfg, path), "cpu", tok)(prompts)
+    r = ShardedRunner(cfg, FileLayerSource(cfg, path), "cpu", tok, mlp_chunk=24)
+    r.ctx.qkv_chunk = 17
+    got = r(prompts)
+    for a, b in zip(want, got):
+        assert np.abs(a.astype(np.float32) - b.astype(np.float32)).max() < 1e-5
+    assert balanced_step(43008, 16384) == 14336 and balanced_step(100, 0) == 100
+    assert balanced_step(43008, 8192) == 7168 and balanced_step(500, 1000) == 500

@@ -1,0 +1,68 @@
+"""--max_vram_gb on an MI355X: the device memory in use (hipMemGetInfo: context, code objects,
+raw weight slots, caching allocator) stays under the cap, and the scores equal the uncapped
+run's bitwise (same kernels per row; only micro-batch / chunk sizes change).  Each run is a
+fresh process: the allocator limit is process-wide."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():
+    pytest.skip("no GPU", allow_module_level=True)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+_WORKER = r"""
+import json, sys, numpy as np, torch
+sys.path.insert(0, {root!r})
+from flexible_llm_sharding_amd.config import preset
+from flexible_llm_sharding_amd.engine import ShardedRunner
+from flexible_llm_sharding_amd.runtime.weights import HostStore
+from flexible_llm_sharding_amd.utils.synthetic import synthetic_prompts
+from flexible_llm_sharding_amd.utils.tokenizer import load_tokenizer, write_synthetic_tokenizer
+cap = {cap}
+dev = torch.device("cuda", 0)
+torch.cuda.set_device(dev)
+cfg = preset("llama2-7b", num_hidden_layers=4)
+store = HostStore.synthetic(cfg, dev, seed=11)
+torch.cuda.empty_cache()
+write_synthetic_tokenizer({tok!r}, cfg.vocab_size)
+tok = load_tokenizer({tok!r})
+prompts = synthetic_prompts(12, 1024, 5, 64, cfg.vocab_size, seed=12)
+r = ShardedRunner(cfg, store, dev, tok, layer_num_per_shard=1, storage_location="cpu", max_vram_gb=cap or None)
+peak = 0
+outs = None
+for _ in range(3):
+    outs = r(prompts)
+    torch.cuda.synchronize()
+    free, total = torch.cuda.mem_get_info(dev)
+    peak = max(peak, total - free)
+np.save({out!r}, np.concatenate([o.reshape(-1) for o in outs]))
+print(json.dumps({{"peak": peak, "plan": r.vram_plan, "mb": r.stats["micro_batches"],
+                  "act_h2d": r.stats["act_h2d_bytes"], "slots": r.prefetcher.n_slots}}))
+"""
+
+
+def _run(tmp_path, cap, name):
+    out = str(tmp_path / f"{name}.npy")
+    code = _WORKER.format(root=ROOT, cap=cap, tok=str(tmp_path / "tok"), out=out)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, PYTORCH_HIP_ALLOC_CONF="expandable_segments:True"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads(r.stdout.strip().splitlines()[-1]), np.load(out)
+
+
+def test_vram_cap_holds_and_scores_match(tmp_path):
+    free = _run(tmp_path, 0, "free")
+    cap = 2.3          # Llama-2-7B geometry: 2 x 0.41 GB weight slots + ~0.67 GB context + activations
+    capped = _run(tmp_path, cap, "cap")
+    meta, got = capped
+    assert meta["peak"] <= cap * 1e9, meta
+    assert meta["slots"] == 2 and meta["plan"]["estimated_peak_bytes"] <= cap * 1e9
+    assert np.array_equal(free[1], got)
