@@ -18,25 +18,11 @@ __device__ __forceinline__ floatx4 mfma16x16x32(half8 a, half8 b, floatx4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-
-// 32x32x16 MFMA (gfx950), in place on an AGPR accumulator, memory-ordered like
-// mfma_acc_inplace_ordered.  A: lane l = row l%32, k 8*(l/32)..+7; same for B;
-// D: lane l = column l%32, element i = row 8*(i/4) + 4*(l/32) + i%4.
-__device__ __forceinline__ void mfma32_acc_inplace_ordered(floatx16& c, const half8& a, const half8& b) {
-  asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b) : "memory");
-}
-
-// In-place accumulate on an AGPR-resident accumulator (dst tied to srcC).
-// Used where all 256 AGPRs hold accumulators: the builtin lets the register
-// allocator rename dst != srcC, which with zero spare AGPRs turns into copies
-// and spills.  The caller owns MFMA->VALU hazards on `c` after the last use.
-__device__ __forceinline__ void mfma_acc_inplace(floatx4& c, const half8& a, const half8& b) {
-  asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
-}
-
-// Same, but also a compiler memory barrier: LDS reads / LDS-DMA written between
-// these statements issue exactly in source order (hand-interleaved schedules).
+// In-place accumulate on an AGPR-resident accumulator (dst tied to srcC), also a compiler
+// memory barrier: LDS reads / LDS-DMA written between these statements issue exactly in
+// source order (hand-interleaved schedules).  Used where all 256 AGPRs hold accumulators: the
+// builtin lets the register allocator rename dst != srcC, which with zero spare AGPRs turns
+// into copies and spills.  The caller owns MFMA->VALU hazards on `c` after the last use.
 __device__ __forceinline__ void mfma_acc_inplace_ordered(floatx4& c, const half8& a, const half8& b) {
   asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b) : "memory");
 }
