@@ -148,6 +148,7 @@ class ExecContext:
     sin: torch.Tensor
     mlp_chunk: int = 16384       # rows per gate/up + down chunk (bounds the [T, I] buffer)
     qkv_chunk: int = 0           # rows per RMSNorm + QKV chunk (0: all rows; bounds the normed-input buffer)
+    attn_rows: int = 0           # attention phase in prompt-aligned groups of <= this many rows (0: one group)
     prefix_entry: Optional[object] = None   # runtime.prefix_cache.PrefixEntry of the current call
     # the last decoder layer computes only the scored rows (its K/V still cover every token):
     # nothing downstream reads the other rows (final norm gathers the scored rows, utils.py:284-286)
@@ -222,21 +223,11 @@ def _attn_inputs(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, 
     return qkv
 
 
-def run_decoder(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, batch,
-                meta: dict, layer_name: str = "") -> torch.Tensor:
-    """One pre-norm decoder block on the packed rows.  With ``prune`` (the last decoder
-    layer) Q/attention/O/MLP run only for the scored rows and the result is
-    [n_scored, H]: K/V are still projected for every token (the scored rows attend to
-    the whole prefix and their own suffix).
-
-    Activation memory per micro-batch of T rows: the hidden state x (updated in place by the
-    residual epilogues) plus one workspace arena holding [normed chunk | QKV] in the attention
-    phase — the attention output overwrites the Q columns it was computed from (each (row,
-    head) is read and written by one work item) and feeds the O projection as a strided view
-    — and [normed chunk | SwiGLU chunk] in the MLP phase."""
+def _attention_whole(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, batch, meta: dict,
+                     prune: bool, layer_name: str) -> torch.Tensor:
+    """Attention phase over the whole micro-batch: QKV of every row, one attention launch, O
+    projection + residual (in place on x; the pruned last layer returns its scored rows)."""
     cfg, ops = ctx.cfg, ctx.ops
-    prune = ctx.prune_last and layer_name == ctx.last_decoder
-    eps = cfg.rms_norm_eps
     qkv = _attn_inputs(ctx, W, x, meta, prune)
     kv0 = None
     pe = ctx.prefix_entry
@@ -261,8 +252,71 @@ def run_decoder(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, b
         idx = meta["last_idx"]
         a = a.index_select(0, idx)
         x = x.index_select(0, idx)
-    x = ops.linear_residual(a, W["wo"], x, bias=W.get("bo"))
-    del a
+    return ops.linear_residual(a, W["wo"], x, bias=W.get("bo"))
+
+
+def _attention_grouped(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, batch,
+                       prune: bool) -> torch.Tensor:
+    """Attention phase in prompt-aligned row groups (``--max_vram_gb``): per group RMSNorm, QKV
+    (+ RoPE), attention with group-relative work items (every key a query sees is in its own
+    prompt), O projection + residual into x's rows — the workspace holds one group's
+    [normed | QKV] instead of the whole micro-batch's.  The pruned last layer keeps only each
+    group's scored rows (its Q for the other rows is computed and unused: 0.1% of a pass)."""
+    cfg, ops = ctx.cfg, ctx.ops
+    H, Qn, qs = cfg.hidden_size, cfg.qkv_size, cfg.q_size
+    nq, nkv, hd = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
+    work_items = getattr(ops, "uses_work_items", False)
+    pos = batch.device_tensors(x.device)["positions"]
+    outs = []
+    for g in batch.group_tensors(x.device, ctx.attn_rows):
+        r0, r1 = g["r0"], g["r1"]
+        n = r1 - r0
+        ctx.phase((n, H), (n, Qn))
+        h = ops.rmsnorm(x[r0:r1], W["ln1"], cfg.rms_norm_eps, out=ctx.scratch(n, H))
+        qkv = ops.qkv_rope(h, W["wqkv"], pos[r0:r1], ctx.cos, ctx.sin, nq, nkv, hd, bias=W.get("bqkv"),
+                           out=ctx.scratch(n, Qn))
+        del h
+        if prune:
+            arg = g["work_last"] if work_items else g["last_segments"]
+        else:
+            arg = g["work"] if work_items else g["segments"]
+        kw = {"seg_lo": g["seg_lo"]} if work_items else {}
+        a = ops.attention(qkv, arg, nq, nkv, hd, q_block=batch.q_block, out=qkv[:, :qs], **kw)
+        if prune:
+            li = g["last_local"]
+            if li.numel():
+                outs.append(ops.linear_residual(a.index_select(0, li), W["wo"], x[r0:r1].index_select(0, li),
+                                                bias=W.get("bo")))
+        else:
+            xr = x[r0:r1]
+            y = ops.linear_residual(a, W["wo"], xr, bias=W.get("bo"))
+            if y.data_ptr() != xr.data_ptr():
+                xr.copy_(y)
+        del a, qkv
+    if prune:
+        return outs[0] if len(outs) == 1 else torch.cat(outs)
+    return x
+
+
+def run_decoder(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, batch,
+                meta: dict, layer_name: str = "") -> torch.Tensor:
+    """One pre-norm decoder block on the packed rows.  With ``prune`` (the last decoder
+    layer) Q/attention/O/MLP run only for the scored rows and the result is
+    [n_scored, H]: K/V are still projected for every token (the scored rows attend to
+    the whole prefix and their own suffix).
+
+    Activation memory per micro-batch of T rows: the hidden state x (updated in place by the
+    residual epilogues) plus one workspace arena holding [normed chunk | QKV] in the attention
+    phase — the attention output overwrites the Q columns it was computed from (each (row,
+    head) is read and written by one work item) and feeds the O projection as a strided view
+    — and [normed chunk | SwiGLU chunk] in the MLP phase."""
+    cfg, ops = ctx.cfg, ctx.ops
+    prune = ctx.prune_last and layer_name == ctx.last_decoder
+    eps = cfg.rms_norm_eps
+    if ctx.attn_rows and x.shape[0] > ctx.attn_rows and ctx.prefix_entry is None:
+        x = _attention_grouped(ctx, W, x, batch, prune)
+    else:
+        x = _attention_whole(ctx, W, x, batch, meta, prune, layer_name)
     T = x.shape[0]
     I, H = cfg.intermediate_size, cfg.hidden_size
     step = balanced_step(T, max(1, ctx.mlp_chunk))

@@ -27,6 +27,7 @@ causal mask they cannot influence it.
 """
 from __future__ import annotations
 
+import dataclasses
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
 
@@ -71,11 +72,74 @@ class PackedBatch:
     q_block: int = Q_BLOCK                # query rows per work item
     pfx_src: Optional[np.ndarray] = None  # capture: packed rows of every prefix token ...
     pfx_dst: Optional[np.ndarray] = None  # ... and their rows in the prefix K/V cache
+    prompt_rows: Optional[np.ndarray] = None    # [n_prompts, 2] packed row range of each prompt
+    prompt_items: Optional[np.ndarray] = None   # [n_prompts, 2] its range of ``work`` items
+    prompt_scored: Optional[np.ndarray] = None  # [n_prompts, 2] its range of ``last_idx`` / ``work_last``
     _dev: dict = field(default_factory=dict, repr=False)
 
     @property
     def n_scored(self) -> int:
         return int(self.last_idx.shape[0])
+
+    def attn_groups(self, max_rows: int) -> List[dict]:
+        """Prompt-aligned row groups of <= ``max_rows`` packed rows (a larger prompt is a group of
+        its own) with their attention work items REBASED to the group's first row, so the
+        attention phase of a layer can run group by group on a [rows, qkv] buffer (every key a
+        query sees belongs to its own prompt).  Each group: r0, r1 (packed rows), work, seg_lo,
+        work_last (scored rows only) and last_local (scored rows, group-relative), s0, s1 (its
+        range of ``last_idx``).  Rows of the prefix K/V cache (``kv_cached``) are not rebased."""
+        groups, cur = [], []
+        n = self.prompt_rows.shape[0]
+        for j in range(n):
+            rows = int(self.prompt_rows[j, 1] - self.prompt_rows[j, 0])
+            if cur and (int(self.prompt_rows[j, 1] - self.prompt_rows[cur[0], 0]) > max_rows):
+                groups.append(cur)
+                cur = []
+            cur.append(j)
+            del rows
+        if cur:
+            groups.append(cur)
+        out = []
+        for g in groups:
+            r0, r1 = int(self.prompt_rows[g[0], 0]), int(self.prompt_rows[g[-1], 1])
+            w0, w1 = int(self.prompt_items[g[0], 0]), int(self.prompt_items[g[-1], 1])
+            s0, s1 = int(self.prompt_scored[g[0], 0]), int(self.prompt_scored[g[-1], 1])
+            out.append({"r0": r0, "r1": r1, "s0": s0, "s1": s1,
+                        "work": self._rebase(self.work[w0:w1], r0),
+                        "work_last": self._rebase(self.work_last[s0:s1], r0),
+                        "seg_lo": (self.seg_lo[r0:r1] - r0).astype(np.int32),
+                        "last_local": (self.last_idx[s0:s1] - r0).astype(np.int32)})
+        return out
+
+    def _rebase(self, work: np.ndarray, r0: int) -> np.ndarray:
+        w = work.copy()
+        w[:, 0] -= r0                                   # q_start
+        if not self.kv_cached:
+            w[:, 3] = np.where(w[:, 4] > 0, w[:, 3] - r0, 0)     # range 0 = packed prefix rows
+        w[:, 6] = np.where(w[:, 7] > 0, w[:, 6] - r0, 0)         # range 1 = packed suffix rows
+        return w
+
+    def _rebase_seg(self, sg: Segment, r0: int) -> Segment:
+        return dataclasses.replace(sg, q_start=sg.q_start - r0,
+                                   r0_start=sg.r0_start if self.kv_cached else sg.r0_start - r0,
+                                   r1_start=sg.r1_start - r0 if sg.r1_len else 0)
+
+    def group_tensors(self, device, max_rows: int) -> List[dict]:
+        """:meth:`attn_groups` with int32 metadata on ``device`` (cached)."""
+        key = (str(device), "groups", int(max_rows))
+        if key not in self._dev:
+            d = torch.device(device)
+            nb = d.type != "cpu"
+            gs = []
+            for g in self.attn_groups(max_rows):
+                t = {k: (torch.from_numpy(v).to(d, non_blocking=nb) if isinstance(v, np.ndarray) else v)
+                     for k, v in g.items()}
+                t["segments"] = [self._rebase_seg(sg, g["r0"]) for sg in self.segments
+                                 if g["r0"] <= sg.q_start < g["r1"]]
+                t["last_segments"] = [self._rebase_seg(sg, g["r0"]) for sg in self.last_segments[g["s0"]:g["s1"]]]
+                gs.append(t)
+            self._dev[key] = gs
+        return self._dev[key]
 
     def device_tensors(self, device) -> dict:
         """int32 metadata on ``device`` (cached; uploaded once, reused by all layers)."""
@@ -115,11 +179,13 @@ def pack_prompts(tps: Sequence[TokenizedPrompt], prompt_ids: Sequence[int],
     ids, pos, segs, last, nsuf, lsegs = [], [], [], [], [], []
     seg_lo, work = [], []
     src, dst = [], []
+    p_rows, p_items, p_scored = [], [], []
     t = 0
     padded = 0
     max_pos = 0
     for j, tp in enumerate(tps):
         Lp = len(tp.prefix)
+        row0, item0, sc0 = t, len(work), len(last)
         if kv_cached:
             p0 = prefix_offsets[j]
         else:
@@ -152,6 +218,9 @@ def pack_prompts(tps: Sequence[TokenizedPrompt], prompt_ids: Sequence[int],
             r1 = seg_lo[c0]
             work.append((c0, c1 - c0, c0 - r1, p0, Lp, 0, r1, c1 - r1))
         max_pos = max(max_pos, Lp + max([len(s) for s in tp.suffixes] or [0]))
+        p_rows.append((row0, t))
+        p_items.append((item0, len(work)))
+        p_scored.append((sc0, len(last)))
         nsuf.append(tp.n_suffix)
         padded += tp.padded_tokens
     work = np.asarray(work, dtype=np.int32).reshape(-1, WORK_ITEM_FIELDS)
@@ -163,7 +232,10 @@ def pack_prompts(tps: Sequence[TokenizedPrompt], prompt_ids: Sequence[int],
         work_last=_work_items(lsegs), num_tokens=t, padded_tokens=padded,
         max_pos=max_pos, kv_cached=kv_cached, q_block=q_block,
         pfx_src=np.asarray(src, dtype=np.int64) if (prefix_offsets is not None and not kv_cached) else None,
-        pfx_dst=np.asarray(dst, dtype=np.int64) if (prefix_offsets is not None and not kv_cached) else None)
+        pfx_dst=np.asarray(dst, dtype=np.int64) if (prefix_offsets is not None and not kv_cached) else None,
+        prompt_rows=np.asarray(p_rows, dtype=np.int64).reshape(-1, 2),
+        prompt_items=np.asarray(p_items, dtype=np.int64).reshape(-1, 2),
+        prompt_scored=np.asarray(p_scored, dtype=np.int64).reshape(-1, 2))
 
 
 def _items(sg: Segment, q_block: int = Q_BLOCK) -> List[tuple]:

@@ -39,14 +39,19 @@ CAP_MARGIN = 0.015
 
 
 def activation_bytes(cfg: ModelConfig, tokens: int, mlp_chunk: int, elem: int = 2, qkv_chunk: int = 0,
-                     states: int = STATES) -> int:
+                     states: int = STATES, attn_rows: int = 0) -> int:
     """Peak activation bytes of one micro-batch of ``tokens`` rows: the workspace arena
-    (models.llama: [normed chunk | QKV], then [normed chunk | SwiGLU chunk]) + live states."""
+    (models.llama: [normed chunk | QKV] — of the whole micro-batch, or of one prompt-aligned
+    group of <= ``attn_rows`` rows — then [normed chunk | SwiGLU chunk]) + live states."""
     from ..models.llama import balanced_step
-    H, I = cfg.hidden_size, cfg.intermediate_size
+    H, I, Q = cfg.hidden_size, cfg.intermediate_size, cfg.qkv_size
     chunk = balanced_step(tokens, mlp_chunk)
-    qc = balanced_step(tokens, qkv_chunk) if qkv_chunk else tokens
-    scratch = max(qc * H + tokens * cfg.qkv_size, chunk * (H + I))   # one arena, two phases
+    if attn_rows and attn_rows < tokens:
+        attn = attn_rows * (H + Q)
+    else:
+        qc = balanced_step(tokens, qkv_chunk) if qkv_chunk else tokens
+        attn = qc * H + tokens * Q
+    scratch = max(attn, chunk * (H + I))                 # one arena, two phases
     slack = SLACK_ONE if states == 1 else SLACK
     return int(slack * elem * (scratch + states * tokens * H))
 
@@ -75,14 +80,19 @@ def weight_slot_bytes(cfg: ModelConfig, lnps: int, n_slots: int = 2) -> int:
 
 def plan_for_vram(cfg: ModelConfig, max_vram_bytes: int, lnps: int = 1, n_slots: int = 2,
                   token_budget: int = 49152, mlp_chunk: int = 16384,
-                  total_tokens: Optional[int] = None) -> Tuple[int, int, int, int]:
-    """-> (token_budget, mlp_chunk, qkv_chunk, estimated peak bytes) for a call of
-    ``total_tokens`` packed tokens (None: unknown, assume several micro-batches).  Preference:
-    fewest micro-batches (one keeps the hidden state in HBM for the whole pass: no activation
-    traffic over PCIe), then the largest smaller chunk, then the largest sum; raises if nothing
-    fits."""
+                  total_tokens: Optional[int] = None, max_prompt_rows: int = 0,
+                  overhead: Optional[int] = None) -> Tuple[int, int, int, int]:
+    """-> (token_budget, mlp_chunk, attn_rows, estimated peak bytes) for a call of
+    ``total_tokens`` packed tokens (None: unknown, assume several micro-batches) whose largest
+    prompt has ``max_prompt_rows`` rows.  ``overhead``: device memory held outside the plan
+    (measured context + code objects; default DEVICE_OVERHEAD).  Preference: fewest
+    micro-batches (one keeps the hidden state in HBM for the whole pass: no activation traffic
+    over PCIe), then the largest smaller GEMM row count (attention group, MLP chunk), then the
+    largest sum; raises if nothing fits."""
+    from ..models.llama import balanced_step
     weights = weight_slot_bytes(cfg, lnps, n_slots)
     target = int(max_vram_bytes * (1.0 - CAP_MARGIN))
+    over = DEVICE_OVERHEAD if overhead is None else overhead
     best = None
     budgets = sorted({token_budget, 49152, 32768, 24576, 16384, 12288, 8192, 6144, 4096, 3072, 2048, 1024})
     chunks = sorted({mlp_chunk, 16384, 12288, 8192, 6144, 4096, 2048, 1024})
@@ -91,15 +101,15 @@ def plan_for_vram(cfg: ModelConfig, max_vram_bytes: int, lnps: int = 1, n_slots:
         n_mb = -(-total_tokens // tb) if total_tokens else 2
         states = 1 if n_mb == 1 else STATES
         for mc in (m for m in chunks if m <= min(mlp_chunk, tb)):
-            for qc in sorted({0, 16384, 8192, 4096, 2048}):
-                if qc and qc >= rows:
+            for ar in sorted({0, 16384, 12288, 8192, 4096}):
+                if ar and (ar >= rows or ar < max_prompt_rows):
                     continue
-                est = weights + activation_bytes(cfg, rows, mc, qkv_chunk=qc, states=states) + DEVICE_OVERHEAD
-                qeff = qc or rows
-                key = (-n_mb, min(rows, mc, qeff), mc + qeff)
+                est = weights + activation_bytes(cfg, rows, mc, states=states, attn_rows=ar) + over
+                aeff = ar or rows
+                key = (-n_mb, min(rows, balanced_step(rows, mc), aeff), mc + aeff)
                 if est <= target and (best is None or key > best[4]):
-                    best = (tb, mc, qc, est, key)
+                    best = (tb, mc, ar, est, key)
     if best is None:
         raise ValueError(f"--max_vram_gb {max_vram_bytes / 1e9:.1f}: the weight slots alone need "
-                         f"{(weights + DEVICE_OVERHEAD) / 1e9:.1f} GB")
+                         f"{(weights + over) / 1e9:.1f} GB")
     return best[:4]

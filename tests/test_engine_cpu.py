@@ -511,3 +511,32 @@ def test_chunked_qkv_and_mlp_rows_match(tiny_model):
         assert np.abs(a.astype(np.float32) - b.astype(np.float32)).max() < 1e-5
     assert balanced_step(43008, 16384) == 14336 and balanced_step(100, 0) == 100
     assert balanced_step(43008, 8192) == 7168 and balanced_step(500, 1000) == 500
+
+
+@pytest.mark.parametrize("prune", [True, False])
+def test_grouped_attention_phase_matches(tiny_model, prune):
+    """--max_vram_gb's attention phase in prompt-aligned row groups (group-relative work items)
+    gives the whole-micro-batch scores, with and without the pruned last layer."""
+    from flexible_llm_sharding_amd.engine import ShardedRunner
+    from flexible_llm_sharding_amd.runtime.batch import pack_prompts
+    from flexible_llm_sharding_amd.runtime.stream import FileLayerSource
+    from flexible_llm_sharding_amd.utils.synthetic import synthetic_prompts
+    from flexible_llm_sharding_amd.utils.tokenizer import load_tokenizer, tokenize_prompts
+    path, cfg = tiny_model
+    tok = load_tokenizer(path)
+    prompts = synthetic_prompts(6, 30, 3, 6, cfg.vocab_size, seed=5, vary=True)
+    want = ShardedRunner(cfg, FileLayerSource(cfg, path), "cpu", tok, prune_last_layer=prune)(prompts)
+    r = ShardedRunner(cfg, FileLayerSource(cfg, path), "cpu", tok, prune_last_layer=prune)
+    r.ctx.attn_rows = 70
+    got = r(prompts)
+    for a, b in zip(want, got):
+        assert np.abs(a.astype(np.float32) - b.astype(np.float32)).max() < 1e-5
+    # the groups cover every row / work item / scored row once, prompt-aligned
+    tps = tokenize_prompts(tok, prompts, 4096)
+    pb = pack_prompts(tps, list(range(len(tps))))
+    gs = pb.attn_groups(70)
+    assert gs[0]["r0"] == 0 and gs[-1]["r1"] == pb.num_tokens and len(gs) > 1
+    assert sum(len(g["work"]) for g in gs) == len(pb.work)
+    assert sum(len(g["last_local"]) for g in gs) == pb.n_scored
+    for g in gs:
+        assert (g["work"][:, 0] >= 0).all() and (g["work"][:, 0] + g["work"][:, 1] <= g["r1"] - g["r0"]).all()

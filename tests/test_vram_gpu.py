@@ -52,15 +52,14 @@ print(json.dumps({{"peak": peak, "plan": r.vram_plan, "mb": r.stats["micro_batch
 def _run(tmp_path, cap, name):
     out = str(tmp_path / f"{name}.npy")
     code = _WORKER.format(root=ROOT, cap=cap, tok=str(tmp_path / "tok"), out=out)
-    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
-                       env=dict(os.environ, PYTORCH_HIP_ALLOC_CONF="expandable_segments:True"))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     return json.loads(r.stdout.strip().splitlines()[-1]), np.load(out)
 
 
 def test_vram_cap_holds_and_scores_match(tmp_path):
     free = _run(tmp_path, 0, "free")
-    cap = 2.3          # Llama-2-7B geometry: 2 x 0.41 GB weight slots + ~0.67 GB context + activations
+    cap = 2.4          # Llama-2-7B geometry: 2 x 0.41 GB weight slots + ~0.67 GB context + activations
     capped = _run(tmp_path, cap, "cap")
     meta, got = capped
     assert meta["peak"] <= cap * 1e9, meta
