@@ -67,6 +67,8 @@ def parse(argv=None):
                     help="--mode mp: shard k on GPU k mod N (reference) or one contiguous stage per GPU")
     ap.add_argument("--token-budget", type=int, default=49152)
     ap.add_argument("--mlp-chunk", type=int, default=16384, help="rows per SwiGLU MLP chunk")
+    ap.add_argument("--attn-rows", type=int, default=0,
+                    help="attention phase in prompt-aligned groups of <= this many rows (A/B of the --max-vram-gb layout)")
     ap.add_argument("--slots", type=int, default=None, help="HBM weight slots (default 3, 2 under --max-vram-gb; 3 prefetches across call boundaries)")
     ap.add_argument("--max-vram-gb", type=float, default=None, help="size token budget / MLP chunk to this HBM cap")
     ap.add_argument("--resident", action="store_true")
@@ -212,6 +214,8 @@ def main(argv=None):
                            data_parallel=dp, n_slots=a.slots, hbm_cache_gb=a.hbm_cache_gb,
                            prefetcher=pf, hip_graphs=a.hip_graphs, prune_last_layer=not a.no_prune_last,
                            pipeline_stages=a.stages, max_vram_gb=a.max_vram_gb)
+    if a.attn_rows:
+        runner.ctx.attn_rows = a.attn_rows
     if runner.vram_plan:
         log(rank, f"[bench] --max-vram-gb {a.max_vram_gb}: {runner.vram_plan}")
     dev_used_peak = 0.0
@@ -238,6 +242,8 @@ def main(argv=None):
         ts = time.perf_counter()
         outs = runner(prompts)
         log(rank, f"[bench] step {i}: {time.perf_counter() - ts:.2f}s  stats={json.dumps({k: round(v, 3) for k, v in runner.stats.items()})}")
+        if i == 0 and runner.vram_plan:
+            log(rank, f"[bench] call plan: {runner.vram_plan}")
     sync()
     comm.barrier()
     elapsed = time.perf_counter() - t_start

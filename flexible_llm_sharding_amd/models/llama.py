@@ -180,8 +180,8 @@ def balanced_step(rows: int, limit: int, align: int = 256) -> int:
     return min(step, limit) if step <= limit else limit
 
 
-def _attn_inputs(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, meta: dict,
-                 prune: bool) -> torch.Tensor:
+def _attn_inputs(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, pos: torch.Tensor,
+                 last_idx: Optional[torch.Tensor], prune: bool) -> torch.Tensor:
     """RMSNorm + QKV projection (+ RoPE, + bias) of every row into one [T, qkv] buffer, in row
     chunks of ``ctx.qkv_chunk`` (only a chunk of normed rows is ever alive: the workspace holds
     [normed chunk | QKV]).  ``prune`` (the last decoder layer): K/V (+ RoPE on K) for every row,
@@ -200,7 +200,6 @@ def _attn_inputs(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, 
     if qkv is None:
         qkv = torch.empty(T0, Qn, dtype=x.dtype, device=x.device)
     w, b = W["wqkv"], W.get("bqkv")
-    pos = meta["positions"]
     for s in range(0, T0, step):
         e = min(T0, s + step)
         h = ops.rmsnorm(x[s:e], W["ln1"], eps, out=hbuf[:e - s] if hbuf is not None else None)
@@ -215,7 +214,7 @@ def _attn_inputs(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, 
             dst.copy_(r)
         del h
     if prune:
-        idx = meta["last_idx"]
+        idx = last_idx
         hq = ops.rmsnorm(x.index_select(0, idx), W["ln1"], eps)
         q = ops.qkv_rope(hq, w[:qs], pos.index_select(0, idx), ctx.cos, ctx.sin, nq, 0, hd,
                          bias=b[:qs] if b is not None else None)
@@ -228,7 +227,7 @@ def _attention_whole(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tens
     """Attention phase over the whole micro-batch: QKV of every row, one attention launch, O
     projection + residual (in place on x; the pruned last layer returns its scored rows)."""
     cfg, ops = ctx.cfg, ctx.ops
-    qkv = _attn_inputs(ctx, W, x, meta, prune)
+    qkv = _attn_inputs(ctx, W, x, meta["positions"], meta["last_idx"], prune)
     kv0 = None
     pe = ctx.prefix_entry
     if pe is not None:
@@ -260,28 +259,23 @@ def _attention_grouped(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Te
     """Attention phase in prompt-aligned row groups (``--max_vram_gb``): per group RMSNorm, QKV
     (+ RoPE), attention with group-relative work items (every key a query sees is in its own
     prompt), O projection + residual into x's rows — the workspace holds one group's
-    [normed | QKV] instead of the whole micro-batch's.  The pruned last layer keeps only each
-    group's scored rows (its Q for the other rows is computed and unused: 0.1% of a pass)."""
+    [normed | QKV] instead of the whole micro-batch's.  Same kernels per row as the whole-batch
+    path (the pruned last layer too: K/V of every row, Q of the scored rows), so the scores are
+    bitwise the same."""
     cfg, ops = ctx.cfg, ctx.ops
-    H, Qn, qs = cfg.hidden_size, cfg.qkv_size, cfg.q_size
     nq, nkv, hd = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
     work_items = getattr(ops, "uses_work_items", False)
     pos = batch.device_tensors(x.device)["positions"]
     outs = []
     for g in batch.group_tensors(x.device, ctx.attn_rows):
         r0, r1 = g["r0"], g["r1"]
-        n = r1 - r0
-        ctx.phase((n, H), (n, Qn))
-        h = ops.rmsnorm(x[r0:r1], W["ln1"], cfg.rms_norm_eps, out=ctx.scratch(n, H))
-        qkv = ops.qkv_rope(h, W["wqkv"], pos[r0:r1], ctx.cos, ctx.sin, nq, nkv, hd, bias=W.get("bqkv"),
-                           out=ctx.scratch(n, Qn))
-        del h
+        qkv = _attn_inputs(ctx, W, x[r0:r1], pos[r0:r1], g["last_local"], prune)
         if prune:
             arg = g["work_last"] if work_items else g["last_segments"]
         else:
             arg = g["work"] if work_items else g["segments"]
         kw = {"seg_lo": g["seg_lo"]} if work_items else {}
-        a = ops.attention(qkv, arg, nq, nkv, hd, q_block=batch.q_block, out=qkv[:, :qs], **kw)
+        a = ops.attention(qkv, arg, nq, nkv, hd, q_block=batch.q_block, out=qkv[:, :cfg.q_size], **kw)
         if prune:
             li = g["last_local"]
             if li.numel():
