@@ -180,6 +180,7 @@ def build_runner(args, cfg: ModelConfig, device, comm: Comm, tok, prompts=None) 
                          prefix_kv_cache=pkv,
                          prefix_cache_entries=getattr(args, "prefix_cache_entries", 8),
                          pipeline_stages=getattr(args, "pipeline_stages", "round_robin"),
+                         rx_window=getattr(args, "rx_window", 2),
                          max_vram_gb=getattr(args, "max_vram_gb", None))
 
 

@@ -79,6 +79,8 @@ def build_parser() -> argparse.ArgumentParser:
                    help="stream layer files with O_DIRECT (bypass the page cache)")
     p.add_argument("--dp_weight_shard", type=str2bool, nargs="?", const=True, default=True,
                    help="data parallel: scatter-load 1/G of each layer per GPU + RCCL all-gather")
+    p.add_argument("--rx_window", type=int, default=2,
+                   help="model parallel: HBM receive-ring slots per rank (receives in flight at the point of use)")
     p.add_argument("--pipeline_stages", choices=["round_robin", "contiguous"], default="round_robin",
                    help="model parallel: shard k on GPU k mod G (reference) or one contiguous stage per GPU")
     p.add_argument("--token_budget", type=int, default=49152,
