@@ -152,6 +152,9 @@ class ShardedRunner:
             from .runtime.prefetch import choose_kept_shards
             sizes = [sum(source.nbytes(self.names[i]) for i in sh) for sh in my]
             keep = choose_kept_shards(sizes, int(hbm_cache_gb * 1e9))
+        if prefetcher is None and self._piece_pool_ok(source, my, resident, keep, max_vram_gb, resume_dir):
+            from .runtime.prefetch import PiecePoolPrefetcher
+            prefetcher = PiecePoolPrefetcher(source, self.names, my, self.dev)
         self.prefetcher = prefetcher or ShardPrefetcher(source, self.names, my, self.dev,
                                                         n_slots=n_slots, resident=resident, keep=keep)
         if self.vram_plan is not None and self.cuda:
@@ -247,6 +250,19 @@ class ShardedRunner:
                                           h2d_stream=self.h2d_stream, d2h_stream=self.d2h_stream)
         return self._store
 
+    def _piece_pool_ok(self, source, shards, resident, keep, max_vram_gb, resume_dir) -> bool:
+        """``--max_vram_gb`` on one GPU, one layer per shard, weights in pinned host RAM: stream
+        each decoder layer as an attention piece + an MLP piece (runtime/prefetch.py
+        PiecePoolPrefetcher: 3.12 GB of weight buffers for 70B instead of 3.42, and the next
+        layer's attention weights land while this layer's MLP runs)."""
+        import os
+        if os.environ.get("FLS_PIECE_POOL", "1") == "0":
+            return False
+        return bool(self.cuda and max_vram_gb and not resident and not keep and not resume_dir
+                    and self.plan.mode == "single" and shards and all(len(s) == 1 for s in shards)
+                    and all(source.host_buffer(self.names[s[0]]) is not None for s in shards)
+                    and self.act_dtype == torch.float16 and getattr(source, "dtype", torch.float16) == torch.float16)
+
     def _mb_major(self) -> bool:
         """Model parallel with contiguous stages held resident: micro-batch-major order (a
         micro-batch runs through the whole stage and moves on), so stage r+1 starts after one
@@ -316,7 +332,8 @@ class ShardedRunner:
         tb, mc, n_slots = self._plan_req
         tb, mc, ar, est = plan_for_vram(self.cfg, self._vram_cap, self.lnps, self.prefetcher.n_slots, tb, mc,
                                         total_tokens=max(1, total), max_prompt_rows=max(rows or [0]),
-                                        overhead=self._outside)
+                                        overhead=self._outside,
+                                        weight_bytes=self.prefetcher.planned_hbm_bytes() if self.cuda else None)
         self.token_budget, self.mlp_chunk = tb, mc
         self.ctx.mlp_chunk, self.ctx.attn_rows = mc, ar
         self.vram_plan.update({"token_budget": tb, "mlp_chunk": mc, "attn_rows": ar, "estimated_peak_bytes": est,
@@ -457,9 +474,12 @@ class ShardedRunner:
                     elif k2 != k and idx + 2 < len(items):
                         store.prefetch(items[idx + 2][1])
                 tc = time.perf_counter()
+                last_use = idx + 1 >= len(items) or items[idx + 1][0] != k
                 with trace.range(f"shard{k}:mb{b}:compute"):
                     for li in shard:
                         name = self.names[li]
+                        if hasattr(W[name], "final_use"):
+                            W[name].final_use = last_use
                         state = run_layer(self.ctx, name, W[name], state, batch, meta)
                         if layer_kind(name) == "decoder":
                             flops += layer_flops(self.cfg, batch, self._pruned(name))

@@ -10,11 +10,15 @@ Decoder layer image (fp16, every slot 256-byte aligned)::
     ln1   [H]              input_layernorm.weight
     ln2   [H]              post_attention_layernorm.weight
     wqkv  [Hq+2Hkv, H]     q_proj | k_proj | v_proj   (rows concatenated)
+    bqkv  [Hq+2Hkv]        q|k|v biases (Qwen2 / attention_bias only)
     wo    [H, Hq]          o_proj
+    bo    [H]              o_proj bias (Llama attention_bias only)
     wgu   [2I, H]          gate_proj | up_proj        (rows concatenated)
     wdown [H, I]           down_proj
-    bqkv  [Hq+2Hkv]        q|k|v biases (Qwen2 / attention_bias only)
-    bo    [H]              o_proj bias (Llama attention_bias only)
+
+Everything the attention phase reads comes before ``wgu``: the image splits into an attention
+piece and an MLP piece (:func:`mlp_offset`) that the ``--max_vram_gb`` prefetcher streams into
+separate HBM pools (runtime/prefetch.py ``PiecePoolPrefetcher``).
 
 Every checkpoint tensor keeps its own row order and byte image: a slot is a
 plain concatenation of whole tensors.  The two places where the fused kernels
@@ -104,12 +108,13 @@ def layer_layout(cfg: ModelConfig, kind: str, elem_size: int = 2) -> LayerLayout
     elif kind == "norm":
         specs = [("norm", (H,))]
     elif kind == "decoder":
-        specs = [("ln1", (H,)), ("ln2", (H,)), ("wqkv", (cfg.qkv_size, H)),
-                 ("wo", (H, cfg.q_size)), ("wgu", (2 * I, H)), ("wdown", (H, I))]
+        specs = [("ln1", (H,)), ("ln2", (H,)), ("wqkv", (cfg.qkv_size, H))]
         if cfg.attention_bias:
             specs.append(("bqkv", (cfg.qkv_size,)))
+        specs.append(("wo", (H, cfg.q_size)))
         if cfg.o_proj_bias:
             specs.append(("bo", (H,)))
+        specs += [("wgu", (2 * I, H)), ("wdown", (H, I))]
     else:
         raise ValueError(kind)
     slots, off = [], 0
@@ -120,6 +125,11 @@ def layer_layout(cfg: ModelConfig, kind: str, elem_size: int = 2) -> LayerLayout
         slots.append(TensorSlot(name, tuple(shape), off))
         off += _align(n * elem_size)
     return LayerLayout(kind, tuple(slots), off, elem_size)
+
+
+def mlp_offset(lay: LayerLayout) -> int:
+    """Byte offset of a decoder image's MLP piece (``wgu``, ``wdown``); 0 for other kinds."""
+    return lay.slot("wgu").offset if lay.kind == "decoder" else 0
 
 
 @dataclass(frozen=True)

@@ -311,6 +311,9 @@ def run_decoder(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, b
         x = _attention_grouped(ctx, W, x, batch, prune)
     else:
         x = _attention_whole(ctx, W, x, batch, meta, prune, layer_name)
+    done = getattr(W, "attention_done", None)
+    if done is not None:
+        done()             # sub-layer weight streaming: the attention piece's HBM can be refilled
     T = x.shape[0]
     I, H = cfg.intermediate_size, cfg.hidden_size
     step = balanced_step(T, max(1, ctx.mlp_chunk))

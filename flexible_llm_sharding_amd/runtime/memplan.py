@@ -81,16 +81,17 @@ def weight_slot_bytes(cfg: ModelConfig, lnps: int, n_slots: int = 2) -> int:
 def plan_for_vram(cfg: ModelConfig, max_vram_bytes: int, lnps: int = 1, n_slots: int = 2,
                   token_budget: int = 49152, mlp_chunk: int = 16384,
                   total_tokens: Optional[int] = None, max_prompt_rows: int = 0,
-                  overhead: Optional[int] = None) -> Tuple[int, int, int, int]:
+                  overhead: Optional[int] = None, weight_bytes: Optional[int] = None) -> Tuple[int, int, int, int]:
     """-> (token_budget, mlp_chunk, attn_rows, estimated peak bytes) for a call of
     ``total_tokens`` packed tokens (None: unknown, assume several micro-batches) whose largest
     prompt has ``max_prompt_rows`` rows.  ``overhead``: device memory held outside the plan
-    (measured context + code objects; default DEVICE_OVERHEAD).  Preference: fewest
+    (measured context + code objects; default DEVICE_OVERHEAD); ``weight_bytes``: the weight
+    buffers actually planned (default ``n_slots`` full-shard slots).  Preference: fewest
     micro-batches (one keeps the hidden state in HBM for the whole pass: no activation traffic
     over PCIe), then the largest smaller GEMM row count (attention group, MLP chunk), then the
     largest sum; raises if nothing fits."""
     from ..models.llama import balanced_step
-    weights = weight_slot_bytes(cfg, lnps, n_slots)
+    weights = weight_slot_bytes(cfg, lnps, n_slots) if weight_bytes is None else weight_bytes
     target = int(max_vram_bytes * (1.0 - CAP_MARGIN))
     over = DEVICE_OVERHEAD if overhead is None else overhead
     best = None

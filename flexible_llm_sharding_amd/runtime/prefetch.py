@@ -331,3 +331,272 @@ class ShardPrefetcher:
         self._loaded_resident.clear()
         self._slots = [None] * len(self._slot_sizes)
         self._free_ev = [None] * len(self._slot_sizes)
+
+
+class _LayerViews(dict):
+    """One decoder layer's weight views whose MLP half may still be in flight: the attention
+    views are filled at acquire, the MLP views on first access (which orders the compute stream
+    after the MLP piece's copy).  ``attention_done()`` (models/llama.py, after the O projection)
+    hands the attention piece's HBM back to the pool when this is the layer's last use in the
+    call (``final_use``, set by the engine)."""
+
+    def __init__(self, pf: "PiecePoolPrefetcher", k: int, name: str, views: Dict[str, torch.Tensor],
+                 mlp_keys):
+        super().__init__(views)
+        self.pf, self.k, self.name = pf, k, name
+        self.mlp_keys = frozenset(mlp_keys)
+        self.final_use = False
+
+    def __missing__(self, key):
+        if key not in self.mlp_keys:
+            raise KeyError(key)
+        self.update(self.pf._mlp_views(self.k, self.name))
+        return dict.__getitem__(self, key)
+
+    def get(self, key, default=None):
+        if dict.__contains__(self, key) or key in self.mlp_keys:
+            return self[key]
+        return default
+
+    def attention_done(self) -> None:
+        if self.final_use:
+            self.pf._release_attn(self.k)
+
+
+class PiecePoolPrefetcher(ShardPrefetcher):
+    """``--max_vram_gb`` weight streaming at sub-layer granularity (lnps = 1, host-resident
+    layers): a decoder layer is an attention piece (ln1/ln2, QKV, O: 0.30 GB for 70B) and an
+    MLP piece (gate/up, down: 1.41 GB) — the packed image puts every attention weight first
+    (models/layout.py).  HBM holds ONE attention slot and TWO MLP slots (the embedding and LM
+    head use the MLP slots), 3.12 GB for 70B instead of the double buffer's 3.42 GB, and loads
+    are issued in pass order as soon as their slot is released:
+
+    * attention(k+1) lands while layer k's MLP computes (its slot frees after k's O projection);
+    * MLP(k+1) has layer k's MLP phase and layer k+1's attention phase to land (its slot held
+      MLP(k-1));
+    * at the call boundary the LM head, the next call's embedding and first attention piece all
+      load under the last layers, and the pool continues into the next call (same weights every
+      call: the reference re-streams them, ``utils.py:228-233``).
+
+    Every load waits (copy stream) for the free event recorded when its slot's previous piece
+    was released on the compute stream; a piece is only issued once that release happened."""
+
+    def __init__(self, source: LayerSource, layer_names: Sequence[str], shards: Sequence[Tuple[int, ...]],
+                 device, dtype=torch.float16):
+        self.src = source
+        self.names = list(layer_names)
+        self.shards = [tuple(s) for s in shards]
+        self.dev = torch.device(device)
+        self.cuda = self.dev.type == "cuda"
+        if not self.cuda or any(len(s) != 1 for s in self.shards):
+            raise ValueError("piece pools stream one layer per shard on a GPU")
+        self.dtype = dtype
+        self.resident = False
+        self._sticky = set()
+        self._loaded_resident = set()
+        self.epoch = 0
+        self.lock = threading.Lock()
+        self._pool = None
+        # piece list of one pass: (kind, shard, byte lo, byte hi); kind a = attention slot,
+        # m = the two alternating MLP slots, o = own small buffer
+        from ..models.layout import mlp_offset
+        self.pieces: List[Tuple[str, int, int, int]] = []
+        self._first: List[int] = []
+        a_max = m_max = 0
+        self._own: Dict[int, int] = {}
+        own_sizes: List[int] = []
+        for k, sh in enumerate(self.shards):
+            name = self.names[sh[0]]
+            lay = source.layout(name)
+            nb = source.nbytes(name)
+            self._first.append(len(self.pieces))
+            if lay.kind == "decoder":
+                split = mlp_offset(lay)
+                self.pieces.append(("a", k, 0, split))
+                self.pieces.append(("m", k, split, nb))
+                a_max, m_max = max(a_max, _align(split)), max(m_max, _align(nb - split))
+            elif nb <= (64 << 20):
+                self._own[k] = len(own_sizes)
+                own_sizes.append(_align(nb))
+                self.pieces.append(("o", k, 0, nb))
+            else:
+                self.pieces.append(("m", k, 0, nb))
+                m_max = max(m_max, _align(nb))
+        self.a_bytes, self.m_bytes = a_max, m_max
+        self._own_sizes = own_sizes
+        self.n_slots = 2
+        self.slot_bytes = m_max
+        self._slot_sizes = [a_max, m_max, m_max] + own_sizes
+        self._slots: List[Optional[torch.Tensor]] = [None] * len(self._slot_sizes)
+        self._slot_owner: List[Optional[int]] = [None] * len(self._slot_sizes)   # global piece id
+        self._slot_free: List[Optional[torch.cuda.Event]] = [None] * len(self._slot_sizes)
+        self._released = set()            # global piece ids released
+        self._issued: Dict[int, Tuple[int, torch.cuda.Event]] = {}   # global piece id -> (slot, ready)
+        self._next = 0                    # next global piece id to issue
+        self._m_turn = 0                  # MLP slot of the next m-piece (alternates across calls)
+        self._acquired = set()
+        self.copy_stream = torch.cuda.Stream(self.dev)
+        self.bytes_h2d = 0
+        self.wait_seconds = 0.0
+        self.load_seconds = 0.0
+        self._stall_ev: List[Tuple[torch.cuda.Event, torch.cuda.Event]] = []
+        for n in (self.names[s[0]] for s in self.shards):
+            if source.host_buffer(n) is None:
+                raise ValueError("piece pools need host-resident layers")
+
+    # ----------------------------------------------------------- bookkeeping
+    def planned_hbm_bytes(self) -> int:
+        return sum(self._slot_sizes)
+
+    def in_rotation(self, k: int) -> bool:
+        return k not in self._own
+
+    def is_kept_loaded(self, k: int) -> bool:
+        return False
+
+    def _gid(self, k: int, which: int = 0) -> int:
+        return self.epoch * len(self.pieces) + self._first[k] + which
+
+    def _slot_for(self, gid: int) -> int:
+        kind, k, _, _ = self.pieces[gid % len(self.pieces)]
+        if kind == "a":
+            return 0
+        if kind == "o":
+            return 3 + self._own[k]
+        return 1 + self._m_turn
+
+    # ------------------------------------------------------------------ loads
+    def _try_issue(self) -> bool:
+        gid = self._next
+        s = self._slot_for(gid)
+        owner = self._slot_owner[s]
+        if owner is not None and owner not in self._released:
+            return False                           # the slot's piece is still in use
+        kind, k, lo, hi = self.pieces[gid % len(self.pieces)]
+        name = self.names[self.shards[k][0]]
+        t0 = time.perf_counter()
+        slot = self._slot(s)
+        hb = self.src.host_buffer(name)
+        ev = torch.cuda.Event()
+        with torch.cuda.stream(self.copy_stream):
+            if self._slot_free[s] is not None:
+                self.copy_stream.wait_event(self._slot_free[s])
+            slot[:hi - lo].copy_(hb[lo:hi], non_blocking=True)
+            ev.record(self.copy_stream)
+        self.load_seconds += time.perf_counter() - t0
+        self.bytes_h2d += hi - lo
+        if owner is not None:
+            self._released.discard(owner)
+            self._issued.pop(owner, None)
+        self._slot_owner[s] = gid
+        self._released.discard(gid)
+        self._issued[gid] = (s, ev)
+        if kind == "m":
+            self._m_turn ^= 1
+        self._next += 1
+        return True
+
+    def _pump(self, need: Optional[int] = None) -> None:
+        """Issue loads in pass order while their slots are free (at least through ``need``)."""
+        while self._try_issue():
+            pass
+        if need is not None and need >= self._next:
+            raise RuntimeError(f"weight piece {need} cannot load: its slot is still held "
+                               f"(next issuable piece {self._next})")
+
+    def prefetch(self, k: int, epoch: Optional[int] = None) -> None:
+        self._pump()
+
+    def _wait(self, gid: int) -> Tuple[int, torch.cuda.Event]:
+        self._pump(gid)
+        s, ev = self._issued[gid]
+        cur = torch.cuda.current_stream(self.dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(cur)
+        cur.wait_event(ev)
+        e1.record(cur)
+        self._stall_ev.append((e0, e1))
+        return s, ev
+
+    def acquire(self, k: int) -> Dict[str, Dict[str, torch.Tensor]]:
+        t0 = time.perf_counter()
+        name = self.names[self.shards[k][0]]
+        lay = self.src.layout(name)
+        s, _ = self._wait(self._gid(k, 0))
+        self._acquired.add(k)
+        if lay.kind == "decoder":
+            from ..models.layout import mlp_offset
+            split = mlp_offset(lay)
+            es = torch.empty((), dtype=self.dtype).element_size()
+            views = {}
+            for ts in lay.slots:
+                if ts.offset < split:
+                    n = ts.numel * es
+                    views[ts.name] = self._slots[s][ts.offset:ts.offset + n].view(self.dtype).view(ts.shape)
+            out = {name: _LayerViews(self, k, name, views, [ts.name for ts in lay.slots if ts.offset >= split])}
+        else:
+            kind, _, lo, hi = self.pieces[self._first[k]]
+            out = {name: lay.views(self._slots[s][:hi - lo], self.dtype)}
+        self.wait_seconds += time.perf_counter() - t0
+        return out
+
+    def _mlp_views(self, k: int, name: str) -> Dict[str, torch.Tensor]:
+        from ..models.layout import mlp_offset
+        lay = self.src.layout(name)
+        split = mlp_offset(lay)
+        s, _ = self._wait(self._gid(k, 1))
+        es = torch.empty((), dtype=self.dtype).element_size()
+        views = {}
+        for ts in lay.slots:
+            if ts.offset >= split:
+                n = ts.numel * es
+                o = ts.offset - split
+                views[ts.name] = self._slots[s][o:o + n].view(self.dtype).view(ts.shape)
+        return views
+
+    def _release_gid(self, gid: int) -> None:
+        if gid in self._released or gid not in self._issued:
+            return
+        s, _ = self._issued[gid]
+        e = torch.cuda.Event()
+        e.record(torch.cuda.current_stream(self.dev))
+        self._slot_free[s] = e
+        self._released.add(gid)
+
+    def _release_attn(self, k: int) -> None:
+        self._release_gid(self._gid(k, 0))
+        self._pump()
+
+    def release(self, k: int) -> None:
+        if k not in self._acquired:
+            return
+        self._acquired.discard(k)
+        n = 2 if self.pieces[self._first[k]][0] == "a" else 1
+        for j in range(n):
+            self._release_gid(self._gid(k, j))
+        self._pump()
+
+    def discard_loaded(self) -> None:
+        """After an empty or aborted pass: every issued piece is dropped (its copy stays ordered
+        on the copy stream before any later load into the same slot) and the next call starts
+        its pass from the first piece."""
+        cur = torch.cuda.current_stream(self.dev)
+        for gid in list(self._issued):
+            if gid not in self._released:
+                s, _ = self._issued[gid]
+                e = torch.cuda.Event()
+                e.record(cur)
+                self._slot_free[s] = e
+                self._released.add(gid)
+        self._acquired.clear()
+        self._next = self.epoch * len(self.pieces)
+        self._m_turn = 0
+
+    def close(self):
+        if self.cuda:
+            torch.cuda.synchronize(self.dev)
+        self._issued.clear()
+        self._released.clear()
+        self._slot_owner = [None] * len(self._slot_sizes)
+        self._slot_free = [None] * len(self._slot_sizes)
+        self._slots = [None] * len(self._slot_sizes)

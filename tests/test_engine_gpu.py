@@ -297,3 +297,34 @@ def test_main_cli_on_gpu_matches_cpu(tiny_model, tmp_path, lnps):
         # agree (fp16 vs fp32 may break a near-tie on random weights)
         steps = 3 if pu == pc else 1
         assert np.abs(a[:, :steps].astype(np.float32) - b[:, :steps].astype(np.float32)).max() < 5e-3
+
+
+def test_piece_pool_prefetcher_matches_slots(mid_model, monkeypatch):
+    """--max_vram_gb on one GPU streams each decoder layer as an attention piece + an MLP piece
+    (one attention slot, two MLP slots): same scores as the double buffer over repeated calls,
+    an empty call and a call that faults mid-pass, with less weight HBM."""
+    from flexible_llm_sharding_amd.runtime.prefetch import PiecePoolPrefetcher
+    cfg, store, tok, prompts = mid_model
+    monkeypatch.setenv("FLS_PIECE_POOL", "0")
+    ref = ShardedRunner(cfg, store, "cuda:0", tok, layer_num_per_shard=1, max_vram_gb=40)
+    want = ref(prompts)
+    slots = ref.prefetcher.planned_hbm_bytes()
+    ref.close()
+    monkeypatch.setenv("FLS_PIECE_POOL", "1")
+    r = ShardedRunner(cfg, store, "cuda:0", tok, layer_num_per_shard=1, max_vram_gb=40)
+    assert isinstance(r.prefetcher, PiecePoolPrefetcher)
+    assert r.prefetcher.planned_hbm_bytes() < slots
+    for step in range(4):
+        if step == 1:
+            assert r([]) == []
+        if step == 2:
+            r._fault = 3
+            with pytest.raises(RuntimeError, match="FLS_FAULT"):
+                r(prompts)
+            r._fault = None
+        got = r(prompts)
+        for a, b in zip(want, got):
+            assert np.array_equal(a, b)
+    assert r.stats["weight_h2d_bytes"] > 0
+    r.close()
+    torch.cuda.set_per_process_memory_fraction(1.0)      # --max_vram_gb bounded the allocator
