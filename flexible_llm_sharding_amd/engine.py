@@ -102,7 +102,7 @@ class ShardedRunner:
             n_slots = 3 if (self.cuda and not resident and not max_vram_gb and prefetcher is None) else 2
         self._vram_cap = int(max_vram_gb * 1e9) if max_vram_gb else 0
         self._plan_req = (token_budget, mlp_chunk, n_slots)
-        attn_rows = 0
+        attn_rows = qkv_chunk = 0
         self._outside = None
         if max_vram_gb:
             # size the micro-batch and the QKV / MLP chunks to the HBM cap (runtime/memplan.py);
@@ -113,11 +113,10 @@ class ShardedRunner:
                 # context, code objects, (RCCL buffers) — planned as measured, not guessed
                 free, total = torch.cuda.mem_get_info(self.dev)
                 self._outside = (total - free) - torch.cuda.memory_reserved(self.dev) + (64 << 20)
-            token_budget, mlp_chunk, attn_rows, est = plan_for_vram(cfg, self._vram_cap, layer_num_per_shard,
-                                                                    n_slots, token_budget, mlp_chunk,
-                                                                    overhead=self._outside)
+            token_budget, mlp_chunk, attn_rows, qkv_chunk, est = plan_for_vram(
+                cfg, self._vram_cap, layer_num_per_shard, n_slots, token_budget, mlp_chunk, overhead=self._outside)
             self.vram_plan = {"token_budget": token_budget, "mlp_chunk": mlp_chunk, "attn_rows": attn_rows,
-                              "estimated_peak_bytes": est}
+                              "qkv_chunk": qkv_chunk, "estimated_peak_bytes": est}
         self.token_budget = token_budget
         self.mlp_chunk = mlp_chunk
         self.comm = comm or Comm(0, 1, self.dev)
@@ -139,7 +138,8 @@ class ShardedRunner:
         self.ops = get_ops(self.dev)
         cos, sin = rope_tables(cfg, max(cfg.max_position_embeddings, max_token_len),
                                torch.float16, self.dev)
-        self.ctx = ExecContext(cfg, self.ops, self.dev, self.act_dtype, cos, sin, mlp_chunk, attn_rows=attn_rows)
+        self.ctx = ExecContext(cfg, self.ops, self.dev, self.act_dtype, cos, sin, mlp_chunk, qkv_chunk=qkv_chunk,
+                               attn_rows=attn_rows)
         decs = [n for n in self.names if layer_kind(n) == "decoder"]
         self.ctx.prune_last = bool(prune_last_layer and decs)
         self.ctx.last_decoder = decs[-1] if decs else ""
@@ -330,13 +330,14 @@ class ShardedRunner:
         rows = [tp.num_tokens - (len(tp.prefix) if cached else 0) for tp in tps]
         total = sum(rows)
         tb, mc, n_slots = self._plan_req
-        tb, mc, ar, est = plan_for_vram(self.cfg, self._vram_cap, self.lnps, self.prefetcher.n_slots, tb, mc,
+        tb, mc, ar, qc, est = plan_for_vram(self.cfg, self._vram_cap, self.lnps, self.prefetcher.n_slots, tb, mc,
                                         total_tokens=max(1, total), max_prompt_rows=max(rows or [0]),
                                         overhead=self._outside,
                                         weight_bytes=self.prefetcher.planned_hbm_bytes() if self.cuda else None)
         self.token_budget, self.mlp_chunk = tb, mc
-        self.ctx.mlp_chunk, self.ctx.attn_rows = mc, ar
-        self.vram_plan.update({"token_budget": tb, "mlp_chunk": mc, "attn_rows": ar, "estimated_peak_bytes": est,
+        self.ctx.mlp_chunk, self.ctx.attn_rows, self.ctx.qkv_chunk = mc, ar, qc
+        self.vram_plan.update({"token_budget": tb, "mlp_chunk": mc, "attn_rows": ar, "qkv_chunk": qc,
+                               "estimated_peak_bytes": est,
                                "call_tokens": total})
 
     # model parallel: micro-batches per pipeline stage wanted before the budget may shrink, and the

@@ -81,15 +81,19 @@ def weight_slot_bytes(cfg: ModelConfig, lnps: int, n_slots: int = 2) -> int:
 def plan_for_vram(cfg: ModelConfig, max_vram_bytes: int, lnps: int = 1, n_slots: int = 2,
                   token_budget: int = 49152, mlp_chunk: int = 16384,
                   total_tokens: Optional[int] = None, max_prompt_rows: int = 0,
-                  overhead: Optional[int] = None, weight_bytes: Optional[int] = None) -> Tuple[int, int, int, int]:
-    """-> (token_budget, mlp_chunk, attn_rows, estimated peak bytes) for a call of
+                  overhead: Optional[int] = None, weight_bytes: Optional[int] = None) -> Tuple[int, int, int, int, int]:
+    """-> (token_budget, mlp_chunk, attn_rows, qkv_chunk, estimated peak bytes) for a call of
     ``total_tokens`` packed tokens (None: unknown, assume several micro-batches) whose largest
     prompt has ``max_prompt_rows`` rows.  ``overhead``: device memory held outside the plan
     (measured context + code objects; default DEVICE_OVERHEAD); ``weight_bytes``: the weight
-    buffers actually planned (default ``n_slots`` full-shard slots).  Preference: fewest
-    micro-batches (one keeps the hidden state in HBM for the whole pass: no activation traffic
-    over PCIe), then the largest smaller GEMM row count (attention group, MLP chunk), then the
-    largest sum; raises if nothing fits."""
+    buffers actually planned (default ``n_slots`` full-shard slots).
+
+    Preference, by measured cost on the 70B pass (one box, ``profiles/r3_vram``): fewest
+    micro-batches (one keeps the hidden state in HBM: no activation traffic over PCIe), then the
+    largest MLP chunk (14,336 vs 10,752 rows: 2.1% of a pass, GEMM tile-round tails), then the
+    whole micro-batch in one attention phase (prompt-aligned groups: ~1%) with the QKV
+    projection in the largest row chunks that fit, then the largest groups; raises if nothing
+    fits."""
     from ..models.llama import balanced_step
     weights = weight_slot_bytes(cfg, lnps, n_slots) if weight_bytes is None else weight_bytes
     target = int(max_vram_bytes * (1.0 - CAP_MARGIN))
@@ -102,15 +106,19 @@ def plan_for_vram(cfg: ModelConfig, max_vram_bytes: int, lnps: int = 1, n_slots:
         n_mb = -(-total_tokens // tb) if total_tokens else 2
         states = 1 if n_mb == 1 else STATES
         for mc in (m for m in chunks if m <= min(mlp_chunk, tb)):
-            for ar in sorted({0, 16384, 12288, 8192, 4096}):
+            mce = balanced_step(rows, mc)
+            for ar in sorted({0, 32768, 24576, 16384, 12288, 8192, 4096}):
                 if ar and (ar >= rows or ar < max_prompt_rows):
                     continue
-                est = weights + activation_bytes(cfg, rows, mc, states=states, attn_rows=ar) + over
-                aeff = ar or rows
-                key = (-n_mb, min(rows, balanced_step(rows, mc), aeff), mc + aeff)
-                if est <= target and (best is None or key > best[4]):
-                    best = (tb, mc, ar, est, key)
+                for qc in ((0, 16384, 8192, 4096, 2048) if ar == 0 else (0,)):
+                    if qc and qc >= rows:
+                        continue
+                    est = weights + over + activation_bytes(cfg, rows, mc, qkv_chunk=qc, states=states,
+                                                            attn_rows=ar)
+                    key = (-n_mb, mce, ar == 0, balanced_step(rows, qc) if qc else rows, ar)
+                    if est <= target and (best is None or key > best[5]):
+                        best = (tb, mc, ar, qc, est, key)
     if best is None:
         raise ValueError(f"--max_vram_gb {max_vram_bytes / 1e9:.1f}: the weight slots alone need "
                          f"{(weights + over) / 1e9:.1f} GB")
-    return best[:4]
+    return best[:5]
