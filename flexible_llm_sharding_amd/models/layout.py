@@ -8,17 +8,18 @@ as large DMAs and every kernel gets raw pointers at fixed offsets.
 Decoder layer image (fp16, every slot 256-byte aligned)::
 
     ln1   [H]              input_layernorm.weight
-    ln2   [H]              post_attention_layernorm.weight
     wqkv  [Hq+2Hkv, H]     q_proj | k_proj | v_proj   (rows concatenated)
     bqkv  [Hq+2Hkv]        q|k|v biases (Qwen2 / attention_bias only)
     wo    [H, Hq]          o_proj
     bo    [H]              o_proj bias (Llama attention_bias only)
+    ln2   [H]              post_attention_layernorm.weight
     wgu   [2I, H]          gate_proj | up_proj        (rows concatenated)
     wdown [H, I]           down_proj
 
-Everything the attention phase reads comes before ``wgu``: the image splits into an attention
-piece and an MLP piece (:func:`mlp_offset`) that the ``--max_vram_gb`` prefetcher streams into
-separate HBM pools (runtime/prefetch.py ``PiecePoolPrefetcher``).
+Everything the attention phase reads comes before ``ln2`` and nothing after it: the image
+splits into an attention piece and an MLP piece (:func:`mlp_offset`) that the
+``--max_vram_gb`` prefetcher streams into separate HBM pools and frees separately
+(runtime/prefetch.py ``PiecePoolPrefetcher``).
 
 Every checkpoint tensor keeps its own row order and byte image: a slot is a
 plain concatenation of whole tensors.  The two places where the fused kernels
@@ -108,13 +109,13 @@ def layer_layout(cfg: ModelConfig, kind: str, elem_size: int = 2) -> LayerLayout
     elif kind == "norm":
         specs = [("norm", (H,))]
     elif kind == "decoder":
-        specs = [("ln1", (H,)), ("ln2", (H,)), ("wqkv", (cfg.qkv_size, H))]
+        specs = [("ln1", (H,)), ("wqkv", (cfg.qkv_size, H))]
         if cfg.attention_bias:
             specs.append(("bqkv", (cfg.qkv_size,)))
         specs.append(("wo", (H, cfg.q_size)))
         if cfg.o_proj_bias:
             specs.append(("bo", (H,)))
-        specs += [("wgu", (2 * I, H)), ("wdown", (H, I))]
+        specs += [("ln2", (H,)), ("wgu", (2 * I, H)), ("wdown", (H, I))]
     else:
         raise ValueError(kind)
     slots, off = [], 0
@@ -128,8 +129,8 @@ def layer_layout(cfg: ModelConfig, kind: str, elem_size: int = 2) -> LayerLayout
 
 
 def mlp_offset(lay: LayerLayout) -> int:
-    """Byte offset of a decoder image's MLP piece (``wgu``, ``wdown``); 0 for other kinds."""
-    return lay.slot("wgu").offset if lay.kind == "decoder" else 0
+    """Byte offset of a decoder image's MLP piece (``ln2``, ``wgu``, ``wdown``); 0 for other kinds."""
+    return lay.slot("ln2").offset if lay.kind == "decoder" else 0
 
 
 @dataclass(frozen=True)

@@ -90,3 +90,16 @@ def test_int8_rejected():
     sd = {"model.norm.weight": torch.ones(cfg.hidden_size, dtype=torch.int8)}
     with pytest.raises(AssertionError, match="int8"):
         pack_layer(cfg, "model.norm", sd)
+
+
+def test_decoder_image_splits_into_attention_and_mlp_pieces():
+    """Sub-layer streaming (PiecePoolPrefetcher) frees the attention piece before the MLP phase:
+    every tensor the MLP phase reads (ln2, gate/up, down) must sit at or after mlp_offset, every
+    attention tensor before it."""
+    from flexible_llm_sharding_amd.config import preset
+    from flexible_llm_sharding_amd.models.layout import layer_layout, mlp_offset
+    for name in ("tiny", "tiny-qwen2", "llama2-70b"):
+        lay = layer_layout(preset(name), "decoder")
+        split = mlp_offset(lay)
+        for ts in lay.slots:
+            assert (ts.offset >= split) == (ts.name in ("ln2", "wgu", "wdown")), (name, ts.name)
