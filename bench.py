@@ -70,7 +70,10 @@ def parse(argv=None):
     ap.add_argument("--attn-rows", type=int, default=0,
                     help="attention phase in prompt-aligned groups of <= this many rows (A/B of the --max-vram-gb layout)")
     ap.add_argument("--slots", type=int, default=None, help="HBM weight slots (default 3, 2 under --max-vram-gb; 3 prefetches across call boundaries)")
-    ap.add_argument("--max-vram-gb", type=float, default=None, help="size token budget / MLP chunk to this HBM cap")
+    ap.add_argument("--max-vram-gb", type=float, default=None,
+                    help="HBM cap per GPU (sizes micro-batch / chunks, sub-layer weight streaming). Default: 6 for "
+                         "the 70B lnps=1 headline on one GPU (the reference's 70B-in-6-GB envelope, README.md:2; "
+                         "BASELINE config 3), none otherwise (e.g. N > 1 data parallel); 0 = no cap")
     ap.add_argument("--resident", action="store_true")
     ap.add_argument("--hbm-cache-gb", type=float, default=0.0,
                     help="keep this many GB of layers resident in HBM, stream the rest (not the headline config)")
@@ -134,6 +137,11 @@ def main(argv=None):
     a = parse(argv)
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return spawn_ranks(a, argv)
+    if a.max_vram_gb is None:
+        headline = a.model == "llama2-70b" and a.lnps == 1 and a.num_layers is None
+        a.max_vram_gb = 6.0 if (headline and a.gpus == 1 and not a.cpu and not a.resident
+                                and a.hbm_cache_gb == 0) else 0.0
+    a.max_vram_gb = a.max_vram_gb or None
     if a.max_vram_gb and not a.cpu:
         # a VRAM cap: let the caching allocator grow segments in place instead of keeping one
         # rounded block per size class and stream (set before the first HIP allocation)

@@ -528,9 +528,9 @@ class ShardedRunner:
                     pf.discard_loaded()
                 if inbox is not None:
                     inbox.abort()
-        h2d_end = pf.bytes_h2d
         if cur_k >= 0:
             pf.release(cur_k)
+        h2d_end = pf.bytes_h2d         # after the last release: loads it triggers count to this call
         if items:
             pf.epoch += 1              # the next call's loads continue the slot round-robin
         elif not collective:
