@@ -226,11 +226,14 @@ def run_all(args, runner: ShardedRunner, comm: Comm, prompts: Sequence) -> List[
     raise RuntimeError("no rank produced scores")
 
 
-def generation_loop(args, runner, comm: Comm, tok, original_prompts: Sequence):
-    """main.py:63-90 — greedy extension of every suffix, full re-run per step."""
+def generation_loop(args, runner, comm: Comm, tok, original_prompts: Sequence, step_times: Optional[list] = None):
+    """main.py:63-90 — greedy extension of every suffix, one full pass per step (the prefix K/V
+    cache and the HBM weight cache, on by default for repeated passes, make the later passes
+    cheaper; the scores are the same).  ``step_times`` collects each step's wall time."""
     input_prompts = copy.deepcopy(list(original_prompts))
     output_scores: List[np.ndarray] = []
     for i_new in range(args.num_gen_token):
+        t_step = time.perf_counter()
         outputs = run_all(args, runner, comm, input_prompts)
         if comm.rank == 0:
             if i_new == 0:
@@ -244,6 +247,10 @@ def generation_loop(args, runner, comm: Comm, tok, original_prompts: Sequence):
                 input_prompts[pi] = (prefix, new_suffix)
         if comm.world > 1:
             input_prompts = comm.broadcast_object(input_prompts, src=0)
+        if step_times is not None:
+            step_times.append(time.perf_counter() - t_step)
+        if getattr(args, "verbose", False) and comm.rank == 0:
+            print(f"step {i_new}: {time.perf_counter() - t_step:.3f}s", flush=True)
     return output_scores, input_prompts
 
 
@@ -268,12 +275,15 @@ def run_rank(args, comm: Comm) -> Optional[dict]:
     runner = build_runner(args, cfg, device, comm, tok, original)
     t_build = time.perf_counter() - t0
     t1 = time.perf_counter()
-    scores, updated = generation_loop(args, runner, comm, tok, original)
+    step_times: List[float] = []
+    scores, updated = generation_loop(args, runner, comm, tok, original, step_times)
     t_run = time.perf_counter() - t1
     tokens = comm.all_reduce_sum(runner.stats.get("tokens", 0.0)) if not (
         comm.world > 1 and not args.data_parallel) else runner.stats.get("tokens", 0.0)
     metrics = {"device": str(device), "world": comm.world, "build_s": t_build, "run_s": t_run,
-               "tokens_last_pass": tokens, "stats": runner.stats}
+               "step_s": step_times, "tokens_last_pass": tokens, "stats": runner.stats,
+               "hbm_cache_kept_shards": len(getattr(runner.prefetcher, "_sticky", ())),
+               "prefix_kv_cache": runner.prefix_cache is not None}
     if device.type == "cuda":
         metrics["peak_hbm_bytes"] = torch.cuda.max_memory_allocated(device)
     if comm.rank == 0:
