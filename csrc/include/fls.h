@@ -82,6 +82,8 @@ int fls_gemm_set_mid(int on);   // 64x128-tile kernel for small / medium M (defa
 int fls_attention(const void* qkv, void* out, const int* work, int n_items, int n_q_heads,
                   int n_kv_heads, int head_dim, int ld_qkv, int ld_out, float scale, const void* kv0,
                   int ld_kv0, const int* seg_lo, int q_block, fls_stream_t s);
+int fls_headnorm_rope(void* x, int ldx, int rows, int n_q, int n_k, const void* qn, const void* kn, const int* pos,
+                      const float* cos_t, const float* sin_t, int hd, float eps, fls_stream_t s);
 int fls_rmsnorm(const void* x, const void* w, void* y, const int* row_idx, int rows, int H,
                 int ldx, int ldy, float eps, fls_stream_t s);
 int fls_embed(const int* ids, const void* table, void* out, int T, int H, int V, fls_stream_t s);

@@ -266,7 +266,51 @@ __global__ __launch_bounds__(256) void gemv_skinny_kernel(const half_t* __restri
     if (nb + r < N) cp[nb + r] = (half_t)a1[r];
   }
 }
+// Qwen3 q/k head norm + RoPE, in place on the projection output:
+//   head h < n_q:        x_h <- rope( fp16( qn * fp16( x_h * rsqrt(mean(x_h^2) + eps) ) ) )
+//   n_q <= h < n_q+n_k:  same with kn
+// (HF Qwen3RMSNorm cast points, then rotate-half RoPE in fp32 on the normalised fp16 values).
+// One wave per (row, head): lane p holds the rotate-half pair (p, p + hd/2), so the norm is one
+// wave reduction and the rotation lane-local.  hd in {64, 128}.
+__global__ __launch_bounds__(256) void headnorm_rope_kernel(half_t* __restrict__ x, int ldx, int rows, int n_q,
+                                                          int n_k, const half_t* __restrict__ qn,
+                                                          const half_t* __restrict__ kn, const int* __restrict__ pos,
+                                                          const float* __restrict__ cos_t,
+                                                          const float* __restrict__ sin_t, int hd, float eps) {
+  const int r = blockIdx.x;
+  const int h = blockIdx.y * 4 + (threadIdx.x >> 6);
+  const int p = threadIdx.x & 63;
+  const int half = hd >> 1;
+  if (r >= rows || h >= n_q + n_k) return;          // wave-uniform
+  half_t* xh = x + (size_t)r * ldx + (size_t)h * hd;
+  const half_t* w = h < n_q ? qn : kn;
+  const bool on = p < half;
+  const float a = on ? (float)xh[p] : 0.f;
+  const float b = on ? (float)xh[p + half] : 0.f;
+  const float ss = warp_sum(a * a + b * b);
+  const float rs = rsqrtf(ss / (float)hd + eps);
+  if (!on) return;
+  const float na = (float)(half_t)((float)w[p] * (float)(half_t)(a * rs));
+  const float nb = (float)(half_t)((float)w[p + half] * (float)(half_t)(b * rs));
+  const int q = pos[r];
+  const float c = cos_t[(size_t)q * half + p], sn = sin_t[(size_t)q * half + p];
+  xh[p] = (half_t)(na * c - nb * sn);
+  xh[p + half] = (half_t)(nb * c + na * sn);
+}
+
 }  // namespace
+
+extern "C" int fls_headnorm_rope(void* x, int ldx, int rows, int n_q, int n_k, const void* qn, const void* kn,
+                                 const int* pos, const float* cos_t, const float* sin_t, int hd, float eps,
+                                 fls_stream_t s) {
+  if (rows <= 0 || n_q + n_k <= 0) return 0;
+  if (hd != 64 && hd != 128) return -3;
+  dim3 grid(rows, (n_q + n_k + 3) / 4);
+  hipLaunchKernelGGL(headnorm_rope_kernel, grid, dim3(256), 0, (hipStream_t)s, (half_t*)x, ldx, rows, n_q, n_k,
+                     (const half_t*)qn, (const half_t*)kn, pos, cos_t, sin_t, hd, eps);
+  FLS_CHECK_LAUNCH();
+  return 0;
+}
 
 extern "C" int fls_rmsnorm(const void* x, const void* w, void* y, const int* row_idx, int rows, int H, int ldx,
                            int ldy, float eps, fls_stream_t s) {

@@ -80,6 +80,8 @@ def _load_kernels():
           c_int, c_int, c_float, c_void_p, c_int, c_void_p, c_int, c_void_p)
     _bind(lib, "fls_rmsnorm", c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
           c_int, c_float, c_void_p)
+    _bind(lib, "fls_headnorm_rope", c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+          c_void_p, c_void_p, c_int, c_float, c_void_p)
     _bind(lib, "fls_embed", c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p)
     _bind(lib, "fls_softmax_rows", c_int, c_void_p, c_void_p, c_int, c_int, c_void_p)
     _bind(lib, "fls_cast_f16", c_int, c_void_p, c_void_p, c_int, c_uint64, c_void_p)

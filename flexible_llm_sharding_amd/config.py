@@ -30,6 +30,7 @@ class ModelConfig:
     tie_word_embeddings: bool = False
     attention_bias: bool = False        # q/k/v projection biases (Qwen2; Llama attention_bias)
     o_proj_bias: bool = False           # o_proj bias (Llama attention_bias=True)
+    qk_norm: bool = False               # Qwen3: RMSNorm over head_dim on every q / k head, before RoPE
     sliding_window: Optional[int] = None  # Mistral; must cover the token cap (checked by the runner)
     # RoPE frequency scaling (HF ``rope_scaling`` / v5 ``rope_parameters``): linear, llama3, yarn
     rope_scaling: Optional[dict] = None
@@ -70,8 +71,9 @@ class ModelConfig:
 
     def decoder_layer_params(self) -> int:
         h, i = self.hidden_size, self.intermediate_size
-        n = h * self.qkv_size + h * h + 3 * h * i + 2 * h
-        return n + (self.qkv_size if self.attention_bias else 0) + (h if self.o_proj_bias else 0)
+        n = h * self.qkv_size + self.q_size * h + 3 * h * i + 2 * h
+        return (n + (self.qkv_size if self.attention_bias else 0) + (h if self.o_proj_bias else 0)
+                + (2 * self.head_dim if self.qk_norm else 0))
 
     def total_params(self) -> int:
         emb = self.vocab_size * self.hidden_size
@@ -128,6 +130,10 @@ class ModelConfig:
             kw["attention_bias"], kw["o_proj_bias"] = True, False
         elif d.get("attention_bias"):
             kw["attention_bias"], kw["o_proj_bias"] = True, True
+        if mt == "qwen3":
+            # HF Qwen3Attention: q_norm / k_norm (RMSNorm over head_dim) on every head before RoPE;
+            # q/k/v/o biases only with attention_bias (off in every released Qwen3 config)
+            kw["qk_norm"] = True
         if not d.get("use_sliding_window", mt == "mistral"):
             kw.pop("sliding_window", None)
         if isinstance(kw.get("eos_token_id"), list):
@@ -157,7 +163,7 @@ class ModelConfig:
 # Llama-structured causal LMs (model.embed_tokens / model.layers.N / model.norm / lm_head with
 # q/k/v/o + gate/up/down + two RMSNorms per layer) -- what the reference's AutoModelForCausalLM
 # path (utils.py:101-115) runs in practice.
-SUPPORTED_MODEL_TYPES = {"llama", "mistral", "qwen2"}
+SUPPORTED_MODEL_TYPES = {"llama", "mistral", "qwen2", "qwen3"}
 # static RoPE scalings: they only change the cos/sin tables (models/llama.py rope_inv_freq)
 ROPE_SCALING_TYPES = {"linear", "llama3", "yarn"}
 
@@ -184,6 +190,15 @@ PRESETS = {
                        num_key_value_heads=2, num_hidden_layers=2, vocab_size=512, rope_theta=1e6,
                        rms_norm_eps=1e-6, attention_bias=True, model_type="qwen2",
                        architectures=["Qwen2ForCausalLM"]),
+    # Qwen3 dense: per-head q/k RMSNorm, explicit head_dim 128 (hidden 4096 = 32 x 128 here)
+    "qwen3-8b": dict(hidden_size=4096, intermediate_size=12288, num_attention_heads=32,
+                     num_key_value_heads=8, num_hidden_layers=36, vocab_size=151936, rope_theta=1e6,
+                     rms_norm_eps=1e-6, qk_norm=True, explicit_head_dim=128, max_position_embeddings=40960,
+                     model_type="qwen3", architectures=["Qwen3ForCausalLM"]),
+    "tiny-qwen3": dict(hidden_size=256, intermediate_size=512, num_attention_heads=4,
+                       num_key_value_heads=2, num_hidden_layers=2, vocab_size=512, rope_theta=1e6,
+                       rms_norm_eps=1e-6, qk_norm=True, explicit_head_dim=128, model_type="qwen3",
+                       architectures=["Qwen3ForCausalLM"]),
     # Llama-3.1 geometry (GQA 8:1, 128k vocab, llama3 RoPE scaling)
     "llama3.1-8b": dict(hidden_size=4096, intermediate_size=14336, num_attention_heads=32,
                         num_key_value_heads=8, num_hidden_layers=32, vocab_size=128256, rope_theta=500000.0,

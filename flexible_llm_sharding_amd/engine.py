@@ -100,6 +100,7 @@ class ShardedRunner:
             # +2.8 GB of HBM on 70B.  The double buffer under a VRAM cap (the 6 GB mode), for
             # resident weights and for the external data-parallel prefetcher.
             n_slots = 3 if (self.cuda and not resident and not max_vram_gb and prefetcher is None) else 2
+        self.comm = comm or Comm(0, 1, self.dev)
         self._vram_cap = int(max_vram_gb * 1e9) if max_vram_gb else 0
         self._plan_req = (token_budget, mlp_chunk, n_slots)
         attn_rows = qkv_chunk = 0
@@ -110,7 +111,14 @@ class ShardedRunner:
             from .runtime.memplan import plan_for_vram
             if self.dev.type == "cuda":
                 # device memory held outside the caching allocator before any weight slot exists:
-                # context, code objects, (RCCL buffers) — planned as measured, not guessed
+                # context, code objects, RCCL buffers — planned as measured, not guessed.  The
+                # communicators allocate their buffers at their first collective: run one on every
+                # group this runner uses first (the data-parallel gather group)
+                if self.comm.active:
+                    self.comm.warmup()
+                    pcomm = getattr(prefetcher, "comm", None)
+                    if pcomm is not None and pcomm is not self.comm:
+                        pcomm.warmup()
                 free, total = torch.cuda.mem_get_info(self.dev)
                 self._outside = (total - free) - torch.cuda.memory_reserved(self.dev) + (64 << 20)
             token_budget, mlp_chunk, attn_rows, qkv_chunk, est = plan_for_vram(
@@ -119,7 +127,6 @@ class ShardedRunner:
                               "qkv_chunk": qkv_chunk, "estimated_peak_bytes": est}
         self.token_budget = token_budget
         self.mlp_chunk = mlp_chunk
-        self.comm = comm or Comm(0, 1, self.dev)
         self.data_parallel = data_parallel
         self.verbose = verbose
         self.max_token_len = max_token_len

@@ -10,6 +10,8 @@ Decoder layer image (fp16, every slot 256-byte aligned)::
     ln1   [H]              input_layernorm.weight
     wqkv  [Hq+2Hkv, H]     q_proj | k_proj | v_proj   (rows concatenated)
     bqkv  [Hq+2Hkv]        q|k|v biases (Qwen2 / attention_bias only)
+    qn    [hd]             q_norm.weight (Qwen3 only)
+    kn    [hd]             k_norm.weight (Qwen3 only)
     wo    [H, Hq]          o_proj
     bo    [H]              o_proj bias (Llama attention_bias only)
     ln2   [H]              post_attention_layernorm.weight
@@ -112,6 +114,8 @@ def layer_layout(cfg: ModelConfig, kind: str, elem_size: int = 2) -> LayerLayout
         specs = [("ln1", (H,)), ("wqkv", (cfg.qkv_size, H))]
         if cfg.attention_bias:
             specs.append(("bqkv", (cfg.qkv_size,)))
+        if cfg.qk_norm:
+            specs += [("qn", (cfg.head_dim,)), ("kn", (cfg.head_dim,))]
         specs.append(("wo", (H, cfg.q_size)))
         if cfg.o_proj_bias:
             specs.append(("bo", (H,)))
@@ -180,6 +184,10 @@ def placements(cfg: ModelConfig, layer_name: str, elem_size: int = 2) -> List[Pl
                 Placement(f"{p}.self_attn.v_proj.bias", o["bqkv"] + es * (qs + ks), ks, (ks,), es)]
     if cfg.o_proj_bias:
         out.append(Placement(f"{p}.self_attn.o_proj.bias", o["bo"], H, (H,), es))
+    if cfg.qk_norm:
+        hd = cfg.head_dim
+        out += [Placement(f"{p}.self_attn.q_norm.weight", o["qn"], hd, (hd,), es),
+                Placement(f"{p}.self_attn.k_norm.weight", o["kn"], hd, (hd,), es)]
     return out
 
 

@@ -200,24 +200,29 @@ def _attn_inputs(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, 
     if qkv is None:
         qkv = torch.empty(T0, Qn, dtype=x.dtype, device=x.device)
     w, b = W["wqkv"], W.get("bqkv")
+
+    def proj(h, wr, p, n_q, n_k, bias, out=None):
+        if cfg.qk_norm:           # Qwen3: per-head RMSNorm on q / k before RoPE
+            return ops.qkv_norm_rope(h, wr, p, ctx.cos, ctx.sin, n_q, n_k, hd, W["qn"], W["kn"], eps,
+                                     bias=bias, out=out)
+        return ops.qkv_rope(h, wr, p, ctx.cos, ctx.sin, n_q, n_k, hd, bias=bias, out=out)
+
     for s in range(0, T0, step):
         e = min(T0, s + step)
         h = ops.rmsnorm(x[s:e], W["ln1"], eps, out=hbuf[:e - s] if hbuf is not None else None)
         if prune:
             dst = qkv[s:e, qs:]
-            r = ops.qkv_rope(h, w[qs:], pos[s:e], ctx.cos, ctx.sin, 0, nkv, hd,
-                             bias=b[qs:] if b is not None else None, out=dst)
+            r = proj(h, w[qs:], pos[s:e], 0, nkv, b[qs:] if b is not None else None, out=dst)
         else:
             dst = qkv[s:e]
-            r = ops.qkv_rope(h, w, pos[s:e], ctx.cos, ctx.sin, nq, nkv, hd, bias=b, out=dst)
+            r = proj(h, w, pos[s:e], nq, nkv, b, out=dst)
         if r.data_ptr() != dst.data_ptr():
             dst.copy_(r)
         del h
     if prune:
         idx = last_idx
         hq = ops.rmsnorm(x.index_select(0, idx), W["ln1"], eps)
-        q = ops.qkv_rope(hq, w[:qs], pos.index_select(0, idx), ctx.cos, ctx.sin, nq, 0, hd,
-                         bias=b[:qs] if b is not None else None)
+        q = proj(hq, w[:qs], pos.index_select(0, idx), nq, 0, b[:qs] if b is not None else None)
         qkv[:, :qs].index_copy_(0, idx if idx.dtype == torch.int64 else idx.long(), q)
     return qkv
 

@@ -43,6 +43,9 @@ def _block(x, sd, p, cfg, pos, cos, sin, mask, past_kv=None):
     q = (h @ g("self_attn.q_proj.weight").t() + b("self_attn.q_proj.bias")).view(B, T, nh, hd).transpose(1, 2)
     k = (h @ g("self_attn.k_proj.weight").t() + b("self_attn.k_proj.bias")).view(B, T, nkv, hd).transpose(1, 2)
     v = (h @ g("self_attn.v_proj.weight").t() + b("self_attn.v_proj.bias")).view(B, T, nkv, hd).transpose(1, 2)
+    if cfg.qk_norm:                   # HF Qwen3Attention: RMSNorm over head_dim before RoPE
+        q = _rms(q, g("self_attn.q_norm.weight"), cfg.rms_norm_eps)
+        k = _rms(k, g("self_attn.k_norm.weight"), cfg.rms_norm_eps)
     q, k = _rope(q, pos, cos, sin), _rope(k, pos, cos, sin)
     if past_kv is not None:
         k = torch.cat([past_kv[0], k], 2)

@@ -103,6 +103,21 @@ class HipOps:
         return self.gemm(x, wqkv, EPI_ROPE, out=out, positions=positions, cos=cos, sin=sin,
                          rope_cols=rope_cols, head_dim=head_dim, bias=bias)
 
+    def qkv_norm_rope(self, x, wqkv, positions, cos, sin, n_q_heads, n_kv_heads, head_dim, qn, kn, eps,
+                      bias=None, out=None):
+        """Qwen3: projection (+ bias), then RMSNorm over head_dim on every q / k head (q_norm /
+        k_norm weights) and RoPE, in place (``headnorm_rope_kernel``); V columns untouched."""
+        if positions.dtype != torch.int32:
+            raise TypeError("positions must be int32")
+        y = self.gemm(x, wqkv, EPI_NONE, out=out, bias=bias)
+        _f16(qn, "q_norm")
+        _f16(kn, "k_norm")
+        rc = self.k.fls_headnorm_rope(y.data_ptr(), y.stride(0), y.shape[0], n_q_heads, n_kv_heads, qn.data_ptr(),
+                                      kn.data_ptr(), positions.data_ptr(), cos.data_ptr(), sin.data_ptr(), head_dim,
+                                      float(eps), _stream())
+        _chk(rc, "fls_headnorm_rope")
+        return y
+
     # ----------------------------------------------------------- attention
     def attention(self, qkv, work, n_q_heads, n_kv_heads, head_dim, kv0=None, q_block: int = 64, out=None,
                   seg_lo=None):

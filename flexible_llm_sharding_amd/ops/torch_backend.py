@@ -67,6 +67,29 @@ class TorchOps:
         qk_out = torch.stack([o1, o2], dim=2).reshape(T, qk_cols)
         return torch.cat([qk_out, y[:, qk_cols:]], dim=1).to(x.dtype)
 
+    def qkv_norm_rope(self, x: torch.Tensor, wqkv: torch.Tensor, positions: torch.Tensor, cos: torch.Tensor,
+                      sin: torch.Tensor, n_q_heads: int, n_kv_heads: int, head_dim: int, qn: torch.Tensor,
+                      kn: torch.Tensor, eps: float, bias: torch.Tensor = None, out=None) -> torch.Tensor:
+        """Qwen3 projection: RMSNorm over head_dim on the q (q_norm) and k (k_norm) heads, then RoPE."""
+        y = self._c(x) @ self._c(wqkv).t()
+        if bias is not None:
+            y = y + self._c(bias)
+        y = y.to(x.dtype)
+        T = y.shape[0]
+        nqk = n_q_heads + n_kv_heads
+        heads = y[:, :nqk * head_dim].reshape(T, nqk, head_dim).float()
+        var = heads.pow(2).mean(-1, keepdim=True)
+        normed = (heads * torch.rsqrt(var + eps)).to(x.dtype)
+        w = torch.cat([qn.reshape(1, -1).expand(n_q_heads, -1), kn.reshape(1, -1).expand(n_kv_heads, -1)])
+        normed = (self._c(w)[None] * self._c(normed)).to(x.dtype)
+        half = head_dim // 2
+        qk = self._c(normed).reshape(T, nqk, 2, half)
+        c = cos.index_select(0, positions.long()).to(self.cdt).reshape(T, 1, half)
+        s = sin.index_select(0, positions.long()).to(self.cdt).reshape(T, 1, half)
+        x1, x2 = qk[:, :, 0, :], qk[:, :, 1, :]
+        qk_out = torch.stack([x1 * c - x2 * s, x2 * c + x1 * s], dim=2).reshape(T, nqk * head_dim)
+        return torch.cat([qk_out.to(x.dtype), y[:, nqk * head_dim:]], dim=1)
+
     def attention(self, qkv: torch.Tensor, segments, n_q_heads: int, n_kv_heads: int,
                   head_dim: int, kv0: torch.Tensor = None, q_block: int = 64, out=None) -> torch.Tensor:
         """Shared-prefix attention over packed segments (see runtime.batch).
@@ -135,7 +158,7 @@ class TorchOps:
 
 def fill_params(slot_name: str, std: float):
     """(mean, std) of the synthetic distribution of a packed slot."""
-    if slot_name in ("ln1", "ln2", "norm"):
+    if slot_name in ("ln1", "ln2", "norm", "qn", "kn"):
         return 1.0, 0.1
     if slot_name == "embed":
         return 0.0, 1.0

@@ -70,6 +70,17 @@ class Comm:
         return Comm(self.rank, self.world, self.device, self.backend,
                     group=dist.new_group(ranks=list(range(self.world))))
 
+    def warmup(self) -> None:
+        """One tiny collective on this communicator (RCCL allocates its buffers at the first one),
+        so memory measured afterwards includes them."""
+        if not self.active:
+            return
+        dev = self.device if self.backend == "nccl" else torch.device("cpu")
+        t = torch.zeros(1, device=dev)
+        dist.all_reduce(t, group=self.group)
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
     # -------------------------------------------------------------- p2p
     def setup_p2p_edges(self, edges) -> None:
         """Create one process group per DIRECTED hand-off edge (src, dst).
@@ -294,6 +305,9 @@ class LoopbackComm(Comm):
 
     def barrier(self):
         self.hub.exchange(self.rank, None)
+
+    def warmup(self) -> None:
+        pass
 
     def all_reduce_max(self, x: float) -> float:
         return max(self.hub.exchange(self.rank, x))

@@ -48,6 +48,9 @@ def synthetic_layer_state_dict(cfg: ModelConfig, layer_name: str, seed: int = 0,
                      f"{p}.self_attn.v_proj.bias": rnd(cfg.kv_size) * 10})
     if cfg.o_proj_bias:
         bias[f"{p}.self_attn.o_proj.bias"] = rnd(H) * 10
+    if cfg.qk_norm:
+        bias[f"{p}.self_attn.q_norm.weight"] = norm_w(cfg.head_dim)
+        bias[f"{p}.self_attn.k_norm.weight"] = norm_w(cfg.head_dim)
     return {
         **bias,
         f"{p}.self_attn.q_proj.weight": rnd(cfg.q_size, H),

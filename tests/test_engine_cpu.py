@@ -225,6 +225,15 @@ def _hf_family_case(tmp_path, family):
             rope_theta=cfg.rope_theta, max_position_embeddings=cfg.max_position_embeddings,
             tie_word_embeddings=False, use_sliding_window=False)
         model = transformers.Qwen2ForCausalLM(hf_cfg)
+    elif family == "qwen3":
+        cfg = preset("tiny-qwen3")
+        hf_cfg = transformers.Qwen3Config(
+            hidden_size=cfg.hidden_size, intermediate_size=cfg.intermediate_size,
+            num_attention_heads=cfg.num_attention_heads, num_key_value_heads=cfg.num_key_value_heads,
+            num_hidden_layers=cfg.num_hidden_layers, vocab_size=cfg.vocab_size, rms_norm_eps=cfg.rms_norm_eps,
+            rope_theta=cfg.rope_theta, max_position_embeddings=cfg.max_position_embeddings,
+            head_dim=cfg.head_dim, tie_word_embeddings=False, use_sliding_window=False, attention_bias=False)
+        model = transformers.Qwen3ForCausalLM(hf_cfg)
     elif family in LLAMA_VARIANTS:
         over = dict(LLAMA_VARIANTS[family])
         cfg = preset("tiny", **over)
@@ -254,13 +263,15 @@ def _hf_family_case(tmp_path, family):
     return path, cfg, sd, model
 
 
-@pytest.mark.parametrize("family", ["qwen2", "mistral"] + sorted(LLAMA_VARIANTS))
+@pytest.mark.parametrize("family", ["qwen2", "qwen3", "mistral"] + sorted(LLAMA_VARIANTS))
 def test_other_llama_families_match_hf(tmp_path, family):
-    """Qwen2 (q/k/v biases, rope_theta 1e6) and Mistral == HF transformers in causal mode,
-    and == the fp32 oracle in the reference's bidirectional-prefix mode."""
+    """Qwen2 (q/k/v biases, rope_theta 1e6), Qwen3 (per-head q/k RMSNorm, head_dim 128 on a
+    256-wide residual) and Mistral == HF transformers in causal mode, and == the fp32 oracle in
+    the reference's bidirectional-prefix mode."""
     from flexible_llm_sharding_amd.config import ModelConfig
     path, cfg, sd, model = _hf_family_case(tmp_path, family)
     assert ModelConfig.from_pretrained(path).attention_bias == (family == "qwen2")
+    assert ModelConfig.from_pretrained(path).qk_norm == (family == "qwen3")
     tok = load_tokenizer(path)
     prompts = synthetic_prompts(3, 20, 2, 5, cfg.vocab_size, seed=9, vary=True)
     out = ShardedRunner(cfg, FileLayerSource(cfg, path), "cpu", tok, prefix_attention="causal")(prompts)

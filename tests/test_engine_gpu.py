@@ -328,3 +328,22 @@ def test_piece_pool_prefetcher_matches_slots(mid_model, monkeypatch):
     assert r.stats["weight_h2d_bytes"] > 0
     r.close()
     torch.cuda.set_per_process_memory_fraction(1.0)      # --max_vram_gb bounded the allocator
+
+
+@pytest.mark.parametrize("lnps", [1, 2])
+def test_qwen3_family_on_gpu(tmp_path, lnps):
+    """Qwen3-structured model (per-head q/k RMSNorm before RoPE: headnorm_rope_kernel after the
+    projection GEMM, head_dim 128 on a 256-wide residual) vs the fp32 oracle, incl. the pruned last
+    layer (K/V for all rows, Q for the scored rows)."""
+    from flexible_llm_sharding_amd.config import preset
+    from flexible_llm_sharding_amd.utils.synthetic import write_synthetic_checkpoint
+    cfg = preset("tiny-qwen3")
+    path = str(tmp_path / "q3")
+    write_synthetic_checkpoint(cfg, path, seed=13, std=0.05)
+    tok = load_tokenizer(path)
+    prompts = synthetic_prompts(4, 70, 3, 12, cfg.vocab_size, seed=14, vary=True)
+    ref = reference_scores(cfg, load_full_state_dict(cfg, path), tok, prompts)
+    r = ShardedRunner(cfg, HostStore.from_model_path(cfg, path), "cuda:0", tok, layer_num_per_shard=lnps)
+    for o, rf in zip(r(prompts), ref):
+        assert np.abs(o.astype(np.float32) - rf).max() < 2e-3
+    r.close()

@@ -398,3 +398,29 @@ def test_gemm_bias_epilogues(ops, ref, mid):
         torch.cuda.synchronize()
     finally:
         ops.k.fls_gemm_set_mid(1)
+
+
+@pytest.mark.parametrize("nq,nk,hd", [(8, 2, 128), (4, 4, 64), (0, 2, 128), (6, 0, 128)])
+def test_qkv_norm_rope(ops, ref, nq, nk, hd):
+    """Qwen3 projection: GEMM + per-head q/k RMSNorm + RoPE (headnorm_rope_kernel) vs the fp32
+    torch backend; V columns untouched; q-only and k/v-only forms (the pruned last layer)."""
+    from flexible_llm_sharding_amd.config import preset
+    from flexible_llm_sharding_amd.models.llama import rope_tables
+    K, M = 512, 70
+    nv = nk
+    N = (nq + nk + nv) * hd
+    x = rnd(M, K, seed=31)
+    w = rnd(N, K, scale=0.05, seed=32)
+    qn = (1 + 0.1 * torch.randn(hd)).half().to(DEV)
+    kn = (1 + 0.1 * torch.randn(hd)).half().to(DEV)
+    pos = torch.randint(0, 4000, (M,), dtype=torch.int32)
+    cfg = preset("tiny-qwen3")
+    cos, sin = rope_tables(cfg, 4096, torch.float16)
+    y = ops.qkv_norm_rope(x, w, pos.to(DEV), cos.to(DEV), sin.to(DEV), nq, nk, hd, qn, kn, 1e-6)
+    r = ref.qkv_norm_rope(x.cpu(), w.cpu(), pos, cos, sin, nq, nk, hd, qn.cpu(), kn.cpu(), 1e-6)
+    torch.cuda.synchronize()
+    assert y.shape == r.shape
+    assert (y.cpu().float() - r.float()).abs().max().item() < 2e-2
+    if nv:
+        v0 = (nq + nk) * hd
+        assert rel_err(y[:, v0:], (x.float() @ w.float().t())[:, v0:]) < 2e-3
