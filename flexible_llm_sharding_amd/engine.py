@@ -121,8 +121,13 @@ class ShardedRunner:
                         pcomm.warmup()
                 free, total = torch.cuda.mem_get_info(self.dev)
                 self._outside = (total - free) - torch.cuda.memory_reserved(self.dev) + (64 << 20)
-            token_budget, mlp_chunk, attn_rows, qkv_chunk, est = plan_for_vram(
-                cfg, self._vram_cap, layer_num_per_shard, n_slots, token_budget, mlp_chunk, overhead=self._outside)
+            try:
+                # provisional (the call's token count is unknown yet); _plan_call is authoritative
+                token_budget, mlp_chunk, attn_rows, qkv_chunk, est = plan_for_vram(
+                    cfg, self._vram_cap, layer_num_per_shard, n_slots, token_budget, mlp_chunk,
+                    overhead=self._outside)
+            except ValueError:
+                token_budget, mlp_chunk, attn_rows, qkv_chunk, est = 1024, 1024, 0, 0, 0
             self.vram_plan = {"token_budget": token_budget, "mlp_chunk": mlp_chunk, "attn_rows": attn_rows,
                               "qkv_chunk": qkv_chunk, "estimated_peak_bytes": est}
         self.token_budget = token_budget
