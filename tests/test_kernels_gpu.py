@@ -414,7 +414,7 @@ def test_qkv_norm_rope(ops, ref, nq, nk, hd):
     qn = (1 + 0.1 * torch.randn(hd)).half().to(DEV)
     kn = (1 + 0.1 * torch.randn(hd)).half().to(DEV)
     pos = torch.randint(0, 4000, (M,), dtype=torch.int32)
-    cfg = preset("tiny-qwen3")
+    cfg = preset("tiny-qwen3", explicit_head_dim=hd)
     cos, sin = rope_tables(cfg, 4096, torch.float16)
     y = ops.qkv_norm_rope(x, w, pos.to(DEV), cos.to(DEV), sin.to(DEV), nq, nk, hd, qn, kn, 1e-6)
     r = ref.qkv_norm_rope(x.cpu(), w.cpu(), pos, cos, sin, nq, nk, hd, qn.cpu(), kn.cpu(), 1e-6)
