@@ -79,6 +79,7 @@ int fls_gemm_set_mid(int on);   // 64x128-tile kernel for small / medium M (defa
 // seg_lo (optional, [T] int32): first packed row of the suffix holding each row; range-1 key j is
 // visible to query row i iff seg_lo[i] <= j <= i, so an item may hold several suffixes of a prompt
 // (null: one suffix per item).  q_block: rows per work item (64 or 128).
+int fls_attention_set_hpb(int hpb);
 int fls_attention(const void* qkv, void* out, const int* work, int n_items, int n_q_heads,
                   int n_kv_heads, int head_dim, int ld_qkv, int ld_out, float scale, const void* kv0,
                   int ld_kv0, const int* seg_lo, int q_block, fls_stream_t s);

@@ -76,6 +76,7 @@ def _load_kernels():
           c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p)
     _bind(lib, "fls_gemm_set_mid", c_int, c_int)
     _bind(lib, "fls_gemm_set_order", c_int, c_int)
+    _bind(lib, "fls_attention_set_hpb", c_int, c_int)
     _bind(lib, "fls_attention", c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
           c_int, c_int, c_float, c_void_p, c_int, c_void_p, c_int, c_void_p)
     _bind(lib, "fls_rmsnorm", c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
