@@ -587,7 +587,10 @@ class PiecePoolPrefetcher(ShardPrefetcher):
                 e = torch.cuda.Event()
                 e.record(cur)
                 self._slot_free[s] = e
-                self._released.add(gid)
+        # every slot is free now (its free event orders the next load after the dropped piece)
+        self._slot_owner = [None] * len(self._slot_sizes)
+        self._issued.clear()
+        self._released.clear()
         self._acquired.clear()
         self._next = self.epoch * len(self.pieces)
         self._m_turn = 0
