@@ -85,7 +85,7 @@ __device__ __forceinline__ unsigned pack_h2(float a, float b) {
 }
 
 template <int HD, int HPB, int WPH>
-__global__ __launch_bounds__(64 * WPH * HPB, (WPH * HPB >= 16 ? 1 : 2)) void attn_fwd(const half_t* __restrict__ qkv, half_t* __restrict__ out,
+__global__ __launch_bounds__(64 * WPH * HPB, 2) void attn_fwd(const half_t* __restrict__ qkv, half_t* __restrict__ out,
                                                     const int* __restrict__ work, const int* __restrict__ seg_lo,
                                                     int nh, int nkv, int ld_qkv, int ld_out, float scale_log2,
                                                     const half_t* __restrict__ kv0, int ld_kv0) {
@@ -317,12 +317,7 @@ int launch(int hpb, dim3 grid, hipStream_t st, const half_t* qkv, half_t* out, c
 #define FLS_ATTN_LAUNCH(HPB_)                                                                                 \
   hipLaunchKernelGGL((attn_fwd<HD, HPB_, WPH>), grid, dim3(64 * WPH * HPB_), 0, st, qkv, out, work, seg_lo, nh, \
                      nkv, ld_qkv, ld_out, scale_log2, kv0, ld_kv0)
-  if constexpr (WPH == 2 && HD == 128) {
-    if (hpb == 8) FLS_ATTN_LAUNCH(8);
-    else if (hpb == 4) FLS_ATTN_LAUNCH(4);
-    else if (hpb == 2) FLS_ATTN_LAUNCH(2);
-    else FLS_ATTN_LAUNCH(1);
-  } else if constexpr (WPH == 2) {
+  if constexpr (WPH == 2) {
     if (hpb == 4) FLS_ATTN_LAUNCH(4);
     else if (hpb == 2) FLS_ATTN_LAUNCH(2);
     else FLS_ATTN_LAUNCH(1);
@@ -340,7 +335,7 @@ int g_hpb = 0;   // heads per block override (0: by group size; tests / A-B)
 
 }  // namespace
 
-// heads of one KV group per block: 0 = by group size (default), else 1 / 2 / 4 / 8 (64-row items)
+// heads of one KV group per block: 0 = by group size (default), else 1 / 2 / 4 (A/B)
 extern "C" int fls_attention_set_hpb(int hpb) {
   const int old = g_hpb;
   g_hpb = hpb;
@@ -362,7 +357,8 @@ extern "C" int fls_attention(const void* qkv, void* out, const int* work, int n_
   int hpb = 1;
   if (q_block == 64) hpb = group % 4 == 0 ? 4 : (group % 2 == 0 ? 2 : 1);
   else hpb = group % 2 == 0 ? 2 : 1;
-  if (g_hpb > 0 && group % g_hpb == 0 && (q_block == 64 ? (g_hpb <= 4 || head_dim == 128) : g_hpb <= 2)) hpb = g_hpb;
+  // 8 heads per block (1024 threads, one block per CU) measured 4x slower (profiles/r3_attn): not built
+  if (g_hpb > 0 && group % g_hpb == 0 && g_hpb <= (q_block == 64 ? 4 : 2)) hpb = g_hpb;
   const dim3 grid(n_items, n_q_heads / hpb);
   auto q = (const half_t*)qkv;
   auto o = (half_t*)out;
