@@ -41,6 +41,8 @@ import subprocess
 import sys
 import time
 
+import numpy as np
+
 METRIC = "tokens/sec + peak GPU mem, Llama-2-70B layer_num_per_shard=1 at 1/2/4/8 MI355X"
 
 
@@ -89,6 +91,9 @@ def parse(argv=None):
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--cpu", action="store_true", help="CPU/gloo rehearsal of the same code path (tests only)")
+    ap.add_argument("--loopback-ranks", type=int, default=0,
+                    help="model-parallel rehearsal on ONE device: R pipeline ranks as threads over the loopback "
+                         "comm (device copies instead of RCCL), the real StageInbox / program; not a scaling number")
     return ap.parse_args(argv)
 
 
@@ -117,6 +122,92 @@ def spawn_ranks(a, argv) -> int:
     return rc
 
 
+def loopback_main(a) -> int:
+    """--loopback-ranks R: the model-parallel pipeline (round-robin or contiguous stages, the
+    per-rank hand-off program, StageInbox ring and parking) with R ranks as threads of this process
+    on one device, exchanging activations by device copies (parallel/comm.py LoopbackComm).  Every
+    rank computes its own layers on the same GPU, so the rate is the single-GPU rate minus the
+    pipeline's overheads: it measures those overheads at full scale, not scaling."""
+    import threading
+
+    import torch
+
+    from flexible_llm_sharding_amd.config import preset
+    from flexible_llm_sharding_amd.engine import ShardedRunner
+    from flexible_llm_sharding_amd.parallel.comm import LoopbackComm, LoopbackHub
+    from flexible_llm_sharding_amd.parallel.pipeline import simulate_single_queue
+    from flexible_llm_sharding_amd.runtime.weights import HostStore
+    from flexible_llm_sharding_amd.utils.synthetic import synthetic_prompts
+    from flexible_llm_sharding_amd.utils.tokenizer import load_tokenizer, write_synthetic_tokenizer
+    R = a.loopback_ranks
+    dev = torch.device("cpu") if a.cpu else torch.device("cuda", 0)
+    if not a.cpu:
+        torch.cuda.set_device(dev)
+    kw = {} if a.num_layers is None else {"num_hidden_layers": a.num_layers}
+    cfg = preset(a.model, **kw)
+    t0 = time.perf_counter()
+    store = HostStore.synthetic(cfg, dev, seed=a.seed, pinned=not a.cpu)
+    log(0, f"[bench] loopback x{R}: host store {store.total_bytes / 1e9:.1f} GB in {time.perf_counter() - t0:.1f}s")
+    if not a.cpu:
+        torch.cuda.empty_cache()
+    tok_dir = f"/tmp/fls_bench_tok_{os.getpid()}"
+    write_synthetic_tokenizer(tok_dir, cfg.vocab_size)
+    tok = load_tokenizer(tok_dir)
+    prompts = synthetic_prompts(a.prompts_per_gpu, a.prefix_len, a.n_suffix, a.suffix_len, cfg.vocab_size,
+                                seed=a.seed)
+    hub = LoopbackHub(R, timeout_s=1800)
+    res, err = {}, []
+
+    def rank(r):
+        try:
+            if not a.cpu:
+                torch.cuda.set_device(dev)
+            comm = LoopbackComm(hub, r, dev)
+            run = ShardedRunner(cfg, store, dev, tok, layer_num_per_shard=a.lnps, storage_location=a.storage,
+                                disk_folder=f"/tmp/fls_bench_spill_lb{r}", prefix_attention=a.prefix_attention,
+                                token_budget=a.token_budget, mlp_chunk=a.mlp_chunk, comm=comm,
+                                pipeline_stages=a.stages, max_activation_in_cpu=4)
+            for _ in range(a.warmup):
+                run(prompts)
+            comm.barrier()
+            if not a.cpu:
+                torch.cuda.synchronize(dev)
+            ts = time.perf_counter()
+            for _ in range(a.steps):
+                out = run(prompts)
+            if not a.cpu:
+                torch.cuda.synchronize(dev)
+            res[r] = (time.perf_counter() - ts, dict(run.stats), out)
+            comm.barrier()
+            run.close()
+        except BaseException as e:  # noqa: BLE001
+            err.append(e)
+            raise
+
+    ts = [threading.Thread(target=rank, args=(r,)) for r in range(R)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    if err:
+        raise err[0]
+    elapsed = max(v[0] for v in res.values())
+    tokens = res[0][1]["tokens"]
+    owner = [v[2] for v in res.values() if v[2] and v[2][0] is not None]
+    finite = bool(owner) and all(np.isfinite(o.astype(np.float32)).all() for o in owner[0])
+    rx = {r: {k: v for k, v in res[r][1].items() if k.startswith("rx_")} for r in range(R)}
+    ok, _ = simulate_single_queue({r: hub.log[r] for r in range(R)})
+    out = {"metric": "model-parallel rehearsal on one device (loopback ranks; not a scaling number)",
+           "value": round(tokens * a.steps / elapsed, 2), "unit": "tokens/s", "n_gpus": 1, "loopback_ranks": R,
+           "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1000.0, 2),
+           "higher_is_better": True, "scores_finite": finite, "single_queue_replay_ok": ok,
+           "micro_batches": res[0][1]["micro_batches"], "rx_stats": rx,
+           "config": {"model": a.model, "stages": a.stages, "storage_location": a.storage, "lnps": a.lnps,
+                      "tokens_per_step": tokens}}
+    print(json.dumps(out), flush=True)
+    return 0
+
+
 def ensure_checkpoint(cfg, d: str, dtype: str, unique: int, rank: int, comm, progress) -> None:
     """Write the synthetic per-layer checkpoint once (rank 0; a marker file makes it reusable)."""
     import torch
@@ -135,6 +226,8 @@ def ensure_checkpoint(cfg, d: str, dtype: str, unique: int, rank: int, comm, pro
 def main(argv=None):
     argv = list(sys.argv[1:] if argv is None else argv)
     a = parse(argv)
+    if a.loopback_ranks:
+        return loopback_main(a)
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return spawn_ranks(a, argv)
     if a.max_vram_gb is None:
