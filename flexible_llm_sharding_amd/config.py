@@ -31,8 +31,10 @@ class ModelConfig:
     attention_bias: bool = False        # q/k/v projection biases (Qwen2; Llama attention_bias)
     o_proj_bias: bool = False           # o_proj bias (Llama attention_bias=True)
     qk_norm: bool = False               # Qwen3: RMSNorm over head_dim on every q / k head, before RoPE
-    sliding_window: Optional[int] = None  # Mistral; must cover the token cap (checked by the runner)
-    # RoPE frequency scaling (HF ``rope_scaling`` / v5 ``rope_parameters``): linear, llama3, yarn
+    # Mistral / Phi-3: every call's sequences must fit the window (checked per call by the runner)
+    sliding_window: Optional[int] = None
+    # RoPE frequency scaling (HF ``rope_scaling`` / v5 ``rope_parameters``): linear, llama3, yarn,
+    # longrope (Phi-3)
     rope_scaling: Optional[dict] = None
     explicit_head_dim: Optional[int] = None   # HF ``head_dim`` when != hidden / heads (Mistral-Nemo)
     bos_token_id: int = 1
@@ -45,6 +47,12 @@ class ModelConfig:
     @property
     def head_dim(self) -> int:
         return self.explicit_head_dim or self.hidden_size // self.num_attention_heads
+
+    @property
+    def fused_projections(self) -> bool:
+        """Phi-3 checkpoints store ``qkv_proj`` ([q; k; v] rows) and ``gate_up_proj`` ([gate; up]
+        rows) as single tensors: the same row order as the packed ``wqkv`` / ``wgu`` slots."""
+        return self.model_type == "phi3"
 
     @property
     def q_size(self) -> int:
@@ -95,6 +103,16 @@ class ModelConfig:
                                           " (dynamic NTK depends on each call's length: not supported)")
             if float(rs.get("factor") or 1.0) <= 0:
                 raise ValueError(f"rope_scaling factor must be > 0: {rs}")
+            if kind == "longrope":
+                for key in ("short_factor", "long_factor"):
+                    if len(rs.get(key) or ()) != self.head_dim // 2:
+                        raise ValueError(f"longrope {key} must hold head_dim/2 = {self.head_dim // 2} values")
+                orig = int(rs.get("original_max_position_embeddings") or self.max_position_embeddings)
+                if orig < MAX_TOKEN_LEN:
+                    # HF switches to long_factor once a sequence exceeds the original context;
+                    # static tables are exact only while no sequence can
+                    raise NotImplementedError(f"longrope with original_max_position_embeddings={orig} < the "
+                                              f"{MAX_TOKEN_LEN}-token cap (length-dependent tables)")
 
     # ---------------------------------------------------------------------- io
     @classmethod
@@ -114,6 +132,17 @@ class ModelConfig:
         rs = kw.get("rope_scaling")
         if rs and rs.get("rope_type", rs.get("type")) == "default":
             kw.pop("rope_scaling")
+        rs = kw.get("rope_scaling")
+        if rs and rs.get("rope_type", rs.get("type")) in ("su", "longrope"):
+            # Phi-3: "su" is the old name; the pretraining context sits at the config's top level
+            rs = dict(rs, rope_type="longrope")
+            rs.pop("type", None)
+            if "original_max_position_embeddings" not in rs and d.get("original_max_position_embeddings"):
+                rs["original_max_position_embeddings"] = d["original_max_position_embeddings"]
+            kw["rope_scaling"] = rs
+        for src in (d, rp if isinstance(rp, dict) else {}, rs or {}):
+            if float(src.get("partial_rotary_factor", 1.0) or 1.0) != 1.0:
+                raise NotImplementedError("partial_rotary_factor < 1 (RoPE on part of each head) is not supported")
         mt = d.get("model_type", "llama")
         if mt not in SUPPORTED_MODEL_TYPES:
             raise NotImplementedError(f"model_type={mt!r}: supported are {sorted(SUPPORTED_MODEL_TYPES)}")
@@ -134,7 +163,8 @@ class ModelConfig:
             # HF Qwen3Attention: q_norm / k_norm (RMSNorm over head_dim) on every head before RoPE;
             # q/k/v/o biases only with attention_bias (off in every released Qwen3 config)
             kw["qk_norm"] = True
-        if not d.get("use_sliding_window", mt == "mistral"):
+        # HF Phi3Model applies its sliding_window whenever it is set; Qwen2/3 only with use_sliding_window
+        if not d.get("use_sliding_window", mt in ("mistral", "phi3")):
             kw.pop("sliding_window", None)
         if isinstance(kw.get("eos_token_id"), list):
             kw["eos_token_id"] = kw["eos_token_id"][0]
@@ -163,9 +193,9 @@ class ModelConfig:
 # Llama-structured causal LMs (model.embed_tokens / model.layers.N / model.norm / lm_head with
 # q/k/v/o + gate/up/down + two RMSNorms per layer) -- what the reference's AutoModelForCausalLM
 # path (utils.py:101-115) runs in practice.
-SUPPORTED_MODEL_TYPES = {"llama", "mistral", "qwen2", "qwen3"}
+SUPPORTED_MODEL_TYPES = {"llama", "mistral", "qwen2", "qwen3", "phi3"}
 # static RoPE scalings: they only change the cos/sin tables (models/llama.py rope_inv_freq)
-ROPE_SCALING_TYPES = {"linear", "llama3", "yarn"}
+ROPE_SCALING_TYPES = {"linear", "llama3", "yarn", "longrope"}
 
 # Standard HF configs (computed sizes in SURVEY.md §2.3).
 PRESETS = {
@@ -199,6 +229,21 @@ PRESETS = {
                        num_key_value_heads=2, num_hidden_layers=2, vocab_size=512, rope_theta=1e6,
                        rms_norm_eps=1e-6, qk_norm=True, explicit_head_dim=128, model_type="qwen3",
                        architectures=["Qwen3ForCausalLM"]),
+    # Phi-3 family: fused qkv_proj / gate_up_proj tensors; Phi-3-medium-4k (sliding window 2047)
+    # and Phi-4 (14B, 100k vocab) have head_dim 128
+    "phi3-medium": dict(hidden_size=5120, intermediate_size=17920, num_attention_heads=40,
+                        num_key_value_heads=10, num_hidden_layers=40, vocab_size=32064, sliding_window=2047,
+                        eos_token_id=32000, model_type="phi3", architectures=["Phi3ForCausalLM"]),
+    "phi4": dict(hidden_size=5120, intermediate_size=17920, num_attention_heads=40, num_key_value_heads=10,
+                 num_hidden_layers=40, vocab_size=100352, rope_theta=250000.0, max_position_embeddings=16384,
+                 bos_token_id=100257, eos_token_id=100265, model_type="phi3", architectures=["Phi3ForCausalLM"]),
+    # tiny Phi-3-128k-style config: longrope short/long factors, attention factor from 131072 / 4096
+    "tiny-phi3": dict(hidden_size=256, intermediate_size=512, num_attention_heads=4, num_key_value_heads=2,
+                      num_hidden_layers=2, vocab_size=512, max_position_embeddings=131072,
+                      rope_scaling={"rope_type": "longrope", "original_max_position_embeddings": 4096,
+                                    "short_factor": [1.0 + 0.05 * i for i in range(32)],
+                                    "long_factor": [2.0 + 0.5 * i for i in range(32)]},
+                      model_type="phi3", architectures=["Phi3ForCausalLM"]),
     # Llama-3.1 geometry (GQA 8:1, 128k vocab, llama3 RoPE scaling)
     "llama3.1-8b": dict(hidden_size=4096, intermediate_size=14336, num_attention_heads=32,
                         num_key_value_heads=8, num_hidden_layers=32, vocab_size=128256, rope_theta=500000.0,

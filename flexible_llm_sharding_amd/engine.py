@@ -306,6 +306,15 @@ class ShardedRunner:
     def run_tokenized(self, tps: Sequence[TokenizedPrompt]) -> List[Optional[np.ndarray]]:
         t_start = time.perf_counter()
         n = len(tps)
+        sw = self.cfg.sliding_window
+        if sw:
+            # windowed attention equals full attention while every sequence fits the window
+            # (HF: query i sees keys i - sw + 1 .. i); longer ones would need the band mask
+            longest = max((len(tp.prefix) + max((len(s) for s in tp.suffixes), default=0) for tp in tps),
+                          default=0)
+            if longest > sw:
+                raise ValueError(f"a prompt spans {longest} tokens > sliding_window={sw}: "
+                                 "sliding-window attention is not implemented")
         entry, cached = self._prefix_entry(tps)
         if self._vram_cap:
             self._plan_call(tps, cached)

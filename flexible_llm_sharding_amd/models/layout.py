@@ -170,14 +170,22 @@ def placements(cfg: ModelConfig, layer_name: str, elem_size: int = 2) -> List[Pl
     out = [
         Placement(f"{p}.input_layernorm.weight", o["ln1"], H, (H,), es),
         Placement(f"{p}.post_attention_layernorm.weight", o["ln2"], H, (H,), es),
-        Placement(f"{p}.self_attn.q_proj.weight", o["wqkv"], qs * H, (qs, H), es),
-        Placement(f"{p}.self_attn.k_proj.weight", o["wqkv"] + es * qs * H, ks * H, (ks, H), es),
-        Placement(f"{p}.self_attn.v_proj.weight", o["wqkv"] + es * (qs + ks) * H, ks * H, (ks, H), es),
         Placement(f"{p}.self_attn.o_proj.weight", o["wo"], H * qs, (H, qs), es),
-        Placement(f"{p}.mlp.gate_proj.weight", o["wgu"], I * H, (I, H), es),
-        Placement(f"{p}.mlp.up_proj.weight", o["wgu"] + es * I * H, I * H, (I, H), es),
         Placement(f"{p}.mlp.down_proj.weight", o["wdown"], H * I, (H, I), es),
     ]
+    if cfg.fused_projections:
+        # Phi-3: one tensor each, already in slot row order
+        qkv = qs + 2 * ks
+        out += [Placement(f"{p}.self_attn.qkv_proj.weight", o["wqkv"], qkv * H, (qkv, H), es),
+                Placement(f"{p}.mlp.gate_up_proj.weight", o["wgu"], 2 * I * H, (2 * I, H), es)]
+    else:
+        out += [
+            Placement(f"{p}.self_attn.q_proj.weight", o["wqkv"], qs * H, (qs, H), es),
+            Placement(f"{p}.self_attn.k_proj.weight", o["wqkv"] + es * qs * H, ks * H, (ks, H), es),
+            Placement(f"{p}.self_attn.v_proj.weight", o["wqkv"] + es * (qs + ks) * H, ks * H, (ks, H), es),
+            Placement(f"{p}.mlp.gate_proj.weight", o["wgu"], I * H, (I, H), es),
+            Placement(f"{p}.mlp.up_proj.weight", o["wgu"] + es * I * H, I * H, (I, H), es),
+        ]
     if cfg.attention_bias:
         out += [Placement(f"{p}.self_attn.q_proj.bias", o["bqkv"], qs, (qs,), es),
                 Placement(f"{p}.self_attn.k_proj.bias", o["bqkv"] + es * qs, ks, (ks,), es),

@@ -77,6 +77,18 @@ def rope_inv_freq(cfg: ModelConfig):
         ramp = ((torch.arange(hd // 2, dtype=torch.float32) - lo) / (hi - lo)).clamp(0, 1)
         extrap = 1 - ramp
         return (inv / factor) * (1 - extrap) + inv * extrap, float(att)
+    if kind == "longrope":
+        # Phi-3 LongRoPE: per-frequency divisors; short_factor while the sequence stays within
+        # the pretraining context (always, under the token cap: ModelConfig.validate), and the
+        # attention factor from max_position_embeddings / original when ``factor`` is unset
+        if rs.get("factor") is None:
+            factor = cfg.max_position_embeddings / orig
+        att = rs.get("attention_factor")
+        if att is None:
+            att = 1.0 if factor <= 1.0 else math.sqrt(1 + math.log(factor) / math.log(orig))
+        ext = torch.tensor(rs["short_factor"], dtype=torch.float32)
+        shape = torch.arange(0, hd, 2, dtype=torch.int64).float() / hd
+        return 1.0 / (ext * base ** shape), float(att)
     raise NotImplementedError(f"rope_scaling {rs}")
 
 

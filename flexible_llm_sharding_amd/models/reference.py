@@ -71,6 +71,8 @@ def reference_scores(cfg: ModelConfig, sd: Dict[str, torch.Tensor], tok, prompts
                      cos=None, sin=None) -> List[np.ndarray]:
     """list of [n_s, 1, V] float32 probabilities, one per prompt."""
     from .llama import rope_tables
+    from ..utils.synthetic import split_projections
+    sd = split_projections(cfg, sd)          # Phi-3 fused qkv_proj / gate_up_proj -> split names
     if cos is None:
         cos, sin = rope_tables(cfg, max_len)
     outs = []

@@ -51,7 +51,7 @@ def synthetic_layer_state_dict(cfg: ModelConfig, layer_name: str, seed: int = 0,
     if cfg.qk_norm:
         bias[f"{p}.self_attn.q_norm.weight"] = norm_w(cfg.head_dim)
         bias[f"{p}.self_attn.k_norm.weight"] = norm_w(cfg.head_dim)
-    return {
+    sd = {
         **bias,
         f"{p}.self_attn.q_proj.weight": rnd(cfg.q_size, H),
         f"{p}.self_attn.k_proj.weight": rnd(cfg.kv_size, H),
@@ -63,6 +63,34 @@ def synthetic_layer_state_dict(cfg: ModelConfig, layer_name: str, seed: int = 0,
         f"{p}.input_layernorm.weight": norm_w(H),
         f"{p}.post_attention_layernorm.weight": norm_w(H),
     }
+    return fuse_projections(cfg, p, sd) if cfg.fused_projections else sd
+
+
+def fuse_projections(cfg: ModelConfig, p: str, sd: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+    """Split q/k/v and gate/up tensors of layer ``p`` -> Phi-3's ``qkv_proj`` / ``gate_up_proj``."""
+    sd = dict(sd)
+    sd[f"{p}.self_attn.qkv_proj.weight"] = torch.cat(
+        [sd.pop(f"{p}.self_attn.{n}_proj.weight") for n in "qkv"], 0)
+    sd[f"{p}.mlp.gate_up_proj.weight"] = torch.cat(
+        [sd.pop(f"{p}.mlp.{n}_proj.weight") for n in ("gate", "up")], 0)
+    return sd
+
+
+def split_projections(cfg: ModelConfig, sd: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+    """Inverse of :func:`fuse_projections` over a whole state dict (HF Phi-3 chunk order)."""
+    out = {}
+    for k, v in sd.items():
+        if k.endswith(".self_attn.qkv_proj.weight"):
+            p = k[:-len("qkv_proj.weight")]
+            q, kk, vv = torch.split(v, [cfg.q_size, cfg.kv_size, cfg.kv_size], 0)
+            out.update({p + "q_proj.weight": q, p + "k_proj.weight": kk, p + "v_proj.weight": vv})
+        elif k.endswith(".mlp.gate_up_proj.weight"):
+            p = k[:-len("gate_up_proj.weight")]
+            g, u = v.chunk(2, 0)
+            out.update({p + "gate_proj.weight": g, p + "up_proj.weight": u})
+        else:
+            out[k] = v
+    return out
 
 
 def write_synthetic_checkpoint(cfg: ModelConfig, out_dir: str, seed: int = 0,

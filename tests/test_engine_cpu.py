@@ -234,6 +234,16 @@ def _hf_family_case(tmp_path, family):
             rope_theta=cfg.rope_theta, max_position_embeddings=cfg.max_position_embeddings,
             head_dim=cfg.head_dim, tie_word_embeddings=False, use_sliding_window=False, attention_bias=False)
         model = transformers.Qwen3ForCausalLM(hf_cfg)
+    elif family == "phi3":
+        cfg = preset("tiny-phi3", sliding_window=64)
+        rs = dict(cfg.rope_scaling, rope_theta=cfg.rope_theta)
+        hf_cfg = transformers.Phi3Config(
+            hidden_size=cfg.hidden_size, intermediate_size=cfg.intermediate_size,
+            num_attention_heads=cfg.num_attention_heads, num_key_value_heads=cfg.num_key_value_heads,
+            num_hidden_layers=cfg.num_hidden_layers, vocab_size=cfg.vocab_size, rms_norm_eps=cfg.rms_norm_eps,
+            max_position_embeddings=cfg.max_position_embeddings, original_max_position_embeddings=4096,
+            rope_parameters=rs, sliding_window=64, tie_word_embeddings=False, pad_token_id=0)
+        model = transformers.Phi3ForCausalLM(hf_cfg)
     elif family in LLAMA_VARIANTS:
         over = dict(LLAMA_VARIANTS[family])
         cfg = preset("tiny", **over)
@@ -263,11 +273,12 @@ def _hf_family_case(tmp_path, family):
     return path, cfg, sd, model
 
 
-@pytest.mark.parametrize("family", ["qwen2", "qwen3", "mistral"] + sorted(LLAMA_VARIANTS))
+@pytest.mark.parametrize("family", ["qwen2", "qwen3", "phi3", "mistral"] + sorted(LLAMA_VARIANTS))
 def test_other_llama_families_match_hf(tmp_path, family):
     """Qwen2 (q/k/v biases, rope_theta 1e6), Qwen3 (per-head q/k RMSNorm, head_dim 128 on a
-    256-wide residual) and Mistral == HF transformers in causal mode, and == the fp32 oracle in
-    the reference's bidirectional-prefix mode."""
+    256-wide residual), Phi-3 (fused qkv_proj / gate_up_proj, LongRoPE with its attention factor,
+    sliding window covering the prompts) and Mistral == HF transformers in causal mode, and ==
+    the fp32 oracle in the reference's bidirectional-prefix mode."""
     from flexible_llm_sharding_amd.config import ModelConfig
     path, cfg, sd, model = _hf_family_case(tmp_path, family)
     assert ModelConfig.from_pretrained(path).attention_bias == (family == "qwen2")
@@ -290,9 +301,28 @@ def test_unsupported_configs_rejected():
     from flexible_llm_sharding_amd.config import ModelConfig
     for bad in ({"model_type": "gemma"}, {"mlp_bias": True}, {"hidden_act": "gelu"},
                 {"rope_scaling": {"rope_type": "dynamic", "factor": 2.0}},
-                {"rope_parameters": {"rope_type": "longrope", "rope_theta": 1e4}}):
+                {"model_type": "phi3", "partial_rotary_factor": 0.75},
+                {"rope_scaling": {"type": "su", "short_factor": [1.0] * 64, "long_factor": [1.0] * 64},
+                 "original_max_position_embeddings": 2048}):
         with pytest.raises(NotImplementedError):
             ModelConfig.from_dict(bad)
+    with pytest.raises(ValueError):           # longrope factors must cover head_dim / 2
+        ModelConfig.from_dict({"rope_parameters": {"rope_type": "longrope", "rope_theta": 1e4}})
+
+
+def test_sliding_window_must_cover_prompts(tmp_path):
+    """Windowed attention is full attention while every sequence fits the window; longer prompts
+    are rejected instead of silently attending past the window."""
+    from flexible_llm_sharding_amd.config import preset
+    cfg = preset("tiny", sliding_window=24)
+    store = HostStore.synthetic(cfg, "cpu", seed=1)
+    from flexible_llm_sharding_amd.utils.tokenizer import write_synthetic_tokenizer
+    write_synthetic_tokenizer(str(tmp_path), cfg.vocab_size)
+    r = ShardedRunner(cfg, store, "cpu", load_tokenizer(str(tmp_path)))
+    ok = synthetic_prompts(2, 16, 2, 8, cfg.vocab_size, seed=2)
+    assert all(np.isfinite(o).all() for o in r(ok))
+    with pytest.raises(ValueError, match="sliding_window"):
+        r(synthetic_prompts(2, 20, 2, 8, cfg.vocab_size, seed=2))
 
 
 def test_config_rope_and_head_dim_forms(tmp_path):

@@ -331,14 +331,16 @@ def test_piece_pool_prefetcher_matches_slots(mid_model, monkeypatch):
 
 
 @pytest.mark.parametrize("lnps", [1, 2])
-def test_qwen3_family_on_gpu(tmp_path, lnps):
+@pytest.mark.parametrize("family", ["tiny-qwen3", "tiny-phi3"])
+def test_qwen3_phi3_families_on_gpu(tmp_path, lnps, family):
     """Qwen3-structured model (per-head q/k RMSNorm before RoPE: headnorm_rope_kernel after the
-    projection GEMM, head_dim 128 on a 256-wide residual) vs the fp32 oracle, incl. the pruned last
-    layer (K/V for all rows, Q for the scored rows)."""
+    projection GEMM, head_dim 128 on a 256-wide residual) and Phi-3 (fused checkpoint tensors,
+    LongRoPE tables with attention factor 1.19 through the fused RoPE epilogue) vs the fp32
+    oracle, incl. the pruned last layer (K/V for all rows, Q for the scored rows)."""
     from flexible_llm_sharding_amd.config import preset
     from flexible_llm_sharding_amd.utils.synthetic import write_synthetic_checkpoint
-    cfg = preset("tiny-qwen3")
-    path = str(tmp_path / "q3")
+    cfg = preset(family)
+    path = str(tmp_path / family)
     write_synthetic_checkpoint(cfg, path, seed=13, std=0.05)
     tok = load_tokenizer(path)
     prompts = synthetic_prompts(4, 70, 3, 12, cfg.vocab_size, seed=14, vary=True)
