@@ -48,10 +48,14 @@ template <int HD>
 struct Lds {
   static constexpr int ROW = HD * 2;            // bytes per row
   static constexpr int NCH = HD / 8;            // 16-byte chunks per row
-  // K: ds_read_b128 row reads -> chunk ^ (row & (NCH-1))
-  __device__ static int k_off(int row, int ch) { return row * ROW + ((ch ^ (row & (NCH - 1))) << 4); }
-  // V: ds_read_b64_tr_b16 -> chunk ^ ((row & (NCH/2-1)) << 1)
-  __device__ static int v_off(int row, int ch) { return row * ROW + ((ch ^ ((row & (NCH / 2 - 1)) << 1)) << 4); }
+  // XOR masks stay inside the row: all chunk bits for power-of-two rows (hd 64 / 128), the low two
+  // bits for hd 96 (12 chunks: an XOR within each aligned group of 4 chunks)
+  static constexpr int KM = (NCH & (NCH - 1)) == 0 ? NCH - 1 : 3;
+  static constexpr int VM = (NCH & (NCH - 1)) == 0 ? NCH / 2 - 1 : 1;
+  // K: ds_read_b128 row reads -> chunk ^ (row & KM)
+  __device__ static int k_off(int row, int ch) { return row * ROW + ((ch ^ (row & KM)) << 4); }
+  // V: ds_read_b64_tr_b16 -> chunk ^ ((row & VM) << 1)
+  __device__ static int v_off(int row, int ch) { return row * ROW + ((ch ^ ((row & VM) << 1)) << 4); }
 };
 
 // max without the canonicalising v_max(x, x) the compiler puts in front of fmaxf on MFMA results
@@ -317,7 +321,9 @@ int launch(int hpb, dim3 grid, hipStream_t st, const half_t* qkv, half_t* out, c
 #define FLS_ATTN_LAUNCH(HPB_)                                                                                 \
   hipLaunchKernelGGL((attn_fwd<HD, HPB_, WPH>), grid, dim3(64 * WPH * HPB_), 0, st, qkv, out, work, seg_lo, nh, \
                      nkv, ld_qkv, ld_out, scale_log2, kv0, ld_kv0)
-  if constexpr (WPH == 2) {
+  if constexpr (HD == 96) {
+    FLS_ATTN_LAUNCH(1);                     // 12 chunks per row: one head per block divides the tile
+  } else if constexpr (WPH == 2) {
     if (hpb == 4) FLS_ATTN_LAUNCH(4);
     else if (hpb == 2) FLS_ATTN_LAUNCH(2);
     else FLS_ATTN_LAUNCH(1);
@@ -347,7 +353,7 @@ extern "C" int fls_attention(const void* qkv, void* out, const int* work, int n_
                              int ld_kv0, const int* seg_lo, int q_block, fls_stream_t s) {
   if (n_items <= 0) return 0;
   if (n_q_heads % n_kv_heads) return -2;
-  if (head_dim != 64 && head_dim != 128) return -3;
+  if (head_dim != 64 && head_dim != 96 && head_dim != 128) return -3;
   if (q_block != 64 && q_block != 128) return -5;
   const float scale_log2 = scale * 1.4426950408889634f;
   auto st = (hipStream_t)s;
@@ -359,10 +365,16 @@ extern "C" int fls_attention(const void* qkv, void* out, const int* work, int n_
   else hpb = group % 2 == 0 ? 2 : 1;
   // 8 heads per block (1024 threads, one block per CU) measured 4x slower (profiles/r3_attn): not built
   if (g_hpb > 0 && group % g_hpb == 0 && g_hpb <= (q_block == 64 ? 4 : 2)) hpb = g_hpb;
+  if (head_dim == 96) hpb = 1;              // Phi-3-mini geometry (multi-head attention anyway)
   const dim3 grid(n_items, n_q_heads / hpb);
   auto q = (const half_t*)qkv;
   auto o = (half_t*)out;
   auto k0 = (const half_t*)kv0;
+  if (head_dim == 96)
+    return q_block == 64 ? launch<96, 2>(hpb, grid, st, q, o, work, seg_lo, n_q_heads, n_kv_heads, ld_qkv, ld_out,
+                                         scale_log2, k0, ld_kv0)
+                         : launch<96, 4>(hpb, grid, st, q, o, work, seg_lo, n_q_heads, n_kv_heads, ld_qkv, ld_out,
+                                         scale_log2, k0, ld_kv0);
   if (q_block == 64)
     return head_dim == 128 ? launch<128, 2>(hpb, grid, st, q, o, work, seg_lo, n_q_heads, n_kv_heads, ld_qkv, ld_out,
                                             scale_log2, k0, ld_kv0)

@@ -271,7 +271,8 @@ __global__ __launch_bounds__(256) void gemv_skinny_kernel(const half_t* __restri
 //   n_q <= h < n_q+n_k:  same with kn
 // (HF Qwen3RMSNorm cast points, then rotate-half RoPE in fp32 on the normalised fp16 values).
 // One wave per (row, head): lane p holds the rotate-half pair (p, p + hd/2), so the norm is one
-// wave reduction and the rotation lane-local.  hd in {64, 128}.
+// wave reduction and the rotation lane-local.  hd in {64, 96, 128}.  qn == nullptr: RoPE only (the
+// unfused path for head sizes the GEMM's RoPE epilogue does not tile: Phi-3-mini's 96).
 __global__ __launch_bounds__(256) void headnorm_rope_kernel(half_t* __restrict__ x, int ldx, int rows, int n_q,
                                                           int n_k, const half_t* __restrict__ qn,
                                                           const half_t* __restrict__ kn, const int* __restrict__ pos,
@@ -287,11 +288,14 @@ __global__ __launch_bounds__(256) void headnorm_rope_kernel(half_t* __restrict__
   const bool on = p < half;
   const float a = on ? (float)xh[p] : 0.f;
   const float b = on ? (float)xh[p + half] : 0.f;
-  const float ss = warp_sum(a * a + b * b);
-  const float rs = rsqrtf(ss / (float)hd + eps);
+  float na = a, nb = b;
+  if (qn != nullptr) {                              // kernel-uniform
+    const float ss = warp_sum(a * a + b * b);
+    const float rs = rsqrtf(ss / (float)hd + eps);
+    na = (float)(half_t)((float)w[p] * (float)(half_t)(a * rs));
+    nb = (float)(half_t)((float)w[p + half] * (float)(half_t)(b * rs));
+  }
   if (!on) return;
-  const float na = (float)(half_t)((float)w[p] * (float)(half_t)(a * rs));
-  const float nb = (float)(half_t)((float)w[p + half] * (float)(half_t)(b * rs));
   const int q = pos[r];
   const float c = cos_t[(size_t)q * half + p], sn = sin_t[(size_t)q * half + p];
   xh[p] = (half_t)(na * c - nb * sn);
@@ -304,7 +308,8 @@ extern "C" int fls_headnorm_rope(void* x, int ldx, int rows, int n_q, int n_k, c
                                  const int* pos, const float* cos_t, const float* sin_t, int hd, float eps,
                                  fls_stream_t s) {
   if (rows <= 0 || n_q + n_k <= 0) return 0;
-  if (hd != 64 && hd != 128) return -3;
+  if (hd != 64 && hd != 96 && hd != 128) return -3;
+  if ((qn == nullptr) != (kn == nullptr)) return -2;
   dim3 grid(rows, (n_q + n_k + 3) / 4);
   hipLaunchKernelGGL(headnorm_rope_kernel, grid, dim3(256), 0, (hipStream_t)s, (half_t*)x, ldx, rows, n_q, n_k,
                      (const half_t*)qn, (const half_t*)kn, pos, cos_t, sin_t, hd, eps);

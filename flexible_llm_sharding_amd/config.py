@@ -237,6 +237,13 @@ PRESETS = {
     "phi4": dict(hidden_size=5120, intermediate_size=17920, num_attention_heads=40, num_key_value_heads=10,
                  num_hidden_layers=40, vocab_size=100352, rope_theta=250000.0, max_position_embeddings=16384,
                  bos_token_id=100257, eos_token_id=100265, model_type="phi3", architectures=["Phi3ForCausalLM"]),
+    # Phi-3-mini-4k: multi-head attention with head_dim 96 (unfused RoPE pass, 12-chunk LDS rows)
+    "phi3-mini": dict(hidden_size=3072, intermediate_size=8192, num_attention_heads=32, num_key_value_heads=32,
+                      num_hidden_layers=32, vocab_size=32064, sliding_window=2047, eos_token_id=32000,
+                      model_type="phi3", architectures=["Phi3ForCausalLM"]),
+    "tiny-phi3-mini": dict(hidden_size=384, intermediate_size=768, num_attention_heads=4, num_key_value_heads=4,
+                           num_hidden_layers=2, vocab_size=512, model_type="phi3",
+                           architectures=["Phi3ForCausalLM"]),
     # tiny Phi-3-128k-style config: longrope short/long factors, attention factor from 131072 / 4096
     "tiny-phi3": dict(hidden_size=256, intermediate_size=512, num_attention_heads=4, num_key_value_heads=2,
                       num_hidden_layers=2, vocab_size=512, max_position_embeddings=131072,

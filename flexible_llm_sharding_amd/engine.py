@@ -141,8 +141,8 @@ class ShardedRunner:
         self.L = len(self.names)
         self.plan: ShardPlan = make_plan(self.L, layer_num_per_shard, self.comm.world, self.comm.rank,
                                          data_parallel, pipeline_stages)
-        if self.cuda and cfg.head_dim not in (64, 128):
-            raise NotImplementedError(f"head_dim={cfg.head_dim}: the HIP attention kernels serve 64 and 128")
+        if self.cuda and cfg.head_dim not in (64, 96, 128):
+            raise NotImplementedError(f"head_dim={cfg.head_dim}: the HIP attention kernels serve 64, 96 and 128")
         self.act_dtype = act_dtype or (torch.float16 if self.cuda else torch.float32)
         # multi-head models (odd GQA group): 128-row attention items, 4 waves share each K/V tile
         mha = (cfg.num_attention_heads // cfg.num_key_value_heads) % 2 == 1

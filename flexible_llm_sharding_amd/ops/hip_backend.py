@@ -100,6 +100,15 @@ class HipOps:
         if positions.dtype != torch.int32:
             raise TypeError("positions must be int32")
         rope_cols = (n_q_heads + n_kv_heads) * head_dim
+        if head_dim not in (64, 128):
+            # the fused epilogue finds a column's rotate-half partner 2 or 4 subtiles away inside
+            # the GEMM tile; other head sizes (Phi-3-mini: 96) rotate in a second pass
+            y = self.gemm(x, wqkv, EPI_NONE, out=out, bias=bias)
+            rc = self.k.fls_headnorm_rope(y.data_ptr(), y.stride(0), y.shape[0], n_q_heads, n_kv_heads, None, None,
+                                          positions.data_ptr(), cos.data_ptr(), sin.data_ptr(), head_dim, 0.0,
+                                          _stream())
+            _chk(rc, "fls_headnorm_rope")
+            return y
         return self.gemm(x, wqkv, EPI_ROPE, out=out, positions=positions, cos=cos, sin=sin,
                          rope_cols=rope_cols, head_dim=head_dim, bias=bias)
 

@@ -234,15 +234,16 @@ def _hf_family_case(tmp_path, family):
             rope_theta=cfg.rope_theta, max_position_embeddings=cfg.max_position_embeddings,
             head_dim=cfg.head_dim, tie_word_embeddings=False, use_sliding_window=False, attention_bias=False)
         model = transformers.Qwen3ForCausalLM(hf_cfg)
-    elif family == "phi3":
-        cfg = preset("tiny-phi3", sliding_window=64)
-        rs = dict(cfg.rope_scaling, rope_theta=cfg.rope_theta)
+    elif family in ("phi3", "phi3_mini"):
+        cfg = (preset("tiny-phi3", sliding_window=64) if family == "phi3"
+               else preset("tiny-phi3-mini", rope_theta=10000.0))
+        rs = dict(cfg.rope_scaling or {"rope_type": "default"}, rope_theta=cfg.rope_theta)
         hf_cfg = transformers.Phi3Config(
             hidden_size=cfg.hidden_size, intermediate_size=cfg.intermediate_size,
             num_attention_heads=cfg.num_attention_heads, num_key_value_heads=cfg.num_key_value_heads,
             num_hidden_layers=cfg.num_hidden_layers, vocab_size=cfg.vocab_size, rms_norm_eps=cfg.rms_norm_eps,
             max_position_embeddings=cfg.max_position_embeddings, original_max_position_embeddings=4096,
-            rope_parameters=rs, sliding_window=64, tie_word_embeddings=False, pad_token_id=0)
+            rope_parameters=rs, sliding_window=cfg.sliding_window, tie_word_embeddings=False, pad_token_id=0)
         model = transformers.Phi3ForCausalLM(hf_cfg)
     elif family in LLAMA_VARIANTS:
         over = dict(LLAMA_VARIANTS[family])
@@ -273,7 +274,7 @@ def _hf_family_case(tmp_path, family):
     return path, cfg, sd, model
 
 
-@pytest.mark.parametrize("family", ["qwen2", "qwen3", "phi3", "mistral"] + sorted(LLAMA_VARIANTS))
+@pytest.mark.parametrize("family", ["qwen2", "qwen3", "phi3", "phi3_mini", "mistral"] + sorted(LLAMA_VARIANTS))
 def test_other_llama_families_match_hf(tmp_path, family):
     """Qwen2 (q/k/v biases, rope_theta 1e6), Qwen3 (per-head q/k RMSNorm, head_dim 128 on a
     256-wide residual), Phi-3 (fused qkv_proj / gate_up_proj, LongRoPE with its attention factor,

@@ -83,7 +83,7 @@ def test_gemm_swiglu(ops, ref, M, I, K):
     assert rel_err(y.cpu(), r) < 3e-3
 
 
-@pytest.mark.parametrize("nh,nkv,hd,M", [(4, 2, 64, 300), (2, 1, 128, 257), (8, 8, 128, 64)])
+@pytest.mark.parametrize("nh,nkv,hd,M", [(4, 2, 64, 300), (2, 1, 128, 257), (8, 8, 128, 64), (4, 4, 96, 300)])
 def test_gemm_rope(ops, ref, nh, nkv, hd, M):
     from flexible_llm_sharding_amd.config import ModelConfig
     from flexible_llm_sharding_amd.models.llama import rope_tables
@@ -113,7 +113,7 @@ def _attn_case(nh, nkv, hd, prompts, prefix_attention, seed=0, q_block=64):
     return b, qkv
 
 
-@pytest.mark.parametrize("nh,nkv,hd", [(4, 4, 128), (6, 2, 64), (4, 2, 128), (3, 3, 64)])
+@pytest.mark.parametrize("nh,nkv,hd", [(4, 4, 128), (6, 2, 64), (4, 2, 128), (3, 3, 64), (4, 4, 96)])
 @pytest.mark.parametrize("mode", ["bidirectional", "causal"])
 def test_attention_128_row_items(ops, ref, nh, nkv, hd, mode):
     """128-row work items (multi-head models): 4 waves per query head share each K/V tile;
@@ -128,7 +128,8 @@ def test_attention_128_row_items(ops, ref, nh, nkv, hd, mode):
     assert rel_err(y.cpu(), r) < 5e-3
 
 
-@pytest.mark.parametrize("nh,nkv,hd", [(4, 2, 64), (8, 1, 128), (2, 2, 128), (16, 2, 128), (12, 2, 64)])
+@pytest.mark.parametrize("nh,nkv,hd", [(4, 2, 64), (8, 1, 128), (2, 2, 128), (16, 2, 128), (12, 2, 64),
+                                        (4, 4, 96), (4, 2, 96)])
 @pytest.mark.parametrize("mode", ["bidirectional", "causal"])
 def test_attention_shared_prefix(ops, ref, nh, nkv, hd, mode):
     prompts = [(70, [5, 64, 1]), (1, [3]), (130, [65, 17, 129]), (200, [33, 64])]
@@ -140,7 +141,7 @@ def test_attention_shared_prefix(ops, ref, nh, nkv, hd, mode):
     assert rel_err(y.cpu(), r) < 5e-3
 
 
-@pytest.mark.parametrize("nh,nkv,hd", [(8, 1, 128), (2, 2, 128), (4, 2, 64)])
+@pytest.mark.parametrize("nh,nkv,hd", [(8, 1, 128), (2, 2, 128), (4, 2, 64), (4, 4, 96)])
 def test_attention_prefix_from_cache(ops, ref, nh, nkv, hd):
     """Range 0 read from a separate prefix K/V tensor (prefix cache) == the full packed pass."""
     from flexible_llm_sharding_amd.runtime.batch import pack_prompts
@@ -184,7 +185,7 @@ def test_attention_softmax_spike(ops, ref):
 
 
 @pytest.mark.parametrize("q_block", [64, 128])
-@pytest.mark.parametrize("nh,nkv,hd", [(8, 2, 128), (4, 4, 128), (4, 2, 64)])
+@pytest.mark.parametrize("nh,nkv,hd", [(8, 2, 128), (4, 4, 128), (4, 2, 64), (4, 4, 96)])
 def test_attention_multi_suffix_items(ops, ref, q_block, nh, nkv, hd):
     """Work items holding several suffixes of one prompt (short suffixes, one crossing an item
     boundary): block-diagonal range 1 via seg_lo; the same rows computed with one suffix per item
@@ -400,7 +401,7 @@ def test_gemm_bias_epilogues(ops, ref, mid):
         ops.k.fls_gemm_set_mid(1)
 
 
-@pytest.mark.parametrize("nq,nk,hd", [(8, 2, 128), (4, 4, 64), (0, 2, 128), (6, 0, 128)])
+@pytest.mark.parametrize("nq,nk,hd", [(8, 2, 128), (4, 4, 64), (0, 2, 128), (6, 0, 128), (4, 4, 96)])
 def test_qkv_norm_rope(ops, ref, nq, nk, hd):
     """Qwen3 projection: GEMM + per-head q/k RMSNorm + RoPE (headnorm_rope_kernel) vs the fp32
     torch backend; V columns untouched; q-only and k/v-only forms (the pruned last layer)."""
