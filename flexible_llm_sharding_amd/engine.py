@@ -108,7 +108,7 @@ class ShardedRunner:
         if max_vram_gb:
             # size the micro-batch and the QKV / MLP chunks to the HBM cap (runtime/memplan.py);
             # re-planned per call once its token count is known (_plan_call)
-            from .runtime.memplan import plan_for_vram
+            from .runtime.memplan import device_used_bytes, plan_for_vram
             if self.dev.type == "cuda":
                 # device memory held outside the caching allocator before any weight slot exists:
                 # context, code objects, RCCL buffers — planned as measured, not guessed.  The
@@ -119,8 +119,7 @@ class ShardedRunner:
                     pcomm = getattr(prefetcher, "comm", None)
                     if pcomm is not None and pcomm is not self.comm:
                         pcomm.warmup()
-                free, total = torch.cuda.mem_get_info(self.dev)
-                self._outside = (total - free) - torch.cuda.memory_reserved(self.dev) + (64 << 20)
+                self._outside = device_used_bytes(self.dev) - torch.cuda.memory_reserved(self.dev) + (64 << 20)
             try:
                 # provisional (the call's token count is unknown yet); _plan_call is authoritative
                 token_budget, mlp_chunk, attn_rows, qkv_chunk, est = plan_for_vram(

@@ -19,6 +19,7 @@ fits.  ``bench.py --max-vram-gb`` reports the measured ``hipMemGetInfo`` peak ne
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Tuple
 
 from ..config import ModelConfig
@@ -56,14 +57,29 @@ def activation_bytes(cfg: ModelConfig, tokens: int, mlp_chunk: int, elem: int = 
     return int(slack * elem * (scratch + states * tokens * H))
 
 
+def shared_device_bytes() -> int:
+    """Device memory held by OTHER processes on the same GPU (``FLS_VRAM_SHARED_GB``, default 0),
+    left out of this process's ``--max_vram_gb`` budget: hipMemGetInfo counts the whole device,
+    so a co-tenant (e.g. the pytest process that launched a capped worker) would otherwise be
+    charged to the cap."""
+    return int(float(os.environ.get("FLS_VRAM_SHARED_GB", "0") or 0) * 1e9)
+
+
+def device_used_bytes(device) -> int:
+    """This process's share of the device memory in use: hipMemGetInfo minus other tenants."""
+    import torch
+    free, total = torch.cuda.mem_get_info(device)
+    return (total - free) - shared_device_bytes()
+
+
 def cap_allocator(device, max_vram_bytes: int, other_device_bytes: int) -> int:
     """Bound the caching allocator so that, with ``other_device_bytes`` held outside it (the
     raw weight slots), the device's memory in use stays <= ``max_vram_bytes``; when a request
     would pass the bound the allocator returns its unused cached blocks and retries.  Returns
     the allocator byte limit."""
     import torch
-    free, total = torch.cuda.mem_get_info(device)
-    outside = (total - free) - torch.cuda.memory_reserved(device)     # context, code objects, raw blocks
+    total = torch.cuda.mem_get_info(device)[1]
+    outside = device_used_bytes(device) - torch.cuda.memory_reserved(device)   # context, code objects, raw blocks
     limit = max_vram_bytes - outside - other_device_bytes - (64 << 20)
     if limit <= 0:
         raise ValueError(f"--max_vram_gb {max_vram_bytes / 1e9:.2f}: context + weight slots alone need "

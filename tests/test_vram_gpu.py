@@ -49,19 +49,36 @@ print(json.dumps({{"peak": peak, "plan": r.vram_plan, "mb": r.stats["micro_batch
 """
 
 
-def _run(tmp_path, cap, name):
+def _shared_bytes():
+    """Device memory held by this (pytest) process and any other tenant while the worker runs:
+    earlier GPU tests leave a context and cached blocks here, and hipMemGetInfo counts the whole
+    device.  Passed to the worker as FLS_VRAM_SHARED_GB so the cap is the worker's own."""
+    if not torch.cuda.is_initialized():
+        return 0
+    import gc
+    gc.collect()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    free, total = torch.cuda.mem_get_info(0)
+    return total - free
+
+
+def _run(tmp_path, cap, name, shared=0):
     out = str(tmp_path / f"{name}.npy")
     code = _WORKER.format(root=ROOT, cap=cap, tok=str(tmp_path / "tok"), out=out)
-    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    env = dict(os.environ, FLS_VRAM_SHARED_GB=str(shared / 1e9))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     return json.loads(r.stdout.strip().splitlines()[-1]), np.load(out)
 
 
 def test_vram_cap_holds_and_scores_match(tmp_path):
-    free = _run(tmp_path, 0, "free")
+    shared = _shared_bytes()
+    free = _run(tmp_path, 0, "free", shared)
     cap = 2.4          # Llama-2-7B geometry: 2 x 0.41 GB weight slots + ~0.67 GB context + activations
-    capped = _run(tmp_path, cap, "cap")
+    capped = _run(tmp_path, cap, "cap", shared)
     meta, got = capped
-    assert meta["peak"] <= cap * 1e9, meta
+    # the worker's peak: whole-device use minus what this process held before it started
+    assert meta["peak"] - shared <= cap * 1e9, (meta, shared)
     assert meta["slots"] == 2 and meta["plan"]["estimated_peak_bytes"] <= cap * 1e9
     assert np.array_equal(free[1], got)
