@@ -71,6 +71,16 @@ enum { FLS_EPI_NONE = 0, FLS_EPI_RESID = 1, FLS_EPI_SWIGLU = 2, FLS_EPI_ROPE = 3
 int fls_gemm(const void* A, const void* W, void* C, const void* R, int M, int N, int K,
              int lda, int ldw, int ldc, int ldr, int epi, const int* pos, const float* cos_t,
              const float* sin_t, int rope_cols, int head_dim, const void* bias, fls_stream_t s);
+// mixture-of-experts FFN (csrc/kernels/moe.hip): routing, stable expert sort, grouped v10 GEMM
+// (every expert of a layer in one launch, optional row gather), fp16-ordered weighted combine
+int fls_moe_route(const void* logits, int ldl, int T, int E, int k, int norm, int round16, int* ids, float* w,
+                  fls_stream_t s);
+int fls_moe_plan(const int* ids, int n, int k, int E, int* offs, int* tiles, int* rows, int* dest, fls_stream_t s);
+int fls_moe_gemm(const void* A, const void* W, void* C, int M_bound, int N, int K, int lda, int ldw, int ldc, int epi,
+                 const int* tiles, const int* offs, const int* rows, int n_groups, long long wstride, int a_rows,
+                 fls_stream_t s);
+int fls_moe_combine(const void* y, int ldy, const int* ids, const int* dest, const float* w, void* x, int ldx, int T,
+                    int k, int H, fls_stream_t s);
 int fls_gemm_set_order(int order);   // tile order: 0 by shape, 8 M-grouped, -4/-8 N-grouped
 int fls_gemm_set_mid(int on);   // 64x128-tile kernel for small / medium M (default on)
 // shared-prefix / varlen flash attention over packed work items (int32 x8:

@@ -63,7 +63,7 @@ class Piece(ctypes.Structure):
                 ("kind", ctypes.c_int32), ("pad", ctypes.c_int32)]
 
 
-KERNELS_ABI = 10   # bumped whenever a C signature in csrc/include/fls.h changes
+KERNELS_ABI = 11   # bumped whenever a C signature in csrc/include/fls.h changes
 
 
 def _load_kernels():
@@ -75,6 +75,13 @@ def _load_kernels():
     _bind(lib, "fls_gemm", c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
           c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p)
     _bind(lib, "fls_gemm_set_mid", c_int, c_int)
+    _bind(lib, "fls_moe_route", c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+          c_void_p)
+    _bind(lib, "fls_moe_plan", c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p)
+    _bind(lib, "fls_moe_gemm", c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+          c_void_p, c_void_p, c_void_p, c_int, ctypes.c_longlong, c_int, c_void_p)
+    _bind(lib, "fls_moe_combine", c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+          c_int, c_int, c_void_p)
     _bind(lib, "fls_gemm_set_order", c_int, c_int)
     _bind(lib, "fls_attention_set_hpb", c_int, c_int)
     _bind(lib, "fls_attention", c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,

@@ -37,6 +37,14 @@ class ModelConfig:
     # longrope (Phi-3)
     rope_scaling: Optional[dict] = None
     explicit_head_dim: Optional[int] = None   # HF ``head_dim`` when != hidden / heads (Mistral-Nemo)
+    # sparse mixture-of-experts FFN (Mixtral, Qwen3-MoE): 0 = dense SwiGLU MLP.  Each token's
+    # post-attention RMSNorm output goes to its top-k experts (router softmax in fp32, top-k,
+    # renormalised when norm_topk_prob), each a SwiGLU MLP of moe_intermediate_size (Mixtral:
+    # intermediate_size), and the weighted expert outputs are summed into the residual
+    num_local_experts: int = 0
+    num_experts_per_tok: int = 2
+    moe_intermediate_size: Optional[int] = None
+    norm_topk_prob: bool = True
     bos_token_id: int = 1
     eos_token_id: int = 2
     torch_dtype: str = "float16"
@@ -47,6 +55,15 @@ class ModelConfig:
     @property
     def head_dim(self) -> int:
         return self.explicit_head_dim or self.hidden_size // self.num_attention_heads
+
+    @property
+    def is_moe(self) -> bool:
+        return self.num_local_experts > 0
+
+    @property
+    def expert_intermediate(self) -> int:
+        """Rows of one expert's gate (= up) projection (the dense MLP's for non-MoE models)."""
+        return self.moe_intermediate_size or self.intermediate_size
 
     @property
     def fused_projections(self) -> bool:
@@ -78,8 +95,20 @@ class ModelConfig:
                 + ["model.norm", "lm_head"])
 
     def decoder_layer_params(self) -> int:
-        h, i = self.hidden_size, self.intermediate_size
-        n = h * self.qkv_size + self.q_size * h + 3 * h * i + 2 * h
+        """Parameters stored per decoder layer (every expert of an MoE layer)."""
+        return self._decoder_params(self.num_local_experts)
+
+    def decoder_active_params(self) -> int:
+        """Parameters one token multiplies per decoder layer (MoE: router + its top-k experts)."""
+        return self._decoder_params(self.num_experts_per_tok) if self.is_moe else self.decoder_layer_params()
+
+    def _decoder_params(self, experts: int) -> int:
+        h = self.hidden_size
+        n = h * self.qkv_size + self.q_size * h + 2 * h
+        if self.is_moe:
+            n += self.num_local_experts * h + experts * 3 * h * self.expert_intermediate
+        else:
+            n += 3 * h * self.intermediate_size
         return (n + (self.qkv_size if self.attention_bias else 0) + (h if self.o_proj_bias else 0)
                 + (2 * self.head_dim if self.qk_norm else 0))
 
@@ -95,6 +124,10 @@ class ModelConfig:
             raise ValueError("num_attention_heads must be a multiple of num_key_value_heads")
         if self.head_dim % 32:
             raise ValueError("head_dim must be a multiple of 32 (RoPE pair blocks of 16)")
+        if self.is_moe and not 1 <= self.num_experts_per_tok <= min(self.num_local_experts, MAX_TOP_K):
+            raise ValueError(f"num_experts_per_tok must be in 1..min(num_local_experts, {MAX_TOP_K})")
+        if self.num_local_experts > MAX_EXPERTS:
+            raise NotImplementedError(f"num_local_experts={self.num_local_experts} > {MAX_EXPERTS}")
         rs = self.rope_scaling
         if rs:
             kind = rs.get("rope_type", rs.get("type"))
@@ -146,6 +179,17 @@ class ModelConfig:
         mt = d.get("model_type", "llama")
         if mt not in SUPPORTED_MODEL_TYPES:
             raise NotImplementedError(f"model_type={mt!r}: supported are {sorted(SUPPORTED_MODEL_TYPES)}")
+        if mt in ("qwen3_moe", "qwen2_moe"):
+            kw["num_local_experts"] = int(d.get("num_experts") or d.get("num_local_experts") or 0)
+            if d.get("shared_expert_intermediate_size"):
+                raise NotImplementedError("MoE shared experts (Qwen2-MoE) are not supported")
+            if d.get("mlp_only_layers") or int(d.get("decoder_sparse_step", 1) or 1) != 1:
+                raise NotImplementedError("dense layers between the MoE layers (mlp_only_layers / "
+                                          "decoder_sparse_step) are not supported")
+        if mt == "mixtral":
+            kw["norm_topk_prob"] = True           # HF MixtralTopKRouter always renormalises
+        elif mt in ("qwen3_moe", "qwen2_moe"):
+            kw["norm_topk_prob"] = bool(d.get("norm_topk_prob", False))     # HF Qwen3MoeConfig default
         if d.get("mlp_bias"):
             raise NotImplementedError("mlp_bias=True is not supported")
         hdim = d.get("head_dim")
@@ -159,12 +203,13 @@ class ModelConfig:
             kw["attention_bias"], kw["o_proj_bias"] = True, False
         elif d.get("attention_bias"):
             kw["attention_bias"], kw["o_proj_bias"] = True, True
-        if mt == "qwen3":
+        if mt in ("qwen3", "qwen3_moe"):
             # HF Qwen3Attention: q_norm / k_norm (RMSNorm over head_dim) on every head before RoPE;
             # q/k/v/o biases only with attention_bias (off in every released Qwen3 config)
             kw["qk_norm"] = True
-        # HF Phi3Model applies its sliding_window whenever it is set; Qwen2/3 only with use_sliding_window
-        if not d.get("use_sliding_window", mt in ("mistral", "phi3")):
+        # HF Phi3Model / Mixtral apply their sliding_window whenever it is set; Qwen2/3 only with
+        # use_sliding_window
+        if not d.get("use_sliding_window", mt in ("mistral", "phi3", "mixtral")):
             kw.pop("sliding_window", None)
         if isinstance(kw.get("eos_token_id"), list):
             kw["eos_token_id"] = kw["eos_token_id"][0]
@@ -186,6 +231,8 @@ class ModelConfig:
         os.makedirs(model_path, exist_ok=True)
         d = asdict(self)
         d["head_dim"] = self.head_dim           # HF key (also read back by from_dict)
+        if self.model_type in ("qwen3_moe", "qwen2_moe"):
+            d["num_experts"] = self.num_local_experts          # the HF key of these families
         with open(os.path.join(model_path, "config.json"), "w") as f:
             json.dump(d, f, indent=2)
 
@@ -193,7 +240,10 @@ class ModelConfig:
 # Llama-structured causal LMs (model.embed_tokens / model.layers.N / model.norm / lm_head with
 # q/k/v/o + gate/up/down + two RMSNorms per layer) -- what the reference's AutoModelForCausalLM
 # path (utils.py:101-115) runs in practice.
-SUPPORTED_MODEL_TYPES = {"llama", "mistral", "qwen2", "qwen3", "phi3"}
+SUPPORTED_MODEL_TYPES = {"llama", "mistral", "qwen2", "qwen3", "phi3", "mixtral", "qwen3_moe"}
+# MoE limits of the routing kernels (csrc/kernels/moe.hip): experts per layer, experts per token
+MAX_EXPERTS = 256
+MAX_TOP_K = 8
 # static RoPE scalings: they only change the cos/sin tables (models/llama.py rope_inv_freq)
 ROPE_SCALING_TYPES = {"linear", "llama3", "yarn", "longrope"}
 
@@ -257,6 +307,25 @@ PRESETS = {
                         max_position_embeddings=131072, bos_token_id=128000, eos_token_id=128001,
                         rope_scaling={"rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0,
                                       "high_freq_factor": 4.0, "original_max_position_embeddings": 8192}),
+    # sparse MoE: Mixtral-8x7B (8 experts, top-2, 32k vocab) and Qwen3-30B-A3B (128 experts of
+    # 768 rows, top-8, q/k norm); tiny variants keep every GEMM on the grouped MFMA path
+    "mixtral-8x7b": dict(hidden_size=4096, intermediate_size=14336, num_attention_heads=32, num_key_value_heads=8,
+                         num_hidden_layers=32, vocab_size=32000, rope_theta=1e6, max_position_embeddings=32768,
+                         num_local_experts=8, num_experts_per_tok=2, model_type="mixtral",
+                         architectures=["MixtralForCausalLM"]),
+    "qwen3-30b-a3b": dict(hidden_size=2048, intermediate_size=6144, num_attention_heads=32, num_key_value_heads=4,
+                          num_hidden_layers=48, vocab_size=151936, rope_theta=1e6, rms_norm_eps=1e-6, qk_norm=True,
+                          explicit_head_dim=128, max_position_embeddings=40960, num_local_experts=128,
+                          num_experts_per_tok=8, moe_intermediate_size=768, norm_topk_prob=True,
+                          model_type="qwen3_moe", architectures=["Qwen3MoeForCausalLM"]),
+    "tiny-mixtral": dict(hidden_size=256, intermediate_size=256, num_attention_heads=4, num_key_value_heads=2,
+                         num_hidden_layers=2, vocab_size=512, rope_theta=1e6, num_local_experts=4,
+                         num_experts_per_tok=2, model_type="mixtral", architectures=["MixtralForCausalLM"]),
+    "tiny-qwen3-moe": dict(hidden_size=256, intermediate_size=512, num_attention_heads=4, num_key_value_heads=2,
+                           num_hidden_layers=2, vocab_size=512, rope_theta=1e6, rms_norm_eps=1e-6, qk_norm=True,
+                           explicit_head_dim=128, num_local_experts=8, num_experts_per_tok=3,
+                           moe_intermediate_size=128, norm_topk_prob=False, model_type="qwen3_moe",
+                           architectures=["Qwen3MoeForCausalLM"]),
     "small": dict(hidden_size=1024, intermediate_size=2816, num_attention_heads=8,
                   num_key_value_heads=2, num_hidden_layers=4, vocab_size=32000),
 }

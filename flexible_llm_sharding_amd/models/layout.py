@@ -18,6 +18,17 @@ Decoder layer image (fp16, every slot 256-byte aligned)::
     wgu   [2I, H]          gate_proj | up_proj        (rows concatenated)
     wdown [H, I]           down_proj
 
+MoE decoder (Mixtral / Qwen3-MoE) — the MLP piece is the router and every expert, each expert's
+tensors whole and in checkpoint row order::
+
+    ln2     [H]            post_attention_layernorm.weight
+    wrouter [E, H]         router (Mixtral block_sparse_moe.gate / Qwen3-MoE mlp.gate)
+    wgu     [E, 2I', H]    per expert: gate (w1 / gate_proj) | up (w3 / up_proj)
+    wdown   [E, H, I']     per expert: down (w2 / down_proj)
+
+so expert e's [gate; up] block is the same stacked operand as the dense wgu, at a fixed stride:
+the grouped GEMM (csrc/kernels/moe.hip) indexes experts by that stride.
+
 Everything the attention phase reads comes before ``ln2`` and nothing after it: the image
 splits into an attention piece and an MLP piece (:func:`mlp_offset`) that the
 ``--max_vram_gb`` prefetcher streams into separate HBM pools and frees separately
@@ -119,7 +130,11 @@ def layer_layout(cfg: ModelConfig, kind: str, elem_size: int = 2) -> LayerLayout
         specs.append(("wo", (H, cfg.q_size)))
         if cfg.o_proj_bias:
             specs.append(("bo", (H,)))
-        specs += [("ln2", (H,)), ("wgu", (2 * I, H)), ("wdown", (H, I))]
+        if cfg.is_moe:
+            E, Ie = cfg.num_local_experts, cfg.expert_intermediate
+            specs += [("ln2", (H,)), ("wrouter", (E, H)), ("wgu", (E, 2 * Ie, H)), ("wdown", (E, H, Ie))]
+        else:
+            specs += [("ln2", (H,)), ("wgu", (2 * I, H)), ("wdown", (H, I))]
     else:
         raise ValueError(kind)
     slots, off = [], 0
@@ -171,8 +186,11 @@ def placements(cfg: ModelConfig, layer_name: str, elem_size: int = 2) -> List[Pl
         Placement(f"{p}.input_layernorm.weight", o["ln1"], H, (H,), es),
         Placement(f"{p}.post_attention_layernorm.weight", o["ln2"], H, (H,), es),
         Placement(f"{p}.self_attn.o_proj.weight", o["wo"], H * qs, (H, qs), es),
-        Placement(f"{p}.mlp.down_proj.weight", o["wdown"], H * I, (H, I), es),
     ]
+    if cfg.is_moe:
+        out += _expert_placements(cfg, p, o, es)
+    else:
+        out.append(Placement(f"{p}.mlp.down_proj.weight", o["wdown"], H * I, (H, I), es))
     if cfg.fused_projections:
         # Phi-3: one tensor each, already in slot row order
         qkv = qs + 2 * ks
@@ -183,9 +201,10 @@ def placements(cfg: ModelConfig, layer_name: str, elem_size: int = 2) -> List[Pl
             Placement(f"{p}.self_attn.q_proj.weight", o["wqkv"], qs * H, (qs, H), es),
             Placement(f"{p}.self_attn.k_proj.weight", o["wqkv"] + es * qs * H, ks * H, (ks, H), es),
             Placement(f"{p}.self_attn.v_proj.weight", o["wqkv"] + es * (qs + ks) * H, ks * H, (ks, H), es),
-            Placement(f"{p}.mlp.gate_proj.weight", o["wgu"], I * H, (I, H), es),
-            Placement(f"{p}.mlp.up_proj.weight", o["wgu"] + es * I * H, I * H, (I, H), es),
         ]
+        if not cfg.is_moe:
+            out += [Placement(f"{p}.mlp.gate_proj.weight", o["wgu"], I * H, (I, H), es),
+                    Placement(f"{p}.mlp.up_proj.weight", o["wgu"] + es * I * H, I * H, (I, H), es)]
     if cfg.attention_bias:
         out += [Placement(f"{p}.self_attn.q_proj.bias", o["bqkv"], qs, (qs,), es),
                 Placement(f"{p}.self_attn.k_proj.bias", o["bqkv"] + es * qs, ks, (ks,), es),
@@ -196,6 +215,33 @@ def placements(cfg: ModelConfig, layer_name: str, elem_size: int = 2) -> List[Pl
         hd = cfg.head_dim
         out += [Placement(f"{p}.self_attn.q_norm.weight", o["qn"], hd, (hd,), es),
                 Placement(f"{p}.self_attn.k_norm.weight", o["kn"], hd, (hd,), es)]
+    return out
+
+
+def expert_names(cfg: ModelConfig, p: str, e: int) -> Tuple[str, str, str]:
+    """Checkpoint names of expert ``e``'s (gate, up, down) weights in decoder layer ``p``: the
+    per-expert tensors of the released checkpoints (Mixtral ``block_sparse_moe.experts.e.w1/w3/w2``,
+    Qwen3-MoE ``mlp.experts.e.gate_proj/up_proj/down_proj``)."""
+    if cfg.model_type == "mixtral":
+        b = f"{p}.block_sparse_moe.experts.{e}"
+        return f"{b}.w1.weight", f"{b}.w3.weight", f"{b}.w2.weight"
+    b = f"{p}.mlp.experts.{e}"
+    return f"{b}.gate_proj.weight", f"{b}.up_proj.weight", f"{b}.down_proj.weight"
+
+
+def router_name(cfg: ModelConfig, p: str) -> str:
+    return f"{p}.block_sparse_moe.gate.weight" if cfg.model_type == "mixtral" else f"{p}.mlp.gate.weight"
+
+
+def _expert_placements(cfg: ModelConfig, p: str, o: Dict[str, int], es: int) -> List[Placement]:
+    H, E, Ie = cfg.hidden_size, cfg.num_local_experts, cfg.expert_intermediate
+    out = [Placement(router_name(cfg, p), o["wrouter"], E * H, (E, H), es)]
+    for e in range(E):
+        g, u, d = expert_names(cfg, p, e)
+        gu = o["wgu"] + es * e * 2 * Ie * H
+        out += [Placement(g, gu, Ie * H, (Ie, H), es),
+                Placement(u, gu + es * Ie * H, Ie * H, (Ie, H), es),
+                Placement(d, o["wdown"] + es * e * H * Ie, H * Ie, (H, Ie), es)]
     return out
 
 

@@ -334,6 +334,8 @@ def run_decoder(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, b
     T = x.shape[0]
     I, H = cfg.intermediate_size, cfg.hidden_size
     step = balanced_step(T, max(1, ctx.mlp_chunk))
+    if cfg.is_moe:
+        return _moe_mlp(ctx, W, x, step)
     if T <= step:
         ctx.phase((T, H), (T, I))               # the attention-phase bytes are dead: reuse them
         h = ops.rmsnorm(x, W["ln2"], eps, out=ctx.scratch(T, H))
@@ -349,6 +351,23 @@ def run_decoder(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, b
             m = ops.swiglu_up(h, W["wgu"], out=ctx.scratch(n, I))
             del h
             x[s:s + step] = ops.linear_residual(m, W["wdown"], xs)
+    return x
+
+
+def _moe_mlp(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, step: int) -> torch.Tensor:
+    """Sparse-MoE MLP phase in token chunks of ``step`` rows, in place on x: per chunk the
+    workspace holds [normed chunk | expert SwiGLU rows (k per token) | expert outputs]."""
+    cfg, ops = ctx.cfg, ctx.ops
+    H, Ie, k = cfg.hidden_size, cfg.expert_intermediate, cfg.num_experts_per_tok
+    for s in range(0, x.shape[0], step):
+        xs = x[s:s + step]
+        n = xs.shape[0]
+        ctx.phase((n, H), (n * k, Ie), (n * k, H))
+        h = ops.rmsnorm(xs, W["ln2"], cfg.rms_norm_eps, out=ctx.scratch(n, H))
+        ops.moe_ffn(h, xs, W["wrouter"], W["wgu"], W["wdown"], k, cfg.norm_topk_prob,
+                    round_w16=cfg.model_type == "qwen3_moe", m_out=ctx.scratch(n * k, Ie),
+                    y_out=ctx.scratch(n * k, H))
+        del h
     return x
 
 
@@ -381,10 +400,10 @@ def layer_flops(cfg: ModelConfig, batch, pruned: bool = False) -> float:
     if pruned:
         S = batch.n_scored
         kv = 2 * cfg.kv_size * cfg.hidden_size
-        gemm = 2.0 * (T * kv + S * (cfg.decoder_layer_params() - kv))
+        gemm = 2.0 * (T * kv + S * (cfg.decoder_active_params() - kv))
         segs = batch.last_segments
     else:
-        gemm = 2.0 * T * cfg.decoder_layer_params()
+        gemm = 2.0 * T * cfg.decoder_active_params()
         segs = batch.segments
     att = 0.0
     for sg in segs:

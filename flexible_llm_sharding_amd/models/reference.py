@@ -61,9 +61,33 @@ def _block(x, sd, p, cfg, pos, cos, sin, mask, past_kv=None):
     a = a.transpose(1, 2).reshape(B, T, nh * hd)
     x = x + a @ g("self_attn.o_proj.weight").t() + b("self_attn.o_proj.bias")
     h = _rms(x, g("post_attention_layernorm.weight"), cfg.rms_norm_eps)
+    if cfg.is_moe:
+        return x + _moe(h, sd, p, cfg), present
     m = F.silu(h @ g("mlp.gate_proj.weight").t()) * (h @ g("mlp.up_proj.weight").t())
     x = x + m @ g("mlp.down_proj.weight").t()
     return x, present
+
+
+def _moe(h, sd, p, cfg):
+    """HF MixtralSparseMoeBlock / Qwen3MoeSparseMoeBlock in fp32: router softmax, top-k,
+    optional renormalisation, weighted sum of the chosen experts' SwiGLU outputs."""
+    from .layout import expert_names, router_name
+    shape = h.shape
+    h = h.reshape(-1, shape[-1])
+    probs = torch.softmax(h @ sd[router_name(cfg, p)].float().t(), -1)
+    w, idx = torch.topk(probs, cfg.num_experts_per_tok, dim=-1)
+    if cfg.norm_topk_prob:
+        w = w / w.sum(-1, keepdim=True)
+    out = torch.zeros_like(h)
+    for e in range(cfg.num_local_experts):
+        tok, slot = torch.where(idx == e)
+        if tok.numel() == 0:
+            continue
+        gn, un, dn = expert_names(cfg, p, e)
+        he = h[tok]
+        y = (F.silu(he @ sd[gn].float().t()) * (he @ sd[un].float().t())) @ sd[dn].float().t()
+        out.index_add_(0, tok, y * w[tok, slot, None])
+    return out.reshape(shape)
 
 
 def reference_scores(cfg: ModelConfig, sd: Dict[str, torch.Tensor], tok, prompts: Sequence,

@@ -12,6 +12,8 @@ own weight layout (``wqkv = [q; k; v]``, ``wgu = [gate; up]``).
 """
 from __future__ import annotations
 
+from dataclasses import dataclass
+
 import torch
 
 from .. import _native
@@ -35,6 +37,20 @@ def _f16(t: torch.Tensor, name: str):
         raise TypeError(f"{name}: expected fp16 CUDA tensor, got {t.dtype} on {t.device}")
     if t.stride(-1) != 1:
         raise ValueError(f"{name}: last dim must be contiguous")
+
+
+@dataclass
+class MoeRoute:
+    """Device-side routing of one MoE call (csrc/kernels/moe.hip): per (token, slot) entry the
+    expert id and weight; per expert its permuted-row offsets and 256-row tile prefix; permuted
+    row -> token (``rows``) and entry -> permuted row (``dest``)."""
+    ids: torch.Tensor
+    w: torch.Tensor
+    offs: torch.Tensor
+    tiles: torch.Tensor
+    rows: torch.Tensor
+    dest: torch.Tensor
+    k: int
 
 
 class HipOps:
@@ -126,6 +142,81 @@ class HipOps:
                                       float(eps), _stream())
         _chk(rc, "fls_headnorm_rope")
         return y
+
+    # ------------------------------------------------------ mixture of experts
+    def moe_ffn(self, h, x, wrouter, wgu, wdown, top_k: int, norm_topk: bool, round_w16: bool = False,
+                m_out=None, y_out=None):
+        """x += sparse-MoE FFN of h, in place (csrc/kernels/moe.hip): router GEMM, top-k routing,
+        stable expert sort, grouped SwiGLU GEMM gathering h's rows, grouped down GEMM, ordered
+        combine.  wgu [E, 2I, H] ([gate; up] per expert), wdown [E, H, I].  No host sync: the
+        grouped GEMMs read the per-expert row counts on the device.  m_out [T*k, I] / y_out
+        [T*k, H]: optional scratch for the expert intermediates."""
+        route = self.moe_route(h, wrouter, top_k, norm_topk, round_w16)
+        return self.moe_experts(h, x, wgu, wdown, route, m_out=m_out, y_out=y_out)
+
+    def moe_route(self, h, wrouter, top_k: int, norm_topk: bool, round_w16: bool = False) -> "MoeRoute":
+        _f16(h, "h")
+        _f16(wrouter, "router")
+        T = h.shape[0]
+        E = wrouter.shape[0]
+        k = int(top_k)
+        logits = self.gemm(h, wrouter)                                    # [T, E] fp16 (HF Linear)
+        return self.moe_route_logits(logits, k, norm_topk, round_w16)
+
+    def moe_route_logits(self, logits, top_k: int, norm_topk: bool, round_w16: bool = False) -> "MoeRoute":
+        """Routing from fp16 router logits [T, E]: top-k ids / weights per token and the stable
+        expert sort (offsets, 256-row tile prefix, permuted row -> token, entry -> permuted row)."""
+        _f16(logits, "logits")
+        T, E = logits.shape
+        k, n, dev = int(top_k), T * int(top_k), logits.device
+        ids = torch.empty(n, dtype=torch.int32, device=dev)
+        w = torch.empty(n, dtype=torch.float32, device=dev)
+        st = _stream()
+        _chk(self.k.fls_moe_route(logits.data_ptr(), logits.stride(0), T, E, k, int(bool(norm_topk)),
+                                  int(bool(round_w16)), ids.data_ptr(), w.data_ptr(), st), "fls_moe_route")
+        meta = torch.empty(2 * (E + 1) + 2 * n, dtype=torch.int32, device=dev)
+        r = MoeRoute(ids, w, meta[:E + 1], meta[E + 1:2 * (E + 1)], meta[2 * (E + 1):2 * (E + 1) + n],
+                     meta[2 * (E + 1) + n:], k)
+        _chk(self.k.fls_moe_plan(ids.data_ptr(), n, k, E, r.offs.data_ptr(), r.tiles.data_ptr(),
+                                 r.rows.data_ptr(), r.dest.data_ptr(), st), "fls_moe_plan")
+        return r
+
+    def moe_experts(self, h, x, wgu, wdown, route: "MoeRoute", m_out=None, y_out=None):
+        """x += sum over each token's routed experts of w * down(swiglu(h)), in place."""
+        for t, nm in ((h, "h"), (x, "x"), (wgu, "wgu"), (wdown, "wdown")):
+            _f16(t, nm)
+        T, H = h.shape
+        E, I2, _ = wgu.shape
+        I, k = I2 // 2, route.k
+        n = T * k
+        dev, st = h.device, _stream()
+        m = m_out if m_out is not None else torch.empty(n, I, dtype=torch.float16, device=dev)
+        y = y_out if y_out is not None else torch.empty(n, H, dtype=torch.float16, device=dev)
+        bound = n + 255 * E                       # >= sum over experts of their rows rounded up to 256
+        rc = self.k.fls_moe_gemm(h.data_ptr(), wgu.data_ptr(), m.data_ptr(), bound, I2, H, h.stride(0),
+                                 wgu.stride(1), m.stride(0), EPI_SWIGLU, route.tiles.data_ptr(),
+                                 route.offs.data_ptr(), route.rows.data_ptr(), E, wgu.stride(0), T, st)
+        if rc == -5:                              # shape outside the grouped kernel: per-expert GEMMs
+            self._moe_per_expert(h, wgu, wdown, route, m, y)
+        else:
+            _chk(rc, "fls_moe_gemm(gate/up)")
+            _chk(self.k.fls_moe_gemm(m.data_ptr(), wdown.data_ptr(), y.data_ptr(), bound, H, I, m.stride(0),
+                                     wdown.stride(1), y.stride(0), EPI_NONE, route.tiles.data_ptr(),
+                                     route.offs.data_ptr(), None, E, wdown.stride(0), n, st), "fls_moe_gemm(down)")
+        _chk(self.k.fls_moe_combine(y.data_ptr(), y.stride(0), route.ids.data_ptr(), route.dest.data_ptr(),
+                                    route.w.data_ptr(), x.data_ptr(), x.stride(0), T, k, H, st), "fls_moe_combine")
+        return x
+
+    def _moe_per_expert(self, h, wgu, wdown, route, m, y):
+        """Fallback for shapes outside the grouped kernel's contract: one host read of the
+        per-expert row counts, then the dense fused GEMMs expert by expert."""
+        o = route.offs.cpu().tolist()
+        for e in range(wgu.shape[0]):
+            a, b = o[e], o[e + 1]
+            if a == b:
+                continue
+            self.gemm(h.index_select(0, route.rows[a:b]), wgu[e], EPI_SWIGLU, out=m[a:b])
+            self.gemm(m[a:b], wdown[e], out=y[a:b])
 
     # ----------------------------------------------------------- attention
     def attention(self, qkv, work, n_q_heads, n_kv_heads, head_dim, kv0=None, q_block: int = 64, out=None,

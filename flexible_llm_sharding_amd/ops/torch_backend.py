@@ -90,6 +90,30 @@ class TorchOps:
         qk_out = torch.stack([x1 * c - x2 * s, x2 * c + x1 * s], dim=2).reshape(T, nqk * head_dim)
         return torch.cat([qk_out.to(x.dtype), y[:, nqk * head_dim:]], dim=1)
 
+    def moe_ffn(self, h: torch.Tensor, x: torch.Tensor, wrouter: torch.Tensor, wgu: torch.Tensor,
+                wdown: torch.Tensor, top_k: int, norm_topk: bool, round_w16: bool = False, m_out=None,
+                y_out=None) -> torch.Tensor:
+        """x += sparse-MoE FFN of h, in place, in the order and rounding of HF's expert loop
+        (transformers MixtralExperts / Qwen3MoeExperts): router Linear in the activation dtype,
+        fp32 softmax, top-k, optional renormalisation (Qwen3-MoE rounds the weights to the
+        activation dtype), each expert's weighted output rounded to the activation dtype and
+        accumulated in expert order, then added to the residual."""
+        logits = self.linear(h, wrouter)
+        w, idx = torch.topk(torch.softmax(logits.float(), dim=-1), top_k, dim=-1)
+        if norm_topk:
+            w = w / w.sum(-1, keepdim=True)
+        if round_w16:
+            w = w.to(h.dtype).float()
+        acc = torch.zeros_like(x)
+        for e in range(wgu.shape[0]):
+            tok, slot = torch.where(idx == e)
+            if tok.numel() == 0:
+                continue
+            y = self.linear(self.swiglu_up(h.index_select(0, tok), wgu[e]), wdown[e])
+            acc.index_add_(0, tok, (y.float() * w[tok, slot, None]).to(x.dtype))
+        x.copy_((x.float() + acc.float()).to(x.dtype))
+        return x
+
     def attention(self, qkv: torch.Tensor, segments, n_q_heads: int, n_kv_heads: int,
                   head_dim: int, kv0: torch.Tensor = None, q_block: int = 64, out=None) -> torch.Tensor:
         """Shared-prefix attention over packed segments (see runtime.batch).

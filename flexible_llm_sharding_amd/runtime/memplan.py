@@ -52,7 +52,9 @@ def activation_bytes(cfg: ModelConfig, tokens: int, mlp_chunk: int, elem: int = 
     else:
         qc = balanced_step(tokens, qkv_chunk) if qkv_chunk else tokens
         attn = qc * H + tokens * Q
-    scratch = max(attn, chunk * (H + I))                 # one arena, two phases
+    # MLP phase: [normed chunk | SwiGLU chunk]; MoE: k SwiGLU rows and k expert outputs per token
+    mlp = chunk * (H + (cfg.num_experts_per_tok * (cfg.expert_intermediate + H) if cfg.is_moe else I))
+    scratch = max(attn, mlp)                             # one arena, two phases
     slack = SLACK_ONE if states == 1 else SLACK
     return int(slack * elem * (scratch + states * tokens * H))
 

@@ -31,6 +31,37 @@ def layer_of_param(name: str) -> str:
     return ".".join(name.replace(".weight", "").split(".")[:3])
 
 
+def normalize_expert_names(model_type: str, sd: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+    """MoE state dicts in transformers-v5 form (``mlp.experts.gate_up_proj`` [E, 2I, H] /
+    ``mlp.experts.down_proj`` [E, H, I], Mixtral's router as ``mlp.gate``) -> the per-expert tensors
+    of the released checkpoints (Mixtral ``block_sparse_moe.experts.e.w1/w3/w2``, Qwen3-MoE
+    ``mlp.experts.e.gate_proj/up_proj/down_proj``), the one form the per-layer files hold
+    (``models.layout.placements``).  Other keys pass through."""
+    if model_type not in ("mixtral", "qwen3_moe"):
+        return sd
+    out = {}
+    for k, v in sd.items():
+        if k.endswith(".mlp.experts.gate_up_proj") or k.endswith(".mlp.experts.down_proj"):
+            p = k[:-len(".mlp.experts.gate_up_proj")] if k.endswith("gate_up_proj") else k[:-len(".mlp.experts.down_proj")]
+            for e in range(v.shape[0]):
+                if model_type == "mixtral":
+                    b = f"{p}.block_sparse_moe.experts.{e}"
+                    names = (f"{b}.w1.weight", f"{b}.w3.weight", f"{b}.w2.weight")
+                else:
+                    b = f"{p}.mlp.experts.{e}"
+                    names = (f"{b}.gate_proj.weight", f"{b}.up_proj.weight", f"{b}.down_proj.weight")
+                if k.endswith("gate_up_proj"):
+                    g, u = v[e].chunk(2, 0)
+                    out[names[0]], out[names[1]] = g.contiguous(), u.contiguous()
+                else:
+                    out[names[2]] = v[e].contiguous()
+        elif model_type == "mixtral" and k.endswith(".mlp.gate.weight"):
+            out[k[:-len(".mlp.gate.weight")] + ".block_sparse_moe.gate.weight"] = v
+        else:
+            out[k] = v
+    return out
+
+
 def layer_file(model_path: str, layer_name: str) -> str:
     return os.path.join(model_path, f"{layer_name}.safetensors")
 
@@ -75,6 +106,7 @@ def split_into_layers(src_dir: str, out_dir: str, verbose: bool = True) -> List[
     for p in wmap:
         layer_params[layer_of_param(p)].append(p)
     tied = "lm_head" not in layer_params and "model.embed_tokens.weight" in wmap and _tied(src_dir)
+    model_type = _config(src_dir).get("model_type", "llama")
     # deterministic order: by the (sorted) source shards each layer needs
     shard_order = {s: i for i, s in enumerate(sorted(set(wmap.values())))}
     layers = sorted(layer_params, key=lambda l: (max(shard_order[wmap[p]] for p in layer_params[l]), l))
@@ -102,7 +134,7 @@ def split_into_layers(src_dir: str, out_dir: str, verbose: bool = True) -> List[
         for p in layer_params[l]:
             sd[p] = cache[wmap[p]][p]
         assert len(sd) == len(layer_params[l]), f"Should have {len(layer_params[l])} keys for {l}"
-        save_file(sd, layer_file(out_dir, l))
+        save_file(normalize_expert_names(model_type, sd), layer_file(out_dir, l))
         written.append(l)
         if tied and l == "model.embed_tokens":
             # tie_word_embeddings checkpoints store no lm_head: give the head its own layer file so
@@ -115,9 +147,13 @@ def split_into_layers(src_dir: str, out_dir: str, verbose: bool = True) -> List[
     return written
 
 
-def _tied(src_dir: str) -> bool:
+def _config(src_dir: str) -> dict:
     try:
         with open(os.path.join(src_dir, "config.json")) as f:
-            return bool(json.load(f).get("tie_word_embeddings", False))
+            return json.load(f)
     except (OSError, ValueError):
-        return False
+        return {}
+
+
+def _tied(src_dir: str) -> bool:
+    return bool(_config(src_dir).get("tie_word_embeddings", False))

@@ -57,12 +57,21 @@ def synthetic_layer_state_dict(cfg: ModelConfig, layer_name: str, seed: int = 0,
         f"{p}.self_attn.k_proj.weight": rnd(cfg.kv_size, H),
         f"{p}.self_attn.v_proj.weight": rnd(cfg.kv_size, H),
         f"{p}.self_attn.o_proj.weight": rnd(H, cfg.q_size),
-        f"{p}.mlp.gate_proj.weight": rnd(I, H),
-        f"{p}.mlp.up_proj.weight": rnd(I, H),
-        f"{p}.mlp.down_proj.weight": rnd(H, I),
         f"{p}.input_layernorm.weight": norm_w(H),
         f"{p}.post_attention_layernorm.weight": norm_w(H),
     }
+    if cfg.is_moe:
+        from ..models.layout import expert_names, router_name
+        Ie = cfg.expert_intermediate
+        # router rows ~ N(0, 1/H): logits of unit-RMS inputs ~ N(0, 1), so tokens spread over experts
+        sd[router_name(cfg, p)] = (torch.randn(cfg.num_local_experts, H, generator=g, device=device)
+                                   * H ** -0.5).to(dtype)
+        for e in range(cfg.num_local_experts):
+            gn, un, dn = expert_names(cfg, p, e)
+            sd[gn], sd[un], sd[dn] = rnd(Ie, H), rnd(Ie, H), rnd(H, Ie)
+    else:
+        sd.update({f"{p}.mlp.gate_proj.weight": rnd(I, H), f"{p}.mlp.up_proj.weight": rnd(I, H),
+                   f"{p}.mlp.down_proj.weight": rnd(H, I)})
     return fuse_projections(cfg, p, sd) if cfg.fused_projections else sd
 
 

@@ -245,6 +245,27 @@ def _hf_family_case(tmp_path, family):
             max_position_embeddings=cfg.max_position_embeddings, original_max_position_embeddings=4096,
             rope_parameters=rs, sliding_window=cfg.sliding_window, tie_word_embeddings=False, pad_token_id=0)
         model = transformers.Phi3ForCausalLM(hf_cfg)
+    elif family == "mixtral":
+        cfg = preset("tiny-mixtral")
+        hf_cfg = transformers.MixtralConfig(
+            hidden_size=cfg.hidden_size, intermediate_size=cfg.intermediate_size,
+            num_attention_heads=cfg.num_attention_heads, num_key_value_heads=cfg.num_key_value_heads,
+            num_hidden_layers=cfg.num_hidden_layers, vocab_size=cfg.vocab_size, rms_norm_eps=cfg.rms_norm_eps,
+            rope_theta=cfg.rope_theta, max_position_embeddings=cfg.max_position_embeddings,
+            num_local_experts=cfg.num_local_experts, num_experts_per_tok=cfg.num_experts_per_tok,
+            tie_word_embeddings=False, sliding_window=None)
+        model = transformers.MixtralForCausalLM(hf_cfg)
+    elif family == "qwen3_moe":
+        cfg = preset("tiny-qwen3-moe")
+        hf_cfg = transformers.Qwen3MoeConfig(
+            hidden_size=cfg.hidden_size, intermediate_size=cfg.intermediate_size,
+            moe_intermediate_size=cfg.moe_intermediate_size, num_experts=cfg.num_local_experts,
+            num_experts_per_tok=cfg.num_experts_per_tok, norm_topk_prob=cfg.norm_topk_prob,
+            num_attention_heads=cfg.num_attention_heads, num_key_value_heads=cfg.num_key_value_heads,
+            num_hidden_layers=cfg.num_hidden_layers, vocab_size=cfg.vocab_size, rms_norm_eps=cfg.rms_norm_eps,
+            rope_theta=cfg.rope_theta, max_position_embeddings=cfg.max_position_embeddings,
+            head_dim=cfg.head_dim, tie_word_embeddings=False, use_sliding_window=False, attention_bias=False)
+        model = transformers.Qwen3MoeForCausalLM(hf_cfg)
     elif family in LLAMA_VARIANTS:
         over = dict(LLAMA_VARIANTS[family])
         cfg = preset("tiny", **over)
@@ -269,12 +290,30 @@ def _hf_family_case(tmp_path, family):
     write_synthetic_checkpoint(cfg, path, seed=5, std=0.05)
     write_synthetic_tokenizer(path, cfg.vocab_size)
     sd = load_full_state_dict(cfg, path)
-    missing, unexpected = model.float().eval().load_state_dict({k: v.float() for k, v in sd.items()}, strict=False)
+    missing, unexpected = model.float().eval().load_state_dict(
+        {k: v.float() for k, v in _hf_v5_names(cfg, sd).items()}, strict=False)
     assert not unexpected and all("rotary" in m for m in missing), (missing, unexpected)
     return path, cfg, sd, model
 
 
-@pytest.mark.parametrize("family", ["qwen2", "qwen3", "phi3", "phi3_mini", "mistral"] + sorted(LLAMA_VARIANTS))
+def _hf_v5_names(cfg, sd):
+    """Per-expert checkpoint tensors (the released form our layer files keep) -> transformers v5's
+    stacked expert parameters (``mlp.experts.gate_up_proj`` / ``down_proj``, router ``mlp.gate``)."""
+    if not cfg.is_moe:
+        return sd
+    from flexible_llm_sharding_amd.models.layout import expert_names, router_name
+    out = dict(sd)
+    for i in range(cfg.num_hidden_layers):
+        p = f"model.layers.{i}"
+        names = [expert_names(cfg, p, e) for e in range(cfg.num_local_experts)]
+        out[f"{p}.mlp.experts.gate_up_proj"] = torch.stack([torch.cat([out.pop(g), out.pop(u)]) for g, u, _ in names])
+        out[f"{p}.mlp.experts.down_proj"] = torch.stack([out.pop(d) for _, _, d in names])
+        out[f"{p}.mlp.gate.weight"] = out.pop(router_name(cfg, p))
+    return out
+
+
+@pytest.mark.parametrize("family", ["qwen2", "qwen3", "phi3", "phi3_mini", "mistral", "mixtral", "qwen3_moe"]
+                         + sorted(LLAMA_VARIANTS))
 def test_other_llama_families_match_hf(tmp_path, family):
     """Qwen2 (q/k/v biases, rope_theta 1e6), Qwen3 (per-head q/k RMSNorm, head_dim 128 on a
     256-wide residual), Phi-3 (fused qkv_proj / gate_up_proj, LongRoPE with its attention factor,
@@ -283,7 +322,8 @@ def test_other_llama_families_match_hf(tmp_path, family):
     from flexible_llm_sharding_amd.config import ModelConfig
     path, cfg, sd, model = _hf_family_case(tmp_path, family)
     assert ModelConfig.from_pretrained(path).attention_bias == (family == "qwen2")
-    assert ModelConfig.from_pretrained(path).qk_norm == (family == "qwen3")
+    assert ModelConfig.from_pretrained(path).qk_norm == (family in ("qwen3", "qwen3_moe"))
+    assert ModelConfig.from_pretrained(path).num_local_experts == cfg.num_local_experts
     tok = load_tokenizer(path)
     prompts = synthetic_prompts(3, 20, 2, 5, cfg.vocab_size, seed=9, vary=True)
     out = ShardedRunner(cfg, FileLayerSource(cfg, path), "cpu", tok, prefix_attention="causal")(prompts)
@@ -582,3 +622,25 @@ def test_grouped_attention_phase_matches(tiny_model, prune):
     assert sum(len(g["last_local"]) for g in gs) == pb.n_scored
     for g in gs:
         assert (g["work"][:, 0] >= 0).all() and (g["work"][:, 0] + g["work"][:, 1] <= g["r1"] - g["r0"]).all()
+
+
+@pytest.mark.parametrize("family", ["tiny-mixtral", "tiny-qwen3-moe"])
+def test_moe_chunks_shards_storage_match_oracle(tmp_path, family):
+    """MoE decoder layers through every engine path that reshapes the MLP phase: token chunks of
+    the expert FFN (routing per chunk), multi-layer shards, activations spilled to disk — all equal
+    the fp32 oracle of HF's MoE block."""
+    from flexible_llm_sharding_amd.config import preset
+    from flexible_llm_sharding_amd.engine import ShardedRunner
+    from flexible_llm_sharding_amd.runtime.stream import FileLayerSource
+    from flexible_llm_sharding_amd.utils.synthetic import synthetic_prompts, write_synthetic_checkpoint
+    cfg = preset(family)
+    path = str(tmp_path / family)
+    write_synthetic_checkpoint(cfg, path, seed=3, std=0.05)
+    tok = load_tokenizer(path)
+    prompts = synthetic_prompts(4, 30, 3, 6, cfg.vocab_size, seed=5, vary=True)
+    ref = reference_scores(cfg, load_full_state_dict(cfg, path), tok, prompts)
+    for kw in ({}, {"mlp_chunk": 24}, {"layer_num_per_shard": 2, "storage_location": "disk",
+                                       "disk_folder": str(tmp_path / "spill"), "token_budget": 64}):
+        out = ShardedRunner(cfg, FileLayerSource(cfg, path), "cpu", tok, **kw)(prompts)
+        for o, rf in zip(out, ref):
+            assert np.abs(o.astype(np.float32) - rf).max() < 1e-4, kw

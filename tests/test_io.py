@@ -224,3 +224,55 @@ def test_dp_slices_read_only_their_range(tiny_model):
             valid = max(0, min(nb, (rank + 1) * c) - rank * c)
             assert torch.equal(st.buffers[n][:valid], full[rank * c:rank * c + valid]), (rank, n)
     assert total == sum(full_src.plan(n).file_bytes for n in cfg.layer_names())
+
+
+@pytest.mark.parametrize("family", ["mixtral", "qwen3_moe"])
+def test_hf_moe_checkpoint_converts_and_matches(tmp_path, family):
+    """An HF MoE checkpoint (transformers save_pretrained: Mixtral's per-expert w1/w2/w3, Qwen3-MoE's
+    per-expert gate/up/down_proj) -> prepare_weights' per-layer files -> the engine == HF logits;
+    the v5 stacked in-memory form (mlp.experts.gate_up_proj) converts to the same files."""
+    transformers = pytest.importorskip("transformers")
+    import numpy as np
+    import torch
+    from flexible_llm_sharding_amd.config import ModelConfig
+    from flexible_llm_sharding_amd.engine import ShardedRunner
+    from flexible_llm_sharding_amd.utils.tokenizer import tokenize_prompt
+    from flexible_llm_sharding_amd.runtime.stream import FileLayerSource
+    from flexible_llm_sharding_amd.utils.layer_format import layer_file, normalize_expert_names
+    from flexible_llm_sharding_amd.utils.safetensors_io import load_file
+    from flexible_llm_sharding_amd.utils.synthetic import synthetic_prompts
+    from flexible_llm_sharding_amd.utils.tokenizer import load_tokenizer, write_synthetic_tokenizer
+    common = dict(hidden_size=128, intermediate_size=256, num_attention_heads=4, num_key_value_heads=2,
+                  num_hidden_layers=2, vocab_size=300, tie_word_embeddings=False, max_position_embeddings=4096)
+    torch.manual_seed(0)
+    if family == "mixtral":
+        hf = transformers.MixtralForCausalLM(transformers.MixtralConfig(num_local_experts=4, **common))
+    else:
+        hf = transformers.Qwen3MoeForCausalLM(transformers.Qwen3MoeConfig(
+            num_experts=6, num_experts_per_tok=3, moe_intermediate_size=64, norm_topk_prob=True, head_dim=32,
+            **common))
+    hf = hf.float().eval()
+    with torch.no_grad():                       # make routing non-trivial (HF inits the router to zeros)
+        for n, p in hf.named_parameters():
+            if n.endswith("mlp.gate.weight"):
+                p.normal_(0, 0.3)
+    src, out = tmp_path / "hf", tmp_path / "layers"
+    hf.save_pretrained(str(src), safe_serialization=True)
+    write_synthetic_tokenizer(str(src), common["vocab_size"])
+    split_into_layers(str(src), str(out), verbose=False)
+    cfg = ModelConfig.from_pretrained(str(out))
+    assert cfg.is_moe and cfg.model_type == family
+    # the stacked v5 state dict of layer 0 normalises to exactly the file's tensors
+    v5 = {k: v for k, v in hf.state_dict().items() if k.startswith("model.layers.0.")}
+    disk = load_file(layer_file(str(out), "model.layers.0"))
+    norm = normalize_expert_names(family, v5)
+    assert sorted(norm) == sorted(disk) and all(torch.equal(norm[k], disk[k]) for k in disk)
+    tok = load_tokenizer(str(out))
+    prompts = synthetic_prompts(2, 16, 2, 4, common["vocab_size"], seed=3, vary=True)
+    got = ShardedRunner(cfg, FileLayerSource(cfg, str(out)), "cpu", tok, prefix_attention="causal")(prompts)
+    for (prefix, sufs), o in zip(prompts, got):
+        tp = tokenize_prompt(tok, prefix, sufs)
+        for j, s in enumerate(tp.suffixes):
+            with torch.no_grad():
+                logits = hf(torch.tensor([tp.prefix + s])).logits[0, -1].float()
+            assert np.abs(o[j, 0].astype(np.float32) - torch.softmax(logits, -1).numpy()).max() < 2e-3
