@@ -256,3 +256,37 @@ def test_model_parallel_resume_after_rank_fault(deeper, tmp_path, storage):
     for a, b in zip(owner[0], ref):
         assert _close(a, b)
     assert not os.path.exists(ck) or not os.listdir(ck)   # cleared once the run completes
+
+
+@pytest.fixture(scope="module")
+def moe_single(tmp_path_factory):
+    from flexible_llm_sharding_amd.config import preset
+    from flexible_llm_sharding_amd.engine import ShardedRunner
+    from flexible_llm_sharding_amd.runtime.stream import FileLayerSource
+    from flexible_llm_sharding_amd.utils.synthetic import synthetic_prompts, write_synthetic_checkpoint
+    from flexible_llm_sharding_amd.utils.tokenizer import load_tokenizer
+    cfg = preset("tiny-mixtral", num_hidden_layers=3)
+    path = str(tmp_path_factory.mktemp("moe") / "m")
+    write_synthetic_checkpoint(cfg, path, seed=31, std=0.05)
+    prompts = synthetic_prompts(5, 25, 3, 6, cfg.vocab_size, seed=32, vary=True)
+    out = ShardedRunner(cfg, FileLayerSource(cfg, path), "cpu", load_tokenizer(path))(prompts)
+    return path, prompts, out
+
+
+@pytest.mark.parametrize("mode", ["mp", "dp_sharded"])
+def test_moe_model_parallel_and_data_parallel(moe_single, tmp_path, mode):
+    """A Mixtral-structured model (router + experts in the layer image) through the pipeline and
+    the data-parallel all-gather of 1/G byte ranges: same scores as one process."""
+    path, prompts, ref = moe_single
+    if mode == "mp":
+        mp.start_processes(_worker, args=(2, _port(), path, prompts, 1, False, "cpu", str(tmp_path), 40),
+                           nprocs=2, start_method="spawn", join=True)
+        allv = pickle.load(open(tmp_path / "out.pkl", "rb"))
+        got = [v for v in allv if v and v[0] is not None][0]
+    else:
+        mp.start_processes(_dp_shard_worker, args=(2, _port(), path, prompts, 1, str(tmp_path)),
+                           nprocs=2, start_method="spawn", join=True)
+        got = sum(pickle.load(open(tmp_path / "out.pkl", "rb")), [])
+    assert len(got) == len(ref)
+    for a, b in zip(got, ref):
+        assert _close(a, b)
