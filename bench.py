@@ -68,7 +68,8 @@ def parse(argv=None):
     ap.add_argument("--stages", default="round_robin", choices=["round_robin", "contiguous"],
                     help="--mode mp: shard k on GPU k mod N (reference) or one contiguous stage per GPU")
     ap.add_argument("--token-budget", type=int, default=49152)
-    ap.add_argument("--mlp-chunk", type=int, default=16384, help="rows per SwiGLU MLP chunk")
+    ap.add_argument("--mlp-chunk", type=int, default=None,
+                    help="rows per SwiGLU MLP chunk (default: 16384, MoE models 65536)")
     ap.add_argument("--attn-rows", type=int, default=0,
                     help="attention phase in prompt-aligned groups of <= this many rows (A/B of the --max-vram-gb layout)")
     ap.add_argument("--slots", type=int, default=None, help="HBM weight slots (default 3, 2 under --max-vram-gb; 3 prefetches across call boundaries)")

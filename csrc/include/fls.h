@@ -75,7 +75,11 @@ int fls_gemm(const void* A, const void* W, void* C, const void* R, int M, int N,
 // (every expert of a layer in one launch, optional row gather), fp16-ordered weighted combine
 int fls_moe_route(const void* logits, int ldl, int T, int E, int k, int norm, int round16, int* ids, float* w,
                   fls_stream_t s);
-int fls_moe_plan(const int* ids, int n, int k, int E, int* offs, int* tiles, int* rows, int* dest, fls_stream_t s);
+int fls_moe_router_route(const void* h, int ldh, const void* wr, int ldw, int T, int H, int E, int k, int norm,
+                         int round16, int* ids, float* w, fls_stream_t s);   // router logits fused (E <= 64)
+int fls_moe_plan_scratch(int n, int E);   // ints of the bhist scratch fls_moe_plan needs
+int fls_moe_plan(const int* ids, int n, int k, int E, int* offs, int* tiles, int* rows, int* dest, int* bhist,
+                 fls_stream_t s);
 int fls_moe_gemm(const void* A, const void* W, void* C, int M_bound, int N, int K, int lda, int ldw, int ldc, int epi,
                  const int* tiles, const int* offs, const int* rows, int n_groups, long long wstride, int a_rows,
                  fls_stream_t s);

@@ -77,7 +77,11 @@ def _load_kernels():
     _bind(lib, "fls_gemm_set_mid", c_int, c_int)
     _bind(lib, "fls_moe_route", c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
           c_void_p)
-    _bind(lib, "fls_moe_plan", c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p)
+    _bind(lib, "fls_moe_router_route", c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
+          c_int, c_void_p, c_void_p, c_void_p)
+    _bind(lib, "fls_moe_plan_scratch", c_int, c_int, c_int)
+    _bind(lib, "fls_moe_plan", c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+          c_void_p)
     _bind(lib, "fls_moe_gemm", c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
           c_void_p, c_void_p, c_void_p, c_int, ctypes.c_longlong, c_int, c_void_p)
     _bind(lib, "fls_moe_combine", c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,

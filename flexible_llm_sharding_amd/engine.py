@@ -52,6 +52,8 @@ from .utils.tokenizer import TokenizedPrompt, tokenize_prompts
 # GEMM tails and per-layer waits, +1.0-1.2% over 16k with 2 GB less device memory in use,
 # profiles/r2_budget_gen); the MLP keeps 16k-row chunks (one 43k chunk measured -1.5%).
 TOKEN_BUDGET = 49152
+MLP_CHUNK = 16384
+MOE_MLP_CHUNK = 65536
 
 
 def _parse_fault(rank: int):
@@ -71,7 +73,7 @@ class ShardedRunner:
                  prefix_attention: str = "bidirectional", token_budget: int = TOKEN_BUDGET,
                  resident: bool = False, comm: Optional[Comm] = None, data_parallel: bool = False,
                  act_dtype: Optional[torch.dtype] = None, n_slots: Optional[int] = None,
-                 mlp_chunk: int = 16384, prefetcher: Optional[ShardPrefetcher] = None,
+                 mlp_chunk: Optional[int] = None, prefetcher: Optional[ShardPrefetcher] = None,
                  verbose: bool = False, resume_dir: Optional[str] = None, checkpoint_every: int = 0,
                  max_token_len: int = MAX_TOKEN_LEN, hip_graphs: bool = False,
                  prefix_kv_cache: bool = False, prefix_cache_entries: int = 8,
@@ -102,6 +104,11 @@ class ShardedRunner:
             n_slots = 3 if (self.cuda and not resident and not max_vram_gb and prefetcher is None) else 2
         self.comm = comm or Comm(0, 1, self.dev)
         self._vram_cap = int(max_vram_gb * 1e9) if max_vram_gb else 0
+        if mlp_chunk is None:
+            # MoE: the expert GEMMs see k/E of a chunk's rows per expert, and each expert's last
+            # 256-row tile is half empty on average: larger chunks (a whole 43k-token micro-batch)
+            # keep that waste near 1% (a VRAM cap re-plans the chunk from the MoE buffer sizes)
+            mlp_chunk = MOE_MLP_CHUNK if cfg.is_moe else MLP_CHUNK
         self._plan_req = (token_budget, mlp_chunk, n_slots)
         attn_rows = qkv_chunk = 0
         self._outside = None

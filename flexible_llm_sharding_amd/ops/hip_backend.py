@@ -157,11 +157,18 @@ class HipOps:
     def moe_route(self, h, wrouter, top_k: int, norm_topk: bool, round_w16: bool = False) -> "MoeRoute":
         _f16(h, "h")
         _f16(wrouter, "router")
-        T = h.shape[0]
+        T, H = h.shape
         E = wrouter.shape[0]
         k = int(top_k)
-        logits = self.gemm(h, wrouter)                                    # [T, E] fp16 (HF Linear)
-        return self.moe_route_logits(logits, k, norm_topk, round_w16)
+        if E > 64:                                # logits by the mid-M GEMM (N = E), then routing
+            return self.moe_route_logits(self.gemm(h, wrouter), k, norm_topk, round_w16)
+        # few experts: router logits fused into the routing kernel (an N = E GEMM would be padding)
+        ids = torch.empty(T * k, dtype=torch.int32, device=h.device)
+        w = torch.empty(T * k, dtype=torch.float32, device=h.device)
+        _chk(self.k.fls_moe_router_route(h.data_ptr(), h.stride(0), wrouter.data_ptr(), wrouter.stride(0), T, H, E,
+                                         k, int(bool(norm_topk)), int(bool(round_w16)), ids.data_ptr(),
+                                         w.data_ptr(), _stream()), "fls_moe_router_route")
+        return self._moe_plan(ids, w, E, k)
 
     def moe_route_logits(self, logits, top_k: int, norm_topk: bool, round_w16: bool = False) -> "MoeRoute":
         """Routing from fp16 router logits [T, E]: top-k ids / weights per token and the stable
@@ -174,11 +181,16 @@ class HipOps:
         st = _stream()
         _chk(self.k.fls_moe_route(logits.data_ptr(), logits.stride(0), T, E, k, int(bool(norm_topk)),
                                   int(bool(round_w16)), ids.data_ptr(), w.data_ptr(), st), "fls_moe_route")
-        meta = torch.empty(2 * (E + 1) + 2 * n, dtype=torch.int32, device=dev)
-        r = MoeRoute(ids, w, meta[:E + 1], meta[E + 1:2 * (E + 1)], meta[2 * (E + 1):2 * (E + 1) + n],
-                     meta[2 * (E + 1) + n:], k)
-        _chk(self.k.fls_moe_plan(ids.data_ptr(), n, k, E, r.offs.data_ptr(), r.tiles.data_ptr(),
-                                 r.rows.data_ptr(), r.dest.data_ptr(), st), "fls_moe_plan")
+        return self._moe_plan(ids, w, E, k)
+
+    def _moe_plan(self, ids, w, E: int, k: int) -> "MoeRoute":
+        n, dev = ids.numel(), ids.device
+        scratch = self.k.fls_moe_plan_scratch(n, E)
+        meta = torch.empty(2 * (E + 1) + 2 * n + scratch, dtype=torch.int32, device=dev)
+        o = 2 * (E + 1)
+        r = MoeRoute(ids, w, meta[:E + 1], meta[E + 1:o], meta[o:o + n], meta[o + n:o + 2 * n], k)
+        _chk(self.k.fls_moe_plan(ids.data_ptr(), n, k, E, r.offs.data_ptr(), r.tiles.data_ptr(), r.rows.data_ptr(),
+                                 r.dest.data_ptr(), meta[o + 2 * n:].data_ptr(), _stream()), "fls_moe_plan")
         return r
 
     def moe_experts(self, h, x, wgu, wdown, route: "MoeRoute", m_out=None, y_out=None):

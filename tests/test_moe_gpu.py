@@ -29,7 +29,8 @@ def rnd(*shape, scale=1.0, seed=0):
 
 @pytest.mark.parametrize("T,E,k,norm,r16", [(1, 4, 2, True, False), (333, 8, 2, True, False),
                                             (1000, 128, 8, False, True), (257, 256, 8, True, False),
-                                            (64, 3, 3, True, False)])
+                                            (64, 3, 3, True, False), (3000, 8, 2, True, False),
+                                            (5000, 64, 8, True, False)])   # last two: multi-block sort
 def test_moe_route_and_plan(ops, T, E, k, norm, r16):
     """Top-k of the fp32 softmax (any tie order), renormalised / fp16-rounded weights, and the
     plan = a stable sort of the (token, slot) entries by expert."""
@@ -59,6 +60,23 @@ def test_moe_route_and_plan(ops, T, E, k, norm, r16):
     dest = torch.empty_like(order)
     dest[order] = torch.arange(order.numel())
     assert torch.equal(r.dest.cpu().long(), dest)
+
+
+@pytest.mark.parametrize("T,H,E,k", [(1, 256, 4, 2), (777, 4096, 8, 2), (130, 2048, 64, 8), (64, 256, 16, 3)])
+def test_fused_router_route(ops, T, H, E, k):
+    """E <= 64: router logits computed inside the routing kernel (fp32 sums, fp16-rounded logits) ==
+    torch's fp16 Linear + softmax + top-k, up to near-ties flipped by the summation order."""
+    h = rnd(T, H, seed=7)
+    wr = rnd(E, H, scale=H ** -0.5, seed=8)
+    r = ops.moe_route(h, wr, k, True)
+    torch.cuda.synchronize()
+    logits = (h.float() @ wr.float().t()).half().float().cpu()
+    p = torch.softmax(logits, -1)
+    top, _ = torch.topk(p, k, -1)
+    got = torch.gather(p, 1, r.ids.cpu().long().view(T, k))
+    assert torch.allclose(got, top, rtol=2e-2, atol=1e-4)
+    assert torch.allclose(r.w.cpu().view(T, k), top / top.sum(-1, keepdim=True), rtol=2e-2, atol=1e-4)
+    assert int(r.offs[-1].item()) == T * k
 
 
 def _torch_experts(h, x, wgu, wdown, ids, w, k):
