@@ -88,11 +88,12 @@ __device__ __forceinline__ unsigned pack_h2(float a, float b) {
   return __builtin_bit_cast(unsigned, __builtin_convertvector(float2_{a, b}, half2_));
 }
 
-template <int HD, int HPB, int WPH>
+template <int HD, int HPB, int WPH, bool R2>
 __global__ __launch_bounds__(64 * WPH * HPB, 2) void attn_fwd(const half_t* __restrict__ qkv, half_t* __restrict__ out,
                                                     const int* __restrict__ work, const int* __restrict__ seg_lo,
                                                     int nh, int nkv, int ld_qkv, int ld_out, float scale_log2,
-                                                    const half_t* __restrict__ kv0, int ld_kv0) {
+                                                    const half_t* __restrict__ kv0, int ld_kv0,
+                                                    const int* __restrict__ work2) {
   constexpr int NT_ = 64 * WPH * HPB;
   constexpr int NS = HD / 32;               // k-steps of QK^T
   constexpr int NU = HD / 16;               // 16-wide d subtiles of O
@@ -117,7 +118,15 @@ __global__ __launch_bounds__(64 * WPH * HPB, 2) void attn_fwd(const half_t* __re
   const int kend0 = r_len0 <= 0 ? 0 : (r_causal0 ? min(r_len0, q_off + q_len) : r_len0);
   const int kend1 = r_len1 <= 0 ? 0 : min(r_len1, q_off + q_len);
   const int n0 = (kend0 + KT - 1) / KT;
-  const int ntiles = n0 + (kend1 + KT - 1) / KT;
+  // R2: range 2 = rows [r_start2, r_start2 + r_len2) of kv0 (a suffix's cached K/V), all visible,
+  // walked between range 0 and range 1
+  int r_start2 = 0, r_len2 = 0;
+  if constexpr (R2) {
+    r_start2 = work2[blockIdx.x * 2];
+    r_len2 = max(work2[blockIdx.x * 2 + 1], 0);
+  }
+  const int n02 = n0 + (r_len2 + KT - 1) / KT;
+  const int ntiles = n02 + (kend1 + KT - 1) / KT;
 
   const int fr = lane & 15, grp = lane >> 4;
   const int k_col = nh * HD + g * HD;
@@ -131,6 +140,10 @@ __global__ __launch_bounds__(64 * WPH * HPB, 2) void attn_fwd(const half_t* __re
       const_cast<half_t*>((cache0 ? kv0 : qkv) + (size_t)r_start0 * ld0), (short)0, -1, 0x00020000);
   const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<half_t*>(qkv + (size_t)r_start1 * ld_qkv), (short)0, -1, 0x00020000);
+  __amdgpu_buffer_rsrc_t rs2 = rs0;
+  if constexpr (R2)
+    rs2 = __builtin_amdgcn_make_buffer_rsrc(const_cast<half_t*>(kv0 + (size_t)r_start2 * ld0), (short)0, -1,
+                                            0x00020000);
 
   half8 qf[2][NS];
   int qi[2], lo[2];
@@ -159,12 +172,13 @@ __global__ __launch_bounds__(64 * WPH * HPB, 2) void attn_fwd(const half_t* __re
 
   u32x4 pk[PER], pv[PER];
   auto load_tile = [&](int t) {
-    const bool r1 = t >= n0;
-    const int k0 = (r1 ? t - n0 : t) * KT;
-    const int klen = r1 ? r_len1 : r_len0;
+    const bool r1 = t >= n02;
+    const bool r2 = R2 && !r1 && t >= n0;
+    const int k0 = (r1 ? t - n02 : (r2 ? t - n0 : t)) * KT;
+    const int klen = r1 ? r_len1 : (r2 ? r_len2 : r_len0);
     const int ldk = r1 ? ld_qkv : ld0;
     const unsigned kc = (unsigned)(r1 ? k_col : kc0) * 2u, vc = (unsigned)(r1 ? v_col : vc0) * 2u;
-    const __amdgpu_buffer_rsrc_t r = r1 ? rs1 : rs0;
+    const __amdgpu_buffer_rsrc_t r = r1 ? rs1 : (r2 ? rs2 : rs0);
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int c = tid + i * NT_;
@@ -193,10 +207,11 @@ __global__ __launch_bounds__(64 * WPH * HPB, 2) void attn_fwd(const half_t* __re
   }
   __syncthreads();
   for (int t = 0; t < ntiles; ++t) {
-    const bool r1 = t >= n0;
-    const int k0 = (r1 ? t - n0 : t) * KT;
-    const int klen = r1 ? r_len1 : r_len0;
-    const bool causal = r1 || r_causal0;
+    const bool r1 = t >= n02;
+    const bool r2 = R2 && !r1 && t >= n0;
+    const int k0 = (r1 ? t - n02 : (r2 ? t - n0 : t)) * KT;
+    const int klen = r1 ? r_len1 : (r2 ? r_len2 : r_len0);
+    const bool causal = r1 || (!r2 && r_causal0);
     const char* Ks = smem + (t & 1) * TILE_BYTES;
     const char* Vs = Ks + KT * HD * 2;
 
@@ -315,12 +330,13 @@ __global__ __launch_bounds__(64 * WPH * HPB, 2) void attn_fwd(const half_t* __re
   }
 }
 
-template <int HD, int WPH>
+template <int HD, int WPH, bool R2>
 int launch(int hpb, dim3 grid, hipStream_t st, const half_t* qkv, half_t* out, const int* work, const int* seg_lo,
-           int nh, int nkv, int ld_qkv, int ld_out, float scale_log2, const half_t* kv0, int ld_kv0) {
-#define FLS_ATTN_LAUNCH(HPB_)                                                                                 \
-  hipLaunchKernelGGL((attn_fwd<HD, HPB_, WPH>), grid, dim3(64 * WPH * HPB_), 0, st, qkv, out, work, seg_lo, nh, \
-                     nkv, ld_qkv, ld_out, scale_log2, kv0, ld_kv0)
+           int nh, int nkv, int ld_qkv, int ld_out, float scale_log2, const half_t* kv0, int ld_kv0,
+           const int* work2) {
+#define FLS_ATTN_LAUNCH(HPB_)                                                                                  \
+  hipLaunchKernelGGL((attn_fwd<HD, HPB_, WPH, R2>), grid, dim3(64 * WPH * HPB_), 0, st, qkv, out, work, seg_lo, nh, \
+                     nkv, ld_qkv, ld_out, scale_log2, kv0, ld_kv0, work2)
   if constexpr (HD == 96) {
     FLS_ATTN_LAUNCH(1);                     // 12 chunks per row: one head per block divides the tile
   } else if constexpr (WPH == 2) {
@@ -348,10 +364,11 @@ extern "C" int fls_attention_set_hpb(int hpb) {
   return old;
 }
 
-extern "C" int fls_attention(const void* qkv, void* out, const int* work, int n_items, int n_q_heads,
-                             int n_kv_heads, int head_dim, int ld_qkv, int ld_out, float scale, const void* kv0,
-                             int ld_kv0, const int* seg_lo, int q_block, fls_stream_t s) {
-  if (n_items <= 0) return 0;
+namespace {
+template <bool R2>
+int dispatch(const void* qkv, void* out, const int* work, int n_items, int n_q_heads, int n_kv_heads, int head_dim,
+             int ld_qkv, int ld_out, float scale, const void* kv0, int ld_kv0, const int* seg_lo, int q_block,
+             const int* work2, fls_stream_t s) {
   if (n_q_heads % n_kv_heads) return -2;
   if (head_dim != 64 && head_dim != 96 && head_dim != 128) return -3;
   if (q_block != 64 && q_block != 128) return -5;
@@ -371,17 +388,29 @@ extern "C" int fls_attention(const void* qkv, void* out, const int* work, int n_
   auto o = (half_t*)out;
   auto k0 = (const half_t*)kv0;
   if (head_dim == 96)
-    return q_block == 64 ? launch<96, 2>(hpb, grid, st, q, o, work, seg_lo, n_q_heads, n_kv_heads, ld_qkv, ld_out,
-                                         scale_log2, k0, ld_kv0)
-                         : launch<96, 4>(hpb, grid, st, q, o, work, seg_lo, n_q_heads, n_kv_heads, ld_qkv, ld_out,
-                                         scale_log2, k0, ld_kv0);
+    return q_block == 64 ? launch<96, 2, R2>(hpb, grid, st, q, o, work, seg_lo, n_q_heads, n_kv_heads, ld_qkv, ld_out,
+                                         scale_log2, k0, ld_kv0, work2)
+                         : launch<96, 4, R2>(hpb, grid, st, q, o, work, seg_lo, n_q_heads, n_kv_heads, ld_qkv, ld_out,
+                                         scale_log2, k0, ld_kv0, work2);
   if (q_block == 64)
-    return head_dim == 128 ? launch<128, 2>(hpb, grid, st, q, o, work, seg_lo, n_q_heads, n_kv_heads, ld_qkv, ld_out,
-                                            scale_log2, k0, ld_kv0)
-                           : launch<64, 2>(hpb, grid, st, q, o, work, seg_lo, n_q_heads, n_kv_heads, ld_qkv, ld_out,
-                                           scale_log2, k0, ld_kv0);
-  return head_dim == 128 ? launch<128, 4>(hpb, grid, st, q, o, work, seg_lo, n_q_heads, n_kv_heads, ld_qkv, ld_out,
-                                          scale_log2, k0, ld_kv0)
-                         : launch<64, 4>(hpb, grid, st, q, o, work, seg_lo, n_q_heads, n_kv_heads, ld_qkv, ld_out,
-                                         scale_log2, k0, ld_kv0);
+    return head_dim == 128 ? launch<128, 2, R2>(hpb, grid, st, q, o, work, seg_lo, n_q_heads, n_kv_heads, ld_qkv, ld_out,
+                                            scale_log2, k0, ld_kv0, work2)
+                           : launch<64, 2, R2>(hpb, grid, st, q, o, work, seg_lo, n_q_heads, n_kv_heads, ld_qkv, ld_out,
+                                           scale_log2, k0, ld_kv0, work2);
+  return head_dim == 128 ? launch<128, 4, R2>(hpb, grid, st, q, o, work, seg_lo, n_q_heads, n_kv_heads, ld_qkv, ld_out,
+                                          scale_log2, k0, ld_kv0, work2)
+                         : launch<64, 4, R2>(hpb, grid, st, q, o, work, seg_lo, n_q_heads, n_kv_heads, ld_qkv, ld_out,
+                                         scale_log2, k0, ld_kv0, work2);
+}
+}  // namespace
+
+extern "C" int fls_attention(const void* qkv, void* out, const int* work, int n_items, int n_q_heads,
+                             int n_kv_heads, int head_dim, int ld_qkv, int ld_out, float scale, const void* kv0,
+                             int ld_kv0, const int* seg_lo, int q_block, const int* work2, fls_stream_t s) {
+  if (n_items <= 0) return 0;
+  if (work2 && !kv0) return -6;             // range 2 indexes the K/V cache
+  return work2 ? dispatch<true>(qkv, out, work, n_items, n_q_heads, n_kv_heads, head_dim, ld_qkv, ld_out, scale, kv0,
+                                ld_kv0, seg_lo, q_block, work2, s)
+               : dispatch<false>(qkv, out, work, n_items, n_q_heads, n_kv_heads, head_dim, ld_qkv, ld_out, scale, kv0,
+                                 ld_kv0, seg_lo, q_block, nullptr, s);
 }

@@ -76,7 +76,7 @@ class ShardedRunner:
                  mlp_chunk: Optional[int] = None, prefetcher: Optional[ShardPrefetcher] = None,
                  verbose: bool = False, resume_dir: Optional[str] = None, checkpoint_every: int = 0,
                  max_token_len: int = MAX_TOKEN_LEN, hip_graphs: bool = False,
-                 prefix_kv_cache: bool = False, prefix_cache_entries: int = 8,
+                 prefix_kv_cache: bool = False, prefix_cache_entries: int = 8, suffix_kv_cache: bool = True,
                  prune_last_layer: bool = True, pipeline_stages: str = "round_robin",
                  max_vram_gb: Optional[float] = None, hbm_cache_gb: float = 0.0, rx_window: int = 2):
         self.cfg = cfg
@@ -206,7 +206,7 @@ class ShardedRunner:
         if prefix_kv_cache and not self.hip_graphs and not resume_dir:
             from .runtime.prefix_cache import PrefixKVCache
             self.prefix_cache = PrefixKVCache(2 * cfg.num_key_value_heads * cfg.head_dim, self.dev,
-                                              self.act_dtype, prefix_cache_entries)
+                                              self.act_dtype, prefix_cache_entries, suffix_reuse=suffix_kv_cache)
         self._n_decoders = sum(1 for n in self.names if layer_kind(n) == "decoder")
         self._W_all: Dict[str, Dict[str, torch.Tensor]] = {}
         self._h2d0: Optional[int] = None     # prefetcher byte count at the start of the next call
@@ -325,9 +325,19 @@ class ShardedRunner:
         if self._vram_cap:
             self._plan_call(tps, cached)
         groups = split_microbatches(tps, self.micro_budget(tps, cached), suffix_only=cached)
+        # suffix K/V reuse (runtime/prefix_cache.py): rows of every suffix in the entry, and with a
+        # cached entry the leading tokens each suffix shares with the last call's (not recomputed)
+        sfx_rows, sfx_keep = (entry.suffix_plan(tps, reuse=cached and not self.hip_graphs)
+                              if entry is not None else (None, None))
+        if sfx_keep is not None and not any(k for ks in sfx_keep for k in ks):
+            sfx_keep = None          # nothing to reuse: keep the multi-suffix work items
+        kept = sum(k for ks in sfx_keep for k in ks) if sfx_keep is not None else 0
         batches = [pack_prompts([tps[i] for i in g], g, self.prefix_attention,
                                 prefix_offsets=[entry.offsets[i] for i in g] if entry is not None else None,
-                                kv_cached=cached, q_block=self.q_block) for g in groups]
+                                kv_cached=cached, q_block=self.q_block,
+                                suffix_rows=[sfx_rows[i] for i in g] if sfx_rows is not None else None,
+                                suffix_keep=[sfx_keep[i] for i in g] if sfx_keep is not None else None)
+                   for g in groups]
         t_pack = time.perf_counter() - t_start
         if self.hip_graphs:
             return self._run_graphed(tps, batches, t_start)
@@ -337,16 +347,20 @@ class ShardedRunner:
         except BaseException:
             if entry is not None and not cached:
                 self.prefix_cache.drop(entry)
+            elif entry is not None:
+                entry.sfx_ids.clear()        # suffix regions may hold part of this call's rows
             raise
         finally:
             self.ctx.prefix_entry = None
         if entry is not None:
             entry.complete = True
+            entry.commit_suffixes(tps, sfx_rows)
             if cached:
                 self.prefix_cache.hits += 1
             else:
                 self.prefix_cache.misses += 1
         self.stats["prefix_cached"] = float(cached)
+        self.stats["suffix_tokens_reused"] = float(kept)
         self.stats["host_pack_s"] = t_pack
         return outputs
 

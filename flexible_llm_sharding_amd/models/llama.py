@@ -254,6 +254,10 @@ def _attention_whole(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tens
         elif "pfx_src" in meta:              # full pass: keep the prefix rows' post-RoPE K/V
             pe.buffer(layer_name, create=True).index_copy_(
                 0, meta["pfx_dst"], qkv[:, qs:qs + kv].index_select(0, meta["pfx_src"]))
+        if "sfx_src" in meta:                # the suffix rows computed now (suffix K/V reuse)
+            if kv0 is None:
+                kv0 = pe.buffer(layer_name, create=True)
+            kv0.index_copy_(0, meta["sfx_dst"], qkv[:, qs:qs + kv].index_select(0, meta["sfx_src"]))
     work_items = getattr(ops, "uses_work_items", False)
     if prune:
         attn_arg = meta["work_last"] if work_items else batch.last_segments
@@ -261,8 +265,10 @@ def _attention_whole(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tens
         attn_arg = meta["work"] if work_items else batch.segments
     # work items span several suffixes of a prompt: seg_lo makes their range 1 block-diagonal
     kw = {"seg_lo": meta["seg_lo"]} if work_items else {}
-    a = ops.attention(qkv, attn_arg, cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim, kv0=kv0,
-                      q_block=batch.q_block, out=qkv[:, :cfg.q_size], **kw)
+    if work_items and "work2" in meta:       # suffix K/V reuse: range 2 = the suffix's kept rows
+        kw["work2"] = meta["work2_last"] if prune else meta["work2"]
+    a = ops.attention(qkv, attn_arg, cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim,
+                      kv0=kv0 if batch.kv_cached else None, q_block=batch.q_block, out=qkv[:, :cfg.q_size], **kw)
     del qkv
     if prune:
         idx = meta["last_idx"]

@@ -232,9 +232,11 @@ class HipOps:
 
     # ----------------------------------------------------------- attention
     def attention(self, qkv, work, n_q_heads, n_kv_heads, head_dim, kv0=None, q_block: int = 64, out=None,
-                  seg_lo=None):
+                  seg_lo=None, work2=None):
         """kv0 ([P, 2 * n_kv * hd], K then V): range 0 of every work item reads these rows (prefix cache).
-        seg_lo ([T] int32, first row of each row's suffix): work items may span several suffixes."""
+        seg_lo ([T] int32, first row of each row's suffix): work items may span several suffixes.
+        work2 ([n_items, 2] int32: r2_start, r2_len): range 2 = kv0 rows of the item's suffix cached
+        by an earlier call (suffix K/V reuse), all visible, between the prefix and the new rows."""
         _f16(qkv, "qkv")
         if work.dtype != torch.int32 or not work.is_cuda:
             raise TypeError("work items must be an int32 CUDA tensor")
@@ -247,13 +249,17 @@ class HipOps:
         # other suffixes of its item, so it is required here (the C ABI's null form is one-suffix items)
         if seg_lo is None or seg_lo.dtype != torch.int32 or not seg_lo.is_cuda or seg_lo.shape[0] < T:
             raise TypeError("seg_lo (PackedBatch.seg_lo: int32 CUDA, one row per packed token) is required")
+        if work2 is not None and (kv0 is None or work2.dtype != torch.int32 or not work2.is_cuda
+                                  or tuple(work2.shape) != (work.shape[0], 2)):
+            raise TypeError("work2 must be int32 CUDA [n_items, 2] and needs kv0")
         if out is None:
             out = torch.empty(T, n_q_heads * head_dim, dtype=torch.float16, device=qkv.device)
         rc = self.k.fls_attention(qkv.data_ptr(), out.data_ptr(), work.data_ptr(), work.shape[0],
                                   n_q_heads, n_kv_heads, head_dim, qkv.stride(0), out.stride(0),
                                   head_dim ** -0.5, kv0.data_ptr() if kv0 is not None else None,
                                   kv0.stride(0) if kv0 is not None else 0,
-                                  seg_lo.data_ptr() if seg_lo is not None else None, q_block, _stream())
+                                  seg_lo.data_ptr() if seg_lo is not None else None, q_block,
+                                  work2.data_ptr() if work2 is not None else None, _stream())
         _chk(rc, "fls_attention")
         return out
 

@@ -138,6 +138,8 @@ class TorchOps:
         for sg in segments:
             q = self._c(q_all[sg.q_start:sg.q_start + sg.q_len])                # [q, nh, d]
             kr = [(sg.r0_start, sg.r0_len, sg.r0_causal, k0_all, v0_all)]
+            if getattr(sg, "r2_len", 0):        # suffix K/V reuse: the suffix's kept rows, all visible
+                kr.append((sg.r2_start, sg.r2_len, 0, k0_all, v0_all))
             if sg.r1_len:
                 kr.append((sg.r1_start, sg.r1_len, 1, k_all, v_all))
             ks_, vs_, masks = [], [], []

@@ -51,6 +51,8 @@ class Segment:
     r1_start: int
     r1_len: int          # r1 (own suffix) is always causal
     q_off: int = 0       # index of the first query inside its segment (causal compare)
+    r2_start: int = 0    # suffix K/V reuse: rows of the K/V cache holding this suffix's earlier
+    r2_len: int = 0      # tokens (all visible), between the prefix (r0) and the new rows (r1)
 
 
 @dataclass
@@ -75,6 +77,10 @@ class PackedBatch:
     prompt_rows: Optional[np.ndarray] = None    # [n_prompts, 2] packed row range of each prompt
     prompt_items: Optional[np.ndarray] = None   # [n_prompts, 2] its range of ``work`` items
     prompt_scored: Optional[np.ndarray] = None  # [n_prompts, 2] its range of ``last_idx`` / ``work_last``
+    work2: Optional[np.ndarray] = None          # [n_items, 2] suffix K/V reuse: range 2 of each item
+    work2_last: Optional[np.ndarray] = None     # [S_total, 2] the same for ``work_last``
+    sfx_src: Optional[np.ndarray] = None        # capture: packed rows of suffix tokens ...
+    sfx_dst: Optional[np.ndarray] = None        # ... and their rows in the K/V cache
     _dev: dict = field(default_factory=dict, repr=False)
 
     @property
@@ -155,21 +161,30 @@ class PackedBatch:
                 "last_idx": torch.from_numpy(self.last_idx).to(d, non_blocking=nb),
                 "work_last": torch.from_numpy(self.work_last).to(d, non_blocking=nb),
             }
-            if self.pfx_src is not None:
-                self._dev[key]["pfx_src"] = torch.from_numpy(self.pfx_src).to(d, non_blocking=nb)
-                self._dev[key]["pfx_dst"] = torch.from_numpy(self.pfx_dst).to(d, non_blocking=nb)
+            for name in ("pfx_src", "pfx_dst", "sfx_src", "sfx_dst", "work2", "work2_last"):
+                v = getattr(self, name)
+                if v is not None:
+                    self._dev[key][name] = torch.from_numpy(v).to(d, non_blocking=nb)
         return self._dev[key]
 
 
 def pack_prompts(tps: Sequence[TokenizedPrompt], prompt_ids: Sequence[int],
                  prefix_attention: str = "bidirectional", prefix_offsets: Optional[Sequence[int]] = None,
-                 kv_cached: bool = False, q_block: int = Q_BLOCK) -> PackedBatch:
+                 kv_cached: bool = False, q_block: int = Q_BLOCK,
+                 suffix_rows: Optional[Sequence[Sequence[int]]] = None,
+                 suffix_keep: Optional[Sequence[Sequence[int]]] = None) -> PackedBatch:
     """Pack prompts into one token matrix + attention work items.
 
     ``prefix_offsets`` (rows of each prompt's prefix in a PrefixEntry) turns on
     prefix K/V reuse: with ``kv_cached`` the prefixes are NOT packed (only the
     suffix tokens are computed; range 0 of each suffix item indexes the cache),
     otherwise the batch records which packed rows to copy into the cache.
+
+    Suffix K/V reuse (``runtime/prefix_cache.py``): ``suffix_rows[j][s]`` is the cache row of
+    suffix s of prompt j (-1: not cached) — the rows computed in this call are recorded for capture
+    there — and ``suffix_keep[j][s]`` (with ``kv_cached``) the number of its leading tokens whose
+    K/V the cache already holds: only the tokens after them are packed and computed, at their true
+    positions, and each suffix gets work items of its own whose range 2 covers the kept rows.
     """
     if prefix_attention not in ("bidirectional", "causal"):
         raise ValueError(prefix_attention)
@@ -177,8 +192,10 @@ def pack_prompts(tps: Sequence[TokenizedPrompt], prompt_ids: Sequence[int],
         raise ValueError("kv_cached needs prefix_offsets")
     pcausal = 1 if prefix_attention == "causal" else 0
     ids, pos, segs, last, nsuf, lsegs = [], [], [], [], [], []
-    seg_lo, work = [], []
-    src, dst = [], []
+    if suffix_keep is not None and not kv_cached:
+        raise ValueError("suffix K/V reuse needs the prefix K/V cache (kv_cached)")
+    seg_lo, work, work2 = [], [], []
+    src, dst, sfx_src, sfx_dst = [], [], [], []
     p_rows, p_items, p_scored = [], [], []
     t = 0
     padded = 0
@@ -195,28 +212,43 @@ def pack_prompts(tps: Sequence[TokenizedPrompt], prompt_ids: Sequence[int],
             segs.append(Segment(p0, Lp, p0, Lp, pcausal, 0, 0))
             seg_lo.extend([p0] * Lp)
             work.extend(_items(segs[-1], q_block))
+            work2.extend([(0, 0)] * (len(work) - len(work2)))
             if prefix_offsets is not None:
                 src.extend(range(t, t + Lp))
                 dst.extend(range(prefix_offsets[j], prefix_offsets[j] + Lp))
             t += Lp
         sfx0 = t
-        for s in tp.suffixes:
-            n = len(s)
+        keep = suffix_keep[j] if suffix_keep is not None else None
+        for si, s in enumerate(tp.suffixes):
+            c = keep[si] if keep is not None else 0
+            c0_row = suffix_rows[j][si] if suffix_rows is not None else -1
+            n = len(s) - c
             s0 = t
-            ids.extend(s)
-            pos.extend(range(Lp, Lp + n))
+            ids.extend(s[c:])
+            pos.extend(range(Lp + c, Lp + c + n))
             seg_lo.extend([s0] * n)
-            segs.append(Segment(s0, n, p0, Lp, 0, s0, n))
+            r2s, r2l = (c0_row, c) if c else (0, 0)
+            segs.append(Segment(s0, n, p0, Lp, 0, s0, n, r2_start=r2s, r2_len=r2l))
             last.append(s0 + n - 1)
             # the scored row alone, for a last decoder layer that computes only scored rows
-            lsegs.append(Segment(s0 + n - 1, 1, p0, Lp, 0, s0, n, q_off=n - 1))
+            lsegs.append(Segment(s0 + n - 1, 1, p0, Lp, 0, s0, n, q_off=n - 1, r2_start=r2s, r2_len=r2l))
+            if c0_row >= 0:
+                sfx_src.extend(range(s0, s0 + n))
+                sfx_dst.extend(range(c0_row + c, c0_row + c + n))
+            if keep is not None:
+                # suffix K/V reuse: items of this suffix only (range 2 is per suffix)
+                for c0 in range(s0, s0 + n, q_block):
+                    c1 = min(c0 + q_block, s0 + n)
+                    work.append((c0, c1 - c0, c0 - s0, p0, Lp, 0, s0, c1 - s0))
+                    work2.append((r2s, r2l))
             t += n
         # the prompt's suffix rows [sfx0, t) in q_block chunks; range 1 of a chunk starts at the
         # suffix holding its first row
-        for c0 in range(sfx0, t, q_block):
+        for c0 in (range(sfx0, t, q_block) if keep is None else ()):
             c1 = min(c0 + q_block, t)
             r1 = seg_lo[c0]
             work.append((c0, c1 - c0, c0 - r1, p0, Lp, 0, r1, c1 - r1))
+            work2.append((0, 0))
         max_pos = max(max_pos, Lp + max([len(s) for s in tp.suffixes] or [0]))
         p_rows.append((row0, t))
         p_items.append((item0, len(work)))
@@ -224,6 +256,7 @@ def pack_prompts(tps: Sequence[TokenizedPrompt], prompt_ids: Sequence[int],
         nsuf.append(tp.n_suffix)
         padded += tp.padded_tokens
     work = np.asarray(work, dtype=np.int32).reshape(-1, WORK_ITEM_FIELDS)
+    reuse = suffix_keep is not None
     return PackedBatch(
         prompt_ids=list(prompt_ids), n_suffix=nsuf,
         ids=np.asarray(ids, dtype=np.int32), positions=np.asarray(pos, dtype=np.int32),
@@ -235,7 +268,12 @@ def pack_prompts(tps: Sequence[TokenizedPrompt], prompt_ids: Sequence[int],
         pfx_dst=np.asarray(dst, dtype=np.int64) if (prefix_offsets is not None and not kv_cached) else None,
         prompt_rows=np.asarray(p_rows, dtype=np.int64).reshape(-1, 2),
         prompt_items=np.asarray(p_items, dtype=np.int64).reshape(-1, 2),
-        prompt_scored=np.asarray(p_scored, dtype=np.int64).reshape(-1, 2))
+        prompt_scored=np.asarray(p_scored, dtype=np.int64).reshape(-1, 2),
+        work2=np.asarray(work2, dtype=np.int32).reshape(-1, 2) if reuse else None,
+        work2_last=(np.asarray([(sg.r2_start, sg.r2_len) for sg in lsegs], dtype=np.int32).reshape(-1, 2)
+                    if reuse else None),
+        sfx_src=np.asarray(sfx_src, dtype=np.int64) if sfx_src else None,
+        sfx_dst=np.asarray(sfx_dst, dtype=np.int64) if sfx_dst else None)
 
 
 def _items(sg: Segment, q_block: int = Q_BLOCK) -> List[tuple]:
@@ -251,15 +289,18 @@ def _work_items(segs: Sequence[Segment], q_block: int = Q_BLOCK) -> np.ndarray:
     return np.asarray(work, dtype=np.int32).reshape(-1, WORK_ITEM_FIELDS)
 
 
-def visible_keys(work: np.ndarray, seg_lo: Optional[np.ndarray], row: int) -> List[tuple]:
+def visible_keys(work: np.ndarray, seg_lo: Optional[np.ndarray], row: int,
+                 work2: Optional[np.ndarray] = None) -> List[tuple]:
     """(range, first key row, last key row) visible to packed query ``row`` under the work items:
     the semantics of the attention kernel (csrc/kernels/attention.hip), for host-side tests."""
-    for q_start, q_len, q_off, r0s, r0l, r0c, r1s, r1l in work.tolist():
+    for it, (q_start, q_len, q_off, r0s, r0l, r0c, r1s, r1l) in enumerate(work.tolist()):
         if q_start <= row < q_start + q_len:
             qi = q_off + row - q_start
             out = []
             if r0l > 0:
                 out.append((0, r0s, r0s + (min(r0l - 1, qi) if r0c else r0l - 1)))
+            if work2 is not None and work2[it, 1] > 0:
+                out.append((2, int(work2[it, 0]), int(work2[it, 0] + work2[it, 1] - 1)))
             if r1l > 0:
                 lo = (int(seg_lo[row]) - r1s) if seg_lo is not None else 0
                 out.append((1, r1s + lo, r1s + min(r1l - 1, qi)))

@@ -18,6 +18,19 @@ rows are the values the full pass computed), so the feature changes cost,
 not semantics.  Entries are LRU-evicted by count; the engine only switches
 to the cached path when EVERY rank holds a complete entry (model parallel
 ranks must pack identical batches).
+
+Suffix K/V reuse (``--suffix_kv_cache``, on with the prefix cache): each entry also
+holds, after the prefixes, a region per (prompt, suffix) with the post-RoPE K/V of that
+suffix's tokens from the last call, and their token ids.  A generation step appends
+``decode(new tokens)`` to every suffix and re-tokenizes it (``main.py:87-90``): the
+longest common token prefix with the cached ids has the same K/V (causal rows depend
+only on the prefix and earlier suffix tokens), so only the tokens after it are packed
+and computed; their attention reads the kept rows as range 2
+(``csrc/kernels/attention.hip``).  At least the scored (last) token is always
+recomputed.  A step then costs the new tokens instead of every suffix token (the
+kernels see different batch shapes than a full recompute, so results agree to
+rounding, not bitwise).  A suffix that outgrows its region is computed in full and
+not cached.
 """
 from __future__ import annotations
 
@@ -37,8 +50,17 @@ def prefix_fingerprint(tps: Sequence) -> str:
     return h.hexdigest()
 
 
+def common_prefix(a: Sequence[int], b: Sequence[int]) -> int:
+    n = min(len(a), len(b))
+    i = 0
+    while i < n and a[i] == b[i]:
+        i += 1
+    return i
+
+
 class PrefixEntry:
-    def __init__(self, key: str, prefix_lens: Sequence[int], kv_cols: int, device, dtype):
+    def __init__(self, key: str, prefix_lens: Sequence[int], kv_cols: int, device, dtype,
+                 suffix_caps: Optional[Sequence[Sequence[int]]] = None):
         self.key = key
         self.offsets: List[int] = []
         t = 0
@@ -46,6 +68,17 @@ class PrefixEntry:
             self.offsets.append(t)
             t += lp
         self.total = t
+        # suffix regions after the prefixes: rows of suffix s of prompt j, capacity, cached ids
+        self.sfx_rows: List[List[int]] = []
+        self.sfx_caps: List[List[int]] = []
+        for caps in (suffix_caps or []):
+            self.sfx_rows.append([])
+            self.sfx_caps.append(list(caps))
+            for c in caps:
+                self.sfx_rows[-1].append(t)
+                t += c
+        self.sfx_ids: Dict[tuple, tuple] = {}
+        self.rows = t
         self.kv_cols = kv_cols
         self.dev = torch.device(device)
         self.dtype = dtype
@@ -55,9 +88,42 @@ class PrefixEntry:
     def buffer(self, layer_name: str, create: bool = False) -> Optional[torch.Tensor]:
         b = self.layers.get(layer_name)
         if b is None and create:
-            b = torch.empty(max(1, self.total), self.kv_cols, dtype=self.dtype, device=self.dev)
+            b = torch.empty(max(1, self.rows), self.kv_cols, dtype=self.dtype, device=self.dev)
             self.layers[layer_name] = b
         return b
+
+    def suffix_plan(self, tps: Sequence, reuse: bool):
+        """-> (rows, keep) for :func:`runtime.batch.pack_prompts`: the cache row of every suffix
+        that fits its region (-1 otherwise) and, with ``reuse``, how many of its leading tokens
+        the cache already holds (the common token prefix with the last call, less the scored
+        token, which is always recomputed)."""
+        if not self.sfx_rows:
+            return None, None
+        rows, keep = [], []
+        for j, tp in enumerate(tps):
+            r, k = [], []
+            for si, s in enumerate(tp.suffixes):
+                if j >= len(self.sfx_rows) or si >= len(self.sfx_rows[j]) or len(s) > self.sfx_caps[j][si]:
+                    r.append(-1)
+                    k.append(0)
+                    continue
+                r.append(self.sfx_rows[j][si])
+                old = self.sfx_ids.get((j, si))
+                k.append(min(common_prefix(old, s), len(s) - 1) if (reuse and old) else 0)
+            rows.append(r)
+            keep.append(k)
+        return rows, (keep if reuse else None)
+
+    def commit_suffixes(self, tps: Sequence, rows) -> None:
+        """After a completed call: the cache regions hold exactly these suffixes' K/V."""
+        if rows is None:
+            return
+        for j, tp in enumerate(tps):
+            for si, s in enumerate(tp.suffixes):
+                if rows[j][si] >= 0:
+                    self.sfx_ids[(j, si)] = tuple(s)
+                else:
+                    self.sfx_ids.pop((j, si), None)
 
     @property
     def nbytes(self) -> int:
@@ -65,7 +131,12 @@ class PrefixEntry:
 
 
 class PrefixKVCache:
-    def __init__(self, kv_cols: int, device, dtype=torch.float16, max_entries: int = 8):
+    # suffix region per (prompt, suffix): its first call's length + this many tokens of growth
+    SUFFIX_GROWTH = 64
+
+    def __init__(self, kv_cols: int, device, dtype=torch.float16, max_entries: int = 8,
+                 suffix_reuse: bool = True):
+        self.suffix_reuse = suffix_reuse
         self.kv_cols = kv_cols
         self.dev = torch.device(device)
         self.dtype = dtype
@@ -87,7 +158,8 @@ class PrefixKVCache:
         self.entries.pop(key, None)
         while len(self.entries) >= self.max_entries:
             self.entries.popitem(last=False)
-        e = PrefixEntry(key, [len(tp.prefix) for tp in tps], self.kv_cols, self.dev, self.dtype)
+        caps = ([[len(s) + self.SUFFIX_GROWTH for s in tp.suffixes] for tp in tps] if self.suffix_reuse else None)
+        e = PrefixEntry(key, [len(tp.prefix) for tp in tps], self.kv_cols, self.dev, self.dtype, caps)
         self.entries[key] = e
         return e
 

@@ -397,21 +397,29 @@ def test_prefix_kv_cache_generation_exact(tiny_model, num_batch_calls):
     src = HostStore.from_model_path(cfg, path, pinned=False)
     args = argparse.Namespace(num_gen_token=3, data_parallel=False, num_batch=num_batch_calls)
     plain = ShardedRunner(cfg, src, "cpu", tok, layer_num_per_shard=2, token_budget=150)
-    cached = ShardedRunner(cfg, src, "cpu", tok, layer_num_per_shard=2, token_budget=150, prefix_kv_cache=True)
     s0, u0 = generation_loop(args, plain, Comm(), tok, prompts)
-    s1, u1 = generation_loop(args, cached, Comm(), tok, prompts)
-    assert u0 == u1
-    for a, b in zip(s0, s1):
-        assert a.shape == b.shape
-        assert np.abs(a.astype(np.float32) - b.astype(np.float32)).max() < 1e-5
-    pc = cached.prefix_cache
-    assert pc.misses == num_batch_calls and pc.hits == 2 * num_batch_calls
-    assert cached.stats["prefix_cached"] == 1.0
-    # the cached pass computed only the suffix tokens of the last call's prompts
     from flexible_llm_sharding_amd.api import batch_ranges
     b0, b1 = batch_ranges(len(prompts), num_batch_calls)[-1]
-    n_prefix = sum(len(tp.prefix) for tp in plain.tokenize(prompts[b0:b1]))
-    assert cached.stats["tokens"] == plain.stats["tokens"] - n_prefix
+    last = plain.tokenize(prompts[b0:b1])
+    n_prefix = sum(len(tp.prefix) for tp in last)
+    for sfx in (False, True):
+        cached = ShardedRunner(cfg, src, "cpu", tok, layer_num_per_shard=2, token_budget=150, prefix_kv_cache=True,
+                               suffix_kv_cache=sfx)
+        s1, u1 = generation_loop(args, cached, Comm(), tok, prompts)
+        assert u0 == u1
+        for a, b in zip(s0, s1):
+            assert a.shape == b.shape
+            assert np.abs(a.astype(np.float32) - b.astype(np.float32)).max() < 1e-5
+        pc = cached.prefix_cache
+        assert pc.misses == num_batch_calls and pc.hits == 2 * num_batch_calls
+        assert cached.stats["prefix_cached"] == 1.0
+        if not sfx:
+            # the cached pass computed only the suffix tokens of the last call's prompts
+            assert cached.stats["tokens"] == plain.stats["tokens"] - n_prefix
+        else:
+            # ... and with suffix K/V reuse only what each suffix gained since the last step (>= 1 each)
+            assert sum(tp.n_suffix for tp in last) <= cached.stats["tokens"] < plain.stats["tokens"] - n_prefix
+            assert cached.stats["suffix_tokens_reused"] > 0
 
 
 def test_prefix_cache_invalidated_by_new_prefix(tiny_model):
@@ -644,3 +652,54 @@ def test_moe_chunks_shards_storage_match_oracle(tmp_path, family):
         out = ShardedRunner(cfg, FileLayerSource(cfg, path), "cpu", tok, **kw)(prompts)
         for o, rf in zip(out, ref):
             assert np.abs(o.astype(np.float32) - rf).max() < 1e-4, kw
+
+
+def test_suffix_kv_reuse_partial_and_overflow(tiny_model):
+    """Suffix K/V reuse keeps only the common token prefix with the last call: suffixes edited in
+    the middle, grown past their cache region, shortened, or new ones — every call's scores equal a
+    runner without any cache."""
+    from flexible_llm_sharding_amd.engine import ShardedRunner
+    from flexible_llm_sharding_amd.runtime.prefix_cache import PrefixKVCache
+    from flexible_llm_sharding_amd.runtime.stream import FileLayerSource
+    from flexible_llm_sharding_amd.utils.synthetic import synthetic_prompts
+    from flexible_llm_sharding_amd.utils.tokenizer import load_tokenizer
+    path, cfg = tiny_model
+    tok = load_tokenizer(path)
+    base = synthetic_prompts(3, 40, 3, 8, cfg.vocab_size, seed=31, vary=True)
+    words = [p[0].split()[:30] for p in base]
+    step2 = [(pre, (sufs[0] + " " + " ".join(words[i][:2]),                     # grew by 2 words
+                    " ".join(words[i][3:6]) + sufs[1][len(sufs[1]) // 2:],      # edited in the middle
+                    sufs[2] + " " + " ".join(words[i][:28])))                   # outgrows its region
+             for i, (pre, sufs) in enumerate(base)]
+    step3 = [(pre, (sufs[0][:max(1, len(sufs[0]) // 2)],)) for pre, sufs in step2]   # shorter, fewer
+    plain = ShardedRunner(cfg, FileLayerSource(cfg, path), "cpu", tok)
+    old = PrefixKVCache.SUFFIX_GROWTH
+    PrefixKVCache.SUFFIX_GROWTH = 8
+    try:
+        r = ShardedRunner(cfg, FileLayerSource(cfg, path), "cpu", tok, prefix_kv_cache=True)
+        reused = []
+        for prompts in (base, step2, step3):
+            got, want = r(prompts), plain(prompts)
+            for a, b in zip(got, want):
+                assert np.abs(a.astype(np.float32) - b.astype(np.float32)).max() < 1e-5
+            reused.append(r.stats["suffix_tokens_reused"])
+        assert reused[0] == 0 and reused[1] > 0
+    finally:
+        PrefixKVCache.SUFFIX_GROWTH = old
+
+
+def test_pack_suffix_reuse_work_items():
+    """Packing with kept suffix rows: only the new tokens, at their true positions; each suffix's
+    items see the prefix (range 0), its kept rows (range 2) and its new rows causally (range 1)."""
+    from flexible_llm_sharding_amd.runtime.batch import pack_prompts, visible_keys
+    from flexible_llm_sharding_amd.utils.tokenizer import TokenizedPrompt
+    tp = TokenizedPrompt(prefix=list(range(10)), suffixes=[[1, 2, 3, 4], [5, 6, 7]], padded_len=4,
+                         eos_index=[3, 2])
+    b = pack_prompts([tp], [0], prefix_offsets=[0], kv_cached=True, suffix_rows=[[20, 40]],
+                     suffix_keep=[[2, 0]])
+    assert b.ids.tolist() == [3, 4, 5, 6, 7] and b.positions.tolist() == [12, 13, 10, 11, 12]
+    assert b.sfx_src.tolist() == [0, 1, 2, 3, 4] and b.sfx_dst.tolist() == [22, 23, 40, 41, 42]
+    assert b.last_idx.tolist() == [1, 4]
+    assert visible_keys(b.work, b.seg_lo, 1, b.work2) == [(0, 0, 9), (2, 20, 21), (1, 0, 1)]
+    assert visible_keys(b.work, b.seg_lo, 3, b.work2) == [(0, 0, 9), (1, 2, 3)]
+    assert b.work2_last.tolist() == [[20, 2], [0, 0]]

@@ -350,3 +350,29 @@ def test_qwen3_phi3_families_on_gpu(tmp_path, lnps, family):
     for o, rf in zip(r(prompts), ref):
         assert np.abs(o.astype(np.float32) - rf).max() < 2e-3
     r.close()
+
+
+@pytest.mark.parametrize("sfx", [False, True])
+def test_generation_suffix_kv_reuse_on_gpu(setup, sfx):
+    """Generation-like calls (every suffix grows by a few words per step) with the prefix K/V
+    cache, with and without suffix K/V reuse (range 2 of the attention kernel, only the new tokens
+    computed): every step's scores == a runner without caches, and == the fp32 oracle."""
+    path, cfg, tok, prompts, ref = setup
+    src = HostStore.from_model_path(cfg, path)
+    plain = ShardedRunner(cfg, src, "cuda:0", tok, layer_num_per_shard=2)
+    r = ShardedRunner(cfg, src, "cuda:0", tok, layer_num_per_shard=2, prefix_kv_cache=True, suffix_kv_cache=sfx)
+    sd = load_full_state_dict(cfg, path)
+    words = prompts[0][0].split()
+    for step in range(4):
+        ps = [(pre, tuple(sf + (" " + " ".join(words[:2 * step]) if step else "") for sf in sufs))
+              for pre, sufs in prompts]
+        got, want = r(ps), plain(ps)
+        for a, b in zip(got, want):
+            assert np.abs(a.astype(np.float32) - b.astype(np.float32)).max() < 2e-3
+        if step == 3:
+            for a, rf in zip(got, reference_scores(cfg, sd, tok, ps)):
+                assert np.abs(a.astype(np.float32) - rf).max() < 2e-3
+        if step:
+            assert (r.stats["suffix_tokens_reused"] > 0) == sfx
+    plain.close()
+    r.close()
