@@ -70,7 +70,9 @@ enum { FLS_EPI_NONE = 0, FLS_EPI_RESID = 1, FLS_EPI_SWIGLU = 2, FLS_EPI_ROPE = 3
 //           [maxpos, head_dim/2]
 int fls_gemm(const void* A, const void* W, void* C, const void* R, int M, int N, int K,
              int lda, int ldw, int ldc, int ldr, int epi, const int* pos, const float* cos_t,
-             const float* sin_t, int rope_cols, int head_dim, const void* bias, fls_stream_t s);
+             const float* sin_t, int rope_cols, int head_dim, const void* bias, void* ws, uint64_t ws_bytes,
+             fls_stream_t s);   // ws: device scratch for the small-M split-K path (may be null)
+int fls_gemm_set_splitk(int on);
 // mixture-of-experts FFN (csrc/kernels/moe.hip): routing, stable expert sort, grouped v10 GEMM
 // (every expert of a layer in one launch, optional row gather), fp16-ordered weighted combine
 int fls_moe_route(const void* logits, int ldl, int T, int E, int k, int norm, int round16, int* ids, float* w,

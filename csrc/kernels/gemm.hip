@@ -257,9 +257,100 @@ void launch_main(int tiles, const half_t* A, const half_t* W, half_t* C, int M, 
 }
 
 
+// ------------------------------------------------------------ split-K
+// Small M (generation steps, small calls): a 256 x 256 tile grid of a few dozen tiles leaves most
+// CUs idle and the mid-M kernel's 64-row tiles re-read every weight panel once per row tile.  Here
+// each tile's K is cut into S slices (tiles x S >= one block per CU), every block streams its slice
+// of the weight panel ONCE (the activation slice comes from L2) and writes fp32 partials
+// (gemm_nt_v10<EPI_F32>); splitk_reduce_kernel sums the S slabs in a fixed order (deterministic)
+// and applies the real epilogue (bias, residual, SwiGLU on the natural [gate; up] columns, RoPE
+// with the partner column d + hd/2 of each head).
+constexpr int SPLITK_MAX_M = 512;
+int g_splitk = 1;            // split-K path for small M on (fls_gemm_set_splitk)
+
+template <int EPI>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part, int S, long long pstride,
+                                                            int M, int N, half_t* __restrict__ C, int ldc, Epi ep) {
+  const int units = N / 4;                                   // 4 raw columns per thread
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long long)M * units) return;
+  const int m = (int)(idx / units), c = (int)(idx % units) * 4;
+  auto sum4 = [&](int col) {
+    floatx4 a = *(const floatx4*)(part + (size_t)m * N + col);
+    for (int k = 1; k < S; ++k) a += *(const floatx4*)(part + (size_t)k * pstride + (size_t)m * N + col);
+    return a;
+  };
+  auto bias4 = [&](floatx4& a, int col) {
+    if (ep.bias) {
+      const half4 b = *(const half4*)(ep.bias + col);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) a[r] += (float)b[r];
+    }
+  };
+  auto store4 = [&](const floatx4& a, int col) {
+    half4 o;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[r] = (half_t)a[r];
+    *(half4*)(C + (size_t)m * ldc + col) = o;
+  };
+  if constexpr (EPI == FLS_EPI_SWIGLU) {
+    const int I = N / 2;
+    if (c >= I) return;                                      // gate threads do both halves
+    const floatx4 g = sum4(c), u = sum4(I + c);
+    floatx4 o;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[r] = silu(g[r]) * u[r];
+    store4(o, c);
+  } else if constexpr (is_rope(EPI)) {
+    const int hd = ep.head_dim, half_hd = hd >> 1, d = c % hd;
+    if (c < ep.rope_cols && d >= half_hd) return;            // the partner thread rotates this pair
+    floatx4 a = sum4(c);
+    bias4(a, c);
+    if (c >= ep.rope_cols) {
+      store4(a, c);
+      return;
+    }
+    floatx4 b = sum4(c + half_hd);
+    bias4(b, c + half_hd);
+    const int p = ep.pos[m];
+    const floatx4 cs = *(const floatx4*)(ep.cos_t + (size_t)p * half_hd + d);
+    const floatx4 sn = *(const floatx4*)(ep.sin_t + (size_t)p * half_hd + d);
+    floatx4 y1, y2;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      y1[r] = a[r] * cs[r] - b[r] * sn[r];
+      y2[r] = b[r] * cs[r] + a[r] * sn[r];
+    }
+    store4(y1, c);
+    store4(y2, c + half_hd);
+  } else {
+    floatx4 a = sum4(c);
+    bias4(a, c);
+    if constexpr (EPI == FLS_EPI_RESID) {
+      const half4 rr = *(const half4*)(ep.R + (size_t)m * ep.ldr + c);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) a[r] += (float)rr[r];
+    }
+    store4(a, c);
+  }
+}
+
+// -> slices per tile (0: split-K not applicable / no room in the workspace)
+int splitk_slices(int M, int N, int K, size_t tiles, size_t ws_bytes) {
+  if (tiles >= 128) return 0;
+  const int nk = K / BK;
+  int best = 0;
+  for (int S = 2; S <= 32; S *= 2) {
+    if (nk % (2 * S) || (size_t)S * M * N * 4 > ws_bytes) break;
+    best = S;
+    if (tiles * S >= 256) break;                           // one block per CU reached
+  }
+  return best;
+}
+
 template <int EPI>
 int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int lda, int ldw, int ldc,
-           const Epi& ep, hipStream_t s) {
+           const Epi& ep, hipStream_t s, void* ws, size_t ws_bytes) {
   const bool mid_ok = N % mid::BNm == 0 && K % mid::BKm == 0 && lda % 8 == 0 && ldw % 8 == 0;
   const size_t tiles256 = (size_t)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   // 32-bit per-lane DMA offsets (X rows; SWIGLU up-block rows)
@@ -274,6 +365,35 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
   // the mid kernel wins below ~128 main tiles, and at M <= 64 (3/4 of every 256-row tile wasted)
   // up to 512; above that its lower L2 reuse (43 vs 128 FLOP per staged byte) costs more than the
   // idle CUs.  It is also the path for odd K-tile counts.
+  // split-K for small M: the whole weight read once, every CU streaming (see splitk_reduce_kernel)
+  const bool split_ok = g_splitk && ws && M <= SPLITK_MAX_M && N % BN == 0 && K % BK == 0 && lda % 8 == 0 &&
+                        ldw % 8 == 0 && (size_t)M * lda * 2 < (1ull << 32) && ldc % 4 == 0 &&
+                        ((uintptr_t)C & 7) == 0 && ((uintptr_t)ws & 15) == 0 &&
+                        (EPI != FLS_EPI_RESID || (ep.ldr % 4 == 0 && ((uintptr_t)ep.R & 7) == 0));
+  const int S = split_ok ? splitk_slices(M, N, K, tiles256, ws_bytes) : 0;
+  if (S >= 2 && (M > 64 || tiles256 * S >= 128)) {
+    static bool attr_f32 = false;
+    if (!attr_f32) {
+      (void)hipFuncSetAttribute((const void*)gemm_nt_v10<EPI_F32>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                2 * BUF);
+      attr_f32 = true;
+    }
+    Epi e = ep;
+    const int tiles_m = (M + BM - 1) / BM, tiles_n = N / BN;
+    e.order = g_order ? g_order : auto_order(tiles_m, tiles_n);
+    e.ksplit = S;
+    e.kslice = K / S;
+    e.part_stride = (long long)M * N;
+    float* part = (float*)ws;
+    hipLaunchKernelGGL((gemm_nt_v10<EPI_F32>), dim3((int)tiles256 * S), dim3(256), 2 * BUF, s, A, W, (half_t*)part, M,
+                       N, K / S, lda, ldw, N, e);
+    FLS_CHECK_LAUNCH();
+    const long long threads = (long long)M * (N / 4);
+    hipLaunchKernelGGL(splitk_reduce_kernel<EPI>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, part, S,
+                       e.part_stride, M, N, C, ldc, e);
+    FLS_CHECK_LAUNCH();
+    return 0;
+  }
   if (mid_ok && (!main_ok || (g_mid && (tiles256 < 128 || (M <= 64 && tiles256 < 512))))) {
     static bool attr_mid = false;
     if (!attr_mid) {
@@ -309,12 +429,19 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
 
 }  // namespace
 
-extern "C" int fls_kernels_version(void) { return 12; }
+extern "C" int fls_kernels_version(void) { return 13; }
 
 // tile order: 0 = by shape (default); g > 0: groups of g M tiles; g < 0: groups of -g N tiles (A/B, tests)
 extern "C" int fls_gemm_set_order(int order) {
   const int old = g_order;
   g_order = order;
+  return old;
+}
+
+// split-K path for small M on (1, default) or off (0; tests / A-B)
+extern "C" int fls_gemm_set_splitk(int on) {
+  const int old = g_splitk;
+  g_splitk = on ? 1 : 0;
   return old;
 }
 
@@ -327,7 +454,8 @@ extern "C" int fls_gemm_set_mid(int on) {
 
 extern "C" int fls_gemm(const void* A, const void* W, void* C, const void* R, int M, int N, int K, int lda, int ldw,
                         int ldc, int ldr, int epi, const int* pos, const float* cos_t, const float* sin_t,
-                        int rope_cols, int head_dim, const void* bias, fls_stream_t s) {
+                        int rope_cols, int head_dim, const void* bias, void* ws, uint64_t ws_bytes,
+                        fls_stream_t s) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
   if (bias && epi == FLS_EPI_SWIGLU) return -4;
   if ((epi == FLS_EPI_SWIGLU || epi == FLS_EPI_ROPE) && (N % 32)) return -2;
@@ -340,12 +468,12 @@ extern "C" int fls_gemm(const void* A, const void* W, void* C, const void* R, in
   auto c = (half_t*)C;
   auto st = (hipStream_t)s;
   switch (epi) {
-    case FLS_EPI_NONE: return launch<FLS_EPI_NONE>(a, w, c, M, N, K, lda, ldw, ldc, ep, st);
-    case FLS_EPI_RESID: return launch<FLS_EPI_RESID>(a, w, c, M, N, K, lda, ldw, ldc, ep, st);
-    case FLS_EPI_SWIGLU: return launch<FLS_EPI_SWIGLU>(a, w, c, M, N, K, lda, ldw, ldc, ep, st);
+    case FLS_EPI_NONE: return launch<FLS_EPI_NONE>(a, w, c, M, N, K, lda, ldw, ldc, ep, st, ws, ws_bytes);
+    case FLS_EPI_RESID: return launch<FLS_EPI_RESID>(a, w, c, M, N, K, lda, ldw, ldc, ep, st, ws, ws_bytes);
+    case FLS_EPI_SWIGLU: return launch<FLS_EPI_SWIGLU>(a, w, c, M, N, K, lda, ldw, ldc, ep, st, ws, ws_bytes);
     case FLS_EPI_ROPE:
-      return head_dim == 128 ? launch<FLS_EPI_ROPE>(a, w, c, M, N, K, lda, ldw, ldc, ep, st)
-                             : launch<EPI_ROPE64>(a, w, c, M, N, K, lda, ldw, ldc, ep, st);
+      return head_dim == 128 ? launch<FLS_EPI_ROPE>(a, w, c, M, N, K, lda, ldw, ldc, ep, st, ws, ws_bytes)
+                             : launch<EPI_ROPE64>(a, w, c, M, N, K, lda, ldw, ldc, ep, st, ws, ws_bytes);
   }
   return -1;
 }

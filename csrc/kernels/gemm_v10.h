@@ -16,6 +16,9 @@ constexpr int BM = 256, BN = 256, BK = 64;
 // internal epilogue code: RoPE with head_dim 64 (FLS_EPI_ROPE inside this file means head_dim 128);
 // a compile-time head dim keeps the v10 RoPE epilogue free of spills
 constexpr int EPI_ROPE64 = 4;
+// internal: split-K partial — raw fp32 accumulators of a K slice to a [S][M][N] workspace (the
+// epilogue runs in splitk_reduce_kernel, gemm.hip)
+constexpr int EPI_F32 = 6;
 constexpr bool is_rope(int epi) { return epi == FLS_EPI_ROPE || epi == EPI_ROPE64; }
 constexpr int BUF = 65536;    // one K-tile stage: X image (32 KiB) then W image (32 KiB)
 constexpr int WIMG = 32768;
@@ -37,6 +40,10 @@ struct Epi {
   const int* g_rows;
   long long g_wstride;
   int g_n;
+  // split-K (EPI_F32): K slices per tile, elements per slice, fp32 workspace elements per slice
+  int ksplit;
+  int kslice;
+  long long part_stride;
 };
 
 // SWIGLU logical row l (gate/up interleaved per 16 rows) -> physical row of [gate; up]
@@ -220,7 +227,18 @@ __device__ __forceinline__ void epilogue_rope(half_t* __restrict__ C, int ldc, i
 template <int EPI>
 __device__ __forceinline__ void epilogue_quadrant(half_t* __restrict__ C, int ldc, int M, int mrow0, int ncol0,
                                                   int grp, floatx4 (&acc)[8][8], const Epi& ep) {
-  if constexpr (EPI == FLS_EPI_ROPE) {
+  if constexpr (EPI == EPI_F32) {                    // split-K partial: fp32, ldc in floats
+    float* Cf = (float*)C;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int m = mrow0 + u * 16;
+      if (m < M) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) *(floatx4*)(Cf + (size_t)m * ldc + ncol0 + t * 16 + 4 * grp) = acc[u][t];
+      }
+    }
+    return;
+  } else if constexpr (EPI == FLS_EPI_ROPE) {
     epilogue_rope<128>(C, ldc, M, mrow0, ncol0, grp, acc, ep);
     return;
   } else if constexpr (EPI == EPI_ROPE64) {
@@ -371,6 +389,11 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_v10(const half_t* __restrict__
     const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7, loc = bid >> 3;
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
   }
+  int ks = 0;
+  if constexpr (EPI == EPI_F32) {                    // split-K: consecutive ids = the K slices of a tile
+    ks = bid % ep.ksplit;
+    bid /= ep.ksplit;
+  }
   const int tiles_m = (M + BM - 1) / BM;
   const int tiles_n = N / BN;
   const int2 tmn = tile_of(bid, tiles_m, tiles_n, ep.order);
@@ -391,6 +414,11 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_v10(const half_t* __restrict__
     Cg = C + (size_t)r0 * ldc;
     if (ep.g_rows) rows = ep.g_rows + r0;
     else Ag = A + (size_t)r0 * lda;
+  }
+  if constexpr (EPI == EPI_F32) {                    // this block's K slice; its own partial slab
+    Ag += (size_t)ks * ep.kslice;
+    Wg += (size_t)ks * ep.kslice;
+    Cg = (half_t*)((float*)C + (size_t)ks * ep.part_stride);
   }
   const int m0 = tm * BM, n0 = tn * BN;
 

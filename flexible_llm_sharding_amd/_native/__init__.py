@@ -63,7 +63,7 @@ class Piece(ctypes.Structure):
                 ("kind", ctypes.c_int32), ("pad", ctypes.c_int32)]
 
 
-KERNELS_ABI = 12   # bumped whenever a C signature in csrc/include/fls.h changes
+KERNELS_ABI = 13   # bumped whenever a C signature in csrc/include/fls.h changes
 
 
 def _load_kernels():
@@ -73,7 +73,9 @@ def _load_kernels():
         raise RuntimeError(f"{_KERNELS} is a stale build (ABI {lib.fls_kernels_version()} != {KERNELS_ABI}); "
                            "rebuild with python -m flexible_llm_sharding_amd._native.build")
     _bind(lib, "fls_gemm", c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
-          c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p)
+          c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
+          c_uint64, c_void_p)
+    _bind(lib, "fls_gemm_set_splitk", c_int, c_int)
     _bind(lib, "fls_gemm_set_mid", c_int, c_int)
     _bind(lib, "fls_moe_route", c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
           c_void_p)

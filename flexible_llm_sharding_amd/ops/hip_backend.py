@@ -20,6 +20,9 @@ from .. import _native
 from .torch_backend import fill_params
 
 EPI_NONE, EPI_RESID, EPI_SWIGLU, EPI_ROPE = 0, 1, 2, 3
+SPLITK_MAX_M = 512                 # csrc/kernels/gemm.hip SPLITK_MAX_M
+SPLITK_WS_SLICES = 8
+SPLITK_WS_BYTES = 64 << 20
 CAST_BF16, CAST_F32 = 1, 2
 
 
@@ -59,6 +62,7 @@ class HipOps:
 
     def __init__(self):
         self.k = _native.kernels()
+        self._ws = {}
 
     # ---------------------------------------------------------------- GEMM
     def gemm(self, x: torch.Tensor, w: torch.Tensor, epi: int = EPI_NONE, out: torch.Tensor = None,
@@ -74,6 +78,7 @@ class HipOps:
         if out is None:
             out = torch.empty(M, ncols, dtype=torch.float16, device=x.device)
         R = resid if resid is not None else out
+        ws = self._splitk_ws(x.device, M, N) if M <= SPLITK_MAX_M else None
         if bias is not None:
             _f16(bias, "bias")
             if bias.numel() != N or not bias.is_contiguous():
@@ -83,9 +88,25 @@ class HipOps:
                              positions.data_ptr() if positions is not None else None,
                              cos.data_ptr() if cos is not None else None,
                              sin.data_ptr() if sin is not None else None,
-                             rope_cols, head_dim, bias.data_ptr() if bias is not None else None, _stream())
+                             rope_cols, head_dim, bias.data_ptr() if bias is not None else None,
+                             ws.data_ptr() if ws is not None else None, ws.numel() if ws is not None else 0, _stream())
         _chk(rc, "fls_gemm")
         return out
+
+    def _splitk_ws(self, device, M: int, N: int):
+        """fp32 partials of the small-M split-K GEMM path (csrc/kernels/gemm.hip): one buffer per
+        ops object, sized for up to SPLITK_WS_SLICES slices of the largest M x N seen (<= 64 MB),
+        allocated on first use.  The GEMMs run on one stream in order, so they share it.  None
+        (the kernel falls back to the mid-M path) if the allocator refuses (e.g. a VRAM cap)."""
+        need = min(SPLITK_WS_BYTES, SPLITK_WS_SLICES * M * N * 4)
+        ws = self._ws.get(device)
+        if ws is None or ws.numel() < need:
+            try:
+                ws = torch.empty(need, dtype=torch.uint8, device=device)
+            except RuntimeError:
+                return self._ws.get(device)
+            self._ws[device] = ws
+        return ws
 
     def gemv_skinny(self, x, w):
         """Weight-streaming GEMV for M <= 16 rows (skinny LM head)."""

@@ -474,3 +474,49 @@ def test_attention_suffix_rows_from_cache(ops, ref, nh, nkv, hd):
     torch.cuda.synchronize()
     assert rel_err(got_ref, want) < 1e-5                 # the oracle agrees with itself across layouts
     assert rel_err(y.cpu(), want) < 5e-3
+
+
+@pytest.mark.parametrize("M", [1, 7, 64, 160, 300, 512])
+@pytest.mark.parametrize("epi", ["none_bias", "resid", "swiglu", "rope128", "rope64"])
+def test_gemm_small_m_splitk(ops, ref, M, epi):
+    """Small-M split-K path (fp32 partial slabs + reduce with the epilogue) == the fp32 reference,
+    == the non-split kernels to rounding, and bitwise reproducible."""
+    from flexible_llm_sharding_amd.config import ModelConfig
+    from flexible_llm_sharding_amd.models.llama import rope_tables
+    K, N = 2048, 1024
+    x = rnd(M, K, seed=11)
+    if epi == "swiglu":
+        w = rnd(2 * N, K, scale=0.05, seed=12)
+        run = lambda: ops.swiglu_up(x, w)                                         # noqa: E731
+        want = ref.swiglu_up(x.float().cpu(), w.float().cpu())
+    elif epi.startswith("rope"):
+        hd = int(epi[4:])
+        nh, nkv = N // hd // 2, N // hd // 4
+        n = (nh + 2 * nkv) * hd
+        w = rnd(n, K, scale=0.05, seed=13)
+        b = rnd(n, scale=0.5, seed=14)
+        cfg = ModelConfig(hidden_size=nh * hd, num_attention_heads=nh, num_key_value_heads=nkv)
+        cos, sin = rope_tables(cfg, 4096)
+        pos = torch.randint(0, 4000, (M,), dtype=torch.int32, device=DEV)
+        run = lambda: ops.qkv_rope(x, w, pos, cos.to(DEV), sin.to(DEV), nh, nkv, hd, bias=b)   # noqa: E731
+        want = ref.qkv_rope(x.float().cpu(), w.float().cpu(), pos.cpu(), cos, sin, nh, nkv, hd, bias=b.float().cpu())
+    else:
+        w = rnd(N, K, scale=0.05, seed=15)
+        r0 = rnd(M, N, seed=16)
+        b = rnd(N, scale=0.5, seed=17)
+        if epi == "resid":
+            run = lambda: ops.linear_residual(x, w, r0.clone(), bias=b)           # noqa: E731
+            want = r0.float().cpu() + x.float().cpu() @ w.float().cpu().t() + b.float().cpu()
+        else:
+            run = lambda: ops.gemm(x, w, EPI_NONE, bias=b)                         # noqa: E731
+            want = x.float().cpu() @ w.float().cpu().t() + b.float().cpu()
+    got, again = run(), run()
+    old = ops.k.fls_gemm_set_splitk(0)
+    try:
+        plain = run()
+    finally:
+        ops.k.fls_gemm_set_splitk(old)
+    torch.cuda.synchronize()
+    assert torch.equal(got, again)
+    assert rel_err(got.cpu(), want) < 3e-3
+    assert rel_err(got.cpu(), plain.cpu()) < 2e-3
