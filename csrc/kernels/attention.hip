@@ -93,7 +93,7 @@ __global__ __launch_bounds__(64 * WPH * HPB, 2) void attn_fwd(const half_t* __re
                                                     const int* __restrict__ work, const int* __restrict__ seg_lo,
                                                     int nh, int nkv, int ld_qkv, int ld_out, float scale_log2,
                                                     const half_t* __restrict__ kv0, int ld_kv0,
-                                                    const int* __restrict__ work2) {
+                                                    const int* __restrict__ work2, const int* __restrict__ r2win) {
   constexpr int NT_ = 64 * WPH * HPB;
   constexpr int NS = HD / 32;               // k-steps of QK^T
   constexpr int NU = HD / 16;               // 16-wide d subtiles of O
@@ -146,7 +146,7 @@ __global__ __launch_bounds__(64 * WPH * HPB, 2) void attn_fwd(const half_t* __re
                                             0x00020000);
 
   half8 qf[2][NS];
-  int qi[2], lo[2];
+  int qi[2], lo[2], lo2[2] = {0, 0}, hi2[2] = {0, 0};
 #pragma unroll
   for (int qg = 0; qg < 2; ++qg) {
     const int qrow = rbase + qg * 16 + fr;
@@ -156,6 +156,10 @@ __global__ __launch_bounds__(64 * WPH * HPB, 2) void attn_fwd(const half_t* __re
     for (int s = 0; s < NS; ++s) qf[qg][s] = *(const half8*)(qp + s * 32);
     qi[qg] = q_off + qrow;                  // range-1 index of this query row (causal upper bound)
     lo[qg] = seg_lo && r_len1 > 0 ? seg_lo[qr] - r_start1 : 0;   // its suffix's first range-1 key
+    if constexpr (R2) {                     // its suffix's window of range 2 (relative rows)
+      lo2[qg] = r2win[2 * qr] - r_start2;
+      hi2[qg] = r2win[2 * qr + 1] - r_start2;
+    }
   }
   // the wave's first query row bounds every causal compare from below: a tile is fully visible to
   // the whole wave iff its last key is visible to that row (range 1 with several suffixes: masked)
@@ -231,13 +235,13 @@ __global__ __launch_bounds__(64 * WPH * HPB, 2) void attn_fwd(const half_t* __re
     }
     // ---- visibility: wave-uniform fast path when every key of the tile is visible to every row
     const int vis_last = causal ? min(klen - 1, qi_min) : klen - 1;
-    if (k0 + KT - 1 > vis_last || (r1 && multi)) {
+    if (k0 + KT - 1 > vis_last || (r1 && multi) || r2) {
       asm volatile("" ::: "memory");        // keep this a branch (not per-score selects on every tile)
 #pragma unroll
       for (int qg = 0; qg < 2; ++qg) {
         // key k0 + 16tt + 4grp + r is visible iff lo_rel <= 16tt + r <= hi_rel
-        const int hi_rel = (causal ? min(klen - 1, qi[qg]) : klen - 1) - k0 - grp * 4;
-        const int lo_rel = (r1 ? lo[qg] : 0) - k0 - grp * 4;
+        const int hi_rel = (r2 ? min(klen, hi2[qg]) - 1 : (causal ? min(klen - 1, qi[qg]) : klen - 1)) - k0 - grp * 4;
+        const int lo_rel = (r1 ? lo[qg] : (r2 ? lo2[qg] : 0)) - k0 - grp * 4;
 #pragma unroll
         for (int tt = 0; tt < 4; ++tt)
 #pragma unroll
@@ -333,10 +337,10 @@ __global__ __launch_bounds__(64 * WPH * HPB, 2) void attn_fwd(const half_t* __re
 template <int HD, int WPH, bool R2>
 int launch(int hpb, dim3 grid, hipStream_t st, const half_t* qkv, half_t* out, const int* work, const int* seg_lo,
            int nh, int nkv, int ld_qkv, int ld_out, float scale_log2, const half_t* kv0, int ld_kv0,
-           const int* work2) {
+           const int* work2, const int* r2win) {
 #define FLS_ATTN_LAUNCH(HPB_)                                                                                  \
   hipLaunchKernelGGL((attn_fwd<HD, HPB_, WPH, R2>), grid, dim3(64 * WPH * HPB_), 0, st, qkv, out, work, seg_lo, nh, \
-                     nkv, ld_qkv, ld_out, scale_log2, kv0, ld_kv0, work2)
+                     nkv, ld_qkv, ld_out, scale_log2, kv0, ld_kv0, work2, r2win)
   if constexpr (HD == 96) {
     FLS_ATTN_LAUNCH(1);                     // 12 chunks per row: one head per block divides the tile
   } else if constexpr (WPH == 2) {
@@ -368,7 +372,7 @@ namespace {
 template <bool R2>
 int dispatch(const void* qkv, void* out, const int* work, int n_items, int n_q_heads, int n_kv_heads, int head_dim,
              int ld_qkv, int ld_out, float scale, const void* kv0, int ld_kv0, const int* seg_lo, int q_block,
-             const int* work2, fls_stream_t s) {
+             const int* work2, const int* r2win, fls_stream_t s) {
   if (n_q_heads % n_kv_heads) return -2;
   if (head_dim != 64 && head_dim != 96 && head_dim != 128) return -3;
   if (q_block != 64 && q_block != 128) return -5;
@@ -389,28 +393,29 @@ int dispatch(const void* qkv, void* out, const int* work, int n_items, int n_q_h
   auto k0 = (const half_t*)kv0;
   if (head_dim == 96)
     return q_block == 64 ? launch<96, 2, R2>(hpb, grid, st, q, o, work, seg_lo, n_q_heads, n_kv_heads, ld_qkv, ld_out,
-                                         scale_log2, k0, ld_kv0, work2)
+                                         scale_log2, k0, ld_kv0, work2, r2win)
                          : launch<96, 4, R2>(hpb, grid, st, q, o, work, seg_lo, n_q_heads, n_kv_heads, ld_qkv, ld_out,
-                                         scale_log2, k0, ld_kv0, work2);
+                                         scale_log2, k0, ld_kv0, work2, r2win);
   if (q_block == 64)
     return head_dim == 128 ? launch<128, 2, R2>(hpb, grid, st, q, o, work, seg_lo, n_q_heads, n_kv_heads, ld_qkv, ld_out,
-                                            scale_log2, k0, ld_kv0, work2)
+                                            scale_log2, k0, ld_kv0, work2, r2win)
                            : launch<64, 2, R2>(hpb, grid, st, q, o, work, seg_lo, n_q_heads, n_kv_heads, ld_qkv, ld_out,
-                                           scale_log2, k0, ld_kv0, work2);
+                                           scale_log2, k0, ld_kv0, work2, r2win);
   return head_dim == 128 ? launch<128, 4, R2>(hpb, grid, st, q, o, work, seg_lo, n_q_heads, n_kv_heads, ld_qkv, ld_out,
-                                          scale_log2, k0, ld_kv0, work2)
+                                          scale_log2, k0, ld_kv0, work2, r2win)
                          : launch<64, 4, R2>(hpb, grid, st, q, o, work, seg_lo, n_q_heads, n_kv_heads, ld_qkv, ld_out,
-                                         scale_log2, k0, ld_kv0, work2);
+                                         scale_log2, k0, ld_kv0, work2, r2win);
 }
 }  // namespace
 
 extern "C" int fls_attention(const void* qkv, void* out, const int* work, int n_items, int n_q_heads,
                              int n_kv_heads, int head_dim, int ld_qkv, int ld_out, float scale, const void* kv0,
-                             int ld_kv0, const int* seg_lo, int q_block, const int* work2, fls_stream_t s) {
+                             int ld_kv0, const int* seg_lo, int q_block, const int* work2, const int* r2win,
+                             fls_stream_t s) {
   if (n_items <= 0) return 0;
-  if (work2 && !kv0) return -6;             // range 2 indexes the K/V cache
+  if (work2 && (!kv0 || !r2win)) return -6;   // range 2 indexes the K/V cache, per-row windows
   return work2 ? dispatch<true>(qkv, out, work, n_items, n_q_heads, n_kv_heads, head_dim, ld_qkv, ld_out, scale, kv0,
-                                ld_kv0, seg_lo, q_block, work2, s)
+                                ld_kv0, seg_lo, q_block, work2, r2win, s)
                : dispatch<false>(qkv, out, work, n_items, n_q_heads, n_kv_heads, head_dim, ld_qkv, ld_out, scale, kv0,
-                                 ld_kv0, seg_lo, q_block, nullptr, s);
+                                 ld_kv0, seg_lo, q_block, nullptr, nullptr, s);
 }

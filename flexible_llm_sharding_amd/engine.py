@@ -126,7 +126,10 @@ class ShardedRunner:
                     pcomm = getattr(prefetcher, "comm", None)
                     if pcomm is not None and pcomm is not self.comm:
                         pcomm.warmup()
-                self._outside = device_used_bytes(self.dev) - torch.cuda.memory_reserved(self.dev) + (64 << 20)
+                # small-M split-K scratch: only if an earlier runner of this process reserved it
+                ws = get_ops(self.dev).reserve_splitk_ws(self.dev, allocate=False)
+                self._outside = (device_used_bytes(self.dev) - torch.cuda.memory_reserved(self.dev) + (64 << 20)
+                                 + ws)
             try:
                 # provisional (the call's token count is unknown yet); _plan_call is authoritative
                 token_budget, mlp_chunk, attn_rows, qkv_chunk, est = plan_for_vram(

@@ -265,8 +265,9 @@ def _attention_whole(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tens
         attn_arg = meta["work"] if work_items else batch.segments
     # work items span several suffixes of a prompt: seg_lo makes their range 1 block-diagonal
     kw = {"seg_lo": meta["seg_lo"]} if work_items else {}
-    if work_items and "work2" in meta:       # suffix K/V reuse: range 2 = the suffix's kept rows
+    if work_items and "work2" in meta:       # suffix K/V reuse: range 2 = the suffixes' kept rows
         kw["work2"] = meta["work2_last"] if prune else meta["work2"]
+        kw["r2win"] = meta["r2win"]
     a = ops.attention(qkv, attn_arg, cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim,
                       kv0=kv0 if batch.kv_cached else None, q_block=batch.q_block, out=qkv[:, :cfg.q_size], **kw)
     del qkv

@@ -21,8 +21,7 @@ from .torch_backend import fill_params
 
 EPI_NONE, EPI_RESID, EPI_SWIGLU, EPI_ROPE = 0, 1, 2, 3
 SPLITK_MAX_M = 512                 # csrc/kernels/gemm.hip SPLITK_MAX_M
-SPLITK_WS_SLICES = 8
-SPLITK_WS_BYTES = 64 << 20
+SPLITK_WS_BYTES = 64 << 20        # fp32 partial slabs: e.g. 8 slices x 160 rows x 10240 columns
 CAST_BF16, CAST_F32 = 1, 2
 
 
@@ -94,19 +93,28 @@ class HipOps:
         return out
 
     def _splitk_ws(self, device, M: int, N: int):
-        """fp32 partials of the small-M split-K GEMM path (csrc/kernels/gemm.hip): one buffer per
-        ops object, sized for up to SPLITK_WS_SLICES slices of the largest M x N seen (<= 64 MB),
-        allocated on first use.  The GEMMs run on one stream in order, so they share it.  None
-        (the kernel falls back to the mid-M path) if the allocator refuses (e.g. a VRAM cap)."""
-        need = min(SPLITK_WS_BYTES, SPLITK_WS_SLICES * M * N * 4)
-        ws = self._ws.get(device)
-        if ws is None or ws.numel() < need:
+        """fp32 partials of the small-M split-K GEMM path (csrc/kernels/gemm.hip): one fixed-size
+        buffer per device, reserved once (``reserve_splitk_ws``; the engine does it before planning
+        a VRAM cap) and never resized, so which GEMM path a shape takes — and its rounding — does not
+        depend on what the allocator could give at the time.  The GEMMs of a device run on one
+        stream in order, so they share it.  None (mid-M kernel) if it could not be reserved."""
+        if device not in self._ws:
+            self.reserve_splitk_ws(device)
+        return self._ws[device]
+
+    def reserve_splitk_ws(self, device, allocate: bool = True):
+        """Decide the device's split-K scratch once: allocate it (``allocate``) or go without (a
+        VRAM-capped runner: the 70B plan has no 64 MB to spare and its small-M GEMMs are the pruned
+        last layer's).  -> bytes reserved."""
+        device = torch.device(device)
+        if device not in self._ws:
             try:
-                ws = torch.empty(need, dtype=torch.uint8, device=device)
+                self._ws[device] = (torch.empty(SPLITK_WS_BYTES, dtype=torch.uint8, device=device)
+                                    if allocate else None)
             except RuntimeError:
-                return self._ws.get(device)
-            self._ws[device] = ws
-        return ws
+                self._ws[device] = None
+        ws = self._ws[device]
+        return 0 if ws is None else ws.numel()
 
     def gemv_skinny(self, x, w):
         """Weight-streaming GEMV for M <= 16 rows (skinny LM head)."""
@@ -253,11 +261,12 @@ class HipOps:
 
     # ----------------------------------------------------------- attention
     def attention(self, qkv, work, n_q_heads, n_kv_heads, head_dim, kv0=None, q_block: int = 64, out=None,
-                  seg_lo=None, work2=None):
+                  seg_lo=None, work2=None, r2win=None):
         """kv0 ([P, 2 * n_kv * hd], K then V): range 0 of every work item reads these rows (prefix cache).
         seg_lo ([T] int32, first row of each row's suffix): work items may span several suffixes.
-        work2 ([n_items, 2] int32: r2_start, r2_len): range 2 = kv0 rows of the item's suffix cached
-        by an earlier call (suffix K/V reuse), all visible, between the prefix and the new rows."""
+        work2 ([n_items, 2] int32: r2_start, r2_len) + r2win ([T, 2] int32: kv0 rows [lo, hi) per row):
+        range 2 = the kv0 rows of the item's suffixes cached by an earlier call (suffix K/V reuse),
+        walked between the prefix and the new rows, each row seeing its own suffix's window."""
         _f16(qkv, "qkv")
         if work.dtype != torch.int32 or not work.is_cuda:
             raise TypeError("work items must be an int32 CUDA tensor")
@@ -271,8 +280,9 @@ class HipOps:
         if seg_lo is None or seg_lo.dtype != torch.int32 or not seg_lo.is_cuda or seg_lo.shape[0] < T:
             raise TypeError("seg_lo (PackedBatch.seg_lo: int32 CUDA, one row per packed token) is required")
         if work2 is not None and (kv0 is None or work2.dtype != torch.int32 or not work2.is_cuda
-                                  or tuple(work2.shape) != (work.shape[0], 2)):
-            raise TypeError("work2 must be int32 CUDA [n_items, 2] and needs kv0")
+                                  or tuple(work2.shape) != (work.shape[0], 2) or r2win is None
+                                  or r2win.dtype != torch.int32 or r2win.shape[0] < T):
+            raise TypeError("work2 must be int32 CUDA [n_items, 2] with r2win [T, 2] and kv0")
         if out is None:
             out = torch.empty(T, n_q_heads * head_dim, dtype=torch.float16, device=qkv.device)
         rc = self.k.fls_attention(qkv.data_ptr(), out.data_ptr(), work.data_ptr(), work.shape[0],
@@ -280,7 +290,8 @@ class HipOps:
                                   head_dim ** -0.5, kv0.data_ptr() if kv0 is not None else None,
                                   kv0.stride(0) if kv0 is not None else 0,
                                   seg_lo.data_ptr() if seg_lo is not None else None, q_block,
-                                  work2.data_ptr() if work2 is not None else None, _stream())
+                                  work2.data_ptr() if work2 is not None else None,
+                                  r2win.data_ptr() if work2 is not None else None, _stream())
         _chk(rc, "fls_attention")
         return out
 

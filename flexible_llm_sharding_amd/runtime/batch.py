@@ -78,6 +78,7 @@ class PackedBatch:
     prompt_items: Optional[np.ndarray] = None   # [n_prompts, 2] its range of ``work`` items
     prompt_scored: Optional[np.ndarray] = None  # [n_prompts, 2] its range of ``last_idx`` / ``work_last``
     work2: Optional[np.ndarray] = None          # [n_items, 2] suffix K/V reuse: range 2 of each item
+    r2win: Optional[np.ndarray] = None          # [T, 2] the cache rows [lo, hi) of range 2 each row sees
     work2_last: Optional[np.ndarray] = None     # [S_total, 2] the same for ``work_last``
     sfx_src: Optional[np.ndarray] = None        # capture: packed rows of suffix tokens ...
     sfx_dst: Optional[np.ndarray] = None        # ... and their rows in the K/V cache
@@ -161,7 +162,7 @@ class PackedBatch:
                 "last_idx": torch.from_numpy(self.last_idx).to(d, non_blocking=nb),
                 "work_last": torch.from_numpy(self.work_last).to(d, non_blocking=nb),
             }
-            for name in ("pfx_src", "pfx_dst", "sfx_src", "sfx_dst", "work2", "work2_last"):
+            for name in ("pfx_src", "pfx_dst", "sfx_src", "sfx_dst", "work2", "work2_last", "r2win"):
                 v = getattr(self, name)
                 if v is not None:
                     self._dev[key][name] = torch.from_numpy(v).to(d, non_blocking=nb)
@@ -194,7 +195,7 @@ def pack_prompts(tps: Sequence[TokenizedPrompt], prompt_ids: Sequence[int],
     ids, pos, segs, last, nsuf, lsegs = [], [], [], [], [], []
     if suffix_keep is not None and not kv_cached:
         raise ValueError("suffix K/V reuse needs the prefix K/V cache (kv_cached)")
-    seg_lo, work, work2 = [], [], []
+    seg_lo, work, work2, r2win = [], [], [], []
     src, dst, sfx_src, sfx_dst = [], [], [], []
     p_rows, p_items, p_scored = [], [], []
     t = 0
@@ -213,6 +214,7 @@ def pack_prompts(tps: Sequence[TokenizedPrompt], prompt_ids: Sequence[int],
             seg_lo.extend([p0] * Lp)
             work.extend(_items(segs[-1], q_block))
             work2.extend([(0, 0)] * (len(work) - len(work2)))
+            r2win.extend([(0, 0)] * Lp)
             if prefix_offsets is not None:
                 src.extend(range(t, t + Lp))
                 dst.extend(range(prefix_offsets[j], prefix_offsets[j] + Lp))
@@ -235,20 +237,18 @@ def pack_prompts(tps: Sequence[TokenizedPrompt], prompt_ids: Sequence[int],
             if c0_row >= 0:
                 sfx_src.extend(range(s0, s0 + n))
                 sfx_dst.extend(range(c0_row + c, c0_row + c + n))
-            if keep is not None:
-                # suffix K/V reuse: items of this suffix only (range 2 is per suffix)
-                for c0 in range(s0, s0 + n, q_block):
-                    c1 = min(c0 + q_block, s0 + n)
-                    work.append((c0, c1 - c0, c0 - s0, p0, Lp, 0, s0, c1 - s0))
-                    work2.append((r2s, r2l))
+            r2win.extend([(r2s, r2s + r2l)] * n)
             t += n
         # the prompt's suffix rows [sfx0, t) in q_block chunks; range 1 of a chunk starts at the
-        # suffix holding its first row
-        for c0 in (range(sfx0, t, q_block) if keep is None else ()):
+        # suffix holding its first row.  Suffix K/V reuse: range 2 of every chunk spans the kept
+        # rows of all the prompt's suffixes, each row seeing only its own suffix's window (r2win)
+        w = [(a, b) for a, b in r2win[sfx0:t] if b > a]
+        r2 = (min(a for a, _ in w), max(b for _, b in w)) if w else (0, 0)
+        for c0 in range(sfx0, t, q_block):
             c1 = min(c0 + q_block, t)
             r1 = seg_lo[c0]
             work.append((c0, c1 - c0, c0 - r1, p0, Lp, 0, r1, c1 - r1))
-            work2.append((0, 0))
+            work2.append((r2[0], r2[1] - r2[0]))
         max_pos = max(max_pos, Lp + max([len(s) for s in tp.suffixes] or [0]))
         p_rows.append((row0, t))
         p_items.append((item0, len(work)))
@@ -270,6 +270,7 @@ def pack_prompts(tps: Sequence[TokenizedPrompt], prompt_ids: Sequence[int],
         prompt_items=np.asarray(p_items, dtype=np.int64).reshape(-1, 2),
         prompt_scored=np.asarray(p_scored, dtype=np.int64).reshape(-1, 2),
         work2=np.asarray(work2, dtype=np.int32).reshape(-1, 2) if reuse else None,
+        r2win=np.asarray(r2win, dtype=np.int32).reshape(-1, 2) if reuse else None,
         work2_last=(np.asarray([(sg.r2_start, sg.r2_len) for sg in lsegs], dtype=np.int32).reshape(-1, 2)
                     if reuse else None),
         sfx_src=np.asarray(sfx_src, dtype=np.int64) if sfx_src else None,
@@ -290,7 +291,7 @@ def _work_items(segs: Sequence[Segment], q_block: int = Q_BLOCK) -> np.ndarray:
 
 
 def visible_keys(work: np.ndarray, seg_lo: Optional[np.ndarray], row: int,
-                 work2: Optional[np.ndarray] = None) -> List[tuple]:
+                 work2: Optional[np.ndarray] = None, r2win: Optional[np.ndarray] = None) -> List[tuple]:
     """(range, first key row, last key row) visible to packed query ``row`` under the work items:
     the semantics of the attention kernel (csrc/kernels/attention.hip), for host-side tests."""
     for it, (q_start, q_len, q_off, r0s, r0l, r0c, r1s, r1l) in enumerate(work.tolist()):
@@ -300,7 +301,11 @@ def visible_keys(work: np.ndarray, seg_lo: Optional[np.ndarray], row: int,
             if r0l > 0:
                 out.append((0, r0s, r0s + (min(r0l - 1, qi) if r0c else r0l - 1)))
             if work2 is not None and work2[it, 1] > 0:
-                out.append((2, int(work2[it, 0]), int(work2[it, 0] + work2[it, 1] - 1)))
+                lo, hi = int(work2[it, 0]), int(work2[it, 0] + work2[it, 1])
+                if r2win is not None:
+                    lo, hi = max(lo, int(r2win[row, 0])), min(hi, int(r2win[row, 1]))
+                if hi > lo:
+                    out.append((2, lo, hi - 1))
             if r1l > 0:
                 lo = (int(seg_lo[row]) - r1s) if seg_lo is not None else 0
                 out.append((1, r1s + lo, r1s + min(r1l - 1, qi)))

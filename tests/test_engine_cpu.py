@@ -700,6 +700,8 @@ def test_pack_suffix_reuse_work_items():
     assert b.ids.tolist() == [3, 4, 5, 6, 7] and b.positions.tolist() == [12, 13, 10, 11, 12]
     assert b.sfx_src.tolist() == [0, 1, 2, 3, 4] and b.sfx_dst.tolist() == [22, 23, 40, 41, 42]
     assert b.last_idx.tolist() == [1, 4]
-    assert visible_keys(b.work, b.seg_lo, 1, b.work2) == [(0, 0, 9), (2, 20, 21), (1, 0, 1)]
-    assert visible_keys(b.work, b.seg_lo, 3, b.work2) == [(0, 0, 9), (1, 2, 3)]
+    assert b.r2win.tolist() == [[20, 22], [20, 22], [0, 0], [0, 0], [0, 0]]
+    assert b.work.shape[0] == 1 and b.work2.tolist() == [[20, 2]]          # one item for both suffixes
+    assert visible_keys(b.work, b.seg_lo, 1, b.work2, b.r2win) == [(0, 0, 9), (2, 20, 21), (1, 0, 1)]
+    assert visible_keys(b.work, b.seg_lo, 3, b.work2, b.r2win) == [(0, 0, 9), (1, 2, 3)]
     assert b.work2_last.tolist() == [[20, 2], [0, 0]]

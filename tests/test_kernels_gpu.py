@@ -468,7 +468,7 @@ def test_attention_suffix_rows_from_cache(ops, ref, nh, nkv, hd):
     qkv_new = qkv[sel].contiguous()
     m = reuse.device_tensors(DEV)
     y = ops.attention(qkv_new.to(DEV), m["work"], nh, nkv, hd, kv0=cache.to(DEV), seg_lo=m["seg_lo"],
-                      work2=m["work2"])
+                      work2=m["work2"], r2win=m["r2win"])
     want = ref.attention(qkv.float(), full.segments, nh, nkv, hd)[sel]
     got_ref = ref.attention(qkv_new.float(), reuse.segments, nh, nkv, hd, kv0=cache.float())
     torch.cuda.synchronize()
