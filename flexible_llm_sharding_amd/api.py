@@ -232,18 +232,26 @@ def generation_loop(args, runner, comm: Comm, tok, original_prompts: Sequence, s
     cache and the HBM weight cache, on by default for repeated passes, make the later passes
     cheaper; the scores are the same).  ``step_times`` collects each step's wall time."""
     input_prompts = copy.deepcopy(list(original_prompts))
-    output_scores: List[np.ndarray] = []
+    # per prompt: every step's [n_s, 1, V] scores and argmax tokens.  The reference concatenates the
+    # scores each step and takes the argmax over all of them (main.py:83-88); the argmax of the
+    # earlier steps cannot change, so each step's is taken once, and the scores are concatenated
+    # once at the end — same tokens, same output
+    step_scores: List[List[np.ndarray]] = []
+    step_tokens: List[List[np.ndarray]] = []
     for i_new in range(args.num_gen_token):
         t_step = time.perf_counter()
         outputs = run_all(args, runner, comm, input_prompts)
         if comm.rank == 0:
             if i_new == 0:
-                output_scores = outputs
+                step_scores = [[o] for o in outputs]
+                step_tokens = [[greedy_tokens(o)] for o in outputs]
             else:
-                output_scores = [np.concatenate((old, new), axis=1) for old, new in zip(output_scores, outputs)]
+                for pi, o in enumerate(outputs):
+                    step_scores[pi].append(o)
+                    step_tokens[pi].append(greedy_tokens(o))
             for pi in range(len(input_prompts)):
                 prefix, suffix = original_prompts[pi]
-                new_tokens = np.argmax(output_scores[pi], axis=-1)
+                new_tokens = np.concatenate(step_tokens[pi], axis=1)
                 new_suffix = tuple(s + tok.decode(t) for s, t in zip(suffix, new_tokens))
                 input_prompts[pi] = (prefix, new_suffix)
         if comm.world > 1:
@@ -252,7 +260,19 @@ def generation_loop(args, runner, comm: Comm, tok, original_prompts: Sequence, s
             step_times.append(time.perf_counter() - t_step)
         if getattr(args, "verbose", False) and comm.rank == 0:
             print(f"step {i_new}: {time.perf_counter() - t_step:.3f}s", flush=True)
+    output_scores = [ss[0] if len(ss) == 1 else np.concatenate(ss, axis=1) for ss in step_scores]
     return output_scores, input_prompts
+
+
+def greedy_tokens(scores: np.ndarray) -> np.ndarray:
+    """np.argmax(scores, axis=-1) (first index on ties).  fp16 probabilities are >= 0, whose bit
+    patterns order like their values: the argmax runs on the uint16 view (numpy has no fast fp16
+    compare: ~30x faster at [160, 1, 32000])."""
+    if scores.dtype == np.float16:
+        bits = scores.view(np.uint16)
+        if not (bits >= 0x8000).any():
+            return np.argmax(bits, axis=-1)
+    return np.argmax(scores, axis=-1)
 
 
 def _device_for(args, comm: Comm) -> torch.device:

@@ -223,3 +223,18 @@ def test_repeated_pass_defaults():
     cfg = preset("tiny")
     assert resolve_hbm_cache_gb(g, cfg, torch.device("cpu")) == 0.0       # nothing to cache on a CPU run
     assert resolve_hbm_cache_gb(parse_args(base + ["--hbm_cache_gb", "3"]), cfg, torch.device("cpu")) == 3.0
+
+
+def test_greedy_tokens_equal_numpy_argmax():
+    """Generation's argmax on the fp16 bit patterns == np.argmax, ties (first index) included."""
+    import numpy as np
+    from flexible_llm_sharding_amd.api import greedy_tokens
+    rng = np.random.default_rng(0)
+    a = rng.random((7, 3, 1000)).astype(np.float16)
+    a[0, 0, 10] = a[0, 0, 20] = 2.0                      # tie: first index wins
+    a[1, 1] = 0.0
+    assert np.array_equal(greedy_tokens(a), np.argmax(a, axis=-1))
+    b = a.copy()
+    b[2, 2, 5] = -1.0                                     # a negative value: generic path
+    assert np.array_equal(greedy_tokens(b), np.argmax(b, axis=-1))
+    assert np.array_equal(greedy_tokens(a.astype(np.float32)), np.argmax(a, axis=-1))
