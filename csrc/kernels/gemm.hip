@@ -267,6 +267,7 @@ void launch_main(int tiles, const half_t* A, const half_t* W, half_t* C, int M, 
 // with the partner column d + hd/2 of each head).
 constexpr int SPLITK_MAX_M = 512;
 int g_splitk = 1;            // split-K path for small M on (fls_gemm_set_splitk)
+int g_gu_split = 1;          // SwiGLU GEMM in this many column launches (fls_gemm_set_gu_split; A/B)
 
 template <int EPI>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part, int S, long long pstride,
@@ -445,6 +446,13 @@ extern "C" int fls_gemm_set_splitk(int on) {
   return old;
 }
 
+// SwiGLU GEMM as P launches over the intermediate columns (1 = one launch, default)
+extern "C" int fls_gemm_set_gu_split(int p) {
+  const int old = g_gu_split;
+  g_gu_split = p > 0 ? p : 1;
+  return old;
+}
+
 // mid-M kernel for small grids on (1, default) or off (0; tests)
 extern "C" int fls_gemm_set_mid(int on) {
   const int old = g_mid;
@@ -470,7 +478,20 @@ extern "C" int fls_gemm(const void* A, const void* W, void* C, const void* R, in
   switch (epi) {
     case FLS_EPI_NONE: return launch<FLS_EPI_NONE>(a, w, c, M, N, K, lda, ldw, ldc, ep, st, ws, ws_bytes);
     case FLS_EPI_RESID: return launch<FLS_EPI_RESID>(a, w, c, M, N, K, lda, ldw, ldc, ep, st, ws, ws_bytes);
-    case FLS_EPI_SWIGLU: return launch<FLS_EPI_SWIGLU>(a, w, c, M, N, K, lda, ldw, ldc, ep, st, ws, ws_bytes);
+    case FLS_EPI_SWIGLU: {
+      // optional: the intermediate columns in g_gu_split launches (gate rows [j I/P, (j+1) I/P) and
+      // the matching up rows; gu_rows stays I), a smaller N-tile grid per launch (A/B knob)
+      const int I = N / 2, P = g_gu_split;
+      if (P > 1 && I % (P * BN / 2) == 0 && M > SPLITK_MAX_M) {
+        for (int j = 0; j < P; ++j) {
+          const int rc = launch<FLS_EPI_SWIGLU>(a, w + (size_t)j * (I / P) * ldw, c + (size_t)j * (I / P), M, N / P, K,
+                                                lda, ldw, ldc, ep, st, ws, ws_bytes);
+          if (rc) return rc;
+        }
+        return 0;
+      }
+      return launch<FLS_EPI_SWIGLU>(a, w, c, M, N, K, lda, ldw, ldc, ep, st, ws, ws_bytes);
+    }
     case FLS_EPI_ROPE:
       return head_dim == 128 ? launch<FLS_EPI_ROPE>(a, w, c, M, N, K, lda, ldw, ldc, ep, st, ws, ws_bytes)
                              : launch<EPI_ROPE64>(a, w, c, M, N, K, lda, ldw, ldc, ep, st, ws, ws_bytes);
