@@ -12,6 +12,7 @@ own weight layout (``wqkv = [q; k; v]``, ``wgu = [gate; up]``).
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import torch
@@ -62,6 +63,8 @@ class HipOps:
     def __init__(self):
         self.k = _native.kernels()
         self._ws = {}
+        if os.environ.get("FLS_SPLITK", "1") == "0":      # small-M split-K path off (A/B, tests)
+            self.k.fls_gemm_set_splitk(0)
 
     # ---------------------------------------------------------------- GEMM
     def gemm(self, x: torch.Tensor, w: torch.Tensor, epi: int = EPI_NONE, out: torch.Tensor = None,
