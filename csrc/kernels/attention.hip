@@ -116,7 +116,9 @@ __global__ __launch_bounds__(64 * WPH * HPB, 2) void attn_fwd(const half_t* __re
   const int r_start0 = wi[3], r_len0 = wi[4], r_causal0 = wi[5];
   const int r_start1 = wi[6], r_len1 = wi[7];
   const int kend0 = r_len0 <= 0 ? 0 : (r_causal0 ? min(r_len0, q_off + q_len) : r_len0);
-  const int kend1 = r_len1 <= 0 ? 0 : min(r_len1, q_off + q_len);
+  // R2 (suffix K/V reuse): every key of a suffix, the new rows' included, is read from the cache
+  // as range 2 through per-row windows, so there is no range 1
+  const int kend1 = (R2 || r_len1 <= 0) ? 0 : min(r_len1, q_off + q_len);
   const int n0 = (kend0 + KT - 1) / KT;
   // R2: range 2 = rows [r_start2, r_start2 + r_len2) of kv0 (a suffix's cached K/V), all visible,
   // walked between range 0 and range 1
@@ -140,10 +142,9 @@ __global__ __launch_bounds__(64 * WPH * HPB, 2) void attn_fwd(const half_t* __re
       const_cast<half_t*>((cache0 ? kv0 : qkv) + (size_t)r_start0 * ld0), (short)0, -1, 0x00020000);
   const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<half_t*>(qkv + (size_t)r_start1 * ld_qkv), (short)0, -1, 0x00020000);
-  __amdgpu_buffer_rsrc_t rs2 = rs0;
-  if constexpr (R2)
-    rs2 = __builtin_amdgcn_make_buffer_rsrc(const_cast<half_t*>(kv0 + (size_t)r_start2 * ld0), (short)0, -1,
-                                            0x00020000);
+  // range 2 rows lie after range 0's in the same cache buffer: read through rs0 at a row offset (a
+  // third descriptor in the tile loader's select costs registers the R2 kernel does not have)
+  const int r2base = R2 ? r_start2 - r_start0 : 0;
 
   half8 qf[2][NS];
   int qi[2], lo[2], lo2[2] = {0, 0}, hi2[2] = {0, 0};
@@ -175,22 +176,31 @@ __global__ __launch_bounds__(64 * WPH * HPB, 2) void attn_fwd(const half_t* __re
   float l_run[2] = {0.f, 0.f};
 
   u32x4 pk[PER], pv[PER];
-  auto load_tile = [&](int t) {
-    const bool r1 = t >= n02;
-    const bool r2 = R2 && !r1 && t >= n0;
-    const int k0 = (r1 ? t - n02 : (r2 ? t - n0 : t)) * KT;
-    const int klen = r1 ? r_len1 : (r2 ? r_len2 : r_len0);
-    const int ldk = r1 ? ld_qkv : ld0;
-    const unsigned kc = (unsigned)(r1 ? k_col : kc0) * 2u, vc = (unsigned)(r1 ? v_col : vc0) * 2u;
-    const __amdgpu_buffer_rsrc_t r = r1 ? rs1 : (r2 ? rs2 : rs0);
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int c = tid + i * NT_;
-      const int row = c / CH, ch = c % CH;
-      const unsigned off = (unsigned)(min(k0 + row, klen - 1) * ldk + ch * 8) * 2u;
-      pk[i] = __builtin_amdgcn_raw_buffer_load_b128(r, off, kc, 0);
-      pv[i] = __builtin_amdgcn_raw_buffer_load_b128(r, off, vc, 0);
+  // tile loader: by-reference captures for the plain kernel (its tuned code), by-value for R2 (whose
+  // three-range selects otherwise keep the captured locals in scratch memory)
+#define FLS_ATTN_LOAD_TILE_BODY \
+    const bool r1 = t >= n02; \
+    const bool r2 = R2 && !r1 && t >= n0; \
+    const int k0 = (r1 ? t - n02 : (r2 ? t - n0 : t)) * KT; \
+    const int klen = r1 ? r_len1 : (r2 ? r_len2 : r_len0); \
+    const int ldk = r1 ? ld_qkv : ld0; \
+    const int rb = r2 ? r2base : 0; \
+    const unsigned kc = (unsigned)(r1 ? k_col : kc0) * 2u, vc = (unsigned)(r1 ? v_col : vc0) * 2u; \
+    const __amdgpu_buffer_rsrc_t r = r1 ? rs1 : rs0; \
+_Pragma("unroll") \
+    for (int i = 0; i < PER; ++i) { \
+      const int c = tid + i * NT_; \
+      const int row = c / CH, ch = c % CH; \
+      const unsigned off = (unsigned)((rb + min(k0 + row, klen - 1)) * ldk + ch * 8) * 2u; \
+      pk[i] = __builtin_amdgcn_raw_buffer_load_b128(r, off, kc, 0); \
+      pv[i] = __builtin_amdgcn_raw_buffer_load_b128(r, off, vc, 0); \
     }
+  auto load_tile_ref = [&](int t) { FLS_ATTN_LOAD_TILE_BODY };
+  auto load_tile_val = [=, &pk, &pv](int t) { FLS_ATTN_LOAD_TILE_BODY };
+#undef FLS_ATTN_LOAD_TILE_BODY
+  auto load_tile = [&](int t) {
+    if constexpr (R2) load_tile_val(t);
+    else load_tile_ref(t);
   };
   auto store_tile = [&](int buf) {
     char* Ks = smem + buf * TILE_BYTES;

@@ -195,7 +195,9 @@ def pack_prompts(tps: Sequence[TokenizedPrompt], prompt_ids: Sequence[int],
     ids, pos, segs, last, nsuf, lsegs = [], [], [], [], [], []
     if suffix_keep is not None and not kv_cached:
         raise ValueError("suffix K/V reuse needs the prefix K/V cache (kv_cached)")
-    seg_lo, work, work2, r2win = [], [], [], []
+    if suffix_keep is not None and any(r < 0 for rows in suffix_rows for r in rows):
+        raise ValueError("suffix K/V reuse needs a cache region for every suffix")
+    seg_lo, work, work2, r2win, lwork, lwork2 = [], [], [], [], [], []
     src, dst, sfx_src, sfx_dst = [], [], [], []
     p_rows, p_items, p_scored = [], [], []
     t = 0
@@ -234,21 +236,35 @@ def pack_prompts(tps: Sequence[TokenizedPrompt], prompt_ids: Sequence[int],
             last.append(s0 + n - 1)
             # the scored row alone, for a last decoder layer that computes only scored rows
             lsegs.append(Segment(s0 + n - 1, 1, p0, Lp, 0, s0, n, q_off=n - 1, r2_start=r2s, r2_len=r2l))
+            if keep is not None:
+                # its work item (HIP): the whole suffix from the cache through the row's window
+                lwork.append((s0 + n - 1, 1, 0, p0, Lp, 0, 0, 0))
+                lwork2.append((c0_row, c + n))
             if c0_row >= 0:
                 sfx_src.extend(range(s0, s0 + n))
                 sfx_dst.extend(range(c0_row + c, c0_row + c + n))
-            r2win.extend([(r2s, r2s + r2l)] * n)
+            if keep is not None:
+                # the new rows' K/V are captured into the cache before the attention runs, right
+                # after the kept ones: new row i sees cache rows [c0_row, c0_row + c + i] (its own
+                # key included: causal by window), so the kernel needs no range 1 at all
+                r2win.extend([(c0_row, c0_row + c + i + 1) for i in range(n)])
+            else:
+                r2win.extend([(0, 0)] * n)
             t += n
         # the prompt's suffix rows [sfx0, t) in q_block chunks; range 1 of a chunk starts at the
         # suffix holding its first row.  Suffix K/V reuse: range 2 of every chunk spans the kept
         # rows of all the prompt's suffixes, each row seeing only its own suffix's window (r2win)
-        w = [(a, b) for a, b in r2win[sfx0:t] if b > a]
-        r2 = (min(a for a, _ in w), max(b for _, b in w)) if w else (0, 0)
         for c0 in range(sfx0, t, q_block):
             c1 = min(c0 + q_block, t)
-            r1 = seg_lo[c0]
-            work.append((c0, c1 - c0, c0 - r1, p0, Lp, 0, r1, c1 - r1))
-            work2.append((r2[0], r2[1] - r2[0]))
+            if keep is not None:
+                w = r2win[c0:c1]
+                lo, hi = min(a for a, _ in w), max(b for _, b in w)
+                work.append((c0, c1 - c0, 0, p0, Lp, 0, 0, 0))
+                work2.append((lo, hi - lo))
+            else:
+                r1 = seg_lo[c0]
+                work.append((c0, c1 - c0, c0 - r1, p0, Lp, 0, r1, c1 - r1))
+                work2.append((0, 0))
         max_pos = max(max_pos, Lp + max([len(s) for s in tp.suffixes] or [0]))
         p_rows.append((row0, t))
         p_items.append((item0, len(work)))
@@ -262,7 +278,8 @@ def pack_prompts(tps: Sequence[TokenizedPrompt], prompt_ids: Sequence[int],
         ids=np.asarray(ids, dtype=np.int32), positions=np.asarray(pos, dtype=np.int32),
         segments=segs, work=work, seg_lo=np.asarray(seg_lo, dtype=np.int32),
         last_idx=np.asarray(last, dtype=np.int32), last_segments=lsegs,
-        work_last=_work_items(lsegs), num_tokens=t, padded_tokens=padded,
+        work_last=(np.asarray(lwork, dtype=np.int32).reshape(-1, WORK_ITEM_FIELDS) if reuse
+                   else _work_items(lsegs)), num_tokens=t, padded_tokens=padded,
         max_pos=max_pos, kv_cached=kv_cached, q_block=q_block,
         pfx_src=np.asarray(src, dtype=np.int64) if (prefix_offsets is not None and not kv_cached) else None,
         pfx_dst=np.asarray(dst, dtype=np.int64) if (prefix_offsets is not None and not kv_cached) else None,
@@ -271,8 +288,7 @@ def pack_prompts(tps: Sequence[TokenizedPrompt], prompt_ids: Sequence[int],
         prompt_scored=np.asarray(p_scored, dtype=np.int64).reshape(-1, 2),
         work2=np.asarray(work2, dtype=np.int32).reshape(-1, 2) if reuse else None,
         r2win=np.asarray(r2win, dtype=np.int32).reshape(-1, 2) if reuse else None,
-        work2_last=(np.asarray([(sg.r2_start, sg.r2_len) for sg in lsegs], dtype=np.int32).reshape(-1, 2)
-                    if reuse else None),
+        work2_last=np.asarray(lwork2, dtype=np.int32).reshape(-1, 2) if reuse else None,
         sfx_src=np.asarray(sfx_src, dtype=np.int64) if sfx_src else None,
         sfx_dst=np.asarray(sfx_dst, dtype=np.int64) if sfx_dst else None)
 

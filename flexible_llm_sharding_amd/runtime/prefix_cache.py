@@ -112,6 +112,8 @@ class PrefixEntry:
                 k.append(min(common_prefix(old, s), len(s) - 1) if (reuse and old) else 0)
             rows.append(r)
             keep.append(k)
+        if any(r < 0 for rr in rows for r in rr):
+            reuse = False        # reuse mode reads every suffix's K/V from its region (batch.pack_prompts)
         return rows, (keep if reuse else None)
 
     def commit_suffixes(self, tps: Sequence, rows) -> None:

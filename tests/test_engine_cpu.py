@@ -656,8 +656,8 @@ def test_moe_chunks_shards_storage_match_oracle(tmp_path, family):
 
 def test_suffix_kv_reuse_partial_and_overflow(tiny_model):
     """Suffix K/V reuse keeps only the common token prefix with the last call: suffixes edited in
-    the middle, grown past their cache region, shortened, or new ones — every call's scores equal a
-    runner without any cache."""
+    the middle, grown past their cache region (reuse off for that call), shortened, or dropped —
+    every call's scores equal a runner without any cache."""
     from flexible_llm_sharding_amd.engine import ShardedRunner
     from flexible_llm_sharding_amd.runtime.prefix_cache import PrefixKVCache
     from flexible_llm_sharding_amd.runtime.stream import FileLayerSource
@@ -669,21 +669,24 @@ def test_suffix_kv_reuse_partial_and_overflow(tiny_model):
     words = [p[0].split()[:30] for p in base]
     step2 = [(pre, (sufs[0] + " " + " ".join(words[i][:2]),                     # grew by 2 words
                     " ".join(words[i][3:6]) + sufs[1][len(sufs[1]) // 2:],      # edited in the middle
-                    sufs[2] + " " + " ".join(words[i][:28])))                   # outgrows its region
+                    sufs[2]))
              for i, (pre, sufs) in enumerate(base)]
-    step3 = [(pre, (sufs[0][:max(1, len(sufs[0]) // 2)],)) for pre, sufs in step2]   # shorter, fewer
+    step3 = [(pre, (sufs[0], sufs[1], sufs[2] + " " + " ".join(words[i][:28])))      # one outgrows its region
+             for i, (pre, sufs) in enumerate(step2)]
+    step4 = [(pre, (sufs[0][:max(1, len(sufs[0]) // 2)],)) for pre, sufs in step3]   # shorter, fewer
     plain = ShardedRunner(cfg, FileLayerSource(cfg, path), "cpu", tok)
     old = PrefixKVCache.SUFFIX_GROWTH
     PrefixKVCache.SUFFIX_GROWTH = 8
     try:
         r = ShardedRunner(cfg, FileLayerSource(cfg, path), "cpu", tok, prefix_kv_cache=True)
         reused = []
-        for prompts in (base, step2, step3):
+        for prompts in (base, step2, step3, step4):
             got, want = r(prompts), plain(prompts)
             for a, b in zip(got, want):
                 assert np.abs(a.astype(np.float32) - b.astype(np.float32)).max() < 1e-5
             reused.append(r.stats["suffix_tokens_reused"])
-        assert reused[0] == 0 and reused[1] > 0
+        # a suffix without a region (grown past it) turns reuse off for that call
+        assert reused[0] == 0 and reused[1] > 0 and reused[2] == 0
     finally:
         PrefixKVCache.SUFFIX_GROWTH = old
 
@@ -700,8 +703,10 @@ def test_pack_suffix_reuse_work_items():
     assert b.ids.tolist() == [3, 4, 5, 6, 7] and b.positions.tolist() == [12, 13, 10, 11, 12]
     assert b.sfx_src.tolist() == [0, 1, 2, 3, 4] and b.sfx_dst.tolist() == [22, 23, 40, 41, 42]
     assert b.last_idx.tolist() == [1, 4]
-    assert b.r2win.tolist() == [[20, 22], [20, 22], [0, 0], [0, 0], [0, 0]]
-    assert b.work.shape[0] == 1 and b.work2.tolist() == [[20, 2]]          # one item for both suffixes
-    assert visible_keys(b.work, b.seg_lo, 1, b.work2, b.r2win) == [(0, 0, 9), (2, 20, 21), (1, 0, 1)]
-    assert visible_keys(b.work, b.seg_lo, 3, b.work2, b.r2win) == [(0, 0, 9), (1, 2, 3)]
-    assert b.work2_last.tolist() == [[20, 2], [0, 0]]
+    # the new rows' K/V are read back from the cache (captured before the attention runs): each row
+    # sees its suffix's region up to and including itself, so the items need no range 1
+    assert b.r2win.tolist() == [[20, 23], [20, 24], [40, 41], [40, 42], [40, 43]]
+    assert b.work.tolist() == [[0, 5, 0, 0, 10, 0, 0, 0]] and b.work2.tolist() == [[20, 23]]
+    assert visible_keys(b.work, b.seg_lo, 1, b.work2, b.r2win) == [(0, 0, 9), (2, 20, 23)]
+    assert visible_keys(b.work, b.seg_lo, 3, b.work2, b.r2win) == [(0, 0, 9), (2, 40, 41)]
+    assert b.work_last[:, :2].tolist() == [[1, 1], [4, 1]] and b.work2_last.tolist() == [[20, 4], [40, 3]]
