@@ -73,7 +73,8 @@ int fls_gemm(const void* A, const void* W, void* C, const void* R, int M, int N,
              const float* sin_t, int rope_cols, int head_dim, const void* bias, void* ws, uint64_t ws_bytes,
              fls_stream_t s);   // ws: device scratch for the small-M split-K path (may be null)
 int fls_gemm_set_splitk(int on);
-int fls_gemm_set_gu_split(int p);   // SwiGLU GEMM in p column launches (A/B; default 1)
+int fls_gemm_set_gu_split(int p);
+int fls_gemm_set_row_chunk(int rows);   // rows per main-path GEMM launch (default 16384; 0 = unlimited)   // SwiGLU GEMM in p column launches (A/B; default 1)
 // mixture-of-experts FFN (csrc/kernels/moe.hip): routing, stable expert sort, grouped v10 GEMM
 // (every expert of a layer in one launch, optional row gather), fp16-ordered weighted combine
 int fls_moe_route(const void* logits, int ldl, int T, int E, int k, int norm, int round16, int* ids, float* w,

@@ -268,6 +268,7 @@ void launch_main(int tiles, const half_t* A, const half_t* W, half_t* C, int M, 
 constexpr int SPLITK_MAX_M = 512;
 int g_splitk = 1;            // split-K path for small M on (fls_gemm_set_splitk)
 int g_gu_split = 1;          // SwiGLU GEMM in this many column launches (fls_gemm_set_gu_split; A/B)
+int ROW_CHUNK = 16384;       // main-path launches cover at most this many rows (fls_gemm_set_row_chunk)
 
 template <int EPI>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part, int S, long long pstride,
@@ -414,6 +415,23 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
     FLS_CHECK_LAUNCH();
     return 0;
   }
+  // Row chunks of <= ROW_CHUNK rows: with more rows the activation panel (M x K) outgrows the 256 MB
+  // Infinity Cache and the N-grouped tile order re-reads it from HBM once per group of weight
+  // columns.  70B O projection over 43,008 rows: one launch 1,361 TFLOP/s, three of 14,336 rows
+  // 1,421 (gate/up + SwiGLU 1,325 -> 1,430; profiles/r3_gemm, scripts/gemm_m_chunks.py).
+  if (M > ROW_CHUNK) {
+    const int n = (M + ROW_CHUNK - 1) / ROW_CHUNK;
+    const int step = ((M + n - 1) / n + BM - 1) / BM * BM;
+    for (int r0 = 0; r0 < M; r0 += step) {
+      Epi e = ep;
+      if (e.pos) e.pos += r0;
+      if (e.R) e.R += (size_t)r0 * e.ldr;
+      const int rc = launch<EPI>(A + (size_t)r0 * lda, W, C + (size_t)r0 * ldc, min(step, M - r0), N, K, lda, ldw,
+                                 ldc, e, s, ws, ws_bytes);
+      if (rc) return rc;
+    }
+    return 0;
+  }
   // One block per tile, dispatched by the hardware as CUs free up.  A persistent form (one block
   // per CU walking its tiles, the next tile's prologue DMA under this tile's epilogue) measured
   // 1.1-3.9% slower on every 70B / 7B shape once the tile order was XCD-aware (profiles/r2_gemm).
@@ -443,6 +461,13 @@ extern "C" int fls_gemm_set_order(int order) {
 extern "C" int fls_gemm_set_splitk(int on) {
   const int old = g_splitk;
   g_splitk = on ? 1 : 0;
+  return old;
+}
+
+// rows per main-path launch (0: unlimited; default 16384)
+extern "C" int fls_gemm_set_row_chunk(int rows) {
+  const int old = ROW_CHUNK;
+  ROW_CHUNK = rows > 0 ? rows : (1 << 30);
   return old;
 }
 

@@ -77,6 +77,7 @@ def _load_kernels():
           c_uint64, c_void_p)
     _bind(lib, "fls_gemm_set_splitk", c_int, c_int)
     _bind(lib, "fls_gemm_set_gu_split", c_int, c_int)
+    _bind(lib, "fls_gemm_set_row_chunk", c_int, c_int)
     _bind(lib, "fls_gemm_set_mid", c_int, c_int)
     _bind(lib, "fls_moe_route", c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
           c_void_p)

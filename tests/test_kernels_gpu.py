@@ -520,3 +520,34 @@ def test_gemm_small_m_splitk(ops, ref, M, epi):
     assert torch.equal(got, again)
     assert rel_err(got.cpu(), want) < 3e-3
     assert rel_err(got.cpu(), plain.cpu()) < 2e-3
+
+
+@pytest.mark.parametrize("epi", ["resid", "rope", "swiglu"])
+def test_gemm_row_chunks_bitwise(ops, epi):
+    """Main-path GEMMs over more than 16,384 rows run as row-chunk launches (the activation panel
+    then fits the Infinity Cache): bitwise equal to one launch over all rows."""
+    from flexible_llm_sharding_amd.config import ModelConfig
+    from flexible_llm_sharding_amd.models.llama import rope_tables
+    M, K = 17000, 256
+    x = rnd(M, K, seed=21)
+    pos = torch.randint(0, 4000, (M,), dtype=torch.int32, device=DEV)
+    cfg = ModelConfig(hidden_size=256, num_attention_heads=2, num_key_value_heads=1)
+    cos, sin = rope_tables(cfg, 4096)
+    cos, sin = cos.to(DEV), sin.to(DEV)
+    w = rnd(512, K, scale=0.05, seed=22)
+    r0 = rnd(M, 512, seed=23)
+
+    def run():
+        if epi == "resid":
+            return ops.linear_residual(x, w, r0.clone())
+        if epi == "rope":
+            return ops.qkv_rope(x, w, pos, cos, sin, 2, 1, 128)
+        return ops.swiglu_up(x, w)
+    a = run()
+    old = ops.k.fls_gemm_set_row_chunk(0)
+    try:
+        b = run()
+    finally:
+        ops.k.fls_gemm_set_row_chunk(old)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
