@@ -419,9 +419,10 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
   // Infinity Cache and the N-grouped tile order re-reads it from HBM once per group of weight
   // columns.  70B O projection over 43,008 rows: one launch 1,361 TFLOP/s, three of 14,336 rows
   // 1,421 (gate/up + SwiGLU 1,325 -> 1,430; profiles/r3_gemm, scripts/gemm_m_chunks.py).
-  if (M > ROW_CHUNK) {
-    const int n = (M + ROW_CHUNK - 1) / ROW_CHUNK;
-    const int step = ((M + n - 1) / n + BM - 1) / BM * BM;
+  // Only when every chunk still fills the chip (>= 256 tiles), so each piece stays on this path.
+  const int n_chunks = (M + ROW_CHUNK - 1) / ROW_CHUNK;
+  const int step = ((M + n_chunks - 1) / n_chunks + BM - 1) / BM * BM;
+  if (M > ROW_CHUNK && (size_t)(step / BM) * (N / BN) >= 256) {
     for (int r0 = 0; r0 < M; r0 += step) {
       Epi e = ep;
       if (e.pos) e.pos += r0;

@@ -2,6 +2,9 @@
 SwiGLU), interleaved rounds in one process: does the 256x256-tile kernel prefer smaller grids?
 
     python scripts/gemm_m_chunks.py [--rows 43008] [--chunks 1,2,3,4]
+
+A chunk count ``0`` is one call with the launcher's own row chunking turned off
+(``fls_gemm_set_row_chunk(0)``); ``1`` is one call with the launcher's default (<= 16384 rows a launch).
 """
 import argparse
 import json
@@ -29,10 +32,13 @@ def main():
         w = ((torch.rand(N, H, device=dev) * 2 - 1) * 0.02).half()
         out = torch.randn(M, N if epi == EPI_RESID else I, device=dev).half()
         cs = [int(c) for c in a.chunks.split(",")]
+        default_chunk = ops.k.fls_gemm_set_row_chunk(0)
+        ops.k.fls_gemm_set_row_chunk(default_chunk)
         times = {c: [] for c in cs}
         for _ in range(a.rounds):
             for c in cs:
-                step = -(-M // c)
+                ops.k.fls_gemm_set_row_chunk(0 if c == 0 else default_chunk)
+                step = -(-M // max(c, 1))
                 step = -(-step // 256) * 256
 
                 def run():

@@ -531,17 +531,18 @@ def test_gemm_row_chunks_bitwise(ops, epi):
     M, K = 17000, 256
     x = rnd(M, K, seed=21)
     pos = torch.randint(0, 4000, (M,), dtype=torch.int32, device=DEV)
-    cfg = ModelConfig(hidden_size=256, num_attention_heads=2, num_key_value_heads=1)
+    cfg = ModelConfig(hidden_size=1024, num_attention_heads=8, num_key_value_heads=4)
     cos, sin = rope_tables(cfg, 4096)
     cos, sin = cos.to(DEV), sin.to(DEV)
-    w = rnd(512, K, scale=0.05, seed=22)
-    r0 = rnd(M, 512, seed=23)
+    # N = 2048: each 8,704-row chunk is 272 tiles of 256 x 256 (the chunks stay on the main path)
+    w = rnd(2048, K, scale=0.05, seed=22)
+    r0 = rnd(M, 2048, seed=23)
 
     def run():
         if epi == "resid":
             return ops.linear_residual(x, w, r0.clone())
         if epi == "rope":
-            return ops.qkv_rope(x, w, pos, cos, sin, 2, 1, 128)
+            return ops.qkv_rope(x, w, pos, cos, sin, 8, 4, 128)
         return ops.swiglu_up(x, w)
     a = run()
     old = ops.k.fls_gemm_set_row_chunk(0)
