@@ -101,10 +101,12 @@ int fls_gemm_set_mid(int on);   // 64x128-tile kernel for small / medium M (defa
 // between range 0 and range 1, of which query row i sees kv0 rows [r2win[2i], r2win[2i+1]) (its
 // suffix's cached K/V rows; needs kv0 and r2win).
 int fls_attention_set_hpb(int hpb);
+int fls_attention_set_split(int ns);
+// ws / ws_bytes / n_rows (rows of qkv and out): fp32 scratch of the split-KV range-2 kernel (null: no split)
 int fls_attention(const void* qkv, void* out, const int* work, int n_items, int n_q_heads,
                   int n_kv_heads, int head_dim, int ld_qkv, int ld_out, float scale, const void* kv0,
                   int ld_kv0, const int* seg_lo, int q_block, const int* work2, const int* r2win,
-                  fls_stream_t s);
+                  void* ws, unsigned long long ws_bytes, int n_rows, fls_stream_t s);
 int fls_headnorm_rope(void* x, int ldx, int rows, int n_q, int n_k, const void* qn, const void* kn, const int* pos,
                       const float* cos_t, const float* sin_t, int hd, float eps, fls_stream_t s);
 int fls_rmsnorm(const void* x, const void* w, void* y, const int* row_idx, int rows, int H,

@@ -81,6 +81,10 @@ __device__ __forceinline__ float max_xor16_32(float v) {
 }
 
 typedef float float2_ __attribute__((ext_vector_type(2)));
+template <int N>
+struct IC {
+  static constexpr int value = N;
+};
 typedef _Float16 half2_ __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
@@ -88,12 +92,18 @@ __device__ __forceinline__ unsigned pack_h2(float a, float b) {
   return __builtin_bit_cast(unsigned, __builtin_convertvector(float2_{a, b}, half2_));
 }
 
-template <int HD, int HPB, int WPH, bool R2>
+// SPL (split-KV, R2 only): blockIdx.z walks one of gridDim.z contiguous slices of the item's key
+// tiles and writes its unnormalised O, running max and row sum in fp32 to `part`
+// ([rows][splits][nh] x (HD + 2)); attn_split_combine merges the slices.  For grids with fewer
+// blocks than CUs (few prompts with long contexts), which otherwise leave most CUs idle.
+template <int HD, int HPB, int WPH, bool R2, bool SPL = false>
 __global__ __launch_bounds__(64 * WPH * HPB, 2) void attn_fwd(const half_t* __restrict__ qkv, half_t* __restrict__ out,
                                                     const int* __restrict__ work, const int* __restrict__ seg_lo,
                                                     int nh, int nkv, int ld_qkv, int ld_out, float scale_log2,
                                                     const half_t* __restrict__ kv0, int ld_kv0,
-                                                    const int* __restrict__ work2, const int* __restrict__ r2win) {
+                                                    const int* __restrict__ work2, const int* __restrict__ r2win,
+                                                    float* __restrict__ part) {
+  static_assert(!SPL || R2, "split-KV is built for the range-2 (suffix K/V reuse) kernel only");
   constexpr int NT_ = 64 * WPH * HPB;
   constexpr int NS = HD / 32;               // k-steps of QK^T
   constexpr int NU = HD / 16;               // 16-wide d subtiles of O
@@ -129,6 +139,13 @@ __global__ __launch_bounds__(64 * WPH * HPB, 2) void attn_fwd(const half_t* __re
   }
   const int n02 = n0 + (r_len2 + KT - 1) / KT;
   const int ntiles = n02 + (kend1 + KT - 1) / KT;
+  // this block's key tiles [t_lo, t_hi): all of them unless split
+  int t_lo = 0, t_hi = ntiles;
+  if constexpr (SPL) {
+    const int per = (ntiles + (int)gridDim.z - 1) / (int)gridDim.z;
+    t_lo = min(ntiles, (int)blockIdx.z * per);
+    t_hi = min(ntiles, t_lo + per);
+  }
 
   const int fr = lane & 15, grp = lane >> 4;
   const int k_col = nh * HD + g * HD;
@@ -166,6 +183,7 @@ __global__ __launch_bounds__(64 * WPH * HPB, 2) void attn_fwd(const half_t* __re
   // the whole wave iff its last key is visible to that row (range 1 with several suffixes: masked)
   const int qi_min = q_off + rbase;
   const bool multi = seg_lo != nullptr;
+  const int live_rows = q_len - rbase;      // query rows of this wave inside the item (uniform)
 
   floatx4 o[2][NU];
 #pragma unroll
@@ -214,13 +232,13 @@ _Pragma("unroll") \
     }
   };
 
-  if (ntiles > 0) {
-    load_tile(0);
-    store_tile(0);
-    if (ntiles > 1) load_tile(1);
+  if (t_hi > t_lo) {
+    load_tile(t_lo);
+    store_tile(t_lo & 1);
+    if (t_hi > t_lo + 1) load_tile(t_lo + 1);
   }
   __syncthreads();
-  for (int t = 0; t < ntiles; ++t) {
+  for (int t = t_lo; t < t_hi; ++t) {
     const bool r1 = t >= n02;
     const bool r2 = R2 && !r1 && t >= n0;
     const int k0 = (r1 ? t - n02 : (r2 ? t - n0 : t)) * KT;
@@ -229,107 +247,132 @@ _Pragma("unroll") \
     const char* Ks = smem + (t & 1) * TILE_BYTES;
     const char* Vs = Ks + KT * HD * 2;
 
-    // ---- S^T = K Q^T for both 16-row query groups (each K fragment read once)
-    floatx4 sc[2][4];
-#pragma unroll
-    for (int tt = 0; tt < 4; ++tt) {
-      sc[0][tt] = floatx4{0.f, 0.f, 0.f, 0.f};
-      sc[1][tt] = floatx4{0.f, 0.f, 0.f, 0.f};
-      const int krow = tt * 16 + fr;
-#pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        const half8 kf = *(const half8*)(Ks + Lds<HD>::k_off(krow, s * 4 + grp));
-        sc[0][tt] = mfma16x16x32(kf, qf[0][s], sc[0][tt]);
-        sc[1][tt] = mfma16x16x32(kf, qf[1][s], sc[1][tt]);
-      }
+    // the tile's math for the wave's first NQ 16-row query groups (NQ = 2: the whole wave)
+#define FLS_ATTN_TILE_MATH \
+    /* ---- S^T = K Q^T for both 16-row query groups (each K fragment read once) */ \
+    floatx4 sc[2][4]; \
+_Pragma("unroll") \
+    for (int tt = 0; tt < 4; ++tt) { \
+      sc[0][tt] = floatx4{0.f, 0.f, 0.f, 0.f}; \
+      if constexpr (NQ > 1) sc[1][tt] = floatx4{0.f, 0.f, 0.f, 0.f}; \
+      const int krow = tt * 16 + fr; \
+_Pragma("unroll") \
+      for (int s = 0; s < NS; ++s) { \
+        const half8 kf = *(const half8*)(Ks + Lds<HD>::k_off(krow, s * 4 + grp)); \
+        sc[0][tt] = mfma16x16x32(kf, qf[0][s], sc[0][tt]); \
+        if constexpr (NQ > 1) sc[1][tt] = mfma16x16x32(kf, qf[1][s], sc[1][tt]); \
+      } \
+    } \
+    /* ---- visibility: wave-uniform fast path when every key of the tile is visible to every row */ \
+    const int vis_last = causal ? min(klen - 1, qi_min) : klen - 1; \
+    if (k0 + KT - 1 > vis_last || (r1 && multi) || r2) { \
+      asm volatile("" ::: "memory");        /* keep this a branch (not per-score selects on every tile) */ \
+_Pragma("unroll") \
+      for (int qg = 0; qg < NQ; ++qg) { \
+        /* key k0 + 16tt + 4grp + r is visible iff lo_rel <= 16tt + r <= hi_rel */ \
+        const int hi_rel = (r2 ? min(klen, hi2[qg]) - 1 : (causal ? min(klen - 1, qi[qg]) : klen - 1)) - k0 - grp * 4; \
+        const int lo_rel = (r1 ? lo[qg] : (r2 ? lo2[qg] : 0)) - k0 - grp * 4; \
+_Pragma("unroll") \
+        for (int tt = 0; tt < 4; ++tt) \
+_Pragma("unroll") \
+          for (int r = 0; r < 4; ++r) \
+            if (tt * 16 + r > hi_rel || tt * 16 + r < lo_rel) sc[qg][tt][r] = -INFINITY; \
+      } \
+    } \
+    /* ---- online softmax per query group */ \
+    half8 pf[2][2]; \
+_Pragma("unroll") \
+    for (int qg = 0; qg < NQ; ++qg) { \
+      /* 16 scores of this lane's query: two independent max3 chains, then across the lane groups */ \
+      float ma = vmax3(sc[qg][0][0], sc[qg][0][1], sc[qg][0][2]); \
+      float mb = vmax3(sc[qg][2][0], sc[qg][2][1], sc[qg][2][2]); \
+      ma = vmax3(ma, sc[qg][0][3], sc[qg][1][0]); \
+      mb = vmax3(mb, sc[qg][2][3], sc[qg][3][0]); \
+      ma = vmax3(ma, sc[qg][1][1], sc[qg][1][2]); \
+      mb = vmax3(mb, sc[qg][3][1], sc[qg][3][2]); \
+      const float mx = max_xor16_32(vmax3(ma, sc[qg][1][3], vmax(mb, sc[qg][3][3]))); \
+      /* deferred rescale: keep the old max unless some row of the wave grew past 2^DEFER_LOG2 */ \
+      /* (the previous tile's P.V is complete: nothing at the old scale is pending) */ \
+      if (!__all((mx - m_run[qg]) * scale_log2 <= DEFER_LOG2)) { \
+        const float m_new = fmaxf(m_run[qg], mx); \
+        const float alpha = fast_exp2((m_run[qg] - m_new) * scale_log2); \
+        l_run[qg] *= alpha; \
+_Pragma("unroll") \
+        for (int u = 0; u < NU; ++u) o[qg][u] *= alpha; \
+        m_run[qg] = m_new; \
+      } \
+      const float mc = m_run[qg] * scale_log2; \
+      float psum = 0.f; \
+      unsigned pw[8]; \
+_Pragma("unroll") \
+      for (int tt = 0; tt < 4; ++tt) { \
+        float p[4]; \
+_Pragma("unroll") \
+        for (int r = 0; r < 4; ++r) { \
+          p[r] = fast_exp2(__builtin_fmaf(sc[qg][tt][r], scale_log2, -mc)); \
+          psum += p[r]; \
+        } \
+        pw[tt * 2] = pack_h2(p[0], p[1]); \
+        pw[tt * 2 + 1] = pack_h2(p[2], p[3]); \
+      } \
+      l_run[qg] += psum; \
+      /* P^T fragment: element (tt & 1) * 4 + r of k-step tt >> 1 = key 16 tt + 4 grp + r */ \
+_Pragma("unroll") \
+      for (int ks = 0; ks < 2; ++ks) \
+        pf[qg][ks] = __builtin_bit_cast(half8, u32x4{pw[ks * 4], pw[ks * 4 + 1], pw[ks * 4 + 2], pw[ks * 4 + 3]}); \
+    } \
+    /* ---- O^T += V^T P^T (each V^T fragment read once for both groups) */ \
+    const int q4 = (lane & 15) >> 2, p4 = lane & 3; \
+_Pragma("unroll") \
+    for (int ks = 0; ks < 2; ++ks) { \
+      const int row_a = ks * 32 + grp * 4 + q4; \
+      const int row_b = row_a + 16; \
+_Pragma("unroll") \
+      for (int u = 0; u < NU; ++u) { \
+        const int ch = u * 2 + (p4 >> 1); \
+        const half4 va = ds_read_tr16(Vs + Lds<HD>::v_off(row_a, ch) + (p4 & 1) * 8); \
+        const half4 vb = ds_read_tr16(Vs + Lds<HD>::v_off(row_b, ch) + (p4 & 1) * 8); \
+        const half8 vf = {va[0], va[1], va[2], va[3], vb[0], vb[1], vb[2], vb[3]}; \
+        o[0][u] = mfma16x16x32(vf, pf[0][ks], o[0][u]); \
+        if constexpr (NQ > 1) o[1][u] = mfma16x16x32(vf, pf[1][ks], o[1][u]); \
+      } \
     }
-    // ---- visibility: wave-uniform fast path when every key of the tile is visible to every row
-    const int vis_last = causal ? min(klen - 1, qi_min) : klen - 1;
-    if (k0 + KT - 1 > vis_last || (r1 && multi) || r2) {
-      asm volatile("" ::: "memory");        // keep this a branch (not per-score selects on every tile)
-#pragma unroll
-      for (int qg = 0; qg < 2; ++qg) {
-        // key k0 + 16tt + 4grp + r is visible iff lo_rel <= 16tt + r <= hi_rel
-        const int hi_rel = (r2 ? min(klen, hi2[qg]) - 1 : (causal ? min(klen - 1, qi[qg]) : klen - 1)) - k0 - grp * 4;
-        const int lo_rel = (r1 ? lo[qg] : (r2 ? lo2[qg] : 0)) - k0 - grp * 4;
-#pragma unroll
-        for (int tt = 0; tt < 4; ++tt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (tt * 16 + r > hi_rel || tt * 16 + r < lo_rel) sc[qg][tt][r] = -INFINITY;
-      }
+    if constexpr (!R2) {
+      constexpr int NQ = 2;
+      FLS_ATTN_TILE_MATH
+    } else {
+      // a decode-like item holds a few new rows (one per suffix): the waves and 16-row groups past
+      // q_len skip their MFMAs and softmax (wave-uniform), instead of padding every item to q_block
+      auto tile_math = [&](auto nq_c) {
+        constexpr int NQ = decltype(nq_c)::value;
+        FLS_ATTN_TILE_MATH
+      };
+      if (live_rows > 16) tile_math(IC<2>{});
+      else if (live_rows > 0) tile_math(IC<1>{});
     }
-    // ---- online softmax per query group
-    half8 pf[2][2];
-#pragma unroll
-    for (int qg = 0; qg < 2; ++qg) {
-      // 16 scores of this lane's query: two independent max3 chains, then across the lane groups
-      float ma = vmax3(sc[qg][0][0], sc[qg][0][1], sc[qg][0][2]);
-      float mb = vmax3(sc[qg][2][0], sc[qg][2][1], sc[qg][2][2]);
-      ma = vmax3(ma, sc[qg][0][3], sc[qg][1][0]);
-      mb = vmax3(mb, sc[qg][2][3], sc[qg][3][0]);
-      ma = vmax3(ma, sc[qg][1][1], sc[qg][1][2]);
-      mb = vmax3(mb, sc[qg][3][1], sc[qg][3][2]);
-      const float mx = max_xor16_32(vmax3(ma, sc[qg][1][3], vmax(mb, sc[qg][3][3])));
-      // deferred rescale: keep the old max unless some row of the wave grew past 2^DEFER_LOG2
-      // (the previous tile's P.V is complete: nothing at the old scale is pending)
-      if (!__all((mx - m_run[qg]) * scale_log2 <= DEFER_LOG2)) {
-        const float m_new = fmaxf(m_run[qg], mx);
-        const float alpha = fast_exp2((m_run[qg] - m_new) * scale_log2);
-        l_run[qg] *= alpha;
-#pragma unroll
-        for (int u = 0; u < NU; ++u) o[qg][u] *= alpha;
-        m_run[qg] = m_new;
-      }
-      const float mc = m_run[qg] * scale_log2;
-      float psum = 0.f;
-      unsigned pw[8];
-#pragma unroll
-      for (int tt = 0; tt < 4; ++tt) {
-        float p[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          p[r] = fast_exp2(__builtin_fmaf(sc[qg][tt][r], scale_log2, -mc));
-          psum += p[r];
-        }
-        pw[tt * 2] = pack_h2(p[0], p[1]);
-        pw[tt * 2 + 1] = pack_h2(p[2], p[3]);
-      }
-      l_run[qg] += psum;
-      // P^T fragment: element (tt & 1) * 4 + r of k-step tt >> 1 = key 16 tt + 4 grp + r
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-        pf[qg][ks] = __builtin_bit_cast(half8, u32x4{pw[ks * 4], pw[ks * 4 + 1], pw[ks * 4 + 2], pw[ks * 4 + 3]});
-    }
-    // ---- O^T += V^T P^T (each V^T fragment read once for both groups)
-    const int q4 = (lane & 15) >> 2, p4 = lane & 3;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int row_a = ks * 32 + grp * 4 + q4;
-      const int row_b = row_a + 16;
-#pragma unroll
-      for (int u = 0; u < NU; ++u) {
-        const int ch = u * 2 + (p4 >> 1);
-        const half4 va = ds_read_tr16(Vs + Lds<HD>::v_off(row_a, ch) + (p4 & 1) * 8);
-        const half4 vb = ds_read_tr16(Vs + Lds<HD>::v_off(row_b, ch) + (p4 & 1) * 8);
-        const half8 vf = {va[0], va[1], va[2], va[3], vb[0], vb[1], vb[2], vb[3]};
-        o[0][u] = mfma16x16x32(vf, pf[0][ks], o[0][u]);
-        o[1][u] = mfma16x16x32(vf, pf[1][ks], o[1][u]);
-      }
-    }
-    if (t + 1 < ntiles) {
+#undef FLS_ATTN_TILE_MATH
+    if (t + 1 < t_hi) {
       store_tile((t + 1) & 1);               // the other buffer's readers (tile t-1) passed the last barrier
-      if (t + 2 < ntiles) load_tile(t + 2);  // in flight under tile t+1's MFMAs
+      if (t + 2 < t_hi) load_tile(t + 2);    // in flight under tile t+1's MFMAs
     }
     __syncthreads();
   }
-  // ---- normalise and store
+  // ---- normalise and store (split: the slice's fp32 partials)
 #pragma unroll
   for (int qg = 0; qg < 2; ++qg) {
     float l = l_run[qg];
     l += __shfl_xor(l, 16, 64);
     l += __shfl_xor(l, 32, 64);
     const int qrow = rbase + qg * 16 + fr;
+    if constexpr (SPL) {
+      if (qrow < q_len) {
+        float* pp = part + ((size_t)((q_start + qrow) * (int)gridDim.z + (int)blockIdx.z) * nh + h) * (HD + 2);
+#pragma unroll
+        for (int u = 0; u < NU; ++u) *(floatx4*)(pp + u * 16 + grp * 4) = o[qg][u];
+        if (grp == 0) *(float2_*)(pp + HD) = float2_{m_run[qg] * scale_log2, l};
+      }
+      continue;
+    }
     if (qrow < q_len) {
       const float inv = 1.f / l;
       half_t* op = out + (size_t)(q_start + qrow) * ld_out + h * HD + grp * 4;
@@ -344,13 +387,57 @@ _Pragma("unroll") \
   }
 }
 
+// merge the split-KV slices of every row of every item: O = sum_z 2^(m_z - M) O_z / sum_z 2^(m_z - M) l_z
+// (m in the log2 domain); block = one (item, head), a thread per head-dim column
+template <int HD>
+__global__ __launch_bounds__(HD) void attn_split_combine(const float* __restrict__ part, half_t* __restrict__ out,
+                                                         const int* __restrict__ work, int nh, int ld_out, int ns) {
+  const int* wi = work + blockIdx.x * 8;
+  const int q_start = wi[0], q_len = wi[1];
+  const int h = blockIdx.y, d = threadIdx.x;
+  for (int r = 0; r < q_len; ++r) {
+    const float* pp = part + ((size_t)(q_start + r) * ns * nh + h) * (HD + 2);
+    const size_t zs = (size_t)nh * (HD + 2);
+    float M = -INFINITY;
+    for (int z = 0; z < ns; ++z) M = fmaxf(M, pp[z * zs + HD]);
+    float L = 0.f, acc = 0.f;
+    for (int z = 0; z < ns; ++z) {
+      const float w = fast_exp2(pp[z * zs + HD] - M);
+      L += w * pp[z * zs + HD + 1];
+      acc += w * pp[z * zs + d];
+    }
+    out[(size_t)(q_start + r) * ld_out + h * HD + d] = (half_t)(acc / L);
+  }
+}
+
 template <int HD, int WPH, bool R2>
 int launch(int hpb, dim3 grid, hipStream_t st, const half_t* qkv, half_t* out, const int* work, const int* seg_lo,
            int nh, int nkv, int ld_qkv, int ld_out, float scale_log2, const half_t* kv0, int ld_kv0,
-           const int* work2, const int* r2win) {
+           const int* work2, const int* r2win, float* part, int ns) {
+  if constexpr (R2 && HD != 96) {
+    if (ns > 1) {
+      const dim3 g3(grid.x, grid.y, ns);
+#define FLS_ATTN_LAUNCH_SPL(HPB_)                                                                              \
+  hipLaunchKernelGGL((attn_fwd<HD, HPB_, WPH, true, true>), g3, dim3(64 * WPH * HPB_), 0, st, qkv, out, work, seg_lo, \
+                     nh, nkv, ld_qkv, ld_out, scale_log2, kv0, ld_kv0, work2, r2win, part)
+      if constexpr (WPH == 2) {
+        if (hpb == 4) FLS_ATTN_LAUNCH_SPL(4);
+        else if (hpb == 2) FLS_ATTN_LAUNCH_SPL(2);
+        else FLS_ATTN_LAUNCH_SPL(1);
+      } else {
+        if (hpb == 2) FLS_ATTN_LAUNCH_SPL(2);
+        else FLS_ATTN_LAUNCH_SPL(1);
+      }
+#undef FLS_ATTN_LAUNCH_SPL
+      FLS_CHECK_LAUNCH();
+      hipLaunchKernelGGL((attn_split_combine<HD>), dim3(grid.x, nh), dim3(HD), 0, st, part, out, work, nh, ld_out, ns);
+      FLS_CHECK_LAUNCH();
+      return 0;
+    }
+  }
 #define FLS_ATTN_LAUNCH(HPB_)                                                                                  \
   hipLaunchKernelGGL((attn_fwd<HD, HPB_, WPH, R2>), grid, dim3(64 * WPH * HPB_), 0, st, qkv, out, work, seg_lo, nh, \
-                     nkv, ld_qkv, ld_out, scale_log2, kv0, ld_kv0, work2, r2win)
+                     nkv, ld_qkv, ld_out, scale_log2, kv0, ld_kv0, work2, r2win, nullptr)
   if constexpr (HD == 96) {
     FLS_ATTN_LAUNCH(1);                     // 12 chunks per row: one head per block divides the tile
   } else if constexpr (WPH == 2) {
@@ -368,6 +455,7 @@ int launch(int hpb, dim3 grid, hipStream_t st, const half_t* qkv, half_t* out, c
 }
 
 int g_hpb = 0;   // heads per block override (0: by group size; tests / A-B)
+int g_split = 0; // split-KV slices of the range-2 kernel: 0 = by grid size, 1 = off, n = n (tests / A-B)
 
 }  // namespace
 
@@ -378,11 +466,18 @@ extern "C" int fls_attention_set_hpb(int hpb) {
   return old;
 }
 
+extern "C" int fls_attention_set_split(int ns) {
+  const int old = g_split;
+  g_split = ns;
+  return old;
+}
+
 namespace {
 template <bool R2>
 int dispatch(const void* qkv, void* out, const int* work, int n_items, int n_q_heads, int n_kv_heads, int head_dim,
              int ld_qkv, int ld_out, float scale, const void* kv0, int ld_kv0, const int* seg_lo, int q_block,
-             const int* work2, const int* r2win, fls_stream_t s) {
+             const int* work2, const int* r2win, void* ws, unsigned long long ws_bytes, int n_rows,
+             fls_stream_t s) {
   if (n_q_heads % n_kv_heads) return -2;
   if (head_dim != 64 && head_dim != 96 && head_dim != 128) return -3;
   if (q_block != 64 && q_block != 128) return -5;
@@ -398,34 +493,46 @@ int dispatch(const void* qkv, void* out, const int* work, int n_items, int n_q_h
   if (g_hpb > 0 && group % g_hpb == 0 && g_hpb <= (q_block == 64 ? 4 : 2)) hpb = g_hpb;
   if (head_dim == 96) hpb = 1;              // Phi-3-mini geometry (multi-head attention anyway)
   const dim3 grid(n_items, n_q_heads / hpb);
+  // split-KV (range-2 kernel) only when the grid leaves CUs idle (a long prompt or two decoding
+  // alone: one block per (item, 4 heads)); at 2 blocks per CU, the occupancy limit, the slices just
+  // queue behind each other and the combine costs extra: 70B, 32 prompts x 5 suffixes (512 blocks),
+  // 0.058 s per generation step unsplit vs 0.061-0.063 s split in 4 (profiles/r3_splitkv)
+  int ns = 1;
+  if (R2 && head_dim != 96 && ws && n_rows > 0) {
+    const long blocks = (long)grid.x * grid.y;
+    ns = g_split > 0 ? g_split : (blocks >= 256 ? 1 : (int)min(8L, (512 + blocks - 1) / blocks));
+    const unsigned long long per = (unsigned long long)n_rows * n_q_heads * (head_dim + 2) * 4ull;
+    while (ns > 1 && per * ns > ws_bytes) --ns;
+  }
+  float* part = (float*)ws;
   auto q = (const half_t*)qkv;
   auto o = (half_t*)out;
   auto k0 = (const half_t*)kv0;
   if (head_dim == 96)
     return q_block == 64 ? launch<96, 2, R2>(hpb, grid, st, q, o, work, seg_lo, n_q_heads, n_kv_heads, ld_qkv, ld_out,
-                                         scale_log2, k0, ld_kv0, work2, r2win)
+                                         scale_log2, k0, ld_kv0, work2, r2win, part, ns)
                          : launch<96, 4, R2>(hpb, grid, st, q, o, work, seg_lo, n_q_heads, n_kv_heads, ld_qkv, ld_out,
-                                         scale_log2, k0, ld_kv0, work2, r2win);
+                                         scale_log2, k0, ld_kv0, work2, r2win, part, ns);
   if (q_block == 64)
     return head_dim == 128 ? launch<128, 2, R2>(hpb, grid, st, q, o, work, seg_lo, n_q_heads, n_kv_heads, ld_qkv, ld_out,
-                                            scale_log2, k0, ld_kv0, work2, r2win)
+                                            scale_log2, k0, ld_kv0, work2, r2win, part, ns)
                            : launch<64, 2, R2>(hpb, grid, st, q, o, work, seg_lo, n_q_heads, n_kv_heads, ld_qkv, ld_out,
-                                           scale_log2, k0, ld_kv0, work2, r2win);
+                                           scale_log2, k0, ld_kv0, work2, r2win, part, ns);
   return head_dim == 128 ? launch<128, 4, R2>(hpb, grid, st, q, o, work, seg_lo, n_q_heads, n_kv_heads, ld_qkv, ld_out,
-                                          scale_log2, k0, ld_kv0, work2, r2win)
+                                          scale_log2, k0, ld_kv0, work2, r2win, part, ns)
                          : launch<64, 4, R2>(hpb, grid, st, q, o, work, seg_lo, n_q_heads, n_kv_heads, ld_qkv, ld_out,
-                                         scale_log2, k0, ld_kv0, work2, r2win);
+                                         scale_log2, k0, ld_kv0, work2, r2win, part, ns);
 }
 }  // namespace
 
 extern "C" int fls_attention(const void* qkv, void* out, const int* work, int n_items, int n_q_heads,
                              int n_kv_heads, int head_dim, int ld_qkv, int ld_out, float scale, const void* kv0,
                              int ld_kv0, const int* seg_lo, int q_block, const int* work2, const int* r2win,
-                             fls_stream_t s) {
+                             void* ws, unsigned long long ws_bytes, int n_rows, fls_stream_t s) {
   if (n_items <= 0) return 0;
   if (work2 && (!kv0 || !r2win)) return -6;   // range 2 indexes the K/V cache, per-row windows
   return work2 ? dispatch<true>(qkv, out, work, n_items, n_q_heads, n_kv_heads, head_dim, ld_qkv, ld_out, scale, kv0,
-                                ld_kv0, seg_lo, q_block, work2, r2win, s)
+                                ld_kv0, seg_lo, q_block, work2, r2win, ws, ws_bytes, n_rows, s)
                : dispatch<false>(qkv, out, work, n_items, n_q_heads, n_kv_heads, head_dim, ld_qkv, ld_out, scale, kv0,
-                                 ld_kv0, seg_lo, q_block, nullptr, nullptr, s);
+                                 ld_kv0, seg_lo, q_block, nullptr, nullptr, nullptr, 0, 0, s);
 }

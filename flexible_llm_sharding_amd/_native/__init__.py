@@ -63,7 +63,7 @@ class Piece(ctypes.Structure):
                 ("kind", ctypes.c_int32), ("pad", ctypes.c_int32)]
 
 
-KERNELS_ABI = 14   # bumped whenever a C signature in csrc/include/fls.h changes
+KERNELS_ABI = 15   # bumped whenever a C signature in csrc/include/fls.h changes
 
 
 def _load_kernels():
@@ -92,8 +92,10 @@ def _load_kernels():
           c_int, c_int, c_void_p)
     _bind(lib, "fls_gemm_set_order", c_int, c_int)
     _bind(lib, "fls_attention_set_hpb", c_int, c_int)
+    _bind(lib, "fls_attention_set_split", c_int, c_int)
     _bind(lib, "fls_attention", c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
-          c_int, c_int, c_float, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p)
+          c_int, c_int, c_float, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_uint64, c_int,
+          c_void_p)
     _bind(lib, "fls_rmsnorm", c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
           c_int, c_float, c_void_p)
     _bind(lib, "fls_headnorm_rope", c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,

@@ -65,6 +65,8 @@ class HipOps:
         self._ws = {}
         if os.environ.get("FLS_SPLITK", "1") == "0":      # small-M split-K path off (A/B, tests)
             self.k.fls_gemm_set_splitk(0)
+        if os.environ.get("FLS_ATTN_SPLIT"):              # split-KV slices of the range-2 kernel (A/B)
+            self.k.fls_attention_set_split(int(os.environ["FLS_ATTN_SPLIT"]))
 
     # ---------------------------------------------------------------- GEMM
     def gemm(self, x: torch.Tensor, w: torch.Tensor, epi: int = EPI_NONE, out: torch.Tensor = None,
@@ -288,13 +290,18 @@ class HipOps:
             raise TypeError("work2 must be int32 CUDA [n_items, 2] with r2win [T, 2] and kv0")
         if out is None:
             out = torch.empty(T, n_q_heads * head_dim, dtype=torch.float16, device=qkv.device)
+        # the range-2 (decode-like) kernel splits its key tiles over blocks when the grid is small;
+        # its fp32 partials live in the split-K GEMM scratch (same stream: never in use by both)
+        ws = self._splitk_ws(qkv.device, 0, 0) if work2 is not None else None
         rc = self.k.fls_attention(qkv.data_ptr(), out.data_ptr(), work.data_ptr(), work.shape[0],
                                   n_q_heads, n_kv_heads, head_dim, qkv.stride(0), out.stride(0),
                                   head_dim ** -0.5, kv0.data_ptr() if kv0 is not None else None,
                                   kv0.stride(0) if kv0 is not None else 0,
                                   seg_lo.data_ptr() if seg_lo is not None else None, q_block,
                                   work2.data_ptr() if work2 is not None else None,
-                                  r2win.data_ptr() if work2 is not None else None, _stream())
+                                  r2win.data_ptr() if work2 is not None else None,
+                                  ws.data_ptr() if ws is not None else None, ws.numel() if ws is not None else 0,
+                                  T, _stream())
         _chk(rc, "fls_attention")
         return out
 

@@ -21,6 +21,7 @@ from __future__ import annotations
 import json
 import os
 import string
+import weakref
 from dataclasses import dataclass
 from typing import List, Sequence, Tuple
 
@@ -124,16 +125,38 @@ def _assemble(p, s, pad) -> TokenizedPrompt:
     return TokenizedPrompt(list(p), real, Ls, eos)
 
 
+# prefix string -> ids, per tokenizer: a generation step re-tokenizes the same prefixes (only the
+# suffixes grow), and the prefixes are ~70% of the tokenizer's time (32 x 1k tokens: ~4.5 ms of a
+# ~65 ms 70B step with suffix K/V reuse).  Tokenization is a pure function of the string.
+_PREFIX_IDS: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+_PREFIX_IDS_MAX = 4096
+
+
+def _prefix_ids(tok, prefixes: Sequence[str], max_len: int):
+    try:
+        cache = _PREFIX_IDS.setdefault(tok, {})
+    except TypeError:                       # a tokenizer that cannot be weakly referenced
+        cache = {}
+    miss = sorted({p for p in prefixes if (p, max_len) not in cache})
+    if miss:
+        if len(cache) + len(miss) > _PREFIX_IDS_MAX:
+            cache.clear()
+        enc = tok(miss, return_attention_mask=False, truncation=True, max_length=max_len)["input_ids"]
+        for p, ids in zip(miss, enc):
+            cache[(p, max_len)] = list(ids)
+    return [cache[(p, max_len)] for p in prefixes]
+
+
 def tokenize_prompts(tok, prompts: Sequence[Tuple[str, Sequence[str]]],
                      max_len: int = MAX_TOKEN_LEN) -> List[TokenizedPrompt]:
     """All prompts in two batched tokenizer calls (the fast tokenizer encodes a batch on
-    all cores; per-prompt calls cost ~75 ms per 32 x 1k-token prompts, inside every pass).
+    all cores; per-prompt calls cost ~75 ms per 32 x 1k-token prompts, inside every pass);
+    prefixes seen before come from a per-tokenizer cache.
     Each prompt's suffix batch is then right-padded to its own longest suffix exactly as
     ``tok(suffixes, padding=True)`` does, so the result equals :func:`tokenize_prompt`."""
     if not prompts:
         return []
-    pre = tok([p for p, _ in prompts], return_attention_mask=False, truncation=True,
-              max_length=max_len)["input_ids"]
+    pre = _prefix_ids(tok, [p for p, _ in prompts], max_len)
     flat = [x for _, sufs in prompts for x in sufs]
     enc = tok(flat, return_attention_mask=False, truncation=True, max_length=max_len)["input_ids"] if flat else []
     pad = tok.pad_token_id

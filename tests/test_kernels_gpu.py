@@ -427,14 +427,41 @@ def test_qkv_norm_rope(ops, ref, nq, nk, hd):
         assert rel_err(y[:, v0:], (x.float() @ w.float().t())[:, v0:]) < 2e-3
 
 
+@pytest.mark.parametrize("split", [0, 1, 3, 8])
 @pytest.mark.parametrize("nh,nkv,hd", [(8, 1, 128), (4, 4, 64), (4, 4, 96)])
-def test_attention_suffix_rows_from_cache(ops, ref, nh, nkv, hd):
+def test_attention_suffix_rows_from_cache(ops, ref, nh, nkv, hd, split):
     """Suffix K/V reuse: the kept rows of each suffix read from the cache as range 2 (with the
-    prefix as range 0) and only the new rows computed == the full packed pass on those rows."""
+    prefix as range 0) and only the new rows computed == the full packed pass on those rows.
+    split: key-tile slices of the split-KV kernel (0 = by grid size, which splits this small grid;
+    1 = one block per item and head; hd 96 never splits)."""
+    old = ops.k.fls_attention_set_split(split)
+    try:
+        _suffix_rows_from_cache(ops, ref, nh, nkv, hd)
+    finally:
+        ops.k.fls_attention_set_split(old)
+
+
+def test_attention_decode_split_matches_unsplit(ops, ref):
+    """Decode-like step at 70B heads (12 prompts x 5 suffixes, one new row each after 40 kept rows,
+    600-row prefixes): the split-KV kernel (by grid size) == one block per item to fp32-partials
+    rounding, and both == the fp32 oracle."""
+    prompts = [(600, [41] * 5)] * 12
+    keep = [[40] * 5] * 12
+    ys = []
+    for split in (1, 0):
+        old = ops.k.fls_attention_set_split(split)
+        try:
+            ys.append(_suffix_rows_from_cache(ops, ref, 64, 8, 128, prompts, keep))
+        finally:
+            ops.k.fls_attention_set_split(old)
+    assert rel_err(ys[1], ys[0]) < 2e-3
+
+
+def _suffix_rows_from_cache(ops, ref, nh, nkv, hd, prompts=None, keep=None):
     from flexible_llm_sharding_amd.runtime.batch import pack_prompts
     from flexible_llm_sharding_amd.utils.tokenizer import TokenizedPrompt
-    prompts = [(70, [5, 80, 1]), (130, [65, 17]), (9, [3, 140])]
-    keep = [[3, 70, 0], [64, 5], [0, 139]]
+    prompts = prompts or [(70, [5, 80, 1]), (130, [65, 17]), (9, [3, 140])]
+    keep = keep or [[3, 70, 0], [64, 5], [0, 139]]
     tps = [TokenizedPrompt(list(range(lp)), [list(range(l)) for l in ls], max(ls), [l - 1 for l in ls])
            for lp, ls in prompts]
     offs, t = [], 0
@@ -474,6 +501,7 @@ def test_attention_suffix_rows_from_cache(ops, ref, nh, nkv, hd):
     torch.cuda.synchronize()
     assert rel_err(got_ref, want) < 1e-5                 # the oracle agrees with itself across layouts
     assert rel_err(y.cpu(), want) < 5e-3
+    return y.cpu()
 
 
 @pytest.mark.parametrize("M", [1, 7, 64, 160, 300, 512])
