@@ -52,6 +52,8 @@ def prefix_fingerprint(tps: Sequence) -> str:
 
 def common_prefix(a: Sequence[int], b: Sequence[int]) -> int:
     n = min(len(a), len(b))
+    if list(a[:n]) == list(b[:n]):            # a generation step: the old suffix is a prefix of the new
+        return n
     i = 0
     while i < n and a[i] == b[i]:
         i += 1

@@ -115,7 +115,7 @@ def _assemble(p, s, pad) -> TokenizedPrompt:
     Ls = len(rows[0]) if rows else 0
     eos, real = [], []
     for r in rows:
-        e = sum(1 for t in r if t != pad) - 1
+        e = len(r) - r.count(pad) - 1         # (suffix != pad).sum(1) - 1
         eos.append(e)
         idx = e if e >= 0 else Ls - 1     # torch index -1 == last column (reference quirk)
         if idx < 0:
