@@ -110,6 +110,18 @@ class ShardedRunner:
             # keep that waste near 1% (a VRAM cap re-plans the chunk from the MoE buffer sizes)
             mlp_chunk = MOE_MLP_CHUNK if cfg.is_moe else MLP_CHUNK
         self._plan_req = (token_budget, mlp_chunk, n_slots)
+        self.names = cfg.layer_names()
+        self.L = len(self.names)
+        self.plan: ShardPlan = make_plan(self.L, layer_num_per_shard, self.comm.world, self.comm.rank,
+                                         data_parallel, pipeline_stages)
+        if self.plan.mode == "mp" and self.comm.active:
+            # one communicator per directed hand-off edge, created before any memory is measured
+            edges = []
+            for li in range(self.L - 1):
+                a, b = self.plan.owner_of_layer(li), self.plan.owner_of_layer(li + 1)
+                if a != b:
+                    edges.append((a, b))
+            self.comm.setup_p2p_edges(edges)
         attn_rows = qkv_chunk = 0
         self._outside = None
         if max_vram_gb:
@@ -123,6 +135,7 @@ class ShardedRunner:
                 # group this runner uses first (the data-parallel gather group)
                 if self.comm.active:
                     self.comm.warmup()
+                    self.comm.warmup_p2p()     # model parallel: the hand-off channels' buffers too
                     pcomm = getattr(prefetcher, "comm", None)
                     if pcomm is not None and pcomm is not self.comm:
                         pcomm.warmup()
@@ -146,10 +159,6 @@ class ShardedRunner:
         self.max_token_len = max_token_len
         self.resume_dir = resume_dir
         self.checkpoint_every = checkpoint_every
-        self.names = cfg.layer_names()
-        self.L = len(self.names)
-        self.plan: ShardPlan = make_plan(self.L, layer_num_per_shard, self.comm.world, self.comm.rank,
-                                         data_parallel, pipeline_stages)
         if self.cuda and cfg.head_dim not in (64, 96, 128):
             raise NotImplementedError(f"head_dim={cfg.head_dim}: the HIP attention kernels serve 64, 96 and 128")
         self.act_dtype = act_dtype or (torch.float16 if self.cuda else torch.float32)
@@ -184,13 +193,6 @@ class ShardedRunner:
             slots = self.prefetcher.planned_hbm_bytes()
             self.vram_plan["allocator_limit_bytes"] = cap_allocator(self.dev, int(max_vram_gb * 1e9), slots)
         self.stats: Dict[str, float] = {}
-        if self.plan.mode == "mp" and self.comm.active:
-            edges = []
-            for li in range(self.L - 1):
-                a, b = self.plan.owner_of_layer(li), self.plan.owner_of_layer(li + 1)
-                if a != b:
-                    edges.append((a, b))
-            self.comm.setup_p2p_edges(edges)
         self._fault = _parse_fault(self.comm.rank)
         self.h2d_stream = torch.cuda.Stream(self.dev) if self.cuda else None
         self.d2h_stream = torch.cuda.Stream(self.dev) if self.cuda else None

@@ -98,6 +98,26 @@ class Comm:
         for (a, b) in sorted(set(edges)):
             self._edge_groups[(a, b)] = dist.new_group(ranks=sorted([a, b]))
 
+    def warmup_p2p(self) -> None:
+        """One tiny send / receive on every directed hand-off edge (RCCL allocates a P2P channel's
+        buffers at its first use), so device memory measured afterwards includes them (ADVICE r2:
+        a VRAM cap).  Every rank walks the edges in one global order and completes each edge it is
+        on before the next (device-synchronised): the first edge not yet done always has both of
+        its ranks at it, so the chain cannot deadlock."""
+        if not self.active or not getattr(self, "_edge_groups", None):
+            return
+        dev = self.device if self.backend == "nccl" else torch.device("cpu")
+        t = torch.zeros(1, device=dev)
+        for (a, b) in sorted(self._edge_groups):
+            if self.rank == a:
+                self.isend(t, b).wait()
+            elif self.rank == b:
+                self.irecv(t, a).wait()
+            else:
+                continue
+            if dev.type == "cuda":
+                torch.cuda.synchronize(dev)
+
     def _group(self, src: int, dst: int):
         return getattr(self, "_edge_groups", {}).get((src, dst))
 

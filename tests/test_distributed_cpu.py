@@ -290,3 +290,26 @@ def test_moe_model_parallel_and_data_parallel(moe_single, tmp_path, mode):
     assert len(got) == len(ref)
     for a, b in zip(got, ref):
         assert _close(a, b)
+
+
+def _p2p_warmup_worker(rank, world, port, edges, out_dir):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    from flexible_llm_sharding_amd.parallel.comm import Comm
+    comm = Comm.from_env("cpu", timeout_s=60)
+    comm.setup_p2p_edges(edges)
+    comm.warmup_p2p()
+    comm.warmup_p2p()                      # idempotent: a second chain matches up the same way
+    comm.barrier()
+    with open(os.path.join(out_dir, f"ok{rank}"), "w") as f:
+        f.write("ok")
+    comm.destroy()
+
+
+@pytest.mark.parametrize("world,edges", [(2, [(0, 1), (1, 0)]), (3, [(0, 1), (1, 2), (2, 0), (2, 1)])])
+def test_p2p_warmup_chain_completes(tmp_path, world, edges):
+    """Comm.warmup_p2p (run before a VRAM cap measures device memory in model parallel): every
+    rank walks the directed hand-off edges in one order and finishes each before the next, so the
+    chain completes for edges in both directions and across more than two ranks."""
+    mp.spawn(_p2p_warmup_worker, args=(world, _port(), edges, str(tmp_path)), nprocs=world, join=True)
+    assert sorted(os.listdir(tmp_path)) == [f"ok{r}" for r in range(world)]
