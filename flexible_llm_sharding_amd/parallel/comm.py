@@ -213,6 +213,17 @@ class LoopbackHub:
         self.log: List[List[tuple]] = [[] for _ in range(world)]
         self._coll: dict = {}
         self._coll_round = [0] * world
+        self._dup_gen = [0] * world
+        self._children: dict = {}
+
+    def child(self, rank: int) -> "LoopbackHub":
+        """The hub of every rank's n-th ``dup()`` (one shared child per generation)."""
+        with self.cv:
+            gen = self._dup_gen[rank]
+            self._dup_gen[rank] += 1
+            if gen not in self._children:
+                self._children[gen] = LoopbackHub(self.world, self.timeout_s)
+            return self._children[gen]
 
     def exchange(self, rank: int, obj: Any) -> List[Any]:
         """All ranks deposit ``obj``; every rank gets the list (a blocking collective)."""
@@ -303,6 +314,16 @@ class _LoopWork:
         return op.done_ev is None or op.done_ev.query()
 
 
+class _DoneWork:
+    """Work of a loopback collective: ordered on the issuing stream when it returns."""
+
+    def wait(self) -> bool:
+        return True
+
+    def is_completed(self) -> bool:
+        return True
+
+
 class LoopbackComm(Comm):
     """``Comm`` for ``world`` ranks as threads of one process (tests / rehearsal): sends and
     receives are device copies ordered by events (no RCCL), collectives go through the hub."""
@@ -312,7 +333,43 @@ class LoopbackComm(Comm):
         self.hub = hub
 
     def dup(self) -> "LoopbackComm":
-        raise NotImplementedError("loopback comm: one communicator per world")
+        """Same thread ranks, own collective sequence (the data-parallel gathers)."""
+        return LoopbackComm(self.hub.child(self.rank), self.rank, self.device)
+
+    def all_gather_into(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False):
+        """``all_gather_into_tensor`` by device copies: every rank's ``inp`` lands in
+        ``out[r * n:(r + 1) * n]`` of every rank (``inp`` may already be this rank's place in
+        ``out``).  Like RCCL's, completion on the calling stream also covers the peers' reads of
+        this rank's ``inp``, so the caller may overwrite it after its stream passes this point:
+        the ranks exchange (input, ready event), copy the peers' slices on their current streams,
+        then exchange and wait for the copy events.  The host blocks until every rank has posted
+        (as gloo does); no device wait."""
+        n = inp.numel()
+        flat = out.view(-1)
+        cuda = inp.is_cuda
+        st = torch.cuda.current_stream(inp.device) if cuda else None
+        ev = None
+        if cuda:
+            ev = torch.cuda.Event()
+            ev.record(st)
+        peers = self.hub.exchange(self.rank, (inp, ev))
+        for r, (t, e) in enumerate(peers):
+            dst = flat[r * n:(r + 1) * n]
+            if r == self.rank:
+                if dst.data_ptr() != t.data_ptr():
+                    dst.copy_(t, non_blocking=cuda)
+                continue
+            if cuda:
+                st.wait_event(e)
+            dst.copy_(t, non_blocking=cuda)
+        done = None
+        if cuda:
+            done = torch.cuda.Event()
+            done.record(st)
+        for r, e in enumerate(self.hub.exchange(self.rank, done)):
+            if cuda and r != self.rank:
+                st.wait_event(e)
+        return _DoneWork()
 
     def setup_p2p_edges(self, edges) -> None:
         self._edge_groups = {}

@@ -206,3 +206,76 @@ def test_engine_contiguous_resident_micro_batch_major(deep6, tmp_path):
     for a, b in zip(owner[0], ref):
         assert np.abs(a.astype(np.float32) - b.astype(np.float32)).max() < 1e-5
     assert simulate_single_queue({r: hub.log[r] for r in range(3)})[0]
+
+
+def test_loopback_all_gather_in_place_and_dup():
+    """LoopbackComm.all_gather_into (the data-parallel weight gather over thread ranks): every
+    rank's slice lands in every rank's buffer, in place, across repeated rounds on a dup()'ed
+    communicator."""
+    from flexible_llm_sharding_amd.parallel.comm import LoopbackComm, LoopbackHub
+    hub = LoopbackHub(3, timeout_s=30)
+    res = {}
+
+    def run(r):
+        c = LoopbackComm(hub, r, "cpu").dup()
+        for it in range(3):
+            out = torch.zeros(12, dtype=torch.uint8)
+            mine = out[r * 4:(r + 1) * 4]
+            mine.fill_(10 * it + r + 1)
+            assert c.all_gather_into(out, mine).wait()
+            res[(r, it)] = out.tolist()
+
+    ts = [threading.Thread(target=run, args=(r,)) for r in range(3)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for r in range(3):
+        for it in range(3):
+            assert res[(r, it)] == sum([[10 * it + q + 1] * 4 for q in range(3)], [])
+
+
+@pytest.mark.parametrize("G", [2, 3])
+def test_data_parallel_over_loopback_threads(deep6, G):
+    """Data parallel with G ranks as threads (AllGatherPrefetcher: 1/G slices + loopback
+    all-gather into the weight slot): each rank's scores == a one-process run on its prompts,
+    over two calls (slot rotation across calls)."""
+    import numpy as np
+    from flexible_llm_sharding_amd.engine import ShardedRunner
+    from flexible_llm_sharding_amd.parallel.comm import LoopbackComm, LoopbackHub
+    from flexible_llm_sharding_amd.parallel.data_parallel import AllGatherPrefetcher, SlicedHostStore
+    from flexible_llm_sharding_amd.parallel.planner import make_plan
+    from flexible_llm_sharding_amd.runtime.stream import FileLayerSource
+    cfg, path, tok, prompts, _ = deep6
+    torch.set_num_threads(1)
+    idx = np.array_split(np.arange(len(prompts)), G)
+    hub = LoopbackHub(G, timeout_s=60)
+    names = cfg.layer_names()
+    res = {}
+
+    def run(r):
+        try:
+            comm = LoopbackComm(hub, r, "cpu")
+            store = SlicedHostStore.from_source(FileLayerSource(cfg, path), r, G, pinned=False)
+            plan = make_plan(len(names), 1, G, r, True)
+            pf = AllGatherPrefetcher(store, names, [s for s in plan.my_shards if len(s)], torch.device("cpu"), comm)
+            rr = ShardedRunner(cfg, store, "cpu", tok, layer_num_per_shard=1, storage_location="gpu", comm=comm,
+                               data_parallel=True, prefetcher=pf, token_budget=40)
+            mine = [prompts[i] for i in idx[r]]
+            res[r] = [rr(mine) for _ in range(2)]
+        except BaseException as e:  # noqa: BLE001
+            res[r] = e
+
+    ts = [threading.Thread(target=run, args=(r,)) for r in range(G)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for r in range(G):
+        if isinstance(res[r], BaseException):
+            raise res[r]
+        want = ShardedRunner(cfg, FileLayerSource(cfg, path), "cpu", tok, token_budget=40)([prompts[i] for i in idx[r]])
+        for call in res[r]:
+            assert len(call) == len(want)
+            for a, b in zip(call, want):
+                assert np.abs(a.astype(np.float32) - b.astype(np.float32)).max() < 1e-5
