@@ -13,6 +13,7 @@ own weight layout (``wqkv = [q; k; v]``, ``wgu = [gate; up]``).
 from __future__ import annotations
 
 import os
+import threading
 from dataclasses import dataclass
 
 import torch
@@ -98,27 +99,31 @@ class HipOps:
         return out
 
     def _splitk_ws(self, device, M: int, N: int):
-        """fp32 partials of the small-M split-K GEMM path (csrc/kernels/gemm.hip): one fixed-size
-        buffer per device, reserved once (``reserve_splitk_ws``; the engine does it before planning
-        a VRAM cap) and never resized, so which GEMM path a shape takes — and its rounding — does not
-        depend on what the allocator could give at the time.  The GEMMs of a device run on one
-        stream in order, so they share it.  None (mid-M kernel) if it could not be reserved."""
-        if device not in self._ws:
+        """fp32 partials of the small-M split-K GEMM path (csrc/kernels/gemm.hip) and of the
+        split-KV attention: one fixed-size buffer per (device, host thread), reserved once
+        (``reserve_splitk_ws``; the engine does it before planning a VRAM cap) and never resized, so
+        which GEMM path a shape takes — and its rounding — does not depend on what the allocator
+        could give at the time.  A runner's kernels run on one stream in order, so its GEMMs and
+        attention share it; runners of one process driven from different threads (ranks as threads
+        on one GPU) each get their own, since their multi-kernel sequences (partials, then reduce)
+        can interleave even on a shared stream.  None (mid-M kernel) if it could not be reserved."""
+        key = (torch.device(device), threading.get_ident())
+        if key not in self._ws:
             self.reserve_splitk_ws(device)
-        return self._ws[device]
+        return self._ws[key]
 
     def reserve_splitk_ws(self, device, allocate: bool = True):
-        """Decide the device's split-K scratch once: allocate it (``allocate``) or go without (a
-        VRAM-capped runner: the 70B plan has no 64 MB to spare and its small-M GEMMs are the pruned
-        last layer's).  -> bytes reserved."""
-        device = torch.device(device)
-        if device not in self._ws:
+        """Decide this thread's split-K scratch on the device once: allocate it (``allocate``) or go
+        without (a VRAM-capped runner: the 70B plan has no 64 MB to spare and its small-M GEMMs are
+        the pruned last layer's).  -> bytes reserved."""
+        key = (torch.device(device), threading.get_ident())
+        if key not in self._ws:
             try:
-                self._ws[device] = (torch.empty(SPLITK_WS_BYTES, dtype=torch.uint8, device=device)
-                                    if allocate else None)
+                self._ws[key] = (torch.empty(SPLITK_WS_BYTES, dtype=torch.uint8, device=key[0])
+                                 if allocate else None)
             except RuntimeError:
-                self._ws[device] = None
-        ws = self._ws[device]
+                self._ws[key] = None
+        ws = self._ws[key]
         return 0 if ws is None else ws.numel()
 
     def gemv_skinny(self, x, w):
