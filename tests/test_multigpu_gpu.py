@@ -3,7 +3,9 @@
 * One GPU: two pipeline ranks as threads over :class:`LoopbackComm` (device copies ordered
   by events, no RCCL) at Llama-2-7B geometry drive the real :class:`StageInbox` — fixed HBM
   receive ring, wrap-around parking in HBM / pinned RAM / disk — and must reproduce the 1-GPU
-  scores bitwise with memory high-water marks that do not grow with the micro-batch count.
+  scores bitwise with memory high-water marks that do not grow with the micro-batch count;
+  2 / 4 data-parallel ranks as threads drive the real :class:`AllGatherPrefetcher` (1/G slices
+  H2D'd into their places in the HBM slot, loopback all-gather) to the same bitwise standard.
 * Two or more GPUs (skipped below that): model-parallel (round-robin and contiguous stages,
   storage gpu / cpu / disk) and data-parallel (pinned slices and streamed files) over RCCL
   against the 1-GPU run, and ``bench.py --gpus 2`` on a real 2-rank ``nccl`` group.
@@ -106,6 +108,58 @@ def test_stage_inbox_loopback_7b_bounded(seven_b, tmp_path, storage):
         seen[n_prompts] = (ring, s0["rx_max_parked_bytes_gpu"], s0["rx_max_parked_bytes_cpu"])
     (ra, ga, ca), (rb, gb, cb) = seen[12], seen[24]
     assert ra == rb and ga == gb and ca == cb
+
+
+@pytest.mark.parametrize("G", [2, 4])
+def test_data_parallel_loopback_7b(seven_b, G):
+    """Data parallel with G ranks as threads on ONE GPU: each rank holds 1/G of every layer in
+    pinned RAM, H2Ds only its slice into its place in the HBM slot on the prefetcher's copy stream,
+    and the loopback all-gather (device copies ordered by events, parallel/comm.py) completes the
+    layer before compute; two calls (slot rotation across calls).  Each rank's scores must equal
+    the 1-GPU run on its prompts bitwise: the weights are assembled exactly."""
+    from flexible_llm_sharding_amd.parallel.data_parallel import AllGatherPrefetcher, SlicedHostStore
+    from flexible_llm_sharding_amd.parallel.planner import make_plan
+    cfg, full, tok = seven_b
+    dev = torch.device("cuda", 0)
+    prompts = synthetic_prompts(4 * G, 1024, 5, 64, cfg.vocab_size, seed=G)
+    idx = np.array_split(np.arange(len(prompts)), G)
+    names = cfg.layer_names()
+    stores = [SlicedHostStore.synthetic(cfg, dev, r, G, seed=5) for r in range(G)]   # seven_b's seed
+    hub = LoopbackHub(G, timeout_s=120)
+    res, runners = {}, {}
+
+    def run(r):
+        try:
+            torch.cuda.set_device(0)
+            comm = LoopbackComm(hub, r, "cuda:0")
+            plan = make_plan(len(names), 1, G, r, True)
+            pf = AllGatherPrefetcher(stores[r], names, [s for s in plan.my_shards if len(s)], dev, comm)
+            rr = ShardedRunner(cfg, stores[r], "cuda:0", tok, layer_num_per_shard=1, storage_location="gpu",
+                               comm=comm, data_parallel=True, prefetcher=pf, token_budget=4096)
+            runners[r] = rr
+            mine = [prompts[i] for i in idx[r]]
+            res[r] = [rr(mine) for _ in range(2)]
+        except BaseException as e:  # noqa: BLE001
+            res[r] = e
+
+    ts = [threading.Thread(target=run, args=(r,)) for r in range(G)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=300)
+    for r in range(G):
+        assert not isinstance(res.get(r), BaseException), res.get(r)
+    torch.cuda.synchronize()
+    for rr in runners.values():
+        rr.close()
+    one = ShardedRunner(cfg, full, "cuda:0", tok, layer_num_per_shard=1, storage_location="gpu", token_budget=4096)
+    for r in range(G):
+        want = one([prompts[i] for i in idx[r]])
+        for call in res[r]:
+            for a, b in zip(want, call):
+                assert np.isfinite(a.astype(np.float32)).all()
+                assert np.array_equal(a, b)
+    one.close()
 
 
 # --------------------------------------------------------------------------- >= 2 GPUs
