@@ -449,7 +449,7 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
 
 }  // namespace
 
-extern "C" int fls_kernels_version(void) { return 15; }
+extern "C" int fls_kernels_version(void) { return 16; }
 
 // tile order: 0 = by shape (default); g > 0: groups of g M tiles; g < 0: groups of -g N tiles (A/B, tests)
 extern "C" int fls_gemm_set_order(int order) {
@@ -486,6 +486,11 @@ extern "C" int fls_gemm_set_mid(int on) {
   return old;
 }
 
+// gemm_v11.hip: the 384 x 256 tile for large projections (returns 1 when it took the GEMM)
+extern "C" int fls_gemm_v11_try(const void* A, const void* W, void* C, const void* R, int M, int N, int K, int lda,
+                                int ldw, int ldc, int ldr, int epi, const int* pos, const float* cos_t,
+                                const float* sin_t, int rope_cols, int head_dim, const void* bias, fls_stream_t s);
+
 extern "C" int fls_gemm(const void* A, const void* W, void* C, const void* R, int M, int N, int K, int lda, int ldw,
                         int ldc, int ldr, int epi, const int* pos, const float* cos_t, const float* sin_t,
                         int rope_cols, int head_dim, const void* bias, void* ws, uint64_t ws_bytes,
@@ -495,6 +500,11 @@ extern "C" int fls_gemm(const void* A, const void* W, void* C, const void* R, in
   if ((epi == FLS_EPI_SWIGLU || epi == FLS_EPI_ROPE) && (N % 32)) return -2;
   if (epi == FLS_EPI_ROPE && ((head_dim != 64 && head_dim != 128) || rope_cols % head_dim || N % head_dim))
     return -3;
+  if (g_gu_split <= 1 || epi != FLS_EPI_SWIGLU) {
+    const int rc = fls_gemm_v11_try(A, W, C, R, M, N, K, lda, ldw, ldc, ldr, epi, pos, cos_t, sin_t, rope_cols,
+                                    head_dim, bias, s);
+    if (rc) return rc > 0 ? 0 : rc;
+  }
   Epi ep{(const half_t*)R, ldr, pos, cos_t, sin_t, rope_cols, head_dim, (const half_t*)bias, N / 2, 0,
          nullptr, nullptr, nullptr, 0, 0};
   auto a = (const half_t*)A;

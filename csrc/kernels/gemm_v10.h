@@ -145,16 +145,16 @@ __device__ __forceinline__ void unwide_pair(uint4 v, half4& a, half4& b) {
 // (wide_pair).  Row group u+1's cos/sin loads are issued before row group u's stores (the
 // tables cannot alias C, so a fence keeps the compiler from hoisting all 8 rows' loads and
 // spilling).
-template <int HD>
+template <int HD, int U = 8, bool LO = false>
 __device__ __forceinline__ void epilogue_rope(half_t* __restrict__ C, int ldc, int M, int mrow0, int ncol0, int grp,
-                                              floatx4 (&acc)[8][8], const Epi& ep) {
+                                              floatx4 (&acc)[U][8], const Epi& ep, int mlo = 0) {
   constexpr int HS = HD / 32;
   constexpr int HALF = HD / 2;
   const int off = 4 * grp;
   const int woff = wide_off(grp);
-  int pos[8];
+  int pos[U];
 #pragma unroll
-  for (int u = 0; u < 8; ++u) pos[u] = ep.pos[min(mrow0 + u * 16, M - 1)];
+  for (int u = 0; u < U; ++u) pos[u] = ep.pos[min(mrow0 + u * 16, M - 1)];
   int f0[4];
   bool rot[4];
   half4 ba[4], bb[4];
@@ -184,9 +184,9 @@ __device__ __forceinline__ void epilogue_rope(half_t* __restrict__ C, int ldc, i
   };
   load(0, 0);
 #pragma unroll
-  for (int u = 0; u < 8; ++u) {
+  for (int u = 0; u < U; ++u) {
     const int sl = u & 1;
-    if (u + 1 < 8) load(u + 1, sl ^ 1);
+    if (u + 1 < U) load(u + 1, sl ^ 1);
     asm volatile("" ::: "memory");
     const int m = mrow0 + u * 16;
     half4 oa[4], ob[4];
@@ -212,7 +212,7 @@ __device__ __forceinline__ void epilogue_rope(half_t* __restrict__ C, int ldc, i
       const uint4 va = wide_pair(oa[q], oa[q + 1]);
       const uint4 vb = wide_pair(ob[q], ob[q + 1]);
       half_t* cp = C + (size_t)m * ldc + ncol0 + ta * 16 + woff;
-      if (m < M) {
+      if (m < M && (!LO || m >= mlo)) {
         *(uint4*)cp = va;
         *(uint4*)(cp + HALF) = vb;
       }
@@ -224,25 +224,28 @@ __device__ __forceinline__ void epilogue_rope(half_t* __restrict__ C, int ldc, i
 // 16-byte stores throughout (wide_pair).  Row group u+1's operand loads (residual rows) are issued
 // before row group u's stores (different rows, so in-place R == C stays correct); the per-column
 // bias is loaded once.
-template <int EPI>
+// U row groups (v10: 8; v11: 12).  LO: the block stores only rows >= mlo (v11's last M tile is
+// shifted back to end at row M, so it recomputes rows its neighbour owns; storing them twice
+// would be wrong for the in-place residual).
+template <int EPI, int U = 8, bool LO = false>
 __device__ __forceinline__ void epilogue_quadrant(half_t* __restrict__ C, int ldc, int M, int mrow0, int ncol0,
-                                                  int grp, floatx4 (&acc)[8][8], const Epi& ep) {
+                                                  int grp, floatx4 (&acc)[U][8], const Epi& ep, int mlo = 0) {
   if constexpr (EPI == EPI_F32) {                    // split-K partial: fp32, ldc in floats
     float* Cf = (float*)C;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < U; ++u) {
       const int m = mrow0 + u * 16;
-      if (m < M) {
+      if (m < M && (!LO || m >= mlo)) {
 #pragma unroll
         for (int t = 0; t < 8; ++t) *(floatx4*)(Cf + (size_t)m * ldc + ncol0 + t * 16 + 4 * grp) = acc[u][t];
       }
     }
     return;
   } else if constexpr (EPI == FLS_EPI_ROPE) {
-    epilogue_rope<128>(C, ldc, M, mrow0, ncol0, grp, acc, ep);
+    epilogue_rope<128, U, LO>(C, ldc, M, mrow0, ncol0, grp, acc, ep, mlo);
     return;
   } else if constexpr (EPI == EPI_ROPE64) {
-    epilogue_rope<64>(C, ldc, M, mrow0, ncol0, grp, acc, ep);
+    epilogue_rope<64, U, LO>(C, ldc, M, mrow0, ncol0, grp, acc, ep, mlo);
     return;
   } else {
     const int off = 4 * grp;
@@ -250,7 +253,7 @@ __device__ __forceinline__ void epilogue_quadrant(half_t* __restrict__ C, int ld
     if constexpr (EPI == FLS_EPI_SWIGLU) {
       // pair p -> intermediate columns [ncol0/2 + 16p, +16); pairs (p, p+1) share one 16-B store
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < U; ++u) {
         const int m = mrow0 + u * 16;
         half4 o[4];
 #pragma unroll
@@ -260,7 +263,7 @@ __device__ __forceinline__ void epilogue_quadrant(half_t* __restrict__ C, int ld
 #pragma unroll
         for (int p = 0; p < 4; p += 2) {
           const uint4 v = wide_pair(o[p], o[p + 1]);
-          if (m < M) *(uint4*)(C + (size_t)m * ldc + ncol0 / 2 + p * 16 + woff) = v;
+          if (m < M && (!LO || m >= mlo)) *(uint4*)(C + (size_t)m * ldc + ncol0 / 2 + p * 16 + woff) = v;
         }
       }
       return;
@@ -288,9 +291,9 @@ __device__ __forceinline__ void epilogue_quadrant(half_t* __restrict__ C, int ld
       auto body = [&](auto has_bias) {
         load(0, 0);
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < U; ++u) {
           const int sl = u & 1;
-          if (u + 1 < 8) load(u + 1, sl ^ 1);
+          if (u + 1 < U) load(u + 1, sl ^ 1);
           asm volatile("" ::: "memory");
           const int m = mrow0 + u * 16;
 #pragma unroll
@@ -310,7 +313,7 @@ __device__ __forceinline__ void epilogue_quadrant(half_t* __restrict__ C, int ld
 #pragma unroll
             for (int r = 0; r < 4; ++r) { oa[r] = (half_t)a[r]; ob[r] = (half_t)b[r]; }
             const uint4 v = wide_pair(oa, ob);
-            if (m < M) *(uint4*)(C + (size_t)m * ldc + ncol0 + p * 32 + woff) = v;
+            if (m < M && (!LO || m >= mlo)) *(uint4*)(C + (size_t)m * ldc + ncol0 + p * 32 + woff) = v;
           }
         }
       };

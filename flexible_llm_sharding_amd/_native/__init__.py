@@ -63,7 +63,7 @@ class Piece(ctypes.Structure):
                 ("kind", ctypes.c_int32), ("pad", ctypes.c_int32)]
 
 
-KERNELS_ABI = 15   # bumped whenever a C signature in csrc/include/fls.h changes
+KERNELS_ABI = 16   # bumped whenever a C signature in csrc/include/fls.h changes
 
 
 def _load_kernels():
@@ -91,6 +91,8 @@ def _load_kernels():
     _bind(lib, "fls_moe_combine", c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
           c_int, c_int, c_void_p)
     _bind(lib, "fls_gemm_set_order", c_int, c_int)
+    _bind(lib, "fls_gemm_set_v11", c_int, c_int)
+    _bind(lib, "fls_gemm_v11_tune", None, c_int, c_int)
     _bind(lib, "fls_attention_set_hpb", c_int, c_int)
     _bind(lib, "fls_attention_set_split", c_int, c_int)
     _bind(lib, "fls_attention", c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,

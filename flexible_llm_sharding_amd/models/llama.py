@@ -181,15 +181,20 @@ def run_embed(ctx: ExecContext, W: Dict[str, torch.Tensor], meta: dict) -> torch
     return ctx.ops.embed(meta["ids"], W["embed"], ctx.act_dtype)
 
 
-def balanced_step(rows: int, limit: int, align: int = 256) -> int:
+def balanced_step(rows: int, limit: int, align: int = 768) -> int:
     """Rows per chunk when ``rows`` are cut into the fewest chunks of <= ``limit`` rows, sized
-    evenly (GEMM tile rounds: 43,008 rows under a 16,384 limit -> 3 x 14,336, not 16k+16k+10k)."""
+    evenly (GEMM tile rounds: 43,008 rows under a 16,384 limit -> 14,592 + 14,592 + 13,824, not
+    16k+16k+10k).  Chunks are multiples of 768 = lcm of the 256-row (v10) and 384-row (v11,
+    csrc/kernels/gemm_v11.hip) GEMM tiles, so no chunk pads a tile; 256 when 768 does not fit."""
     if limit <= 0 or rows <= limit:
         return max(rows, 1)
     n = -(-rows // limit)
     step = -(-rows // n)
-    step = -(-step // align) * align
-    return min(step, limit) if step <= limit else limit
+    for a in (align, 256):
+        s = -(-step // a) * a
+        if s <= limit:
+            return s
+    return limit
 
 
 def _attn_inputs(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, pos: torch.Tensor,

@@ -272,6 +272,23 @@ def test_fill_random(ops):
     assert abs(f.mean().item()) < 0.01 and abs(f.std().item() - 1) < 0.01
 
 
+@pytest.mark.parametrize("M", [17, 100, 517])
+def test_gemm_mid_rope64(ops, ref, M):
+    """mid-M kernel, RoPE epilogue with head_dim 64 (partner column 2 subtiles away) vs fp32."""
+    from flexible_llm_sharding_amd.config import ModelConfig
+    from flexible_llm_sharding_amd.models.llama import rope_tables
+    H, nh, nkv, hd = 512, 8, 2, 64
+    x = rnd(M, H, seed=51)
+    wqkv = rnd((nh + 2 * nkv) * hd, H, scale=0.05, seed=52)
+    pos = torch.randint(0, 4000, (M,), dtype=torch.int32, device=DEV)
+    cfg = ModelConfig(hidden_size=nh * hd, num_attention_heads=nh, num_key_value_heads=nkv)
+    cos, sin = rope_tables(cfg, 4096)
+    y = ops.gemm(x, wqkv, EPI_ROPE, positions=pos, cos=cos.to(DEV), sin=sin.to(DEV),
+                 rope_cols=(nh + nkv) * hd, head_dim=hd)
+    r = ref.qkv_rope(x.float().cpu(), wqkv.float().cpu(), pos.cpu(), cos, sin, nh, nkv, hd)
+    assert rel_err(y.cpu(), r) < 3e-3
+
+
 @pytest.mark.parametrize("M", [1, 17, 64, 100, 416, 517, 1000])
 def test_gemm_mid_all_epilogues(ops, ref, M):
     """64x128-tile mid-M kernel (chosen when 256x256 tiles cannot fill the chip) vs fp32 references."""
@@ -580,3 +597,77 @@ def test_gemm_row_chunks_bitwise(ops, epi):
         ops.k.fls_gemm_set_row_chunk(old)
     torch.cuda.synchronize()
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("M", [384, 768, 1000, 1537])
+@pytest.mark.parametrize("epi", ["none", "resid", "rope", "rope64", "swiglu", "bias"])
+def test_gemm_v11_bitwise_vs_v10(ops, ref, M, epi):
+    """gemm_nt_v11 (384 x 256 tile, gemm_v11.hip) accumulates every output in the same k order as
+    v10, so every epilogue but RoPE (FMA contraction, <= 1 ulp) is bitwise equal to v10 -- including ragged M, where v11's last tile is
+    shifted back and must not store its neighbour's rows twice (in-place residual)."""
+    from flexible_llm_sharding_amd.config import ModelConfig
+    from flexible_llm_sharding_amd.models.llama import rope_tables
+    K = 384                                            # 6 K-tiles (v11 needs an even count)
+    x = rnd(M, K, seed=31)
+    pos = torch.randint(0, 4000, (M,), dtype=torch.int32, device=DEV)
+    hd = 64 if epi == "rope64" else 128
+    cfg = ModelConfig(hidden_size=1024, num_attention_heads=1024 // hd, num_key_value_heads=2)
+    cos, sin = rope_tables(cfg, 4096)
+    cos, sin = cos.to(DEV), sin.to(DEV)
+    w = rnd(1024, K, scale=0.05, seed=32)
+    b = rnd(1024, scale=0.1, seed=33)
+    r0 = rnd(M, 1024, seed=34)
+
+    def run():
+        if epi == "resid":
+            return ops.linear_residual(x, w, r0.clone())
+        if epi.startswith("rope"):
+            nh = 1024 // hd
+            return ops.qkv_rope(x, w, pos, cos, sin, nh - 4, 2, hd)
+        if epi == "swiglu":
+            return ops.swiglu_up(x, w)
+        if epi == "bias":
+            return ops.linear_residual(x, w, r0.clone(), bias=b)
+        return ops.linear(x, w)
+    old = ops.k.fls_gemm_set_v11(2)
+    old_mid = ops.k.fls_gemm_set_mid(0)      # the v10 arm runs v10, not the 64 x 128 mid-M kernel
+    try:
+        a = run()
+        ops.k.fls_gemm_set_v11(0)
+        v10 = run()
+    finally:
+        ops.k.fls_gemm_set_v11(old)
+        ops.k.fls_gemm_set_mid(old_mid)
+    torch.cuda.synchronize()
+    if epi.startswith("rope"):
+        nh = 1024 // hd
+        r = ref.qkv_rope(x.float().cpu(), w.float().cpu(), pos.cpu(), cos.cpu(), sin.cpu(), nh - 4, 2, hd)
+        assert rel_err(a.cpu(), r) < 3e-3
+        # the rotation's FMA contraction may differ between the two kernels' epilogues: <= 1 ulp
+        af, bf = a.float(), v10.float()
+        assert bool(((af - bf).abs() <= torch.maximum(af.abs(), bf.abs()) * 2.0 ** -10 + 1e-7).all())
+    else:
+        assert torch.equal(a, v10)
+    if epi == "none":
+        assert rel_err(a, x.float() @ w.float().t()) < 2e-3
+
+
+def test_gemm_v11_production_shape_bitwise(ops):
+    """A 70B O-projection-sized launch (43,008 x 8,192 x 8,192 would take 2 GB; 4,608 rows keep the
+    full N / K): v11 in auto mode vs v10, bitwise, and vs fp32 on a row sample."""
+    M, N, K = 4608, 8192, 8192
+    x = rnd(M, K, seed=41)
+    w = rnd(N, K, scale=0.02, seed=42)
+    r0 = rnd(M, N, seed=43)
+    old = ops.k.fls_gemm_set_v11(1)
+    try:
+        a = ops.linear_residual(x, w, r0.clone())
+        ops.k.fls_gemm_set_v11(0)
+        b = ops.linear_residual(x, w, r0.clone())
+    finally:
+        ops.k.fls_gemm_set_v11(old)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    rows = torch.arange(0, M, 97, device=DEV)
+    want = x[rows].float() @ w.float().t() + r0[rows].float()
+    assert rel_err(a[rows], want) < 2e-3
