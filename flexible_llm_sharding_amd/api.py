@@ -98,19 +98,33 @@ def repeated_passes(args) -> bool:
 
 def resolve_prefix_kv_cache(args) -> bool:
     """``--prefix_kv_cache auto``: on for greedy generation (exact: later steps re-score the same
-    prefixes, runtime/prefix_cache.py)."""
+    prefixes, runtime/prefix_cache.py) unless ``--max_vram_gb`` caps the device memory: the cache
+    holds every prompt's K/V for every layer (~320 KB per token for 70B), which no capped plan can
+    hold; asking for both explicitly is an error."""
     v = getattr(args, "prefix_kv_cache", False)
+    capped = bool(getattr(args, "max_vram_gb", None))
     if v == "auto":
-        return getattr(args, "num_gen_token", 1) > 1 and not getattr(args, "resume_dir", None)
+        return getattr(args, "num_gen_token", 1) > 1 and not getattr(args, "resume_dir", None) and not capped
+    if v and capped:
+        raise ValueError("--prefix_kv_cache keeps every prompt's K/V of every layer in HBM, outside the "
+                         "--max_vram_gb plan: use one or the other")
     return bool(v)
 
 
-def prefix_kv_bytes(cfg: ModelConfig, tok, prompts, n_decoders: int, elem: int = 2) -> int:
-    """HBM the prefix K/V cache needs for ``prompts`` (post-RoPE K and V of every prefix token,
-    every decoder layer this rank runs)."""
+def prefix_kv_bytes(cfg: ModelConfig, tok, prompts, n_decoders: int, elem: int = 2,
+                    suffix_kv_cache: bool = False) -> int:
+    """HBM the prefix K/V cache needs for ``prompts``: post-RoPE K and V of every prefix token, and
+    with ``suffix_kv_cache`` every suffix's region too (its tokens + ``PrefixKVCache.SUFFIX_GROWTH``
+    rows, as ``PrefixKVCache.begin`` sizes them), for every decoder layer this rank runs."""
     if tok is None or not prompts:
         return 0
+    from .runtime.prefix_cache import PrefixKVCache
     n = sum(len(tok(p[0]).input_ids) for p in prompts)
+    if suffix_kv_cache:
+        for p in prompts:
+            sfx = list(p[1])
+            if sfx:
+                n += sum(len(ids) + PrefixKVCache.SUFFIX_GROWTH for ids in tok(sfx).input_ids)
     return n * 2 * cfg.num_key_value_heads * cfg.head_dim * elem * n_decoders
 
 
@@ -147,7 +161,8 @@ def build_runner(args, cfg: ModelConfig, device, comm: Comm, tok, prompts=None) 
     n_dec = sum(1 for n in cfg.layer_names() if layer_kind(n) == "decoder")
     if not args.data_parallel and comm.world > 1:
         n_dec = -(-n_dec // comm.world)
-    reserve = prefix_kv_bytes(cfg, tok, prompts, n_dec) if pkv else 0
+    reserve = prefix_kv_bytes(cfg, tok, prompts, n_dec,
+                              suffix_kv_cache=getattr(args, "suffix_kv_cache", False)) if pkv else 0
     if args.data_parallel and comm.world > 1 and args.dp_weight_shard:
         from .parallel.data_parallel import build_dp_sharded_runner
         hv = getattr(args, "hbm_cache_gb", 0.0)
@@ -179,7 +194,7 @@ def build_runner(args, cfg: ModelConfig, device, comm: Comm, tok, prompts=None) 
                          hbm_cache_gb=resolve_hbm_cache_gb(args, cfg, device, reserve),
                          prefix_kv_cache=pkv,
                          prefix_cache_entries=getattr(args, "prefix_cache_entries", 8),
-                         suffix_kv_cache=getattr(args, "suffix_kv_cache", True),
+                         suffix_kv_cache=getattr(args, "suffix_kv_cache", False),
                          pipeline_stages=getattr(args, "pipeline_stages", "round_robin"),
                          rx_window=getattr(args, "rx_window", 2),
                          max_vram_gb=getattr(args, "max_vram_gb", None))

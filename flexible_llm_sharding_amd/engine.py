@@ -76,7 +76,7 @@ class ShardedRunner:
                  mlp_chunk: Optional[int] = None, prefetcher: Optional[ShardPrefetcher] = None,
                  verbose: bool = False, resume_dir: Optional[str] = None, checkpoint_every: int = 0,
                  max_token_len: int = MAX_TOKEN_LEN, hip_graphs: bool = False,
-                 prefix_kv_cache: bool = False, prefix_cache_entries: int = 8, suffix_kv_cache: bool = True,
+                 prefix_kv_cache: bool = False, prefix_cache_entries: int = 8, suffix_kv_cache: bool = False,
                  prune_last_layer: bool = True, pipeline_stages: str = "round_robin",
                  max_vram_gb: Optional[float] = None, hbm_cache_gb: float = 0.0, rx_window: int = 2):
         self.cfg = cfg
@@ -124,6 +124,10 @@ class ShardedRunner:
             self.comm.setup_p2p_edges(edges)
         attn_rows = qkv_chunk = 0
         self._outside = None
+        self.ops = get_ops(self.dev)
+        # this runner's split-K / split-KV scratch: reserved before any memory is planned, so a
+        # capped and an uncapped run take the same GEMM paths (bitwise-equal scores)
+        self._splitk_ws = self.ops.new_workspace(self.dev) if hasattr(self.ops, "new_workspace") else None
         if max_vram_gb:
             # size the micro-batch and the QKV / MLP chunks to the HBM cap (runtime/memplan.py);
             # re-planned per call once its token count is known (_plan_call)
@@ -139,8 +143,8 @@ class ShardedRunner:
                     pcomm = getattr(prefetcher, "comm", None)
                     if pcomm is not None and pcomm is not self.comm:
                         pcomm.warmup()
-                # small-M split-K scratch: only if an earlier runner of this process reserved it
-                ws = get_ops(self.dev).reserve_splitk_ws(self.dev, allocate=False)
+                # + the split-K scratch (allocator memory, outside the activation plan)
+                ws = self._splitk_ws.numel() if self._splitk_ws is not None else 0
                 self._outside = (device_used_bytes(self.dev) - torch.cuda.memory_reserved(self.dev) + (64 << 20)
                                  + ws)
             try:
@@ -165,7 +169,6 @@ class ShardedRunner:
         # multi-head models (odd GQA group): 128-row attention items, 4 waves share each K/V tile
         mha = (cfg.num_attention_heads // cfg.num_key_value_heads) % 2 == 1
         self.q_block = Q_BLOCK_MHA if (self.cuda and mha) else Q_BLOCK
-        self.ops = get_ops(self.dev)
         cos, sin = rope_tables(cfg, max(cfg.max_position_embeddings, max_token_len),
                                torch.float16, self.dev)
         self.ctx = ExecContext(cfg, self.ops, self.dev, self.act_dtype, cos, sin, mlp_chunk, qkv_chunk=qkv_chunk,
@@ -251,6 +254,13 @@ class ShardedRunner:
         out = self.run_tokenized(tps)
         self.stats["host_tokenize_s"] = t_tok
         return out
+
+    def _workspace(self):
+        """This runner's split-K scratch installed for the calling thread (ops/hip_backend.py)."""
+        if self._splitk_ws is None:
+            import contextlib
+            return contextlib.nullcontext()
+        return self.ops.use_workspace(self._splitk_ws)
 
     def _get_inbox(self) -> StageInbox:
         if self._inbox is None:
@@ -345,10 +355,12 @@ class ShardedRunner:
                    for g in groups]
         t_pack = time.perf_counter() - t_start
         if self.hip_graphs:
-            return self._run_graphed(tps, batches, t_start)
+            with self._workspace():
+                return self._run_graphed(tps, batches, t_start)
         self.ctx.prefix_entry = entry
         try:
-            outputs = self._run_batches(tps, batches, t_start)
+            with self._workspace():
+                outputs = self._run_batches(tps, batches, t_start)
         except BaseException:
             if entry is not None and not cached:
                 self.prefix_cache.drop(entry)
@@ -540,6 +552,11 @@ class ShardedRunner:
                 if ck is not None and not mp and self._ckpt_due(k):
                     ck.save_state(self._ckpt_key(k), b, state)     # single / DP: a shard's outputs
                 send_w = None
+                if from_rx and last < self.L - 1 and dst_rank == comm.rank:
+                    # the residual GEMMs update the received state in place, so it may still BE the
+                    # receive-ring slot that inbox.release() hands to the next receive: a state that
+                    # stays on this rank (contiguous stages) leaves the slot first
+                    state = state.clone()
                 if last == self.L - 1:
                     out_pending.append(self._start_output_copy(batch, state))
                 elif dst_rank != comm.rank:
@@ -853,3 +870,4 @@ class ShardedRunner:
         if self._store is not None:
             self._store.close()
             self._store = None
+        self._splitk_ws = None

@@ -17,6 +17,7 @@ PyTorch on CPU).
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import Dict, Optional
 
@@ -181,16 +182,21 @@ def run_embed(ctx: ExecContext, W: Dict[str, torch.Tensor], meta: dict) -> torch
     return ctx.ops.embed(meta["ids"], W["embed"], ctx.act_dtype)
 
 
-def balanced_step(rows: int, limit: int, align: int = 768) -> int:
+CHUNK_ALIGN = int(os.environ.get("FLS_CHUNK_ALIGN", "3072"))   # A/B knob (256: round 3's chunks)
+
+
+def balanced_step(rows: int, limit: int, align: int = 0) -> int:
     """Rows per chunk when ``rows`` are cut into the fewest chunks of <= ``limit`` rows, sized
-    evenly (GEMM tile rounds: 43,008 rows under a 16,384 limit -> 14,592 + 14,592 + 13,824, not
-    16k+16k+10k).  Chunks are multiples of 768 = lcm of the 256-row (v10) and 384-row (v11,
-    csrc/kernels/gemm_v11.hip) GEMM tiles, so no chunk pads a tile; 256 when 768 does not fit."""
+    evenly (43,008 rows under a 16,384 limit -> 15,360 + 15,360 + 12,288, not 16k+16k+10k).
+    Chunks are multiples of 3,072 = 8 of v11's 384-row GEMM tiles (csrc/kernels/gemm_v11.hip):
+    with 32 or 224 column tiles (the 70B O / down and gate/up projections) every launch is then a
+    whole number of 256-CU tile rounds, no tail round; else of 768 = lcm(256, 384) (no chunk pads
+    a v10 or v11 tile), else of 256."""
     if limit <= 0 or rows <= limit:
         return max(rows, 1)
     n = -(-rows // limit)
     step = -(-rows // n)
-    for a in (align, 256):
+    for a in (align or CHUNK_ALIGN, 768, 256):
         s = -(-step // a) * a
         if s <= limit:
             return s

@@ -64,8 +64,13 @@ class HipOps:
     def __init__(self):
         self.k = _native.kernels()
         self._ws = {}
+        self._tl = threading.local()
         if os.environ.get("FLS_SPLITK", "1") == "0":      # small-M split-K path off (A/B, tests)
             self.k.fls_gemm_set_splitk(0)
+        if os.environ.get("FLS_GEMM_V11"):                # 0: v10 only, 1: auto (default), 2: forced (A/B)
+            self.k.fls_gemm_set_v11(int(os.environ["FLS_GEMM_V11"]))
+        if os.environ.get("FLS_V11_ORDER") or os.environ.get("FLS_V11_ROWS"):   # v11 tile order / rows (A/B)
+            self.k.fls_gemm_v11_tune(int(os.environ.get("FLS_V11_ORDER", "0")), int(os.environ.get("FLS_V11_ROWS", "0")))
         if os.environ.get("FLS_ATTN_SPLIT"):              # split-KV slices of the range-2 kernel (A/B)
             self.k.fls_attention_set_split(int(os.environ["FLS_ATTN_SPLIT"]))
 
@@ -98,33 +103,40 @@ class HipOps:
         _chk(rc, "fls_gemm")
         return out
 
-    def _splitk_ws(self, device, M: int, N: int):
-        """fp32 partials of the small-M split-K GEMM path (csrc/kernels/gemm.hip) and of the
-        split-KV attention: one fixed-size buffer per (device, host thread), reserved once
-        (``reserve_splitk_ws``; the engine does it before planning a VRAM cap) and never resized, so
-        which GEMM path a shape takes — and its rounding — does not depend on what the allocator
-        could give at the time.  A runner's kernels run on one stream in order, so its GEMMs and
-        attention share it; runners of one process driven from different threads (ranks as threads
-        on one GPU) each get their own, since their multi-kernel sequences (partials, then reduce)
-        can interleave even on a shared stream.  None (mid-M kernel) if it could not be reserved."""
-        key = (torch.device(device), threading.get_ident())
-        if key not in self._ws:
-            self.reserve_splitk_ws(device)
-        return self._ws[key]
+    @staticmethod
+    def new_workspace(device) -> torch.Tensor:
+        """A split-K / split-KV scratch buffer (``SPLITK_WS_BYTES``).  Each ShardedRunner owns one,
+        allocated before it plans its memory (so a ``--max_vram_gb`` plan charges it) and installed
+        for its calls with :meth:`use_workspace`: which GEMM path a shape takes, and its rounding,
+        then never depends on what the allocator could give or on which thread ran before."""
+        return torch.empty(SPLITK_WS_BYTES, dtype=torch.uint8, device=device)
 
-    def reserve_splitk_ws(self, device, allocate: bool = True):
-        """Decide this thread's split-K scratch on the device once: allocate it (``allocate``) or go
-        without (a VRAM-capped runner: the 70B plan has no 64 MB to spare and its small-M GEMMs are
-        the pruned last layer's).  -> bytes reserved."""
+    def use_workspace(self, ws):
+        """Context manager: GEMMs / attention issued by this host thread use ``ws`` as their fp32
+        partial scratch.  A runner's kernels run on one stream in order, so its GEMMs and attention
+        share it; runners driven from different threads (ranks as threads on one GPU) each install
+        their own, since their multi-kernel sequences (partials, then reduce) can interleave."""
+        ops = self
+
+        class _Use:
+            def __enter__(self):
+                self.prev = getattr(ops._tl, "ws", None)
+                ops._tl.ws = ws
+
+            def __exit__(self, *exc):
+                ops._tl.ws = self.prev
+        return _Use()
+
+    def _splitk_ws(self, device, M: int, N: int):
+        """The scratch of the calling thread's runner (:meth:`use_workspace`); outside a runner
+        (kernel tests, tools) one buffer per (device, thread), reserved at first use."""
+        ws = getattr(self._tl, "ws", None)
+        if ws is not None:
+            return ws
         key = (torch.device(device), threading.get_ident())
         if key not in self._ws:
-            try:
-                self._ws[key] = (torch.empty(SPLITK_WS_BYTES, dtype=torch.uint8, device=key[0])
-                                 if allocate else None)
-            except RuntimeError:
-                self._ws[key] = None
-        ws = self._ws[key]
-        return 0 if ws is None else ws.numel()
+            self._ws[key] = self.new_workspace(key[0])
+        return self._ws[key]
 
     def gemv_skinny(self, x, w):
         """Weight-streaming GEMV for M <= 16 rows (skinny LM head)."""

@@ -194,5 +194,5 @@ def build_dp_sharded_runner(args, cfg, device, comm: Comm, tok, store: Optional[
                          prefix_kv_cache=(prefix_kv_cache if prefix_kv_cache is not None
                                           else getattr(args, "prefix_kv_cache", False) is True),
                          prefix_cache_entries=getattr(args, "prefix_cache_entries", 8),
-                         suffix_kv_cache=getattr(args, "suffix_kv_cache", True),
+                         suffix_kv_cache=getattr(args, "suffix_kv_cache", False),
                          max_vram_gb=getattr(args, "max_vram_gb", None))

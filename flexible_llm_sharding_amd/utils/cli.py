@@ -57,10 +57,12 @@ def build_parser() -> argparse.ArgumentParser:
                    help="keep every prompt's prefix K/V per layer in HBM and reuse it in later calls on the same "
                         "prefixes (each --num_gen_token step then computes only the suffix tokens; exact). "
                         "auto (default): on when --num_gen_token > 1")
-    p.add_argument("--suffix_kv_cache", type=str2bool, nargs="?", const=True, default=True,
+    p.add_argument("--suffix_kv_cache", type=str2bool, nargs="?", const=True, default=False,
                    help="with the prefix K/V cache: also keep every suffix's K/V and, in the next call (generation "
                         "step), compute only the tokens after the longest common token prefix with the last call's "
-                        "suffix (each step then costs its new tokens; scores agree to rounding)")
+                        "suffix (each step then costs its new tokens).  Off by default: scores then agree with the "
+                        "reference's full re-computation only to rounding, so a near-tie argmax may pick another "
+                        "token (PARITY.md); the prefix-only cache is exact")
     p.add_argument("--prefix_cache_entries", type=int, default=8,
                    help="prefix K/V cache: calls (prompt batches) kept, LRU")
     p.add_argument("--resident", type=str2bool, nargs="?", const=True, default=False,

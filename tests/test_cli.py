@@ -219,6 +219,14 @@ def test_repeated_pass_defaults():
     assert repeated_passes(g) and resolve_prefix_kv_cache(g)
     assert repeated_passes(parse_args(base + ["--num_batch", "2"]))
     assert not resolve_prefix_kv_cache(parse_args(base + ["--num_gen_token", "4", "--prefix_kv_cache", "false"]))
+    # a VRAM cap: the K/V cache is outside its plan -> auto is off, explicit is an error
+    capped = parse_args(base + ["--num_gen_token", "4", "--max_vram_gb", "6"])
+    assert not resolve_prefix_kv_cache(capped)
+    with pytest.raises(ValueError):
+        resolve_prefix_kv_cache(parse_args(base + ["--num_gen_token", "4", "--max_vram_gb", "6",
+                                                   "--prefix_kv_cache", "true"]))
+    # generation is exact by default: suffix K/V reuse is opt-in
+    assert g.suffix_kv_cache is False
     assert parse_args(base + ["--hbm_cache_gb", "12.5"]).hbm_cache_gb == 12.5
     cfg = preset("tiny")
     assert resolve_hbm_cache_gb(g, cfg, torch.device("cpu")) == 0.0       # nothing to cache on a CPU run
@@ -238,3 +246,21 @@ def test_greedy_tokens_equal_numpy_argmax():
     b[2, 2, 5] = -1.0                                     # a negative value: generic path
     assert np.array_equal(greedy_tokens(b), np.argmax(b, axis=-1))
     assert np.array_equal(greedy_tokens(a.astype(np.float32)), np.argmax(a, axis=-1))
+
+
+def test_prefix_kv_bytes_counts_suffix_regions(tmp_path):
+    """The --hbm_cache_gb auto reserve covers the suffix regions PrefixKVCache.begin allocates
+    (len(suffix) + SUFFIX_GROWTH rows each) when suffix reuse is on."""
+    from flexible_llm_sharding_amd.api import prefix_kv_bytes
+    from flexible_llm_sharding_amd.config import preset
+    from flexible_llm_sharding_amd.runtime.prefix_cache import PrefixKVCache
+    from flexible_llm_sharding_amd.utils.tokenizer import load_tokenizer, write_synthetic_tokenizer
+    cfg = preset("tiny")
+    write_synthetic_tokenizer(str(tmp_path), cfg.vocab_size)
+    tok = load_tokenizer(str(tmp_path))
+    prompts = [("alpha beta gamma", ("x y", "z")), ("delta", ("one two three",))]
+    per_row = 2 * cfg.num_key_value_heads * cfg.head_dim * 2 * 3
+    pre = sum(len(tok(p[0]).input_ids) for p in prompts)
+    sfx = sum(len(ids) + PrefixKVCache.SUFFIX_GROWTH for p in prompts for ids in tok(list(p[1])).input_ids)
+    assert prefix_kv_bytes(cfg, tok, prompts, 3) == pre * per_row
+    assert prefix_kv_bytes(cfg, tok, prompts, 3, suffix_kv_cache=True) == (pre + sfx) * per_row

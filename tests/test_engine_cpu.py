@@ -599,7 +599,7 @@ def test_chunked_qkv_and_mlp_rows_match(tiny_model):
     got = r(prompts)
     for a, b in zip(want, got):
         assert np.abs(a.astype(np.float32) - b.astype(np.float32)).max() < 1e-5
-    assert balanced_step(43008, 16384) == 14592 and balanced_step(100, 0) == 100
+    assert balanced_step(43008, 16384) == 15360 and balanced_step(100, 0) == 100
     assert balanced_step(43008, 8192) == 7680 and balanced_step(500, 1000) == 500
     assert balanced_step(43008, 16384, align=256) == 14336 and balanced_step(1000, 800) == 768
 

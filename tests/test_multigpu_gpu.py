@@ -49,7 +49,7 @@ def seven_b(tmp_path_factory):
     return cfg, store, load_tokenizer(d)
 
 
-def _loopback_pass(cfg, store, tok, prompts, storage, tmp, max_act=1, window=2):
+def _loopback_pass(cfg, store, tok, prompts, storage, tmp, max_act=1, window=2, stages="round_robin"):
     hub = LoopbackHub(2, timeout_s=120)
     res, runners = {}, {}
 
@@ -58,7 +58,8 @@ def _loopback_pass(cfg, store, tok, prompts, storage, tmp, max_act=1, window=2):
             torch.cuda.set_device(0)
             rr = ShardedRunner(cfg, store, "cuda:0", tok, layer_num_per_shard=1, storage_location=storage,
                                disk_folder=os.path.join(tmp, f"spill{r}"), comm=LoopbackComm(hub, r, "cuda:0"),
-                               token_budget=4096, max_activation_in_cpu=max_act, rx_window=window)
+                               token_budget=4096, max_activation_in_cpu=max_act, rx_window=window,
+                               pipeline_stages=stages)
             runners[r] = rr
             res[r] = rr(prompts)
         except BaseException as e:  # noqa: BLE001
@@ -108,6 +109,26 @@ def test_stage_inbox_loopback_7b_bounded(seven_b, tmp_path, storage):
         seen[n_prompts] = (ring, s0["rx_max_parked_bytes_gpu"], s0["rx_max_parked_bytes_cpu"])
     (ra, ga, ca), (rb, gb, cb) = seen[12], seen[24]
     assert ra == rb and ga == gb and ca == cb
+
+
+@pytest.mark.parametrize("storage", ["gpu", "cpu"])
+def test_contiguous_stages_loopback_7b(seven_b, tmp_path, storage):
+    """Contiguous stages (rank r owns one block of layers): rank 1's first shard computes on a
+    received state IN its receive-ring slot (the residual GEMMs are in place) and keeps the result
+    on the rank for its next shard, while later receives reuse the ring (window 2, >= 3
+    micro-batches).  The state must leave the slot before release: scores bitwise
+    equal to the 1-GPU run."""
+    cfg, store, tok = seven_b
+    prompts = synthetic_prompts(12, 1024, 5, 64, cfg.vocab_size, seed=77)
+    one = ShardedRunner(cfg, store, "cuda:0", tok, layer_num_per_shard=1, storage_location="gpu",
+                        token_budget=4096)
+    want = one(prompts)
+    one.close()
+    got, stats, _ = _loopback_pass(cfg, store, tok, prompts, storage, str(tmp_path), stages="contiguous")
+    assert stats[1]["micro_batches"] >= 3
+    for a, b in zip(want, got):
+        assert np.isfinite(a.astype(np.float32)).all()
+        assert np.array_equal(a, b)
 
 
 @pytest.mark.parametrize("G", [2, 4])

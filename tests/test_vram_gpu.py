@@ -66,9 +66,10 @@ def _shared_bytes():
 def _run(tmp_path, cap, name, shared=0):
     out = str(tmp_path / f"{name}.npy")
     code = _WORKER.format(root=ROOT, cap=cap, tok=str(tmp_path / "tok"), out=out)
-    # split-K off in both runs: a capped runner has no split-K workspace (the plan has no 64 MB to
-    # spare), and the pruned last layer's small-M GEMMs would otherwise round differently
-    env = dict(os.environ, FLS_VRAM_SHARED_GB=str(shared / 1e9), FLS_SPLITK="0")
+    # every runner owns its split-K scratch, reserved before its memory plan (charged to a cap):
+    # capped and uncapped runs take the same GEMM paths, split-K small-M ones included
+    env = dict(os.environ, FLS_VRAM_SHARED_GB=str(shared / 1e9))
+    env.pop("FLS_SPLITK", None)
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     return json.loads(r.stdout.strip().splitlines()[-1]), np.load(out)
