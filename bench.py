@@ -232,9 +232,12 @@ def main(argv=None):
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return spawn_ranks(a, argv)
     if a.max_vram_gb is None:
+        # the headline (70B, lnps=1) runs in the reference's 6 GB envelope at every GPU count: one
+        # GPU and data parallel (sub-layer piece pool, all-gathered per piece) alike, so a scaling
+        # curve compares one memory configuration
         headline = a.model == "llama2-70b" and a.lnps == 1 and a.num_layers is None
-        a.max_vram_gb = 6.0 if (headline and a.gpus == 1 and not a.cpu and not a.resident
-                                and a.hbm_cache_gb == 0) else 0.0
+        a.max_vram_gb = 6.0 if (headline and (a.gpus == 1 or a.mode in ("auto", "dp")) and not a.cpu
+                                and not a.resident and a.hbm_cache_gb == 0) else 0.0
     a.max_vram_gb = a.max_vram_gb or None
     if a.max_vram_gb and not a.cpu:
         # a VRAM cap: let the caching allocator grow segments in place instead of keeping one
@@ -250,7 +253,8 @@ def main(argv=None):
     from flexible_llm_sharding_amd.config import preset
     from flexible_llm_sharding_amd.engine import ShardedRunner
     from flexible_llm_sharding_amd.parallel.comm import Comm
-    from flexible_llm_sharding_amd.parallel.data_parallel import AllGatherPrefetcher, SlicedHostStore
+    from flexible_llm_sharding_amd.parallel.data_parallel import (AllGatherPiecePool, AllGatherPrefetcher,
+                                                                  SlicedHostStore)
     from flexible_llm_sharding_amd.parallel.planner import make_plan
     from flexible_llm_sharding_amd.runtime import hostmem
     from flexible_llm_sharding_amd.runtime.stream import FileLayerSource
@@ -308,8 +312,11 @@ def main(argv=None):
                                 seed=a.seed + (rank if dp else 0))
     pf = None
     if dp:
-        pf = AllGatherPrefetcher(store, names, [s for s in plan.my_shards if len(s)], dev, comm,
-                                 resident=a.resident)
+        my = [s for s in plan.my_shards if len(s)]
+        if a.max_vram_gb and a.lnps == 1 and not a.resident and isinstance(store, SlicedHostStore) and not a.cpu:
+            pf = AllGatherPiecePool(store, names, my, dev, comm)       # the 1-GPU memory envelope
+        else:
+            pf = AllGatherPrefetcher(store, names, my, dev, comm, resident=a.resident)
     runner = ShardedRunner(cfg, store, dev, tok, layer_num_per_shard=a.lnps, storage_location=a.storage,
                            disk_folder=f"/tmp/fls_bench_spill_{rank}", prefix_attention=a.prefix_attention,
                            token_budget=a.token_budget, mlp_chunk=a.mlp_chunk, resident=a.resident, comm=comm,

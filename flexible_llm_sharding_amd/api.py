@@ -53,7 +53,7 @@ def resolve_weight_cache(args, cfg: ModelConfig, comm: Comm, names: Sequence[str
     (e.g. ``--dp_weight_shard false`` would pin the whole model once per rank)."""
     from .models.layout import layer_kind, layer_layout
     from .runtime.stream import host_ram_available
-    from .runtime.weights import shard_chunk_bytes
+    from .runtime.weights import piece_slices
     mode = getattr(args, "weight_cache", "auto")
     if getattr(args, "synthetic", None):
         return "host"                  # generated in host RAM; there are no files to stream
@@ -61,8 +61,8 @@ def resolve_weight_cache(args, cfg: ModelConfig, comm: Comm, names: Sequence[str
         return "stream"
     need = 0
     for n in names:
-        nb = layer_layout(cfg, layer_kind(n)).nbytes
-        need += shard_chunk_bytes(nb, comm.world) if sliced else nb
+        lay = layer_layout(cfg, layer_kind(n))
+        need += sum(p.chunk for p in piece_slices(lay, comm.world)) if sliced else lay.nbytes
     local = int(os.environ.get("LOCAL_WORLD_SIZE", comm.world))
     if getattr(args, "host_mem_gb", None):
         budget = int(args.host_mem_gb * 1e9) // max(1, local)
@@ -230,7 +230,7 @@ def run_all(args, runner: ShardedRunner, comm: Comm, prompts: Sequence) -> List[
             outs += runner(mine[b0:b1])
     if comm.world == 1:
         return outs
-    allv = comm.gather_object(outs, dst=0)
+    allv = comm.gather_scores(outs, dst=0)
     if comm.rank != 0:
         return []
     if args.data_parallel:

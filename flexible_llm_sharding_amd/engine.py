@@ -122,6 +122,18 @@ class ShardedRunner:
                 if a != b:
                     edges.append((a, b))
             self.comm.setup_p2p_edges(edges)
+        if self.comm.active:
+            # RCCL creates a communicator's buffers (and, for P2P, its channels) at its first
+            # operation, behind a host-blocking rendezvous.  Run one on every group this runner
+            # uses now, in one global order on every rank — the default group, every directed
+            # hand-off edge, the data-parallel gather group — so none is created lazily inside
+            # a pass (where the single-queue schedule does not model it) and a VRAM cap measures
+            # their memory
+            self.comm.warmup()
+            self.comm.warmup_p2p()
+            pcomm = getattr(prefetcher, "comm", None)
+            if pcomm is not None and pcomm is not self.comm:
+                pcomm.warmup()
         attn_rows = qkv_chunk = 0
         self._outside = None
         self.ops = get_ops(self.dev)
@@ -134,15 +146,7 @@ class ShardedRunner:
             from .runtime.memplan import device_used_bytes, plan_for_vram
             if self.dev.type == "cuda":
                 # device memory held outside the caching allocator before any weight slot exists:
-                # context, code objects, RCCL buffers — planned as measured, not guessed.  The
-                # communicators allocate their buffers at their first collective: run one on every
-                # group this runner uses first (the data-parallel gather group)
-                if self.comm.active:
-                    self.comm.warmup()
-                    self.comm.warmup_p2p()     # model parallel: the hand-off channels' buffers too
-                    pcomm = getattr(prefetcher, "comm", None)
-                    if pcomm is not None and pcomm is not self.comm:
-                        pcomm.warmup()
+                # context, code objects, RCCL buffers (warmed up above) — planned as measured
                 # + the split-K scratch (allocator memory, outside the activation plan)
                 ws = self._splitk_ws.numel() if self._splitk_ws is not None else 0
                 self._outside = (device_used_bytes(self.dev) - torch.cuda.memory_reserved(self.dev) + (64 << 20)

@@ -166,6 +166,69 @@ class Comm:
         dist.broadcast_object_list(lst, src=src, device=self.device if self.backend == "nccl" else None)
         return lst[0]
 
+    def gather_scores(self, outs: List[Optional["np.ndarray"]], dst: int = 0) -> Optional[List[list]]:
+        """Every rank's score arrays (``[n_s, k, V]`` fp16 each; ``None`` for prompts a rank does not
+        own) to ``dst`` -> per-rank lists on ``dst``, None elsewhere.
+
+        Each rank sends ONE packed fp16 tensor plus its shapes, point-to-point to ``dst``, after a
+        fixed-size header (array count, element count) all-gathered on the default communicator.
+        A rank other than ``dst`` stages only its own scores (on the device for ``nccl``); ``dst``
+        receives rank by rank into one staging buffer.  Nothing is pickled and nothing grows with
+        the world size except ``dst``'s result (``all_gather_object`` sent every rank's pickled
+        scores to every rank).  ``self.gather_stats`` records this rank's bytes."""
+        import numpy as np
+        if not self.active:
+            return [outs]
+        on_dev = self.backend == "nccl"
+        dev = self.device if on_dev else torch.device("cpu")
+        shapes = [(-1, -1, -1) if o is None else tuple(int(x) for x in o.shape) for o in outs]
+        total = sum(int(np.prod(sh)) for sh in shapes if sh[0] >= 0)
+        hdr = torch.tensor([len(outs), total], dtype=torch.int64, device=dev)
+        allh = torch.empty(2 * self.world, dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(allh, hdr)
+        allh = allh.cpu().view(self.world, 2).tolist()
+        self.gather_stats = {"sent_bytes": 0, "staged_bytes": 0, "received_bytes": 0}
+        if self.rank != dst:
+            if allh[self.rank][0]:
+                sh = torch.tensor(shapes, dtype=torch.int64, device=dev)
+                flat = (np.concatenate([o.reshape(-1) for o in outs if o is not None]) if total
+                        else np.zeros(0, np.float16))
+                data = torch.from_numpy(np.ascontiguousarray(flat, dtype=np.float16)).to(dev)
+                dist.send(sh, dst)
+                if total:
+                    dist.send(data, dst)
+                self.gather_stats.update(sent_bytes=total * 2, staged_bytes=total * 2)
+            return None
+        res: List[list] = []
+        cap = max([t for r, (n, t) in enumerate(allh) if r != dst] or [0])
+        stage = torch.empty(cap, dtype=torch.float16, device=dev) if cap else None
+        self.gather_stats["staged_bytes"] = cap * 2
+        for r, (n, t) in enumerate(allh):
+            if r == dst:
+                res.append(list(outs))
+                continue
+            if not n:
+                res.append([])
+                continue
+            sh = torch.empty(n, 3, dtype=torch.int64, device=dev)
+            dist.recv(sh, r)
+            sh = sh.cpu().tolist()
+            host = None
+            if t:
+                dist.recv(stage[:t], r)
+                host = stage[:t].cpu().numpy()
+                self.gather_stats["received_bytes"] += t * 2
+            lst, off = [], 0
+            for a, b, c in sh:
+                if a < 0:
+                    lst.append(None)
+                    continue
+                m = a * b * c
+                lst.append(host[off:off + m].reshape(a, b, c).copy())
+                off += m
+            res.append(lst)
+        return res
+
     def gather_object(self, obj: Any, dst: int = 0) -> Optional[List[Any]]:
         if not self.active:
             return [obj]
@@ -401,6 +464,10 @@ class LoopbackComm(Comm):
     def gather_object(self, obj: Any, dst: int = 0) -> Optional[List[Any]]:
         allv = self.hub.exchange(self.rank, obj)
         return allv if self.rank == dst else None
+
+    def gather_scores(self, outs, dst: int = 0):
+        """Threads share the host arrays: dst takes every rank's list as is."""
+        return self.gather_object(list(outs), dst)
 
     def all_gather_object(self, obj: Any) -> List[Any]:
         return self.hub.exchange(self.rank, obj)

@@ -34,8 +34,8 @@ import torch
 
 from ..models.layout import ALIGN_BYTES
 from ..runtime import hostmem
-from ..runtime.prefetch import ShardPrefetcher
-from ..runtime.weights import HostStore, LayerSource, shard_chunk_bytes
+from ..runtime.prefetch import PiecePoolPrefetcher, ShardPrefetcher
+from ..runtime.weights import HostStore, LayerSource, PieceSlice, piece_slices, piece_views
 from .comm import Comm
 
 
@@ -44,14 +44,20 @@ def _align(n: int) -> int:
 
 
 class SlicedHostStore(HostStore):
-    """Rank ``rank``'s byte slice of every packed layer (pinned)."""
+    """Rank ``rank``'s 1/G byte slice of every piece of every packed layer (pinned), concatenated
+    per layer (:func:`~..runtime.weights.piece_slices`): the slices serve the whole-layer
+    all-gather (:class:`AllGatherPrefetcher`) and the sub-layer one (:class:`AllGatherPiecePool`)."""
 
     def __init__(self, cfg, rank: int, world: int, dtype=torch.float16, pinned=True, names=None):
         super().__init__(cfg, dtype, pinned, names)
         self.rank, self.world = rank, world
 
+    def slices(self, name: str) -> List[PieceSlice]:
+        return piece_slices(self.layout(name), self.world)
+
     def chunk_bytes(self, name: str) -> int:
-        return shard_chunk_bytes(self.nbytes(name), self.world)
+        """Bytes of this rank's buffer for ``name`` (its slices of every piece)."""
+        return sum(p.chunk for p in self.slices(name))
 
     def read_into(self, name: str, dst: torch.Tensor) -> None:   # pragma: no cover - not a full source
         raise RuntimeError("a sliced store holds only 1/G of each layer")
@@ -59,14 +65,14 @@ class SlicedHostStore(HostStore):
     @classmethod
     def from_source(cls, src: LayerSource, rank: int, world: int, pinned: bool = True,
                     names: Optional[Sequence[str]] = None) -> "SlicedHostStore":
-        """Read only this rank's byte slice of every layer (``read_range_into``)."""
+        """Read only this rank's byte slices of every layer (``read_range_into``)."""
         st = cls(src.cfg, rank, world, src.dtype, pinned, names)
         for n in st.names:
-            nb, c = st.nbytes(n), st.chunk_bytes(n)
-            buf = hostmem.alloc_host(c, pinned=pinned)
-            lo, hi = rank * c, min(nb, (rank + 1) * c)
-            if hi > lo:
-                src.read_range_into(n, buf, lo, hi)
+            buf = hostmem.alloc_host(st.chunk_bytes(n), pinned=pinned)
+            for p in st.slices(n):
+                a, b = p.rank_range(rank)
+                if b > a:
+                    src.read_range_into(n, buf[p.buf_off:p.buf_off + p.chunk], a, b)
             st.buffers[n] = buf
         return st
 
@@ -100,12 +106,12 @@ class AllGatherPrefetcher(ShardPrefetcher):
             self._pool = None                 # slices are host-resident: no loader thread
         self.bytes_read = 0                   # file bytes this rank read (streaming)
 
-    def chunk_bytes(self, name: str) -> int:
-        return shard_chunk_bytes(self.store.nbytes(name), self.comm.world)
+    def slices(self, name: str) -> List[PieceSlice]:
+        return piece_slices(self.store.layout(name), self.comm.world)
 
     def shard_bytes(self, k: int) -> int:
         G = self.comm.world
-        return sum(_align(self.chunk_bytes(self.names[i]) * G) for i in self.shards[k])
+        return sum(_align(p.chunk * G) for i in self.shards[k] for p in self.slices(self.names[i]))
 
     def _load(self, k: int, epoch=None):
         t0 = time.perf_counter()
@@ -121,34 +127,79 @@ class AllGatherPrefetcher(ShardPrefetcher):
             off = 0
             for i in self.shards[k]:
                 name = self.names[i]
-                nb = self.store.nbytes(name)
-                c = self.chunk_bytes(name)
-                region = slot[off:off + c * G]
-                # in-place all-gather: this rank's slice lands straight in its own place in the
-                # slot (RCCL's sendbuff == recvbuff + rank * count form), so no staging buffer in HBM
-                mine = region[r * c:(r + 1) * c]
-                lo, hi = r * c, min(nb, (r + 1) * c)
-                if not self.streaming:
-                    mine.copy_(self.store.buffers[name][:c], non_blocking=self.cuda)
-                elif hi > lo and self.cuda:
-                    self.bytes_read += self.store.stream_into(name, mine, self.copy_stream, lo, hi, cast=False)
-                elif hi > lo:
-                    before = self.store.read_bytes
-                    self.store.read_range_into(name, mine, lo, hi)
-                    self.bytes_read += self.store.read_bytes - before
-                w = self.comm.all_gather_into(region, mine, async_op=self.cuda)
-                if self.cuda:
-                    w.wait()                  # the copy stream waits for the gather, not the host
-                if self.streaming and self.cuda:
-                    self.store.cast_on_gpu(name, region)
-                views[name] = self.store.layout(name).views(region[:nb], self.dtype)
-                off += _align(c * G)
-                self.bytes_h2d += max(0, hi - lo)
+                regions = []
+                for p in self.slices(name):
+                    region = slot[off:off + p.chunk * G]
+                    # in-place all-gather: this rank's slice lands straight in its own place in the
+                    # slot (RCCL's sendbuff == recvbuff + rank * count form): no staging buffer in HBM
+                    mine = region[r * p.chunk:(r + 1) * p.chunk]
+                    lo, hi = p.rank_range(r)
+                    if not self.streaming:
+                        mine.copy_(self.store.buffers[name][p.buf_off:p.buf_off + p.chunk], non_blocking=self.cuda)
+                    elif hi > lo and self.cuda:
+                        self.bytes_read += self.store.stream_into(name, mine, self.copy_stream, lo, hi, cast=False)
+                    elif hi > lo:
+                        before = self.store.read_bytes
+                        self.store.read_range_into(name, mine, lo, hi)
+                        self.bytes_read += self.store.read_bytes - before
+                    w = self.comm.all_gather_into(region, mine, async_op=self.cuda)
+                    if self.cuda:
+                        w.wait()              # the copy stream waits for the gather, not the host
+                    if self.streaming and self.cuda:
+                        self.store.cast_on_gpu(name, region, p.lo, p.hi)
+                    regions.append((p.lo, region))
+                    off += _align(p.chunk * G)
+                    self.bytes_h2d += hi - lo
+                views[name] = piece_views(self.store.layout(name), regions, self.dtype)
             if self.cuda:
                 ev = torch.cuda.Event()
                 ev.record(self.copy_stream)
         self.load_seconds += time.perf_counter() - t0
         return ev, views, s
+
+
+class AllGatherPiecePool(PiecePoolPrefetcher):
+    """The sub-layer piece pool (``--max_vram_gb``, :class:`~..runtime.prefetch.PiecePoolPrefetcher`:
+    one attention slot + two MLP slots, pieces loaded in pass order as slots free up) for data
+    parallel: each piece is scatter-loaded — this rank H2Ds its 1/G slice into its place in the
+    slot — and completed by an in-place all-gather on this prefetcher's own communicator, so every
+    rank runs in the single-GPU memory envelope (VERDICT r3 #2a).  Pieces are issued in the same
+    (global pass) order on every rank, so the gathers line up; each slot holds a gathered piece
+    (``chunk x G`` bytes >= the piece)."""
+
+    collective = True      # every rank acquires every shard (engine: empty prompt slices too)
+
+    def __init__(self, store: SlicedHostStore, layer_names, shards, device, comm: Comm, dtype=torch.float16):
+        self.comm = comm.dup()
+        self.G, self.r = comm.world, comm.rank
+        super().__init__(store, layer_names, shards, device, dtype)
+        # slot sizes of the gathered pieces (>= the image bytes PiecePoolPrefetcher sized them for)
+        self._slice = {}
+        a_max = m_max = 0
+        own = list(self._own_sizes)
+        for kind, k, lo, hi in self.pieces:
+            name = self.names[self.shards[k][0]]
+            p = next(q for q in store.slices(name) if q.lo == lo)
+            self._slice[(name, lo)] = p
+            g = _align(p.chunk * self.G)
+            if kind == "a":
+                a_max = max(a_max, g)
+            elif kind == "m":
+                m_max = max(m_max, g)
+            else:
+                own[self._own[k]] = max(own[self._own[k]], g)
+        self.a_bytes, self.m_bytes = a_max, m_max
+        self.slot_bytes = m_max
+        self._slot_sizes = [a_max, m_max, m_max] + own
+
+    def _copy_piece(self, slot: torch.Tensor, name: str, lo: int, hi: int) -> int:
+        p = self._slice[(name, lo)]
+        mine = slot[self.r * p.chunk:(self.r + 1) * p.chunk]
+        mine.copy_(self.src.buffers[name][p.buf_off:p.buf_off + p.chunk], non_blocking=True)
+        w = self.comm.all_gather_into(slot[:p.chunk * self.G], mine, async_op=True)
+        w.wait()                   # the copy stream waits for the gather, not the host
+        a, b = p.rank_range(self.r)
+        return b - a
 
 
 class _nullctx:
@@ -177,7 +228,11 @@ def build_dp_sharded_runner(args, cfg, device, comm: Comm, tok, store: Optional[
     names = cfg.layer_names()
     plan = make_plan(len(names), args.layer_num_per_shard, comm.world, comm.rank, True)
     shards = [s for s in plan.my_shards if len(s)]
-    pf = AllGatherPrefetcher(store, names, shards, device, comm, resident=getattr(args, "resident", False))
+    if (getattr(args, "max_vram_gb", None) and args.layer_num_per_shard == 1 and device.type == "cuda"
+            and not getattr(args, "resident", False) and isinstance(store, SlicedHostStore)):
+        pf = AllGatherPiecePool(store, names, shards, device, comm)   # sub-layer pieces under a cap
+    else:
+        pf = AllGatherPrefetcher(store, names, shards, device, comm, resident=getattr(args, "resident", False))
     act = None
     if getattr(args, "dtype", None):
         act = torch.float16 if args.dtype == "float16" else torch.float32

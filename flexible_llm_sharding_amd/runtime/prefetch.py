@@ -476,15 +476,14 @@ class PiecePoolPrefetcher(ShardPrefetcher):
         name = self.names[self.shards[k][0]]
         t0 = time.perf_counter()
         slot = self._slot(s)
-        hb = self.src.host_buffer(name)
         ev = torch.cuda.Event()
         with torch.cuda.stream(self.copy_stream):
             if self._slot_free[s] is not None:
                 self.copy_stream.wait_event(self._slot_free[s])
-            slot[:hi - lo].copy_(hb[lo:hi], non_blocking=True)
+            nbytes = self._copy_piece(slot, name, lo, hi)
             ev.record(self.copy_stream)
         self.load_seconds += time.perf_counter() - t0
-        self.bytes_h2d += hi - lo
+        self.bytes_h2d += nbytes
         if owner is not None:
             self._released.discard(owner)
             self._issued.pop(owner, None)
@@ -495,6 +494,12 @@ class PiecePoolPrefetcher(ShardPrefetcher):
             self._m_turn ^= 1
         self._next += 1
         return True
+
+    def _copy_piece(self, slot: torch.Tensor, name: str, lo: int, hi: int) -> int:
+        """Enqueue image bytes [lo, hi) of ``name`` into ``slot[0:]`` on the copy stream (current
+        stream) -> host bytes moved."""
+        slot[:hi - lo].copy_(self.src.host_buffer(name)[lo:hi], non_blocking=True)
+        return hi - lo
 
     def _pump(self, need: Optional[int] = None) -> None:
         """Issue loads in pass order while their slots are free (at least through ``need``)."""
@@ -573,7 +578,13 @@ class PiecePoolPrefetcher(ShardPrefetcher):
         self._acquired.discard(k)
         n = 2 if self.pieces[self._first[k]][0] == "a" else 1
         for j in range(n):
-            self._release_gid(self._gid(k, j))
+            gid = self._gid(k, j)
+            if gid not in self._issued and gid not in self._released:
+                # a piece never used (a data-parallel rank with no prompts acquires and releases
+                # every layer): issue it now — its load / gather keeps the pass order on every
+                # rank — so that its slot is freed like any other
+                self._pump(gid)
+            self._release_gid(gid)
         self._pump()
 
     def discard_loaded(self) -> None:

@@ -263,7 +263,8 @@ class FileLayerSource(LayerSource):
         return int(r)
 
     def cast_on_gpu(self, name: str, dst: torch.Tensor, lo: int = 0, hi: Optional[int] = None) -> None:
-        """In-place bf16 -> fp16 of the bf16 tensors in [lo, hi) of ``dst`` (current stream)."""
+        """In-place bf16 -> fp16 of the bf16 tensors in image bytes [lo, hi) of ``dst``, whose byte 0
+        is image byte ``lo`` (current stream)."""
         runs = self.plan(name).bf16_runs(lo, hi)
         if not runs:
             return

@@ -15,14 +15,15 @@ Here a source yields the *packed* layer image (see :mod:`..models.layout`):
   (read once), so each shard H2D is one DMA at PCIe line rate
   (``--weight_cache host``).  Also built directly from synthetic random-init
   weights (generated on the GPU and copied down) for the 70B benchmark.
-* ``shard_fraction`` (data-parallel scatter-load): a rank keeps only its
-  1/G byte-slice of every layer; the full layer is re-assembled in HBM with an
-  RCCL all-gather over xGMI (:mod:`..parallel.data_parallel`).
+* data-parallel scatter-load (:func:`piece_slices`): a rank keeps only its
+  1/G byte-slice of every layer piece; the layer (or one piece of it) is
+  re-assembled in HBM with an RCCL all-gather over xGMI
+  (:mod:`..parallel.data_parallel`).
 """
 from __future__ import annotations
 
 import threading
-from typing import Dict, List, Optional, Sequence
+from typing import Dict, List, NamedTuple, Optional, Sequence, Tuple
 
 import torch
 
@@ -136,12 +137,12 @@ class HostStore(LayerSource):
                 buf.copy_(full, non_blocking=False)
             else:
                 r, G = byte_range
-                chunk = shard_chunk_bytes(lay.nbytes, G)
-                buf = hostmem.alloc_host(chunk, pinned=pinned)
-                lo = r * chunk
-                hi = min(lay.nbytes, lo + chunk)
-                if hi > lo:
-                    buf[:hi - lo].copy_(full[lo:hi])
+                sl = piece_slices(lay, G)
+                buf = hostmem.alloc_host(sum(p.chunk for p in sl), pinned=pinned)
+                for p in sl:
+                    a, b = p.rank_range(r)
+                    if b > a:
+                        buf[p.buf_off:p.buf_off + b - a].copy_(full[a:b])
                 st.buffers[n] = buf
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
@@ -152,3 +153,51 @@ class HostStore(LayerSource):
 def shard_chunk_bytes(nbytes: int, world: int, align: int = 4096) -> int:
     c = (nbytes + world - 1) // world
     return (c + align - 1) // align * align
+
+
+def layer_pieces(lay: LayerLayout) -> List[Tuple[int, int]]:
+    """Byte ranges of a packed layer image that load as one unit: a decoder layer's attention
+    piece and MLP piece (``models.layout.mlp_offset``; the sub-layer piece pool streams them
+    separately), one range for every other kind."""
+    from ..models.layout import mlp_offset
+    if lay.kind == "decoder":
+        s = mlp_offset(lay)
+        return [(0, s), (s, lay.nbytes)]
+    return [(0, lay.nbytes)]
+
+
+class PieceSlice(NamedTuple):
+    """Data-parallel scatter-load of one piece ``[lo, hi)`` of a layer image over G ranks: rank r
+    holds bytes ``[lo + r * chunk, min(hi, lo + (r + 1) * chunk))`` at ``buf_off`` of its host
+    buffer, and the all-gather rebuilds the piece in a ``chunk * G``-byte HBM region."""
+    lo: int
+    hi: int
+    chunk: int
+    buf_off: int
+
+    def rank_range(self, r: int) -> Tuple[int, int]:
+        a = self.lo + r * self.chunk
+        return a, max(a, min(self.hi, a + self.chunk))
+
+
+def piece_slices(lay: LayerLayout, world: int) -> List[PieceSlice]:
+    """Every rank's slices of ``lay``, piece by piece (:func:`layer_pieces`): each piece is split
+    on its own, so a rank's slices serve the whole-layer all-gather and the per-piece one alike."""
+    out, off = [], 0
+    for lo, hi in layer_pieces(lay):
+        c = shard_chunk_bytes(hi - lo, world)
+        out.append(PieceSlice(lo, hi, c, off))
+        off += c
+    return out
+
+
+def piece_views(lay: LayerLayout, regions: Sequence[Tuple[int, torch.Tensor]], dtype) -> Dict[str, torch.Tensor]:
+    """Typed tensor views of a layer whose pieces sit in separate byte regions: ``regions`` =
+    [(image offset of the piece, uint8 region holding it)] in image order."""
+    es = torch.empty((), dtype=dtype).element_size()
+    out = {}
+    for ts in lay.slots:
+        lo, reg = [(lo, reg) for lo, reg in regions if lo <= ts.offset][-1]
+        o = ts.offset - lo
+        out[ts.name] = reg[o:o + ts.numel * es].view(dtype).view(ts.shape)
+    return out

@@ -55,7 +55,7 @@ def _worker(rank, world, port, path, prompts, lnps, dp, storage, out_dir, budget
         assert (a is None and b is None) or (_close(a, b) if pkv else np.array_equal(a, b))
     if pkv:
         assert r.stats["prefix_cached"] == 1.0 and r.prefix_cache.hits == 1
-    allv = comm.gather_object(outs, dst=0)
+    allv = comm.gather_scores(outs, dst=0)
     resumed = comm.gather_object(r.stats["resumed_from_shard"], dst=0)
     if rank == 0:
         with open(os.path.join(out_dir, "out.pkl"), "wb") as f:
@@ -125,7 +125,7 @@ def _dp_shard_worker(rank, world, port, path, prompts, lnps, out_dir, resume_dir
     assert r.prefetcher.__class__.__name__ == "AllGatherPrefetcher"
     idx = np.array_split(np.arange(len(prompts)), world)[rank]
     outs = r([prompts[i] for i in idx])
-    allv = comm.gather_object(outs, dst=0)
+    allv = comm.gather_scores(outs, dst=0)
     resumed = comm.gather_object(r.stats["resumed_from_shard"], dst=0)
     if rank == 0:
         with open(os.path.join(out_dir, "out.pkl"), "wb") as f:
@@ -208,7 +208,7 @@ def _mp_resume_worker(rank, world, port, path, prompts, out_dir, resume_dir, fau
                       storage_location=storage, disk_folder=os.path.join(out_dir, f"spill{rank}"), comm=comm,
                       token_budget=40, resume_dir=resume_dir, checkpoint_every=2)
     outs = r(prompts)
-    allv = comm.gather_object(outs, dst=0)
+    allv = comm.gather_scores(outs, dst=0)
     resumed = comm.gather_object(r.stats["resumed_from_shard"], dst=0)
     if rank == 0:
         with open(os.path.join(out_dir, "out.pkl"), "wb") as f:
@@ -313,3 +313,51 @@ def test_p2p_warmup_chain_completes(tmp_path, world, edges):
     chain completes for edges in both directions and across more than two ranks."""
     mp.spawn(_p2p_warmup_worker, args=(world, _port(), edges, str(tmp_path)), nprocs=world, join=True)
     assert sorted(os.listdir(tmp_path)) == [f"ok{r}" for r in range(world)]
+
+
+def _gather_worker(rank, world, port, out_dir):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    import json
+    from flexible_llm_sharding_amd.parallel.comm import Comm
+    comm = Comm.from_env("cpu", timeout_s=60)
+
+    def scores(r):
+        g = np.random.default_rng(r)
+        outs = [g.random((3 + i, 1, 1000)).astype(np.float16) for i in range(3)]
+        if r % 2 == 1:
+            outs.insert(1, None)                 # a prompt this rank does not own (model parallel)
+        return outs
+    got = comm.gather_scores(scores(rank), dst=0)
+    if rank == 0:
+        assert len(got) == world
+        for r in range(world):
+            want = scores(r)
+            assert len(got[r]) == len(want)
+            for a, b in zip(got[r], want):
+                assert (a is None and b is None) or np.array_equal(a, b)
+    else:
+        assert got is None
+    with open(os.path.join(out_dir, f"stats{rank}.json"), "w") as f:
+        json.dump(comm.gather_stats, f)
+    comm.destroy()
+
+
+def test_gather_scores_memory_does_not_grow_with_world(tmp_path):
+    """Rank-0 score return (Comm.gather_scores: one packed fp16 tensor + shapes per rank, after a
+    fixed-size header): the bytes a rank other than 0 stages and sends are its own scores, the
+    same at world 2 and 4 (all_gather_object sent every rank's scores to every rank)."""
+    import json
+    staged = {}
+    for world in (2, 4):
+        d = tmp_path / f"w{world}"
+        d.mkdir()
+        mp.spawn(_gather_worker, args=(world, _port(), str(d)), nprocs=world, join=True)
+        st = {r: json.load(open(d / f"stats{r}.json")) for r in range(world)}
+        own = (3 + 4 + 5) * 1000 * 2
+        for r in range(1, world):
+            assert st[r]["staged_bytes"] == st[r]["sent_bytes"] == own
+            assert st[r]["received_bytes"] == 0
+        assert st[0]["received_bytes"] == (world - 1) * own
+        staged[world] = st[1]["staged_bytes"]
+    assert staged[2] == staged[4]

@@ -205,8 +205,9 @@ def test_f32_to_f16_rounding_matches_torch():
 
 
 def test_dp_slices_read_only_their_range(tiny_model):
-    """SlicedHostStore.from_source: rank r's slices == bytes [r*c, (r+1)*c) of the full images,
-    and the G ranks together read each layer file's tensor bytes exactly once."""
+    """SlicedHostStore.from_source: rank r's slice of every layer piece (attention / MLP piece of a
+    decoder, the whole image otherwise) == bytes [lo + r*c, lo + (r+1)*c) of the full image, and
+    the G ranks together read each layer file's tensor bytes exactly once."""
     from flexible_llm_sharding_amd.parallel.data_parallel import SlicedHostStore
     from flexible_llm_sharding_amd.runtime.stream import FileLayerSource
     path, cfg = tiny_model
@@ -218,11 +219,15 @@ def test_dp_slices_read_only_their_range(tiny_model):
         st = SlicedHostStore.from_source(src, rank, G, pinned=False)
         total += src.read_bytes
         for n in cfg.layer_names():
-            nb, c = st.nbytes(n), st.chunk_bytes(n)
+            nb = st.nbytes(n)
             full = torch.zeros(nb, dtype=torch.uint8)
             full_src.read_into(n, full)
-            valid = max(0, min(nb, (rank + 1) * c) - rank * c)
-            assert torch.equal(st.buffers[n][:valid], full[rank * c:rank * c + valid]), (rank, n)
+            sl = st.slices(n)
+            assert len(sl) == (2 if n.startswith("model.layers.") else 1)
+            assert sl[0].lo == 0 and sl[-1].hi == nb and st.buffers[n].numel() == st.chunk_bytes(n)
+            for p in sl:
+                a, b = p.rank_range(rank)
+                assert torch.equal(st.buffers[n][p.buf_off:p.buf_off + b - a], full[a:b]), (rank, n)
     assert total == sum(full_src.plan(n).file_bytes for n in cfg.layer_names())
 
 

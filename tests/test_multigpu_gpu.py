@@ -131,18 +131,23 @@ def test_contiguous_stages_loopback_7b(seven_b, tmp_path, storage):
         assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("G", [2, 4])
-def test_data_parallel_loopback_7b(seven_b, G):
+@pytest.mark.parametrize("G,pool,n_prompts", [(2, "layer", 8), (4, "layer", 16), (2, "pieces", 8),
+                                               (4, "pieces", 3)])
+def test_data_parallel_loopback_7b(seven_b, G, pool, n_prompts):
     """Data parallel with G ranks as threads on ONE GPU: each rank holds 1/G of every layer in
     pinned RAM, H2Ds only its slice into its place in the HBM slot on the prefetcher's copy stream,
     and the loopback all-gather (device copies ordered by events, parallel/comm.py) completes the
     layer before compute; two calls (slot rotation across calls).  Each rank's scores must equal
-    the 1-GPU run on its prompts bitwise: the weights are assembled exactly."""
-    from flexible_llm_sharding_amd.parallel.data_parallel import AllGatherPrefetcher, SlicedHostStore
+    the 1-GPU run on its prompts bitwise: the weights are assembled exactly.  ``pieces``: the
+    sub-layer piece pool of the --max_vram_gb mode (AllGatherPiecePool: one attention + two MLP
+    slots, each piece all-gathered on its own), with 3 prompts on 4 ranks (an empty rank acquires
+    and releases every layer, its pieces still gathered in pass order)."""
+    from flexible_llm_sharding_amd.parallel.data_parallel import (AllGatherPiecePool, AllGatherPrefetcher,
+                                                                  SlicedHostStore)
     from flexible_llm_sharding_amd.parallel.planner import make_plan
     cfg, full, tok = seven_b
     dev = torch.device("cuda", 0)
-    prompts = synthetic_prompts(4 * G, 1024, 5, 64, cfg.vocab_size, seed=G)
+    prompts = synthetic_prompts(n_prompts, 1024, 5, 64, cfg.vocab_size, seed=G)
     idx = np.array_split(np.arange(len(prompts)), G)
     names = cfg.layer_names()
     stores = [SlicedHostStore.synthetic(cfg, dev, r, G, seed=5) for r in range(G)]   # seven_b's seed
@@ -154,9 +159,15 @@ def test_data_parallel_loopback_7b(seven_b, G):
             torch.cuda.set_device(0)
             comm = LoopbackComm(hub, r, "cuda:0")
             plan = make_plan(len(names), 1, G, r, True)
-            pf = AllGatherPrefetcher(stores[r], names, [s for s in plan.my_shards if len(s)], dev, comm)
+            shards = [s for s in plan.my_shards if len(s)]
+            pf = (AllGatherPiecePool(stores[r], names, shards, dev, comm) if pool == "pieces"
+                  else AllGatherPrefetcher(stores[r], names, shards, dev, comm))
             rr = ShardedRunner(cfg, stores[r], "cuda:0", tok, layer_num_per_shard=1, storage_location="gpu",
                                comm=comm, data_parallel=True, prefetcher=pf, token_budget=4096)
+            if pool == "pieces":
+                # one attention + two MLP piece slots (+ small own buffers) < the double buffer
+                dec = next(n for n in names if n.startswith("model.layers."))
+                assert pf.planned_hbm_bytes() < 2 * full.nbytes(dec)
             runners[r] = rr
             mine = [prompts[i] for i in idx[r]]
             res[r] = [rr(mine) for _ in range(2)]
@@ -175,6 +186,9 @@ def test_data_parallel_loopback_7b(seven_b, G):
         rr.close()
     one = ShardedRunner(cfg, full, "cuda:0", tok, layer_num_per_shard=1, storage_location="gpu", token_budget=4096)
     for r in range(G):
+        if not len(idx[r]):
+            assert all(call == [] for call in res[r])
+            continue
         want = one([prompts[i] for i in idx[r]])
         for call in res[r]:
             for a, b in zip(want, call):

@@ -279,3 +279,26 @@ def test_data_parallel_over_loopback_threads(deep6, G):
             assert len(call) == len(want)
             for a, b in zip(call, want):
                 assert np.abs(a.astype(np.float32) - b.astype(np.float32)).max() < 1e-5
+
+
+def test_runner_warms_every_communicator_at_construction(deep6, tmp_path):
+    """No VRAM cap: a model-parallel runner still warms the default group and every directed
+    hand-off edge in its constructor (VERDICT r3 #2b), so no communicator is created lazily
+    inside the first pass."""
+    from flexible_llm_sharding_amd.engine import ShardedRunner
+    from flexible_llm_sharding_amd.parallel.comm import LoopbackComm, LoopbackHub
+    from flexible_llm_sharding_amd.runtime.stream import FileLayerSource
+    cfg, path, tok, prompts, ref = deep6
+    calls = []
+
+    class Recording(LoopbackComm):
+        def warmup(self):
+            calls.append((self.rank, "warmup"))
+
+        def warmup_p2p(self):
+            calls.append((self.rank, "warmup_p2p"))
+
+    hub = LoopbackHub(2, timeout_s=60)
+    for r in range(2):
+        ShardedRunner(cfg, FileLayerSource(cfg, path), "cpu", tok, comm=Recording(hub, r, "cpu")).close()
+    assert sorted(calls) == [(0, "warmup"), (0, "warmup_p2p"), (1, "warmup"), (1, "warmup_p2p")]
