@@ -27,7 +27,7 @@ model-parallel schedule (shard k on GPU k mod N, RCCL send/recv of
 activations; each GPU streams only its own shards).
 
 Memory is reported as measured: ``peak_gpu_mem_gb`` (allocator high-water),
-``peak_device_used_gb`` (``hipMemGetInfo`` total - free sampled after every
+``peak_device_used_gb`` (``hipMemGetInfo`` total - free sampled every 2 ms by a thread during every
 step: context, code objects, RCCL buffers and allocator slack included),
 ``host_pinned_gb`` and ``host_peak_rss_gb``.
 """
@@ -44,6 +44,34 @@ import time
 import numpy as np
 
 METRIC = "tokens/sec + peak GPU mem, Llama-2-70B layer_num_per_shard=1 at 1/2/4/8 MI355X"
+
+
+class DeviceSampler:
+    """hipMemGetInfo (total - free) sampled every ``period_s`` by a thread for the whole run —
+    warmup and timed steps, inside the passes, not only at step boundaries (VERDICT r3 #4)."""
+
+    def __init__(self, dev, period_s: float = 0.002):
+        import threading
+
+        import torch
+        self.dev, self.period, self.peak, self.n = dev, period_s, 0.0, 0
+        self._stop = threading.Event()
+
+        def run():
+            torch.cuda.set_device(dev)
+            while not self._stop.is_set():
+                free, total = torch.cuda.mem_get_info(dev)
+                self.peak = max(self.peak, float(total - free))
+                self.n += 1
+                self._stop.wait(self.period)
+
+        self._t = threading.Thread(target=run, daemon=True)
+        self._t.start()
+
+    def stop(self):
+        self._stop.set()
+        self._t.join()
+        return self.peak, self.n
 
 
 def log(rank, *a):
@@ -260,7 +288,7 @@ def main(argv=None):
     from flexible_llm_sharding_amd.runtime.stream import FileLayerSource
     from flexible_llm_sharding_amd.runtime.weights import HostStore
     from flexible_llm_sharding_amd.utils.synthetic import synthetic_prompts
-    from flexible_llm_sharding_amd.utils.tokenizer import load_tokenizer, write_synthetic_tokenizer
+    from flexible_llm_sharding_amd.utils.tokenizer import clear_prefix_ids, load_tokenizer, write_synthetic_tokenizer
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != a.gpus:
@@ -327,21 +355,14 @@ def main(argv=None):
         runner.ctx.attn_rows = a.attn_rows
     if runner.vram_plan:
         log(rank, f"[bench] --max-vram-gb {a.max_vram_gb}: {runner.vram_plan}")
-    dev_used_peak = 0.0
-
-    def sample_device():
-        nonlocal dev_used_peak
-        if not a.cpu:
-            free, total = torch.cuda.mem_get_info(dev)
-            dev_used_peak = max(dev_used_peak, float(total - free))
-
+    sampler = DeviceSampler(dev) if not a.cpu else None
     if not a.cpu:
         torch.cuda.reset_peak_memory_stats(dev)
 
     for i in range(a.warmup):
         tw = time.perf_counter()
+        clear_prefix_ids()
         runner(prompts)
-        sample_device()
         log(rank, f"[bench] warmup {i}: {time.perf_counter() - tw:.2f}s")
     comm.barrier()
     sync()
@@ -349,6 +370,7 @@ def main(argv=None):
     outs = None
     for i in range(a.steps):
         ts = time.perf_counter()
+        clear_prefix_ids()       # every timed call tokenizes its prompts in full
         outs = runner(prompts)
         log(rank, f"[bench] step {i}: {time.perf_counter() - ts:.2f}s  stats={json.dumps({k: round(v, 3) for k, v in runner.stats.items()})}")
         if i == 0 and runner.vram_plan:
@@ -356,7 +378,7 @@ def main(argv=None):
     sync()
     comm.barrier()
     elapsed = time.perf_counter() - t_start
-    sample_device()
+    dev_used_peak, n_samples = sampler.stop() if sampler is not None else (0.0, 0)
     if not a.cpu:
         ms_ = torch.cuda.memory_stats(dev)
         log(rank, f"[bench] allocator: device mallocs {ms_.get('num_device_alloc')}, "
@@ -393,7 +415,7 @@ def main(argv=None):
         "scaling": "weak", "vs_baseline": None, "dtype": "fp32-cpu-rehearsal" if a.cpu else "fp16",
         "data": f"synthetic prompts (synthetic tokenizer) + {data_w}",
         "peak_gpu_mem_gb": round(peak / 1e9, 3), "peak_gpu_reserved_gb": round(peak_res / 1e9, 3),
-        "peak_device_used_gb": round(dev_used_peak / 1e9, 3),
+        "peak_device_used_gb": round(dev_used_peak / 1e9, 3), "device_mem_samples": n_samples,
         "host_pinned_gb": round(pinned / 1e9, 3), "host_peak_rss_gb": round(rss / 1e9, 3),
         "scores_finite": finite,
         "world": world, "process_group_ranks": pg_world,

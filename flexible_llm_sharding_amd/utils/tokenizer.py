@@ -132,6 +132,12 @@ _PREFIX_IDS: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
 _PREFIX_IDS_MAX = 4096
 
 
+def clear_prefix_ids() -> None:
+    """Forget every cached prefix tokenization (benchmarks: each timed call then tokenizes its
+    prefixes like a fresh ``main.py`` call, ``/root/reference/utils.py:246-259``)."""
+    _PREFIX_IDS.clear()
+
+
 def _prefix_ids(tok, prefixes: Sequence[str], max_len: int):
     try:
         cache = _PREFIX_IDS.setdefault(tok, {})
