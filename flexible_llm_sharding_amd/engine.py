@@ -434,175 +434,243 @@ class ShardedRunner:
             return e, True
         return pc.begin(tps), False
 
+    # ------------------------------------------------------------------ one pass
+    # A pass is a list of (shard, micro-batch) items (``schedule``) run by one of two executors —
+    # ``_exec_local`` (single GPU, data parallel) and ``_exec_pipeline`` (model parallel, a fixed
+    # send / receive program) — over shared per-item routines.  Each lifetime rule lives in one
+    # routine: weight slots in ``_enter_shard`` / ``_close_weights`` (acquire, release, prefetch,
+    # discard on abort), activation ownership in ``_emit`` (output copy, send, carry, store; a
+    # received state leaves its ring slot), receive-ring slots in ``_exec_pipeline`` (release after
+    # the item's send), checkpoints in ``_enter_shard`` / the executors.
+
+    class _Pass:
+        """Mutable state of one ``_run_batches`` call."""
+
+        def __init__(self, tps, batches, metas, store, items):
+            self.tps, self.batches, self.metas, self.store, self.items = tps, batches, metas, store, items
+            self.pos = {it: i for i, it in enumerate(items)}
+            self.outputs: List[Optional[np.ndarray]] = [None] * len(tps)
+            self.out_pending = []      # (batch, host tensor, event, pool buffer)
+            self.carry = {}            # micro-batch -> device activation kept across a shard boundary
+            self.sends = []            # (tensor, work) of outputs in flight to another rank
+            self.shard_ev: List = []   # end-of-shard events on the compute stream (host run-ahead bound)
+            self.flops = 0.0
+            self.compute_s = 0.0
+            self.cur_k = -1
+            self.W = None
+            self.dst_rank = 0
+            self.prefetch_due = -1
+            self.ck = None
+            self.prog = self.inbox = None
+            self.pbar = None
+
     def _run_batches(self, tps, batches, t_start: float) -> List[Optional[np.ndarray]]:
-        n = len(tps)
         metas = [b.device_tensors(self.dev) for b in batches]   # all uploads before any compute
         store = self._get_store()
         store.bytes_d2h = store.bytes_h2d = 0
-        outputs: List[Optional[np.ndarray]] = [None] * n
-        out_pending = []     # (batch, host tensor, event)
-        comm = self.comm
-        mp = self.plan.mode == "mp"
         pf = self.prefetcher
-        flops = 0.0
-        compute_s = 0.0
-        sends = []
         # weight bytes of this call: counted from its early prefetch (or the previous call's
         # speculative one), not from the first acquire
         h2d0 = pf.bytes_h2d if self._h2d0 is None else self._h2d0
         self._h2d0 = None
-        items = self.schedule(len(batches))
+        px = self._Pass(tps, batches, metas, store, self.schedule(len(batches)))
         collective = getattr(pf, "collective", False)
-        if not items and self.my_shards and collective:
+        if not px.items and self.my_shards and collective:
             # a data-parallel rank with no prompts in this call still joins every shard's weight
             # all-gather, so all ranks issue the same collective sequence (ADVICE r1)
             for k in range(len(self.my_shards)):
                 pf.acquire(k)
                 pf.prefetch(k + 1)
                 pf.release(k)
-        ck, k0, ck_loaded = self._open_checkpoint(tps)
+        px.ck, k0, ck_loaded = self._open_checkpoint(tps)
         if k0 > 0 or ck_loaded:
             for b, t in ck_loaded.items():
                 store.put(b, t.to(self.dev))
-            items = [it for it in items if it[0] >= k0]
-        carry = {}                     # micro-batch -> device activation kept across a shard boundary
-        pos = {it: i for i, it in enumerate(items)}
-        shard_ev: List = []            # end-of-shard events on the compute stream (host run-ahead bound)
-        prog = inbox = None
-        if mp and comm.active and items:
-            prog = self._mp_program(len(batches))
-            if list(prog.items) != list(items):
+            px.items = [it for it in px.items if it[0] >= k0]
+            px.pos = {it: i for i, it in enumerate(px.items)}
+        if self.plan.mode == "mp" and self.comm.active and px.items:
+            px.prog = self._mp_program(len(batches))
+            if list(px.prog.items) != list(px.items):
                 raise RuntimeError("model-parallel program does not match this rank's schedule")
-            inbox = self._get_inbox()
-            inbox.begin_call(max([self._rx_bytes(k, batches[b]) for (k, b), s in zip(items, prog.src)
-                                  if s is not None] or [0]))
-        cur_k = -1
-        W = None
+            px.inbox = self._get_inbox()
+            px.inbox.begin_call(max([self._rx_bytes(k, batches[b]) for (k, b), src in zip(px.items, px.prog.src)
+                                     if src is not None] or [0]))
+        if self.my_shards and px.items:
+            pf.prefetch(px.items[0][0])
+        px.pbar = self._progress(len(px.items))
         ok = False
-        # data parallel: the next shard's all-gather is enqueued after this shard's first compute
-        # (a collective kernel sharing a hardware queue with compute then sits behind it, never
-        # ahead of it); single GPU / model parallel: right after the acquire
-        prefetch_due = -1
-        if self.my_shards and items:
-            pf.prefetch(items[0][0])
-        pbar = self._progress(len(items))
         try:
-            for idx, (k, b) in enumerate(items):
-                shard = self.my_shards[k]
-                first, last = shard[0], shard[-1]
-                if k != cur_k:
-                    if ck is not None and cur_k >= 0 and self._ckpt_due(cur_k):
-                        ck.commit(self._ckpt_key(cur_k), range(len(batches)), self.act_dtype)
-                    if self._fault is not None and k == self._fault:
-                        raise RuntimeError(f"FLS_FAULT injected on rank {comm.rank} at shard {k}")
-                    if cur_k >= 0:
-                        pf.release(cur_k)
-                        self._throttle(shard_ev)
-                    with trace.range(f"shard{k}:acquire"):
-                        W = pf.acquire(k)
-                    cur_k = k
-                    if collective:
-                        prefetch_due = k
-                    else:
-                        with trace.range(f"shard{k + 1}:prefetch"):
-                            self._prefetch_ahead(k)
-                    dst_rank = self._owner(last + 1) if (mp and last + 1 < self.L) else comm.rank
-
-                batch, meta = batches[b], metas[b]
-                if prog is not None:
-                    for c in prog.posts[idx]:         # receives due before this item (program order)
-                        kc, bc = items[c]
-                        inbox.post(rx_key(kc, bc), prog.src[c], self._state_shape(self.my_shards[kc][0] - 1,
-                                                                                  batches[bc]),
-                                   park=c in prog.parked)
-                from_rx = prog is not None and prog.src[idx] is not None
-                if first == 0:
-                    state = None
-                elif from_rx:
-                    state = inbox.get(rx_key(k, b))
-                elif b in carry:
-                    state = carry.pop(b)
-                else:
-                    state = store.get(b)
-                if ck is not None and mp and self._ckpt_due(k) and state is not None:
-                    ck.save_state(self._ckpt_key(k), b, state)     # model parallel: a stage's inputs
-                # one-ahead activation prefetch (crosses shard boundaries)
-                if idx + 1 < len(items):
-                    k2, b2 = items[idx + 1]
-                    if prog is not None and prog.src[idx + 1] is not None:
-                        if idx + 1 in prog.parked:
-                            inbox.prefetch(rx_key(k2, b2))
-                    elif self.my_shards[k2][0] > 0 and k2 == k:
-                        store.prefetch(b2)
-                    elif k2 != k and idx + 2 < len(items):
-                        store.prefetch(items[idx + 2][1])
-                tc = time.perf_counter()
-                last_use = idx + 1 >= len(items) or items[idx + 1][0] != k
-                with trace.range(f"shard{k}:mb{b}:compute"):
-                    for li in shard:
-                        name = self.names[li]
-                        if hasattr(W[name], "final_use"):
-                            W[name].final_use = last_use
-                        state = run_layer(self.ctx, name, W[name], state, batch, meta)
-                        if layer_kind(name) == "decoder":
-                            flops += layer_flops(self.cfg, batch, self._pruned(name))
-                compute_s += time.perf_counter() - tc
-                if prefetch_due == k:
-                    prefetch_due = -1
-                    with trace.range(f"shard{k + 1}:prefetch"):
-                        self._prefetch_ahead(k)
-                if pbar is not None:
-                    pbar.update(1)
-                if ck is not None and not mp and self._ckpt_due(k):
-                    ck.save_state(self._ckpt_key(k), b, state)     # single / DP: a shard's outputs
-                send_w = None
-                if from_rx and last < self.L - 1 and dst_rank == comm.rank:
-                    # the residual GEMMs update the received state in place, so it may still BE the
-                    # receive-ring slot that inbox.release() hands to the next receive: a state that
-                    # stays on this rank (contiguous stages) leaves the slot first
-                    state = state.clone()
-                if last == self.L - 1:
-                    out_pending.append(self._start_output_copy(batch, state))
-                elif dst_rank != comm.rank:
-                    st = state.contiguous()
-                    send_w = comm.isend(st, dst_rank)
-                    sends.append((st, send_w))
-                elif self.storage != "gpu" and pos.get((k + 1, b), len(items)) - idx <= self.CARRY_WINDOW:
-                    # re-used within CARRY_WINDOW micro-batch computes (the zigzag boundary micro-batch
-                    # and its neighbour): a PCIe round trip would only add traffic, keep it in HBM
-                    carry[b] = state
-                else:
-                    store.put(b, state)
-                del state
-                if from_rx:
-                    inbox.release(rx_key(k, b), send_w)
-                # pending sends are retired per micro-batch (the consumer posts its receive at the
-                # point of use); at most SEND_WINDOW outputs stay alive waiting for their consumer
-                sends = [(t, w) for (t, w) in sends if not w.is_completed()]
-                while len(sends) > self.SEND_WINDOW:
-                    host_wait(sends.pop(0)[1], cuda=self.cuda)
-            if ck is not None and mp and cur_k >= 0 and self._ckpt_due(cur_k):
-                ck.commit(self._ckpt_key(cur_k), range(len(batches)), self.act_dtype)
+            if px.prog is not None:
+                self._exec_pipeline(px)
+            else:
+                self._exec_local(px)
             ok = True
         finally:
-            if not ok:
-                # an aborted pass: the held shard is released and every loaded-but-unused shard
-                # forgotten, so a later call's loads never land on weights still waiting to be used
-                if cur_k >= 0:
-                    pf.release(cur_k)
-                    cur_k = -1
-                if not collective:
-                    pf.discard_loaded()
-                if inbox is not None:
-                    inbox.abort()
-        if cur_k >= 0:
-            pf.release(cur_k)
-        h2d_end = pf.bytes_h2d         # after the last release: loads it triggers count to this call
-        if items:
+            self._close_weights(px, ok)
+        return self._finish_pass(px, t_start, h2d0, k0)
+
+    def _exec_local(self, px: "_Pass") -> None:
+        """Single GPU / data parallel: every shard on every micro-batch, activations through the
+        carry window or the store."""
+        collective = getattr(self.prefetcher, "collective", False)
+        for idx, (k, b) in enumerate(px.items):
+            self._enter_shard(px, k)
+            state = self._take_state(px, k, b)
+            self._prefetch_activation(px, idx)
+            state = self._compute(px, k, b, state)
+            if collective and px.prefetch_due == k:
+                # data parallel: the next shard's all-gather is enqueued after this shard's first
+                # compute (a collective kernel sharing a hardware queue with compute then sits
+                # behind it, never ahead of it)
+                px.prefetch_due = -1
+                with trace.range(f"shard{k + 1}:prefetch"):
+                    self._prefetch_ahead(k)
+            if px.ck is not None and self._ckpt_due(k):
+                px.ck.save_state(self._ckpt_key(k), b, state)     # a shard's outputs
+            self._emit(px, k, b, state, from_rx=False)
+
+    def _exec_pipeline(self, px: "_Pass") -> None:
+        """Model parallel: this rank's items in program order; inputs from the previous stage
+        arrive in the StageInbox (receives posted per the program, never ahead of work they depend
+        on); a received slot is released once the item's output no longer needs it."""
+        prog, inbox = px.prog, px.inbox
+        for idx, (k, b) in enumerate(px.items):
+            self._enter_shard(px, k)
+            for c in prog.posts[idx]:                  # receives due before this item
+                kc, bc = px.items[c]
+                inbox.post(rx_key(kc, bc), prog.src[c],
+                           self._state_shape(self.my_shards[kc][0] - 1, px.batches[bc]), park=c in prog.parked)
+            from_rx = prog.src[idx] is not None
+            state = inbox.get(rx_key(k, b)) if from_rx else self._take_state(px, k, b)
+            if px.ck is not None and self._ckpt_due(k) and state is not None:
+                px.ck.save_state(self._ckpt_key(k), b, state)     # a stage's inputs
+            self._prefetch_activation(px, idx)
+            state = self._compute(px, k, b, state)
+            send_w = self._emit(px, k, b, state, from_rx)
+            del state
+            if from_rx:
+                inbox.release(rx_key(k, b), send_w)
+            # pending sends are retired per micro-batch (the consumer posts its receive at the
+            # point of use); at most SEND_WINDOW outputs stay alive waiting for their consumer
+            px.sends = [(t, w) for (t, w) in px.sends if not w.is_completed()]
+            while len(px.sends) > self.SEND_WINDOW:
+                host_wait(px.sends.pop(0)[1], cuda=self.cuda)
+        if px.ck is not None and px.cur_k >= 0 and self._ckpt_due(px.cur_k):
+            px.ck.commit(self._ckpt_key(px.cur_k), range(len(px.batches)), self.act_dtype)
+
+    def _enter_shard(self, px: "_Pass", k: int) -> None:
+        """Weights of shard k in HBM (the previous shard's released, the next ones prefetched)."""
+        if k == px.cur_k:
+            return
+        pf = self.prefetcher
+        if px.ck is not None and px.cur_k >= 0 and self._ckpt_due(px.cur_k):
+            px.ck.commit(self._ckpt_key(px.cur_k), range(len(px.batches)), self.act_dtype)
+        if self._fault is not None and k == self._fault:
+            raise RuntimeError(f"FLS_FAULT injected on rank {self.comm.rank} at shard {k}")
+        if px.cur_k >= 0:
+            pf.release(px.cur_k)
+            self._throttle(px.shard_ev)
+        with trace.range(f"shard{k}:acquire"):
+            px.W = pf.acquire(k)
+        px.cur_k = k
+        if getattr(pf, "collective", False):
+            px.prefetch_due = k                    # _exec_local: after this shard's first compute
+        else:
+            with trace.range(f"shard{k + 1}:prefetch"):
+                self._prefetch_ahead(k)
+        last = self.my_shards[k][-1]
+        mp = self.plan.mode == "mp"
+        px.dst_rank = self._owner(last + 1) if (mp and last + 1 < self.L) else self.comm.rank
+
+    def _take_state(self, px: "_Pass", k: int, b: int):
+        """Input activation of (shard k, micro-batch b) held on this rank."""
+        if self.my_shards[k][0] == 0:
+            return None
+        if b in px.carry:
+            return px.carry.pop(b)
+        return px.store.get(b)
+
+    def _prefetch_activation(self, px: "_Pass", idx: int) -> None:
+        """One-ahead activation prefetch (crosses shard boundaries; parked receives too)."""
+        if idx + 1 >= len(px.items):
+            return
+        k, _ = px.items[idx]
+        k2, b2 = px.items[idx + 1]
+        if px.prog is not None and px.prog.src[idx + 1] is not None:
+            if idx + 1 in px.prog.parked:
+                px.inbox.prefetch(rx_key(k2, b2))
+        elif self.my_shards[k2][0] > 0 and k2 == k:
+            px.store.prefetch(b2)
+        elif k2 != k and idx + 2 < len(px.items):
+            px.store.prefetch(px.items[idx + 2][1])
+
+    def _compute(self, px: "_Pass", k: int, b: int, state):
+        """Every layer of shard k on micro-batch b."""
+        batch, meta = px.batches[b], px.metas[b]
+        idx = px.pos[(k, b)]
+        last_use = idx + 1 >= len(px.items) or px.items[idx + 1][0] != k
+        tc = time.perf_counter()
+        with trace.range(f"shard{k}:mb{b}:compute"):
+            for li in self.my_shards[k]:
+                name = self.names[li]
+                if hasattr(px.W[name], "final_use"):
+                    px.W[name].final_use = last_use
+                state = run_layer(self.ctx, name, px.W[name], state, batch, meta)
+                if layer_kind(name) == "decoder":
+                    px.flops += layer_flops(self.cfg, batch, self._pruned(name))
+        px.compute_s += time.perf_counter() - tc
+        if px.pbar is not None:
+            px.pbar.update(1)
+        return state
+
+    def _emit(self, px: "_Pass", k: int, b: int, state, from_rx: bool):
+        """Where the output of (shard k, micro-batch b) goes -> the send's work handle, if sent."""
+        last = self.my_shards[k][-1]
+        if from_rx and last < self.L - 1 and px.dst_rank == self.comm.rank:
+            # the residual GEMMs update the received state in place, so it may still BE the
+            # receive-ring slot that inbox.release() hands to the next receive: a state that
+            # stays on this rank (contiguous stages) leaves the slot first (ADVICE r3)
+            state = state.clone()
+        if last == self.L - 1:
+            px.out_pending.append(self._start_output_copy(px.batches[b], state))
+        elif px.dst_rank != self.comm.rank:
+            st = state.contiguous()
+            w = self.comm.isend(st, px.dst_rank)
+            px.sends.append((st, w))
+            return w
+        elif self.storage != "gpu" and px.pos.get((k + 1, b), len(px.items)) - px.pos[(k, b)] <= self.CARRY_WINDOW:
+            # re-used within CARRY_WINDOW micro-batch computes (the zigzag boundary micro-batch
+            # and its neighbour): a PCIe round trip would only add traffic, keep it in HBM
+            px.carry[b] = state
+        else:
+            px.store.put(b, state)
+        return None
+
+    def _close_weights(self, px: "_Pass", ok: bool) -> None:
+        """End of a pass: release the held shard; after an aborted one forget every loaded-but-
+        unused shard (so a later call's loads never land on weights still waiting to be used)
+        and abort the receive ring; after an empty one drop the early prefetch."""
+        pf = self.prefetcher
+        collective = getattr(pf, "collective", False)
+        if px.cur_k >= 0:
+            pf.release(px.cur_k)
+            px.cur_k = -1
+        if not ok:
+            if not collective:
+                pf.discard_loaded()
+            if px.inbox is not None:
+                px.inbox.abort()
+            return
+        if px.items:
             pf.epoch += 1              # the next call's loads continue the slot round-robin
         elif not collective:
-            pf.discard_loaded()        # nothing ran: drop the early prefetch
-        for t, w in sends:
+            pf.discard_loaded()
+
+    def _finish_pass(self, px: "_Pass", t_start: float, h2d0: int, k0: int) -> List[Optional[np.ndarray]]:
+        """Wait for sends and copies, assemble the scores, record the pass statistics."""
+        pf, store = self.prefetcher, px.store
+        h2d_end = pf.bytes_h2d         # after the last release: loads it triggers count to this call
+        for t, w in px.sends:
             w.wait()
         if self.cuda:
             # the compute and activation streams, not the whole device: the weight copy stream
@@ -611,31 +679,32 @@ class ShardedRunner:
             self.h2d_stream.synchronize()
             self.d2h_stream.synchronize()
         rx_stats = {}
-        if inbox is not None:
-            inbox.end_call()
-            rx_stats = {f"rx_{k}": float(v) for k, v in inbox.stats.items()}
-        for batch, host, ev, pool_buf in out_pending:
+        if px.inbox is not None:
+            px.inbox.end_call()
+            rx_stats = {f"rx_{k}": float(v) for k, v in px.inbox.stats.items()}
+        for batch, host, ev, pool_buf in px.out_pending:
             probs = host.numpy()
             r = 0
             for j, pid in enumerate(batch.prompt_ids):
                 ns = batch.n_suffix[j]
-                outputs[pid] = np.expand_dims(probs[r:r + ns].astype(np.float16, copy=True), axis=1)
+                px.outputs[pid] = np.expand_dims(probs[r:r + ns].astype(np.float16, copy=True), axis=1)
                 r += ns
             if pool_buf is not None:
                 store.recycle_host(pool_buf)
         store.clear()
         store.trim()                   # pinned pool follows this call's shapes
         wait_s = pf.take_wait_seconds()
-        if pbar is not None:
-            pbar.close()
-        if ck is not None:
-            ck.clear()                     # run complete: nothing to resume
+        if px.pbar is not None:
+            px.pbar.close()
+        if px.ck is not None:
+            px.ck.clear()              # run complete: nothing to resume
         wall = time.perf_counter() - t_start
+        batches = px.batches
         self.stats = {
-            "wall_s": wall, "compute_launch_s": compute_s,
+            "wall_s": wall, "compute_launch_s": px.compute_s,
             "tokens": float(sum(b.num_tokens for b in batches)),
             "padded_tokens": float(sum(b.padded_tokens for b in batches)),
-            "decoder_flops": flops, "micro_batches": float(len(batches)),
+            "decoder_flops": px.flops, "micro_batches": float(len(batches)),
             "weight_wait_s": wait_s, "weight_h2d_bytes": float(h2d_end - h2d0),
             "act_d2h_bytes": float(store.bytes_d2h), "act_h2d_bytes": float(store.bytes_h2d),
             "resumed_from_shard": float(k0),
@@ -647,10 +716,10 @@ class ShardedRunner:
         if self.verbose:
             # utils.py:304 prints "loaded N layers in Ts" per device
             n_layers = sum(len(s) for s in self.my_shards[k0:])
-            print(f"{self.dev} rank{comm.rank}: loaded {n_layers} layers in {wait_s:.2f}s "
+            print(f"{self.dev} rank{self.comm.rank}: loaded {n_layers} layers in {wait_s:.2f}s "
                   f"(exposed weight wait); {len(self.my_shards)} shards, {len(batches)} micro-batches, "
                   f"{self.stats['tokens']:.0f} tokens in {wall:.2f}s")
-        return outputs
+        return px.outputs
 
     # model parallel: outputs waiting for their consumer before the host waits for the oldest
     SEND_WINDOW = 3

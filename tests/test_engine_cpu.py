@@ -679,7 +679,7 @@ def test_suffix_kv_reuse_partial_and_overflow(tiny_model):
     old = PrefixKVCache.SUFFIX_GROWTH
     PrefixKVCache.SUFFIX_GROWTH = 8
     try:
-        r = ShardedRunner(cfg, FileLayerSource(cfg, path), "cpu", tok, prefix_kv_cache=True)
+        r = ShardedRunner(cfg, FileLayerSource(cfg, path), "cpu", tok, prefix_kv_cache=True, suffix_kv_cache=True)
         reused = []
         for prompts in (base, step2, step3, step4):
             got, want = r(prompts), plain(prompts)
