@@ -661,8 +661,11 @@ class ShardedRunner:
             if px.inbox is not None:
                 px.inbox.abort()
             return
-        if px.items:
-            pf.epoch += 1              # the next call's loads continue the slot round-robin
+        if px.items or (collective and self.my_shards):
+            # the next call's loads continue the slot round-robin (a data-parallel rank with no
+            # prompts also went through every shard: its piece / slot numbering must advance with
+            # the other ranks', whose gathers it joins)
+            pf.epoch += 1
         elif not collective:
             pf.discard_loaded()
 

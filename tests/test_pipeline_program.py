@@ -235,11 +235,12 @@ def test_loopback_all_gather_in_place_and_dup():
             assert res[(r, it)] == sum([[10 * it + q + 1] * 4 for q in range(3)], [])
 
 
-@pytest.mark.parametrize("G", [2, 3])
-def test_data_parallel_over_loopback_threads(deep6, G):
+@pytest.mark.parametrize("G,n", [(2, 7), (3, 7), (9, 7)])
+def test_data_parallel_over_loopback_threads(deep6, G, n):
     """Data parallel with G ranks as threads (AllGatherPrefetcher: 1/G slices + loopback
     all-gather into the weight slot): each rank's scores == a one-process run on its prompts,
-    over two calls (slot rotation across calls)."""
+    over two calls (slot rotation across calls); G > prompts: ranks with no prompts join every
+    gather of both calls."""
     import numpy as np
     from flexible_llm_sharding_amd.engine import ShardedRunner
     from flexible_llm_sharding_amd.parallel.comm import LoopbackComm, LoopbackHub
@@ -247,6 +248,7 @@ def test_data_parallel_over_loopback_threads(deep6, G):
     from flexible_llm_sharding_amd.parallel.planner import make_plan
     from flexible_llm_sharding_amd.runtime.stream import FileLayerSource
     cfg, path, tok, prompts, _ = deep6
+    prompts = prompts[:n]
     torch.set_num_threads(1)
     idx = np.array_split(np.arange(len(prompts)), G)
     hub = LoopbackHub(G, timeout_s=60)
@@ -274,6 +276,9 @@ def test_data_parallel_over_loopback_threads(deep6, G):
     for r in range(G):
         if isinstance(res[r], BaseException):
             raise res[r]
+        if not len(idx[r]):
+            assert all(call == [] for call in res[r])
+            continue
         want = ShardedRunner(cfg, FileLayerSource(cfg, path), "cpu", tok, token_budget=40)([prompts[i] for i in idx[r]])
         for call in res[r]:
             assert len(call) == len(want)
