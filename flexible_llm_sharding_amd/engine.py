@@ -137,9 +137,13 @@ class ShardedRunner:
         attn_rows = qkv_chunk = 0
         self._outside = None
         self.ops = get_ops(self.dev)
-        # this runner's split-K / split-KV scratch: reserved before any memory is planned, so a
-        # capped and an uncapped run take the same GEMM paths (bitwise-equal scores)
-        self._splitk_ws = self.ops.new_workspace(self.dev) if hasattr(self.ops, "new_workspace") else None
+        # this runner's split-K / split-KV scratch (64 MB): the free tail of the activation arena —
+        # split-K only runs for <= 512-row GEMMs, whose phase carves a sliver of an arena sized for
+        # the whole micro-batch — or, when the arena is too small, a buffer of its own.  Every
+        # runner gets the same 64 MB either way, so a capped and an uncapped run take the same GEMM
+        # paths (bitwise-equal scores) and a cap is not charged for memory that is already there.
+        self._splitk_own = None
+        self._splitk_ws = self._splitk_scratch if hasattr(self.ops, "new_workspace") else None
         if max_vram_gb:
             # size the micro-batch and the QKV / MLP chunks to the HBM cap (runtime/memplan.py);
             # re-planned per call once its token count is known (_plan_call)
@@ -147,10 +151,7 @@ class ShardedRunner:
             if self.dev.type == "cuda":
                 # device memory held outside the caching allocator before any weight slot exists:
                 # context, code objects, RCCL buffers (warmed up above) — planned as measured
-                # + the split-K scratch (allocator memory, outside the activation plan)
-                ws = self._splitk_ws.numel() if self._splitk_ws is not None else 0
-                self._outside = (device_used_bytes(self.dev) - torch.cuda.memory_reserved(self.dev) + (64 << 20)
-                                 + ws)
+                self._outside = device_used_bytes(self.dev) - torch.cuda.memory_reserved(self.dev) + (64 << 20)
             try:
                 # provisional (the call's token count is unknown yet); _plan_call is authoritative
                 token_budget, mlp_chunk, attn_rows, qkv_chunk, est = plan_for_vram(
@@ -258,6 +259,15 @@ class ShardedRunner:
         out = self.run_tokenized(tps)
         self.stats["host_tokenize_s"] = t_tok
         return out
+
+    def _splitk_scratch(self):
+        from .ops.hip_backend import SPLITK_WS_BYTES
+        ws = self.ctx.ws.tail(SPLITK_WS_BYTES) if self.ctx.ws is not None else None
+        if ws is not None:
+            return ws
+        if self._splitk_own is None:
+            self._splitk_own = self.ops.new_workspace(self.dev)
+        return self._splitk_own
 
     def _workspace(self):
         """This runner's split-K scratch installed for the calling thread (ops/hip_backend.py)."""
@@ -946,4 +956,4 @@ class ShardedRunner:
         if self._store is not None:
             self._store.close()
             self._store = None
-        self._splitk_ws = None
+        self._splitk_ws = self._splitk_own = None

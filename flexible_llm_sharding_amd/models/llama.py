@@ -147,6 +147,18 @@ class Workspace:
             self.buf = torch.empty(need, dtype=self.dtype, device=self.device)
         self.pos = 0
 
+    def tail(self, nbytes: int) -> Optional[torch.Tensor]:
+        """The arena's free bytes after the current phase's carvings, as a uint8 view of exactly
+        ``nbytes`` (None if fewer are free): scratch for a kernel that runs between this phase's
+        carvings and the next (the small-M split-K GEMM partials; the compute stream orders it)."""
+        if self.buf is None:
+            return None
+        es = self.buf.element_size()
+        start = (self.pos * es + 255) // 256 * 256
+        if start + nbytes > self.buf.numel() * es:
+            return None
+        return self.buf.view(torch.uint8)[start:start + nbytes]
+
     def nbytes(self) -> int:
         return 0 if self.buf is None else self.buf.numel() * self.buf.element_size()
 

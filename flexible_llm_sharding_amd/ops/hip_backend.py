@@ -112,8 +112,8 @@ class HipOps:
         return torch.empty(SPLITK_WS_BYTES, dtype=torch.uint8, device=device)
 
     def use_workspace(self, ws):
-        """Context manager: GEMMs / attention issued by this host thread use ``ws`` as their fp32
-        partial scratch.  A runner's kernels run on one stream in order, so its GEMMs and attention
+        """Context manager: GEMMs / attention issued by this host thread use ``ws`` (a buffer of
+        ``SPLITK_WS_BYTES``, or a callable returning one at each use) as their fp32 partial scratch.  A runner's kernels run on one stream in order, so its GEMMs and attention
         share it; runners driven from different threads (ranks as threads on one GPU) each install
         their own, since their multi-kernel sequences (partials, then reduce) can interleave."""
         ops = self
@@ -128,9 +128,12 @@ class HipOps:
         return _Use()
 
     def _splitk_ws(self, device, M: int, N: int):
-        """The scratch of the calling thread's runner (:meth:`use_workspace`); outside a runner
-        (kernel tests, tools) one buffer per (device, thread), reserved at first use."""
+        """The scratch of the calling thread's runner (:meth:`use_workspace`: a buffer, or a callable
+        returning one); outside a runner (kernel tests, tools) one buffer per (device, thread),
+        reserved at first use."""
         ws = getattr(self._tl, "ws", None)
+        if callable(ws):
+            ws = ws()
         if ws is not None:
             return ws
         key = (torch.device(device), threading.get_ident())
