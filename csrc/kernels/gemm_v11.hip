@@ -33,6 +33,10 @@
 // every LDS-DMA source row is in bounds and the per-piece row offsets live in the scalar soffset.
 #include "gemm_v10.h"
 
+#ifndef V11_SCHED
+#define V11_SCHED 1        // LDS-DMA placement (A/B builds): 1 = 4 / 4 / 12 per super-phase, 2 = 8 / 4 / 8
+#endif
+
 namespace {
 namespace v11 {
 constexpr int TM = 384, TN = 256, TK = 64;
@@ -234,10 +238,17 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_v11(const half_t* __restrict__
     for (int i = 0; i < 4; ++i) V11_DMA_X(rA, 1, 0, i, k1);
 #pragma unroll
     for (int i = 0; i < 4; ++i) V11_DMA_X(rA, 1, 1, i, k1);
+#if V11_SCHED == 2
+#pragma unroll
+    for (int i = 0; i < 4; ++i) V11_DMA_W(rW, 1, i, k1);     // W-lo(1); W-hi(1) in SP0 of tile 0
+  }
+  asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+#else
 #pragma unroll
     for (int i = 0; i < 8; ++i) V11_DMA_W(rW, 1, i, k1);
   }
   asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+#endif
   __builtin_amdgcn_s_barrier();
 #pragma unroll
   for (int u = 0; u < 8; ++u) V11_RX(u, 0, 0);
@@ -274,8 +285,38 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_v11(const half_t* __restrict__
     V11_PHASE_C((B) ^ 1, 0, dW2, 6);                     /* C s1 */                              \
     V11_SYNC(8, 16);                                     /* SP2 */                               \
   }
+#if V11_SCHED == 2
+#undef V11_TILE
+    // rebalanced: 8 / 4 / 8 DMAs per super-phase (W split: W-lo(t+2) in SP2 of tile t, W-hi(t+2)
+    // in SP0 of tile t+1, waited at the end of SP1 of tile t+1 with everything older)
+    //   SP0: X2(t+1) + W-hi(t+1) -> b^1   lgkmcnt(6) vmcnt(16)
+    //   SP1: X0(t+2) -> b                 lgkmcnt(6) vmcnt(4)
+    //   SP2: X1(t+2) + W-lo(t+2) -> b     lgkmcnt(8) vmcnt(12)
+    const __amdgpu_buffer_rsrc_t rW1 = kt + 1 < nk ? rW : rZW;
+#define V11_TILE(B, rXn, rWn, kn, rXf, rWf, kf)                                                    \
+  {                                                                                               \
+    auto dX2 = [&](int d) { V11_DMA_X(rXn, (B) ^ 1, 2, d, kn); };                                 \
+    auto dWhi = [&](int d) { V11_DMA_W(rWn, (B) ^ 1, d + 4, kn); };                               \
+    auto dX0a = [&](int d) { V11_DMA_X(rXf, B, 0, d, kf); };                                      \
+    auto dX0b = [&](int d) { V11_DMA_X(rXf, B, 0, d + 2, kf); };                                  \
+    auto dX1 = [&](int d) { V11_DMA_X(rXf, B, 1, d, kf); };                                       \
+    auto dWlo = [&](int d) { V11_DMA_W(rWf, B, d, kf); };                                         \
+    V11_PHASE_A(B, 0, B, 1, dX2, 4);                     /* A s0 */                              \
+    V11_PHASE_B(B, 0, B, 1, dWhi, 4);                    /* B s0 */                              \
+    V11_SYNC(6, 16);                                     /* SP0 */                               \
+    V11_PHASE_C(B, 1, dX0a, 2);                          /* C s0 */                              \
+    V11_PHASE_A(B, 1, (B) ^ 1, 0, dX0b, 2);              /* A s1 */                              \
+    V11_SYNC(6, 4);                                      /* SP1 */                               \
+    V11_PHASE_B(B, 1, (B) ^ 1, 0, dX1, 4);               /* B s1 */                              \
+    V11_PHASE_C((B) ^ 1, 0, dWlo, 4);                    /* C s1 */                              \
+    V11_SYNC(8, 12);                                     /* SP2 */                               \
+  }
+    V11_TILE(0, rX1, rW1, k1, rX2, rW2, k2);   // tile kt,   stage 0
+    V11_TILE(1, rX2, rW2, k2, rX3, rW3, k3);   // tile kt+1, stage 1
+#else
     V11_TILE(0, rX1, k1, rX2, rW2, k2);        // tile kt,   stage 0
     V11_TILE(1, rX2, k2, rX3, rW3, k3);        // tile kt+1, stage 1
+#endif
 #undef V11_TILE
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

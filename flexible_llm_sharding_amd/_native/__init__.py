@@ -66,11 +66,13 @@ class Piece(ctypes.Structure):
 KERNELS_ABI = 16   # bumped whenever a C signature in csrc/include/fls.h changes
 
 
-def _load_kernels():
-    lib = ctypes.CDLL(_KERNELS)
+def _load_kernels(path: str = _KERNELS):
+    """Load and bind a kernel library (``path``: the in-tree build, or an A/B variant build of the
+    same sources, ``build.py --variant``)."""
+    lib = ctypes.CDLL(path)
     _bind(lib, "fls_kernels_version", c_int)
     if lib.fls_kernels_version() != KERNELS_ABI:
-        raise RuntimeError(f"{_KERNELS} is a stale build (ABI {lib.fls_kernels_version()} != {KERNELS_ABI}); "
+        raise RuntimeError(f"{path} is a stale build (ABI {lib.fls_kernels_version()} != {KERNELS_ABI}); "
                            "rebuild with python -m flexible_llm_sharding_amd._native.build")
     _bind(lib, "fls_gemm", c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
           c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,

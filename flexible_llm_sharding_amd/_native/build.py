@@ -57,8 +57,13 @@ def _run(cmd, verbose):
         print(r.stdout)
 
 
-def build_kernels(force=False, jobs=8, verbose=False, extra_flags=()):
-    os.makedirs(OBJ, exist_ok=True)
+def build_kernels(force=False, jobs=8, verbose=False, extra_flags=(), variant: str = ""):
+    """``variant`` (A/B builds): objects under obj/<variant>/ and the library
+    ``variants/libfls_kernels_<variant>.so``, compiled with ``extra_flags`` (e.g. -DV11_SCHED=2)."""
+    obj_dir = os.path.join(OBJ, variant) if variant else OBJ
+    out_so = os.path.join(HERE, "variants", f"libfls_kernels_{variant}.so") if variant else KERNELS_SO
+    os.makedirs(obj_dir, exist_ok=True)
+    os.makedirs(os.path.dirname(out_so), exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     hdrs = _headers()
     inc = ["-I", os.path.join(CSRC, "include"), "-I", os.path.join(CSRC, "kernels")]
@@ -66,16 +71,16 @@ def build_kernels(force=False, jobs=8, verbose=False, extra_flags=()):
              "-munsafe-fp-atomics", "-Wno-unused-result"] + list(extra_flags)
     objs, cmds = [], []
     for s in srcs:
-        o = os.path.join(OBJ, os.path.basename(s) + ".o")
+        o = os.path.join(obj_dir, os.path.basename(s) + ".o")
         objs.append(o)
         if force or _stale(o, [s] + hdrs):
             cmds.append([_hipcc()] + flags + inc + ["-c", s, "-o", o])
     if cmds:
         with ThreadPoolExecutor(max(1, jobs)) as ex:
             list(ex.map(lambda c: _run(c, verbose), cmds))
-    if force or cmds or _stale(KERNELS_SO, objs):
-        _run([_hipcc(), "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", KERNELS_SO] + objs, verbose)
-    return KERNELS_SO
+    if force or cmds or _stale(out_so, objs):
+        _run([_hipcc(), "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", out_so] + objs, verbose)
+    return out_so
 
 
 def build_runtime(force=False, verbose=False, sanitize=False):
@@ -106,7 +111,12 @@ def main(argv=None):
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 4))
     ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--variant", default="", help="A/B build: name of a kernel-library variant")
+    ap.add_argument("--define", action="append", default=[], help="-D flags of the variant (NAME=VALUE)")
     a = ap.parse_args(argv)
+    if a.variant:
+        print("built", build_kernels(a.force, a.jobs, a.verbose, ["-D" + d for d in a.define], a.variant))
+        return 0
     for p in build_all(a.force, a.jobs, a.verbose):
         print("built", p)
 
