@@ -341,19 +341,43 @@ def main(argv=None):
     n_prompts = a.prompts_per_gpu * (world if mode == "mp" else 1)
     prompts = synthetic_prompts(n_prompts, a.prefix_len, a.n_suffix, a.suffix_len, cfg.vocab_size,
                                 seed=a.seed + (rank if dp else 0))
-    pf = None
-    if dp:
-        my = [s for s in plan.my_shards if len(s)]
-        if a.max_vram_gb and a.lnps == 1 and not a.resident and isinstance(store, SlicedHostStore) and not a.cpu:
-            pf = AllGatherPiecePool(store, names, my, dev, comm)       # the 1-GPU memory envelope
-        else:
-            pf = AllGatherPrefetcher(store, names, my, dev, comm, resident=a.resident)
-    runner = ShardedRunner(cfg, store, dev, tok, layer_num_per_shard=a.lnps, storage_location=a.storage,
-                           disk_folder=f"/tmp/fls_bench_spill_{rank}", prefix_attention=a.prefix_attention,
-                           token_budget=a.token_budget, mlp_chunk=a.mlp_chunk, resident=a.resident, comm=comm,
-                           data_parallel=dp, n_slots=a.slots, hbm_cache_gb=a.hbm_cache_gb,
-                           prefetcher=pf, hip_graphs=a.hip_graphs, prune_last_layer=not a.no_prune_last,
-                           pipeline_stages=a.stages, max_vram_gb=a.max_vram_gb)
+    def build(cap):
+        pf = None
+        if dp:
+            my = [s for s in plan.my_shards if len(s)]
+            if cap and a.lnps == 1 and not a.resident and isinstance(store, SlicedHostStore) and not a.cpu:
+                pf = AllGatherPiecePool(store, names, my, dev, comm)       # the 1-GPU memory envelope
+            else:
+                pf = AllGatherPrefetcher(store, names, my, dev, comm, resident=a.resident)
+        return ShardedRunner(cfg, store, dev, tok, layer_num_per_shard=a.lnps, storage_location=a.storage,
+                             disk_folder=f"/tmp/fls_bench_spill_{rank}", prefix_attention=a.prefix_attention,
+                             token_budget=a.token_budget, mlp_chunk=a.mlp_chunk, resident=a.resident, comm=comm,
+                             data_parallel=dp, n_slots=a.slots, hbm_cache_gb=a.hbm_cache_gb,
+                             prefetcher=pf, hip_graphs=a.hip_graphs, prune_last_layer=not a.no_prune_last,
+                             pipeline_stages=a.stages, max_vram_gb=cap)
+
+    runner, cap_note = None, None
+    try:
+        runner = build(a.max_vram_gb)
+        if a.max_vram_gb:
+            runner._plan_call(runner.tokenize(prompts), False)    # the cap must hold this call's plan
+        ok = 1.0
+    except ValueError as e:
+        ok, cap_note = 0.0, str(e)
+    if world > 1:
+        # every rank takes the same path (the rebuild creates communicators collectively); the
+        # capped plan can fail only on multi-GPU boxes, where RCCL's buffers are counted
+        ok = comm.all_reduce_min(ok)
+    if not ok:
+        log(rank, f"[bench] --max-vram-gb {a.max_vram_gb} cannot hold this run ({cap_note or 'another rank'}): "
+                  "running uncapped")
+        if runner is not None:
+            runner.close()
+        if not a.cpu:
+            torch.cuda.set_per_process_memory_fraction(1.0, dev)
+        cap_note = f"--max-vram-gb {a.max_vram_gb} infeasible: {cap_note or 'on another rank'}"
+        a.max_vram_gb = None
+        runner = build(None)
     if a.attn_rows:
         runner.ctx.attn_rows = a.attn_rows
     if runner.vram_plan:
@@ -435,7 +459,7 @@ def main(argv=None):
                    "weights": a.weights, "resident": a.resident, "hip_graphs": bool(runner.hip_graphs),
                    "token_budget": runner.token_budget, "mlp_chunk": runner.mlp_chunk,
                    "weight_slots": runner.prefetcher.n_slots, "hbm_cache_gb": a.hbm_cache_gb,
-                   "max_vram_gb": a.max_vram_gb},
+                   "max_vram_gb": a.max_vram_gb, "cap_fallback": cap_note},
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
