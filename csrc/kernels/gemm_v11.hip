@@ -36,6 +36,9 @@
 #ifndef V11_SCHED
 #define V11_SCHED 1        // LDS-DMA placement (A/B builds): 1 = 4 / 4 / 12 per super-phase, 2 = 8 / 4 / 8
 #endif
+#ifndef V11_AORDER
+#define V11_AORDER 0       // phase A MFMA order (A/B builds): 0 = column-major, 1 = row-major
+#endif
 
 namespace {
 namespace v11 {
@@ -189,6 +192,18 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_v11(const half_t* __restrict__
 // refills of the preceding C phase have ~29 MFMAs to land).  After MFMA 1 / 3 read x rows 8 / 9
 // of the current k-step (cbuf, cs); after the last use of x row u (MFMA 28 + u) refill it with
 // the next k-step (nbuf, ns).
+#if V11_AORDER == 1
+// A/B build: phase A row-major (x row u refilled after its 8th MFMA; w column t first used at MFMA t)
+#define V11_PHASE_A(cbuf, cs, nbuf, ns, DMA_STMT, ND)                                             \
+  _Pragma("unroll") for (int i_ = 0; i_ < 32; ++i_) {                                             \
+    const int u_ = i_ >> 3, t_ = i_ & 7;                                                          \
+    V11_MFMA(u_, t_);                                                                             \
+    if (i_ == 1) V11_RX(8, cbuf, cs);                                                             \
+    if (i_ == 3) V11_RX(9, cbuf, cs);                                                             \
+    if ((i_ & 7) == 7) V11_RX(u_, nbuf, ns);                                                      \
+    V11_DMAS(i_, DMA_STMT, ND);                                                                   \
+  }
+#else
 #define V11_PHASE_A(cbuf, cs, nbuf, ns, DMA_STMT, ND)                                             \
   _Pragma("unroll") for (int i_ = 0; i_ < 32; ++i_) {                                             \
     const int t_ = i_ >> 2, u_ = i_ & 3;                                                          \
@@ -198,6 +213,7 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_v11(const half_t* __restrict__
     if (i_ >= 28) V11_RX(u_, nbuf, ns);                                                           \
     V11_DMAS(i_, DMA_STMT, ND);                                                                   \
   }
+#endif
 // Phase B: x rows 4..7 x w 0..7, row-major; reads x rows 10 / 11 of the current k-step after
 // MFMAs 1 / 3 and refills x row u after its last MFMA (8u' + 7).
 #define V11_PHASE_B(cbuf, cs, nbuf, ns, DMA_STMT, ND)                                             \
