@@ -34,7 +34,8 @@
 #include "gemm_v10.h"
 
 #ifndef V11_SCHED
-#define V11_SCHED 1        // LDS-DMA placement (A/B builds): 1 = 4 / 4 / 12 per super-phase, 2 = 8 / 4 / 8
+#define V11_SCHED 2        // LDS-DMA placement: 2 = 8 / 4 / 8 per super-phase (default: +0-1.5% over 1 on the
+                           // four 70B shapes, profiles/r4_gemm/variant_ab_s2_a1.log), 1 = 4 / 4 / 12
 #endif
 #ifndef V11_AORDER
 #define V11_AORDER 0       // phase A MFMA order (A/B builds): 0 = column-major, 1 = row-major
