@@ -420,7 +420,10 @@ int launch(int hpb, dim3 grid, hipStream_t st, const half_t* qkv, half_t* out, c
 #define FLS_ATTN_LAUNCH_SPL(HPB_)                                                                              \
   hipLaunchKernelGGL((attn_fwd<HD, HPB_, WPH, true, true>), g3, dim3(64 * WPH * HPB_), 0, st, qkv, out, work, seg_lo, \
                      nh, nkv, ld_qkv, ld_out, scale_log2, kv0, ld_kv0, work2, r2win, part)
-      if constexpr (WPH == 2) {
+      if constexpr (WPH == 1) {
+        if (hpb == 8) FLS_ATTN_LAUNCH_SPL(8);
+        else FLS_ATTN_LAUNCH_SPL(4);
+      } else if constexpr (WPH == 2) {
         if (hpb == 4) FLS_ATTN_LAUNCH_SPL(4);
         else if (hpb == 2) FLS_ATTN_LAUNCH_SPL(2);
         else FLS_ATTN_LAUNCH_SPL(1);
@@ -440,6 +443,9 @@ int launch(int hpb, dim3 grid, hipStream_t st, const half_t* qkv, half_t* out, c
                      nkv, ld_qkv, ld_out, scale_log2, kv0, ld_kv0, work2, r2win, nullptr)
   if constexpr (HD == 96) {
     FLS_ATTN_LAUNCH(1);                     // 12 chunks per row: one head per block divides the tile
+  } else if constexpr (WPH == 1) {          // 4 or 8 heads (dispatch)
+    if (hpb == 8) FLS_ATTN_LAUNCH(8);
+    else FLS_ATTN_LAUNCH(4);
   } else if constexpr (WPH == 2) {
     if (hpb == 4) FLS_ATTN_LAUNCH(4);
     else if (hpb == 2) FLS_ATTN_LAUNCH(2);
@@ -480,17 +486,22 @@ int dispatch(const void* qkv, void* out, const int* work, int n_items, int n_q_h
              fls_stream_t s) {
   if (n_q_heads % n_kv_heads) return -2;
   if (head_dim != 64 && head_dim != 96 && head_dim != 128) return -3;
-  if (q_block != 64 && q_block != 128) return -5;
+  // q_block 32 (one wave per head): range-2 items of at most 32 rows (generation steps)
+  if (q_block != 64 && q_block != 128 && !(R2 && q_block == 32)) return -5;
   const float scale_log2 = scale * 1.4426950408889634f;
   auto st = (hipStream_t)s;
   const int group = n_q_heads / n_kv_heads;
   // heads of one KV group per block share every staged K/V tile: up to 4 (64-row items) or 2
   // (128-row items, 4 waves per head) as the group allows, else 1 (multi-head attention)
+  // (32-row items: up to 8, a whole 70B KV group, so every prompt's prefix K/V is read once per
+  // layer; 8 heads x 2 waves = 1024 threads measured 4x slower (profiles/r3_attn): not built)
+  // one wave per head pays only with several heads per block (a 64-thread block of 16 staging
+  // chunks per lane and 2 waves per CU would not): small groups keep the 2-wave layout
+  if (q_block == 32 && (group % 4 || head_dim == 96)) q_block = 64;
+  const int hpb_max = q_block == 32 ? 8 : (q_block == 64 ? 4 : 2);
   int hpb = 1;
-  if (q_block == 64) hpb = group % 4 == 0 ? 4 : (group % 2 == 0 ? 2 : 1);
-  else hpb = group % 2 == 0 ? 2 : 1;
-  // 8 heads per block (1024 threads, one block per CU) measured 4x slower (profiles/r3_attn): not built
-  if (g_hpb > 0 && group % g_hpb == 0 && g_hpb <= (q_block == 64 ? 4 : 2)) hpb = g_hpb;
+  while (hpb * 2 <= hpb_max && group % (hpb * 2) == 0) hpb *= 2;
+  if (g_hpb > 0 && group % g_hpb == 0 && g_hpb <= hpb_max && (q_block != 32 || g_hpb >= 4)) hpb = g_hpb;
   if (head_dim == 96) hpb = 1;              // Phi-3-mini geometry (multi-head attention anyway)
   const dim3 grid(n_items, n_q_heads / hpb);
   // split-KV (range-2 kernel) only when the grid leaves CUs idle (a long prompt or two decoding
@@ -508,6 +519,13 @@ int dispatch(const void* qkv, void* out, const int* work, int n_items, int n_q_h
   auto q = (const half_t*)qkv;
   auto o = (half_t*)out;
   auto k0 = (const half_t*)kv0;
+  if constexpr (R2) {
+    if (q_block == 32)                      // head_dim 64 / 128 here (96 fell back above)
+      return head_dim == 128 ? launch<128, 1, true>(hpb, grid, st, q, o, work, seg_lo, n_q_heads, n_kv_heads, ld_qkv,
+                                                    ld_out, scale_log2, k0, ld_kv0, work2, r2win, part, ns)
+                             : launch<64, 1, true>(hpb, grid, st, q, o, work, seg_lo, n_q_heads, n_kv_heads, ld_qkv,
+                                                   ld_out, scale_log2, k0, ld_kv0, work2, r2win, part, ns);
+  }
   if (head_dim == 96)
     return q_block == 64 ? launch<96, 2, R2>(hpb, grid, st, q, o, work, seg_lo, n_q_heads, n_kv_heads, ld_qkv, ld_out,
                                          scale_log2, k0, ld_kv0, work2, r2win, part, ns)

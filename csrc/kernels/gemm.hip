@@ -337,6 +337,8 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
 }
 
+#include "gemm_skinny.h"
+
 // -> slices per tile (0: split-K not applicable / no room in the workspace)
 int splitk_slices(int M, int N, int K, size_t tiles, size_t ws_bytes) {
   if (tiles >= 128) return 0;
@@ -372,6 +374,10 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
                         ldw % 8 == 0 && (size_t)M * lda * 2 < (1ull << 32) && ldc % 4 == 0 &&
                         ((uintptr_t)C & 7) == 0 && ((uintptr_t)ws & 15) == 0 &&
                         (EPI != FLS_EPI_RESID || (ep.ldr % 4 == 0 && ((uintptr_t)ep.R & 7) == 0));
+  {
+    const int rc = try_skinny<EPI>(A, W, C, M, N, K, lda, ldw, ldc, ep, s, ws, ws_bytes);
+    if (rc) return rc > 0 ? 0 : rc;
+  }
   const int S = split_ok ? splitk_slices(M, N, K, tiles256, ws_bytes) : 0;
   if (S >= 2 && (M > 64 || tiles256 * S >= 128)) {
     static bool attr_f32 = false;
@@ -449,12 +455,21 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
 
 }  // namespace
 
-extern "C" int fls_kernels_version(void) { return 16; }
+extern "C" int fls_kernels_version(void) { return 17; }
 
 // tile order: 0 = by shape (default); g > 0: groups of g M tiles; g < 0: groups of -g N tiles (A/B, tests)
 extern "C" int fls_gemm_set_order(int order) {
   const int old = g_order;
   g_order = order;
+  return old;
+}
+
+// skinny-M path (gemm_skinny.h): 0 off, 1 auto (default), 2 every M <= 256 it supports; blocks: the
+// K-split target (0 keeps the current); returns the previous mode
+extern "C" int fls_gemm_set_skinny(int mode, int blocks) {
+  const int old = g_skinny;
+  g_skinny = mode < 0 ? 0 : mode > 2 ? 2 : mode;
+  if (blocks > 0) g_skinny_blocks = blocks;
   return old;
 }
 

@@ -291,8 +291,9 @@ def _attention_whole(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tens
     if work_items and "work2" in meta:       # suffix K/V reuse: range 2 = the suffixes' kept rows
         kw["work2"] = meta["work2_last"] if prune else meta["work2"]
         kw["r2win"] = meta["r2win"]
+    qb = batch.r2_q_block if "work2" in kw else batch.q_block     # (work_last items: one row each)
     a = ops.attention(qkv, attn_arg, cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim,
-                      kv0=kv0 if batch.kv_cached else None, q_block=batch.q_block, out=qkv[:, :cfg.q_size], **kw)
+                      kv0=kv0 if batch.kv_cached else None, q_block=qb, out=qkv[:, :cfg.q_size], **kw)
     del qkv
     if prune:
         idx = meta["last_idx"]

@@ -28,6 +28,7 @@ causal mask they cannot influence it.
 from __future__ import annotations
 
 import dataclasses
+import os
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
 
@@ -53,6 +54,11 @@ class Segment:
     q_off: int = 0       # index of the first query inside its segment (causal compare)
     r2_start: int = 0    # suffix K/V reuse: rows of the K/V cache holding this suffix's earlier
     r2_len: int = 0      # tokens (all visible), between the prefix (r0) and the new rows (r1)
+
+
+# range-2 attention of <= 32-row items with one wave per head (32, default) or the 2-wave kernel
+# (64: A/B of the generation step, FLS_R2_QBLOCK=64)
+R2_Q_BLOCK = int(os.environ.get("FLS_R2_QBLOCK", "32"))
 
 
 @dataclass
@@ -87,6 +93,16 @@ class PackedBatch:
     @property
     def n_scored(self) -> int:
         return int(self.last_idx.shape[0])
+
+    @property
+    def r2_q_block(self) -> int:
+        """q_block for the range-2 (suffix K/V reuse) attention: 32 when every work item holds at
+        most 32 rows (a generation step: one new row per suffix), so the kernel runs one wave per
+        query head and a whole KV group per block (each prompt's prefix K/V read once per layer);
+        the batch's own q_block otherwise."""
+        if R2_Q_BLOCK != 32 or self.work2 is None or self.work.shape[0] == 0 or int(self.work[:, 1].max()) > 32:
+            return self.q_block
+        return 32
 
     def attn_groups(self, max_rows: int) -> List[dict]:
         """Prompt-aligned row groups of <= ``max_rows`` packed rows (a larger prompt is a group of

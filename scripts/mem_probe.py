@@ -58,10 +58,18 @@ def sample():
 
 t = threading.Thread(target=sample, daemon=True)
 t.start()
+def stats():
+    st = torch.cuda.memory_stats(dev)
+    return {k: st.get(k, 0) for k in ("num_alloc_retries", "num_device_alloc", "num_device_free", "num_ooms")}
+
+
 for i in range(3):
     t0 = time.perf_counter()
+    s0 = stats()
     r(prompts)
     torch.cuda.synchronize()
+    s1 = stats()
+    print(f"[probe] allocator during call {i}: " + ", ".join(f"{k} +{s1[k] - s0[k]}" for k in s0), flush=True)
     print(f"[probe] call {i}: {time.perf_counter() - t0:.2f}s outside-now {outside(slots()):.0f} MB, peak outside "
           f"{peak['v']:.0f} MB, peak used {peak['used']:.3f} GB, reserved peak "
           f"{torch.cuda.max_memory_reserved(dev) / 1e9:.3f} GB", flush=True)

@@ -444,16 +444,18 @@ def test_qkv_norm_rope(ops, ref, nq, nk, hd):
         assert rel_err(y[:, v0:], (x.float() @ w.float().t())[:, v0:]) < 2e-3
 
 
+@pytest.mark.parametrize("q_block", [64, 32])
 @pytest.mark.parametrize("split", [0, 1, 3, 8])
-@pytest.mark.parametrize("nh,nkv,hd", [(8, 1, 128), (4, 4, 64), (4, 4, 96)])
-def test_attention_suffix_rows_from_cache(ops, ref, nh, nkv, hd, split):
+@pytest.mark.parametrize("nh,nkv,hd", [(8, 1, 128), (16, 2, 128), (8, 2, 64), (4, 4, 64), (4, 4, 96)])
+def test_attention_suffix_rows_from_cache(ops, ref, nh, nkv, hd, split, q_block):
     """Suffix K/V reuse: the kept rows of each suffix read from the cache as range 2 (with the
     prefix as range 0) and only the new rows computed == the full packed pass on those rows.
     split: key-tile slices of the split-KV kernel (0 = by grid size, which splits this small grid;
-    1 = one block per item and head; hd 96 never splits)."""
+    1 = one block per item and head; hd 96 never splits).  q_block 32: one wave per head, 4 or 8
+    heads of a KV group per block (groups of < 4 heads fall back to the 2-wave kernel)."""
     old = ops.k.fls_attention_set_split(split)
     try:
-        _suffix_rows_from_cache(ops, ref, nh, nkv, hd)
+        _suffix_rows_from_cache(ops, ref, nh, nkv, hd, q_block=q_block)
     finally:
         ops.k.fls_attention_set_split(old)
 
@@ -465,16 +467,19 @@ def test_attention_decode_split_matches_unsplit(ops, ref):
     prompts = [(600, [41] * 5)] * 12
     keep = [[40] * 5] * 12
     ys = []
-    for split in (1, 0):
+    for split, qb in ((1, 64), (0, 64), (1, 32), (0, 32)):
         old = ops.k.fls_attention_set_split(split)
         try:
-            ys.append(_suffix_rows_from_cache(ops, ref, 64, 8, 128, prompts, keep))
+            ys.append(_suffix_rows_from_cache(ops, ref, 64, 8, 128, prompts, keep, q_block=qb))
         finally:
             ops.k.fls_attention_set_split(old)
     assert rel_err(ys[1], ys[0]) < 2e-3
+    # one wave per head, 8 heads per block: the same per-row math as the 2-wave kernel, unsplit
+    assert torch.equal(ys[2], ys[0])
+    assert rel_err(ys[3], ys[0]) < 2e-3
 
 
-def _suffix_rows_from_cache(ops, ref, nh, nkv, hd, prompts=None, keep=None):
+def _suffix_rows_from_cache(ops, ref, nh, nkv, hd, prompts=None, keep=None, q_block=64):
     from flexible_llm_sharding_amd.runtime.batch import pack_prompts
     from flexible_llm_sharding_amd.utils.tokenizer import TokenizedPrompt
     prompts = prompts or [(70, [5, 80, 1]), (130, [65, 17]), (9, [3, 140])]
@@ -511,8 +516,11 @@ def _suffix_rows_from_cache(ops, ref, nh, nkv, hd, prompts=None, keep=None):
     sel = torch.tensor(sel)
     qkv_new = qkv[sel].contiguous()
     m = reuse.device_tensors(DEV)
+    if q_block == 32:
+        assert reuse.r2_q_block == (32 if int(reuse.work[:, 1].max()) <= 32 else 64)
+        q_block = reuse.r2_q_block
     y = ops.attention(qkv_new.to(DEV), m["work"], nh, nkv, hd, kv0=cache.to(DEV), seg_lo=m["seg_lo"],
-                      work2=m["work2"], r2win=m["r2win"])
+                      work2=m["work2"], r2win=m["r2win"], q_block=q_block)
     want = ref.attention(qkv.float(), full.segments, nh, nkv, hd)[sel]
     got_ref = ref.attention(qkv_new.float(), reuse.segments, nh, nkv, hd, kv0=cache.float())
     torch.cuda.synchronize()
@@ -565,6 +573,90 @@ def test_gemm_small_m_splitk(ops, ref, M, epi):
     assert torch.equal(got, again)
     assert rel_err(got.cpu(), want) < 3e-3
     assert rel_err(got.cpu(), plain.cpu()) < 2e-3
+
+
+@pytest.mark.parametrize("blocks", [0, 1])
+@pytest.mark.parametrize("M", [1, 7, 17, 33, 100, 160, 256])
+@pytest.mark.parametrize("epi", ["none_bias", "resid", "swiglu", "rope128", "rope64"])
+def test_gemm_skinny_m(ops, ref, M, epi, blocks):
+    """Skinny-M kernel (gemm_skinny.h: every row of M in one block, weights and activations by
+    LDS-DMA) == the fp32 reference and == the other small-M paths to rounding, bitwise
+    reproducible.  blocks 0: the default K split (fp32 partials + reduce, this N splits in 2);
+    blocks 1: no split, the NONE / RESID / SWIGLU epilogues applied in the kernel.  M < 17 only
+    runs here with the path forced (mode 2)."""
+    from flexible_llm_sharding_amd.config import ModelConfig
+    from flexible_llm_sharding_amd.models.llama import rope_tables
+    K, N = 2048, 1024
+    x = rnd(M, K, seed=61)
+    if epi == "swiglu":
+        w = rnd(2 * N, K, scale=0.05, seed=62)
+        run = lambda: ops.swiglu_up(x, w)                                         # noqa: E731
+        want = ref.swiglu_up(x.float().cpu(), w.float().cpu())
+    elif epi.startswith("rope"):
+        hd = int(epi[4:])
+        nh, nkv = N // hd // 2, N // hd // 4
+        n = (nh + 2 * nkv) * hd
+        w = rnd(n, K, scale=0.05, seed=63)
+        b = rnd(n, scale=0.5, seed=64)
+        cfg = ModelConfig(hidden_size=nh * hd, num_attention_heads=nh, num_key_value_heads=nkv)
+        cos, sin = rope_tables(cfg, 4096)
+        pos = torch.randint(0, 4000, (M,), dtype=torch.int32, device=DEV)
+        run = lambda: ops.qkv_rope(x, w, pos, cos.to(DEV), sin.to(DEV), nh, nkv, hd, bias=b)   # noqa: E731
+        want = ref.qkv_rope(x.float().cpu(), w.float().cpu(), pos.cpu(), cos, sin, nh, nkv, hd, bias=b.float().cpu())
+    else:
+        w = rnd(N, K, scale=0.05, seed=65)
+        r0 = rnd(M, N, seed=66)
+        b = rnd(N, scale=0.5, seed=67)
+        if epi == "resid":
+            run = lambda: ops.linear_residual(x, w, r0.clone(), bias=b)           # noqa: E731
+            want = r0.float().cpu() + x.float().cpu() @ w.float().cpu().t() + b.float().cpu()
+        else:
+            run = lambda: ops.gemm(x, w, EPI_NONE, bias=b)                         # noqa: E731
+            want = x.float().cpu() @ w.float().cpu().t() + b.float().cpu()
+    old = ops.k.fls_gemm_set_skinny(0, 0)
+    try:
+        plain = run()                                   # the mid / split-K / generic paths
+        ops.k.fls_gemm_set_skinny(2, blocks or 256)
+        got, again = run(), run()
+    finally:
+        ops.k.fls_gemm_set_skinny(old, 256)
+    torch.cuda.synchronize()
+    assert torch.equal(got, again)
+    assert rel_err(got.cpu(), want) < 3e-3
+    assert rel_err(got.cpu(), plain.cpu()) < 2e-3
+
+
+def test_gemm_skinny_70b_generation_shapes(ops):
+    """The 70B projections at a generation step's 160 rows (QKV + RoPE, O + residual, gate/up +
+    SwiGLU, down + residual) on the skinny kernel == the same GEMMs with it off, to rounding."""
+    from flexible_llm_sharding_amd.config import preset
+    from flexible_llm_sharding_amd.models.llama import rope_tables
+    cfg = preset("llama2-70b")
+    M, H, I = 160, cfg.hidden_size, cfg.intermediate_size
+    nh, nkv, hd = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
+    cos, sin = rope_tables(cfg, 4096)
+    cos, sin = cos.to(DEV), sin.to(DEV)
+    pos = torch.randint(0, 4000, (M,), dtype=torch.int32, device=DEV)
+    x = rnd(M, H, seed=71)
+    xi = rnd(M, I, seed=72)
+    wqkv = rnd((nh + 2 * nkv) * hd, H, scale=0.02, seed=73)
+    wo = rnd(H, H, scale=0.02, seed=74)
+    wgu = rnd(2 * I, H, scale=0.02, seed=75)
+    wd = rnd(H, I, scale=0.02, seed=76)
+    r0 = rnd(M, H, seed=77)
+    runs = [lambda: ops.qkv_rope(x, wqkv, pos, cos, sin, nh, nkv, hd),
+            lambda: ops.linear_residual(x, wo, r0.clone()),
+            lambda: ops.swiglu_up(x, wgu),
+            lambda: ops.linear_residual(xi, wd, r0.clone())]
+    for run in runs:
+        got = run()
+        old = ops.k.fls_gemm_set_skinny(0, 0)
+        try:
+            plain = run()
+        finally:
+            ops.k.fls_gemm_set_skinny(old, 0)
+        torch.cuda.synchronize()
+        assert rel_err(got, plain) < 2e-3
 
 
 @pytest.mark.parametrize("epi", ["resid", "rope", "swiglu"])
