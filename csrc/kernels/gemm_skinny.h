@@ -14,30 +14,19 @@
 //     reduce, which applies the epilogue); with S = 1 the NONE / RESID / SWIGLU epilogues run in
 //     the kernel (SWIGLU: each wave's two subtiles are matching gate and up rows).
 namespace sk {
-template <int N>
-struct IC {
-  static constexpr int value = N;
-};
-template <int I, int N, class F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (I < N) {
-    f(IC<I>{});
-    static_for<I + 1, N>(f);
-  }
-}
-#ifndef SK_NR
-#define SK_NR 4
-#endif
 constexpr int BNW = 128;        // weight rows per block
 constexpr int KT = 64;          // K per tile
-constexpr int NX = 4;           // activation stages in LDS (2 K-tiles ahead)
-constexpr int NR = SK_NR;       // weight register ring (NR - 1 K-tiles ahead)
-constexpr int QW = 4;           // weight loads per lane per K-tile
+constexpr int WST = BNW * KT * 2;
+constexpr int LDS_MAX = 160 * 1024;
 template <int RS>
 struct Geo {
   static constexpr int XST = RS * 16 * KT * 2;             // activation bytes per stage
-  static constexpr int QX = RS / 2;                        // 8-row DMA groups per wave
-  static constexpr int LDS = NX * XST;
+  static constexpr int STG = XST + WST;
+  static constexpr int NX = 4 * STG <= LDS_MAX ? 4 : 3;    // stages
+  static constexpr int DIST = NX - 2;                      // K-tiles in flight ahead
+  static constexpr int QX = RS / 2;                        // 8-row DMA groups per wave: activations
+  static constexpr int QW = BNW / 32;                      // ... and weights
+  static constexpr int LDS = NX * STG;
 };
 }  // namespace sk
 
@@ -51,52 +40,33 @@ __global__ __launch_bounds__(256) void gemm_nt_skinny(const half_t* __restrict__
   extern __shared__ __attribute__((aligned(16))) char lds_sk[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, grp = lane >> 4;
-  const int nk = K / KT;                      // K-tiles of this block's slice (a multiple of NR)
+  const int nk = K / KT;                      // K-tiles of this block's slice
   const size_t kofs = (size_t)blockIdx.y * K; // the slice's first K element
+  const bool swiglu = EPI == FLS_EPI_SWIGLU;
+  // block-local weight row l (wave l / 32, subtile (l / 16) & 1) -> physical row; SWIGLU: subtile 0
+  // = gate rows, subtile 1 = the matching up rows
+  auto phys_row = [&](int l) -> int {
+    if (swiglu) return ((l >> 4) & 1) * ep.gu_rows + (int)blockIdx.x * (BNW / 2) + (l >> 5) * 16 + (l & 15);
+    return (int)blockIdx.x * BNW + l;
+  };
+  const int cbase = swiglu ? (int)blockIdx.x * (BNW / 2) + wave * 16 : (int)blockIdx.x * BNW + wave * 32;
 
-  // weight rows of this lane's two subtiles; output column base of the wave
-  int wrow0, wrow1, cbase;
-  if constexpr (EPI == FLS_EPI_SWIGLU) {
-    cbase = (int)blockIdx.x * (BNW / 2) + wave * 16;
-    wrow0 = cbase + fr;                       // gate
-    wrow1 = ep.gu_rows + cbase + fr;          // up (same intermediate column)
-  } else {
-    cbase = (int)blockIdx.x * BNW + wave * 32;
-    wrow0 = cbase + fr;
-    wrow1 = cbase + 16 + fr;
-  }
-  // lane group g holds k = 16 g + 8 s .. + 7 for K-step s (both operands): one 32-byte run per
-  // subtile and K-tile
-  const half_t* wp0 = W + (size_t)wrow0 * ldw + kofs + grp * 16;
-  const half_t* wp1 = W + (size_t)wrow1 * ldw + kofs + grp * 16;
-
-  // activation LDS-DMA sources: group g = wave + 4 i covers rows 8 g .. 8 g + 7
+  // LDS-DMA sources: group g = wave + 4 i covers rows 8 g .. 8 g + 7 of its image
   const int sub = lane >> 3;
   const int kc = ((lane & 7) ^ sub) * 8;      // source chunk pre-swizzled (the read XORs it back)
   const half_t* xsrc[G::QX];
+  const half_t* wsrc[G::QW];
 #pragma unroll
   for (int i = 0; i < G::QX; ++i)
     xsrc[i] = A + kofs + (size_t)min((wave + 4 * i) * 8 + sub, M - 1) * lda + kc;
-  auto stage_x = [&](int t) {
-    char* base = lds_sk + (t % NX) * G::XST;
+#pragma unroll
+  for (int i = 0; i < G::QW; ++i) wsrc[i] = W + kofs + (size_t)phys_row((wave + 4 * i) * 8 + sub) * ldw + kc;
+  auto stage = [&](int t) {
+    char* base = lds_sk + (t % G::NX) * G::STG;
 #pragma unroll
     for (int i = 0; i < G::QX; ++i) glds16(xsrc[i] + (size_t)t * KT, base + (wave + 4 * i) * 1024);
-  };
-  // weights HBM -> VGPR directly (each weight element feeds exactly one wave), streamed past the
-  // caches (nt), NR - 1 K-tiles in flight.  The loads are asm: a compiled load's result crossing
-  // the loop's back edge makes the compiler drain vmcnt at the loop head every NR tiles.  Nothing
-  // reads the ring registers but the asm MFMAs, after the counted vmcnt below covers their tile.
-  half8 wf[NR][2][2];
-  auto ld16 = [](half8& d, const half_t* p) {
-    asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(d) : "v"(p) : "memory");
-  };
-  auto load_w = [&](auto slot_c, int t) {
-    constexpr int S_ = decltype(slot_c)::value;
-    const size_t o = (size_t)t * KT;
-    ld16(wf[S_][0][0], wp0 + o);
-    ld16(wf[S_][0][1], wp0 + o + 8);
-    ld16(wf[S_][1][0], wp1 + o);
-    ld16(wf[S_][1][1], wp1 + o + 8);
+#pragma unroll
+    for (int i = 0; i < G::QW; ++i) glds16(wsrc[i] + (size_t)t * KT, base + G::XST + (wave + 4 * i) * 1024);
   };
 
   // accumulators pinned in AGPRs and updated in place by asm MFMAs (common.h): compiled MFMAs let
@@ -112,49 +82,48 @@ __global__ __launch_bounds__(256) void gemm_nt_skinny(const half_t* __restrict__
   SK_FENCE_ACC();
   asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");  // zero-init VALU writes before the first MFMA
 
-  // prologue: activations of tiles 0, 1; weights of tiles 0 .. NR - 2
-  stage_x(0);
-  stage_x(1);
-  asm volatile("" ::: "memory");
-  static_for<0, NR - 1>([&](auto c) { load_w(c, decltype(c)::value); });
-
-  // Loads are never conditional (past the last tile they re-read it into a stage / slot nobody
-  // reads again), so the vmcnt count is one constant.
-  auto step = [&](auto u_c, int t) {
-    constexpr int U = decltype(u_c)::value;   // ring slot of tile t (t % NR)
-    stage_x(min(t + 2, nk - 1));              // into stage (t + 2) % 4, last read by tile t - 2
-    asm volatile("" ::: "memory");            // keep the issue order the vmcnt count below assumes
-    load_w(IC<(U + NR - 1) % NR>{}, min(t + NR - 1, nk - 1));
-    // activations of tile t landed (and the weights of tile t, issued before them): the ops issued
-    // after its LDS-DMA are W(t+NR-3) | X(t+1) W(t+NR-2) | X(t+2) W(t+NR-1)
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * QW + 2 * G::QX) : "memory");
+  // DMA is never conditional: past the last tile it re-reads it into a stage nobody reads again,
+  // so the vmcnt count is one constant
+#pragma unroll
+  for (int d = 0; d < G::DIST; ++d) stage(min(d, nk - 1));
+  for (int t = 0; t < nk; ++t) {
+    stage(min(t + G::DIST, nk - 1));          // into stage (t + DIST) % NX, last read by tile t - 2
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::DIST * (G::QX + G::QW)) : "memory");
     __builtin_amdgcn_s_barrier();             // every wave's part of tile t is in LDS
-    const char* Xs = lds_sk + (t % NX) * G::XST;
+    const char* Xs = lds_sk + (t % G::NX) * G::STG;
+    const char* Ws = Xs + G::XST;
     // the asm MFMAs are ordered against memory (no read placed after one is hoisted over it), so
     // the schedule is spelled out: K-step 0's fragments, then its MFMAs each followed by one read
     // of K-step 1, whose MFMAs close the tile
-    half8 xf[2][RS];
+    half8 wf[2][2], xf[2][RS];
+    auto rd_w = [&](int s, int j) {
+      const int r = wave * 32 + j * 16 + fr, c = s * 4 + grp;
+      wf[s][j] = *(const half8*)(Ws + r * 128 + ((c ^ (r & 7)) << 4));
+    };
     auto rd_x = [&](int s, int i) {
-      const int r = i * 16 + fr, c = grp * 2 + s;
+      const int r = i * 16 + fr, c = s * 4 + grp;
       xf[s][i] = *(const half8*)(Xs + r * 128 + ((c ^ (r & 7)) << 4));
     };
+    rd_w(0, 0);
+    rd_w(0, 1);
 #pragma unroll
     for (int i = 0; i < RS; ++i) rd_x(0, i);
+    rd_w(1, 0);
+    rd_w(1, 1);
 #pragma unroll
     for (int i = 0; i < RS; ++i) {
-      mfma_acc_inplace_ordered(acc[i][0], wf[U][0][0], xf[0][i]);
-      mfma_acc_inplace_ordered(acc[i][1], wf[U][1][0], xf[0][i]);
+      mfma_acc_inplace_ordered(acc[i][0], wf[0][0], xf[0][i]);
+      mfma_acc_inplace_ordered(acc[i][1], wf[0][1], xf[0][i]);
       rd_x(1, i);
     }
 #pragma unroll
     for (int i = 0; i < RS; ++i) {
-      mfma_acc_inplace_ordered(acc[i][0], wf[U][0][1], xf[1][i]);
-      mfma_acc_inplace_ordered(acc[i][1], wf[U][1][1], xf[1][i]);
+      mfma_acc_inplace_ordered(acc[i][0], wf[1][0], xf[1][i]);
+      mfma_acc_inplace_ordered(acc[i][1], wf[1][1], xf[1][i]);
     }
-  };
-  for (int t0 = 0; t0 < nk; t0 += NR) static_for<0, NR>([&](auto c) { step(c, t0 + decltype(c)::value); });
-  // the tail's redundant loads must land before the block's LDS / registers are released; the
-  // accumulators were written by MFMAs the hazard recognizer cannot see
+  }
+  // the tail's redundant DMA must land before this block's LDS can be handed to another block;
+  // the accumulators were written by MFMAs the hazard recognizer cannot see
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   SK_FENCE_ACC();
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
@@ -241,8 +210,7 @@ int try_skinny(const half_t* A, const half_t* W, half_t* C, int M, int N, int K,
   if (g_skinny == 1 && M < 17) return 0;      // a GEMV-like M: the mid / split-K paths (A/B: profiles/r4_gen)
   const int nblk = N / sk::BNW, nkt = K / sk::KT;
   int S = 1;
-  if (nkt % sk::NR) return 0;                 // K-tiles per slice: a multiple of the ring (the unroll)
-  while (nblk * S < g_skinny_blocks && S < 16 && nkt % (2 * S * sk::NR) == 0 && nkt / (2 * S) >= 16) S *= 2;
+  while (nblk * S < g_skinny_blocks && S < 16 && nkt % (2 * S) == 0 && nkt / (2 * S) >= 8) S *= 2;
   const bool direct_epi = EPI == FLS_EPI_NONE || EPI == FLS_EPI_RESID || EPI == FLS_EPI_SWIGLU;
   const bool direct = S == 1 && direct_epi;
   const int rs = ((M + 31) / 32) * 2;

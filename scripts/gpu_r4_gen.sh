@@ -6,7 +6,7 @@ set -o pipefail
 O=gpurun_out/${1:-r4_gen}
 mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py -x -v -k "skinny or suffix_rows or decode_split or small_m" --timeout 150 --timeout-method thread > $O/tests.log 2>&1 || exit 1
-timeout -k 10 400 python -u scripts/gemm_skinny_ab.py --ms 64,160,256 --variants nr8 > $O/skinny_ab.log 2>&1 || exit 1
+timeout -k 10 400 python -u scripts/gemm_skinny_ab.py --ms 64,160,256 > $O/skinny_ab.log 2>&1 || exit 1
 python -c "import pickle,sys; sys.path.insert(0,'.'); from flexible_llm_sharding_amd.utils.synthetic import synthetic_prompts; pickle.dump(synthetic_prompts(32,1024,5,64,32000,seed=0), open('/tmp/p.pkl','wb'))" || exit 1
 FLS_SKINNY=0 FLS_R2_QBLOCK=64 timeout -k 10 400 python main.py --synthetic llama2-70b --prompt_pickle /tmp/p.pkl --output_file /tmp/s_before.pkl --num_gen_token 6 --suffix_kv_cache --metrics_json $O/metrics_before.json > $O/gen_before.log 2>&1 || exit 1
 timeout -k 10 400 python main.py --synthetic llama2-70b --prompt_pickle /tmp/p.pkl --output_file /tmp/s_after.pkl --num_gen_token 6 --suffix_kv_cache --metrics_json $O/metrics_after.json > $O/gen_after.log 2>&1 || exit 1

@@ -46,14 +46,48 @@ peak = {"v": 0.0, "used": 0.0}
 stop = threading.Event()
 
 
+timeline = []          # (time, outside MB) for the last call
+events = []            # (time, host call name, '>' enter / '<' exit) for the last call
+
+
+def _wrap(obj, name):
+    f = getattr(obj, name, None)
+    if f is None or not callable(f):
+        return
+    tag = f"{type(obj).__name__}.{name}"
+
+    def w(*a, **k):
+        events.append((time.perf_counter(), tag, ">"))
+        try:
+            return f(*a, **k)
+        finally:
+            events.append((time.perf_counter(), tag, "<"))
+    setattr(obj, name, w)
+
+
+for _n in dir(r.ops):
+    if not _n.startswith("_") or _n in ("_splitk_ws",):
+        _wrap(r.ops, _n)
+for _n in ("_copy_piece", "_try_issue", "_wait", "acquire", "release", "_release_gid", "discard_loaded"):
+    _wrap(r.prefetcher, _n)
+for _n in [n for n in dir(r) if n.startswith("_") and not n.startswith("__")]:
+    if callable(getattr(r, _n, None)) and _n not in ("_workspace",):
+        try:
+            _wrap(r, _n)
+        except (AttributeError, TypeError):
+            pass
+
+
 def sample():
     torch.cuda.set_device(dev)
     while not stop.is_set():
         free, total = torch.cuda.mem_get_info(dev)
         used = total - free
         peak["used"] = max(peak["used"], used / 1e9)
-        peak["v"] = max(peak["v"], (used - torch.cuda.memory_reserved(dev) - slots()) / 1e6)
-        stop.wait(0.005)
+        o = (used - torch.cuda.memory_reserved(dev) - slots()) / 1e6
+        peak["v"] = max(peak["v"], o)
+        timeline.append((time.perf_counter(), o))
+        stop.wait(0.002)
 
 
 t = threading.Thread(target=sample, daemon=True)
@@ -63,8 +97,10 @@ def stats():
     return {k: st.get(k, 0) for k in ("num_alloc_retries", "num_device_alloc", "num_device_free", "num_ooms")}
 
 
-for i in range(3):
+for i in range(int(os.environ.get("PROBE_CALLS", "3"))):
     t0 = time.perf_counter()
+    timeline.clear()
+    events.clear()
     s0 = stats()
     r(prompts)
     torch.cuda.synchronize()
@@ -75,3 +111,24 @@ for i in range(3):
           f"{torch.cuda.max_memory_reserved(dev) / 1e9:.3f} GB", flush=True)
 stop.set()
 t.join()
+# where in the last call the outside-allocator memory rose above its steady value: intervals of
+# samples > steady + 50 MB, relative to the call start
+steady = sorted(o for _, o in timeline)[len(timeline) // 2]
+segs, cur = [], None
+for t, o in timeline:
+    if o > steady + 50:
+        cur = [t, t, o] if cur is None else [cur[0], t, max(cur[2], o)]
+    elif cur is not None:
+        segs.append(cur)
+        cur = None
+if cur is not None:
+    segs.append(cur)
+print(f"[probe] last call: {len(timeline)} samples, steady outside {steady:.0f} MB, "
+      f"{len(segs)} excursions > +50 MB:", flush=True)
+for a_, b_, m_ in segs[:40]:
+    print(f"[probe]   {a_ - t0:7.3f}-{b_ - t0:7.3f} s  max {m_:.0f} MB", flush=True)
+for a_, b_, m_ in segs[:8]:
+    near = [(t - t0, n, d) for t, n, d in events if a_ - 0.006 <= t <= b_ + 0.003]
+    print(f"[probe] host calls around the excursion at {a_ - t0:.3f} s:", flush=True)
+    for t, n, d in near[-60:]:
+        print(f"[probe]     {t:8.4f} {d} {n}", flush=True)
