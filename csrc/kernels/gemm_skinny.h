@@ -207,10 +207,19 @@ int try_skinny(const half_t* A, const half_t* W, half_t* C, int M, int N, int K,
   if (!g_skinny || M > 256 || N % sk::BNW || K % sk::KT || lda % 8 || ldw % 8 || ((uintptr_t)A & 15) ||
       ((uintptr_t)W & 15))
     return 0;
-  if (g_skinny == 1 && M < 17) return 0;      // a GEMV-like M: the mid / split-K paths (A/B: profiles/r4_gen)
   const int nblk = N / sk::BNW, nkt = K / sk::KT;
+  // auto: the measured range (profiles/r4_gen/skinny_ab.log, 70B shapes): M 17..192, except the
+  // wide gate/up GEMM (N / 128 >= 256 blocks) below 97 rows, where the split-K / main paths win
+  if (g_skinny == 1 && (M < 17 || M > 192 || (nblk >= 256 && M < 97))) return 0;
+  // K slices: the fewest that give whole 256-CU rounds or at least two rounds (one block per CU:
+  // a fractional single round leaves a tail of full-K blocks; 70B at M = 160: O / down S = 4,
+  // QKV S = 8, gate/up S = 2 measured fastest); g_skinny_blocks != 256 (A/B) sets a block target
   int S = 1;
-  while (nblk * S < g_skinny_blocks && S < 16 && nkt % (2 * S) == 0 && nkt / (2 * S) >= 8) S *= 2;
+  auto good = [&](int s) {
+    const long b = (long)nblk * s;
+    return g_skinny_blocks != 256 ? b >= g_skinny_blocks : (b % 256 == 0 || b >= 512);
+  };
+  while (!good(S) && S < 16 && nkt % (2 * S) == 0 && nkt / (2 * S) >= 8) S *= 2;
   const bool direct_epi = EPI == FLS_EPI_NONE || EPI == FLS_EPI_RESID || EPI == FLS_EPI_SWIGLU;
   const bool direct = S == 1 && direct_epi;
   const int rs = ((M + 31) / 32) * 2;

@@ -21,14 +21,15 @@
 //   C: x rows 8..11 x w 0..7 (column-major) -- refills w[0..7]
 // LDS regions per stage: X0 / X1 / X2 = stage rows {0..63, 192..255} / {64..127, 256..319} /
 // {128..191, 320..383} (16 KiB each; the two wave rows of a region), W (32 KiB).  Phases pair into
-// super-phases SP0 = (A s0, B s0), SP1 = (C s0, A s1), SP2 = (B s1, C s1), each ending in lgkmcnt(0) +
-// counted vmcnt + raw s_barrier.  Region r of a stage is refilled (tile t -> t+2) in the SP after
-// the barrier that follows its last read, and every DMA is waited for two SPs after issue:
-//   SP0 of tile t: DMA X2(t+1)         (4 pieces / wave)  end: vmcnt(12)
-//   SP1 of tile t: DMA X0, X1(t+2)     (8 pieces / wave)  end: vmcnt(12)
-//   SP2 of tile t: DMA W(t+2)          (8 pieces / wave)  end: vmcnt(16)
-// (the full read/write interval table is in profiles/r4_gemm/README.md).  Requires an even number
-// of K-tiles (the loop body is unrolled over both stages) and M >= 384: the last M tile is shifted
+// super-phases SP0 = (A s0, B s0), SP1 = (C s0, A s1), SP2 = (B s1, C s1), each ending in a relaxed
+// lgkmcnt (LDS reads retire in order) + counted vmcnt + raw s_barrier.  Region r of a stage is refilled (tile t -> t+2) in an SP after
+// the barrier that follows its last read.  LDS-DMA plan per wave (V11_SCHED 2, the default):
+//   SP0 of tile t: X2(t+1), W half 2 (t+1)          (4 + 4 pieces)   end: lgkmcnt(6) vmcnt(16)
+//   SP1 of tile t: X0(t+2)                          (4 pieces)       end: lgkmcnt(6) vmcnt(4)
+//   SP2 of tile t: X1(t+2), W half 1 (t+2)          (4 + 4 pieces)   end: lgkmcnt(8) vmcnt(12)
+// (W half h = each wave's DMA groups 4h-4 .. 4h-1 of its 8.)
+// V11_SCHED 1 (A/B build): 4 / 4 / 12 pieces, all of W(t+2) in SP2 (profiles/r4_gemm).  Requires an
+// even number of K-tiles (the loop body is unrolled over both stages) and M >= 384: the last M tile is shifted
 // back to end at row M and stores only the rows its neighbour does not (epilogue_quadrant's LO), so
 // every LDS-DMA source row is in bounds and the per-piece row offsets live in the scalar soffset.
 #include "gemm_v10.h"

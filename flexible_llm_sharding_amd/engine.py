@@ -147,11 +147,12 @@ class ShardedRunner:
         if max_vram_gb:
             # size the micro-batch and the QKV / MLP chunks to the HBM cap (runtime/memplan.py);
             # re-planned per call once its token count is known (_plan_call)
-            from .runtime.memplan import device_used_bytes, plan_for_vram
+            from .runtime.memplan import RUNTIME_RESERVE, device_used_bytes, plan_for_vram
             if self.dev.type == "cuda":
                 # device memory held outside the caching allocator before any weight slot exists:
                 # context, code objects, RCCL buffers (warmed up above) — planned as measured
-                self._outside = device_used_bytes(self.dev) - torch.cuda.memory_reserved(self.dev) + (64 << 20)
+                self._outside = (device_used_bytes(self.dev) - torch.cuda.memory_reserved(self.dev) + (64 << 20)
+                                 + RUNTIME_RESERVE)
             try:
                 # provisional (the call's token count is unknown yet); _plan_call is authoritative
                 token_budget, mlp_chunk, attn_rows, qkv_chunk, est = plan_for_vram(
@@ -195,15 +196,24 @@ class ShardedRunner:
             prefetcher = PiecePoolPrefetcher(source, self.names, my, self.dev)
         self.prefetcher = prefetcher or ShardPrefetcher(source, self.names, my, self.dev,
                                                         n_slots=n_slots, resident=resident, keep=keep)
+        self.h2d_stream = torch.cuda.Stream(self.dev) if self.cuda else None
+        self.d2h_stream = torch.cuda.Stream(self.dev) if self.cuda else None
+        if self.cuda:
+            # the HIP runtime sets up its copy path at the first host<->device copy, holding ~0.2-0.35
+            # GB of device memory for a moment (profiles/r4_vram): do it now, while nothing else is
+            # allocated, on every stream this runner copies on
+            from .runtime.memplan import warm_copy_paths
+            warm_copy_paths(self.dev, [getattr(self.prefetcher, "copy_stream", None), self.h2d_stream,
+                                       self.d2h_stream])
         if self.vram_plan is not None and self.cuda:
             # the weight slots are raw hipMalloc blocks: the allocator gets the rest of the cap
-            from .runtime.memplan import cap_allocator
+            from .runtime.memplan import RUNTIME_RESERVE, cap_allocator, device_used_bytes
+            self._outside = (device_used_bytes(self.dev) - torch.cuda.memory_reserved(self.dev) + (64 << 20)
+                             + RUNTIME_RESERVE)
             slots = self.prefetcher.planned_hbm_bytes()
             self.vram_plan["allocator_limit_bytes"] = cap_allocator(self.dev, int(max_vram_gb * 1e9), slots)
         self.stats: Dict[str, float] = {}
         self._fault = _parse_fault(self.comm.rank)
-        self.h2d_stream = torch.cuda.Stream(self.dev) if self.cuda else None
-        self.d2h_stream = torch.cuda.Stream(self.dev) if self.cuda else None
         self._store: Optional[ActivationStore] = None
         self._inbox: Optional[StageInbox] = None
         self._mp_start_layer = 0

@@ -37,6 +37,11 @@ SLACK = 1.10
 SLACK_ONE = 1.02
 # the plan aims this far below the cap (the estimate is a model; hipMemGetInfo is the judge)
 CAP_MARGIN = 0.015
+# device memory the HIP runtime takes outside any allocator for a moment while a pass runs: up to
+# ~185 MB above the steady context for <= 2 ms around some host -> device weight copies, sampled
+# every 2 ms on the 70B headline (profiles/r4_vram); kept free under a cap, by the allocator limit
+# and by the plan
+RUNTIME_RESERVE = int(os.environ.get("FLS_RUNTIME_RESERVE_MB", "192")) << 20
 
 
 def activation_bytes(cfg: ModelConfig, tokens: int, mlp_chunk: int, elem: int = 2, qkv_chunk: int = 0,
@@ -74,6 +79,24 @@ def device_used_bytes(device) -> int:
     return (total - free) - shared_device_bytes()
 
 
+def warm_copy_paths(device, streams, nbytes: int = 8 << 20) -> None:
+    """One host -> device and one device -> host copy on each stream (and the current one).  The
+    first copy of a process makes the HIP runtime set up its copy path, which holds ~0.2-0.35 GB
+    of device memory outside any allocator for a moment (scripts/copy_probe.py: +340 MB and a
+    150 ms enqueue on the first 1.4 GB copy, nothing on later ones); under ``--max_vram_gb`` that
+    belongs before the plan measures the context, not inside the first pass."""
+    import torch
+    from . import hostmem
+    host = hostmem.alloc_host(nbytes, pinned=True)
+    dev = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    for st in [s for s in streams if s is not None] + [torch.cuda.current_stream(device)]:
+        with torch.cuda.stream(st):
+            dev.copy_(host, non_blocking=True)
+            host.copy_(dev, non_blocking=True)
+        st.synchronize()
+    del dev, host
+
+
 def cap_allocator(device, max_vram_bytes: int, other_device_bytes: int) -> int:
     """Bound the caching allocator so that, with ``other_device_bytes`` held outside it (the
     raw weight slots), the device's memory in use stays <= ``max_vram_bytes``; when a request
@@ -82,7 +105,7 @@ def cap_allocator(device, max_vram_bytes: int, other_device_bytes: int) -> int:
     import torch
     total = torch.cuda.mem_get_info(device)[1]
     outside = device_used_bytes(device) - torch.cuda.memory_reserved(device)   # context, code objects, raw blocks
-    limit = max_vram_bytes - outside - other_device_bytes - (64 << 20)
+    limit = max_vram_bytes - outside - other_device_bytes - (64 << 20) - RUNTIME_RESERVE
     if limit <= 0:
         raise ValueError(f"--max_vram_gb {max_vram_bytes / 1e9:.2f}: context + weight slots alone need "
                          f"{(outside + other_device_bytes) / 1e9:.2f} GB")
@@ -118,7 +141,8 @@ def plan_for_vram(cfg: ModelConfig, max_vram_bytes: int, lnps: int = 1, n_slots:
     over = DEVICE_OVERHEAD if overhead is None else overhead
     best = None
     budgets = sorted({token_budget, 49152, 32768, 24576, 16384, 12288, 8192, 6144, 4096, 3072, 2048, 1024})
-    chunks = sorted({mlp_chunk, 16384, 12288, 8192, 6144, 4096, 2048, 1024})
+    # multiples of 3072 rows give whole 256-CU rounds of the 384-row GEMM tile (models/llama.py)
+    chunks = sorted({mlp_chunk, 16384, 15360, 12288, 9216, 8192, 6144, 4096, 3072, 2048, 1024})
     for tb in (t for t in budgets if t <= token_budget):
         rows = min(tb, total_tokens) if total_tokens else tb
         n_mb = -(-total_tokens // tb) if total_tokens else 2
@@ -128,7 +152,7 @@ def plan_for_vram(cfg: ModelConfig, max_vram_bytes: int, lnps: int = 1, n_slots:
             for ar in sorted({0, 32768, 24576, 16384, 12288, 8192, 4096}):
                 if ar and (ar >= rows or ar < max_prompt_rows):
                     continue
-                for qc in ((0, 16384, 8192, 4096, 2048) if ar == 0 else (0,)):
+                for qc in ((0, 16384, 12288, 9216, 8192, 6144, 4096, 3072, 2048) if ar == 0 else (0,)):
                     if qc and qc >= rows:
                         continue
                     est = weights + over + activation_bytes(cfg, rows, mc, qkv_chunk=qc, states=states,

@@ -92,6 +92,27 @@ def sample():
 
 t = threading.Thread(target=sample, daemon=True)
 t.start()
+def excursions(t0, label):
+    """Intervals of the call where the outside-allocator memory rose > 50 MB above its median,
+    with the host calls made around each."""
+    steady = sorted(o for _, o in timeline)[len(timeline) // 2]
+    segs, cur = [], None
+    for t, o in timeline:
+        if o > steady + 50:
+            cur = [t, t, o] if cur is None else [cur[0], t, max(cur[2], o)]
+        elif cur is not None:
+            segs.append(cur)
+            cur = None
+    if cur is not None:
+        segs.append(cur)
+    print(f"[probe] {label}: {len(timeline)} samples, steady outside {steady:.0f} MB, "
+          f"{len(segs)} excursions > +50 MB", flush=True)
+    for a_, b_, m_ in segs[:8]:
+        print(f"[probe]   {a_ - t0:7.3f}-{b_ - t0:7.3f} s  max {m_:.0f} MB; host calls around it:", flush=True)
+        for t, n, d in [(t - t0, n, d) for t, n, d in events if a_ - 0.006 <= t <= b_ + 0.003][-60:]:
+            print(f"[probe]     {t:8.4f} {d} {n}", flush=True)
+
+
 def stats():
     st = torch.cuda.memory_stats(dev)
     return {k: st.get(k, 0) for k in ("num_alloc_retries", "num_device_alloc", "num_device_free", "num_ooms")}
@@ -109,26 +130,6 @@ for i in range(int(os.environ.get("PROBE_CALLS", "3"))):
     print(f"[probe] call {i}: {time.perf_counter() - t0:.2f}s outside-now {outside(slots()):.0f} MB, peak outside "
           f"{peak['v']:.0f} MB, peak used {peak['used']:.3f} GB, reserved peak "
           f"{torch.cuda.max_memory_reserved(dev) / 1e9:.3f} GB", flush=True)
+    excursions(t0, f"call {i}")
 stop.set()
 t.join()
-# where in the last call the outside-allocator memory rose above its steady value: intervals of
-# samples > steady + 50 MB, relative to the call start
-steady = sorted(o for _, o in timeline)[len(timeline) // 2]
-segs, cur = [], None
-for t, o in timeline:
-    if o > steady + 50:
-        cur = [t, t, o] if cur is None else [cur[0], t, max(cur[2], o)]
-    elif cur is not None:
-        segs.append(cur)
-        cur = None
-if cur is not None:
-    segs.append(cur)
-print(f"[probe] last call: {len(timeline)} samples, steady outside {steady:.0f} MB, "
-      f"{len(segs)} excursions > +50 MB:", flush=True)
-for a_, b_, m_ in segs[:40]:
-    print(f"[probe]   {a_ - t0:7.3f}-{b_ - t0:7.3f} s  max {m_:.0f} MB", flush=True)
-for a_, b_, m_ in segs[:8]:
-    near = [(t - t0, n, d) for t, n, d in events if a_ - 0.006 <= t <= b_ + 0.003]
-    print(f"[probe] host calls around the excursion at {a_ - t0:.3f} s:", flush=True)
-    for t, n, d in near[-60:]:
-        print(f"[probe]     {t:8.4f} {d} {n}", flush=True)
