@@ -208,9 +208,10 @@ int try_skinny(const half_t* A, const half_t* W, half_t* C, int M, int N, int K,
       ((uintptr_t)W & 15))
     return 0;
   const int nblk = N / sk::BNW, nkt = K / sk::KT;
-  // auto: the measured range (profiles/r4_gen/skinny_ab.log, 70B shapes): M 17..192, except the
-  // wide gate/up GEMM (N / 128 >= 256 blocks) below 97 rows, where the split-K / main paths win
-  if (g_skinny == 1 && (M < 17 || M > 192 || (nblk >= 256 && M < 97))) return 0;
+  // auto: the measured range (profiles/r4_gen, 70B shapes): M 17..192 on the narrow projections;
+  // the wide gate/up GEMM (N / 128 >= 256 blocks, 224 main-path tiles) runs faster on the main
+  // path at every M measured (64 / 160 / 256 rows: 175 / 209 / 221 us vs 195 / 246 / 332)
+  if (g_skinny == 1 && (M < 17 || M > 192 || nblk >= 256)) return 0;
   // K slices: the fewest that give whole 256-CU rounds or at least two rounds (one block per CU:
   // a fractional single round leaves a tail of full-K blocks; 70B at M = 160: O / down S = 4,
   // QKV S = 8, gate/up S = 2 measured fastest); g_skinny_blocks != 256 (A/B) sets a block target

@@ -45,6 +45,9 @@ class ModelConfig:
     num_experts_per_tok: int = 2
     moe_intermediate_size: Optional[int] = None
     norm_topk_prob: bool = True
+    # Qwen2-MoE: a dense SwiGLU "shared expert" of this width on every token, scaled by
+    # sigmoid(h . shared_expert_gate) and added to the routed experts' sum (0: none)
+    shared_expert_intermediate_size: int = 0
     bos_token_id: int = 1
     eos_token_id: int = 2
     torch_dtype: str = "float16"
@@ -107,6 +110,7 @@ class ModelConfig:
         n = h * self.qkv_size + self.q_size * h + 2 * h
         if self.is_moe:
             n += self.num_local_experts * h + experts * 3 * h * self.expert_intermediate
+            n += 3 * h * self.shared_expert_intermediate_size + (h if self.shared_expert_intermediate_size else 0)
         else:
             n += 3 * h * self.intermediate_size
         return (n + (self.qkv_size if self.attention_bias else 0) + (h if self.o_proj_bias else 0)
@@ -181,8 +185,8 @@ class ModelConfig:
             raise NotImplementedError(f"model_type={mt!r}: supported are {sorted(SUPPORTED_MODEL_TYPES)}")
         if mt in ("qwen3_moe", "qwen2_moe"):
             kw["num_local_experts"] = int(d.get("num_experts") or d.get("num_local_experts") or 0)
-            if d.get("shared_expert_intermediate_size"):
-                raise NotImplementedError("MoE shared experts (Qwen2-MoE) are not supported")
+            if mt == "qwen3_moe" and d.get("shared_expert_intermediate_size"):
+                raise NotImplementedError("shared experts in a Qwen3-MoE config")
             if d.get("mlp_only_layers") or int(d.get("decoder_sparse_step", 1) or 1) != 1:
                 raise NotImplementedError("dense layers between the MoE layers (mlp_only_layers / "
                                           "decoder_sparse_step) are not supported")
@@ -198,8 +202,9 @@ class ModelConfig:
             kw["explicit_head_dim"] = int(hdim)
         if d.get("hidden_act", "silu") != "silu":
             raise NotImplementedError(f"hidden_act={d.get('hidden_act')!r} (SwiGLU/silu only)")
-        if mt == "qwen2":
-            # HF Qwen2Attention: q/k/v Linear with bias, o_proj without
+        if mt == "qwen2" or (mt == "qwen2_moe" and d.get("qkv_bias", d.get("attention_bias", True))):
+            # HF Qwen2Attention / Qwen2MoeAttention (qkv_bias, default True): q/k/v Linear with
+            # bias, o_proj without
             kw["attention_bias"], kw["o_proj_bias"] = True, False
         elif d.get("attention_bias"):
             kw["attention_bias"], kw["o_proj_bias"] = True, True
@@ -240,7 +245,7 @@ class ModelConfig:
 # Llama-structured causal LMs (model.embed_tokens / model.layers.N / model.norm / lm_head with
 # q/k/v/o + gate/up/down + two RMSNorms per layer) -- what the reference's AutoModelForCausalLM
 # path (utils.py:101-115) runs in practice.
-SUPPORTED_MODEL_TYPES = {"llama", "mistral", "qwen2", "qwen3", "phi3", "mixtral", "qwen3_moe"}
+SUPPORTED_MODEL_TYPES = {"llama", "mistral", "qwen2", "qwen3", "phi3", "mixtral", "qwen3_moe", "qwen2_moe"}
 # MoE limits of the routing kernels (csrc/kernels/moe.hip): experts per layer, experts per token
 MAX_EXPERTS = 256
 MAX_TOP_K = 8
@@ -326,6 +331,18 @@ PRESETS = {
                            explicit_head_dim=128, num_local_experts=8, num_experts_per_tok=3,
                            moe_intermediate_size=128, norm_topk_prob=False, model_type="qwen3_moe",
                            architectures=["Qwen3MoeForCausalLM"]),
+    # Qwen1.5-MoE-A2.7B: 60 routed experts (top 4, not renormalised) + a gated shared expert
+    "qwen1.5-moe-a2.7b": dict(hidden_size=2048, intermediate_size=5632, num_attention_heads=16,
+                              num_key_value_heads=16, num_hidden_layers=24, vocab_size=151936, rope_theta=1e6,
+                              rms_norm_eps=1e-6, attention_bias=True, num_local_experts=60, num_experts_per_tok=4,
+                              moe_intermediate_size=1408, shared_expert_intermediate_size=5632,
+                              norm_topk_prob=False, bos_token_id=151643, eos_token_id=151643,
+                              model_type="qwen2_moe", architectures=["Qwen2MoeForCausalLM"]),
+    "tiny-qwen2-moe": dict(hidden_size=256, intermediate_size=512, num_attention_heads=4, num_key_value_heads=2,
+                           num_hidden_layers=2, vocab_size=512, rope_theta=1e6, rms_norm_eps=1e-6,
+                           attention_bias=True, num_local_experts=8, num_experts_per_tok=3,
+                           moe_intermediate_size=128, shared_expert_intermediate_size=256, norm_topk_prob=False,
+                           model_type="qwen2_moe", architectures=["Qwen2MoeForCausalLM"]),
     "small": dict(hidden_size=1024, intermediate_size=2816, num_attention_heads=8,
                   num_key_value_heads=2, num_hidden_layers=4, vocab_size=32000),
 }

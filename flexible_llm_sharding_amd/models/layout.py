@@ -18,13 +18,16 @@ Decoder layer image (fp16, every slot 256-byte aligned)::
     wgu   [2I, H]          gate_proj | up_proj        (rows concatenated)
     wdown [H, I]           down_proj
 
-MoE decoder (Mixtral / Qwen3-MoE) — the MLP piece is the router and every expert, each expert's
-tensors whole and in checkpoint row order::
+MoE decoder (Mixtral / Qwen3-MoE / Qwen2-MoE) — the MLP piece is the router and every expert, each
+expert's tensors whole and in checkpoint row order::
 
     ln2     [H]            post_attention_layernorm.weight
     wrouter [E, H]         router (Mixtral block_sparse_moe.gate / Qwen3-MoE mlp.gate)
     wgu     [E, 2I', H]    per expert: gate (w1 / gate_proj) | up (w3 / up_proj)
     wdown   [E, H, I']     per expert: down (w2 / down_proj)
+    wsgu    [2Is, H]       Qwen2-MoE shared expert: gate_proj | up_proj
+    wsdown  [H, Is]        shared expert down_proj
+    wsg     [1, H]         shared_expert_gate
 
 so expert e's [gate; up] block is the same stacked operand as the dense wgu, at a fixed stride:
 the grouped GEMM (csrc/kernels/moe.hip) indexes experts by that stride.
@@ -133,6 +136,9 @@ def layer_layout(cfg: ModelConfig, kind: str, elem_size: int = 2) -> LayerLayout
         if cfg.is_moe:
             E, Ie = cfg.num_local_experts, cfg.expert_intermediate
             specs += [("ln2", (H,)), ("wrouter", (E, H)), ("wgu", (E, 2 * Ie, H)), ("wdown", (E, H, Ie))]
+            Is = cfg.shared_expert_intermediate_size
+            if Is:
+                specs += [("wsgu", (2 * Is, H)), ("wsdown", (H, Is)), ("wsg", (1, H))]
         else:
             specs += [("ln2", (H,)), ("wgu", (2 * I, H)), ("wdown", (H, I))]
     else:
@@ -242,6 +248,13 @@ def _expert_placements(cfg: ModelConfig, p: str, o: Dict[str, int], es: int) -> 
         out += [Placement(g, gu, Ie * H, (Ie, H), es),
                 Placement(u, gu + es * Ie * H, Ie * H, (Ie, H), es),
                 Placement(d, o["wdown"] + es * e * H * Ie, H * Ie, (H, Ie), es)]
+    Is = cfg.shared_expert_intermediate_size
+    if Is:
+        b = f"{p}.mlp.shared_expert"
+        out += [Placement(f"{b}.gate_proj.weight", o["wsgu"], Is * H, (Is, H), es),
+                Placement(f"{b}.up_proj.weight", o["wsgu"] + es * Is * H, Is * H, (Is, H), es),
+                Placement(f"{b}.down_proj.weight", o["wsdown"], H * Is, (H, Is), es),
+                Placement(f"{p}.mlp.shared_expert_gate.weight", o["wsg"], H, (1, H), es)]
     return out
 
 

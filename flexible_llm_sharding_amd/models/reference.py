@@ -69,8 +69,9 @@ def _block(x, sd, p, cfg, pos, cos, sin, mask, past_kv=None):
 
 
 def _moe(h, sd, p, cfg):
-    """HF MixtralSparseMoeBlock / Qwen3MoeSparseMoeBlock in fp32: router softmax, top-k,
-    optional renormalisation, weighted sum of the chosen experts' SwiGLU outputs."""
+    """HF MixtralSparseMoeBlock / Qwen3MoeSparseMoeBlock / Qwen2MoeSparseMoeBlock in fp32: router
+    softmax, top-k, optional renormalisation, weighted sum of the chosen experts' SwiGLU outputs
+    (+ the sigmoid-gated shared expert)."""
     from .layout import expert_names, router_name
     shape = h.shape
     h = h.reshape(-1, shape[-1])
@@ -87,6 +88,11 @@ def _moe(h, sd, p, cfg):
         he = h[tok]
         y = (F.silu(he @ sd[gn].float().t()) * (he @ sd[un].float().t())) @ sd[dn].float().t()
         out.index_add_(0, tok, y * w[tok, slot, None])
+    if cfg.shared_expert_intermediate_size:   # HF Qwen2MoeSparseMoeBlock: gated shared expert
+        b = f"{p}.mlp.shared_expert"
+        s = (F.silu(h @ sd[f"{b}.gate_proj.weight"].float().t()) * (h @ sd[f"{b}.up_proj.weight"].float().t())) \
+            @ sd[f"{b}.down_proj.weight"].float().t()
+        out = out + torch.sigmoid(h @ sd[f"{p}.mlp.shared_expert_gate.weight"].float().t()) * s
     return out.reshape(shape)
 
 

@@ -69,6 +69,12 @@ def synthetic_layer_state_dict(cfg: ModelConfig, layer_name: str, seed: int = 0,
         for e in range(cfg.num_local_experts):
             gn, un, dn = expert_names(cfg, p, e)
             sd[gn], sd[un], sd[dn] = rnd(Ie, H), rnd(Ie, H), rnd(H, Ie)
+        Is = cfg.shared_expert_intermediate_size
+        if Is:
+            b = f"{p}.mlp.shared_expert"
+            sd[f"{b}.gate_proj.weight"], sd[f"{b}.up_proj.weight"] = rnd(Is, H), rnd(Is, H)
+            sd[f"{b}.down_proj.weight"] = rnd(H, Is)
+            sd[f"{p}.mlp.shared_expert_gate.weight"] = rnd(1, H) * 10
     else:
         sd.update({f"{p}.mlp.gate_proj.weight": rnd(I, H), f"{p}.mlp.up_proj.weight": rnd(I, H),
                    f"{p}.mlp.down_proj.weight": rnd(H, I)})
