@@ -88,7 +88,7 @@ int fls_moe_gemm(const void* A, const void* W, void* C, int M_bound, int N, int 
                  const int* tiles, const int* offs, const int* rows, int n_groups, long long wstride, int a_rows,
                  fls_stream_t s);
 int fls_moe_combine(const void* y, int ldy, const int* ids, const int* dest, const float* w, void* x, int ldx, int T,
-                    int k, int H, fls_stream_t s);
+                    int k, int H, const void* sh, int ldsh, fls_stream_t s);   // sh: optional shared-expert term
 int fls_gemm_set_order(int order);   // tile order: 0 by shape, 8 M-grouped, -4/-8 N-grouped
 int fls_gemm_set_mid(int on);   // 64x128-tile kernel for small / medium M (default on)
 // shared-prefix / varlen flash attention over packed work items (int32 x8:

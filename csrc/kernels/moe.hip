@@ -1,4 +1,4 @@
-// Sparse mixture-of-experts FFN on gfx950 (Mixtral, Qwen3-MoE).
+// Sparse mixture-of-experts FFN on gfx950 (Mixtral, Qwen3-MoE, Qwen2-MoE).
 //
 // Per MLP chunk of T tokens (h = post-attention RMSNorm output, x = residual stream):
 //   1. router logits   [T, E]  = h . Wr^T                     (fls_gemm, fp16 out like HF's Linear)
@@ -270,11 +270,12 @@ __global__ __launch_bounds__(PB_THREADS) void moe_place_kernel(const int* __rest
 }
 
 // x[t] = fp16(x[t] + acc), acc = fp16 sum over the token's slots in ascending expert order of
-// fp16(y[dest] * w); one block per token row, 8 columns (16 B) per thread and step
+// fp16(y[dest] * w) (+ sh[t], the gated shared-expert output, as one more fp16 add: HF
+// Qwen2MoeSparseMoeBlock); one block per token row, 8 columns (16 B) per thread and step
 __global__ __launch_bounds__(256) void moe_combine_kernel(const half_t* __restrict__ y, int ldy,
                                                           const int* __restrict__ ids, const int* __restrict__ dest,
                                                           const float* __restrict__ w, half_t* __restrict__ x, int ldx,
-                                                          int k, int H) {
+                                                          int k, int H, const half_t* __restrict__ sh, int ldsh) {
   const int t = blockIdx.x;
   // the token's k experts are distinct: slot j goes in place rank_j of the ascending-id order
   int id[MAX_K], order[MAX_K];
@@ -302,6 +303,11 @@ __global__ __launch_bounds__(256) void moe_combine_kernel(const half_t* __restri
       const half8 v = *(const half8*)(y + (size_t)dest[e] * ldy + c);
 #pragma unroll
       for (int q = 0; q < 8; ++q) acc[q] = (half_t)((float)acc[q] + (float)(half_t)((float)v[q] * wj));
+    }
+    if (sh) {
+      const half8 s = *(const half8*)(sh + (size_t)t * ldsh + c);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] = (half_t)((float)acc[q] + (float)s[q]);
     }
     half8 xv = *(const half8*)(x + (size_t)t * ldx + c);
 #pragma unroll
@@ -376,11 +382,11 @@ extern "C" int fls_moe_plan(const int* ids, int n, int k, int E, int* offs, int*
 }
 
 extern "C" int fls_moe_combine(const void* y, int ldy, const int* ids, const int* dest, const float* w, void* x,
-                               int ldx, int T, int k, int H, fls_stream_t s) {
+                               int ldx, int T, int k, int H, const void* sh, int ldsh, fls_stream_t s) {
   if (T <= 0) return 0;
-  if (k < 1 || k > MAX_K || H % 8 || ldx % 8 || ldy % 8) return -2;
+  if (k < 1 || k > MAX_K || H % 8 || ldx % 8 || ldy % 8 || (sh && ldsh % 8)) return -2;
   hipLaunchKernelGGL(moe_combine_kernel, dim3(T), dim3(256), 0, (hipStream_t)s, (const half_t*)y, ldy, ids, dest, w,
-                     (half_t*)x, ldx, k, H);
+                     (half_t*)x, ldx, k, H, (const half_t*)sh, ldsh);
   FLS_CHECK_LAUNCH();
   return 0;
 }

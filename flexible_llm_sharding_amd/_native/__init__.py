@@ -63,7 +63,7 @@ class Piece(ctypes.Structure):
                 ("kind", ctypes.c_int32), ("pad", ctypes.c_int32)]
 
 
-KERNELS_ABI = 17   # bumped whenever a C signature in csrc/include/fls.h changes
+KERNELS_ABI = 18   # bumped whenever a C signature in csrc/include/fls.h changes
 
 
 def _load_kernels(path: str = _KERNELS):
@@ -91,7 +91,7 @@ def _load_kernels(path: str = _KERNELS):
     _bind(lib, "fls_moe_gemm", c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
           c_void_p, c_void_p, c_void_p, c_int, ctypes.c_longlong, c_int, c_void_p)
     _bind(lib, "fls_moe_combine", c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
-          c_int, c_int, c_void_p)
+          c_int, c_int, c_void_p, c_int, c_void_p)
     _bind(lib, "fls_gemm_set_order", c_int, c_int)
     _bind(lib, "fls_gemm_set_v11", c_int, c_int)
     _bind(lib, "fls_gemm_set_skinny", c_int, c_int, c_int)

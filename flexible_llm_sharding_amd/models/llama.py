@@ -395,11 +395,22 @@ def _moe_mlp(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, step
         n = xs.shape[0]
         ctx.phase((n, H), (n * k, Ie), (n * k, H))
         h = ops.rmsnorm(xs, W["ln2"], cfg.rms_norm_eps, out=ctx.scratch(n, H))
+        shared = _shared_expert(ctx, W, h) if cfg.shared_expert_intermediate_size else None
         ops.moe_ffn(h, xs, W["wrouter"], W["wgu"], W["wdown"], k, cfg.norm_topk_prob,
-                    round_w16=cfg.model_type == "qwen3_moe", m_out=ctx.scratch(n * k, Ie),
-                    y_out=ctx.scratch(n * k, H))
+                    round_w16=cfg.model_type in ("qwen3_moe", "qwen2_moe"), m_out=ctx.scratch(n * k, Ie),
+                    y_out=ctx.scratch(n * k, H), shared=shared)
+        del shared
         del h
     return x
+
+
+def _shared_expert(ctx: ExecContext, W: Dict[str, torch.Tensor], h: torch.Tensor) -> torch.Tensor:
+    """Qwen2-MoE's shared expert on the normed rows h, in HF's fp16 roundings
+    (Qwen2MoeSparseMoeBlock): sigmoid(h . w_gate) * down(silu(gate(h)) * up(h))."""
+    ops = ctx.ops
+    s = ops.linear(ops.swiglu_up(h, W["wsgu"]), W["wsdown"])
+    g = torch.sigmoid(ops.linear(h, W["wsg"]))
+    return s * g
 
 
 def run_norm(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, meta: dict) -> torch.Tensor:

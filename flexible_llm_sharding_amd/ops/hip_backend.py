@@ -201,14 +201,15 @@ class HipOps:
 
     # ------------------------------------------------------ mixture of experts
     def moe_ffn(self, h, x, wrouter, wgu, wdown, top_k: int, norm_topk: bool, round_w16: bool = False,
-                m_out=None, y_out=None):
+                m_out=None, y_out=None, shared=None):
         """x += sparse-MoE FFN of h, in place (csrc/kernels/moe.hip): router GEMM, top-k routing,
         stable expert sort, grouped SwiGLU GEMM gathering h's rows, grouped down GEMM, ordered
         combine.  wgu [E, 2I, H] ([gate; up] per expert), wdown [E, H, I].  No host sync: the
         grouped GEMMs read the per-expert row counts on the device.  m_out [T*k, I] / y_out
-        [T*k, H]: optional scratch for the expert intermediates."""
+        [T*k, H]: optional scratch for the expert intermediates.  shared ([T, H] fp16): the gated
+        shared-expert output (Qwen2-MoE), added to the experts' sum before the residual."""
         route = self.moe_route(h, wrouter, top_k, norm_topk, round_w16)
-        return self.moe_experts(h, x, wgu, wdown, route, m_out=m_out, y_out=y_out)
+        return self.moe_experts(h, x, wgu, wdown, route, m_out=m_out, y_out=y_out, shared=shared)
 
     def moe_route(self, h, wrouter, top_k: int, norm_topk: bool, round_w16: bool = False) -> "MoeRoute":
         _f16(h, "h")
@@ -249,7 +250,7 @@ class HipOps:
                                  r.dest.data_ptr(), meta[o + 2 * n:].data_ptr(), _stream()), "fls_moe_plan")
         return r
 
-    def moe_experts(self, h, x, wgu, wdown, route: "MoeRoute", m_out=None, y_out=None):
+    def moe_experts(self, h, x, wgu, wdown, route: "MoeRoute", m_out=None, y_out=None, shared=None):
         """x += sum over each token's routed experts of w * down(swiglu(h)), in place."""
         for t, nm in ((h, "h"), (x, "x"), (wgu, "wgu"), (wdown, "wdown")):
             _f16(t, nm)
@@ -271,8 +272,14 @@ class HipOps:
             _chk(self.k.fls_moe_gemm(m.data_ptr(), wdown.data_ptr(), y.data_ptr(), bound, H, I, m.stride(0),
                                      wdown.stride(1), y.stride(0), EPI_NONE, route.tiles.data_ptr(),
                                      route.offs.data_ptr(), None, E, wdown.stride(0), n, st), "fls_moe_gemm(down)")
+        if shared is not None:
+            _f16(shared, "shared")
+            if tuple(shared.shape) != (T, H) or shared.stride(1) != 1:
+                raise ValueError(f"shared must be a row-major [{T}, {H}] tensor, got {tuple(shared.shape)}")
         _chk(self.k.fls_moe_combine(y.data_ptr(), y.stride(0), route.ids.data_ptr(), route.dest.data_ptr(),
-                                    route.w.data_ptr(), x.data_ptr(), x.stride(0), T, k, H, st), "fls_moe_combine")
+                                    route.w.data_ptr(), x.data_ptr(), x.stride(0), T, k, H,
+                                    shared.data_ptr() if shared is not None else None,
+                                    shared.stride(0) if shared is not None else 0, st), "fls_moe_combine")
         return x
 
     def _moe_per_expert(self, h, wgu, wdown, route, m, y):

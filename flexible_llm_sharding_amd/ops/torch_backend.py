@@ -92,12 +92,13 @@ class TorchOps:
 
     def moe_ffn(self, h: torch.Tensor, x: torch.Tensor, wrouter: torch.Tensor, wgu: torch.Tensor,
                 wdown: torch.Tensor, top_k: int, norm_topk: bool, round_w16: bool = False, m_out=None,
-                y_out=None) -> torch.Tensor:
+                y_out=None, shared=None) -> torch.Tensor:
         """x += sparse-MoE FFN of h, in place, in the order and rounding of HF's expert loop
         (transformers MixtralExperts / Qwen3MoeExperts): router Linear in the activation dtype,
         fp32 softmax, top-k, optional renormalisation (Qwen3-MoE rounds the weights to the
         activation dtype), each expert's weighted output rounded to the activation dtype and
-        accumulated in expert order, then added to the residual."""
+        accumulated in expert order, plus the gated shared-expert output (Qwen2-MoE) in one more
+        rounding, then added to the residual."""
         logits = self.linear(h, wrouter)
         w, idx = torch.topk(torch.softmax(logits.float(), dim=-1), top_k, dim=-1)
         if norm_topk:
@@ -111,6 +112,8 @@ class TorchOps:
                 continue
             y = self.linear(self.swiglu_up(h.index_select(0, tok), wgu[e]), wdown[e])
             acc.index_add_(0, tok, (y.float() * w[tok, slot, None]).to(x.dtype))
+        if shared is not None:
+            acc = (acc.float() + shared.float()).to(x.dtype)
         x.copy_((x.float() + acc.float()).to(x.dtype))
         return x
 

@@ -37,7 +37,7 @@ def normalize_expert_names(model_type: str, sd: Dict[str, torch.Tensor]) -> Dict
     of the released checkpoints (Mixtral ``block_sparse_moe.experts.e.w1/w3/w2``, Qwen3-MoE
     ``mlp.experts.e.gate_proj/up_proj/down_proj``), the one form the per-layer files hold
     (``models.layout.placements``).  Other keys pass through."""
-    if model_type not in ("mixtral", "qwen3_moe"):
+    if model_type not in ("mixtral", "qwen3_moe", "qwen2_moe"):
         return sd
     out = {}
     for k, v in sd.items():

@@ -266,6 +266,18 @@ def _hf_family_case(tmp_path, family):
             rope_theta=cfg.rope_theta, max_position_embeddings=cfg.max_position_embeddings,
             head_dim=cfg.head_dim, tie_word_embeddings=False, use_sliding_window=False, attention_bias=False)
         model = transformers.Qwen3MoeForCausalLM(hf_cfg)
+    elif family == "qwen2_moe":
+        cfg = preset("tiny-qwen2-moe")
+        hf_cfg = transformers.Qwen2MoeConfig(
+            hidden_size=cfg.hidden_size, intermediate_size=cfg.intermediate_size,
+            moe_intermediate_size=cfg.moe_intermediate_size, num_experts=cfg.num_local_experts,
+            num_experts_per_tok=cfg.num_experts_per_tok, norm_topk_prob=cfg.norm_topk_prob,
+            shared_expert_intermediate_size=cfg.shared_expert_intermediate_size,
+            num_attention_heads=cfg.num_attention_heads, num_key_value_heads=cfg.num_key_value_heads,
+            num_hidden_layers=cfg.num_hidden_layers, vocab_size=cfg.vocab_size, rms_norm_eps=cfg.rms_norm_eps,
+            rope_theta=cfg.rope_theta, max_position_embeddings=cfg.max_position_embeddings,
+            tie_word_embeddings=False, use_sliding_window=False, qkv_bias=True)
+        model = transformers.Qwen2MoeForCausalLM(hf_cfg)
     elif family in LLAMA_VARIANTS:
         over = dict(LLAMA_VARIANTS[family])
         cfg = preset("tiny", **over)
@@ -312,16 +324,17 @@ def _hf_v5_names(cfg, sd):
     return out
 
 
-@pytest.mark.parametrize("family", ["qwen2", "qwen3", "phi3", "phi3_mini", "mistral", "mixtral", "qwen3_moe"]
-                         + sorted(LLAMA_VARIANTS))
+@pytest.mark.parametrize("family", ["qwen2", "qwen3", "phi3", "phi3_mini", "mistral", "mixtral", "qwen3_moe",
+                                    "qwen2_moe"] + sorted(LLAMA_VARIANTS))
 def test_other_llama_families_match_hf(tmp_path, family):
     """Qwen2 (q/k/v biases, rope_theta 1e6), Qwen3 (per-head q/k RMSNorm, head_dim 128 on a
     256-wide residual), Phi-3 (fused qkv_proj / gate_up_proj, LongRoPE with its attention factor,
-    sliding window covering the prompts) and Mistral == HF transformers in causal mode, and ==
-    the fp32 oracle in the reference's bidirectional-prefix mode."""
+    sliding window covering the prompts), Mistral, the MoE families (Mixtral, Qwen3-MoE, Qwen2-MoE
+    with its sigmoid-gated shared expert) == HF transformers in causal mode, and == the fp32
+    oracle in the reference's bidirectional-prefix mode."""
     from flexible_llm_sharding_amd.config import ModelConfig
     path, cfg, sd, model = _hf_family_case(tmp_path, family)
-    assert ModelConfig.from_pretrained(path).attention_bias == (family == "qwen2")
+    assert ModelConfig.from_pretrained(path).attention_bias == (family in ("qwen2", "qwen2_moe"))
     assert ModelConfig.from_pretrained(path).qk_norm == (family in ("qwen3", "qwen3_moe"))
     assert ModelConfig.from_pretrained(path).num_local_experts == cfg.num_local_experts
     tok = load_tokenizer(path)

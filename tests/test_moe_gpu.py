@@ -121,14 +121,22 @@ def test_moe_experts_match_torch(ops, T, H, I, E, k):
     full = ops.moe_ffn(h, x.clone(), wr, wgu, wdown, k, True)
     torch.cuda.synchronize()
     assert torch.equal(full, out)
+    # Qwen2-MoE: the gated shared-expert output joins the experts' fp16 sum before the residual
+    sh = rnd(T, H, seed=6)
+    with_sh = ops.moe_experts(h, x.clone(), wgu, wdown, route, shared=sh)
+    torch.cuda.synchronize()
+    acc = (out.float() - x.float())               # the experts' sum as the combine rounded it
+    ref_sh = (x.float() + (acc + sh.float()).half().float()).half()
+    assert ((with_sh.float() - ref_sh.float()).norm() / (ref_sh.float() - x.float()).norm()).item() < 2e-3
 
 
 @pytest.mark.parametrize("lnps", [1, 3])
-@pytest.mark.parametrize("family", ["tiny-mixtral", "tiny-qwen3-moe"])
+@pytest.mark.parametrize("family", ["tiny-mixtral", "tiny-qwen3-moe", "tiny-qwen2-moe"])
 def test_moe_families_on_gpu(tmp_path, family, lnps):
-    """Mixtral (8 experts -> tiny 4, top-2, renormalised) and Qwen3-MoE (q/k norm, top-3 of 8,
-    fp16 routing weights, no renormalisation) end to end through the HIP engine vs the fp32 oracle,
-    incl. the pruned last layer; storage cpu so activations cross PCIe between shards."""
+    """Mixtral (8 experts -> tiny 4, top-2, renormalised), Qwen3-MoE (q/k norm, top-3 of 8,
+    fp16 routing weights, no renormalisation) and Qwen2-MoE (q/k/v biases, a sigmoid-gated shared
+    expert) end to end through the HIP engine vs the fp32 oracle, incl. the pruned last layer;
+    storage cpu so activations cross PCIe between shards."""
     from flexible_llm_sharding_amd.config import preset
     from flexible_llm_sharding_amd.engine import ShardedRunner
     from flexible_llm_sharding_amd.models.reference import reference_scores
