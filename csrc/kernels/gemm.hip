@@ -465,11 +465,11 @@ extern "C" int fls_gemm_set_order(int order) {
 }
 
 // skinny-M path (gemm_skinny.h): 0 off, 1 auto (default), 2 every M <= 256 it supports; blocks: the
-// K-split target (0 keeps the current); returns the previous mode
+// K-split block target (0: the whole-round rule, the default); returns the previous mode
 extern "C" int fls_gemm_set_skinny(int mode, int blocks) {
   const int old = g_skinny;
   g_skinny = mode < 0 ? 0 : mode > 2 ? 2 : mode;
-  if (blocks > 0) g_skinny_blocks = blocks;
+  g_skinny_blocks = blocks > 0 ? blocks : 0;
   return old;
 }
 

@@ -168,7 +168,7 @@ __global__ __launch_bounds__(256) void gemm_nt_skinny(const half_t* __restrict__
 }
 
 int g_skinny = 1;            // skinny-M path: 0 off, 1 auto, 2 any M <= 256 it supports (tests / A-B)
-int g_skinny_blocks = 256;   // split K until N / 128 x S reaches this many blocks
+int g_skinny_blocks = 0;     // K split: 0 = whole-round rule (try_skinny), n = until N / 128 x S >= n (A/B)
 
 template <int EPI, int RS>
 int launch_skinny_rs(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int lda, int ldw, int ldc,
@@ -214,11 +214,11 @@ int try_skinny(const half_t* A, const half_t* W, half_t* C, int M, int N, int K,
   if (g_skinny == 1 && (M < 17 || M > 192 || nblk >= 256)) return 0;
   // K slices: the fewest that give whole 256-CU rounds or at least two rounds (one block per CU:
   // a fractional single round leaves a tail of full-K blocks; 70B at M = 160: O / down S = 4,
-  // QKV S = 8, gate/up S = 2 measured fastest); g_skinny_blocks != 256 (A/B) sets a block target
+  // QKV S = 8 measured fastest); g_skinny_blocks > 0 (A/B) sets a block target instead
   int S = 1;
   auto good = [&](int s) {
     const long b = (long)nblk * s;
-    return g_skinny_blocks != 256 ? b >= g_skinny_blocks : (b % 256 == 0 || b >= 512);
+    return g_skinny_blocks > 0 ? b >= g_skinny_blocks : (b % 256 == 0 || b >= 512);
   };
   while (!good(S) && S < 16 && nkt % (2 * S) == 0 && nkt / (2 * S) >= 8) S *= 2;
   const bool direct_epi = EPI == FLS_EPI_NONE || EPI == FLS_EPI_RESID || EPI == FLS_EPI_SWIGLU;

@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--ms", default="32,64,128,160,256")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=8)
-    ap.add_argument("--blocks", default="256,512", help="skinny K-split targets to sweep")
+    ap.add_argument("--blocks", default="", help="skinny K-split block targets to sweep besides the default rule")
     ap.add_argument("--only", default="")
     ap.add_argument("--variants", default="", help="kernel-library variants (build.py --variant) to add")
     a = ap.parse_args()
@@ -45,7 +45,7 @@ def main():
     pos = torch.randint(0, 4096, (256,), dtype=torch.int32, device=dev)
     cos = torch.rand(4096, hd // 2, device=dev)
     sin = torch.rand(4096, hd // 2, device=dev)
-    variants = [("before", 0, 256)] + [(f"skinny_b{b}", 2, int(b)) for b in a.blocks.split(",")]
+    variants = [("before", 0, 0), ("skinny", 2, 0)] + [(f"skinny_b{b}", 2, int(b)) for b in a.blocks.split(",") if b]
     for name, N, K, epi in shapes:
         wbytes = N * K * 2
         ncopy = max(1, -(-600_000_000 // wbytes))
@@ -87,10 +87,10 @@ def main():
                     k.fls_gemm_set_skinny(mode, b)
                     times[vn].append(timed(lambda w: ops.gemm(x, w, epi, **kw)))
                 for v, o in vops.items():
-                    o.k.fls_gemm_set_skinny(2, 256)
+                    o.k.fls_gemm_set_skinny(2, 0)
                     times[v].append(timed(lambda w: o.gemm(x, w, epi, **kw)))
                 times["hipblaslt"].append(timed(lambda w: torch.matmul(x, w.t())))
-            k.fls_gemm_set_skinny(1, 256)
+            k.fls_gemm_set_skinny(1, 0)
             med = {v: sorted(t)[len(t) // 2] for v, t in times.items()}
             print(json.dumps({"op": name, "M": M, "N": N, "K": K, "rel_err_vs_before": err,
                               "us": {v: round(t, 1) for v, t in med.items()},

@@ -616,10 +616,10 @@ def test_gemm_skinny_m(ops, ref, M, epi, blocks):
     old = ops.k.fls_gemm_set_skinny(0, 0)
     try:
         plain = run()                                   # the mid / split-K / generic paths
-        ops.k.fls_gemm_set_skinny(2, blocks or 256)
+        ops.k.fls_gemm_set_skinny(2, blocks)
         got, again = run(), run()
     finally:
-        ops.k.fls_gemm_set_skinny(old, 256)
+        ops.k.fls_gemm_set_skinny(old, 0)
     torch.cuda.synchronize()
     assert torch.equal(got, again)
     assert rel_err(got.cpu(), want) < 3e-3
