@@ -253,9 +253,20 @@ def generation_loop(args, runner, comm: Comm, tok, original_prompts: Sequence, s
     # once at the end — same tokens, same output
     step_scores: List[List[np.ndarray]] = []
     step_tokens: List[List[np.ndarray]] = []
+    # host-side profile of chosen steps (FLS_PROFILE_GEN_STEPS="2,3" -> cProfile stats in
+    # FLS_PROFILE_OUT.<step>): where a generation step's host time goes
+    prof_steps = {int(s) for s in os.environ.get("FLS_PROFILE_GEN_STEPS", "").split(",") if s.strip()}
     for i_new in range(args.num_gen_token):
         t_step = time.perf_counter()
+        prof = None
+        if i_new in prof_steps:
+            import cProfile
+            prof = cProfile.Profile()
+            prof.enable()
         outputs = run_all(args, runner, comm, input_prompts)
+        if prof is not None:
+            prof.disable()
+            prof.dump_stats(f"{os.environ.get('FLS_PROFILE_OUT', 'gen_profile')}.{i_new}")
         if comm.rank == 0:
             if i_new == 0:
                 step_scores = [[o] for o in outputs]

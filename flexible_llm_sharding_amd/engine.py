@@ -475,6 +475,7 @@ class ShardedRunner:
             self.sends = []            # (tensor, work) of outputs in flight to another rank
             self.shard_ev: List = []   # end-of-shard events on the compute stream (host run-ahead bound)
             self.flops = 0.0
+            self.flops_of = {}              # (micro-batch, pruned layer) -> FLOPs of one decoder layer
             self.compute_s = 0.0
             self.cur_k = -1
             self.W = None
@@ -637,7 +638,10 @@ class ShardedRunner:
                     px.W[name].final_use = last_use
                 state = run_layer(self.ctx, name, px.W[name], state, batch, meta)
                 if layer_kind(name) == "decoder":
-                    px.flops += layer_flops(self.cfg, batch, self._pruned(name))
+                    key = (b, self._pruned(name))        # same FLOPs for every layer of a batch
+                    if key not in px.flops_of:
+                        px.flops_of[key] = layer_flops(self.cfg, batch, key[1])
+                    px.flops += px.flops_of[key]
         px.compute_s += time.perf_counter() - tc
         if px.pbar is not None:
             px.pbar.update(1)
@@ -755,6 +759,13 @@ class ShardedRunner:
         return self.ctx.prune_last and name == self.ctx.last_decoder
 
     def _speculative_prefetch(self) -> bool:
+        """Cached :meth:`_speculative_prefetch_policy` (static for a runner; asked per scanned shard)."""
+        v = getattr(self, "_spec_cached", None)
+        if v is None:
+            v = self._spec_cached = self._speculative_prefetch_policy()
+        return v
+
+    def _speculative_prefetch_policy(self) -> bool:
         """Let the prefetch run on into the next call's first shards (same weights every call)?
         On with 3+ slots (the default): the next call's embedding and first layer then load under
         this call's last layers (profiles/r2_slots_own, profiles/r2_slots7b).  With 2 slots the
@@ -780,6 +791,8 @@ class ShardedRunner:
         rotating slots (each lands in the slot of a shard already released; shards with a buffer of
         their own on the way load too); past the last shard, the next call's first shards."""
         pf = self.prefetcher
+        if getattr(pf, "all_kept_loaded", None) is not None and pf.all_kept_loaded():
+            return                            # (the scan below would walk every shard for nothing)
         n = len(self.my_shards)
         depth = 1 if pf.resident else max(1, pf.n_slots - 1)
         issued, j = 0, k + 1

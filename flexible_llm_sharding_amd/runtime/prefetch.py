@@ -291,6 +291,11 @@ class ShardPrefetcher:
         """Shard k stays in HBM and is already there (prefetching it is a no-op)."""
         return k in self._sticky and k in self._loaded_resident
 
+    def all_kept_loaded(self) -> bool:
+        """Every shard stays in HBM and is there (resident, or an HBM cache holding the model):
+        no prefetch has anything to do."""
+        return len(self._loaded_resident) == len(self.shards)
+
     def kept_bytes(self) -> int:
         return sum(self.shard_bytes(k) for k in self._sticky)
 
