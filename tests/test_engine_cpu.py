@@ -731,3 +731,29 @@ def test_pack_suffix_reuse_work_items():
     assert int(b2.work[:, 1].max()) == 38 and b2.r2_q_block == b2.q_block
     full = pack_prompts([tp], [0], prefix_offsets=[0], suffix_rows=[[20, 40]])
     assert full.r2_q_block == full.q_block               # no range 2: the batch's own q_block
+
+
+def test_qwen2_moe_config_forms():
+    """A released Qwen1.5-MoE config.json maps to q/k/v biases (no o_proj bias), 60 routed
+    experts (top 4, not renormalised) and the shared expert; dense layers between MoE layers and
+    a shared expert in a Qwen3-MoE config are rejected."""
+    from flexible_llm_sharding_amd.config import ModelConfig, preset
+    d = {"model_type": "qwen2_moe", "architectures": ["Qwen2MoeForCausalLM"], "hidden_size": 2048,
+         "intermediate_size": 5632, "moe_intermediate_size": 1408, "shared_expert_intermediate_size": 5632,
+         "num_experts": 60, "num_experts_per_tok": 4, "norm_topk_prob": False, "num_attention_heads": 16,
+         "num_key_value_heads": 16, "num_hidden_layers": 24, "vocab_size": 151936, "rope_theta": 1000000.0,
+         "rms_norm_eps": 1e-06, "decoder_sparse_step": 1, "mlp_only_layers": [], "use_sliding_window": False,
+         "sliding_window": 32768, "hidden_act": "silu"}
+    cfg = ModelConfig.from_dict(d)
+    assert cfg.attention_bias and not cfg.o_proj_bias
+    assert (cfg.num_local_experts, cfg.num_experts_per_tok, cfg.expert_intermediate) == (60, 4, 1408)
+    assert cfg.shared_expert_intermediate_size == 5632 and not cfg.norm_topk_prob and cfg.sliding_window is None
+    ref = preset("qwen1.5-moe-a2.7b")
+    assert cfg.decoder_layer_params() == ref.decoder_layer_params()
+    # 14.3B parameters in all (the released model card's count)
+    assert abs(cfg.total_params() / 1e9 - 14.32) < 0.05
+    assert not ModelConfig.from_dict(dict(d, qkv_bias=False)).attention_bias
+    for bad in (dict(d, mlp_only_layers=[3]), dict(d, decoder_sparse_step=2),
+                dict(d, model_type="qwen3_moe")):
+        with pytest.raises(NotImplementedError):
+            ModelConfig.from_dict(bad)
