@@ -389,11 +389,12 @@ int launch_v11(const half_t* A, const half_t* W, half_t* C, int M, int N, int K,
 
 }  // namespace
 
-// 1 = use v11 where it pays (default), 0 = v10 everywhere, 2 = v11 on every shape it supports
-// (tests: small and ragged shapes); returns the previous mode
+// 1 = use v11 where it pays (default: no more rows than v10), 3 = by 256-CU round counts (A/B),
+// 0 = v10 everywhere, 2 = v11 on every shape it supports (tests: small and ragged shapes);
+// returns the previous mode
 extern "C" int fls_gemm_set_v11(int mode) {
   const int old = g_v11;
-  g_v11 = mode < 0 ? 0 : mode > 2 ? 2 : mode;
+  g_v11 = mode < 0 ? 0 : mode > 3 ? 3 : mode;
   return old;
 }
 
@@ -413,11 +414,21 @@ extern "C" int fls_gemm_v11_try(const void* A, const void* W, void* C, const voi
   if (!g_v11 || M < TM || N % TN || K % TK || (K / TK) % 2 || lda % 8 || ldw % 8) return 0;
   const int rows = g_v11_rows > 0 ? min(g_v11_rows, M) : M;
   if (rows < TM) return 0;
-  if (g_v11 == 1) {
-    // fills the chip (at least one tile per CU per launch), and computes no more rows than v10's
-    // 256-row tiles would (callers chunk rows in multiples of 768 = lcm(256, 384))
+  if (g_v11 == 1 || g_v11 == 3) {
+    // fills the chip (at least one tile per CU per launch)
     if ((size_t)((rows + TM - 1) / TM) * (N / TN) < 256) return 0;
-    if ((size_t)((M + TM - 1) / TM) * TM > (size_t)((M + 255) / 256) * 256) return 0;
+    if (g_v11 == 1) {
+      // computes no more rows than v10's 256-row tiles would (callers chunk rows in multiples of
+      // 768 = lcm(256, 384))
+      if ((size_t)((M + TM - 1) / TM) * TM > (size_t)((M + 255) / 256) * 256) return 0;
+    } else {
+      // by 256-CU rounds: a v11 tile is 1.5x a v10 tile's work at ~10% more FLOP/s on the 70B
+      // shapes (profiles/r4_gemm), so v11 takes the launch when rounds11 x 15 < rounds10 x 11
+      // (e.g. 4,096-row QKV chunks: 2 rounds of 440 tiles vs 3 rounds of 640)
+      const long r10 = ((long)((M + 255) / 256) * (N / 256) + 255) / 256;
+      const long r11 = ((long)((M + TM - 1) / TM) * (N / TN) + 255) / 256;
+      if (r11 * 15 >= r10 * 11) return 0;
+    }
   }
   // 32-bit DMA offsets: every row of A (piece rows + lane rows + K) and of the (stacked) weight
   if ((size_t)M * lda * 2 >= (1ull << 32)) return 0;
