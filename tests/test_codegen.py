@@ -28,8 +28,8 @@ def _asm(src, tmp):
     return open(out).read().split("\n")
 
 
-def _main_loops(lines, kernel_re):
-    """(kernel name, loop body lines) of every loop with >= 100 MFMAs in the matching kernels."""
+def _main_loops(lines, kernel_re, min_mfma=100):
+    """(kernel name, loop body lines) of every loop with >= min_mfma MFMAs in the matching kernels."""
     starts = [i for i, l in enumerate(lines) if re.match(r"^_Z\S*" + kernel_re + r"\S*:", l)]
     ends = [next((j for j in range(s + 1, len(lines)) if lines[j].startswith(".Lfunc_end")), len(lines)) for s in starts]
     for s, e in zip(starts, ends):
@@ -45,7 +45,7 @@ def _main_loops(lines, kernel_re):
             if not be:
                 continue
             body = k[h:be[0] + 1]
-            if sum("v_mfma" in x for x in body) >= 100:
+            if sum("v_mfma" in x for x in body) >= min_mfma:
                 yield k[0].split(":")[0], body
 
 
@@ -60,3 +60,21 @@ def test_gemm_main_loop_has_no_register_copies(tmp_path, src, kernel, mfmas):
         assert n_mfma == mfmas, (name, n_mfma)
         copies = [x.strip() for x in body if re.search(r"\bv_mov|\bv_accvgpr|\bv_pk_mov", x)]
         assert not copies, (name, copies[:8])
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not installed")
+def test_skinny_gemm_loop_has_no_register_copies(tmp_path):
+    """gemm_nt_skinny<RS, EPI> (gemm_skinny.h): one K-tile per iteration, 2 K-steps x RS row
+    subtiles x 2 weight subtiles of asm MFMAs into pinned AGPR accumulators; no copy of any
+    register in the loop (a compiled-MFMA build rotated the accumulators through AGPR copies every
+    K-tile) and no scratch."""
+    lines = _asm(os.path.join(ROOT, "csrc", "kernels", "gemm.hip"), str(tmp_path))
+    loops = list(_main_loops(lines, "gemm_nt_skinny", min_mfma=8))
+    names = {n for n, _ in loops}
+    assert len(names) == 32, sorted(names)               # RS 2..16 (even) x NONE / RESID / SWIGLU / F32
+    for name, body in loops:
+        rs = int(re.search(r"gemm_nt_skinnyILi(\d+)E", name).group(1))
+        assert sum("v_mfma" in x for x in body) == 4 * rs, name
+        copies = [x.strip() for x in body if re.search(r"\bv_mov|\bv_accvgpr|\bv_pk_mov|scratch_", x)]
+        assert not copies, (name, copies[:8])
+
