@@ -275,11 +275,13 @@ def generation_loop(args, runner, comm: Comm, tok, original_prompts: Sequence, s
                 for pi, o in enumerate(outputs):
                     step_scores[pi].append(o)
                     step_tokens[pi].append(greedy_tokens(o))
+            # s + tok.decode(t) for every suffix (main.py:86-88), the decodes in one batched call
+            news = [np.concatenate(step_tokens[pi], axis=1) for pi in range(len(input_prompts))]
+            flat = [t for nt in news for t in nt]
+            texts = iter(tok.batch_decode(flat) if hasattr(tok, "batch_decode") else [tok.decode(t) for t in flat])
             for pi in range(len(input_prompts)):
                 prefix, suffix = original_prompts[pi]
-                new_tokens = np.concatenate(step_tokens[pi], axis=1)
-                new_suffix = tuple(s + tok.decode(t) for s, t in zip(suffix, new_tokens))
-                input_prompts[pi] = (prefix, new_suffix)
+                input_prompts[pi] = (prefix, tuple(s + next(texts) for s in suffix))
         if comm.world > 1:
             input_prompts = comm.broadcast_object(input_prompts, src=0)
         if step_times is not None:
