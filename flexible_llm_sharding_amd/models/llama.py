@@ -180,6 +180,7 @@ class ExecContext:
     prune_last: bool = True
     last_decoder: str = ""
     ws: Optional[Workspace] = None          # scratch arena (None: fresh allocations, e.g. graph capture)
+    side_stream: Optional[object] = None    # second compute stream (two-stream QKV chunks), made on first use
 
     def phase(self, *shapes) -> None:
         """Start a workspace phase that will carve ``shapes`` (rows, cols) in order."""
@@ -195,6 +196,10 @@ def run_embed(ctx: ExecContext, W: Dict[str, torch.Tensor], meta: dict) -> torch
 
 
 CHUNK_ALIGN = int(os.environ.get("FLS_CHUNK_ALIGN", "3072"))   # A/B knob (256: round 3's chunks)
+# RMSNorm + QKV row chunks alternate between two streams over the two halves of the normed buffer,
+# so one chunk's GEMM fills the CUs the other's last tile round leaves idle (2, default: +1.1% on the
+# capped 70B headline, profiles/r4_gemm/qkv_two_streams; A/B: 1 = one stream)
+QKV_STREAMS = int(os.environ.get("FLS_QKV_STREAMS", "2"))
 
 
 def balanced_step(rows: int, limit: int, align: int = 0) -> int:
@@ -242,6 +247,11 @@ def _attn_inputs(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, 
                                      bias=bias, out=out)
         return ops.qkv_rope(h, wr, p, ctx.cos, ctx.sin, n_q, n_k, hd, bias=bias, out=out)
 
+    if (QKV_STREAMS == 2 and not prune and hbuf is not None and x.is_cuda and T0 > step
+            and step % 512 == 0):
+        _qkv_two_streams(ctx, x, pos, W["ln1"], hbuf, qkv, step // 2,
+                         lambda h, p, out: proj(h, w, p, nq, nkv, b, out=out))
+        return qkv
     for s in range(0, T0, step):
         e = min(T0, s + step)
         h = ops.rmsnorm(x[s:e], W["ln1"], eps, out=hbuf[:e - s] if hbuf is not None else None)
@@ -260,6 +270,31 @@ def _attn_inputs(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, 
         q = proj(hq, w[:qs], pos.index_select(0, idx), nq, 0, b[:qs] if b is not None else None)
         qkv[:, :qs].index_copy_(0, idx if idx.dtype == torch.int64 else idx.long(), q)
     return qkv
+
+
+def _qkv_two_streams(ctx: ExecContext, x: torch.Tensor, pos: torch.Tensor, ln1: torch.Tensor,
+                     hbuf: torch.Tensor, qkv: torch.Tensor, half: int, proj) -> None:
+    """RMSNorm + QKV over row chunks of ``half`` rows, chunk i on stream i % 2 with normed half
+    buffer i % 2 (its previous user, chunk i - 2, ran on the same stream): the two streams' GEMMs
+    overlap, so a chunk's partial last round of tiles shares the CUs with the next chunk's first.
+    Same kernels per row as one stream (bitwise equal)."""
+    ops, cfg = ctx.ops, ctx.cfg
+    main = torch.cuda.current_stream(x.device)
+    if ctx.side_stream is None:
+        ctx.side_stream = torch.cuda.Stream(x.device)
+    side = ctx.side_stream
+    side.wait_stream(main)                            # x and the weights are ready
+    bufs = (hbuf[:half], hbuf[half:2 * half])
+    T0 = x.shape[0]
+    for i, s in enumerate(range(0, T0, half)):
+        e = min(T0, s + half)
+        with torch.cuda.stream(main if i % 2 == 0 else side):
+            h = ops.rmsnorm(x[s:e], ln1, cfg.rms_norm_eps, out=bufs[i % 2][:e - s])
+            dst = qkv[s:e]
+            r = proj(h, pos[s:e], dst)
+            if r.data_ptr() != dst.data_ptr():
+                dst.copy_(r)
+    main.wait_stream(side)                            # every row's Q / K / V before the attention
 
 
 def _attention_whole(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, batch, meta: dict,

@@ -202,6 +202,27 @@ def test_activation_store_no_race_large_batches(mid_model, tmp_path, storage):
     r.close()
 
 
+def test_qkv_two_streams_bitwise(mid_model):
+    """RMSNorm + QKV row chunks alternating between two streams (models/llama.py
+    ``_qkv_two_streams``, FLS_QKV_STREAMS=2) == one stream, bitwise: the same kernels per row."""
+    from flexible_llm_sharding_amd.models import llama
+    cfg, store, tok, prompts = mid_model
+    outs = []
+    old = llama.QKV_STREAMS
+    try:
+        for n in (1, 2):
+            llama.QKV_STREAMS = n
+            r = ShardedRunner(cfg, store, "cuda:0", tok, layer_num_per_shard=1, storage_location="gpu")
+            r.ctx.qkv_chunk = 2048                    # 16,128 packed rows -> 8 chunks (4 per stream)
+            outs.append(r(prompts))
+            r.close()
+    finally:
+        llama.QKV_STREAMS = old
+    for a, b in zip(*outs):
+        assert np.isfinite(a.astype(np.float32)).all()
+        assert np.array_equal(a, b)
+
+
 @pytest.mark.parametrize("streaming", [False, True])
 def test_dp_allgather_prefetcher_over_rccl(setup, tmp_path, streaming):
     """The data-parallel weight path on real RCCL: a one-rank `nccl` process group, each layer
