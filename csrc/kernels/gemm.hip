@@ -455,7 +455,7 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
 
 }  // namespace
 
-extern "C" int fls_kernels_version(void) { return 18; }
+extern "C" int fls_kernels_version(void) { return 19; }
 
 // tile order: 0 = by shape (default); g > 0: groups of g M tiles; g < 0: groups of -g N tiles (A/B, tests)
 extern "C" int fls_gemm_set_order(int order) {
@@ -470,6 +470,13 @@ extern "C" int fls_gemm_set_skinny(int mode, int blocks) {
   const int old = g_skinny;
   g_skinny = mode < 0 ? 0 : mode > 2 ? 2 : mode;
   g_skinny_blocks = blocks > 0 ? blocks : 0;
+  return old;
+}
+
+// skinny-M weight rows per block: 0 auto (default), 128 or 256 where supported; returns the previous
+extern "C" int fls_gemm_set_skinny_bn(int bn) {
+  const int old = g_skinny_bn;
+  g_skinny_bn = bn == 128 || bn == 256 ? bn : 0;
   return old;
 }
 

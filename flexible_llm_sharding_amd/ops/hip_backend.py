@@ -75,6 +75,8 @@ class HipOps:
             self.k.fls_gemm_v11_tune(int(os.environ.get("FLS_V11_ORDER", "0")), int(os.environ.get("FLS_V11_ROWS", "0")))
         if os.environ.get("FLS_SKINNY"):                  # skinny-M GEMM: 0 off, 1 auto (default), 2 forced (A/B)
             self.k.fls_gemm_set_skinny(int(os.environ["FLS_SKINNY"]), int(os.environ.get("FLS_SKINNY_BLOCKS", "0")))
+        if os.environ.get("FLS_SKINNY_BN"):               # skinny-M weight rows per block: 0 auto, 128 / 256
+            self.k.fls_gemm_set_skinny_bn(int(os.environ["FLS_SKINNY_BN"]))
         if os.environ.get("FLS_ATTN_SPLIT"):              # split-KV slices of the range-2 kernel (A/B)
             self.k.fls_attention_set_split(int(os.environ["FLS_ATTN_SPLIT"]))
 

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=8)
     ap.add_argument("--blocks", default="", help="skinny K-split block targets to sweep besides the default rule")
+    ap.add_argument("--blocks256", default="", help="the same for the 256-row weight block")
     ap.add_argument("--only", default="")
     ap.add_argument("--variants", default="", help="kernel-library variants (build.py --variant) to add")
     a = ap.parse_args()
@@ -45,7 +46,9 @@ def main():
     pos = torch.randint(0, 4096, (256,), dtype=torch.int32, device=dev)
     cos = torch.rand(4096, hd // 2, device=dev)
     sin = torch.rand(4096, hd // 2, device=dev)
-    variants = [("before", 0, 0), ("skinny", 2, 0)] + [(f"skinny_b{b}", 2, int(b)) for b in a.blocks.split(",") if b]
+    variants = ([("before", 0, 0, 0), ("skinny", 2, 0, 128), ("skinny256", 2, 0, 256)]
+                + [(f"skinny_b{b}", 2, int(b), 128) for b in a.blocks.split(",") if b]
+                + [(f"skinny256_b{b}", 2, int(b), 256) for b in a.blocks256.split(",") if b])
     for name, N, K, epi in shapes:
         wbytes = N * K * 2
         ncopy = max(1, -(-600_000_000 // wbytes))
@@ -59,8 +62,9 @@ def main():
             if epi == EPI_ROPE:
                 kw = dict(positions=pos[:M], cos=cos, sin=sin, rope_cols=(nh + nkv) * hd, head_dim=hd)
             outs = {}
-            for vn, mode, b in variants:
+            for vn, mode, b, bn in variants:
                 k.fls_gemm_set_skinny(mode, b)
+                k.fls_gemm_set_skinny_bn(bn)
                 outs[vn] = ops.gemm(x, ws[0], epi, **({} if epi == EPI_RESID else kw)).float()
             torch.cuda.synchronize()
             ref = outs["before"]
@@ -83,14 +87,16 @@ def main():
             for v in vops:
                 times[v] = []
             for _ in range(a.rounds):
-                for vn, mode, b in variants:
+                for vn, mode, b, bn in variants:
                     k.fls_gemm_set_skinny(mode, b)
+                    k.fls_gemm_set_skinny_bn(bn)
                     times[vn].append(timed(lambda w: ops.gemm(x, w, epi, **kw)))
                 for v, o in vops.items():
                     o.k.fls_gemm_set_skinny(2, 0)
                     times[v].append(timed(lambda w: o.gemm(x, w, epi, **kw)))
                 times["hipblaslt"].append(timed(lambda w: torch.matmul(x, w.t())))
             k.fls_gemm_set_skinny(1, 0)
+            k.fls_gemm_set_skinny_bn(0)
             med = {v: sorted(t)[len(t) // 2] for v, t in times.items()}
             print(json.dumps({"op": name, "M": M, "N": N, "K": K, "rel_err_vs_before": err,
                               "us": {v: round(t, 1) for v, t in med.items()},

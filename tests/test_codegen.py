@@ -64,17 +64,18 @@ def test_gemm_main_loop_has_no_register_copies(tmp_path, src, kernel, mfmas):
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not installed")
 def test_skinny_gemm_loop_has_no_register_copies(tmp_path):
-    """gemm_nt_skinny<RS, EPI> (gemm_skinny.h): one K-tile per iteration, 2 K-steps x RS row
-    subtiles x 2 weight subtiles of asm MFMAs into pinned AGPR accumulators; no copy of any
+    """gemm_nt_skinny<RS, EPI, BN> (gemm_skinny.h): one K-tile per iteration, 2 K-steps x RS row
+    subtiles x BN / 64 weight subtiles of asm MFMAs into pinned AGPR accumulators; no copy of any
     register in the loop (a compiled-MFMA build rotated the accumulators through AGPR copies every
     K-tile) and no scratch."""
     lines = _asm(os.path.join(ROOT, "csrc", "kernels", "gemm.hip"), str(tmp_path))
     loops = list(_main_loops(lines, "gemm_nt_skinny", min_mfma=8))
     names = {n for n, _ in loops}
-    assert len(names) == 32, sorted(names)               # RS 2..16 (even) x NONE / RESID / SWIGLU / F32
+    # (BN 128: RS 2..16 even, BN 256: RS 2..10 even) x NONE / RESID / SWIGLU / F32
+    assert len(names) == 4 * (8 + 5), sorted(names)
     for name, body in loops:
-        rs = int(re.search(r"gemm_nt_skinnyILi(\d+)E", name).group(1))
-        assert sum("v_mfma" in x for x in body) == 4 * rs, name
+        rs, bn = map(int, re.search(r"gemm_nt_skinnyILi(\d+)ELin?\d+ELi(\d+)E", name).groups())
+        assert sum("v_mfma" in x for x in body) == rs * bn // 32, name
         copies = [x.strip() for x in body if re.search(r"\bv_mov|\bv_accvgpr|\bv_pk_mov|scratch_", x)]
         assert not copies, (name, copies[:8])
 

@@ -575,15 +575,17 @@ def test_gemm_small_m_splitk(ops, ref, M, epi):
     assert rel_err(got.cpu(), plain.cpu()) < 2e-3
 
 
+@pytest.mark.parametrize("bn", [128, 256])
 @pytest.mark.parametrize("blocks", [0, 1])
 @pytest.mark.parametrize("M", [1, 7, 17, 33, 100, 160, 256])
 @pytest.mark.parametrize("epi", ["none_bias", "resid", "swiglu", "rope128", "rope64"])
-def test_gemm_skinny_m(ops, ref, M, epi, blocks):
+def test_gemm_skinny_m(ops, ref, M, epi, blocks, bn):
     """Skinny-M kernel (gemm_skinny.h: every row of M in one block, weights and activations by
     LDS-DMA) == the fp32 reference and == the other small-M paths to rounding, bitwise
-    reproducible.  blocks 0: the default K split (fp32 partials + reduce, this N splits in 2);
-    blocks 1: no split, the NONE / RESID / SWIGLU epilogues applied in the kernel.  M < 17 only
-    runs here with the path forced (mode 2)."""
+    reproducible.  blocks 0: the default K split (fp32 partials + reduce); blocks 1: no split, the
+    NONE / RESID / SWIGLU epilogues applied in the kernel.  bn: weight rows per block (256: four
+    subtiles per wave, refill after the barrier; M > 160 falls back to 128).  M < 17 only runs
+    here with the path forced (mode 2)."""
     from flexible_llm_sharding_amd.config import ModelConfig
     from flexible_llm_sharding_amd.models.llama import rope_tables
     K, N = 2048, 1024
@@ -614,21 +616,25 @@ def test_gemm_skinny_m(ops, ref, M, epi, blocks):
             run = lambda: ops.gemm(x, w, EPI_NONE, bias=b)                         # noqa: E731
             want = x.float().cpu() @ w.float().cpu().t() + b.float().cpu()
     old = ops.k.fls_gemm_set_skinny(0, 0)
+    old_bn = ops.k.fls_gemm_set_skinny_bn(bn)
     try:
         plain = run()                                   # the mid / split-K / generic paths
         ops.k.fls_gemm_set_skinny(2, blocks)
         got, again = run(), run()
     finally:
         ops.k.fls_gemm_set_skinny(old, 0)
+        ops.k.fls_gemm_set_skinny_bn(old_bn)
     torch.cuda.synchronize()
     assert torch.equal(got, again)
     assert rel_err(got.cpu(), want) < 3e-3
     assert rel_err(got.cpu(), plain.cpu()) < 2e-3
 
 
-def test_gemm_skinny_70b_generation_shapes(ops):
+@pytest.mark.parametrize("bn", [0, 256])
+def test_gemm_skinny_70b_generation_shapes(ops, bn):
     """The 70B projections at a generation step's 160 rows (QKV + RoPE, O + residual, gate/up +
-    SwiGLU, down + residual) on the skinny kernel == the same GEMMs with it off, to rounding."""
+    SwiGLU, down + residual) on the skinny kernel (mode 2: every projection, bn 0 = the default
+    block) == the same GEMMs with it off, to rounding."""
     from flexible_llm_sharding_amd.config import preset
     from flexible_llm_sharding_amd.models.llama import rope_tables
     cfg = preset("llama2-70b")
@@ -649,12 +655,15 @@ def test_gemm_skinny_70b_generation_shapes(ops):
             lambda: ops.swiglu_up(x, wgu),
             lambda: ops.linear_residual(xi, wd, r0.clone())]
     for run in runs:
-        got = run()
-        old = ops.k.fls_gemm_set_skinny(0, 0)
+        old = ops.k.fls_gemm_set_skinny(2, 0)
+        old_bn = ops.k.fls_gemm_set_skinny_bn(bn)
         try:
+            got = run()
+            ops.k.fls_gemm_set_skinny(0, 0)
             plain = run()
         finally:
             ops.k.fls_gemm_set_skinny(old, 0)
+            ops.k.fls_gemm_set_skinny_bn(old_bn)
         torch.cuda.synchronize()
         assert rel_err(got, plain) < 2e-3
 
