@@ -48,6 +48,13 @@ class ModelConfig:
     # Qwen2-MoE: a dense SwiGLU "shared expert" of this width on every token, scaled by
     # sigmoid(h . shared_expert_gate) and added to the routed experts' sum (0: none)
     shared_expert_intermediate_size: int = 0
+    # Granite (HF GraniteModel / GraniteDecoderLayer / GraniteForCausalLM): token embeddings x
+    # embedding_multiplier; each sub-layer output x residual_multiplier before the residual add;
+    # attention scores x attention_multiplier (instead of head_dim^-1/2); logits / logits_scaling
+    embedding_multiplier: float = 1.0
+    residual_multiplier: float = 1.0
+    attention_multiplier: Optional[float] = None
+    logits_scaling: float = 1.0
     bos_token_id: int = 1
     eos_token_id: int = 2
     torch_dtype: str = "float16"
@@ -58,6 +65,11 @@ class ModelConfig:
     @property
     def head_dim(self) -> int:
         return self.explicit_head_dim or self.hidden_size // self.num_attention_heads
+
+    @property
+    def attn_scale(self) -> float:
+        """Softmax scale of the attention scores (Granite: attention_multiplier)."""
+        return self.attention_multiplier if self.attention_multiplier is not None else self.head_dim ** -0.5
 
     @property
     def is_moe(self) -> bool:
@@ -245,7 +257,8 @@ class ModelConfig:
 # Llama-structured causal LMs (model.embed_tokens / model.layers.N / model.norm / lm_head with
 # q/k/v/o + gate/up/down + two RMSNorms per layer) -- what the reference's AutoModelForCausalLM
 # path (utils.py:101-115) runs in practice.
-SUPPORTED_MODEL_TYPES = {"llama", "mistral", "qwen2", "qwen3", "phi3", "mixtral", "qwen3_moe", "qwen2_moe"}
+SUPPORTED_MODEL_TYPES = {"llama", "mistral", "qwen2", "qwen3", "phi3", "mixtral", "qwen3_moe", "qwen2_moe",
+                         "granite"}
 # MoE limits of the routing kernels (csrc/kernels/moe.hip): experts per layer, experts per token
 MAX_EXPERTS = 256
 MAX_TOP_K = 8
@@ -343,6 +356,16 @@ PRESETS = {
                            attention_bias=True, num_local_experts=8, num_experts_per_tok=3,
                            moe_intermediate_size=128, shared_expert_intermediate_size=256, norm_topk_prob=False,
                            model_type="qwen2_moe", architectures=["Qwen2MoeForCausalLM"]),
+    # Granite-3.0-8B: Llama geometry with the four Granite scalars and a tied 49k head
+    "granite-3-8b": dict(hidden_size=4096, intermediate_size=12800, num_attention_heads=32, num_key_value_heads=8,
+                         num_hidden_layers=40, vocab_size=49155, rope_theta=10000.0, tie_word_embeddings=True,
+                         embedding_multiplier=12.0, residual_multiplier=0.22, attention_multiplier=0.0078125,
+                         logits_scaling=16.0, bos_token_id=0, eos_token_id=0, model_type="granite",
+                         architectures=["GraniteForCausalLM"]),
+    "tiny-granite": dict(hidden_size=256, intermediate_size=512, num_attention_heads=4, num_key_value_heads=2,
+                         num_hidden_layers=2, vocab_size=512, embedding_multiplier=6.0, residual_multiplier=0.4,
+                         attention_multiplier=0.09, logits_scaling=3.0, model_type="granite",
+                         architectures=["GraniteForCausalLM"]),
     "small": dict(hidden_size=1024, intermediate_size=2816, num_attention_heads=8,
                   num_key_value_heads=2, num_hidden_layers=4, vocab_size=32000),
 }

@@ -192,7 +192,23 @@ class ExecContext:
 
 
 def run_embed(ctx: ExecContext, W: Dict[str, torch.Tensor], meta: dict) -> torch.Tensor:
-    return ctx.ops.embed(meta["ids"], W["embed"], ctx.act_dtype)
+    x = ctx.ops.embed(meta["ids"], W["embed"], ctx.act_dtype)
+    if ctx.cfg.embedding_multiplier != 1.0:          # Granite: GraniteModel scales the embeddings
+        x.mul_(ctx.cfg.embedding_multiplier)
+    return x
+
+
+def _resid(ctx: ExecContext, a: torch.Tensor, w: torch.Tensor, x: torch.Tensor, bias=None) -> torch.Tensor:
+    """x + a @ w^T (+ bias): the fused residual GEMM (in place on x).  Granite's
+    residual_multiplier r: x + fp16(fp16(a @ w^T) * r), HF GraniteDecoderLayer's roundings, as a
+    plain GEMM and an in-place add."""
+    r = ctx.cfg.residual_multiplier
+    if r == 1.0:
+        return ctx.ops.linear_residual(a, w, x, bias=bias)
+    y = ctx.ops.linear(a, w)
+    if bias is not None:
+        y.add_(bias)
+    return x.add_(y.mul_(r))
 
 
 CHUNK_ALIGN = int(os.environ.get("FLS_CHUNK_ALIGN", "3072"))   # A/B knob (256: round 3's chunks)
@@ -328,13 +344,14 @@ def _attention_whole(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tens
         kw["r2win"] = meta["r2win"]
     qb = batch.r2_q_block if "work2" in kw else batch.q_block     # (work_last items: one row each)
     a = ops.attention(qkv, attn_arg, cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim,
-                      kv0=kv0 if batch.kv_cached else None, q_block=qb, out=qkv[:, :cfg.q_size], **kw)
+                      kv0=kv0 if batch.kv_cached else None, q_block=qb, out=qkv[:, :cfg.q_size],
+                      scale=cfg.attn_scale, **kw)
     del qkv
     if prune:
         idx = meta["last_idx"]
         a = a.index_select(0, idx)
         x = x.index_select(0, idx)
-    return ops.linear_residual(a, W["wo"], x, bias=W.get("bo"))
+    return _resid(ctx, a, W["wo"], x, bias=W.get("bo"))
 
 
 def _attention_grouped(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, batch,
@@ -358,15 +375,16 @@ def _attention_grouped(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Te
         else:
             arg = g["work"] if work_items else g["segments"]
         kw = {"seg_lo": g["seg_lo"]} if work_items else {}
-        a = ops.attention(qkv, arg, nq, nkv, hd, q_block=batch.q_block, out=qkv[:, :cfg.q_size], **kw)
+        a = ops.attention(qkv, arg, nq, nkv, hd, q_block=batch.q_block, out=qkv[:, :cfg.q_size],
+                          scale=cfg.attn_scale, **kw)
         if prune:
             li = g["last_local"]
             if li.numel():
-                outs.append(ops.linear_residual(a.index_select(0, li), W["wo"], x[r0:r1].index_select(0, li),
-                                                bias=W.get("bo")))
+                outs.append(_resid(ctx, a.index_select(0, li), W["wo"], x[r0:r1].index_select(0, li),
+                                   bias=W.get("bo")))
         else:
             xr = x[r0:r1]
-            y = ops.linear_residual(a, W["wo"], xr, bias=W.get("bo"))
+            y = _resid(ctx, a, W["wo"], xr, bias=W.get("bo"))
             if y.data_ptr() != xr.data_ptr():
                 xr.copy_(y)
         del a, qkv
@@ -407,7 +425,7 @@ def run_decoder(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, b
         h = ops.rmsnorm(x, W["ln2"], eps, out=ctx.scratch(T, H))
         m = ops.swiglu_up(h, W["wgu"], out=ctx.scratch(T, I))
         del h
-        x = ops.linear_residual(m, W["wdown"], x)
+        x = _resid(ctx, m, W["wdown"], x)
     else:
         for s in range(0, T, step):
             xs = x[s:s + step]
@@ -416,7 +434,7 @@ def run_decoder(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, b
             h = ops.rmsnorm(xs, W["ln2"], eps, out=ctx.scratch(n, H))
             m = ops.swiglu_up(h, W["wgu"], out=ctx.scratch(n, I))
             del h
-            x[s:s + step] = ops.linear_residual(m, W["wdown"], xs)
+            x[s:s + step] = _resid(ctx, m, W["wdown"], xs)
     return x
 
 
@@ -455,7 +473,7 @@ def run_norm(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, meta
 
 
 def run_head(ctx: ExecContext, W: Dict[str, torch.Tensor], h: torch.Tensor) -> torch.Tensor:
-    return ctx.ops.lm_head_softmax(h, W["head"])
+    return ctx.ops.lm_head_softmax(h, W["head"], logits_scaling=ctx.cfg.logits_scaling)
 
 
 def run_layer(ctx: ExecContext, layer_name: str, W: Dict[str, torch.Tensor],

@@ -54,17 +54,18 @@ def _block(x, sd, p, cfg, pos, cos, sin, mask, past_kv=None):
     rep = nh // nkv
     kk = k.repeat_interleave(rep, 1)
     vv = v.repeat_interleave(rep, 1)
-    s = q @ kk.transpose(2, 3) / (hd ** 0.5)
+    s = q @ kk.transpose(2, 3) * cfg.attn_scale
     if mask is not None:
         s = s + mask
     a = torch.softmax(s, -1) @ vv
     a = a.transpose(1, 2).reshape(B, T, nh * hd)
-    x = x + a @ g("self_attn.o_proj.weight").t() + b("self_attn.o_proj.bias")
+    r = cfg.residual_multiplier                       # Granite; 1 elsewhere
+    x = x + (a @ g("self_attn.o_proj.weight").t() + b("self_attn.o_proj.bias")) * r
     h = _rms(x, g("post_attention_layernorm.weight"), cfg.rms_norm_eps)
     if cfg.is_moe:
-        return x + _moe(h, sd, p, cfg), present
+        return x + _moe(h, sd, p, cfg) * r, present
     m = F.silu(h @ g("mlp.gate_proj.weight").t()) * (h @ g("mlp.up_proj.weight").t())
-    x = x + m @ g("mlp.down_proj.weight").t()
+    x = x + (m @ g("mlp.down_proj.weight").t()) * r
     return x, present
 
 
@@ -113,8 +114,8 @@ def reference_scores(cfg: ModelConfig, sd: Dict[str, torch.Tensor], tok, prompts
                                 padding=True)["input_ids"])[:, 1:]
         eos = (sids != tok.pad_token_id).sum(1) - 1
         Lp, Ls, ns = pids.shape[1], sids.shape[1], sids.shape[0]
-        P = sd["model.embed_tokens.weight"].float()[pids]
-        S = sd["model.embed_tokens.weight"].float()[sids]
+        P = sd["model.embed_tokens.weight"].float()[pids] * cfg.embedding_multiplier
+        S = sd["model.embed_tokens.weight"].float()[sids] * cfg.embedding_multiplier
         ppos = torch.arange(Lp)[None]
         spos = torch.arange(Lp, Lp + Ls)[None].expand(ns, -1)
         pmask = None
@@ -130,6 +131,6 @@ def reference_scores(cfg: ModelConfig, sd: Dict[str, torch.Tensor], tok, prompts
         last = S[torch.arange(ns), eos][:, None]                             # utils.py:286
         h = _rms(last, sd["model.norm.weight"].float(), cfg.rms_norm_eps)
         head = sd.get("lm_head.weight", sd["model.embed_tokens.weight"]).float()
-        logits = (h @ head.t())[:, 0]
+        logits = (h @ head.t())[:, 0] / cfg.logits_scaling
         outs.append(torch.softmax(logits, -1)[:, None].numpy())
     return outs

@@ -299,7 +299,7 @@ class HipOps:
 
     # ----------------------------------------------------------- attention
     def attention(self, qkv, work, n_q_heads, n_kv_heads, head_dim, kv0=None, q_block: int = 64, out=None,
-                  seg_lo=None, work2=None, r2win=None):
+                  seg_lo=None, work2=None, r2win=None, scale=None):
         """kv0 ([P, 2 * n_kv * hd], K then V): range 0 of every work item reads these rows (prefix cache).
         seg_lo ([T] int32, first row of each row's suffix): work items may span several suffixes.
         work2 ([n_items, 2] int32: r2_start, r2_len) + r2win ([T, 2] int32: kv0 rows [lo, hi) per row):
@@ -328,7 +328,8 @@ class HipOps:
         ws = self._splitk_ws(qkv.device, 0, 0) if work2 is not None else None
         rc = self.k.fls_attention(qkv.data_ptr(), out.data_ptr(), work.data_ptr(), work.shape[0],
                                   n_q_heads, n_kv_heads, head_dim, qkv.stride(0), out.stride(0),
-                                  head_dim ** -0.5, kv0.data_ptr() if kv0 is not None else None,
+                                  head_dim ** -0.5 if scale is None else float(scale),
+                                  kv0.data_ptr() if kv0 is not None else None,
                                   kv0.stride(0) if kv0 is not None else 0,
                                   seg_lo.data_ptr() if seg_lo is not None else None, q_block,
                                   work2.data_ptr() if work2 is not None else None,
@@ -373,8 +374,11 @@ class HipOps:
         _chk(self.k.fls_softmax_rows(logits.data_ptr(), probs.data_ptr(), rows, V, _stream()), "fls_softmax")
         return probs
 
-    def lm_head_softmax(self, h, w):
-        return self.softmax(self.linear(h, w))
+    def lm_head_softmax(self, h, w, logits_scaling: float = 1.0):
+        logits = self.linear(h, w)
+        if logits_scaling != 1.0:                       # Granite: fp16 logits / logits_scaling
+            logits.div_(logits_scaling)
+        return self.softmax(logits)
 
     def cast_f16(self, dst: torch.Tensor, src: torch.Tensor, src_code: int) -> None:
         """dst (fp16 bytes) = fp16(src bytes of bf16 (code 1; may be in place) or fp32 (code 2))."""

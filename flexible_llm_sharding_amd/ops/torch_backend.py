@@ -118,7 +118,8 @@ class TorchOps:
         return x
 
     def attention(self, qkv: torch.Tensor, segments, n_q_heads: int, n_kv_heads: int,
-                  head_dim: int, kv0: torch.Tensor = None, q_block: int = 64, out=None) -> torch.Tensor:
+                  head_dim: int, kv0: torch.Tensor = None, q_block: int = 64, out=None,
+                  scale: float = None) -> torch.Tensor:
         """Shared-prefix attention over packed segments (see runtime.batch).
 
         ``kv0`` ([P, 2 * n_kv * hd], K then V): range 0 of every segment indexes
@@ -136,7 +137,7 @@ class TorchOps:
             k0_all, v0_all = k_all, v_all
         out = torch.empty(T, qs, dtype=qkv.dtype, device=qkv.device)
         rep = n_q_heads // n_kv_heads
-        scale = head_dim ** -0.5
+        scale = head_dim ** -0.5 if scale is None else scale
         dev = qkv.device
         for sg in segments:
             q = self._c(q_all[sg.q_start:sg.q_start + sg.q_len])                # [q, nh, d]
@@ -168,8 +169,10 @@ class TorchOps:
     def gather_rmsnorm(self, x: torch.Tensor, idx: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
         return self.rmsnorm(x.index_select(0, idx.long()), w, eps)
 
-    def lm_head_softmax(self, h: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    def lm_head_softmax(self, h: torch.Tensor, w: torch.Tensor, logits_scaling: float = 1.0) -> torch.Tensor:
         logits = (self._c(h) @ self._c(w).t()).to(h.dtype)   # fp16 logits like nn.Linear in fp16
+        if logits_scaling != 1.0:                            # Granite: logits / logits_scaling
+            logits = logits / logits_scaling
         return torch.softmax(logits.float(), dim=-1).to(torch.float16)
 
     def synchronize(self):

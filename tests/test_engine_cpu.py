@@ -278,6 +278,17 @@ def _hf_family_case(tmp_path, family):
             rope_theta=cfg.rope_theta, max_position_embeddings=cfg.max_position_embeddings,
             tie_word_embeddings=False, use_sliding_window=False, qkv_bias=True)
         model = transformers.Qwen2MoeForCausalLM(hf_cfg)
+    elif family == "granite":
+        cfg = preset("tiny-granite")
+        hf_cfg = transformers.GraniteConfig(
+            hidden_size=cfg.hidden_size, intermediate_size=cfg.intermediate_size,
+            num_attention_heads=cfg.num_attention_heads, num_key_value_heads=cfg.num_key_value_heads,
+            num_hidden_layers=cfg.num_hidden_layers, vocab_size=cfg.vocab_size, rms_norm_eps=cfg.rms_norm_eps,
+            rope_theta=cfg.rope_theta, max_position_embeddings=cfg.max_position_embeddings,
+            embedding_multiplier=cfg.embedding_multiplier, residual_multiplier=cfg.residual_multiplier,
+            attention_multiplier=cfg.attention_multiplier, logits_scaling=cfg.logits_scaling,
+            tie_word_embeddings=False)
+        model = transformers.GraniteForCausalLM(hf_cfg)
     elif family in LLAMA_VARIANTS:
         over = dict(LLAMA_VARIANTS[family])
         cfg = preset("tiny", **over)
@@ -325,13 +336,14 @@ def _hf_v5_names(cfg, sd):
 
 
 @pytest.mark.parametrize("family", ["qwen2", "qwen3", "phi3", "phi3_mini", "mistral", "mixtral", "qwen3_moe",
-                                    "qwen2_moe"] + sorted(LLAMA_VARIANTS))
+                                    "qwen2_moe", "granite"] + sorted(LLAMA_VARIANTS))
 def test_other_llama_families_match_hf(tmp_path, family):
     """Qwen2 (q/k/v biases, rope_theta 1e6), Qwen3 (per-head q/k RMSNorm, head_dim 128 on a
     256-wide residual), Phi-3 (fused qkv_proj / gate_up_proj, LongRoPE with its attention factor,
     sliding window covering the prompts), Mistral, the MoE families (Mixtral, Qwen3-MoE, Qwen2-MoE
-    with its sigmoid-gated shared expert) == HF transformers in causal mode, and == the fp32
-    oracle in the reference's bidirectional-prefix mode."""
+    with its sigmoid-gated shared expert), Granite (embedding / residual / attention multipliers,
+    logits scaling) == HF transformers in causal mode, and == the fp32 oracle in the reference's
+    bidirectional-prefix mode."""
     from flexible_llm_sharding_amd.config import ModelConfig
     path, cfg, sd, model = _hf_family_case(tmp_path, family)
     assert ModelConfig.from_pretrained(path).attention_bias == (family in ("qwen2", "qwen2_moe"))

@@ -352,13 +352,15 @@ def test_piece_pool_prefetcher_matches_slots(mid_model, monkeypatch):
 
 
 @pytest.mark.parametrize("lnps", [1, 2])
-@pytest.mark.parametrize("family", ["tiny-qwen3", "tiny-phi3", "tiny-phi3-mini"])
+@pytest.mark.parametrize("family", ["tiny-qwen3", "tiny-phi3", "tiny-phi3-mini", "tiny-granite"])
 def test_qwen3_phi3_families_on_gpu(tmp_path, lnps, family):
     """Qwen3-structured model (per-head q/k RMSNorm before RoPE: headnorm_rope_kernel after the
-    projection GEMM, head_dim 128 on a 256-wide residual) and Phi-3 (fused checkpoint tensors,
+    projection GEMM, head_dim 128 on a 256-wide residual), Phi-3 (fused checkpoint tensors,
     LongRoPE tables with attention factor 1.19 through the fused RoPE epilogue; Phi-3-mini's
-    head_dim 96: projection GEMM + RoPE pass, 12-chunk attention tiles) vs the fp32
-    oracle, incl. the pruned last layer (K/V for all rows, Q for the scored rows)."""
+    head_dim 96: projection GEMM + RoPE pass, 12-chunk attention tiles) and Granite (the
+    attention kernel's softmax scale = attention_multiplier, unfused scaled residuals, scaled
+    embeddings and logits) vs the fp32 oracle, incl. the pruned last layer (K/V for all rows, Q
+    for the scored rows)."""
     from flexible_llm_sharding_amd.config import preset
     from flexible_llm_sharding_amd.utils.synthetic import write_synthetic_checkpoint
     cfg = preset(family)
