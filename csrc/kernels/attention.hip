@@ -42,6 +42,10 @@
 namespace {
 
 constexpr int KT = 64;                 // keys per tile
+// range-2 one-wave-per-head kernel with two K/V register sets (DEEP in attn_fwd): 0 off (default),
+// 1 on (A/B).  Same-box 70B generation traces: the kernel 4.5-4.7 vs 4.6-4.8 ms per step, the step's
+// wall time no better (profiles/r4_gen/attn_deep)
+int g_deep = 0;
 constexpr float DEFER_LOG2 = 8.0f;     // deferred-rescale threshold (log2 units)
 
 template <int HD>
@@ -96,7 +100,7 @@ __device__ __forceinline__ unsigned pack_h2(float a, float b) {
 // tiles and writes its unnormalised O, running max and row sum in fp32 to `part`
 // ([rows][splits][nh] x (HD + 2)); attn_split_combine merges the slices.  For grids with fewer
 // blocks than CUs (few prompts with long contexts), which otherwise leave most CUs idle.
-template <int HD, int HPB, int WPH, bool R2, bool SPL = false>
+template <int HD, int HPB, int WPH, bool R2, bool SPL = false, bool DEEP_ = false>
 __global__ __launch_bounds__(64 * WPH * HPB, 2) void attn_fwd(const half_t* __restrict__ qkv, half_t* __restrict__ out,
                                                     const int* __restrict__ work, const int* __restrict__ seg_lo,
                                                     int nh, int nkv, int ld_qkv, int ld_out, float scale_log2,
@@ -193,7 +197,12 @@ __global__ __launch_bounds__(64 * WPH * HPB, 2) void attn_fwd(const half_t* __re
   float m_run[2] = {-1e30f, -1e30f};        // raw-score domain
   float l_run[2] = {0.f, 0.f};
 
+  // DEEP (the one-wave-per-head range-2 kernel of a generation step: few keys per query, so a
+  // tile's math is short against the HBM latency of the next): two register sets, tile t + 2's
+  // loads issued one tile earlier, so they have two tiles' math to land instead of one
+  constexpr bool DEEP = DEEP_ && R2 && WPH == 1 && HPB == 8;   // (at HPB 4 the second set spills)
   u32x4 pk[PER], pv[PER];
+  u32x4 pk1[PER], pv1[PER];                 // DEEP's second set (dead code otherwise)
   // tile loader: by-reference captures for the plain kernel (its tuned code), by-value for R2 (whose
   // three-range selects otherwise keep the captured locals in scratch memory)
 #define FLS_ATTN_LOAD_TILE_BODY \
@@ -210,41 +219,42 @@ _Pragma("unroll") \
       const int c = tid + i * NT_; \
       const int row = c / CH, ch = c % CH; \
       const unsigned off = (unsigned)((rb + min(k0 + row, klen - 1)) * ldk + ch * 8) * 2u; \
-      pk[i] = __builtin_amdgcn_raw_buffer_load_b128(r, off, kc, 0); \
-      pv[i] = __builtin_amdgcn_raw_buffer_load_b128(r, off, vc, 0); \
+      K_[i] = __builtin_amdgcn_raw_buffer_load_b128(r, off, kc, 0); \
+      V_[i] = __builtin_amdgcn_raw_buffer_load_b128(r, off, vc, 0); \
     }
-  auto load_tile_ref = [&](int t) { FLS_ATTN_LOAD_TILE_BODY };
-  auto load_tile_val = [=, &pk, &pv](int t) { FLS_ATTN_LOAD_TILE_BODY };
+  auto load_tile_ref = [&](int t) { u32x4(&K_)[PER] = pk; u32x4(&V_)[PER] = pv; FLS_ATTN_LOAD_TILE_BODY };
+  auto load_tile_val = [=, &pk, &pv](int t) { u32x4(&K_)[PER] = pk; u32x4(&V_)[PER] = pv; FLS_ATTN_LOAD_TILE_BODY };
+  auto load_tile_set1 = [=, &pk1, &pv1](int t) __attribute__((always_inline)) {
+    u32x4(&K_)[PER] = pk1;
+    u32x4(&V_)[PER] = pv1;
+    FLS_ATTN_LOAD_TILE_BODY
+  };
 #undef FLS_ATTN_LOAD_TILE_BODY
   auto load_tile = [&](int t) {
     if constexpr (R2) load_tile_val(t);
     else load_tile_ref(t);
   };
-  auto store_tile = [&](int buf) {
+  auto store_set = [&](int buf, const u32x4(&K_)[PER], const u32x4(&V_)[PER]) __attribute__((always_inline)) {
     char* Ks = smem + buf * TILE_BYTES;
     char* Vs = Ks + KT * HD * 2;
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int c = tid + i * NT_;
       const int row = c / CH, ch = c % CH;
-      *(u32x4*)(Ks + Lds<HD>::k_off(row, ch)) = pk[i];
-      *(u32x4*)(Vs + Lds<HD>::v_off(row, ch)) = pv[i];
+      *(u32x4*)(Ks + Lds<HD>::k_off(row, ch)) = K_[i];
+      *(u32x4*)(Vs + Lds<HD>::v_off(row, ch)) = V_[i];
     }
   };
+  auto store_tile = [&](int buf) { store_set(buf, pk, pv); };
 
-  if (t_hi > t_lo) {
-    load_tile(t_lo);
-    store_tile(t_lo & 1);
-    if (t_hi > t_lo + 1) load_tile(t_lo + 1);
-  }
-  __syncthreads();
-  for (int t = t_lo; t < t_hi; ++t) {
-    const bool r1 = t >= n02;
-    const bool r2 = R2 && !r1 && t >= n0;
-    const int k0 = (r1 ? t - n02 : (r2 ? t - n0 : t)) * KT;
-    const int klen = r1 ? r_len1 : (r2 ? r_len2 : r_len0);
-    const bool causal = r1 || (!r2 && r_causal0);
-    const char* Ks = smem + (t & 1) * TILE_BYTES;
+  // per-tile key range of tile t
+#define FLS_ATTN_TILE_PRE \
+    const bool r1 = t >= n02; \
+    const bool r2 = R2 && !r1 && t >= n0; \
+    const int k0 = (r1 ? t - n02 : (r2 ? t - n0 : t)) * KT; \
+    const int klen = r1 ? r_len1 : (r2 ? r_len2 : r_len0); \
+    const bool causal = r1 || (!r2 && r_causal0); \
+    const char* Ks = smem + (t & 1) * TILE_BYTES; \
     const char* Vs = Ks + KT * HD * 2;
 
     // the tile's math for the wave's first NQ 16-row query groups (NQ = 2: the whole wave)
@@ -337,6 +347,15 @@ _Pragma("unroll") \
         if constexpr (NQ > 1) o[1][u] = mfma16x16x32(vf, pf[1][ks], o[1][u]); \
       } \
     }
+  if constexpr (!DEEP) {
+  if (t_hi > t_lo) {
+    load_tile(t_lo);
+    store_tile(t_lo & 1);
+    if (t_hi > t_lo + 1) load_tile(t_lo + 1);
+  }
+  __syncthreads();
+  for (int t = t_lo; t < t_hi; ++t) {
+    FLS_ATTN_TILE_PRE
     if constexpr (!R2) {
       constexpr int NQ = 2;
       FLS_ATTN_TILE_MATH
@@ -350,13 +369,53 @@ _Pragma("unroll") \
       if (live_rows > 16) tile_math(IC<2>{});
       else if (live_rows > 0) tile_math(IC<1>{});
     }
-#undef FLS_ATTN_TILE_MATH
     if (t + 1 < t_hi) {
       store_tile((t + 1) & 1);               // the other buffer's readers (tile t-1) passed the last barrier
       if (t + 2 < t_hi) load_tile(t + 2);    // in flight under tile t+1's MFMAs
     }
     __syncthreads();
   }
+  } else {
+    // tile j (> t_lo) is staged in set (j - t_lo - 1) & 1: set 0 holds t_lo + 1, set 1 t_lo + 2
+#define FLS_ATTN_DEEP_MATH(T_)                                                                     \
+  {                                                                                                \
+    const int t_cur_ = (T_); /* (T_ may name the loop's t) */                                      \
+    const int t = t_cur_;                                                                          \
+    FLS_ATTN_TILE_PRE                                                                              \
+    auto tile_math = [&](auto nq_c) {                                                              \
+      constexpr int NQ = decltype(nq_c)::value;                                                    \
+      FLS_ATTN_TILE_MATH                                                                           \
+    };                                                                                             \
+    if (live_rows > 16) tile_math(IC<2>{});                                                        \
+    else if (live_rows > 0) tile_math(IC<1>{});                                                    \
+  }
+    if (t_hi > t_lo) {
+      load_tile_val(t_lo);
+      store_tile(t_lo & 1);
+      if (t_hi > t_lo + 1) load_tile_val(t_lo + 1);
+      if (t_hi > t_lo + 2) load_tile_set1(t_lo + 2);
+    }
+    __syncthreads();
+    for (int t = t_lo; t < t_hi; t += 2) {
+      FLS_ATTN_DEEP_MATH(t)
+      if (t + 1 < t_hi) {
+        store_set((t + 1) & 1, pk, pv);      // tile t + 1 (set 0); its buffer's readers passed the barrier
+        if (t + 3 < t_hi) load_tile_val(t + 3);
+      }
+      __syncthreads();
+      if (t + 1 < t_hi) {
+        FLS_ATTN_DEEP_MATH(t + 1)
+        if (t + 2 < t_hi) {
+          store_set(t & 1, pk1, pv1);        // tile t + 2 (set 1)
+          if (t + 4 < t_hi) load_tile_set1(t + 4);
+        }
+        __syncthreads();
+      }
+    }
+  }
+#undef FLS_ATTN_DEEP_MATH
+#undef FLS_ATTN_TILE_PRE
+#undef FLS_ATTN_TILE_MATH
   // ---- normalise and store (split: the slice's fp32 partials)
 #pragma unroll
   for (int qg = 0; qg < 2; ++qg) {
@@ -417,19 +476,20 @@ int launch(int hpb, dim3 grid, hipStream_t st, const half_t* qkv, half_t* out, c
   if constexpr (R2 && HD != 96) {
     if (ns > 1) {
       const dim3 g3(grid.x, grid.y, ns);
-#define FLS_ATTN_LAUNCH_SPL(HPB_)                                                                              \
-  hipLaunchKernelGGL((attn_fwd<HD, HPB_, WPH, true, true>), g3, dim3(64 * WPH * HPB_), 0, st, qkv, out, work, seg_lo, \
+#define FLS_ATTN_LAUNCH_SPL(HPB_, D_)                                                                          \
+  hipLaunchKernelGGL((attn_fwd<HD, HPB_, WPH, true, true, D_>), g3, dim3(64 * WPH * HPB_), 0, st, qkv, out, work, seg_lo, \
                      nh, nkv, ld_qkv, ld_out, scale_log2, kv0, ld_kv0, work2, r2win, part)
       if constexpr (WPH == 1) {
-        if (hpb == 8) FLS_ATTN_LAUNCH_SPL(8);
-        else FLS_ATTN_LAUNCH_SPL(4);
+        if (hpb == 8 && g_deep) FLS_ATTN_LAUNCH_SPL(8, true);
+        else if (hpb == 8) FLS_ATTN_LAUNCH_SPL(8, false);
+        else FLS_ATTN_LAUNCH_SPL(4, false);
       } else if constexpr (WPH == 2) {
-        if (hpb == 4) FLS_ATTN_LAUNCH_SPL(4);
-        else if (hpb == 2) FLS_ATTN_LAUNCH_SPL(2);
-        else FLS_ATTN_LAUNCH_SPL(1);
+        if (hpb == 4) FLS_ATTN_LAUNCH_SPL(4, false);
+        else if (hpb == 2) FLS_ATTN_LAUNCH_SPL(2, false);
+        else FLS_ATTN_LAUNCH_SPL(1, false);
       } else {
-        if (hpb == 2) FLS_ATTN_LAUNCH_SPL(2);
-        else FLS_ATTN_LAUNCH_SPL(1);
+        if (hpb == 2) FLS_ATTN_LAUNCH_SPL(2, false);
+        else FLS_ATTN_LAUNCH_SPL(1, false);
       }
 #undef FLS_ATTN_LAUNCH_SPL
       FLS_CHECK_LAUNCH();
@@ -444,6 +504,14 @@ int launch(int hpb, dim3 grid, hipStream_t st, const half_t* qkv, half_t* out, c
   if constexpr (HD == 96) {
     FLS_ATTN_LAUNCH(1);                     // 12 chunks per row: one head per block divides the tile
   } else if constexpr (WPH == 1) {          // 4 or 8 heads (dispatch)
+    if constexpr (R2) {
+      if (hpb == 8 && g_deep) {
+        hipLaunchKernelGGL((attn_fwd<HD, 8, 1, true, false, true>), grid, dim3(64 * 8), 0, st, qkv, out, work, seg_lo,
+                           nh, nkv, ld_qkv, ld_out, scale_log2, kv0, ld_kv0, work2, r2win, nullptr);
+        FLS_CHECK_LAUNCH();
+        return 0;
+      }
+    }
     if (hpb == 8) FLS_ATTN_LAUNCH(8);
     else FLS_ATTN_LAUNCH(4);
   } else if constexpr (WPH == 2) {
@@ -469,6 +537,12 @@ int g_split = 0; // split-KV slices of the range-2 kernel: 0 = by grid size, 1 =
 extern "C" int fls_attention_set_hpb(int hpb) {
   const int old = g_hpb;
   g_hpb = hpb;
+  return old;
+}
+
+extern "C" int fls_attention_set_deep(int on) {
+  const int old = g_deep;
+  g_deep = on ? 1 : 0;
   return old;
 }
 

@@ -63,7 +63,7 @@ class Piece(ctypes.Structure):
                 ("kind", ctypes.c_int32), ("pad", ctypes.c_int32)]
 
 
-KERNELS_ABI = 19   # bumped whenever a C signature in csrc/include/fls.h changes
+KERNELS_ABI = 20   # bumped whenever a C signature in csrc/include/fls.h changes
 
 
 def _load_kernels(path: str = _KERNELS):
@@ -99,6 +99,7 @@ def _load_kernels(path: str = _KERNELS):
     _bind(lib, "fls_gemm_v11_tune", None, c_int, c_int)
     _bind(lib, "fls_attention_set_hpb", c_int, c_int)
     _bind(lib, "fls_attention_set_split", c_int, c_int)
+    _bind(lib, "fls_attention_set_deep", c_int, c_int)
     _bind(lib, "fls_attention", c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
           c_int, c_int, c_float, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_uint64, c_int,
           c_void_p)

@@ -79,6 +79,8 @@ class HipOps:
             self.k.fls_gemm_set_skinny_bn(int(os.environ["FLS_SKINNY_BN"]))
         if os.environ.get("FLS_ATTN_SPLIT"):              # split-KV slices of the range-2 kernel (A/B)
             self.k.fls_attention_set_split(int(os.environ["FLS_ATTN_SPLIT"]))
+        if os.environ.get("FLS_ATTN_DEEP"):               # range-2 two-register-set K/V staging: 0 off (default), 1 on
+            self.k.fls_attention_set_deep(int(os.environ["FLS_ATTN_DEEP"]))
 
     # ---------------------------------------------------------------- GEMM
     def gemm(self, x: torch.Tensor, w: torch.Tensor, epi: int = EPI_NONE, out: torch.Tensor = None,
