@@ -142,6 +142,9 @@ class ModelConfig:
             raise ValueError("head_dim must be a multiple of 32 (RoPE pair blocks of 16)")
         if self.is_moe and not 1 <= self.num_experts_per_tok <= min(self.num_local_experts, MAX_TOP_K):
             raise ValueError(f"num_experts_per_tok must be in 1..min(num_local_experts, {MAX_TOP_K})")
+        if self.is_moe and self.residual_multiplier != 1.0:
+            # the MoE combine kernel adds the experts' sum to the residual unscaled
+            raise NotImplementedError("residual_multiplier with a mixture-of-experts MLP")
         if self.num_local_experts > MAX_EXPERTS:
             raise NotImplementedError(f"num_local_experts={self.num_local_experts} > {MAX_EXPERTS}")
         rs = self.rope_scaling
