@@ -81,6 +81,8 @@ class HipOps:
             self.k.fls_attention_set_split(int(os.environ["FLS_ATTN_SPLIT"]))
         if os.environ.get("FLS_ATTN_DEEP"):               # range-2 two-register-set K/V staging: 0 off (default), 1 on
             self.k.fls_attention_set_deep(int(os.environ["FLS_ATTN_DEEP"]))
+        if os.environ.get("FLS_ATTN_DMA"):                # range-2 LDS-DMA K/V ring (8-head blocks): 0 off (default), 1 on
+            self.k.fls_attention_set_dma(int(os.environ["FLS_ATTN_DMA"]))
 
     # ---------------------------------------------------------------- GEMM
     def gemm(self, x: torch.Tensor, w: torch.Tensor, epi: int = EPI_NONE, out: torch.Tensor = None,

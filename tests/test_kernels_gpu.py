@@ -456,6 +456,12 @@ def test_attention_suffix_rows_from_cache(ops, ref, nh, nkv, hd, split, q_block)
     old = ops.k.fls_attention_set_split(split)
     try:
         _suffix_rows_from_cache(ops, ref, nh, nkv, hd, q_block=q_block)
+        if q_block == 32 and split == 1:         # the LDS-DMA ring variant (8-head blocks, hd 128)
+            old_dma = ops.k.fls_attention_set_dma(1)
+            try:
+                _suffix_rows_from_cache(ops, ref, nh, nkv, hd, q_block=q_block)
+            finally:
+                ops.k.fls_attention_set_dma(old_dma)
     finally:
         ops.k.fls_attention_set_split(old)
 
@@ -487,6 +493,15 @@ def test_attention_decode_split_matches_unsplit(ops, ref):
         ops.k.fls_attention_set_deep(old)
         ops.k.fls_attention_set_split(old_split)
     assert torch.equal(two_sets, ys[2])
+    # ... with the K/V tiles staged by LDS-DMA into a 4-tile ring (FLS_ATTN_DMA=1)
+    old = ops.k.fls_attention_set_dma(1)
+    old_split = ops.k.fls_attention_set_split(1)
+    try:
+        dma = _suffix_rows_from_cache(ops, ref, 64, 8, 128, prompts, keep, q_block=32)
+    finally:
+        ops.k.fls_attention_set_dma(old)
+        ops.k.fls_attention_set_split(old_split)
+    assert torch.equal(dma, ys[2])
 
 
 def _suffix_rows_from_cache(ops, ref, nh, nkv, hd, prompts=None, keep=None, q_block=64):
