@@ -402,7 +402,7 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
     FLS_CHECK_LAUNCH();
     return 0;
   }
-  if (mid_ok && (!main_ok || (g_mid && (tiles256 < 128 || (M <= 64 && tiles256 < 512))))) {
+  if (mid_ok && (!main_ok || g_mid == 2 || (g_mid && (tiles256 < 128 || (M <= 64 && tiles256 < 512))))) {
     static bool attr_mid = false;
     if (!attr_mid) {
       (void)hipFuncSetAttribute((const void*)gemm_nt_mid<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -502,9 +502,9 @@ extern "C" int fls_gemm_set_gu_split(int p) {
 }
 
 // mid-M kernel for small grids on (1, default) or off (0; tests)
-extern "C" int fls_gemm_set_mid(int on) {
+extern "C" int fls_gemm_set_mid(int on) {   // 0 off, 1 auto, 2 forced wherever it applies (A/B)
   const int old = g_mid;
-  g_mid = on ? 1 : 0;
+  g_mid = on < 0 ? 0 : on > 2 ? 2 : on;
   return old;
 }
 

@@ -249,8 +249,12 @@ int try_skinny(const half_t* A, const half_t* W, half_t* C, int M, int N, int K,
   const int nkt = K / sk::KT;
   // auto: the measured range (profiles/r4_gen, 70B shapes): M 17..192 on the narrow projections;
   // the wide gate/up GEMM (N / 128 >= 256 blocks, 224 main-path tiles) runs faster on the main
-  // path at every M measured (64 / 160 / 256 rows: 175 / 209 / 221 us vs 195 / 246 / 332)
-  if (g_skinny == 1 && (M < 17 || M > 192 || N / 128 >= 256)) return 0;
+  // path at M = 64 / 160 / 256 (175 / 209 / 221 us vs 195 / 246 / 332 with 128-row blocks), but at
+  // 65..144 rows the 256-row block without a K split beats it (same box, M = 96 / 112 / 128 / 144:
+  // 180 / 182 / 184 / 199 us vs 216 / 205 / 199 / 206; profiles/r4_gen/gateup_mid_m)
+  const bool wide = N / 128 >= 256;
+  const bool wide_bn256 = wide && M > 64 && M <= 144 && N % 256 == 0;
+  if (g_skinny == 1 && (M < 17 || M > 192 || (wide && !wide_bn256))) return 0;
   // K slices.  BN = 128: the fewest that give whole 256-CU rounds or at least two rounds (one
   // block per CU: a fractional single round leaves a tail of full-K blocks; 70B at M = 160: O /
   // down S = 4, QKV S = 8 measured fastest).  BN = 256: the fewest that give 192 blocks (3/4 of
@@ -272,7 +276,9 @@ int try_skinny(const half_t* A, const half_t* W, half_t* C, int M, int N, int K,
   // run slower with it (profiles/r4_gen/bn256/skinny_ab.log)
   const bool bn256_ok = N % 256 == 0 && rs <= SK_BN256_MAX_RS;
   int bn = 128;
-  if (bn256_ok && (g_skinny_bn == 256 || (g_skinny_bn == 0 && (long)(N / 256) * slices(256) % 256 == 0))) bn = 256;
+  if (bn256_ok && (g_skinny_bn == 256 ||
+                   (g_skinny_bn == 0 && (wide_bn256 || (long)(N / 256) * slices(256) % 256 == 0))))
+    bn = 256;
   const int S = slices(bn);
   const bool direct_epi = EPI == FLS_EPI_NONE || EPI == FLS_EPI_RESID || EPI == FLS_EPI_SWIGLU;
   const bool direct = S == 1 && direct_epi;
