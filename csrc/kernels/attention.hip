@@ -42,12 +42,6 @@
 namespace {
 
 constexpr int KT = 64;                 // keys per tile
-// range-2 one-wave-per-head kernel with two K/V register sets (DEEP in attn_fwd): 0 off (default),
-// 1 on (A/B).  Same-box 70B generation traces: the kernel 4.5-4.7 vs 4.6-4.8 ms per step, the step's
-// wall time no better (profiles/r4_gen/attn_deep)
-int g_deep = 0;
-// range-2 8-head kernel with LDS-DMA K/V staging (DMA in attn_fwd): 0 off (default), 1 on (A/B)
-int g_dma = 0;
 constexpr float DEFER_LOG2 = 8.0f;     // deferred-rescale threshold (log2 units)
 
 template <int HD>
@@ -94,14 +88,6 @@ struct IC {
 typedef _Float16 half2_ __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-// ds_read_b64_tr_b16 as asm: the caller waits lgkmcnt itself (DMA variant of attn_fwd)
-__device__ __forceinline__ half4 ds_read_tr16_asm(const void* lds_addr) {
-  half4 r;
-  const unsigned a = (unsigned)(size_t)((LDS_AS const char*)lds_addr);
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
-  return r;
-}
-
 __device__ __forceinline__ unsigned pack_h2(float a, float b) {
   return __builtin_bit_cast(unsigned, __builtin_convertvector(float2_{a, b}, half2_));
 }
@@ -110,7 +96,7 @@ __device__ __forceinline__ unsigned pack_h2(float a, float b) {
 // tiles and writes its unnormalised O, running max and row sum in fp32 to `part`
 // ([rows][splits][nh] x (HD + 2)); attn_split_combine merges the slices.  For grids with fewer
 // blocks than CUs (few prompts with long contexts), which otherwise leave most CUs idle.
-template <int HD, int HPB, int WPH, bool R2, bool SPL = false, bool DEEP_ = false, bool DMA_ = false>
+template <int HD, int HPB, int WPH, bool R2, bool SPL = false>
 __global__ __launch_bounds__(64 * WPH * HPB, 2) void attn_fwd(const half_t* __restrict__ qkv, half_t* __restrict__ out,
                                                     const int* __restrict__ work, const int* __restrict__ seg_lo,
                                                     int nh, int nkv, int ld_qkv, int ld_out, float scale_log2,
@@ -125,11 +111,7 @@ __global__ __launch_bounds__(64 * WPH * HPB, 2) void attn_fwd(const half_t* __re
   constexpr int PER = KT * CH / NT_;        // chunks per thread per operand
   static_assert(PER >= 1 && (KT * CH) % NT_ == 0, "tile / block mismatch");
   constexpr int TILE_BYTES = 2 * KT * HD * 2;         // K + V
-  // DMA (A/B variant of the 8-head range-2 kernel): K/V tiles staged by buffer_load ... lds into a
-  // ring of NSTG tiles, NSTG - 1 in flight behind one counted vmcnt + raw barrier per tile
-  constexpr bool DMA = DMA_ && R2 && WPH == 1 && HPB == 8 && !SPL && HD == 128;
-  constexpr int NSTG = DMA ? 4 : 2;
-  __shared__ __attribute__((aligned(16))) char smem[NSTG * TILE_BYTES];
+  __shared__ __attribute__((aligned(16))) char smem[2 * TILE_BYTES];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -211,12 +193,7 @@ __global__ __launch_bounds__(64 * WPH * HPB, 2) void attn_fwd(const half_t* __re
   float m_run[2] = {-1e30f, -1e30f};        // raw-score domain
   float l_run[2] = {0.f, 0.f};
 
-  // DEEP (the one-wave-per-head range-2 kernel of a generation step: few keys per query, so a
-  // tile's math is short against the HBM latency of the next): two register sets, tile t + 2's
-  // loads issued one tile earlier, so they have two tiles' math to land instead of one
-  constexpr bool DEEP = DEEP_ && R2 && WPH == 1 && HPB == 8;   // (at HPB 4 the second set spills)
   u32x4 pk[PER], pv[PER];
-  u32x4 pk1[PER], pv1[PER];                 // DEEP's second set (dead code otherwise)
   // tile loader: by-reference captures for the plain kernel (its tuned code), by-value for R2 (whose
   // three-range selects otherwise keep the captured locals in scratch memory)
 #define FLS_ATTN_LOAD_TILE_BODY \
@@ -238,28 +215,22 @@ _Pragma("unroll") \
     }
   auto load_tile_ref = [&](int t) { u32x4(&K_)[PER] = pk; u32x4(&V_)[PER] = pv; FLS_ATTN_LOAD_TILE_BODY };
   auto load_tile_val = [=, &pk, &pv](int t) { u32x4(&K_)[PER] = pk; u32x4(&V_)[PER] = pv; FLS_ATTN_LOAD_TILE_BODY };
-  auto load_tile_set1 = [=, &pk1, &pv1](int t) __attribute__((always_inline)) {
-    u32x4(&K_)[PER] = pk1;
-    u32x4(&V_)[PER] = pv1;
-    FLS_ATTN_LOAD_TILE_BODY
-  };
 #undef FLS_ATTN_LOAD_TILE_BODY
   auto load_tile = [&](int t) {
     if constexpr (R2) load_tile_val(t);
     else load_tile_ref(t);
   };
-  auto store_set = [&](int buf, const u32x4(&K_)[PER], const u32x4(&V_)[PER]) __attribute__((always_inline)) {
+  auto store_tile = [&](int buf) {
     char* Ks = smem + buf * TILE_BYTES;
     char* Vs = Ks + KT * HD * 2;
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int c = tid + i * NT_;
       const int row = c / CH, ch = c % CH;
-      *(u32x4*)(Ks + Lds<HD>::k_off(row, ch)) = K_[i];
-      *(u32x4*)(Vs + Lds<HD>::v_off(row, ch)) = V_[i];
+      *(u32x4*)(Ks + Lds<HD>::k_off(row, ch)) = pk[i];
+      *(u32x4*)(Vs + Lds<HD>::v_off(row, ch)) = pv[i];
     }
   };
-  auto store_tile = [&](int buf) { store_set(buf, pk, pv); };
 
   // per-tile key range of tile t
 #define FLS_ATTN_TILE_PRE \
@@ -268,7 +239,7 @@ _Pragma("unroll") \
     const int k0 = (r1 ? t - n02 : (r2 ? t - n0 : t)) * KT; \
     const int klen = r1 ? r_len1 : (r2 ? r_len2 : r_len0); \
     const bool causal = r1 || (!r2 && r_causal0); \
-    const char* Ks = smem + (DMA ? (t - t_lo) % NSTG : (t & 1)) * TILE_BYTES; \
+    const char* Ks = smem + (t & 1) * TILE_BYTES; \
     const char* Vs = Ks + KT * HD * 2;
 
     // the tile's math for the wave's first NQ 16-row query groups (NQ = 2: the whole wave)
@@ -351,26 +322,6 @@ _Pragma("unroll") \
     for (int ks = 0; ks < 2; ++ks) { \
       const int row_a = ks * 32 + grp * 4 + q4; \
       const int row_b = row_a + 16; \
-      if constexpr (DMA) { \
-        /* asm reads (a builtin LDS read makes the compiler drain the LDS-DMA queue, vmcnt(0)), */ \
-        /* then one lgkmcnt wait that also orders the MFMAs after the data */ \
-        half4 va_[NU], vb_[NU]; \
-_Pragma("unroll") \
-        for (int u = 0; u < NU; ++u) { \
-          const int ch = u * 2 + (p4 >> 1); \
-          va_[u] = ds_read_tr16_asm(Vs + Lds<HD>::v_off(row_a, ch) + (p4 & 1) * 8); \
-          vb_[u] = ds_read_tr16_asm(Vs + Lds<HD>::v_off(row_b, ch) + (p4 & 1) * 8); \
-        } \
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(va_[0]), "+v"(vb_[0]), "+v"(va_[1]), "+v"(vb_[1]), \
-                     "+v"(va_[2]), "+v"(vb_[2]), "+v"(va_[3]), "+v"(vb_[3]), "+v"(va_[4]), "+v"(vb_[4]), \
-                     "+v"(va_[5]), "+v"(vb_[5]), "+v"(va_[6]), "+v"(vb_[6]), "+v"(va_[7]), "+v"(vb_[7])); \
-_Pragma("unroll") \
-        for (int u = 0; u < NU; ++u) { \
-          const half8 vf = {va_[u][0], va_[u][1], va_[u][2], va_[u][3], vb_[u][0], vb_[u][1], vb_[u][2], vb_[u][3]}; \
-          o[0][u] = mfma16x16x32(vf, pf[0][ks], o[0][u]); \
-          if constexpr (NQ > 1) o[1][u] = mfma16x16x32(vf, pf[1][ks], o[1][u]); \
-        } \
-      } else { \
 _Pragma("unroll") \
       for (int u = 0; u < NU; ++u) { \
         const int ch = u * 2 + (p4 >> 1); \
@@ -380,56 +331,7 @@ _Pragma("unroll") \
         o[0][u] = mfma16x16x32(vf, pf[0][ks], o[0][u]); \
         if constexpr (NQ > 1) o[1][u] = mfma16x16x32(vf, pf[1][ks], o[1][u]); \
       } \
-      } \
     }
-#define FLS_ATTN_DEEP_MATH(T_)                                                                     \
-  {                                                                                                \
-    const int t_cur_ = (T_); /* (T_ may name the loop's t) */                                      \
-    const int t = t_cur_;                                                                          \
-    FLS_ATTN_TILE_PRE                                                                              \
-    auto tile_math = [&](auto nq_c) {                                                              \
-      constexpr int NQ = decltype(nq_c)::value;                                                    \
-      FLS_ATTN_TILE_MATH                                                                           \
-    };                                                                                             \
-    if (live_rows > 16) tile_math(IC<2>{});                                                        \
-    else if (live_rows > 0) tile_math(IC<1>{});                                                    \
-  }
-  if constexpr (DMA) {
-    // tile t -> stage (t - t_lo) % NSTG.  Lane l of wave w's i-th DMA fills LDS chunk
-    // q = (8 i + w) * 64 + l of the K (V) image, i.e. row q / 16, slot q % 16, which holds source
-    // chunk slot ^ the row's swizzle (Lds<HD>::k_off / v_off read it back).  Rows are clamped into
-    // the item's range (DMA only runs for items with key tiles).
-    auto dma_tile = [=](int t, int st) {
-      const bool r2 = t >= n0;
-      const int k0 = (r2 ? t - n0 : t) * KT;
-      const int klen = r2 ? r_len2 : r_len0;
-      const int rb = r2 ? r2base : 0;
-      char* Kb = smem + st * TILE_BYTES;
-      char* Vb = Kb + KT * HD * 2;
-#pragma unroll
-      for (int i = 0; i < PER; ++i) {
-        const int q = (i * 8 + wave) * 64 + lane;
-        const int row = q / CH, slot = q % CH;
-        const half_t* rp = kv0 + (size_t)(r_start0 + rb + max(min(k0 + row, klen - 1), 0)) * ld0;
-        glds16(rp + kc0 + (slot ^ (row & Lds<HD>::KM)) * 8, Kb + (i * 8 + wave) * 1024);
-        glds16(rp + vc0 + (slot ^ ((row & Lds<HD>::VM) << 1)) * 8, Vb + (i * 8 + wave) * 1024);
-      }
-    };
-    constexpr int DIST = NSTG - 1;
-    // never conditional (a tile past the end re-reads the last one into a stage nobody reads), so
-    // the count each wait allows is one constant
-    if (t_hi > t_lo) {
-#pragma unroll
-      for (int d = 0; d < DIST; ++d) dma_tile(min(t_lo + d, t_hi - 1), d);
-    }
-    for (int t = t_lo; t < t_hi; ++t) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((DIST - 1) * 2 * PER) : "memory");
-      __builtin_amdgcn_s_barrier();          // tile t landed for every wave; every wave is past t - 1
-      dma_tile(min(t + DIST, t_hi - 1), (t - t_lo + DIST) % NSTG);
-      FLS_ATTN_DEEP_MATH(t)
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the tail's redundant DMA lands before exit
-  } else if constexpr (!DEEP) {
   if (t_hi > t_lo) {
     load_tile(t_lo);
     store_tile(t_lo & 1);
@@ -457,33 +359,6 @@ _Pragma("unroll") \
     }
     __syncthreads();
   }
-  } else {
-    // tile j (> t_lo) is staged in set (j - t_lo - 1) & 1: set 0 holds t_lo + 1, set 1 t_lo + 2
-    if (t_hi > t_lo) {
-      load_tile_val(t_lo);
-      store_tile(t_lo & 1);
-      if (t_hi > t_lo + 1) load_tile_val(t_lo + 1);
-      if (t_hi > t_lo + 2) load_tile_set1(t_lo + 2);
-    }
-    __syncthreads();
-    for (int t = t_lo; t < t_hi; t += 2) {
-      FLS_ATTN_DEEP_MATH(t)
-      if (t + 1 < t_hi) {
-        store_set((t + 1) & 1, pk, pv);      // tile t + 1 (set 0); its buffer's readers passed the barrier
-        if (t + 3 < t_hi) load_tile_val(t + 3);
-      }
-      __syncthreads();
-      if (t + 1 < t_hi) {
-        FLS_ATTN_DEEP_MATH(t + 1)
-        if (t + 2 < t_hi) {
-          store_set(t & 1, pk1, pv1);        // tile t + 2 (set 1)
-          if (t + 4 < t_hi) load_tile_set1(t + 4);
-        }
-        __syncthreads();
-      }
-    }
-  }
-#undef FLS_ATTN_DEEP_MATH
 #undef FLS_ATTN_TILE_PRE
 #undef FLS_ATTN_TILE_MATH
   // ---- normalise and store (split: the slice's fp32 partials)
@@ -546,20 +421,19 @@ int launch(int hpb, dim3 grid, hipStream_t st, const half_t* qkv, half_t* out, c
   if constexpr (R2 && HD != 96) {
     if (ns > 1) {
       const dim3 g3(grid.x, grid.y, ns);
-#define FLS_ATTN_LAUNCH_SPL(HPB_, D_)                                                                          \
-  hipLaunchKernelGGL((attn_fwd<HD, HPB_, WPH, true, true, D_>), g3, dim3(64 * WPH * HPB_), 0, st, qkv, out, work, seg_lo, \
+#define FLS_ATTN_LAUNCH_SPL(HPB_)                                                                              \
+  hipLaunchKernelGGL((attn_fwd<HD, HPB_, WPH, true, true>), g3, dim3(64 * WPH * HPB_), 0, st, qkv, out, work, seg_lo, \
                      nh, nkv, ld_qkv, ld_out, scale_log2, kv0, ld_kv0, work2, r2win, part)
       if constexpr (WPH == 1) {
-        if (hpb == 8 && g_deep) FLS_ATTN_LAUNCH_SPL(8, true);
-        else if (hpb == 8) FLS_ATTN_LAUNCH_SPL(8, false);
-        else FLS_ATTN_LAUNCH_SPL(4, false);
+        if (hpb == 8) FLS_ATTN_LAUNCH_SPL(8);
+        else FLS_ATTN_LAUNCH_SPL(4);
       } else if constexpr (WPH == 2) {
-        if (hpb == 4) FLS_ATTN_LAUNCH_SPL(4, false);
-        else if (hpb == 2) FLS_ATTN_LAUNCH_SPL(2, false);
-        else FLS_ATTN_LAUNCH_SPL(1, false);
+        if (hpb == 4) FLS_ATTN_LAUNCH_SPL(4);
+        else if (hpb == 2) FLS_ATTN_LAUNCH_SPL(2);
+        else FLS_ATTN_LAUNCH_SPL(1);
       } else {
-        if (hpb == 2) FLS_ATTN_LAUNCH_SPL(2, false);
-        else FLS_ATTN_LAUNCH_SPL(1, false);
+        if (hpb == 2) FLS_ATTN_LAUNCH_SPL(2);
+        else FLS_ATTN_LAUNCH_SPL(1);
       }
 #undef FLS_ATTN_LAUNCH_SPL
       FLS_CHECK_LAUNCH();
@@ -574,22 +448,6 @@ int launch(int hpb, dim3 grid, hipStream_t st, const half_t* qkv, half_t* out, c
   if constexpr (HD == 96) {
     FLS_ATTN_LAUNCH(1);                     // 12 chunks per row: one head per block divides the tile
   } else if constexpr (WPH == 1) {          // 4 or 8 heads (dispatch)
-    if constexpr (R2 && HD == 128) {
-      if (hpb == 8 && g_dma) {
-        hipLaunchKernelGGL((attn_fwd<HD, 8, 1, true, false, false, true>), grid, dim3(64 * 8), 0, st, qkv, out, work,
-                           seg_lo, nh, nkv, ld_qkv, ld_out, scale_log2, kv0, ld_kv0, work2, r2win, nullptr);
-        FLS_CHECK_LAUNCH();
-        return 0;
-      }
-    }
-    if constexpr (R2) {
-      if (hpb == 8 && g_deep) {
-        hipLaunchKernelGGL((attn_fwd<HD, 8, 1, true, false, true>), grid, dim3(64 * 8), 0, st, qkv, out, work, seg_lo,
-                           nh, nkv, ld_qkv, ld_out, scale_log2, kv0, ld_kv0, work2, r2win, nullptr);
-        FLS_CHECK_LAUNCH();
-        return 0;
-      }
-    }
     if (hpb == 8) FLS_ATTN_LAUNCH(8);
     else FLS_ATTN_LAUNCH(4);
   } else if constexpr (WPH == 2) {
@@ -615,18 +473,6 @@ int g_split = 0; // split-KV slices of the range-2 kernel: 0 = by grid size, 1 =
 extern "C" int fls_attention_set_hpb(int hpb) {
   const int old = g_hpb;
   g_hpb = hpb;
-  return old;
-}
-
-extern "C" int fls_attention_set_dma(int on) {
-  const int old = g_dma;
-  g_dma = on ? 1 : 0;
-  return old;
-}
-
-extern "C" int fls_attention_set_deep(int on) {
-  const int old = g_deep;
-  g_deep = on ? 1 : 0;
   return old;
 }
 

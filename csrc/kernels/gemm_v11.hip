@@ -23,24 +23,17 @@
 // {128..191, 320..383} (16 KiB each; the two wave rows of a region), W (32 KiB).  Phases pair into
 // super-phases SP0 = (A s0, B s0), SP1 = (C s0, A s1), SP2 = (B s1, C s1), each ending in a relaxed
 // lgkmcnt (LDS reads retire in order) + counted vmcnt + raw s_barrier.  Region r of a stage is refilled (tile t -> t+2) in an SP after
-// the barrier that follows its last read.  LDS-DMA plan per wave (V11_SCHED 2, the default):
+// the barrier that follows its last read.  LDS-DMA plan per wave:
 //   SP0 of tile t: X2(t+1), W half 2 (t+1)          (4 + 4 pieces)   end: lgkmcnt(6) vmcnt(16)
 //   SP1 of tile t: X0(t+2)                          (4 pieces)       end: lgkmcnt(6) vmcnt(4)
 //   SP2 of tile t: X1(t+2), W half 1 (t+2)          (4 + 4 pieces)   end: lgkmcnt(8) vmcnt(12)
 // (W half h = each wave's DMA groups 4h-4 .. 4h-1 of its 8.)
-// V11_SCHED 1 (A/B build): 4 / 4 / 12 pieces, all of W(t+2) in SP2 (profiles/r4_gemm).  Requires an
-// even number of K-tiles (the loop body is unrolled over both stages) and M >= 384: the last M tile is shifted
+// (+0-1.5% over 4 / 4 / 12 pieces with all of W(t+2) in SP2 on the four 70B shapes,
+// profiles/r4_gemm/variant_ab_s2_a1.log.)  Requires an even number of K-tiles (the loop body is unrolled over both stages) and M >= 384: the last M tile is shifted
 // back to end at row M and stores only the rows its neighbour does not (epilogue_quadrant's LO), so
 // every LDS-DMA source row is in bounds and the per-piece row offsets live in the scalar soffset.
 #include "gemm_v10.h"
 
-#ifndef V11_SCHED
-#define V11_SCHED 2        // LDS-DMA placement: 2 = 8 / 4 / 8 per super-phase (default: +0-1.5% over 1 on the
-                           // four 70B shapes, profiles/r4_gemm/variant_ab_s2_a1.log), 1 = 4 / 4 / 12
-#endif
-#ifndef V11_AORDER
-#define V11_AORDER 0       // phase A MFMA order (A/B builds): 0 = column-major, 1 = row-major
-#endif
 
 namespace {
 namespace v11 {
@@ -194,18 +187,6 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_v11(const half_t* __restrict__
 // refills of the preceding C phase have ~29 MFMAs to land).  After MFMA 1 / 3 read x rows 8 / 9
 // of the current k-step (cbuf, cs); after the last use of x row u (MFMA 28 + u) refill it with
 // the next k-step (nbuf, ns).
-#if V11_AORDER == 1
-// A/B build: phase A row-major (x row u refilled after its 8th MFMA; w column t first used at MFMA t)
-#define V11_PHASE_A(cbuf, cs, nbuf, ns, DMA_STMT, ND)                                             \
-  _Pragma("unroll") for (int i_ = 0; i_ < 32; ++i_) {                                             \
-    const int u_ = i_ >> 3, t_ = i_ & 7;                                                          \
-    V11_MFMA(u_, t_);                                                                             \
-    if (i_ == 1) V11_RX(8, cbuf, cs);                                                             \
-    if (i_ == 3) V11_RX(9, cbuf, cs);                                                             \
-    if ((i_ & 7) == 7) V11_RX(u_, nbuf, ns);                                                      \
-    V11_DMAS(i_, DMA_STMT, ND);                                                                   \
-  }
-#else
 #define V11_PHASE_A(cbuf, cs, nbuf, ns, DMA_STMT, ND)                                             \
   _Pragma("unroll") for (int i_ = 0; i_ < 32; ++i_) {                                             \
     const int t_ = i_ >> 2, u_ = i_ & 3;                                                          \
@@ -215,7 +196,6 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_v11(const half_t* __restrict__
     if (i_ >= 28) V11_RX(u_, nbuf, ns);                                                           \
     V11_DMAS(i_, DMA_STMT, ND);                                                                   \
   }
-#endif
 // Phase B: x rows 4..7 x w 0..7, row-major; reads x rows 10 / 11 of the current k-step after
 // MFMAs 1 / 3 and refills x row u after its last MFMA (8u' + 7).
 #define V11_PHASE_B(cbuf, cs, nbuf, ns, DMA_STMT, ND)                                             \
@@ -256,57 +236,24 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_v11(const half_t* __restrict__
     for (int i = 0; i < 4; ++i) V11_DMA_X(rA, 1, 0, i, k1);
 #pragma unroll
     for (int i = 0; i < 4; ++i) V11_DMA_X(rA, 1, 1, i, k1);
-#if V11_SCHED == 2
 #pragma unroll
     for (int i = 0; i < 4; ++i) V11_DMA_W(rW, 1, i, k1);     // W-lo(1); W-hi(1) in SP0 of tile 0
   }
   asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-#else
-#pragma unroll
-    for (int i = 0; i < 8; ++i) V11_DMA_W(rW, 1, i, k1);
-  }
-  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-#endif
   __builtin_amdgcn_s_barrier();
 #pragma unroll
   for (int u = 0; u < 8; ++u) V11_RX(u, 0, 0);
 #pragma unroll
   for (int t = 0; t < 8; ++t) V11_RW(t, 0, 0);
 
-  // DMA plan of tile t (stage b = t & 1):  SP0: X2(t+1) -> stage b^1 (2 + 2)
-  //                                        SP1: X0(t+2) -> stage b   (2 + 2)
-  //                                        SP2: X1(t+2), W(t+2) -> b (6 + 6)
-  // SP ends: SP0 lgkmcnt(6) vmcnt(16); SP1 lgkmcnt(6) vmcnt(8); SP2 lgkmcnt(8) vmcnt(16).
   for (int kt = 0; kt < nk; kt += 2) {
     const int k1 = min(kt + 1, nk - 1) * TK, k2 = min(kt + 2, nk - 1) * TK, k3 = min(kt + 3, nk - 1) * TK;
     const __amdgpu_buffer_rsrc_t rX1 = kt + 1 < nk ? rA : rZA;
     const __amdgpu_buffer_rsrc_t rX2 = kt + 2 < nk ? rA : rZA, rW2 = kt + 2 < nk ? rW : rZW;
     const __amdgpu_buffer_rsrc_t rX3 = kt + 3 < nk ? rA : rZA, rW3 = kt + 3 < nk ? rW : rZW;
-#define V11_TILE(B, rXn, kn, rXf, rWf, kf)                                                         \
-  {                                                                                               \
-    auto dX2a = [&](int d) { V11_DMA_X(rXn, (B) ^ 1, 2, d, kn); };                                \
-    auto dX2b = [&](int d) { V11_DMA_X(rXn, (B) ^ 1, 2, d + 2, kn); };                            \
-    auto dX0a = [&](int d) { V11_DMA_X(rXf, B, 0, d, kf); };                                      \
-    auto dX0b = [&](int d) { V11_DMA_X(rXf, B, 0, d + 2, kf); };                                  \
-    auto dXW1 = [&](int d) {                                                                      \
-      if (d < 4) V11_DMA_X(rXf, B, 1, d, kf);                                                     \
-      else V11_DMA_W(rWf, B, d - 4, kf);                                                          \
-    };                                                                                            \
-    auto dW2 = [&](int d) { V11_DMA_W(rWf, B, d + 2, kf); };                                      \
-    V11_PHASE_A(B, 0, B, 1, dX2a, 2);                    /* A s0 */                              \
-    V11_PHASE_B(B, 0, B, 1, dX2b, 2);                    /* B s0 */                              \
-    V11_SYNC(6, 16);                                     /* SP0 */                               \
-    V11_PHASE_C(B, 1, dX0a, 2);                          /* C s0 */                              \
-    V11_PHASE_A(B, 1, (B) ^ 1, 0, dX0b, 2);              /* A s1 */                              \
-    V11_SYNC(6, 8);                                      /* SP1 */                               \
-    V11_PHASE_B(B, 1, (B) ^ 1, 0, dXW1, 6);              /* B s1 */                              \
-    V11_PHASE_C((B) ^ 1, 0, dW2, 6);                     /* C s1 */                              \
-    V11_SYNC(8, 16);                                     /* SP2 */                               \
-  }
-#if V11_SCHED == 2
-#undef V11_TILE
-    // rebalanced: 8 / 4 / 8 DMAs per super-phase (W split: W-lo(t+2) in SP2 of tile t, W-hi(t+2)
-    // in SP0 of tile t+1, waited at the end of SP1 of tile t+1 with everything older)
+    // DMA plan of tile t (stage b = t & 1), 8 / 4 / 8 DMAs per super-phase (W split: W-lo(t+2) in
+    // SP2 of tile t, W-hi(t+2) in SP0 of tile t+1, waited at the end of SP1 of tile t+1 with
+    // everything older):
     //   SP0: X2(t+1) + W-hi(t+1) -> b^1   lgkmcnt(6) vmcnt(16)
     //   SP1: X0(t+2) -> b                 lgkmcnt(6) vmcnt(4)
     //   SP2: X1(t+2) + W-lo(t+2) -> b     lgkmcnt(8) vmcnt(12)
@@ -331,10 +278,6 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_v11(const half_t* __restrict__
   }
     V11_TILE(0, rX1, rW1, k1, rX2, rW2, k2);   // tile kt,   stage 0
     V11_TILE(1, rX2, rW2, k2, rX3, rW3, k3);   // tile kt+1, stage 1
-#else
-    V11_TILE(0, rX1, k1, rX2, rW2, k2);        // tile kt,   stage 0
-    V11_TILE(1, rX2, k2, rX3, rW3, k3);        // tile kt+1, stage 1
-#endif
 #undef V11_TILE
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -360,8 +303,6 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_v11(const half_t* __restrict__
 }
 
 int g_v11 = 1;               // 0 off, 1 auto (large GEMMs, no extra row padding), 2 any valid shape (tests)
-int g_v11_order = 0;         // 0: auto_order; else a fixed signed group size
-int g_v11_rows = 0;          // rows per launch (0: all)
 
 template <int EPI>
 int launch_v11(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int lda, int ldw, int ldc, Epi ep,
@@ -372,36 +313,22 @@ int launch_v11(const half_t* A, const half_t* W, half_t* C, int M, int N, int K,
     (void)hipFuncSetAttribute((const void*)gemm_nt_v11<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     attr = true;
   }
-  const int rows = g_v11_rows > 0 ? g_v11_rows : M;
-  for (int r0 = 0; r0 < M; r0 += rows) {
-    const int m = min(rows, M - r0);
-    Epi e = ep;
-    if (e.pos) e.pos += r0;
-    if (e.R) e.R += (size_t)r0 * e.ldr;
-    const int tiles_m = (m + TM - 1) / TM, tiles_n = N / TN;
-    e.order = g_v11_order ? g_v11_order : auto_order(tiles_m, tiles_n);
-    hipLaunchKernelGGL((gemm_nt_v11<EPI>), dim3(tiles_m * tiles_n), dim3(256), LDS_BYTES, s, A + (size_t)r0 * lda, W,
-                       C + (size_t)r0 * ldc, m, N, K, lda, ldw, ldc, e);
-    FLS_CHECK_LAUNCH();
-  }
+  const int tiles_m = (M + TM - 1) / TM, tiles_n = N / TN;
+  ep.order = auto_order(tiles_m, tiles_n);
+  hipLaunchKernelGGL((gemm_nt_v11<EPI>), dim3(tiles_m * tiles_n), dim3(256), LDS_BYTES, s, A, W, C, M, N, K, lda, ldw,
+                     ldc, ep);
+  FLS_CHECK_LAUNCH();
   return 0;
 }
 
 }  // namespace
 
-// 1 = use v11 where it pays (default: no more rows than v10), 3 = by 256-CU round counts (A/B),
-// 0 = v10 everywhere, 2 = v11 on every shape it supports (tests: small and ragged shapes);
-// returns the previous mode
+// 1 = use v11 where it pays (default: no more rows than v10), 0 = v10 everywhere, 2 = v11 on every
+// shape it supports (tests: small and ragged shapes); returns the previous mode
 extern "C" int fls_gemm_set_v11(int mode) {
   const int old = g_v11;
-  g_v11 = mode < 0 ? 0 : mode > 3 ? 3 : mode;
+  g_v11 = mode < 0 ? 0 : mode > 2 ? 2 : mode;
   return old;
-}
-
-// v11 tile order (0 = auto_order) and rows per launch (0 = all); returns nothing (A/B knobs)
-extern "C" void fls_gemm_v11_tune(int order, int rows) {
-  g_v11_order = order;
-  g_v11_rows = rows > 0 ? rows : 0;
 }
 
 // Applicability of v11 for a launch; the shape rules of gemm.hip's v10 main path plus M >= 384.
@@ -412,23 +339,12 @@ extern "C" int fls_gemm_v11_try(const void* A, const void* W, void* C, const voi
                                 const float* sin_t, int rope_cols, int head_dim, const void* bias, fls_stream_t s) {
   using namespace v11;
   if (!g_v11 || M < TM || N % TN || K % TK || (K / TK) % 2 || lda % 8 || ldw % 8) return 0;
-  const int rows = g_v11_rows > 0 ? min(g_v11_rows, M) : M;
-  if (rows < TM) return 0;
-  if (g_v11 == 1 || g_v11 == 3) {
+  if (g_v11 == 1) {
     // fills the chip (at least one tile per CU per launch)
-    if ((size_t)((rows + TM - 1) / TM) * (N / TN) < 256) return 0;
-    if (g_v11 == 1) {
-      // computes no more rows than v10's 256-row tiles would (callers chunk rows in multiples of
-      // 768 = lcm(256, 384))
-      if ((size_t)((M + TM - 1) / TM) * TM > (size_t)((M + 255) / 256) * 256) return 0;
-    } else {
-      // by 256-CU rounds: a v11 tile is 1.5x a v10 tile's work at ~10% more FLOP/s on the 70B
-      // shapes (profiles/r4_gemm), so v11 takes the launch when rounds11 x 15 < rounds10 x 11
-      // (e.g. 4,096-row QKV chunks: 2 rounds of 440 tiles vs 3 rounds of 640)
-      const long r10 = ((long)((M + 255) / 256) * (N / 256) + 255) / 256;
-      const long r11 = ((long)((M + TM - 1) / TM) * (N / TN) + 255) / 256;
-      if (r11 * 15 >= r10 * 11) return 0;
-    }
+    if ((size_t)((M + TM - 1) / TM) * (N / TN) < 256) return 0;
+    // computes no more rows than v10's 256-row tiles would (callers chunk rows in multiples of
+    // 768 = lcm(256, 384))
+    if ((size_t)((M + TM - 1) / TM) * TM > (size_t)((M + 255) / 256) * 256) return 0;
   }
   // 32-bit DMA offsets: every row of A (piece rows + lane rows + K) and of the (stacked) weight
   if ((size_t)M * lda * 2 >= (1ull << 32)) return 0;

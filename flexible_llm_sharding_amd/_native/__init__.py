@@ -96,11 +96,8 @@ def _load_kernels(path: str = _KERNELS):
     _bind(lib, "fls_gemm_set_v11", c_int, c_int)
     _bind(lib, "fls_gemm_set_skinny", c_int, c_int, c_int)
     _bind(lib, "fls_gemm_set_skinny_bn", c_int, c_int)
-    _bind(lib, "fls_gemm_v11_tune", None, c_int, c_int)
     _bind(lib, "fls_attention_set_hpb", c_int, c_int)
     _bind(lib, "fls_attention_set_split", c_int, c_int)
-    _bind(lib, "fls_attention_set_deep", c_int, c_int)
-    _bind(lib, "fls_attention_set_dma", c_int, c_int)
     _bind(lib, "fls_attention", c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
           c_int, c_int, c_float, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_uint64, c_int,
           c_void_p)

@@ -24,7 +24,7 @@ ROOT = os.path.abspath(os.path.join(HERE, "..", ".."))
 CSRC = os.path.join(ROOT, "csrc")
 OBJ = os.path.join(HERE, "obj")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
-ARCH = os.environ.get("FLS_OFFLOAD_ARCH", "gfx950")
+ARCH = os.environ.get("FLS_OFFLOAD_ARCH", "gfx950")   # knobs.py (not imported: the build runs standalone)
 
 KERNELS_SO = os.path.join(HERE, "libfls_kernels.so")
 RUNTIME_SO = os.path.join(HERE, "libfls_runtime.so")

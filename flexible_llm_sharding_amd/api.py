@@ -26,6 +26,7 @@ from typing import List, Optional, Sequence
 import numpy as np
 import torch
 
+from . import knobs
 from .config import MAX_TOKEN_LEN, ModelConfig
 from .engine import ShardedRunner
 from .parallel.comm import Comm
@@ -255,7 +256,7 @@ def generation_loop(args, runner, comm: Comm, tok, original_prompts: Sequence, s
     step_tokens: List[List[np.ndarray]] = []
     # host-side profile of chosen steps (FLS_PROFILE_GEN_STEPS="2,3" -> cProfile stats in
     # FLS_PROFILE_OUT.<step>): where a generation step's host time goes
-    prof_steps = {int(s) for s in os.environ.get("FLS_PROFILE_GEN_STEPS", "").split(",") if s.strip()}
+    prof_steps = {int(s) for s in knobs.get("FLS_PROFILE_GEN_STEPS").split(",") if s.strip()}
     for i_new in range(args.num_gen_token):
         t_step = time.perf_counter()
         prof = None
@@ -266,7 +267,7 @@ def generation_loop(args, runner, comm: Comm, tok, original_prompts: Sequence, s
         outputs = run_all(args, runner, comm, input_prompts)
         if prof is not None:
             prof.disable()
-            prof.dump_stats(f"{os.environ.get('FLS_PROFILE_OUT', 'gen_profile')}.{i_new}")
+            prof.dump_stats(f"{knobs.get('FLS_PROFILE_OUT')}.{i_new}")
         if comm.rank == 0:
             if i_new == 0:
                 step_scores = [[o] for o in outputs]

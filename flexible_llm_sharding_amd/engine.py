@@ -27,13 +27,13 @@ MI355X design of the same schedule:
 """
 from __future__ import annotations
 
-import os
 import time
 from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 import torch
 
+from . import knobs
 from .config import MAX_TOKEN_LEN, ModelConfig
 from .models.layout import layer_kind
 from .models.llama import ExecContext, layer_flops, rope_tables, run_layer
@@ -58,8 +58,7 @@ MOE_MLP_CHUNK = 65536
 
 def _parse_fault(rank: int):
     """FLS_FAULT="rank:shard" — fault injection for failure-handling tests."""
-    import os
-    spec = os.environ.get("FLS_FAULT", "")
+    spec = knobs.get("FLS_FAULT")
     if not spec:
         return None
     r, _, k = spec.partition(":")
@@ -312,8 +311,7 @@ class ShardedRunner:
         each decoder layer as an attention piece + an MLP piece (runtime/prefetch.py
         PiecePoolPrefetcher: 3.12 GB of weight buffers for 70B instead of 3.42, and the next
         layer's attention weights land while this layer's MLP runs)."""
-        import os
-        if os.environ.get("FLS_PIECE_POOL", "1") == "0":
+        if knobs.get_int("FLS_PIECE_POOL") == 0:
             return False
         return bool(self.cuda and max_vram_gb and not resident and not keep and not resume_dir
                     and self.plan.mode == "single" and shards and all(len(s) == 1 for s in shards)
@@ -774,10 +772,9 @@ class ShardedRunner:
         ``FLS_SPECULATIVE_PREFETCH=0/1`` overrides.  Never when resuming (the next call may start
         elsewhere), resident (nothing to load), model parallel, or with the data-parallel
         all-gather prefetcher (no collectives left in flight after a call)."""
-        import os
         from .parallel.data_parallel import AllGatherPrefetcher
         pf = self.prefetcher
-        env = os.environ.get("FLS_SPECULATIVE_PREFETCH")
+        env = knobs.get("FLS_SPECULATIVE_PREFETCH") or None
         if env is not None and env != "1":
             return False
         if env is None and pf.n_slots < 3:

@@ -17,12 +17,12 @@ PyTorch on CPU).
 from __future__ import annotations
 
 import math
-import os
 from dataclasses import dataclass
 from typing import Dict, Optional
 
 import torch
 
+from .. import knobs
 from ..config import ModelConfig, MAX_TOKEN_LEN
 from .layout import layer_kind
 
@@ -211,11 +211,11 @@ def _resid(ctx: ExecContext, a: torch.Tensor, w: torch.Tensor, x: torch.Tensor, 
     return x.add_(y.mul_(r))
 
 
-CHUNK_ALIGN = int(os.environ.get("FLS_CHUNK_ALIGN", "3072"))   # A/B knob (256: round 3's chunks)
+CHUNK_ALIGN = knobs.get_int("FLS_CHUNK_ALIGN")   # A/B knob (256: round 3's chunks)
 # RMSNorm + QKV row chunks alternate between two streams over the two halves of the normed buffer,
 # so one chunk's GEMM fills the CUs the other's last tile round leaves idle (2, default: +1.1% on the
 # capped 70B headline, profiles/r4_gemm/qkv_two_streams; A/B: 1 = one stream)
-QKV_STREAMS = int(os.environ.get("FLS_QKV_STREAMS", "2"))
+QKV_STREAMS = knobs.get_int("FLS_QKV_STREAMS")
 
 
 def balanced_step(rows: int, limit: int, align: int = 0) -> int:

@@ -18,7 +18,7 @@ from dataclasses import dataclass
 
 import torch
 
-from .. import _native
+from .. import _native, knobs
 from .torch_backend import fill_params
 
 EPI_NONE, EPI_RESID, EPI_SWIGLU, EPI_ROPE = 0, 1, 2, 3
@@ -67,22 +67,15 @@ class HipOps:
         self.k = _native.kernels()
         self._ws = {}
         self._tl = threading.local()
-        if os.environ.get("FLS_SPLITK", "1") == "0":      # small-M split-K path off (A/B, tests)
+        # A/B switches (knobs.py); the kernels' defaults are the measured winners
+        if knobs.get_int("FLS_SPLITK") == 0:
             self.k.fls_gemm_set_splitk(0)
-        if os.environ.get("FLS_GEMM_V11"):                # 0: v10 only, 1: auto (default), 2: forced (A/B)
-            self.k.fls_gemm_set_v11(int(os.environ["FLS_GEMM_V11"]))
-        if os.environ.get("FLS_V11_ORDER") or os.environ.get("FLS_V11_ROWS"):   # v11 tile order / rows (A/B)
-            self.k.fls_gemm_v11_tune(int(os.environ.get("FLS_V11_ORDER", "0")), int(os.environ.get("FLS_V11_ROWS", "0")))
-        if os.environ.get("FLS_SKINNY"):                  # skinny-M GEMM: 0 off, 1 auto (default), 2 forced (A/B)
-            self.k.fls_gemm_set_skinny(int(os.environ["FLS_SKINNY"]), int(os.environ.get("FLS_SKINNY_BLOCKS", "0")))
-        if os.environ.get("FLS_SKINNY_BN"):               # skinny-M weight rows per block: 0 auto, 128 / 256
-            self.k.fls_gemm_set_skinny_bn(int(os.environ["FLS_SKINNY_BN"]))
-        if os.environ.get("FLS_ATTN_SPLIT"):              # split-KV slices of the range-2 kernel (A/B)
-            self.k.fls_attention_set_split(int(os.environ["FLS_ATTN_SPLIT"]))
-        if os.environ.get("FLS_ATTN_DEEP"):               # range-2 two-register-set K/V staging: 0 off (default), 1 on
-            self.k.fls_attention_set_deep(int(os.environ["FLS_ATTN_DEEP"]))
-        if os.environ.get("FLS_ATTN_DMA"):                # range-2 LDS-DMA K/V ring (8-head blocks): 0 off (default), 1 on
-            self.k.fls_attention_set_dma(int(os.environ["FLS_ATTN_DMA"]))
+        if knobs.is_set("FLS_GEMM_V11"):
+            self.k.fls_gemm_set_v11(knobs.get_int("FLS_GEMM_V11"))
+        if knobs.is_set("FLS_SKINNY"):
+            self.k.fls_gemm_set_skinny(knobs.get_int("FLS_SKINNY"), 0)
+        if knobs.is_set("FLS_ATTN_SPLIT"):
+            self.k.fls_attention_set_split(knobs.get_int("FLS_ATTN_SPLIT"))
 
     # ---------------------------------------------------------------- GEMM
     def gemm(self, x: torch.Tensor, w: torch.Tensor, epi: int = EPI_NONE, out: torch.Tensor = None,

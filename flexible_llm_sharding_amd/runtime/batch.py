@@ -28,13 +28,13 @@ causal mask they cannot influence it.
 from __future__ import annotations
 
 import dataclasses
-import os
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
 
 import numpy as np
 import torch
 
+from .. import knobs
 from ..utils.tokenizer import TokenizedPrompt
 
 Q_BLOCK = 64            # query rows per attention work item (kernel tile)
@@ -58,7 +58,7 @@ class Segment:
 
 # range-2 attention of <= 32-row items with one wave per head (32, default) or the 2-wave kernel
 # (64: A/B of the generation step, FLS_R2_QBLOCK=64)
-R2_Q_BLOCK = int(os.environ.get("FLS_R2_QBLOCK", "32"))
+R2_Q_BLOCK = knobs.get_int("FLS_R2_QBLOCK")
 
 
 @dataclass

@@ -15,10 +15,10 @@ from typing import Dict
 
 import torch
 
-from .. import _native
+from .. import _native, knobs
 from ..utils import safetensors_io
 
-_IO_THREADS = int(os.environ.get("FLS_IO_THREADS", "8"))
+_IO_THREADS = knobs.get_int("FLS_IO_THREADS")
 
 # pinned bytes currently held / high-water mark (alloc_host blocks; the streamer's ring is
 # reported by runtime.stream separately)

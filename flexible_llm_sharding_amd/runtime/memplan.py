@@ -22,6 +22,7 @@ from __future__ import annotations
 import os
 from typing import Optional, Tuple
 
+from .. import knobs
 from ..config import ModelConfig
 from ..models.layout import layer_kind, layer_layout
 
@@ -41,7 +42,7 @@ CAP_MARGIN = 0.015
 # ~185 MB above the steady context for <= 2 ms around some host -> device weight copies, sampled
 # every 2 ms on the 70B headline (profiles/r4_vram); kept free under a cap, by the allocator limit
 # and by the plan
-RUNTIME_RESERVE = int(os.environ.get("FLS_RUNTIME_RESERVE_MB", "192")) << 20
+RUNTIME_RESERVE = knobs.get_int("FLS_RUNTIME_RESERVE_MB") << 20
 
 
 def activation_bytes(cfg: ModelConfig, tokens: int, mlp_chunk: int, elem: int = 2, qkv_chunk: int = 0,
@@ -71,7 +72,7 @@ def shared_device_bytes() -> int:
     left out of this process's ``--max_vram_gb`` budget: hipMemGetInfo counts the whole device,
     so a co-tenant (e.g. the pytest process that launched a capped worker) would otherwise be
     charged to the cap."""
-    return int(float(os.environ.get("FLS_VRAM_SHARED_GB", "0") or 0) * 1e9)
+    return int(float(knobs.get("FLS_VRAM_SHARED_GB") or 0) * 1e9)
 
 
 def device_used_bytes(device) -> int:

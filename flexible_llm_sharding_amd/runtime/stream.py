@@ -36,7 +36,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 
-from .. import _native
+from .. import _native, knobs
 from ..config import ModelConfig
 from ..models.layout import layer_kind, layer_layout, placements, source_key
 from ..utils.layer_format import layer_file
@@ -139,11 +139,6 @@ def _piece_array(pieces) -> ctypes.Array:
     return arr
 
 
-def _env_int(name: str, default: int) -> int:
-    v = os.environ.get(name)
-    return int(v) if v else default
-
-
 class FileLayerSource(LayerSource):
     """Per-layer safetensors files streamed to HBM on every pass (``--weight_cache stream``).
 
@@ -162,10 +157,10 @@ class FileLayerSource(LayerSource):
         missing = [n for n in self.names if not os.path.exists(layer_file(model_path, n))]
         if missing:
             raise FileNotFoundError(f"{model_path}: missing layer files {missing[:4]}...")
-        self.chunk_bytes = (chunk_mb or _env_int("FLS_STREAM_CHUNK_MB", 64)) << 20
-        self.n_chunks = n_chunks or _env_int("FLS_STREAM_CHUNKS", 4)
-        self.io_threads = io_threads or _env_int("FLS_IO_THREADS", 8)
-        self.direct = bool(int(os.environ.get("FLS_O_DIRECT", "0"))) if direct is None else bool(direct)
+        self.chunk_bytes = (chunk_mb or knobs.get_int("FLS_STREAM_CHUNK_MB")) << 20
+        self.n_chunks = n_chunks or knobs.get_int("FLS_STREAM_CHUNKS")
+        self.io_threads = io_threads or knobs.get_int("FLS_IO_THREADS")
+        self.direct = bool(knobs.get_int("FLS_O_DIRECT")) if direct is None else bool(direct)
         self._plans: Dict[str, LayerPlan] = {}
         self._lock = threading.Lock()
         self._streamer = None

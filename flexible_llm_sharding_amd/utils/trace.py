@@ -15,8 +15,10 @@ import os
 import time
 from collections import defaultdict
 
+from .. import knobs
+
 _roctx = None
-_enabled = os.environ.get("FLS_TRACE", "0") not in ("0", "", "false")
+_enabled = knobs.get("FLS_TRACE") not in ("0", "", "false")
 
 
 def _load():

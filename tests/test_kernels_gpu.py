@@ -456,12 +456,6 @@ def test_attention_suffix_rows_from_cache(ops, ref, nh, nkv, hd, split, q_block)
     old = ops.k.fls_attention_set_split(split)
     try:
         _suffix_rows_from_cache(ops, ref, nh, nkv, hd, q_block=q_block)
-        if q_block == 32 and split == 1:         # the LDS-DMA ring variant (8-head blocks, hd 128)
-            old_dma = ops.k.fls_attention_set_dma(1)
-            try:
-                _suffix_rows_from_cache(ops, ref, nh, nkv, hd, q_block=q_block)
-            finally:
-                ops.k.fls_attention_set_dma(old_dma)
     finally:
         ops.k.fls_attention_set_split(old)
 
@@ -469,8 +463,7 @@ def test_attention_suffix_rows_from_cache(ops, ref, nh, nkv, hd, split, q_block)
 def test_attention_decode_split_matches_unsplit(ops, ref):
     """Decode-like step at 70B heads (12 prompts x 5 suffixes, one new row each after 40 kept rows,
     600-row prefixes): the split-KV kernel (by grid size) == one block per item to fp32-partials
-    rounding, and both == the fp32 oracle; the one-wave-per-head kernel with two K/V register sets
-    (A/B variant) == with one (default), bitwise."""
+    rounding, and both == the fp32 oracle."""
     prompts = [(600, [41] * 5)] * 12
     keep = [[40] * 5] * 12
     ys = []
@@ -484,24 +477,6 @@ def test_attention_decode_split_matches_unsplit(ops, ref):
     # one wave per head, 8 heads per block: the same per-row math as the 2-wave kernel, unsplit
     assert torch.equal(ys[2], ys[0])
     assert rel_err(ys[3], ys[0]) < 2e-3
-    # ... with two K/V register sets instead of one (FLS_ATTN_DEEP=1): only the load schedule differs
-    old = ops.k.fls_attention_set_deep(1)
-    old_split = ops.k.fls_attention_set_split(1)
-    try:
-        two_sets = _suffix_rows_from_cache(ops, ref, 64, 8, 128, prompts, keep, q_block=32)
-    finally:
-        ops.k.fls_attention_set_deep(old)
-        ops.k.fls_attention_set_split(old_split)
-    assert torch.equal(two_sets, ys[2])
-    # ... with the K/V tiles staged by LDS-DMA into a 4-tile ring (FLS_ATTN_DMA=1)
-    old = ops.k.fls_attention_set_dma(1)
-    old_split = ops.k.fls_attention_set_split(1)
-    try:
-        dma = _suffix_rows_from_cache(ops, ref, 64, 8, 128, prompts, keep, q_block=32)
-    finally:
-        ops.k.fls_attention_set_dma(old)
-        ops.k.fls_attention_set_split(old_split)
-    assert torch.equal(dma, ys[2])
 
 
 def _suffix_rows_from_cache(ops, ref, nh, nkv, hd, prompts=None, keep=None, q_block=64):
