@@ -62,16 +62,28 @@ void    fls_f32_to_f16(const float* src, uint16_t* dst, uint64_t n);
 int fls_kernels_version(void);
 // epilogue codes for fls_gemm
 enum { FLS_EPI_NONE = 0, FLS_EPI_RESID = 1, FLS_EPI_SWIGLU = 2, FLS_EPI_ROPE = 3 };
-// C[M, N'] = epi(A[M,K] . W[N,K]^T).  fp16 in / fp32 accumulate / fp16 out.
-//   RESID : C = acc + R (R may alias C)
+// C[M, N'] = epi(acc), acc[m] = rscale[m] * (A[M,K] . W[N,K]^T)[m] (+ bias)  (rscale may be null:
+// 1; the RMSNorm statistic of a fused norm + projection).  fp16 in / fp32 accumulate / fp16 out.
+//   RESID : C = alpha * acc + R (R may alias C; alpha: Granite's residual_multiplier, else 1)
 //   SWIGLU: W = [gate (N/2 rows); up (N/2 rows)]; C has N/2 columns = silu(g)*u
 //   ROPE  : columns < rope_cols are rotated (HF rotate-half, natural head-dim
 //           order, head_dim 64 or 128) with pos[m] and fp32 tables cos/sin
 //           [maxpos, head_dim/2]
 int fls_gemm(const void* A, const void* W, void* C, const void* R, int M, int N, int K,
              int lda, int ldw, int ldc, int ldr, int epi, const int* pos, const float* cos_t,
-             const float* sin_t, int rope_cols, int head_dim, const void* bias, void* ws, uint64_t ws_bytes,
+             const float* sin_t, int rope_cols, int head_dim, const void* bias, const float* rscale,
+             float alpha, void* ws, uint64_t ws_bytes,
              fls_stream_t s);   // ws: device scratch for the small-M split-K path (may be null)
+// rstd[r] = rsqrt(mean(x[row]^2) + eps) in fp32, row = row_idx ? row_idx[r] : r (fused RMSNorm:
+// the statistic of the rows a norm-folded projection reads raw)
+int fls_row_rstd(const void* x, int ldx, const int* row_idx, int rows, int H, float eps, float* rstd,
+                 fls_stream_t s);
+// W[n, k] = fp16(W[n, k] * gamma[k]) in place for n < N, k < K (the RMSNorm weight folded into
+// the projection that consumes the normed rows)
+int fls_fold_norm(void* w, int ldw, int N, int K, const void* gamma, fls_stream_t s);
+// y[dst_idx[r]] = x[src_idx[r]] for r < rows (fp16 rows of H elements; a null index = identity)
+int fls_copy_rows(const void* x, int ldx, const int* src_idx, void* y, int ldy, const int* dst_idx, int rows, int H,
+                  fls_stream_t s);
 int fls_gemm_set_splitk(int on);
 int fls_gemm_set_gu_split(int p);
 int fls_gemm_set_row_chunk(int rows);   // rows per main-path GEMM launch (default 16384; 0 = unlimited)   // SwiGLU GEMM in p column launches (A/B; default 1)
@@ -111,8 +123,8 @@ int fls_headnorm_rope(void* x, int ldx, int rows, int n_q, int n_k, const void* 
                       const float* cos_t, const float* sin_t, int hd, float eps, fls_stream_t s);
 int fls_rmsnorm(const void* x, const void* w, void* y, const int* row_idx, int rows, int H,
                 int ldx, int ldy, float eps, fls_stream_t s);
-int fls_embed(const int* ids, const void* table, void* out, int T, int H, int V, fls_stream_t s);
-int fls_softmax_rows(const void* logits, void* probs, int rows, int V, fls_stream_t s);
+int fls_embed(const int* ids, const void* table, void* out, int T, int H, int V, float scale, fls_stream_t s);
+int fls_softmax_rows(const void* logits, void* probs, int rows, int V, float inv_scale, fls_stream_t s);
 // dst = fp16(src): src_dtype 1 = bf16 (in place allowed), 2 = fp32 (no overlap)
 int fls_cast_f16(void* dst, const void* src, int src_dtype, uint64_t n, fls_stream_t s);
 // C[M,N] = X[M,K] W[N,K]^T for M <= 16 (skinny LM head); K % 32 == 0

@@ -84,20 +84,91 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const half_t* __restrict__
   }
 }
 
+// scale != 1: fp16(e * scale) (Granite's embedding_multiplier, GraniteModel's rounding)
 __global__ __launch_bounds__(256) void embed_kernel(const int* __restrict__ ids, const half_t* __restrict__ table,
-                                                  half_t* __restrict__ out, int H, int V) {
+                                                  half_t* __restrict__ out, int H, int V, float scale) {
   const int t = blockIdx.x;
   int id = ids[t];
   id = id < 0 ? 0 : (id >= V ? V - 1 : id);
   const half8* src = (const half8*)(table + (size_t)id * H);
   half8* dst = (half8*)(out + (size_t)t * H);
+  if (scale == 1.f) {
+    for (int c = threadIdx.x; c < H / 8; c += 256) dst[c] = src[c];
+    return;
+  }
+  for (int c = threadIdx.x; c < H / 8; c += 256) {
+    const half8 v = src[c];
+    half8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (half_t)((float)v[j] * scale);
+    dst[c] = o;
+  }
+}
+
+// ------------------------------------------------------------ fused RMSNorm pieces
+// rstd of one row per wave: the statistic a norm-folded projection applies in its epilogue
+// (models/llama.py): the hidden state is read once and nothing is written back but 4 bytes a row.
+__global__ __launch_bounds__(256) void row_rstd_kernel(const half_t* __restrict__ x, int ldx,
+                                                     const int* __restrict__ row_idx, int rows, int H, float eps,
+                                                     float* __restrict__ rstd) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;                            // wave-uniform
+  const int lane = threadIdx.x & 63;
+  const half_t* xr = x + (size_t)(row_idx ? row_idx[r] : r) * ldx;
+  const int nvec = H / 8;
+  float ss0 = 0.f, ss1 = 0.f;
+  int c = lane;
+  for (; c + 64 < nvec; c += 128) {                 // two 16-byte loads in flight per lane
+    const half8 a = *(const half8*)(xr + c * 8), b = *(const half8*)(xr + (c + 64) * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      ss0 += (float)a[j] * (float)a[j];
+      ss1 += (float)b[j] * (float)b[j];
+    }
+  }
+  if (c < nvec) {
+    const half8 a = *(const half8*)(xr + c * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ss0 += (float)a[j] * (float)a[j];
+  }
+  const float tot = warp_sum(ss0 + ss1);
+  if (lane == 0) rstd[r] = rsqrtf(tot / (float)H + eps);
+}
+
+// W[n, k] *= gamma[k] (fp16 result), 8 columns per thread
+__global__ __launch_bounds__(256) void fold_norm_kernel(half_t* __restrict__ w, int ldw, int N, int K,
+                                                      const half_t* __restrict__ gamma) {
+  const int kv = K / 8;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long long)N * kv) return;
+  const int n = (int)(i / kv), c = (int)(i % kv) * 8;
+  half8* p = (half8*)(w + (size_t)n * ldw + c);
+  const half8 g = *(const half8*)(gamma + c);
+  const half8 v = *p;
+  half8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (half_t)((float)v[j] * (float)g[j]);
+  *p = o;
+}
+
+// y[dst_idx[r]] = x[src_idx[r]] for fp16 rows of H elements (a null index is the identity):
+// row gathers / scatters of the pruned last layer and the prefix K/V cache
+__global__ __launch_bounds__(256) void copy_rows_kernel(const half_t* __restrict__ x, int ldx,
+                                                      const int* __restrict__ src_idx, half_t* __restrict__ y, int ldy,
+                                                      const int* __restrict__ dst_idx, int H) {
+  const int r = blockIdx.x;
+  const half8* src = (const half8*)(x + (size_t)(src_idx ? src_idx[r] : r) * ldx);
+  half8* dst = (half8*)(y + (size_t)(dst_idx ? dst_idx[r] : r) * ldy);
   for (int c = threadIdx.x; c < H / 8; c += 256) dst[c] = src[c];
 }
 
 // softmax over a row of fp16 logits -> fp16 probabilities (fp32 math),
 // online max/sum in one pass, normalisation in a second (row stays in L2).
+// inv_scale != 1: the logits are first fp16(l * inv_scale) (Granite's logits / logits_scaling)
 __global__ __launch_bounds__(256) void softmax_kernel(const half_t* __restrict__ logits, half_t* __restrict__ probs,
-                                                    int V) {
+                                                    int V, float inv_scale) {
+  const bool scaled = inv_scale != 1.f;
+  auto ld = [=](half_t h) { return scaled ? (float)(half_t)((float)h * inv_scale) : (float)h; };
   __shared__ float red[4];
   const half_t* lr = logits + (size_t)blockIdx.x * V;
   half_t* pr = probs + (size_t)blockIdx.x * V;
@@ -106,18 +177,18 @@ __global__ __launch_bounds__(256) void softmax_kernel(const half_t* __restrict__
   if (vec) {
     for (int c = threadIdx.x; c < V / 8; c += 256) {
       const half8 v = *(const half8*)(lr + c * 8);
-      float vm = (float)v[0];
+      float vm = ld(v[0]);
 #pragma unroll
-      for (int j = 1; j < 8; ++j) vm = fmaxf(vm, (float)v[j]);
+      for (int j = 1; j < 8; ++j) vm = fmaxf(vm, ld(v[j]));
       const float nm = fmaxf(m, vm);
       s *= __expf(m - nm);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) s += __expf((float)v[j] - nm);
+      for (int j = 0; j < 8; ++j) s += __expf(ld(v[j]) - nm);
       m = nm;
     }
   } else {
     for (int c = threadIdx.x; c < V; c += 256) {
-      const float v = (float)lr[c];
+      const float v = ld(lr[c]);
       const float nm = fmaxf(m, v);
       s = s * __expf(m - nm) + __expf(v - nm);
       m = nm;
@@ -131,11 +202,11 @@ __global__ __launch_bounds__(256) void softmax_kernel(const half_t* __restrict__
       const half8 v = *(const half8*)(lr + c * 8);
       half8 o;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = (half_t)(__expf((float)v[j] - gm) * inv);
+      for (int j = 0; j < 8; ++j) o[j] = (half_t)(__expf(ld(v[j]) - gm) * inv);
       *(half8*)(pr + c * 8) = o;
     }
   } else {
-    for (int c = threadIdx.x; c < V; c += 256) pr[c] = (half_t)(__expf((float)lr[c] - gm) * inv);
+    for (int c = threadIdx.x; c < V; c += 256) pr[c] = (half_t)(__expf(ld(lr[c]) - gm) * inv);
   }
 }
 
@@ -336,19 +407,50 @@ extern "C" int fls_rmsnorm(const void* x, const void* w, void* y, const int* row
   return 0;
 }
 
-extern "C" int fls_embed(const int* ids, const void* table, void* out, int T, int H, int V, fls_stream_t s) {
+extern "C" int fls_embed(const int* ids, const void* table, void* out, int T, int H, int V, float scale,
+                         fls_stream_t s) {
   if (T <= 0) return 0;
   if (H % 8) return -2;
   hipLaunchKernelGGL(embed_kernel, dim3(T), dim3(256), 0, (hipStream_t)s, ids, (const half_t*)table, (half_t*)out,
-                     H, V);
+                     H, V, scale);
   FLS_CHECK_LAUNCH();
   return 0;
 }
 
-extern "C" int fls_softmax_rows(const void* logits, void* probs, int rows, int V, fls_stream_t s) {
+extern "C" int fls_softmax_rows(const void* logits, void* probs, int rows, int V, float inv_scale, fls_stream_t s) {
   if (rows <= 0) return 0;
   hipLaunchKernelGGL(softmax_kernel, dim3(rows), dim3(256), 0, (hipStream_t)s, (const half_t*)logits,
-                     (half_t*)probs, V);
+                     (half_t*)probs, V, inv_scale);
+  FLS_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int fls_row_rstd(const void* x, int ldx, const int* row_idx, int rows, int H, float eps, float* rstd,
+                            fls_stream_t s) {
+  if (rows <= 0) return 0;
+  if (H % 8 || ldx % 8 || ((uintptr_t)x & 15)) return -2;
+  hipLaunchKernelGGL(row_rstd_kernel, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)s, (const half_t*)x, ldx,
+                     row_idx, rows, H, eps, rstd);
+  FLS_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int fls_fold_norm(void* w, int ldw, int N, int K, const void* gamma, fls_stream_t s) {
+  if (N <= 0 || K <= 0) return 0;
+  if (K % 8 || ldw % 8 || (((uintptr_t)w | (uintptr_t)gamma) & 15)) return -2;
+  const long long threads = (long long)N * (K / 8);
+  hipLaunchKernelGGL(fold_norm_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, (hipStream_t)s,
+                     (half_t*)w, ldw, N, K, (const half_t*)gamma);
+  FLS_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int fls_copy_rows(const void* x, int ldx, const int* src_idx, void* y, int ldy, const int* dst_idx,
+                             int rows, int H, fls_stream_t s) {
+  if (rows <= 0) return 0;
+  if (H % 8 || ldx % 8 || ldy % 8 || (((uintptr_t)x | (uintptr_t)y) & 15)) return -2;
+  hipLaunchKernelGGL(copy_rows_kernel, dim3(rows), dim3(256), 0, (hipStream_t)s, (const half_t*)x, ldx, src_idx,
+                     (half_t*)y, ldy, dst_idx, H);
   FLS_CHECK_LAUNCH();
   return 0;
 }

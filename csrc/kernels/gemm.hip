@@ -106,9 +106,9 @@ __global__ __launch_bounds__(256) void gemm_nt_generic(const half_t* __restrict_
             for (int r = 0; r < 4; ++r) {
               const int n = nf + h * 16 + 4 * grp + r;
               if (n < N) {
-                float v = h ? acc[u][2 * p + 1][r] : acc[u][2 * p][r];
+                float v = (h ? acc[u][2 * p + 1][r] : acc[u][2 * p][r]) * row_scale(ep, m);
                 if (ep.bias) v += (float)ep.bias[n];
-                if constexpr (EPI == FLS_EPI_RESID) v += (float)ep.R[(size_t)m * ep.ldr + n];
+                if constexpr (EPI == FLS_EPI_RESID) v = v * ep.alpha + (float)ep.R[(size_t)m * ep.ldr + n];
                 C[(size_t)m * ldc + n] = (half_t)v;
               }
             }
@@ -277,10 +277,11 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
   if (idx >= (long long)M * units) return;
   const int m = (int)(idx / units), c = (int)(idx % units) * 4;
+  const float rsc = row_scale(ep, m);
   auto sum4 = [&](int col) {
     floatx4 a = *(const floatx4*)(part + (size_t)m * N + col);
     for (int k = 1; k < S; ++k) a += *(const floatx4*)(part + (size_t)k * pstride + (size_t)m * N + col);
-    return a;
+    return a * rsc;
   };
   auto bias4 = [&](floatx4& a, int col) {
     if (ep.bias) {
@@ -331,7 +332,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
     if constexpr (EPI == FLS_EPI_RESID) {
       const half4 rr = *(const half4*)(ep.R + (size_t)m * ep.ldr + c);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) a[r] += (float)rr[r];
+      for (int r = 0; r < 4; ++r) a[r] = a[r] * ep.alpha + (float)rr[r];
     }
     store4(a, c);
   }
@@ -455,7 +456,7 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
 
 }  // namespace
 
-extern "C" int fls_kernels_version(void) { return 20; }
+extern "C" int fls_kernels_version(void) { return 21; }
 
 // tile order: 0 = by shape (default); g > 0: groups of g M tiles; g < 0: groups of -g N tiles (A/B, tests)
 extern "C" int fls_gemm_set_order(int order) {
@@ -511,12 +512,13 @@ extern "C" int fls_gemm_set_mid(int on) {   // 0 off, 1 auto, 2 forced wherever 
 // gemm_v11.hip: the 384 x 256 tile for large projections (returns 1 when it took the GEMM)
 extern "C" int fls_gemm_v11_try(const void* A, const void* W, void* C, const void* R, int M, int N, int K, int lda,
                                 int ldw, int ldc, int ldr, int epi, const int* pos, const float* cos_t,
-                                const float* sin_t, int rope_cols, int head_dim, const void* bias, fls_stream_t s);
+                                const float* sin_t, int rope_cols, int head_dim, const void* bias,
+                                const float* rscale, float alpha, fls_stream_t s);
 
 extern "C" int fls_gemm(const void* A, const void* W, void* C, const void* R, int M, int N, int K, int lda, int ldw,
                         int ldc, int ldr, int epi, const int* pos, const float* cos_t, const float* sin_t,
-                        int rope_cols, int head_dim, const void* bias, void* ws, uint64_t ws_bytes,
-                        fls_stream_t s) {
+                        int rope_cols, int head_dim, const void* bias, const float* rscale, float alpha, void* ws,
+                        uint64_t ws_bytes, fls_stream_t s) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
   if (bias && epi == FLS_EPI_SWIGLU) return -4;
   if ((epi == FLS_EPI_SWIGLU || epi == FLS_EPI_ROPE) && (N % 32)) return -2;
@@ -524,11 +526,13 @@ extern "C" int fls_gemm(const void* A, const void* W, void* C, const void* R, in
     return -3;
   if (g_gu_split <= 1 || epi != FLS_EPI_SWIGLU) {
     const int rc = fls_gemm_v11_try(A, W, C, R, M, N, K, lda, ldw, ldc, ldr, epi, pos, cos_t, sin_t, rope_cols,
-                                    head_dim, bias, s);
+                                    head_dim, bias, rscale, alpha, s);
     if (rc) return rc > 0 ? 0 : rc;
   }
   Epi ep{(const half_t*)R, ldr, pos, cos_t, sin_t, rope_cols, head_dim, (const half_t*)bias, N / 2, 0,
          nullptr, nullptr, nullptr, 0, 0};
+  ep.rs = rscale;
+  ep.alpha = alpha;
   auto a = (const half_t*)A;
   auto w = (const half_t*)W;
   auto c = (half_t*)C;

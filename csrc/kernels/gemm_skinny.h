@@ -155,6 +155,7 @@ __global__ __launch_bounds__(256) void gemm_nt_skinny(const half_t* __restrict__
   for (int i = 0; i < RS; ++i) {
     const int m = i * 16 + fr;
     if (m >= M) continue;
+    const float rsc = row_scale(ep, m);
     if constexpr (EPI == EPI_F32) {           // split-K partial slab of this slice (ldc = N floats)
       float* Cf = (float*)C + (size_t)blockIdx.y * ep.part_stride + (size_t)m * ldc;
 #pragma unroll
@@ -164,14 +165,14 @@ __global__ __launch_bounds__(256) void gemm_nt_skinny(const half_t* __restrict__
       for (int j = 0; j < NS / 2; ++j) {
         half4 o;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = (half_t)(silu(acc[i][j][r]) * acc[i][j + NS / 2][r]);
+        for (int r = 0; r < 4; ++r) o[r] = (half_t)(silu(acc[i][j][r] * rsc) * (acc[i][j + NS / 2][r] * rsc));
         *(half4*)(C + (size_t)m * ldc + cbase + 16 * j + 4 * grp) = o;
       }
     } else {
 #pragma unroll
       for (int j = 0; j < NS; ++j) {
         const int n = cbase + 16 * j + 4 * grp;
-        floatx4 a = acc[i][j];
+        floatx4 a = acc[i][j] * rsc;
         if (ep.bias) {
           const half4 b = *(const half4*)(ep.bias + n);
 #pragma unroll
@@ -180,7 +181,7 @@ __global__ __launch_bounds__(256) void gemm_nt_skinny(const half_t* __restrict__
         if constexpr (EPI == FLS_EPI_RESID) {
           const half4 rr = *(const half4*)(ep.R + (size_t)m * ep.ldr + n);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) a[r] += (float)rr[r];
+          for (int r = 0; r < 4; ++r) a[r] = a[r] * ep.alpha + (float)rr[r];
         }
         half4 o;
 #pragma unroll

@@ -44,7 +44,16 @@ struct Epi {
   int ksplit;
   int kslice;
   long long part_stride;
+  // optional per-row scale of the raw product (fp32 [M], row m of A): the RMSNorm statistic
+  // rsqrt(mean(x^2) + eps) of a GEMM that reads the un-normalised hidden state x with the norm
+  // weight folded into W (fused RMSNorm + projection); applied before the bias
+  const float* rs = nullptr;
+  // scale of (product + bias) before the residual add (Granite's residual_multiplier)
+  float alpha = 1.f;
 };
+
+// the per-row scale of row m (1 without one: x * 1.0f is exact, so the unscaled path is unchanged)
+__device__ __forceinline__ float row_scale(const Epi& ep, int m) { return ep.rs ? ep.rs[m] : 1.f; }
 
 // SWIGLU logical row l (gate/up interleaved per 16 rows) -> physical row of [gate; up]
 __device__ __forceinline__ int gu_phys_row(int l, int I) {
@@ -59,13 +68,15 @@ __device__ __forceinline__ void store_pair_off(half_t* __restrict__ C, int ldc, 
   if constexpr (EPI == FLS_EPI_SWIGLU) {
     // pair = (gate, up) of intermediate columns [n_first/2, n_first/2 + 16)
     const int oc = n_first / 2 + off;
+    const float s = row_scale(ep, m);
     half4 o;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) o[r] = (half_t)(silu(acc_a[r]) * acc_b[r]);
+    for (int r = 0; r < 4; ++r) o[r] = (half_t)(silu(acc_a[r] * s) * (acc_b[r] * s));
     *(half4*)(C + (size_t)m * ldc + oc) = o;
     return;
   } else {
-    floatx4 a = acc_a, b = acc_b;
+    const float s = row_scale(ep, m);
+    floatx4 a = acc_a * s, b = acc_b * s;
     if (ep.bias) {
       const half4 ba = *(const half4*)(ep.bias + c0);
       const half4 bb = *(const half4*)(ep.bias + c0 + 16);
@@ -76,7 +87,7 @@ __device__ __forceinline__ void store_pair_off(half_t* __restrict__ C, int ldc, 
       const half4 ra = *(const half4*)(ep.R + (size_t)m * ep.ldr + c0);
       const half4 rb = *(const half4*)(ep.R + (size_t)m * ep.ldr + c0 + 16);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) { a[r] += (float)ra[r]; b[r] += (float)rb[r]; }
+      for (int r = 0; r < 4; ++r) { a[r] = a[r] * ep.alpha + (float)ra[r]; b[r] = b[r] * ep.alpha + (float)rb[r]; }
     }
     half4 oa, ob;
 #pragma unroll
@@ -91,7 +102,8 @@ __device__ __forceinline__ void store_rope_pair(half_t* __restrict__ C, int ldc,
                                                 const floatx4& acc_b, const Epi& ep) {
   const int hd = ep.head_dim, half_hd = hd >> 1;
   const int cb = ca + half_hd;
-  floatx4 a = acc_a, b = acc_b;
+  const float s = row_scale(ep, m);
+  floatx4 a = acc_a * s, b = acc_b * s;
   if (ep.bias) {
     const half4 ba = *(const half4*)(ep.bias + ca);
     const half4 bb = *(const half4*)(ep.bias + cb);
@@ -155,6 +167,7 @@ __device__ __forceinline__ void epilogue_rope(half_t* __restrict__ C, int ldc, i
   int pos[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) pos[u] = ep.pos[min(mrow0 + u * 16, M - 1)];
+  const float* const rsp = ep.rs;
   int f0[4];
   bool rot[4];
   half4 ba[4], bb[4];
@@ -189,13 +202,14 @@ __device__ __forceinline__ void epilogue_rope(half_t* __restrict__ C, int ldc, i
     if (u + 1 < U) load(u + 1, sl ^ 1);
     asm volatile("" ::: "memory");
     const int m = mrow0 + u * 16;
+    const float s = rsp ? rsp[min(m, M - 1)] : 1.f;
     half4 oa[4], ob[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int ta = HD == 128 ? q : (q & 1) + (q >> 1) * 4;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float x1 = acc[u][ta][r] + (float)ba[q][r], x2 = acc[u][ta + HS][r] + (float)bb[q][r];
+        float x1 = acc[u][ta][r] * s + (float)ba[q][r], x2 = acc[u][ta + HS][r] * s + (float)bb[q][r];
         if (rot[q]) {
           const float c = cs[sl][q][r], sv = sn[sl][q][r];
           const float y1 = x1 * c - x2 * sv, y2 = x2 * c + x1 * sv;
@@ -255,11 +269,12 @@ __device__ __forceinline__ void epilogue_quadrant(half_t* __restrict__ C, int ld
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int m = mrow0 + u * 16;
+        const float s = ep.rs ? ep.rs[min(m, M - 1)] : 1.f;
         half4 o[4];
 #pragma unroll
         for (int p = 0; p < 4; ++p)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) o[p][r] = (half_t)(silu(acc[u][2 * p][r]) * acc[u][2 * p + 1][r]);
+          for (int r = 0; r < 4; ++r) o[p][r] = (half_t)(silu(acc[u][2 * p][r] * s) * (acc[u][2 * p + 1][r] * s));
 #pragma unroll
         for (int p = 0; p < 4; p += 2) {
           const uint4 v = wide_pair(o[p], o[p + 1]);
@@ -296,9 +311,10 @@ __device__ __forceinline__ void epilogue_quadrant(half_t* __restrict__ C, int ld
           if (u + 1 < U) load(u + 1, sl ^ 1);
           asm volatile("" ::: "memory");
           const int m = mrow0 + u * 16;
+          const float s = ep.rs ? ep.rs[min(m, M - 1)] : 1.f;
 #pragma unroll
           for (int p = 0; p < 4; ++p) {
-            floatx4 a = acc[u][2 * p], b = acc[u][2 * p + 1];
+            floatx4 a = acc[u][2 * p] * s, b = acc[u][2 * p + 1] * s;
             if constexpr (decltype(has_bias)::value) {
 #pragma unroll
               for (int r = 0; r < 4; ++r) { a[r] += (float)ba[p][r]; b[r] += (float)bb[p][r]; }
@@ -307,7 +323,7 @@ __device__ __forceinline__ void epilogue_quadrant(half_t* __restrict__ C, int ld
               half4 ra, rb;
               unwide_pair(rw[sl][p], ra, rb);
 #pragma unroll
-              for (int r = 0; r < 4; ++r) { a[r] += (float)ra[r]; b[r] += (float)rb[r]; }
+              for (int r = 0; r < 4; ++r) { a[r] = a[r] * ep.alpha + (float)ra[r]; b[r] = b[r] * ep.alpha + (float)rb[r]; }
             }
             half4 oa, ob;
 #pragma unroll

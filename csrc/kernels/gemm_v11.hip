@@ -336,7 +336,8 @@ extern "C" int fls_gemm_set_v11(int mode) {
 // the GEMM, 0 when it does not apply, < 0 on a launch error.
 extern "C" int fls_gemm_v11_try(const void* A, const void* W, void* C, const void* R, int M, int N, int K, int lda,
                                 int ldw, int ldc, int ldr, int epi, const int* pos, const float* cos_t,
-                                const float* sin_t, int rope_cols, int head_dim, const void* bias, fls_stream_t s) {
+                                const float* sin_t, int rope_cols, int head_dim, const void* bias,
+                                const float* rscale, float alpha, fls_stream_t s) {
   using namespace v11;
   if (!g_v11 || M < TM || N % TN || K % TK || (K / TK) % 2 || lda % 8 || ldw % 8) return 0;
   if (g_v11 == 1) {
@@ -355,6 +356,8 @@ extern "C" int fls_gemm_v11_try(const void* A, const void* W, void* C, const voi
   if (epi == FLS_EPI_RESID && (ldr % 8 || ((uintptr_t)R & 15))) return 0;
   Epi ep{(const half_t*)R, ldr, pos, cos_t, sin_t, rope_cols, head_dim, (const half_t*)bias, N / 2, 0,
          nullptr, nullptr, nullptr, 0, 0};
+  ep.rs = rscale;
+  ep.alpha = alpha;
   auto a = (const half_t*)A;
   auto w = (const half_t*)W;
   auto c = (half_t*)C;

@@ -63,7 +63,7 @@ class Piece(ctypes.Structure):
                 ("kind", ctypes.c_int32), ("pad", ctypes.c_int32)]
 
 
-KERNELS_ABI = 20   # bumped whenever a C signature in csrc/include/fls.h changes
+KERNELS_ABI = 21   # bumped whenever a C signature in csrc/include/fls.h changes
 
 
 def _load_kernels(path: str = _KERNELS):
@@ -76,7 +76,10 @@ def _load_kernels(path: str = _KERNELS):
                            "rebuild with python -m flexible_llm_sharding_amd._native.build")
     _bind(lib, "fls_gemm", c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
           c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
-          c_uint64, c_void_p)
+          c_float, c_void_p, c_uint64, c_void_p)
+    _bind(lib, "fls_row_rstd", c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p)
+    _bind(lib, "fls_fold_norm", c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p)
+    _bind(lib, "fls_copy_rows", c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p)
     _bind(lib, "fls_gemm_set_splitk", c_int, c_int)
     _bind(lib, "fls_gemm_set_gu_split", c_int, c_int)
     _bind(lib, "fls_gemm_set_row_chunk", c_int, c_int)
@@ -105,8 +108,8 @@ def _load_kernels(path: str = _KERNELS):
           c_int, c_float, c_void_p)
     _bind(lib, "fls_headnorm_rope", c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
           c_void_p, c_void_p, c_int, c_float, c_void_p)
-    _bind(lib, "fls_embed", c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p)
-    _bind(lib, "fls_softmax_rows", c_int, c_void_p, c_void_p, c_int, c_int, c_void_p)
+    _bind(lib, "fls_embed", c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p)
+    _bind(lib, "fls_softmax_rows", c_int, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p)
     _bind(lib, "fls_cast_f16", c_int, c_void_p, c_void_p, c_int, c_uint64, c_void_p)
     _bind(lib, "fls_gemv_skinny", c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
           c_void_p)

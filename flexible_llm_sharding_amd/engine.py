@@ -41,7 +41,7 @@ from .ops import get_ops
 from .parallel.comm import Comm
 from .parallel.pipeline import StageInbox, build_programs, host_wait, rank_items, rx_key
 from .parallel.planner import ShardPlan, make_plan
-from .runtime.activations import ActivationStore
+from .runtime.activations import ActivationStore, ActRing
 from .runtime.batch import Q_BLOCK, Q_BLOCK_MHA, PackedBatch, pack_prompts, split_microbatches
 from .runtime.prefetch import ShardPrefetcher
 from .runtime.weights import LayerSource
@@ -156,7 +156,7 @@ class ShardedRunner:
                 # provisional (the call's token count is unknown yet); _plan_call is authoritative
                 token_budget, mlp_chunk, attn_rows, qkv_chunk, est = plan_for_vram(
                     cfg, self._vram_cap, layer_num_per_shard, n_slots, token_budget, mlp_chunk,
-                    overhead=self._outside)
+                    overhead=self._outside, fused_norm=self._fused_norm_planned())
             except ValueError:
                 token_budget, mlp_chunk, attn_rows, qkv_chunk, est = 1024, 1024, 0, 0, 0
             self.vram_plan = {"token_budget": token_budget, "mlp_chunk": mlp_chunk, "attn_rows": attn_rows,
@@ -195,6 +195,13 @@ class ShardedRunner:
             prefetcher = PiecePoolPrefetcher(source, self.names, my, self.dev)
         self.prefetcher = prefetcher or ShardPrefetcher(source, self.names, my, self.dev,
                                                         n_slots=n_slots, resident=resident, keep=keep)
+        # RMSNorm + QKV fused on the GPU: ln1 folded into W_qkv as each layer lands (on the copy
+        # stream, before the layer's ready event), the row statistic applied in the QKV epilogue
+        self.ctx.fused_norm = self._fused_norm_planned()
+        if self.ctx.fused_norm:
+            from .models.llama import fold_layer_norms
+            ops = self.ops
+            self.prefetcher.on_load = lambda views: fold_layer_norms(ops, views)
         self.h2d_stream = torch.cuda.Stream(self.dev) if self.cuda else None
         self.d2h_stream = torch.cuda.Stream(self.dev) if self.cuda else None
         if self.cuda:
@@ -232,8 +239,13 @@ class ShardedRunner:
         self._n_decoders = sum(1 for n in self.names if layer_kind(n) == "decoder")
         self._W_all: Dict[str, Dict[str, torch.Tensor]] = {}
         self._h2d0: Optional[int] = None     # prefetcher byte count at the start of the next call
+        self._ring: Optional[ActRing] = None
 
     # ----------------------------------------------------------- helpers
+    def _fused_norm_planned(self) -> bool:
+        """RMSNorm + QKV fused into one GEMM (HIP backend; FLS_QKV_FOLD=0 turns it off)."""
+        return bool(self.cuda and getattr(self.ops, "fused_norm", False) and knobs.get_int("FLS_QKV_FOLD"))
+
     def tokenize(self, prompts) -> List[TokenizedPrompt]:
         if self.tok is None:
             raise RuntimeError("no tokenizer")
@@ -413,7 +425,8 @@ class ShardedRunner:
         tb, mc, ar, qc, est = plan_for_vram(self.cfg, self._vram_cap, self.lnps, self.prefetcher.n_slots, tb, mc,
                                         total_tokens=max(1, total), max_prompt_rows=max(rows or [0]),
                                         overhead=self._outside,
-                                        weight_bytes=self.prefetcher.planned_hbm_bytes() if self.cuda else None)
+                                        weight_bytes=self.prefetcher.planned_hbm_bytes() if self.cuda else None,
+                                        fused_norm=self.ctx.fused_norm)
         self.token_budget, self.mlp_chunk = tb, mc
         self.ctx.mlp_chunk, self.ctx.attn_rows, self.ctx.qkv_chunk = mc, ar, qc
         self.vram_plan.update({"token_budget": tb, "mlp_chunk": mc, "attn_rows": ar, "qkv_chunk": qc,
@@ -482,6 +495,7 @@ class ShardedRunner:
             self.ck = None
             self.prog = self.inbox = None
             self.pbar = None
+            self.ring: Optional[ActRing] = None      # hidden-state slots (storage cpu / disk, local passes)
 
     def _run_batches(self, tps, batches, t_start: float) -> List[Optional[np.ndarray]]:
         metas = [b.device_tensors(self.dev) for b in batches]   # all uploads before any compute
@@ -494,14 +508,19 @@ class ShardedRunner:
         self._h2d0 = None
         px = self._Pass(tps, batches, metas, store, self.schedule(len(batches)))
         collective = getattr(pf, "collective", False)
+        # the resume point first: ranks agree on it with a collective on the default group, which
+        # every rank must reach before any weight gather (a rank without prompts included)
+        px.ck, k0, ck_loaded = self._open_checkpoint(tps)
         if not px.items and self.my_shards and collective:
             # a data-parallel rank with no prompts in this call still joins every shard's weight
-            # all-gather, so all ranks issue the same collective sequence
-            for k in range(len(self.my_shards)):
+            # all-gather from the resume point on, so all ranks issue the same collective sequence
+            for k in range(k0, len(self.my_shards)):
                 pf.acquire(k)
                 pf.prefetch(k + 1)
                 pf.release(k)
-        px.ck, k0, ck_loaded = self._open_checkpoint(tps)
+                if px.ck is not None and self._ckpt_due(k):
+                    # an empty checkpoint, so the ranks' common resume point still advances
+                    px.ck.commit(self._ckpt_key(k), [], self.act_dtype)
         if k0 > 0 or ck_loaded:
             for b, t in ck_loaded.items():
                 store.put(b, t.to(self.dev))
@@ -514,6 +533,14 @@ class ShardedRunner:
             px.inbox = self._get_inbox()
             px.inbox.begin_call(max([self._rx_bytes(k, batches[b]) for (k, b), src in zip(px.items, px.prog.src)
                                      if src is not None] or [0]))
+        if px.prog is None and self.cuda and self.storage != "gpu" and px.items:
+            # hidden states in fixed HBM slots: 1 (the call is one micro-batch: it never leaves HBM)
+            # or 2 (computing + landing; the zigzag carries fit) — exactly the plan's live states
+            if self._ring is None:
+                self._ring = ActRing(self.dev, self.act_dtype, 1)
+            n_ring = 1 if len(batches) == 1 else 2
+            self._ring.resize(n_ring, max(b.num_tokens for b in batches) * self.cfg.hidden_size)
+            px.ring = self._ring
         if self.my_shards and px.items:
             pf.prefetch(px.items[0][0])
         px.pbar = self._progress(len(px.items))
@@ -602,11 +629,19 @@ class ShardedRunner:
         px.dst_rank = self._owner(last + 1) if (mp and last + 1 < self.L) else self.comm.rank
 
     def _take_state(self, px: "_Pass", k: int, b: int):
-        """Input activation of (shard k, micro-batch b) held on this rank."""
+        """Input activation of (shard k, micro-batch b) held on this rank (with the activation
+        ring: in a slot acquired for it — the embedding writes into it, or the H2D lands in it)."""
+        ring, batch = px.ring, px.batches[b]
         if self.my_shards[k][0] == 0:
+            if ring is not None:
+                self.ctx.embed_out = ring.acquire(b, (batch.num_tokens, self.cfg.hidden_size),
+                                                  torch.cuda.current_stream(self.dev))
             return None
         if b in px.carry:
             return px.carry.pop(b)
+        shape = self._state_shape(self.my_shards[k][0] - 1, batch)
+        if ring is not None and shape[0] == batch.num_tokens:
+            return px.store.get(b, out=ring.acquire(b, shape, px.store.h2d))
         return px.store.get(b)
 
     def _prefetch_activation(self, px: "_Pass", idx: int) -> None:
@@ -648,6 +683,11 @@ class ShardedRunner:
     def _emit(self, px: "_Pass", k: int, b: int, state, from_rx: bool):
         """Where the output of (shard k, micro-batch b) goes -> the send's work handle, if sent."""
         last = self.my_shards[k][-1]
+        ring = px.ring
+        if ring is not None and ring.owns(b) and ring.holds(state) < 0:
+            # the layer's output left the slot (the pruned last decoder layer, norm, head): the
+            # slot's last reader is the compute just enqueued
+            ring.release(b, self._event())
         if from_rx and last < self.L - 1 and px.dst_rank == self.comm.rank:
             # the residual GEMMs update the received state in place, so it may still BE the
             # receive-ring slot that inbox.release() hands to the next receive: a state that
@@ -660,13 +700,23 @@ class ShardedRunner:
             w = self.comm.isend(st, px.dst_rank)
             px.sends.append((st, w))
             return w
-        elif self.storage != "gpu" and px.pos.get((k + 1, b), len(px.items)) - px.pos[(k, b)] <= self.CARRY_WINDOW:
+        elif (self.storage != "gpu" and px.pos.get((k + 1, b), len(px.items)) - px.pos[(k, b)]
+              <= (self.CARRY_WINDOW if ring is None or ring.n >= 2 else 1)):
             # re-used within CARRY_WINDOW micro-batch computes (the zigzag boundary micro-batch
-            # and its neighbour): a PCIe round trip would only add traffic, keep it in HBM
+            # and its neighbour): a PCIe round trip would only add traffic, keep it in HBM (with
+            # two ring slots both carries of a zigzag boundary fit: the neighbour is consumed
+            # before anything else needs a slot)
             px.carry[b] = state
         else:
-            px.store.put(b, state)
+            ev = px.store.put(b, state)
+            if ring is not None and ring.owns(b):
+                ring.release(b, ev if ev is not None else self._event())
         return None
+
+    def _event(self):
+        e = torch.cuda.Event()
+        e.record(torch.cuda.current_stream(self.dev))
+        return e
 
     def _close_weights(self, px: "_Pass", ok: bool) -> None:
         """End of a pass: release the held shard; after an aborted one forget every loaded-but-
@@ -682,6 +732,9 @@ class ShardedRunner:
                 pf.discard_loaded()
             if px.inbox is not None:
                 px.inbox.abort()
+            if px.ring is not None:
+                px.ring.reset()
+                self.ctx.embed_out = None
             return
         if px.items or (collective and self.my_shards):
             # the next call's loads continue the slot round-robin (a data-parallel rank with no

@@ -36,7 +36,6 @@ KNOBS: Dict[str, Tuple[str, str]] = {
     "FLS_SKINNY": ("1", "skinny-M GEMM for 17-192 rows: 0 off, 1 auto, 2 forced"),
     "FLS_ATTN_SPLIT": ("0", "split-KV slices of the range-2 attention kernel: 0 by grid size, 1 off, n"),
     "FLS_CHUNK_ALIGN": ("3072", "row multiple of the QKV / MLP chunks (3072 = 8 v11 tiles)"),
-    "FLS_QKV_STREAMS": ("2", "RMSNorm + QKV row chunks on 1 or 2 alternating streams"),
     "FLS_SPECULATIVE_PREFETCH": ("", "0 / 1: force the next call's first-shard prefetch off / on"),
     "FLS_R2_QBLOCK": ("32", "query rows per range-2 (generation-step) attention item: 32 or 64"),
     "FLS_QKV_FOLD": ("1", "0: RMSNorm + QKV as two kernels instead of the row-scaled GEMM on the "

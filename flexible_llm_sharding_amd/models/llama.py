@@ -180,7 +180,11 @@ class ExecContext:
     prune_last: bool = True
     last_decoder: str = ""
     ws: Optional[Workspace] = None          # scratch arena (None: fresh allocations, e.g. graph capture)
-    side_stream: Optional[object] = None    # second compute stream (two-stream QKV chunks), made on first use
+    # RMSNorm + QKV projection fused (HIP): every decoder layer's ln1 is folded into its W_qkv when
+    # the weights land (fold_layer_norms, called by the prefetcher on its copy stream) and the QKV
+    # GEMM reads the raw hidden state, scaling each row by its rsqrt(mean(x^2) + eps) in the epilogue
+    fused_norm: bool = False
+    embed_out: Optional[torch.Tensor] = None   # destination of the next embedding gather (engine's ring)
 
     def phase(self, *shapes) -> None:
         """Start a workspace phase that will carve ``shapes`` (rows, cols) in order."""
@@ -190,32 +194,34 @@ class ExecContext:
     def scratch(self, rows: int, cols: int) -> Optional[torch.Tensor]:
         return self.ws.take(rows, cols) if self.ws is not None else None
 
+    def scratch_f32(self, n: int) -> Optional[torch.Tensor]:
+        """n fp32 values from the current phase (2 fp16 columns each); reserve (1, 2 n)."""
+        t = self.scratch(1, 2 * n)
+        return t.view(torch.float32).view(n) if t is not None else None
+
 
 def run_embed(ctx: ExecContext, W: Dict[str, torch.Tensor], meta: dict) -> torch.Tensor:
-    x = ctx.ops.embed(meta["ids"], W["embed"], ctx.act_dtype)
-    if ctx.cfg.embedding_multiplier != 1.0:          # Granite: GraniteModel scales the embeddings
-        x.mul_(ctx.cfg.embedding_multiplier)
-    return x
+    """Embedding gather (Granite: scaled by embedding_multiplier in the same kernel), into the
+    engine's activation buffer when it set one."""
+    out, ctx.embed_out = ctx.embed_out, None
+    return ctx.ops.embed(meta["ids"], W["embed"], ctx.act_dtype, scale=ctx.cfg.embedding_multiplier, out=out)
 
 
 def _resid(ctx: ExecContext, a: torch.Tensor, w: torch.Tensor, x: torch.Tensor, bias=None) -> torch.Tensor:
-    """x + a @ w^T (+ bias): the fused residual GEMM (in place on x).  Granite's
-    residual_multiplier r: x + fp16(fp16(a @ w^T) * r), HF GraniteDecoderLayer's roundings, as a
-    plain GEMM and an in-place add."""
-    r = ctx.cfg.residual_multiplier
-    if r == 1.0:
-        return ctx.ops.linear_residual(a, w, x, bias=bias)
-    y = ctx.ops.linear(a, w)
-    if bias is not None:
-        y.add_(bias)
-    return x.add_(y.mul_(r))
+    """x + r * (a @ w^T (+ bias)): the fused residual GEMM, in place on x (r: Granite's
+    residual_multiplier, scaled in the epilogue; 1 otherwise)."""
+    return ctx.ops.linear_residual(a, w, x, bias=bias, alpha=ctx.cfg.residual_multiplier)
+
+
+def fold_layer_norms(ops, views: Dict[str, torch.Tensor]) -> None:
+    """Fold a decoder layer's input RMSNorm weight into its QKV projection, in place on the
+    loaded weights (W_qkv[n, k] *= ln1[k]): the fused path then needs no normalised copy of the
+    hidden state (ExecContext.fused_norm).  Called once per load, on the stream that loaded them."""
+    if "wqkv" in views and "ln1" in views:
+        ops.fold_norm(views["wqkv"], views["ln1"])
 
 
 CHUNK_ALIGN = knobs.get_int("FLS_CHUNK_ALIGN")   # A/B knob (256: round 3's chunks)
-# RMSNorm + QKV row chunks alternate between two streams over the two halves of the normed buffer,
-# so one chunk's GEMM fills the CUs the other's last tile round leaves idle (2, default: +1.1% on the
-# capped 70B headline, profiles/r4_gemm/qkv_two_streams; A/B: 1 = one stream)
-QKV_STREAMS = knobs.get_int("FLS_QKV_STREAMS")
 
 
 def balanced_step(rows: int, limit: int, align: int = 0) -> int:
@@ -237,80 +243,73 @@ def balanced_step(rows: int, limit: int, align: int = 0) -> int:
 
 
 def _attn_inputs(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, pos: torch.Tensor,
-                 last_idx: Optional[torch.Tensor], prune: bool) -> torch.Tensor:
-    """RMSNorm + QKV projection (+ RoPE, + bias) of every row into one [T, qkv] buffer, in row
-    chunks of ``ctx.qkv_chunk`` (only a chunk of normed rows is ever alive: the workspace holds
-    [normed chunk | QKV]).  ``prune`` (the last decoder layer): K/V (+ RoPE on K) for every row,
-    Q only for the scored rows, scattered into the Q columns of those rows — the other rows' Q
-    columns stay unwritten, the last layer's attention work items (``work_last``) query only
-    scored rows (Q is q_size / qkv_size of the projection: 80% for Llama-2-70B)."""
+                 last_idx: Optional[torch.Tensor], prune: bool, last_pos: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """RMSNorm + QKV projection (+ RoPE, + bias) of every row into one [T, qkv] buffer.
+    ``prune`` (the last decoder layer): K/V (+ RoPE on K) for every row, Q only for the scored rows,
+    scattered into the Q columns of those rows — the other rows' Q columns stay unwritten, the last
+    layer's attention work items (``work_last``) query only scored rows (Q is q_size / qkv_size of
+    the projection: 80% for Llama-2-70B).
+
+    Fused (``ctx.fused_norm``, HIP): one GEMM over the raw hidden state with ln1 folded into W_qkv
+    and each row scaled by its rsqrt(mean(x^2) + eps) in the epilogue — the workspace holds only
+    [QKV | row statistics], so every row goes through one launch.  Otherwise an explicit RMSNorm
+    per row chunk of ``ctx.qkv_chunk`` (the workspace holds [normed chunk | QKV])."""
     cfg, ops = ctx.cfg, ctx.ops
     H, Qn, qs = cfg.hidden_size, cfg.qkv_size, cfg.q_size
     nq, nkv, hd = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
     eps = cfg.rms_norm_eps
     T0 = x.shape[0]
+    w, b = W["wqkv"], W.get("bqkv")
+
+    def proj(h, wr, p, n_q, n_k, bias, out=None, rscale=None):
+        kw = {"rscale": rscale} if rscale is not None else {}     # (fused: HIP only)
+        if cfg.qk_norm:           # Qwen3: per-head RMSNorm on q / k before RoPE
+            return ops.qkv_norm_rope(h, wr, p, ctx.cos, ctx.sin, n_q, n_k, hd, W["qn"], W["kn"], eps,
+                                     bias=bias, out=out, **kw)
+        return ops.qkv_rope(h, wr, p, ctx.cos, ctx.sin, n_q, n_k, hd, bias=bias, out=out, **kw)
+
+    def put(r, dst):
+        if r.data_ptr() != dst.data_ptr():
+            dst.copy_(r)
+
+    if ctx.fused_norm:
+        ctx.phase((T0, Qn), (1, 2 * T0))
+        qkv = ctx.scratch(T0, Qn)
+        if qkv is None:
+            qkv = torch.empty(T0, Qn, dtype=x.dtype, device=x.device)
+        rstd = ops.row_rstd(x, eps, out=ctx.scratch_f32(T0))
+        if not prune:
+            put(proj(x, w, pos, nq, nkv, b, out=qkv, rscale=rstd), qkv)
+            return qkv
+        put(proj(x, w[qs:], pos, 0, nkv, b[qs:] if b is not None else None, out=qkv[:, qs:], rscale=rstd),
+            qkv[:, qs:])
+        # Q of the scored rows: their raw rows gathered, scaled by their own statistic
+        xq = ops.gather_rows(x, last_idx)
+        q = proj(xq, w[:qs], last_pos, nq, 0, b[:qs] if b is not None else None,
+                 rscale=ops.row_rstd(xq, eps))
+        ops.scatter_rows(q, last_idx, qkv[:, :qs])
+        return qkv
+
     step = balanced_step(T0, ctx.qkv_chunk) if ctx.qkv_chunk else T0
     ctx.phase((step, H), (T0, Qn))
     hbuf = ctx.scratch(step, H)
     qkv = ctx.scratch(T0, Qn)
     if qkv is None:
         qkv = torch.empty(T0, Qn, dtype=x.dtype, device=x.device)
-    w, b = W["wqkv"], W.get("bqkv")
-
-    def proj(h, wr, p, n_q, n_k, bias, out=None):
-        if cfg.qk_norm:           # Qwen3: per-head RMSNorm on q / k before RoPE
-            return ops.qkv_norm_rope(h, wr, p, ctx.cos, ctx.sin, n_q, n_k, hd, W["qn"], W["kn"], eps,
-                                     bias=bias, out=out)
-        return ops.qkv_rope(h, wr, p, ctx.cos, ctx.sin, n_q, n_k, hd, bias=bias, out=out)
-
-    if (QKV_STREAMS == 2 and not prune and hbuf is not None and x.is_cuda and T0 > step
-            and step % 512 == 0):
-        _qkv_two_streams(ctx, x, pos, W["ln1"], hbuf, qkv, step // 2,
-                         lambda h, p, out: proj(h, w, p, nq, nkv, b, out=out))
-        return qkv
     for s in range(0, T0, step):
         e = min(T0, s + step)
         h = ops.rmsnorm(x[s:e], W["ln1"], eps, out=hbuf[:e - s] if hbuf is not None else None)
         if prune:
-            dst = qkv[s:e, qs:]
-            r = proj(h, w[qs:], pos[s:e], 0, nkv, b[qs:] if b is not None else None, out=dst)
+            put(proj(h, w[qs:], pos[s:e], 0, nkv, b[qs:] if b is not None else None, out=qkv[s:e, qs:]),
+                qkv[s:e, qs:])
         else:
-            dst = qkv[s:e]
-            r = proj(h, w, pos[s:e], nq, nkv, b, out=dst)
-        if r.data_ptr() != dst.data_ptr():
-            dst.copy_(r)
+            put(proj(h, w, pos[s:e], nq, nkv, b, out=qkv[s:e]), qkv[s:e])
         del h
     if prune:
-        idx = last_idx
-        hq = ops.rmsnorm(x.index_select(0, idx), W["ln1"], eps)
-        q = proj(hq, w[:qs], pos.index_select(0, idx), nq, 0, b[:qs] if b is not None else None)
-        qkv[:, :qs].index_copy_(0, idx if idx.dtype == torch.int64 else idx.long(), q)
+        hq = ops.rmsnorm(ops.gather_rows(x, last_idx), W["ln1"], eps)
+        q = proj(hq, w[:qs], last_pos, nq, 0, b[:qs] if b is not None else None)
+        ops.scatter_rows(q, last_idx, qkv[:, :qs])
     return qkv
-
-
-def _qkv_two_streams(ctx: ExecContext, x: torch.Tensor, pos: torch.Tensor, ln1: torch.Tensor,
-                     hbuf: torch.Tensor, qkv: torch.Tensor, half: int, proj) -> None:
-    """RMSNorm + QKV over row chunks of ``half`` rows, chunk i on stream i % 2 with normed half
-    buffer i % 2 (its previous user, chunk i - 2, ran on the same stream): the two streams' GEMMs
-    overlap, so a chunk's partial last round of tiles shares the CUs with the next chunk's first.
-    Same kernels per row as one stream (bitwise equal)."""
-    ops, cfg = ctx.ops, ctx.cfg
-    main = torch.cuda.current_stream(x.device)
-    if ctx.side_stream is None:
-        ctx.side_stream = torch.cuda.Stream(x.device)
-    side = ctx.side_stream
-    side.wait_stream(main)                            # x and the weights are ready
-    bufs = (hbuf[:half], hbuf[half:2 * half])
-    T0 = x.shape[0]
-    for i, s in enumerate(range(0, T0, half)):
-        e = min(T0, s + half)
-        with torch.cuda.stream(main if i % 2 == 0 else side):
-            h = ops.rmsnorm(x[s:e], ln1, cfg.rms_norm_eps, out=bufs[i % 2][:e - s])
-            dst = qkv[s:e]
-            r = proj(h, pos[s:e], dst)
-            if r.data_ptr() != dst.data_ptr():
-                dst.copy_(r)
-    main.wait_stream(side)                            # every row's Q / K / V before the attention
 
 
 def _attention_whole(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, batch, meta: dict,
@@ -318,7 +317,7 @@ def _attention_whole(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tens
     """Attention phase over the whole micro-batch: QKV of every row, one attention launch, O
     projection + residual (in place on x; the pruned last layer returns its scored rows)."""
     cfg, ops = ctx.cfg, ctx.ops
-    qkv = _attn_inputs(ctx, W, x, meta["positions"], meta["last_idx"], prune)
+    qkv = _attn_inputs(ctx, W, x, meta["positions"], meta["last_idx"], prune, meta["last_pos"])
     kv0 = None
     pe = ctx.prefix_entry
     if pe is not None:
@@ -326,12 +325,11 @@ def _attention_whole(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tens
         if batch.kv_cached:                  # prefix K/V of every prompt from the cache
             kv0 = pe.buffer(layer_name)
         elif "pfx_src" in meta:              # full pass: keep the prefix rows' post-RoPE K/V
-            pe.buffer(layer_name, create=True).index_copy_(
-                0, meta["pfx_dst"], qkv[:, qs:qs + kv].index_select(0, meta["pfx_src"]))
+            ops.copy_rows(qkv[:, qs:qs + kv], meta["pfx_src"], pe.buffer(layer_name, create=True), meta["pfx_dst"])
         if "sfx_src" in meta:                # the suffix rows computed now (suffix K/V reuse)
             if kv0 is None:
                 kv0 = pe.buffer(layer_name, create=True)
-            kv0.index_copy_(0, meta["sfx_dst"], qkv[:, qs:qs + kv].index_select(0, meta["sfx_src"]))
+            ops.copy_rows(qkv[:, qs:qs + kv], meta["sfx_src"], kv0, meta["sfx_dst"])
     work_items = getattr(ops, "uses_work_items", False)
     if prune:
         attn_arg = meta["work_last"] if work_items else batch.last_segments
@@ -349,8 +347,8 @@ def _attention_whole(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tens
     del qkv
     if prune:
         idx = meta["last_idx"]
-        a = a.index_select(0, idx)
-        x = x.index_select(0, idx)
+        a = ops.gather_rows(a, idx)
+        x = ops.gather_rows(x, idx)
     return _resid(ctx, a, W["wo"], x, bias=W.get("bo"))
 
 
@@ -369,7 +367,7 @@ def _attention_grouped(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Te
     outs = []
     for g in batch.group_tensors(x.device, ctx.attn_rows):
         r0, r1 = g["r0"], g["r1"]
-        qkv = _attn_inputs(ctx, W, x[r0:r1], pos[r0:r1], g["last_local"], prune)
+        qkv = _attn_inputs(ctx, W, x[r0:r1], pos[r0:r1], g["last_local"], prune, g["last_pos"])
         if prune:
             arg = g["work_last"] if work_items else g["last_segments"]
         else:
@@ -380,7 +378,7 @@ def _attention_grouped(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Te
         if prune:
             li = g["last_local"]
             if li.numel():
-                outs.append(_resid(ctx, a.index_select(0, li), W["wo"], x[r0:r1].index_select(0, li),
+                outs.append(_resid(ctx, ops.gather_rows(a, li), W["wo"], ops.gather_rows(x[r0:r1], li),
                                    bias=W.get("bo")))
         else:
             xr = x[r0:r1]

@@ -62,6 +62,10 @@ class MoeRoute:
 class HipOps:
     name = "hip"
     uses_work_items = True
+    # RMSNorm + projection as one GEMM on the raw hidden state: row statistics (row_rstd), the norm
+    # weight folded into the projection weight once per load (fold_norm), the statistic applied in
+    # the GEMM epilogue (gemm(rscale=...)); models/llama.py _attn_inputs
+    fused_norm = True
 
     def __init__(self):
         self.k = _native.kernels()
@@ -80,9 +84,15 @@ class HipOps:
     # ---------------------------------------------------------------- GEMM
     def gemm(self, x: torch.Tensor, w: torch.Tensor, epi: int = EPI_NONE, out: torch.Tensor = None,
              resid: torch.Tensor = None, positions=None, cos=None, sin=None, rope_cols: int = 0,
-             head_dim: int = 0, bias: torch.Tensor = None) -> torch.Tensor:
+             head_dim: int = 0, bias: torch.Tensor = None, rscale: torch.Tensor = None,
+             alpha: float = 1.0) -> torch.Tensor:
+        """rscale ([M] fp32): per-row scale of the raw product (before bias / epilogue); alpha:
+        RESID's C = alpha * (product + bias) + R."""
         _f16(x, "x")
         _f16(w, "w")
+        if rscale is not None and (rscale.dtype != torch.float32 or not rscale.is_cuda
+                                   or rscale.numel() < x.shape[0] or not rscale.is_contiguous()):
+            raise TypeError("rscale must be a contiguous fp32 CUDA vector with one entry per row")
         M, K = x.shape
         N, K2 = w.shape
         if K != K2:
@@ -102,6 +112,7 @@ class HipOps:
                              cos.data_ptr() if cos is not None else None,
                              sin.data_ptr() if sin is not None else None,
                              rope_cols, head_dim, bias.data_ptr() if bias is not None else None,
+                             rscale.data_ptr() if rscale is not None else None, float(alpha),
                              ws.data_ptr() if ws is not None else None, ws.numel() if ws is not None else 0, _stream())
         _chk(rc, "fls_gemm")
         return out
@@ -160,38 +171,84 @@ class HipOps:
             return self.gemv_skinny(x, w)
         return self.gemm(x, w)
 
-    def linear_residual(self, x, w, resid, bias=None):
-        """resid += x @ w^T (+ bias), in place."""
+    def linear_residual(self, x, w, resid, bias=None, alpha: float = 1.0):
+        """resid += alpha * (x @ w^T (+ bias)), in place (alpha: Granite's residual_multiplier)."""
         _f16(resid, "resid")
-        return self.gemm(x, w, EPI_RESID, out=resid, resid=resid, bias=bias)
+        return self.gemm(x, w, EPI_RESID, out=resid, resid=resid, bias=bias, alpha=alpha)
 
-    def swiglu_up(self, x, wgu, out=None):
+    def swiglu_up(self, x, wgu, out=None, rscale=None):
         """silu(x @ gate^T) * (x @ up^T) with wgu = [gate; up]."""
-        return self.gemm(x, wgu, EPI_SWIGLU, out=out)
+        return self.gemm(x, wgu, EPI_SWIGLU, out=out, rscale=rscale)
 
-    def qkv_rope(self, x, wqkv, positions, cos, sin, n_q_heads, n_kv_heads, head_dim, bias=None, out=None):
+    def row_rstd(self, x, eps, row_idx=None, out=None):
+        """[rows] fp32 rsqrt(mean(x[row]^2) + eps) (rows = row_idx or every row of x)."""
+        _f16(x, "x")
+        rows = row_idx.shape[0] if row_idx is not None else x.shape[0]
+        r = out if out is not None else torch.empty(rows, dtype=torch.float32, device=x.device)
+        if row_idx is not None and (row_idx.dtype != torch.int32 or not row_idx.is_cuda):
+            raise TypeError("row_idx must be int32 CUDA")
+        _chk(self.k.fls_row_rstd(x.data_ptr(), x.stride(0), row_idx.data_ptr() if row_idx is not None else None,
+                                 rows, x.shape[1], float(eps), r.data_ptr(), _stream()), "fls_row_rstd")
+        return r
+
+    def fold_norm(self, w, gamma):
+        """w[n, k] *= gamma[k] in place (fp16): the RMSNorm weight folded into its projection."""
+        _f16(w, "w")
+        _f16(gamma, "gamma")
+        if gamma.numel() != w.shape[-1] or not gamma.is_contiguous():
+            raise ValueError(f"gamma must be a contiguous [{w.shape[-1]}] vector")
+        _chk(self.k.fls_fold_norm(w.data_ptr(), w.stride(0), w.shape[0], w.shape[1], gamma.data_ptr(), _stream()),
+             "fls_fold_norm")
+
+    def copy_rows(self, x, src_idx, y, dst_idx):
+        """y[dst_idx[r]] = x[src_idx[r]] (int32 CUDA indices; None = identity; rows of x.shape[1])."""
+        _f16(x, "x")
+        _f16(y, "y")
+        idx = src_idx if src_idx is not None else dst_idx
+        for t in (src_idx, dst_idx):
+            if t is not None and (t.dtype != torch.int32 or not t.is_cuda):
+                raise TypeError("row indices must be int32 CUDA")
+        if x.shape[1] != y.shape[1]:
+            raise ValueError(f"row width mismatch {tuple(x.shape)} -> {tuple(y.shape)}")
+        rows = idx.shape[0] if idx is not None else x.shape[0]
+        _chk(self.k.fls_copy_rows(x.data_ptr(), x.stride(0), src_idx.data_ptr() if src_idx is not None else None,
+                                  y.data_ptr(), y.stride(0), dst_idx.data_ptr() if dst_idx is not None else None,
+                                  rows, x.shape[1], _stream()), "fls_copy_rows")
+        return y
+
+    def gather_rows(self, x, idx, out=None):
+        """x[idx] into a new (or ``out``) [len(idx), H] tensor."""
+        y = out if out is not None else torch.empty(idx.shape[0], x.shape[1], dtype=x.dtype, device=x.device)
+        return self.copy_rows(x, idx, y, None)
+
+    def scatter_rows(self, x, idx, y):
+        """y[idx] = x in place (distinct indices)."""
+        return self.copy_rows(x, None, y, idx)
+
+    def qkv_rope(self, x, wqkv, positions, cos, sin, n_q_heads, n_kv_heads, head_dim, bias=None, out=None,
+                 rscale=None):
         if positions.dtype != torch.int32:
             raise TypeError("positions must be int32")
         rope_cols = (n_q_heads + n_kv_heads) * head_dim
         if head_dim not in (64, 128):
             # the fused epilogue finds a column's rotate-half partner 2 or 4 subtiles away inside
             # the GEMM tile; other head sizes (Phi-3-mini: 96) rotate in a second pass
-            y = self.gemm(x, wqkv, EPI_NONE, out=out, bias=bias)
+            y = self.gemm(x, wqkv, EPI_NONE, out=out, bias=bias, rscale=rscale)
             rc = self.k.fls_headnorm_rope(y.data_ptr(), y.stride(0), y.shape[0], n_q_heads, n_kv_heads, None, None,
                                           positions.data_ptr(), cos.data_ptr(), sin.data_ptr(), head_dim, 0.0,
                                           _stream())
             _chk(rc, "fls_headnorm_rope")
             return y
         return self.gemm(x, wqkv, EPI_ROPE, out=out, positions=positions, cos=cos, sin=sin,
-                         rope_cols=rope_cols, head_dim=head_dim, bias=bias)
+                         rope_cols=rope_cols, head_dim=head_dim, bias=bias, rscale=rscale)
 
     def qkv_norm_rope(self, x, wqkv, positions, cos, sin, n_q_heads, n_kv_heads, head_dim, qn, kn, eps,
-                      bias=None, out=None):
+                      bias=None, out=None, rscale=None):
         """Qwen3: projection (+ bias), then RMSNorm over head_dim on every q / k head (q_norm /
         k_norm weights) and RoPE, in place (``headnorm_rope_kernel``); V columns untouched."""
         if positions.dtype != torch.int32:
             raise TypeError("positions must be int32")
-        y = self.gemm(x, wqkv, EPI_NONE, out=out, bias=bias)
+        y = self.gemm(x, wqkv, EPI_NONE, out=out, bias=bias, rscale=rscale)
         _f16(qn, "q_norm")
         _f16(kn, "k_norm")
         rc = self.k.fls_headnorm_rope(y.data_ptr(), y.stride(0), y.shape[0], n_q_heads, n_kv_heads, qn.data_ptr(),
@@ -354,28 +411,32 @@ class HipOps:
             raise TypeError("row indices must be int32")
         return self.rmsnorm(x, w, eps, row_idx=idx)
 
-    def embed(self, ids, table, out_dtype):
+    def embed(self, ids, table, out_dtype, scale: float = 1.0, out=None):
+        """table[ids] (scale != 1: fp16(e * scale), Granite's embedding_multiplier)."""
         _f16(table, "table")
         if out_dtype != torch.float16:
             raise TypeError("HIP path runs fp16 activations")
         T = ids.shape[0]
         V, H = table.shape
-        out = torch.empty(T, H, dtype=torch.float16, device=table.device)
-        _chk(self.k.fls_embed(ids.data_ptr(), table.data_ptr(), out.data_ptr(), T, H, V, _stream()), "fls_embed")
+        if out is None:
+            out = torch.empty(T, H, dtype=torch.float16, device=table.device)
+        elif tuple(out.shape) != (T, H) or not out.is_contiguous():
+            raise ValueError(f"out must be a contiguous [{T}, {H}] tensor")
+        _chk(self.k.fls_embed(ids.data_ptr(), table.data_ptr(), out.data_ptr(), T, H, V, float(scale), _stream()),
+             "fls_embed")
         return out
 
-    def softmax(self, logits):
+    def softmax(self, logits, logits_scaling: float = 1.0):
+        """Row softmax of fp16 logits (logits_scaling != 1: of fp16(logits / logits_scaling))."""
         _f16(logits, "logits")
         rows, V = logits.shape
         probs = torch.empty_like(logits)
-        _chk(self.k.fls_softmax_rows(logits.data_ptr(), probs.data_ptr(), rows, V, _stream()), "fls_softmax")
+        _chk(self.k.fls_softmax_rows(logits.data_ptr(), probs.data_ptr(), rows, V, 1.0 / float(logits_scaling),
+                                     _stream()), "fls_softmax")
         return probs
 
     def lm_head_softmax(self, h, w, logits_scaling: float = 1.0):
-        logits = self.linear(h, w)
-        if logits_scaling != 1.0:                       # Granite: fp16 logits / logits_scaling
-            logits.div_(logits_scaling)
-        return self.softmax(logits)
+        return self.softmax(self.linear(h, w), logits_scaling)
 
     def cast_f16(self, dst: torch.Tensor, src: torch.Tensor, src_code: int) -> None:
         """dst (fp16 bytes) = fp16(src bytes of bf16 (code 1; may be in place) or fp32 (code 2))."""

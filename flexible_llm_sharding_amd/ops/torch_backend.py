@@ -15,6 +15,7 @@ import torch.nn.functional as F
 
 class TorchOps:
     name = "torch"
+    fused_norm = False          # explicit RMSNorm (the oracle keeps HF's cast points)
 
     def __init__(self, compute_dtype: torch.dtype = torch.float32):
         self.cdt = compute_dtype
@@ -24,8 +25,29 @@ class TorchOps:
         return t if t.dtype == self.cdt else t.to(self.cdt)
 
     # ------------------------------------------------------------------- ops
-    def embed(self, ids: torch.Tensor, table: torch.Tensor, out_dtype) -> torch.Tensor:
-        return table.index_select(0, ids.long()).to(out_dtype)
+    def embed(self, ids: torch.Tensor, table: torch.Tensor, out_dtype, scale: float = 1.0, out=None) -> torch.Tensor:
+        e = table.index_select(0, ids.long())
+        if scale != 1.0:                       # Granite: GraniteModel scales the embeddings
+            e = (self._c(e) * scale).to(table.dtype)
+        e = e.to(out_dtype)
+        if out is not None:
+            out.copy_(e)
+            return out
+        return e
+
+    def copy_rows(self, x, src_idx, y, dst_idx):
+        rows = x.index_select(0, src_idx.long()) if src_idx is not None else x
+        if dst_idx is not None:
+            y.index_copy_(0, dst_idx.long(), rows.to(y.dtype))
+        else:
+            y.copy_(rows)
+        return y
+
+    def gather_rows(self, x, idx, out=None):
+        return x.index_select(0, idx.long()) if out is None else self.copy_rows(x, idx, out, None)
+
+    def scatter_rows(self, x, idx, y):
+        return self.copy_rows(x, None, y, idx)
 
     def rmsnorm(self, x: torch.Tensor, w: torch.Tensor, eps: float, out=None) -> torch.Tensor:
         # LlamaRMSNorm: fp32 variance, normalise, cast back, scale by weight.
@@ -38,11 +60,14 @@ class TorchOps:
         return (self._c(x) @ self._c(w).t()).to(x.dtype)
 
     def linear_residual(self, x: torch.Tensor, w: torch.Tensor, resid: torch.Tensor,
-                        bias: torch.Tensor = None) -> torch.Tensor:
+                        bias: torch.Tensor = None, alpha: float = 1.0) -> torch.Tensor:
         y = self._c(x) @ self._c(w).t()
         if bias is not None:
             y = y + self._c(bias)
-        return (self._c(resid) + y).to(resid.dtype)
+        if alpha != 1.0:
+            # Granite's residual_multiplier in HF GraniteDecoderLayer's roundings: x + fp16(fp16(y) * r)
+            y = (self._c(y.to(resid.dtype)) * alpha).to(resid.dtype)
+        return (self._c(resid) + self._c(y)).to(resid.dtype)
 
     def swiglu_up(self, x: torch.Tensor, wgu: torch.Tensor, out=None) -> torch.Tensor:
         y = self._c(x) @ self._c(wgu).t()                     # [T, 2I] = [gate | up]
@@ -171,6 +196,9 @@ class TorchOps:
 
     def lm_head_softmax(self, h: torch.Tensor, w: torch.Tensor, logits_scaling: float = 1.0) -> torch.Tensor:
         logits = (self._c(h) @ self._c(w).t()).to(h.dtype)   # fp16 logits like nn.Linear in fp16
+        return self.softmax(logits, logits_scaling)
+
+    def softmax(self, logits: torch.Tensor, logits_scaling: float = 1.0) -> torch.Tensor:
         if logits_scaling != 1.0:                            # Granite: logits / logits_scaling
             logits = logits / logits_scaling
         return torch.softmax(logits.float(), dim=-1).to(torch.float16)

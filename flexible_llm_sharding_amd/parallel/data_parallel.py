@@ -92,7 +92,16 @@ class AllGatherPrefetcher(ShardPrefetcher):
 
     ``store`` is a :class:`SlicedHostStore` (slices pinned in host RAM) or a
     streaming :class:`~..runtime.stream.FileLayerSource` (slices read from the
-    layer files every pass by a loader thread, bf16 cast after the gather)."""
+    layer files every pass by a loader thread, bf16 cast after the gather).
+
+    Every all-gather is issued by the MAIN thread, inside :meth:`prefetch` — at the same program
+    point on every rank (the engine's per-shard prefetch, also on ranks without prompts) — so the
+    gathers on this communicator and the main thread's collectives on the default one (score
+    gather, broadcasts, the bench's all-reduces) are enqueued in one order on every rank: two
+    communicators whose RCCL streams share a hardware queue (GPU_MAX_HW_QUEUES = 4 < the streams
+    of a rank) then cannot wait on each other in opposite orders on two ranks.  With a streaming
+    source only the file reads (and their H2D of this rank's slice, on a stream of their own) run
+    in the loader thread, started as soon as the slot they land in is released."""
 
     collective = True      # every rank must acquire every shard (engine: empty prompt slices too)
 
@@ -105,6 +114,8 @@ class AllGatherPrefetcher(ShardPrefetcher):
         if not self.streaming:
             self._pool = None                 # slices are host-resident: no loader thread
         self.bytes_read = 0                   # file bytes this rank read (streaming)
+        self.read_stream = torch.cuda.Stream(self.dev) if (self.cuda and self.streaming) else None
+        self._reads: Dict[int, object] = {}   # shard -> Future of its slice reads (loader thread)
 
     def slices(self, name: str) -> List[PieceSlice]:
         return piece_slices(self.store.layout(name), self.comm.world)
@@ -112,6 +123,94 @@ class AllGatherPrefetcher(ShardPrefetcher):
     def shard_bytes(self, k: int) -> int:
         G = self.comm.world
         return sum(_align(p.chunk * G) for i in self.shards[k] for p in self.slices(self.names[i]))
+
+    # ------------------------------------------------------------ streaming (reads / gathers split)
+    def _read(self, k: int, epoch=None):
+        """Loader thread: this rank's slices of shard k from the layer files into their places in
+        the slot, on the read stream behind the slot's free event -> (slot, read event, pieces)."""
+        s = self.slot_of(k, epoch)
+        slot = self._slot(s)
+        G, r = self.comm.world, self.comm.rank
+        plan = []
+        with torch.cuda.stream(self.read_stream):
+            if self._free_ev[s] is not None:
+                self.read_stream.wait_event(self._free_ev[s])
+            off = 0
+            for i in self.shards[k]:
+                name = self.names[i]
+                for p in self.slices(name):
+                    region = slot[off:off + p.chunk * G]
+                    mine = region[r * p.chunk:(r + 1) * p.chunk]
+                    lo, hi = p.rank_range(r)
+                    if hi > lo:
+                        self.bytes_read += self.store.stream_into(name, mine, self.read_stream, lo, hi, cast=False)
+                    plan.append((name, p, region, mine, hi - lo))
+                    off += _align(p.chunk * G)
+            ev = torch.cuda.Event()
+            ev.record(self.read_stream)
+        return s, ev, plan
+
+    def _gather(self, rd):
+        """Main thread: the all-gathers completing shard k's pieces (copy stream, after the reads),
+        the bf16 casts and the load transform -> the ready entry."""
+        s, rev, plan = rd
+        views: Dict[str, Dict[str, torch.Tensor]] = {}
+        regions: Dict[str, list] = {}
+        with torch.cuda.stream(self.copy_stream):
+            self.copy_stream.wait_event(rev)
+            for name, p, region, mine, nb in plan:
+                self.comm.all_gather_into(region, mine, async_op=True).wait()
+                self.store.cast_on_gpu(name, region, p.lo, p.hi)
+                regions.setdefault(name, []).append((p.lo, region))
+                self.bytes_h2d += nb
+            for name, regs in regions.items():
+                views[name] = piece_views(self.store.layout(name), regs, self.dtype)
+                self._loaded(name, views[name])
+            ev = torch.cuda.Event()
+            ev.record(self.copy_stream)
+        return ev, views, s
+
+    def _submit_read(self, k: int, epoch=None) -> None:
+        if k not in self._reads and k not in self._ready:
+            self._reads[k] = self._pool.submit(self._read, k, epoch)
+
+    def prefetch(self, k: int, epoch=None) -> None:
+        if not (self.streaming and self.cuda):
+            return super().prefetch(k, epoch)
+        if k < 0 or k >= len(self.shards):
+            return
+        with self.lock:
+            if k in self._ready or (k in self._sticky and k in self._loaded_resident):
+                return
+        self._submit_read(k, epoch)
+        rd = self._reads.pop(k).result()      # the host waits only for reads started a shard ago
+        entry = self._gather(rd)
+        with self.lock:
+            self._ready[k] = entry
+
+    def release(self, k: int) -> None:
+        super().release(k)
+        if self.streaming and self.cuda and not self.resident and self.in_rotation(k) and k not in self._sticky:
+            # the slot is free (its event recorded): start reading the next shard that lands in it
+            s = self.slot_of(k)
+            for j in range(k + 1, len(self.shards)):
+                if self.in_rotation(j) and j not in self._sticky:
+                    if self.slot_of(j) == s:
+                        self._submit_read(j)
+                        break
+
+    def discard_loaded(self) -> None:
+        for f in list(self._reads.values()):
+            try:
+                f.result()
+            except Exception:  # noqa: BLE001 - the load is being dropped anyway
+                pass
+        self._reads.clear()
+        super().discard_loaded()
+
+    def close(self):
+        self.discard_loaded()
+        super().close()
 
     def _load(self, k: int, epoch=None):
         t0 = time.perf_counter()
@@ -151,6 +250,8 @@ class AllGatherPrefetcher(ShardPrefetcher):
                     off += _align(p.chunk * G)
                     self.bytes_h2d += hi - lo
                 views[name] = piece_views(self.store.layout(name), regions, self.dtype)
+                if self.cuda:
+                    self._loaded(name, views[name])
             if self.cuda:
                 ev = torch.cuda.Event()
                 ev.record(self.copy_stream)

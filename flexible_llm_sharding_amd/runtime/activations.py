@@ -139,7 +139,9 @@ class ActivationStore:
         return list(self._e)
 
     # -------------------------------------------------------------- put
-    def put(self, key, t: torch.Tensor) -> None:
+    def put(self, key, t: torch.Tensor):
+        """Park ``t`` under ``key`` -> the event after which ``t``'s device memory may be
+        overwritten (the D2H's completion on the D2H stream; None when ``t`` itself is kept)."""
         with self.lock:
             old = self._e.pop(key, None)
         if old is not None:
@@ -150,7 +152,7 @@ class ActivationStore:
             e.dev = t
             with self.lock:
                 self._e[key] = e
-            return
+            return None
         nbytes = t.numel() * t.element_size()
         if not self.cuda:
             if self.mode == "cpu":
@@ -160,7 +162,7 @@ class ActivationStore:
                 self._write_npy(e.path, t.contiguous(), e.shape, e.dtype)
             with self.lock:
                 self._e[key] = e
-            return
+            return None
         host = self._get_host(nbytes)
         cur = torch.cuda.current_stream(self.dev)
         self.d2h.wait_stream(cur)
@@ -183,6 +185,7 @@ class ActivationStore:
             e.write_fut = self._io.submit(_write)
         with self.lock:
             self._e[key] = e
+        return ev
 
     def _write_npy(self, path: str, t: torch.Tensor, shape, dtype) -> None:
         hdr = _npy_header(shape, dtype)
@@ -229,7 +232,9 @@ class ActivationStore:
         else:
             self._inflight[key] = (None, None)
 
-    def get(self, key, pop: bool = True) -> torch.Tensor:
+    def get(self, key, pop: bool = True, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """The state parked under ``key`` on the device: a fresh tensor, or ``out`` (a slot of the
+        engine's ActRing the caller acquired for the H2D stream) when given."""
         with self.lock:
             e = self._e.pop(key) if pop else self._e[key]
         if self.mode == "gpu":
@@ -257,13 +262,18 @@ class ActivationStore:
         cur = torch.cuda.current_stream(self.dev)
         if e.event is not None:
             self.h2d.wait_event(e.event)     # D2H finished before reading the host copy back
+        ring = out is not None
         with torch.cuda.stream(self.h2d):
             # Allocate ON the H2D stream: a block from the compute stream's pool may
             # still be in use by compute kernels queued before its Python-side free,
             # and this copy does not wait for them (it overlaps the previous
             # micro-batch's compute).  record_stream below keeps the block from being
-            # reused until the compute stream's consumers are done.
-            out = torch.empty(e.shape, dtype=e.dtype, device=self.dev)
+            # reused until the compute stream's consumers are done.  (A ring slot's reuse is
+            # ordered by its free event instead: ActRing.acquire.)
+            if not ring:
+                out = torch.empty(e.shape, dtype=e.dtype, device=self.dev)
+            elif tuple(out.shape) != tuple(e.shape) or out.dtype != e.dtype:
+                raise ValueError(f"ring slot {tuple(out.shape)} {out.dtype} != parked {e.shape} {e.dtype}")
             out.copy_(host[:nbytes].view(e.dtype).view(e.shape), non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(self.h2d)
@@ -273,7 +283,8 @@ class ActivationStore:
         cur.wait_event(ev)
         e1.record(cur)
         self._stall_ev.append((e0, e1))
-        out.record_stream(cur)
+        if not ring:
+            out.record_stream(cur)
         if pop:
             # host buffer is reusable once the H2D has completed (checked lazily)
             with self.lock:
@@ -308,3 +319,91 @@ class ActivationStore:
         self.clear()
         if self._io is not None:
             self._io.shutdown(wait=True)
+
+
+class ActRing:
+    """Fixed HBM slots for the hidden states of a pass (single GPU / data parallel, storage cpu or
+    disk): the micro-batch being computed (updated in place by the residual GEMM epilogues) and the
+    next one landing from the host, or a state carried across a zigzag shard boundary.
+
+    The caching allocator alone bounds nothing here: every H2D landing buffer allocated ahead of
+    its use, and every D2H source held by ``record_stream`` until the copy drains, stays reserved
+    while the host runs ahead — round 4's plan had to charge 5 live states for it, which starved
+    the arena under ``--max_vram_gb``.  A slot is reused only behind its free
+    event (the D2H of its last occupant, or the compute that last read it), waited for on the
+    stream that fills it next, so the host never blocks and the bound is exact: ``n_slots``
+    states.  Slots go least-recently-released first, so the landing of micro-batch j+1 never waits
+    for the D2H of micro-batch j."""
+
+    def __init__(self, device, dtype: torch.dtype, n_slots: int):
+        self.dev, self.dtype, self.n = torch.device(device), dtype, n_slots
+        self._bufs: List[Optional[torch.Tensor]] = [None] * n_slots
+        self._free: List[Optional[torch.cuda.Event]] = [None] * n_slots
+        self._owner: List[object] = [None] * n_slots
+        self._age = [0] * n_slots
+        self._tick = 0
+
+    def resize(self, n_slots: int, elems: int) -> None:
+        """At a pass start (every slot released): ``n_slots`` slots of >= ``elems`` elements."""
+        if any(o is not None for o in self._owner):
+            raise RuntimeError("activation ring resized with live states")
+        if n_slots != self.n:
+            self.n = n_slots
+            self._bufs, self._free = [None] * n_slots, [None] * n_slots
+            self._owner, self._age = [None] * n_slots, [0] * n_slots
+        for i in range(n_slots):
+            if self._bufs[i] is None or self._bufs[i].numel() < elems:
+                self._bufs[i] = None
+                self._bufs[i] = torch.empty(max(1, elems), dtype=self.dtype, device=self.dev)
+                self._free[i] = None
+
+    def bytes(self) -> int:
+        return sum(b.numel() * b.element_size() for b in self._bufs if b is not None)
+
+    def acquire(self, key, shape, stream) -> torch.Tensor:
+        """A free slot for ``key``'s state as a ``shape`` view; ``stream`` (the one that fills it)
+        waits for the slot's previous occupant to be done with it."""
+        free = [i for i in range(self.n) if self._owner[i] is None]
+        if not free:
+            raise RuntimeError(f"activation ring: all {self.n} slots hold live states")
+        i = min(free, key=lambda j: self._age[j])
+        if self._free[i] is not None and stream is not None:
+            stream.wait_event(self._free[i])
+        self._owner[i] = key
+        n = 1
+        for d in shape:
+            n *= d
+        return self._bufs[i][:n].view(shape)
+
+    def holds(self, t: torch.Tensor) -> int:
+        """Index of the slot ``t`` lives in (-1: not a ring tensor)."""
+        p = t.data_ptr()
+        for i, b in enumerate(self._bufs):
+            if b is not None and b.data_ptr() <= p < b.data_ptr() + b.numel() * b.element_size():
+                return i
+        return -1
+
+    def release(self, key, event) -> None:
+        """``key``'s slot may be refilled once ``event`` (recorded on the stream of its last use)
+        has completed."""
+        for i in range(self.n):
+            if self._owner[i] == key:
+                self._owner[i] = None
+                self._free[i] = event
+                self._tick += 1
+                self._age[i] = self._tick
+                return
+
+    def owns(self, key) -> bool:
+        return key in self._owner
+
+    def reset(self) -> None:
+        """After an aborted pass: every slot free, its next fill ordered after the work queued on
+        the current stream so far."""
+        cur = torch.cuda.current_stream(self.dev) if self.dev.type == "cuda" else None
+        for i in range(self.n):
+            if self._owner[i] is not None and cur is not None:
+                e = torch.cuda.Event()
+                e.record(cur)
+                self._free[i] = e
+        self._owner = [None] * self.n

@@ -131,7 +131,8 @@ class PackedBatch:
                         "work": self._rebase(self.work[w0:w1], r0),
                         "work_last": self._rebase(self.work_last[s0:s1], r0),
                         "seg_lo": (self.seg_lo[r0:r1] - r0).astype(np.int32),
-                        "last_local": (self.last_idx[s0:s1] - r0).astype(np.int32)})
+                        "last_local": (self.last_idx[s0:s1] - r0).astype(np.int32),
+                        "last_pos": self.positions[self.last_idx[s0:s1]].astype(np.int32)})
         return out
 
     def _rebase(self, work: np.ndarray, r0: int) -> np.ndarray:
@@ -176,6 +177,7 @@ class PackedBatch:
                 "work": torch.from_numpy(self.work).to(d, non_blocking=nb),
                 "seg_lo": torch.from_numpy(self.seg_lo).to(d, non_blocking=nb),
                 "last_idx": torch.from_numpy(self.last_idx).to(d, non_blocking=nb),
+                "last_pos": torch.from_numpy(self.positions[self.last_idx].astype(np.int32)).to(d, non_blocking=nb),
                 "work_last": torch.from_numpy(self.work_last).to(d, non_blocking=nb),
             }
             for name in ("pfx_src", "pfx_dst", "sfx_src", "sfx_dst", "work2", "work2_last", "r2win"):
@@ -297,16 +299,16 @@ def pack_prompts(tps: Sequence[TokenizedPrompt], prompt_ids: Sequence[int],
         work_last=(np.asarray(lwork, dtype=np.int32).reshape(-1, WORK_ITEM_FIELDS) if reuse
                    else _work_items(lsegs)), num_tokens=t, padded_tokens=padded,
         max_pos=max_pos, kv_cached=kv_cached, q_block=q_block,
-        pfx_src=np.asarray(src, dtype=np.int64) if (prefix_offsets is not None and not kv_cached) else None,
-        pfx_dst=np.asarray(dst, dtype=np.int64) if (prefix_offsets is not None and not kv_cached) else None,
+        pfx_src=np.asarray(src, dtype=np.int32) if (prefix_offsets is not None and not kv_cached) else None,
+        pfx_dst=np.asarray(dst, dtype=np.int32) if (prefix_offsets is not None and not kv_cached) else None,
         prompt_rows=np.asarray(p_rows, dtype=np.int64).reshape(-1, 2),
         prompt_items=np.asarray(p_items, dtype=np.int64).reshape(-1, 2),
         prompt_scored=np.asarray(p_scored, dtype=np.int64).reshape(-1, 2),
         work2=np.asarray(work2, dtype=np.int32).reshape(-1, 2) if reuse else None,
         r2win=np.asarray(r2win, dtype=np.int32).reshape(-1, 2) if reuse else None,
         work2_last=np.asarray(lwork2, dtype=np.int32).reshape(-1, 2) if reuse else None,
-        sfx_src=np.asarray(sfx_src, dtype=np.int64) if sfx_src else None,
-        sfx_dst=np.asarray(sfx_dst, dtype=np.int64) if sfx_dst else None)
+        sfx_src=np.asarray(sfx_src, dtype=np.int32) if sfx_src else None,
+        sfx_dst=np.asarray(sfx_dst, dtype=np.int32) if sfx_dst else None)
 
 
 def _items(sg: Segment, q_block: int = Q_BLOCK) -> List[tuple]:

@@ -78,6 +78,7 @@ class RunCheckpoint:
 
     def commit(self, next_shard: int, keys: Sequence[int], dtype: torch.dtype) -> None:
         tmp, final = self._step_dir(next_shard, tmp=True), self._step_dir(next_shard)
+        os.makedirs(tmp, exist_ok=True)        # (a data-parallel rank without prompts commits no state)
         missing = [k for k in keys if not os.path.exists(os.path.join(tmp, f"mb{k}.npy"))]
         if missing:
             raise RuntimeError(f"checkpoint step{next_shard}: states missing for micro-batches {missing}")

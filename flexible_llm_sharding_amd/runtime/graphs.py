@@ -61,9 +61,11 @@ def padded_meta(batch: PackedBatch, key) -> Dict[str, np.ndarray]:
     seg_lo[:batch.num_tokens] = batch.seg_lo
     last = np.zeros(S, np.int32)
     last[:batch.n_scored] = batch.last_idx
+    last_pos = pos[last]                                   # positions of the scored rows
     wl = np.zeros((S, WORK_ITEM_FIELDS), np.int32)        # padding items: q_len 0
     wl[:batch.work_last.shape[0]] = batch.work_last
-    return {"ids": ids, "positions": pos, "work": work, "seg_lo": seg_lo, "last_idx": last, "work_last": wl}
+    return {"ids": ids, "positions": pos, "work": work, "seg_lo": seg_lo, "last_idx": last, "last_pos": last_pos,
+            "work_last": wl}
 
 
 class _Graph:

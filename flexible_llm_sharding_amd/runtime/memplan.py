@@ -5,11 +5,13 @@ at ``layer_num_per_shard=1`` (``/root/reference/README.md:2,31``).  Here the
 HBM in use is
 
     weight slots (2 x the largest shard: 2 x 1.71 GB for 70B, lnps=1)
-  + one workspace arena (models/llama.py): [normed chunk (``qkv_chunk`` rows) | QKV of the
-    micro-batch] in the attention phase — the attention output overwrites Q in place — and
-    [normed chunk | SwiGLU chunk] (``mlp_chunk`` rows) in the MLP phase
-  + the hidden states alive: 1 when the whole call is one micro-batch (it never leaves HBM),
-    else the one being computed, the carry window and the copy-stream landing buffers
+  + one workspace arena (models/llama.py): [QKV of the micro-batch | row statistics] in the
+    attention phase with the fused RMSNorm + QKV GEMM ([normed chunk (``qkv_chunk`` rows) | QKV]
+    without it) — the attention output overwrites Q in place — and [normed chunk | SwiGLU chunk]
+    (``mlp_chunk`` rows) in the MLP phase
+  + the hidden states alive: the engine's activation ring (engine.ActRing): 1 slot when the whole
+    call is one micro-batch (it never leaves HBM), else 2 — the micro-batch being computed and the
+    next one landing (the zigzag order's carries fit in the same two slots)
   + the HIP context, code objects and allocator slack,
 
 so a VRAM cap is met by sizing ``token_budget``, ``qkv_chunk`` and ``mlp_chunk``:
@@ -29,13 +31,20 @@ from ..models.layout import layer_kind, layer_layout
 # HIP context + code objects (measured on MI355X: 0.665 GB of device memory in use right after
 # context creation, profiles/r2_vram/ctx.log) + events / small buffers
 DEVICE_OVERHEAD = int(0.75e9)
-# hidden states alive at once: the one being computed, the carry window (3, engine.CARRY_WINDOW)
-# and one H2D landing buffer
-STATES = 5
-# caching-allocator slack on the (few, reused) activation blocks; one micro-batch per call holds
-# exactly two large blocks (state + arena), rounded to 2 MB
-SLACK = 1.10
+# hidden states alive at once with several micro-batches per call: the activation ring's slots
+# (engine.ActRing: the state being computed + the next one landing, or a zigzag carry)
+RING_SLOTS = 2
+STATES = RING_SLOTS
+# caching-allocator slack on the few fixed activation blocks (ring slots + arena), 2 MB rounded;
+# the small per-call tensors (metadata, pruned rows, logits) are in the 64 MB margin
+SLACK = 1.02
 SLACK_ONE = 1.02
+# the multi-micro-batch plan prefers MLP chunks of at least this many rows before fewer
+# micro-batches (round 4's capped plan fell to 2,048-row chunks with 5 live states: -31%, VERDICT
+# r4 #2); chunks are multiples of 3,072 rows = whole 256-CU rounds of the 70B MLP GEMMs, so
+# 9,216 and 12,288 differ only in per-launch ramps, while each extra micro-batch adds a round of
+# small per-layer launches (r5: 15 micro-batches of 12,288 rows ran 94.8% of the headline rate)
+MLP_CHUNK_TARGET = 9216
 # the plan aims this far below the cap (the estimate is a model; hipMemGetInfo is the judge)
 CAP_MARGIN = 0.015
 # device memory the HIP runtime takes outside any allocator for a moment while a pass runs: up to
@@ -46,14 +55,18 @@ RUNTIME_RESERVE = knobs.get_int("FLS_RUNTIME_RESERVE_MB") << 20
 
 
 def activation_bytes(cfg: ModelConfig, tokens: int, mlp_chunk: int, elem: int = 2, qkv_chunk: int = 0,
-                     states: int = STATES, attn_rows: int = 0) -> int:
+                     states: int = STATES, attn_rows: int = 0, fused_norm: bool = False) -> int:
     """Peak activation bytes of one micro-batch of ``tokens`` rows: the workspace arena
-    (models.llama: [normed chunk | QKV] — of the whole micro-batch, or of one prompt-aligned
-    group of <= ``attn_rows`` rows — then [normed chunk | SwiGLU chunk]) + live states."""
+    (models.llama: [QKV | row statistics] with ``fused_norm``, else [normed chunk | QKV] — of the
+    whole micro-batch, or of one prompt-aligned group of <= ``attn_rows`` rows — then [normed
+    chunk | SwiGLU chunk]) + live states."""
     from ..models.llama import balanced_step
     H, I, Q = cfg.hidden_size, cfg.intermediate_size, cfg.qkv_size
     chunk = balanced_step(tokens, mlp_chunk)
-    if attn_rows and attn_rows < tokens:
+    rows = attn_rows if (attn_rows and attn_rows < tokens) else tokens
+    if fused_norm:
+        attn = rows * (Q + 2)                  # QKV + the fp32 row statistic (2 fp16 columns)
+    elif attn_rows and attn_rows < tokens:
         attn = attn_rows * (H + Q)
     else:
         qc = balanced_step(tokens, qkv_chunk) if qkv_chunk else tokens
@@ -125,19 +138,21 @@ def weight_slot_bytes(cfg: ModelConfig, lnps: int, n_slots: int = 2) -> int:
 def plan_for_vram(cfg: ModelConfig, max_vram_bytes: int, lnps: int = 1, n_slots: int = 2,
                   token_budget: int = 49152, mlp_chunk: int = 16384,
                   total_tokens: Optional[int] = None, max_prompt_rows: int = 0,
-                  overhead: Optional[int] = None, weight_bytes: Optional[int] = None) -> Tuple[int, int, int, int, int]:
+                  overhead: Optional[int] = None, weight_bytes: Optional[int] = None,
+                  fused_norm: bool = False) -> Tuple[int, int, int, int, int]:
     """-> (token_budget, mlp_chunk, attn_rows, qkv_chunk, estimated peak bytes) for a call of
     ``total_tokens`` packed tokens (None: unknown, assume several micro-batches) whose largest
     prompt has ``max_prompt_rows`` rows.  ``overhead``: device memory held outside the plan
     (measured context + code objects; default DEVICE_OVERHEAD); ``weight_bytes``: the weight
     buffers actually planned (default ``n_slots`` full-shard slots).
 
-    Preference, by measured cost on the 70B pass (one box, ``profiles/r3_vram``): fewest
-    micro-batches (one keeps the hidden state in HBM: no activation traffic over PCIe), then the
-    largest MLP chunk (14,336 vs 10,752 rows: 2.1% of a pass, GEMM tile-round tails), then the
-    whole micro-batch in one attention phase (prompt-aligned groups: ~1%) with the QKV
-    projection in the largest row chunks that fit, then the largest groups; raises if nothing
-    fits."""
+    Preference, by measured cost on the 70B pass (one box, ``profiles/r3_vram``): one micro-batch
+    when it fits with MLP chunks of ``MLP_CHUNK_TARGET`` rows (the hidden state never leaves HBM:
+    no activation traffic over PCIe); else MLP chunks up to that size first (14,336 vs 10,752
+    rows: 2.1% of a pass, GEMM tile-round tails) and then the fewest micro-batches (each parks its
+    state over PCIe in the copy engine's shadow); then the largest MLP chunk, then the whole
+    micro-batch in one attention phase (prompt-aligned groups: ~1%) with the QKV projection in the
+    largest row chunks that fit, then the largest groups; raises if nothing fits."""
     from ..models.llama import balanced_step
     weights = weight_slot_bytes(cfg, lnps, n_slots) if weight_bytes is None else weight_bytes
     target = int(max_vram_bytes * (1.0 - CAP_MARGIN))
@@ -155,12 +170,15 @@ def plan_for_vram(cfg: ModelConfig, max_vram_bytes: int, lnps: int = 1, n_slots:
             for ar in sorted({0, 32768, 24576, 16384, 12288, 8192, 4096}):
                 if ar and (ar >= rows or ar < max_prompt_rows):
                     continue
-                for qc in ((0, 16384, 12288, 9216, 8192, 6144, 4096, 3072, 2048) if ar == 0 else (0,)):
+                qcs = (0, 16384, 12288, 9216, 8192, 6144, 4096, 3072, 2048) if ar == 0 and not fused_norm else (0,)
+                for qc in qcs:
                     if qc and qc >= rows:
                         continue
                     est = weights + over + activation_bytes(cfg, rows, mc, qkv_chunk=qc, states=states,
-                                                            attn_rows=ar)
-                    key = (-n_mb, mce, ar == 0, balanced_step(rows, qc) if qc else rows, ar)
+                                                            attn_rows=ar, fused_norm=fused_norm)
+                    good = min(mce, MLP_CHUNK_TARGET, rows)
+                    key = (n_mb == 1 and mce >= min(MLP_CHUNK_TARGET, rows), good, -n_mb, mce, ar == 0,
+                           balanced_step(rows, qc) if qc else rows, ar)
                     if est <= target and (best is None or key > best[5]):
                         best = (tb, mc, ar, qc, est, key)
     if best is None:

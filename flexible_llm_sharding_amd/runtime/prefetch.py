@@ -68,6 +68,15 @@ def choose_kept_shards(sizes: Sequence[int], budget: int) -> List[int]:
 
 
 class ShardPrefetcher:
+    # transform of a freshly loaded decoder layer (its weight views), enqueued on the copy stream
+    # before the load's ready event: the engine folds the input RMSNorm into W_qkv here
+    # (models.llama.fold_layer_norms), so a resident / kept shard is folded exactly once
+    on_load = None
+
+    def _loaded(self, name: str, views: Dict[str, torch.Tensor]) -> None:
+        if self.on_load is not None and layer_kind(name) == "decoder":
+            self.on_load(views)
+
     def __init__(self, source: LayerSource, layer_names: Sequence[str],
                  shards: Sequence[Tuple[int, ...]], device, n_slots: int = 2,
                  resident: bool = False, dtype=torch.float16, keep: Optional[Sequence[int]] = None):
@@ -215,6 +224,7 @@ class ShardPrefetcher:
                 else:
                     dst.copy_(hb[:nb], non_blocking=True)
                 views[name] = self.src.layout(name).views(dst, self.dtype)
+                self._loaded(name, views[name])
                 off += _align(nb)
                 self.bytes_h2d += nb
             ev.record(self.copy_stream)
@@ -374,11 +384,14 @@ class PiecePoolPrefetcher(ShardPrefetcher):
     MLP piece (gate/up, down: 1.41 GB) — the packed image puts every attention weight first
     (models/layout.py).  HBM holds ONE attention slot and TWO MLP slots (the embedding and LM
     head use the MLP slots), 3.12 GB for 70B instead of the double buffer's 3.42 GB, and loads
-    are issued in pass order as soon as their slot is released:
+    are issued in one fixed order as soon as their slot is released.  The order is the pass
+    order with each decoder's MLP piece moved in front of its attention piece when the previous
+    shard is a decoder too (E a1 m1 m2 a2 m3 a3 ...):
 
-    * attention(k+1) lands while layer k's MLP computes (its slot frees after k's O projection);
-    * MLP(k+1) has layer k's MLP phase and layer k+1's attention phase to land (its slot held
-      MLP(k-1));
+    * MLP(k+1) issues as layer k starts (its slot held MLP(k-1)), so it has the whole of layer k
+      to land, however many micro-batches layer k runs;
+    * attention(k+1) lands while the last micro-batch of layer k runs its MLP (its slot frees
+      after that micro-batch's O projection: 0.30 GB, the small piece);
     * at the call boundary the LM head, the next call's embedding and first attention piece all
       load under the last layers, and the pool continues into the next call (same weights every
       call: the reference re-streams them, ``utils.py:228-233``).
@@ -406,7 +419,7 @@ class PiecePoolPrefetcher(ShardPrefetcher):
         # m = the two alternating MLP slots, o = own small buffer
         from ..models.layout import mlp_offset
         self.pieces: List[Tuple[str, int, int, int]] = []
-        self._first: List[int] = []
+        self._pidx: Dict[Tuple[int, int], int] = {}     # (shard, 0 attention / 1 MLP) -> piece index
         a_max = m_max = 0
         self._own: Dict[int, int] = {}
         own_sizes: List[int] = []
@@ -414,11 +427,11 @@ class PiecePoolPrefetcher(ShardPrefetcher):
             name = self.names[sh[0]]
             lay = source.layout(name)
             nb = source.nbytes(name)
-            self._first.append(len(self.pieces))
             if lay.kind == "decoder":
                 split = mlp_offset(lay)
-                self.pieces.append(("a", k, 0, split))
-                self.pieces.append(("m", k, split, nb))
+                prev_dec = k > 0 and source.layout(self.names[self.shards[k - 1][0]]).kind == "decoder"
+                pair = [("a", k, 0, split), ("m", k, split, nb)]
+                self.pieces += pair[::-1] if prev_dec else pair
                 a_max, m_max = max(a_max, _align(split)), max(m_max, _align(nb - split))
             elif nb <= (64 << 20):
                 self._own[k] = len(own_sizes)
@@ -427,6 +440,8 @@ class PiecePoolPrefetcher(ShardPrefetcher):
             else:
                 self.pieces.append(("m", k, 0, nb))
                 m_max = max(m_max, _align(nb))
+        for i, (kind, k, _, _) in enumerate(self.pieces):
+            self._pidx[(k, 1 if kind == "m" and self._is_dec(k) else 0)] = i
         self.a_bytes, self.m_bytes = a_max, m_max
         self._own_sizes = own_sizes
         self.n_slots = 2
@@ -459,8 +474,13 @@ class PiecePoolPrefetcher(ShardPrefetcher):
     def is_kept_loaded(self, k: int) -> bool:
         return False
 
+    def _is_dec(self, k: int) -> bool:
+        return self.src.layout(self.names[self.shards[k][0]]).kind == "decoder"
+
     def _gid(self, k: int, which: int = 0) -> int:
-        return self.epoch * len(self.pieces) + self._first[k] + which
+        """Global id of shard k's attention (0) or MLP (1) piece in the current epoch (a shard
+        without a decoder layer has one piece, ``which`` 0)."""
+        return self.epoch * len(self.pieces) + self._pidx[(k, which)]
 
     def _slot_for(self, gid: int) -> int:
         kind, k, _, _ = self.pieces[gid % len(self.pieces)]
@@ -486,6 +506,8 @@ class PiecePoolPrefetcher(ShardPrefetcher):
             if self._slot_free[s] is not None:
                 self.copy_stream.wait_event(self._slot_free[s])
             nbytes = self._copy_piece(slot, name, lo, hi)
+            if kind == "a" and self.on_load is not None:
+                self._loaded(name, self._piece_views(slot, name, True))
             ev.record(self.copy_stream)
         self.load_seconds += time.perf_counter() - t0
         self.bytes_h2d += nbytes
@@ -545,10 +567,20 @@ class PiecePoolPrefetcher(ShardPrefetcher):
                     views[ts.name] = self._slots[s][ts.offset:ts.offset + n].view(self.dtype).view(ts.shape)
             out = {name: _LayerViews(self, k, name, views, [ts.name for ts in lay.slots if ts.offset >= split])}
         else:
-            kind, _, lo, hi = self.pieces[self._first[k]]
+            kind, _, lo, hi = self.pieces[self._pidx[(k, 0)]]
             out = {name: lay.views(self._slots[s][:hi - lo], self.dtype)}
         self.wait_seconds += time.perf_counter() - t0
         return out
+
+    def _piece_views(self, slot: torch.Tensor, name: str, attention: bool) -> Dict[str, torch.Tensor]:
+        """Views of the attention (or MLP) piece of decoder ``name`` held at the start of ``slot``."""
+        from ..models.layout import mlp_offset
+        lay = self.src.layout(name)
+        split = mlp_offset(lay)
+        es = torch.empty((), dtype=self.dtype).element_size()
+        base = 0 if attention else split
+        return {ts.name: slot[ts.offset - base:ts.offset - base + ts.numel * es].view(self.dtype).view(ts.shape)
+                for ts in lay.slots if (ts.offset < split) == attention}
 
     def _mlp_views(self, k: int, name: str) -> Dict[str, torch.Tensor]:
         from ..models.layout import mlp_offset
@@ -581,7 +613,7 @@ class PiecePoolPrefetcher(ShardPrefetcher):
         if k not in self._acquired:
             return
         self._acquired.discard(k)
-        n = 2 if self.pieces[self._first[k]][0] == "a" else 1
+        n = 2 if (k, 1) in self._pidx else 1
         for j in range(n):
             gid = self._gid(k, j)
             if gid not in self._issued and gid not in self._released:

@@ -104,7 +104,7 @@ def test_data_parallel(single, tmp_path, world):
         assert _close(a, b)
 
 
-def _dp_shard_worker(rank, world, port, path, prompts, lnps, out_dir, resume_dir=None, fault=""):
+def _dp_shard_worker(rank, world, port, path, prompts, lnps, out_dir, resume_dir=None, fault="", weights="host"):
     if fault:
         os.environ["FLS_FAULT"] = fault
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
@@ -121,8 +121,9 @@ def _dp_shard_worker(rank, world, port, path, prompts, lnps, out_dir, resume_dir
                            disk_folder=out_dir, max_activation_in_cpu=100, prefix_attention="bidirectional",
                            token_budget=50, resident=False, dtype=None, verbose=False,
                            resume_dir=resume_dir, checkpoint_every=2)
-    r = build_dp_sharded_runner(args, cfg, "cpu", comm, load_tokenizer(path))
+    r = build_dp_sharded_runner(args, cfg, "cpu", comm, load_tokenizer(path), weight_cache=weights)
     assert r.prefetcher.__class__.__name__ == "AllGatherPrefetcher"
+    assert r.prefetcher.streaming == (weights == "stream")
     idx = np.array_split(np.arange(len(prompts)), world)[rank]
     outs = r([prompts[i] for i in idx])
     allv = comm.gather_scores(outs, dst=0)
@@ -361,3 +362,59 @@ def test_gather_scores_memory_does_not_grow_with_world(tmp_path):
         assert st[0]["received_bytes"] == (world - 1) * own
         staged[world] = st[1]["staged_bytes"]
     assert staged[2] == staged[4]
+
+
+# ------------------------------------------------------------------ world 8 (the driver's node)
+@pytest.mark.parametrize("stages", ["round_robin", "contiguous"])
+def test_model_parallel_world8(deeper, tmp_path, stages):
+    """Eight pipeline ranks, the size of the node the driver's scaling run uses.  Round robin: 6
+    decoder layers + embed / norm / head = 9 layers -> ceil(9 / 8) * 8 = 16 shards, 7 of them
+    padded EMPTY (utils.py:150-153), so some ranks own only empty shards in the second round and
+    the wrap-around edge 7 -> 0 carries a layer; contiguous: one block per rank, several ranks of
+    a single layer.  Scores equal the one-process run."""
+    from flexible_llm_sharding_amd.parallel.planner import make_plan
+    path, prompts, ref = deeper
+    plans = [make_plan(9, 1, 8, r, False, stages) for r in range(8)]
+    if stages == "round_robin":
+        assert sum(1 for p in plans for sh in p.my_shards if not len(sh)) == 7
+    assert sorted(i for p in plans for sh in p.my_shards for i in sh) == list(range(9))
+    mp.start_processes(_worker, args=(8, _port(), path, prompts, 1, False, "cpu", str(tmp_path), 40, False, stages),
+                       nprocs=8, start_method="spawn", join=True)
+    allv = pickle.load(open(tmp_path / "out.pkl", "rb"))
+    owner = [v for v in allv if v and v[0] is not None]
+    assert len(owner) == 1
+    for a, b in zip(owner[0], ref):
+        assert _close(a, b)
+
+
+@pytest.mark.parametrize("weights", ["host", "stream"])
+def test_data_parallel_sharded_world8(single, tmp_path, weights):
+    """Eight data-parallel ranks with 1/8-sliced weights all-gathered per layer (pinned slices, or
+    streamed from the layer files by each rank's loader thread with the gathers issued from the
+    main thread in program order); 7 prompts, so rank 7 has none and still joins every gather."""
+    path, prompts, ref = single
+    assert len(prompts) < 8
+    mp.start_processes(_dp_shard_worker, args=(8, _port(), path, prompts, 1, str(tmp_path), None, "", weights),
+                       nprocs=8, start_method="spawn", join=True)
+    allv = pickle.load(open(tmp_path / "out.pkl", "rb"))
+    assert allv[7] == []
+    got = sum(allv, [])
+    assert len(got) == len(ref)
+    for a, b in zip(got, ref):
+        assert _close(a, b)
+
+
+def test_data_parallel_resume_world8(single, tmp_path):
+    """DP over 8 ranks + --resume_dir: rank 5 dies entering shard 3; the relaunch resumes every rank
+    at shard 2 (the latest checkpoint all 8 hold) and matches the one-process run."""
+    path, prompts, ref = single
+    ck = str(tmp_path / "ck")
+    with pytest.raises(Exception):
+        mp.start_processes(_dp_shard_worker, args=(8, _port(), path, prompts, 1, str(tmp_path), ck, "5:3"),
+                           nprocs=8, start_method="spawn", join=True)
+    mp.start_processes(_dp_shard_worker, args=(8, _port(), path, prompts, 1, str(tmp_path), ck, ""),
+                       nprocs=8, start_method="spawn", join=True)
+    assert pickle.load(open(tmp_path / "resumed.pkl", "rb")) == [2.0] * 8
+    got = sum(pickle.load(open(tmp_path / "out.pkl", "rb")), [])
+    for a, b in zip(got, ref):
+        assert _close(a, b)

@@ -1,4 +1,6 @@
 """End-to-end engine on an MI355X (HIP kernels) vs the fp32 CPU oracle."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -202,25 +204,29 @@ def test_activation_store_no_race_large_batches(mid_model, tmp_path, storage):
     r.close()
 
 
-def test_qkv_two_streams_bitwise(mid_model):
-    """RMSNorm + QKV row chunks alternating between two streams (models/llama.py
-    ``_qkv_two_streams``, FLS_QKV_STREAMS=2) == one stream, bitwise: the same kernels per row."""
-    from flexible_llm_sharding_amd.models import llama
+def test_fused_norm_qkv_matches_unfused(mid_model):
+    """RMSNorm + QKV fused (ln1 folded into W_qkv when the weights land, the row statistic in the
+    GEMM epilogue: the default) vs the explicit RMSNorm + GEMM (FLS_QKV_FOLD=0, 2,048-row chunks):
+    the same math in other fp16 roundings, so the scores agree to fp16 noise, with the same argmax;
+    the pruned last layer and every-row last layer agree too."""
+    from flexible_llm_sharding_amd import knobs
     cfg, store, tok, prompts = mid_model
     outs = []
-    old = llama.QKV_STREAMS
-    try:
-        for n in (1, 2):
-            llama.QKV_STREAMS = n
+    for fold in ("1", "0"):
+        os.environ["FLS_QKV_FOLD"] = fold
+        try:
             r = ShardedRunner(cfg, store, "cuda:0", tok, layer_num_per_shard=1, storage_location="gpu")
-            r.ctx.qkv_chunk = 2048                    # 16,128 packed rows -> 8 chunks (4 per stream)
+            assert r.ctx.fused_norm == (fold == "1")
+            r.ctx.qkv_chunk = 2048
             outs.append(r(prompts))
             r.close()
-    finally:
-        llama.QKV_STREAMS = old
+        finally:
+            os.environ.pop("FLS_QKV_FOLD", None)
+    assert knobs.get("FLS_QKV_FOLD") == "1"
     for a, b in zip(*outs):
         assert np.isfinite(a.astype(np.float32)).all()
-        assert np.array_equal(a, b)
+        assert np.abs(a.astype(np.float32) - b.astype(np.float32)).max() < 2e-3
+        assert (a.argmax(-1) == b.argmax(-1)).mean() > 0.9
 
 
 @pytest.mark.parametrize("streaming", [False, True])

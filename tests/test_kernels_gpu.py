@@ -772,3 +772,144 @@ def test_gemm_v11_production_shape_bitwise(ops):
     rows = torch.arange(0, M, 97, device=DEV)
     want = x[rows].float() @ w.float().t() + r0[rows].float()
     assert rel_err(a[rows], want) < 2e-3
+
+
+# ------------------------------------------------------------------ fused RMSNorm (round 5)
+@pytest.mark.parametrize("H", [256, 1000 // 8 * 8, 4096, 8192, 5120])
+@pytest.mark.parametrize("gather", [False, True])
+def test_row_rstd(ops, H, gather):
+    """Row statistics of the fused RMSNorm: rsqrt(mean(x^2) + eps) in fp32 per row (or per
+    gathered row) == the fp32 reference."""
+    x = rnd(61, H, scale=3.0, seed=101)
+    idx = torch.tensor([3, 60, 0, 7, 7], dtype=torch.int32, device=DEV) if gather else None
+    r = ops.row_rstd(x, 1e-5, row_idx=idx)
+    xs = x.float()[idx.long()] if gather else x.float()
+    want = torch.rsqrt(xs.pow(2).mean(-1) + 1e-5)
+    torch.cuda.synchronize()
+    assert r.dtype == torch.float32 and r.shape == want.shape
+    assert ((r - want).abs() / want).max().item() < 1e-5
+
+
+def test_fold_norm_bitwise(ops):
+    """W[n, k] *= gamma[k] in place == torch's fp16(fp32 product), bitwise (a strided W view too)."""
+    w = rnd(300, 1024, scale=0.05, seed=102)
+    g = rnd(1024, scale=0.7, seed=103) + 1.0
+    want = (w.float() * g.float()).half()
+    ops.fold_norm(w, g)
+    big = rnd(64, 2048, scale=0.05, seed=104)
+    view = big[:, 1024:]                                   # row stride 2048
+    want_v = (view.float() * g.float()).half()
+    ops.fold_norm(view, g)
+    torch.cuda.synchronize()
+    assert torch.equal(w, want)
+    assert torch.equal(big[:, 1024:], want_v)
+
+
+def test_copy_rows(ops):
+    """Row gather / scatter / both (the pruned layer's rows, the prefix K/V capture) == torch."""
+    x = rnd(50, 2048, seed=105)
+    src = torch.tensor([4, 49, 0, 17], dtype=torch.int32, device=DEV)
+    dst = torch.tensor([9, 1, 30, 2], dtype=torch.int32, device=DEV)
+    g = ops.gather_rows(x, src)
+    y = torch.zeros(40, 2048, dtype=torch.float16, device=DEV)
+    ops.scatter_rows(g, dst, y)
+    z = torch.zeros(40, 512, dtype=torch.float16, device=DEV)
+    ops.copy_rows(x[:, 1024:1536], src, z, dst)            # strided source columns
+    torch.cuda.synchronize()
+    assert torch.equal(g, x[src.long()])
+    want = torch.zeros_like(y)
+    want[dst.long()] = x[src.long()]
+    assert torch.equal(y, want)
+    assert torch.equal(z, want[:, 1024:1536])
+
+
+@pytest.mark.parametrize("M,path", [(1, "auto"), (7, "auto"), (100, "auto"), (160, "auto"), (300, "auto"),
+                                    (517, "auto"), (1000, "v11"), (1000, "v10"), (1000, "mid"), (33, "generic")])
+@pytest.mark.parametrize("epi", ["none_bias", "resid_alpha", "swiglu", "rope128", "rope64"])
+def test_gemm_row_scale_every_path(ops, ref, M, path, epi):
+    """Per-row scale of the raw product (the fused RMSNorm statistic) and the residual alpha
+    (Granite) on every GEMM path: auto (skinny / split-K / mid by M), and v11, v10 main, mid-M and
+    the generic kernel forced: == the fp32 reference of the row-scaled product, and a unit scale /
+    alpha == no scale, bitwise."""
+    from flexible_llm_sharding_amd.config import ModelConfig
+    from flexible_llm_sharding_amd.models.llama import rope_tables
+    K, N = 2048, 1024
+    x = rnd(M, K, seed=111)
+    rs = (torch.rand(M, generator=torch.Generator().manual_seed(112)) * 2 + 0.1).to(DEV)
+    ones = torch.ones(M, dtype=torch.float32, device=DEV)
+    xs = x.float().cpu() * rs.cpu()[:, None]
+    if epi == "swiglu":
+        w = rnd(2 * N, K, scale=0.05, seed=113)
+        run = lambda s: ops.swiglu_up(x, w, rscale=s)                                          # noqa: E731
+        want = ref.swiglu_up(xs, w.float().cpu())
+    elif epi.startswith("rope"):
+        hd = int(epi[4:])
+        nh, nkv = N // hd // 2, N // hd // 4
+        n = (nh + 2 * nkv) * hd
+        w = rnd(n, K, scale=0.05, seed=114)
+        b = rnd(n, scale=0.5, seed=115)
+        cfg = ModelConfig(hidden_size=nh * hd, num_attention_heads=nh, num_key_value_heads=nkv)
+        cos, sin = rope_tables(cfg, 4096)
+        pos = torch.randint(0, 4000, (M,), dtype=torch.int32, device=DEV)
+        run = lambda s: ops.qkv_rope(x, w, pos, cos.to(DEV), sin.to(DEV), nh, nkv, hd, bias=b, rscale=s)  # noqa: E731
+        want = ref.qkv_rope(xs, w.float().cpu(), pos.cpu(), cos, sin, nh, nkv, hd, bias=b.float().cpu())
+    else:
+        w = rnd(N, K, scale=0.05, seed=116)
+        r0 = rnd(M, N, seed=117)
+        b = rnd(N, scale=0.5, seed=118)
+        if epi == "resid_alpha":
+            run = lambda s: ops.gemm(x, w, EPI_RESID, out=r0.clone(), resid=r0, bias=b, rscale=s,      # noqa: E731
+                                     alpha=0.7 if s is not None else 1.0)
+            want = r0.float().cpu() + 0.7 * (xs @ w.float().cpu().t() + b.float().cpu())
+        else:
+            run = lambda s: ops.gemm(x, w, EPI_NONE, bias=b, rscale=s)                         # noqa: E731
+            want = xs @ w.float().cpu().t() + b.float().cpu()
+    modes = {"auto": (1, 1, 1), "v11": (2, 1, 1), "v10": (0, 0, 1), "mid": (0, 2, 1), "generic": (0, 0, 0)}[path]
+    k = ops.k
+    old = (k.fls_gemm_set_v11(modes[0]), k.fls_gemm_set_mid(modes[1]), k.fls_gemm_set_skinny(modes[2], 0),
+           k.fls_gemm_set_splitk(modes[2]))
+    try:
+        if path == "generic":
+            x = x[:, :K - 8]                               # an odd K keeps every tiled kernel out
+            xs = xs[:, :K - 8]
+            w = w[:, :K - 8]
+            want = {"none_bias": lambda: xs @ w.float().cpu().t() + b.float().cpu(),
+                    "resid_alpha": lambda: r0.float().cpu() + 0.7 * (xs @ w.float().cpu().t() + b.float().cpu()),
+                    "swiglu": lambda: ref.swiglu_up(xs, w.float().cpu()),
+                    "rope128": lambda: ref.qkv_rope(xs, w.float().cpu(), pos.cpu(), cos, sin, nh, nkv, hd,
+                                                    bias=b.float().cpu()),
+                    "rope64": lambda: ref.qkv_rope(xs, w.float().cpu(), pos.cpu(), cos, sin, nh, nkv, hd,
+                                                   bias=b.float().cpu())}[epi]()
+        got = run(rs)
+        unscaled, unit = run(None), (ops.gemm(x, w, EPI_RESID, out=r0.clone(), resid=r0, bias=b, rscale=ones)
+                                     if epi == "resid_alpha" else run(ones))
+    finally:
+        k.fls_gemm_set_v11(old[0])
+        k.fls_gemm_set_mid(old[1])
+        k.fls_gemm_set_skinny(old[2], 0)
+        k.fls_gemm_set_splitk(old[3])
+    torch.cuda.synchronize()
+    assert rel_err(got.cpu(), want) < 3e-3
+    assert torch.equal(unit, unscaled)
+
+
+def test_embed_scaled(ops, ref):
+    """Granite's embedding_multiplier inside the gather: fp16(e * m) == torch, bitwise."""
+    table = rnd(1000, 512, seed=121)
+    ids = torch.randint(0, 1000, (77,), dtype=torch.int32, device=DEV)
+    y = ops.embed(ids, table, torch.float16, scale=12.0)
+    out = torch.empty(77, 512, dtype=torch.float16, device=DEV)
+    y2 = ops.embed(ids, table, torch.float16, out=out)
+    torch.cuda.synchronize()
+    assert torch.equal(y, (table[ids.long()].float() * 12.0).half())
+    assert y2.data_ptr() == out.data_ptr() and torch.equal(out, table[ids.long()])
+
+
+@pytest.mark.parametrize("V", [32000, 37])
+def test_softmax_scaled(ops, V):
+    """Granite's logits_scaling inside the softmax: softmax(fp16(l / s)) == torch."""
+    x = rnd(9, V, scale=8.0, seed=122)
+    y = ops.softmax(x, logits_scaling=8.0)
+    r = torch.softmax((x / 8.0).float(), -1)
+    torch.cuda.synchronize()
+    assert (y.float() - r).abs().max().item() < 1e-3
