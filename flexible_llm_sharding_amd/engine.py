@@ -130,6 +130,7 @@ class ShardedRunner:
             # their memory
             self.comm.warmup()
             self.comm.warmup_p2p()
+            self.comm.warmup_gather(0)         # the score gather to rank 0 after every call
             pcomm = getattr(prefetcher, "comm", None)
             if pcomm is not None and pcomm is not self.comm:
                 pcomm.warmup()
@@ -151,7 +152,7 @@ class ShardedRunner:
                 # device memory held outside the caching allocator before any weight slot exists:
                 # context, code objects, RCCL buffers (warmed up above) — planned as measured
                 self._outside = (device_used_bytes(self.dev) - torch.cuda.memory_reserved(self.dev) + (64 << 20)
-                                 + RUNTIME_RESERVE)
+                                 + RUNTIME_RESERVE + self._splitk_reserve())
             try:
                 # provisional (the call's token count is unknown yet); _plan_call is authoritative
                 token_budget, mlp_chunk, attn_rows, qkv_chunk, est = plan_for_vram(
@@ -215,7 +216,7 @@ class ShardedRunner:
             # the weight slots are raw hipMalloc blocks: the allocator gets the rest of the cap
             from .runtime.memplan import RUNTIME_RESERVE, cap_allocator, device_used_bytes
             self._outside = (device_used_bytes(self.dev) - torch.cuda.memory_reserved(self.dev) + (64 << 20)
-                             + RUNTIME_RESERVE)
+                             + RUNTIME_RESERVE + self._splitk_reserve())
             slots = self.prefetcher.planned_hbm_bytes()
             self.vram_plan["allocator_limit_bytes"] = cap_allocator(self.dev, int(max_vram_gb * 1e9), slots)
         self.stats: Dict[str, float] = {}
@@ -280,6 +281,12 @@ class ShardedRunner:
         out = self.run_tokenized(tps)
         self.stats["host_tokenize_s"] = t_tok
         return out
+
+    def _splitk_reserve(self) -> int:
+        """Bytes the plan keeps for this runner's split-K scratch when the arena's tail cannot hold
+        it (a small-M call under a cap allocates it lazily, inside the allocator limit: ADVICE r4)."""
+        from .ops.hip_backend import SPLITK_WS_BYTES
+        return SPLITK_WS_BYTES if self._splitk_ws is not None else 0
 
     def _splitk_scratch(self):
         from .ops.hip_backend import SPLITK_WS_BYTES

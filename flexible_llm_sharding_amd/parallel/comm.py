@@ -81,6 +81,27 @@ class Comm:
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
 
+    def warmup_gather(self, dst: int = 0) -> None:
+        """The operations of :meth:`gather_scores` once, tiny: a header all-gather on the default
+        group and a send / receive from every rank to ``dst`` (RCCL sets up the default group's P2P
+        channels at the first one).  Run at runner construction, before a ``--max_vram_gb`` plan
+        measures device memory, so the first score gather after a pass allocates nothing the plan
+        did not count."""
+        if not self.active:
+            return
+        dev = self.device if self.backend == "nccl" else torch.device("cpu")
+        t = torch.zeros(1, dtype=torch.int64, device=dev)
+        allh = torch.empty(self.world, dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(allh, t)
+        if self.rank != dst:
+            dist.send(t, dst)
+        else:
+            for r in range(self.world):
+                if r != dst:
+                    dist.recv(t, r)
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
     # -------------------------------------------------------------- p2p
     def setup_p2p_edges(self, edges) -> None:
         """Create one process group per DIRECTED hand-off edge (src, dst).
@@ -447,6 +468,9 @@ class LoopbackComm(Comm):
         self.hub.exchange(self.rank, None)
 
     def warmup(self) -> None:
+        pass
+
+    def warmup_gather(self, dst: int = 0) -> None:
         pass
 
     def all_reduce_max(self, x: float) -> float:

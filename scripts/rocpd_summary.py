@@ -28,10 +28,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("db")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--embeds-per-pass", type=int, default=1,
+                    help="embedding launches per pass (one per micro-batch)")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     rows = c.execute("select name, start, end from kernels order by start").fetchall()
-    starts = [i for i, r in enumerate(rows) if "embed_kernel" in r[0]]
+    starts = [i for i, r in enumerate(rows) if "embed_kernel" in r[0]][::a.embeds_per_pass]
     passes = []
     for j, i0 in enumerate(starts):
         i1 = starts[j + 1] if j + 1 < len(starts) else len(rows)

@@ -142,16 +142,36 @@ def test_data_parallel_loopback_7b(seven_b, G, pool, n_prompts):
     sub-layer piece pool of the --max_vram_gb mode (AllGatherPiecePool: one attention + two MLP
     slots, each piece all-gathered on its own), with 3 prompts on 4 ranks (an empty rank acquires
     and releases every layer, its pieces still gathered in pass order)."""
+    cfg, full, tok = seven_b
+    prompts = synthetic_prompts(n_prompts, 1024, 5, 64, cfg.vocab_size, seed=G)
+    _dp_loopback_check(cfg, full, tok, G, pool, prompts, seed=5)             # seven_b's seed
+
+
+def test_data_parallel_loopback_70b_eight_ranks(tmp_path):
+    """The scaling run's default path (bench.py --gpus 8: data parallel, sub-layer pieces all-gathered
+    under the 6 GB plan, AllGatherPiecePool) with 8 ranks as threads on one MI355X at Llama-2-70B
+    layer geometry (2 decoder layers: 70B-sized attention / MLP pieces, 8-way slices of them),
+    12 prompts over 8 ranks (uneven slices), two calls each: every rank's scores equal the 1-GPU run
+    on its prompts bitwise."""
+    from flexible_llm_sharding_amd.config import preset
+    cfg = preset("llama2-70b", num_hidden_layers=2)
+    full = HostStore.synthetic(cfg, torch.device("cuda", 0), seed=7)
+    d = str(tmp_path / "tok")
+    write_synthetic_tokenizer(d, cfg.vocab_size)
+    tok = load_tokenizer(d)
+    prompts = synthetic_prompts(12, 1024, 5, 64, cfg.vocab_size, seed=8)
+    _dp_loopback_check(cfg, full, tok, 8, "pieces", prompts, seed=7)
+
+
+def _dp_loopback_check(cfg, full, tok, G, pool, prompts, seed):
     from flexible_llm_sharding_amd.parallel.data_parallel import (AllGatherPiecePool, AllGatherPrefetcher,
                                                                   SlicedHostStore)
     from flexible_llm_sharding_amd.parallel.planner import make_plan
-    cfg, full, tok = seven_b
     dev = torch.device("cuda", 0)
-    prompts = synthetic_prompts(n_prompts, 1024, 5, 64, cfg.vocab_size, seed=G)
     idx = np.array_split(np.arange(len(prompts)), G)
     names = cfg.layer_names()
-    stores = [SlicedHostStore.synthetic(cfg, dev, r, G, seed=5) for r in range(G)]   # seven_b's seed
-    hub = LoopbackHub(G, timeout_s=120)
+    stores = [SlicedHostStore.synthetic(cfg, dev, r, G, seed=seed) for r in range(G)]
+    hub = LoopbackHub(G, timeout_s=300)
     res, runners = {}, {}
 
     def run(r):
@@ -178,12 +198,13 @@ def test_data_parallel_loopback_7b(seven_b, G, pool, n_prompts):
     for t in ts:
         t.start()
     for t in ts:
-        t.join(timeout=300)
+        t.join(timeout=600)
     for r in range(G):
         assert not isinstance(res.get(r), BaseException), res.get(r)
     torch.cuda.synchronize()
     for rr in runners.values():
         rr.close()
+    del stores
     one = ShardedRunner(cfg, full, "cuda:0", tok, layer_num_per_shard=1, storage_location="gpu", token_budget=4096)
     for r in range(G):
         if not len(idx[r]):
@@ -208,7 +229,7 @@ def _port():
     return p
 
 
-def _mp_worker(rank, world, port, out_dir, storage, stages, dp, weights):
+def _mp_worker(rank, world, port, out_dir, storage, stages, dp, weights, cap=None, n_prompts=16):
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
                        "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
     from flexible_llm_sharding_amd.config import preset
@@ -223,15 +244,19 @@ def _mp_worker(rank, world, port, out_dir, storage, stages, dp, weights):
         write_synthetic_checkpoint(cfg, ck, seed=5, device=comm.device, unique_layers=2)
     comm.barrier()
     tok = load_tokenizer(ck)
-    prompts = synthetic_prompts(16, 1024, 5, 64, cfg.vocab_size, seed=3)
+    prompts = synthetic_prompts(16, 1024, 5, 64, cfg.vocab_size, seed=3)[:n_prompts]
     if dp:
         args = SimpleNamespace(model_path=ck, layer_num_per_shard=1, storage_location=storage,
                                disk_folder=os.path.join(out_dir, f"spill{rank}"), max_activation_in_cpu=100,
                                prefix_attention="bidirectional", token_budget=4096, resident=False, dtype=None,
-                               verbose=False)
+                               verbose=False, max_vram_gb=cap)
         r = build_dp_sharded_runner(args, cfg, comm.device, comm, tok, weight_cache=weights)
+        if cap:
+            # the capped data-parallel default: sub-layer pieces all-gathered per piece
+            assert type(r.prefetcher).__name__ == "AllGatherPiecePool"
         idx = np.array_split(np.arange(len(prompts)), world)[rank]
         outs = r([prompts[i] for i in idx])
+        outs = r([prompts[i] for i in idx])           # second call: the piece / slot rotation
     else:
         from flexible_llm_sharding_amd.runtime.stream import FileLayerSource
         r = ShardedRunner(cfg, FileLayerSource(cfg, ck), comm.device, tok, layer_num_per_shard=1,
@@ -239,7 +264,7 @@ def _mp_worker(rank, world, port, out_dir, storage, stages, dp, weights):
                           comm=comm, token_budget=4096, pipeline_stages=stages, max_activation_in_cpu=2)
         outs = r(prompts)
         outs = r(prompts)                             # the runner-lifetime inbox, second call
-    allv = comm.gather_object(outs, dst=0)
+    allv = comm.gather_scores(outs, dst=0)           # the production score path (api.run_all)
     if rank == 0:
         with open(os.path.join(out_dir, "out.pkl"), "wb") as f:
             pickle.dump(allv, f)
@@ -266,6 +291,7 @@ def one_gpu_ref(tmp_path_factory):
 
 def _spawn(d, world, *args):
     import torch.multiprocessing as mp
+    world = min(world, torch.cuda.device_count())
     mp.start_processes(_mp_worker, args=(world, _port(), d) + args, nprocs=world, start_method="spawn", join=True)
     return pickle.load(open(os.path.join(d, "out.pkl"), "rb"))
 
@@ -289,6 +315,50 @@ def test_data_parallel_rccl_matches_one_gpu(one_gpu_ref, weights):
     got = sum(_spawn(d, 2, "cpu", "round_robin", True, weights), [])
     assert len(got) == len(want)
     for a, b in zip(got, want):
+        assert np.abs(a.astype(np.float32) - b.astype(np.float32)).max() < 2e-3
+
+
+@multi
+@pytest.mark.parametrize("n_prompts", [16, 1])
+def test_data_parallel_rccl_capped_piece_pool(one_gpu_ref, n_prompts):
+    """The bench's data-parallel default under --max_vram_gb (AllGatherPiecePool: each rank H2Ds
+    1/G of every attention / MLP piece, RCCL all-gathers complete them in pass order) over a real
+    2-rank nccl group, two calls; with 1 prompt rank 1 is empty and still joins every gather."""
+    d, want = one_gpu_ref
+    got = sum(_spawn(d, 2, "cpu", "round_robin", True, "host", 2.4, n_prompts), [])
+    assert len(got) == n_prompts
+    for a, b in zip(got, want):
+        assert np.abs(a.astype(np.float32) - b.astype(np.float32)).max() < 2e-3
+
+
+def _main_cli(tmp, ck, n_gpus, extra):
+    out = os.path.join(tmp, f"scores_{n_gpus}_{'_'.join(extra) or 'mp'}.pkl")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "main.py"), "--model_path", ck, "--prompt_pickle",
+                        os.path.join(tmp, "prompts.pkl"), "--output_file", out, "--num_gpus", str(n_gpus),
+                        "--storage_location", "cpu"] + extra, cwd=tmp, capture_output=True, text=True, timeout=900,
+                       env=dict(os.environ, PYTHONPATH=ROOT))
+    assert r.returncode == 0, r.stderr[-3000:]
+    return pickle.load(open(out, "rb"))
+
+
+@multi
+@pytest.mark.parametrize("extra", [[], ["--data_parallel", "True"], ["--data_parallel", "True", "--max_vram_gb", "2.4"]])
+def test_main_cli_two_gpus_matches_one(one_gpu_ref, extra):
+    """``main.py --num_gpus 2`` end to end (spawned ranks, RCCL hand-offs or all-gathers, rank-0
+    score gather, output pickles): model parallel (default) and data parallel (capped too) equal
+    the one-GPU CLI run."""
+    d, _ = one_gpu_ref
+    ck = os.path.join(d, "ckpt")
+    from flexible_llm_sharding_amd.config import preset
+    cfg = preset("llama2-7b", num_hidden_layers=4)
+    prompts = synthetic_prompts(5, 300, 4, 12, cfg.vocab_size, seed=4)
+    with open(os.path.join(d, "prompts.pkl"), "wb") as f:
+        pickle.dump(prompts, f)
+    one = _main_cli(d, ck, 1, [x for x in extra if x != "True" and x != "--data_parallel"])
+    two = _main_cli(d, ck, 2, extra)
+    assert len(one) == len(two) == len(prompts)
+    for a, b in zip(one, two):
+        assert a.shape == b.shape
         assert np.abs(a.astype(np.float32) - b.astype(np.float32)).max() < 2e-3
 
 
