@@ -74,6 +74,8 @@ int fls_gemm(const void* A, const void* W, void* C, const void* R, int M, int N,
              const float* sin_t, int rope_cols, int head_dim, const void* bias, const float* rscale,
              float alpha, void* ws, uint64_t ws_bytes,
              fls_stream_t s);   // ws: device scratch for the small-M split-K path (may be null)
+// out[r] = first index of the maximum of row r of non-negative fp16 values (greedy decoding)
+int fls_argmax_rows(const void* x, int ld, int rows, int V, int* out, fls_stream_t s);
 // rstd[r] = rsqrt(mean(x[row]^2) + eps) in fp32, row = row_idx ? row_idx[r] : r (fused RMSNorm:
 // the statistic of the rows a norm-folded projection reads raw)
 int fls_row_rstd(const void* x, int ldx, const int* row_idx, int rows, int H, float eps, float* rstd,

@@ -210,6 +210,41 @@ __global__ __launch_bounds__(256) void softmax_kernel(const half_t* __restrict__
   }
 }
 
+// greedy token of each row of fp16 probabilities: the FIRST index of the row's maximum (numpy
+// argmax on the scores the reference hands back, main.py:85-88).  Probabilities are >= 0, so
+// their bit patterns order like their values; each thread keeps (bits, first index), then a tree
+// reduction over the block.
+__global__ __launch_bounds__(256) void argmax_rows_kernel(const half_t* __restrict__ x, int ld, int V,
+                                                        int* __restrict__ out) {
+  __shared__ unsigned sb[256];
+  __shared__ int si[256];
+  const unsigned short* r = (const unsigned short*)(x + (size_t)blockIdx.x * ld);
+  unsigned best = 0;
+  int bi = 0x7fffffff;
+  for (int c = threadIdx.x; c < V; c += 256) {
+    const unsigned b = r[c];
+    if (b > best || (b == best && c < bi)) {
+      best = b;
+      bi = c;
+    }
+  }
+  sb[threadIdx.x] = best;
+  si[threadIdx.x] = bi;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+      const unsigned b = sb[threadIdx.x + s];
+      const int i = si[threadIdx.x + s];
+      if (b > sb[threadIdx.x] || (b == sb[threadIdx.x] && i < si[threadIdx.x])) {
+        sb[threadIdx.x] = b;
+        si[threadIdx.x] = i;
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[blockIdx.x] = si[0] == 0x7fffffff ? 0 : si[0];
+}
+
 // counter-based normal generator (splitmix64 -> Box-Muller), 8 values/thread
 __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
   z += 0x9E3779B97F4A7C15ull;
@@ -421,6 +456,13 @@ extern "C" int fls_softmax_rows(const void* logits, void* probs, int rows, int V
   if (rows <= 0) return 0;
   hipLaunchKernelGGL(softmax_kernel, dim3(rows), dim3(256), 0, (hipStream_t)s, (const half_t*)logits,
                      (half_t*)probs, V, inv_scale);
+  FLS_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int fls_argmax_rows(const void* x, int ld, int rows, int V, int* out, fls_stream_t s) {
+  if (rows <= 0) return 0;
+  hipLaunchKernelGGL(argmax_rows_kernel, dim3(rows), dim3(256), 0, (hipStream_t)s, (const half_t*)x, ld, V, out);
   FLS_CHECK_LAUNCH();
   return 0;
 }

@@ -77,6 +77,7 @@ def _load_kernels(path: str = _KERNELS):
     _bind(lib, "fls_gemm", c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
           c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
           c_float, c_void_p, c_uint64, c_void_p)
+    _bind(lib, "fls_argmax_rows", c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p)
     _bind(lib, "fls_row_rstd", c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p)
     _bind(lib, "fls_fold_norm", c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p)
     _bind(lib, "fls_copy_rows", c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p)

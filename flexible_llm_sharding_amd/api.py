@@ -265,17 +265,23 @@ def generation_loop(args, runner, comm: Comm, tok, original_prompts: Sequence, s
             prof = cProfile.Profile()
             prof.enable()
         outputs = run_all(args, runner, comm, input_prompts)
+        # the greedy tokens the runner took on the device (one rank holding every prompt), else a
+        # host argmax over the gathered scores
+        dev_tok = getattr(runner, "last_tokens", None) if comm.world == 1 else None
+        if not dev_tok or len(dev_tok) != len(outputs) or any(t is None for t in dev_tok):
+            dev_tok = None
         if prof is not None:
             prof.disable()
             prof.dump_stats(f"{knobs.get('FLS_PROFILE_OUT')}.{i_new}")
         if comm.rank == 0:
+            toks = dev_tok if dev_tok is not None else [greedy_tokens(o) for o in outputs]
             if i_new == 0:
                 step_scores = [[o] for o in outputs]
-                step_tokens = [[greedy_tokens(o)] for o in outputs]
+                step_tokens = [[t] for t in toks]
             else:
                 for pi, o in enumerate(outputs):
                     step_scores[pi].append(o)
-                    step_tokens[pi].append(greedy_tokens(o))
+                    step_tokens[pi].append(toks[pi])
             # s + tok.decode(t) for every suffix (main.py:86-88), the decodes in one batched call
             news = [np.concatenate(step_tokens[pi], axis=1) for pi in range(len(input_prompts))]
             flat = [t for nt in news for t in nt]

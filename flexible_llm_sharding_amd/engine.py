@@ -228,6 +228,8 @@ class ShardedRunner:
         self.hip_graphs = bool(hip_graphs and self.cuda and resident and self.plan.mode != "mp"
                                and not resume_dir)
         self._graphs = None
+        self._decode_graphs = None
+        self.last_tokens: List[Optional[np.ndarray]] = []   # last call's greedy token per suffix
         if self.cuda and not self.hip_graphs:
             from .models.llama import Workspace
             self.ctx.ws = Workspace(self.dev, self.act_dtype)   # fixed scratch buffers (VRAM plan)
@@ -401,7 +403,10 @@ class ShardedRunner:
         self.ctx.prefix_entry = entry
         try:
             with self._workspace():
-                outputs = self._run_batches(tps, batches, t_start)
+                if self._decode_graphable(batches, cached):
+                    outputs = self._run_graphed(tps, batches, t_start, entry=entry)
+                else:
+                    outputs = self._run_batches(tps, batches, t_start)
         except BaseException:
             if entry is not None and not cached:
                 self.prefix_cache.drop(entry)
@@ -767,13 +772,9 @@ class ShardedRunner:
         if px.inbox is not None:
             px.inbox.end_call()
             rx_stats = {f"rx_{k}": float(v) for k, v in px.inbox.stats.items()}
-        for batch, host, ev, pool_buf in px.out_pending:
-            probs = host.numpy()
-            r = 0
-            for j, pid in enumerate(batch.prompt_ids):
-                ns = batch.n_suffix[j]
-                px.outputs[pid] = np.expand_dims(probs[r:r + ns].astype(np.float16, copy=True), axis=1)
-                r += ns
+        self.last_tokens = [None] * len(px.tps)
+        for batch, host, ev, pool_buf, am in px.out_pending:
+            self._collect(batch, host.numpy(), am, px.outputs)
             if pool_buf is not None:
                 store.recycle_host(pool_buf)
         store.clear()
@@ -897,40 +898,63 @@ class ShardedRunner:
             state = run_layer(self.ctx, name, self._W_all[name], state, batch, meta)
         return state
 
-    def _run_graphed(self, tps, batches, t_start: float) -> List[Optional[np.ndarray]]:
-        """Resident-weights path: one graph replay per micro-batch (runtime/graphs.py).
+    def _decode_graphable(self, batches, cached: bool) -> bool:
+        """A decode-like call (suffix K/V reuse: prefixes and kept suffix tokens from the cache)
+        on weights that stay at fixed HBM addresses (resident, or an HBM cache holding every
+        shard), on one rank: the whole call replays as captured HIP graphs (``DecodeGraphs``)."""
+        pf = self.prefetcher
+        return bool(cached and self.cuda and self.plan.mode == "single" and not self.resume_dir
+                    and knobs.get_int("FLS_DECODE_GRAPHS") and batches
+                    and all(b.work2 is not None for b in batches)
+                    and (pf.resident or (getattr(pf, "all_kept_loaded", None) is not None and pf.all_kept_loaded())))
+
+    def _run_graphed(self, tps, batches, t_start: float, entry=None) -> List[Optional[np.ndarray]]:
+        """Static-weights path: one graph replay per micro-batch (runtime/graphs.py): resident
+        full forwards (``--hip_graphs``), or decode-like calls on the prefix / suffix K/V cache
+        ``entry`` (exact shapes; the graph reads and writes the entry's per-layer K/V in place).
 
         Activations never leave HBM (there is no shard boundary inside the
         graph), so ``storage_location`` has nothing to park.
         """
-        from .runtime.graphs import GraphedForward
+        from .runtime.graphs import DecodeGraphs, GraphedForward
         pf = self.prefetcher
         if not self._W_all:
             for k in range(len(self.my_shards)):
                 self._W_all.update(pf.acquire(k))
-        if self._graphs is None:
-            self._graphs = GraphedForward(self.dev, self._forward_all)
+        if entry is not None:
+            if getattr(self, "_decode_graphs", None) is None:
+                self._decode_graphs = DecodeGraphs(self.dev, self._forward_all)
+            graphs = self._decode_graphs
+            run = lambda b: graphs.run(b, entry)          # noqa: E731
+        else:
+            if self._graphs is None:
+                self._graphs = GraphedForward(self.dev, self._forward_all)
+            graphs = self._graphs
+            run = graphs.run
         outputs: List[Optional[np.ndarray]] = [None] * len(tps)
         flops = 0.0
         pending = []
         store = self._get_store()
-        for batch in batches:
-            probs = self._graphs.run(batch)
-            nbytes = probs.numel() * probs.element_size()
-            pool_buf = store.host_buffer(nbytes)
-            host = pool_buf[:nbytes].view(probs.dtype).view(probs.shape)
-            host.copy_(probs, non_blocking=True)     # same stream: ordered before the next replay
-            pending.append((batch, host, pool_buf))
-            flops += sum(layer_flops(self.cfg, batch, self._pruned(n)) for n in self.names
-                         if layer_kind(n) == "decoder")
+        ws, self.ctx.ws = self.ctx.ws, None           # the graph's own memory pool, not the arena
+        try:
+            for batch in batches:
+                probs = run(batch)
+                am = self.ops.argmax_rows(probs)
+                nbytes = probs.numel() * probs.element_size()
+                pool_buf = store.host_buffer(nbytes + 4 * probs.shape[0])
+                host = pool_buf[:nbytes].view(probs.dtype).view(probs.shape)
+                host_am = pool_buf[nbytes:nbytes + 4 * probs.shape[0]].view(torch.int32)
+                host.copy_(probs, non_blocking=True)     # same stream: ordered before the next replay
+                host_am.copy_(am, non_blocking=True)
+                pending.append((batch, host, pool_buf, host_am))
+                flops += sum(layer_flops(self.cfg, batch, self._pruned(n)) for n in self.names
+                             if layer_kind(n) == "decoder")
+        finally:
+            self.ctx.ws = ws
         torch.cuda.synchronize(self.dev)
-        for batch, host, pool_buf in pending:
-            probs = host.numpy()
-            r = 0
-            for j, pid in enumerate(batch.prompt_ids):
-                ns = batch.n_suffix[j]
-                outputs[pid] = np.expand_dims(probs[r:r + ns].astype(np.float16, copy=True), axis=1)
-                r += ns
+        self.last_tokens = [None] * len(tps)
+        for batch, host, pool_buf, host_am in pending:
+            self._collect(batch, host.numpy(), host_am, outputs)
             store.recycle_host(pool_buf)
         wall = time.perf_counter() - t_start
         self.stats = {
@@ -940,7 +964,7 @@ class ShardedRunner:
             "decoder_flops": flops, "micro_batches": float(len(batches)),
             "weight_wait_s": pf.take_wait_seconds(), "weight_h2d_bytes": 0.0,
             "act_d2h_bytes": 0.0, "act_h2d_bytes": 0.0, "resumed_from_shard": 0.0,
-            "graph_captures": float(self._graphs.captures), "graph_replays": float(self._graphs.replays),
+            "graph_captures": float(graphs.captures), "graph_replays": float(graphs.replays),
         }
         return outputs
 
@@ -1011,20 +1035,39 @@ class ShardedRunner:
             print(f"rank{self.comm.rank}: resuming at shard {k0} from {ck.dir}")
         return ck, k0, (ck.load(k0) if k0 else {})
 
+    def _collect(self, batch: PackedBatch, probs: np.ndarray, am, outputs) -> None:
+        """Host scores of a finished micro-batch into ``outputs`` (prompt order) and its greedy
+        tokens into ``self.last_tokens`` (``am``: the rows' argmax, computed on the device)."""
+        am = am.numpy() if am is not None else None
+        r = 0
+        for j, pid in enumerate(batch.prompt_ids):
+            ns = batch.n_suffix[j]
+            outputs[pid] = np.expand_dims(probs[r:r + ns].astype(np.float16, copy=True), axis=1)
+            if am is not None:
+                self.last_tokens[pid] = am[r:r + ns].astype(np.int64).reshape(ns, 1)
+            r += ns
+
     def _start_output_copy(self, batch: PackedBatch, probs: torch.Tensor):
+        """D2H of a micro-batch's probabilities and of their row argmax (the greedy token of
+        each suffix: api.generation_loop needs no host pass over the [n_s, V] scores)."""
+        am = self.ops.argmax_rows(probs) if hasattr(self.ops, "argmax_rows") else None
         if not self.cuda:
-            return batch, probs.detach().to(torch.float16).cpu(), None, None
+            return batch, probs.detach().to(torch.float16).cpu(), None, None, am
         store = self._get_store()
         nbytes = probs.numel() * probs.element_size()
-        pool_buf = store.host_buffer(nbytes)
+        pool_buf = store.host_buffer(nbytes + 4 * probs.shape[0])
         host = pool_buf[:nbytes].view(probs.dtype).view(probs.shape)
+        host_am = pool_buf[nbytes:nbytes + 4 * probs.shape[0]].view(torch.int32)
         self.d2h_stream.wait_stream(torch.cuda.current_stream(self.dev))
         with torch.cuda.stream(self.d2h_stream):
             host.copy_(probs, non_blocking=True)
             probs.record_stream(self.d2h_stream)
+            if am is not None:
+                host_am.copy_(am, non_blocking=True)
+                am.record_stream(self.d2h_stream)
             ev = torch.cuda.Event()
             ev.record(self.d2h_stream)
-        return batch, host, ev, pool_buf
+        return batch, host, ev, pool_buf, (host_am if am is not None else None)
 
     def close(self):
         if self._inbox is not None:

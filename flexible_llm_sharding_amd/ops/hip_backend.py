@@ -435,6 +435,14 @@ class HipOps:
                                      _stream()), "fls_softmax")
         return probs
 
+    def argmax_rows(self, probs):
+        """[rows] int32: the first index of each row's maximum (non-negative fp16 probabilities)."""
+        _f16(probs, "probs")
+        out = torch.empty(probs.shape[0], dtype=torch.int32, device=probs.device)
+        _chk(self.k.fls_argmax_rows(probs.data_ptr(), probs.stride(0), probs.shape[0], probs.shape[1],
+                                    out.data_ptr(), _stream()), "fls_argmax_rows")
+        return out
+
     def lm_head_softmax(self, h, w, logits_scaling: float = 1.0):
         return self.softmax(self.linear(h, w), logits_scaling)
 

@@ -198,6 +198,9 @@ class TorchOps:
         logits = (self._c(h) @ self._c(w).t()).to(h.dtype)   # fp16 logits like nn.Linear in fp16
         return self.softmax(logits, logits_scaling)
 
+    def argmax_rows(self, probs: torch.Tensor) -> torch.Tensor:
+        return probs.float().argmax(-1).to(torch.int32)
+
     def softmax(self, logits: torch.Tensor, logits_scaling: float = 1.0) -> torch.Tensor:
         if logits_scaling != 1.0:                            # Granite: logits / logits_scaling
             logits = logits / logits_scaling

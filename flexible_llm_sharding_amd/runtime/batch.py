@@ -165,25 +165,25 @@ class PackedBatch:
             self._dev[key] = gs
         return self._dev[key]
 
+    def host_meta(self) -> dict:
+        """Every int32 metadata array the layers read (the keys of :meth:`device_tensors`)."""
+        m = {"ids": self.ids, "positions": self.positions, "work": self.work, "seg_lo": self.seg_lo,
+             "last_idx": self.last_idx, "last_pos": self.positions[self.last_idx].astype(np.int32),
+             "work_last": self.work_last}
+        for name in ("pfx_src", "pfx_dst", "sfx_src", "sfx_dst", "work2", "work2_last", "r2win"):
+            v = getattr(self, name)
+            if v is not None:
+                m[name] = v
+        return m
+
     def device_tensors(self, device) -> dict:
         """int32 metadata on ``device`` (cached; uploaded once, reused by all layers)."""
         key = str(device)
         if key not in self._dev:
             d = torch.device(device)
             nb = d.type != "cpu"
-            self._dev[key] = {
-                "ids": torch.from_numpy(self.ids).to(d, non_blocking=nb),
-                "positions": torch.from_numpy(self.positions).to(d, non_blocking=nb),
-                "work": torch.from_numpy(self.work).to(d, non_blocking=nb),
-                "seg_lo": torch.from_numpy(self.seg_lo).to(d, non_blocking=nb),
-                "last_idx": torch.from_numpy(self.last_idx).to(d, non_blocking=nb),
-                "last_pos": torch.from_numpy(self.positions[self.last_idx].astype(np.int32)).to(d, non_blocking=nb),
-                "work_last": torch.from_numpy(self.work_last).to(d, non_blocking=nb),
-            }
-            for name in ("pfx_src", "pfx_dst", "sfx_src", "sfx_dst", "work2", "work2_last", "r2win"):
-                v = getattr(self, name)
-                if v is not None:
-                    self._dev[key][name] = torch.from_numpy(v).to(d, non_blocking=nb)
+            self._dev[key] = {k: torch.from_numpy(np.ascontiguousarray(v)).to(d, non_blocking=nb)
+                              for k, v in self.host_meta().items()}
         return self._dev[key]
 
 

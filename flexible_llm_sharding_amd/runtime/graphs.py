@@ -126,3 +126,61 @@ class GraphedForward:
         g.replays += 1
         self.replays += 1
         return g.out[:batch.n_scored]
+
+
+class DecodeGraphs:
+    """Graph replay of decode-like calls: the later steps of ``--num_gen_token`` with the prefix
+    and suffix K/V caches (every prompt's prefix K/V and its suffixes' earlier tokens come from
+    the cache, one new row per suffix is computed) when every weight is in HBM (resident, or the
+    HBM cache holding every shard).  Such a step is ~800 launches of a few tens of microseconds
+    each; one graph replays them all.
+
+    Unlike :class:`GraphedForward` the shapes are EXACT (no bucket padding: a padded row would
+    also be captured into the suffix K/V cache), keyed by the batch's array shapes and the cache
+    entry, whose per-layer K/V buffers the graph reads and writes in place; consecutive steps of
+    one generation have the same shapes, so one capture serves them all.  The metadata of each
+    step (new token ids, positions, work items, cache rows and windows) is copied into the
+    graph's static inputs before the replay."""
+
+    def __init__(self, device, forward: Callable, max_graphs: int = 4):
+        self.dev = torch.device(device)
+        self.forward = forward
+        self.max_graphs = max_graphs
+        self.pool = torch.cuda.graph_pool_handle()
+        self.graphs: "OrderedDict[tuple, _Graph]" = OrderedDict()
+        self.captures = 0
+        self.replays = 0
+
+    @staticmethod
+    def key(batch: PackedBatch, entry) -> tuple:
+        return (id(entry), batch.r2_q_block, batch.q_block) + tuple(
+            (k, v.shape) for k, v in sorted(batch.host_meta().items()))
+
+    def run(self, batch: PackedBatch, entry) -> torch.Tensor:
+        key = self.key(batch, entry)
+        host = batch.host_meta()
+        g = self.graphs.get(key)
+        if g is None:
+            if len(self.graphs) >= self.max_graphs:
+                self.graphs.popitem(last=False)
+            meta = {k: torch.from_numpy(np.ascontiguousarray(v)).to(self.dev) for k, v in host.items()}
+            g = _Graph(meta)
+            s = torch.cuda.Stream(self.dev)
+            s.wait_stream(torch.cuda.current_stream(self.dev))
+            with torch.cuda.stream(s):
+                eager = self.forward(meta, batch)            # this step's result (+ lazy inits)
+            torch.cuda.current_stream(self.dev).wait_stream(s)
+            torch.cuda.synchronize(self.dev)
+            with torch.cuda.graph(g.graph, pool=self.pool, stream=s):
+                g.out = self.forward(meta, batch)            # captured, not run: the eager pass computed
+            torch.cuda.synchronize(self.dev)                 # this step (its cache writes are idempotent)
+            self.captures += 1
+            self.graphs[key] = g
+            return eager
+        self.graphs.move_to_end(key)
+        for k, v in host.items():
+            g.meta[k].copy_(torch.from_numpy(np.ascontiguousarray(v)), non_blocking=False)
+        g.graph.replay()
+        g.replays += 1
+        self.replays += 1
+        return g.out

@@ -405,3 +405,39 @@ def test_generation_suffix_kv_reuse_on_gpu(setup, sfx):
             assert (r.stats["suffix_tokens_reused"] > 0) == sfx
     plain.close()
     r.close()
+
+
+@pytest.mark.parametrize("weights", ["resident", "hbm_cache"])
+def test_decode_graphs_match_eager(setup, weights):
+    """Generation steps with the prefix + suffix K/V caches on weights that stay in HBM replay as
+    captured HIP graphs (DecodeGraphs: one capture, exact shapes, the cache entry's K/V written in
+    place by the graph): every step's scores == the eager runner (FLS_DECODE_GRAPHS=0) bitwise,
+    the graph captured once and replayed on the later steps of the same shape."""
+    path, cfg, tok, prompts, ref = setup
+    src = HostStore.from_model_path(cfg, path)
+    kw = {"resident": True} if weights == "resident" else {"hbm_cache_gb": 100.0}
+    outs = {}
+    for graphs in ("1", "0"):
+        os.environ["FLS_DECODE_GRAPHS"] = graphs
+        try:
+            r = ShardedRunner(cfg, src, "cuda:0", tok, layer_num_per_shard=1, prefix_kv_cache=True,
+                              suffix_kv_cache=True, **kw)
+            words = prompts[0][0].split()
+            steps = []
+            for step in range(5):
+                # one word per suffix per step: the decode shape (one new row per suffix) repeats
+                ps = [(pre, tuple(sf + (" " + " ".join(words[:step]) if step else "") for sf in sufs))
+                      for pre, sufs in prompts]
+                steps.append(r(ps))
+                if graphs == "1" and step >= 2:
+                    assert r.stats.get("graph_captures", 0) >= 1
+            if graphs == "1":
+                assert r.stats["graph_replays"] >= 1
+            outs[graphs] = steps
+            r.close()
+        finally:
+            os.environ.pop("FLS_DECODE_GRAPHS", None)
+    for sg, se in zip(outs["1"], outs["0"]):
+        for a, b in zip(sg, se):
+            assert np.isfinite(a.astype(np.float32)).all()
+            assert np.array_equal(a, b)

@@ -913,3 +913,15 @@ def test_softmax_scaled(ops, V):
     r = torch.softmax((x / 8.0).float(), -1)
     torch.cuda.synchronize()
     assert (y.float() - r).abs().max().item() < 1e-3
+
+
+def test_argmax_rows_first_index(ops):
+    """Greedy tokens on the device == numpy's argmax of the fp16 probabilities (first index on
+    ties, the reference's np.argmax, main.py:85-88)."""
+    x = torch.softmax(rnd(37, 32000, scale=3.0, seed=131).float(), -1).half()
+    x[3, 100] = x[3, 2000] = 0.5                          # a tie: the first index wins
+    x[5] = 0                                              # all equal
+    got = ops.argmax_rows(x)
+    torch.cuda.synchronize()
+    assert np.array_equal(got.cpu().numpy(), np.argmax(x.cpu().numpy(), axis=-1))
+    assert got[3].item() == 100 and got[5].item() == 0
