@@ -178,7 +178,9 @@ def loopback_main(a) -> int:
     kw = {} if a.num_layers is None else {"num_hidden_layers": a.num_layers}
     cfg = preset(a.model, **kw)
     t0 = time.perf_counter()
-    store = HostStore.synthetic(cfg, dev, seed=a.seed, pinned=not a.cpu)
+    from flexible_llm_sharding_amd import knobs
+    store = HostStore.synthetic(cfg, dev, seed=a.seed, pinned=not a.cpu,
+                                fold_norms=not a.cpu and knobs.get_int("FLS_QKV_FOLD") == 1)
     log(0, f"[bench] loopback x{R}: host store {store.total_bytes / 1e9:.1f} GB in {time.perf_counter() - t0:.1f}s")
     if not a.cpu:
         torch.cuda.empty_cache()
@@ -293,6 +295,11 @@ def main(argv=None):
     from flexible_llm_sharding_amd.utils.synthetic import synthetic_prompts
     from flexible_llm_sharding_amd.utils.tokenizer import clear_prefix_ids, load_tokenizer, write_synthetic_tokenizer
 
+    from flexible_llm_sharding_amd import knobs
+    # the pinned host store holds the weights with their RMSNorms folded into the projections that
+    # read the normalised rows (done once on the GPU while generating them): the fused-norm GEMMs
+    # stream them as they are (HostStore.fold_norms)
+    fold = not a.cpu and knobs.get_int("FLS_QKV_FOLD") == 1
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
@@ -327,9 +334,10 @@ def main(argv=None):
         if dp:
             # scatter-load: this rank keeps 1/G of every layer; layers re-assembled by RCCL all-gather
             store = SlicedHostStore.synthetic(cfg, dev, rank, world, seed=a.seed, names=[names[i] for i in mine],
-                                              progress=prog)
+                                              progress=prog, fold_norms=fold)
         else:
-            store = HostStore.synthetic(cfg, dev, seed=a.seed, names=[names[i] for i in mine], progress=prog)
+            store = HostStore.synthetic(cfg, dev, seed=a.seed, names=[names[i] for i in mine], progress=prog,
+                                        fold_norms=fold)
         log(rank, f"[bench] host store {store.total_bytes / 1e9:.1f} GB in {time.perf_counter() - t0:.1f}s")
         data_w = f"random-init {a.model} weights in {'HBM (resident)' if a.resident else 'pinned host RAM'}"
 

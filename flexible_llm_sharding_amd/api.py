@@ -83,12 +83,16 @@ def build_source(args, cfg: ModelConfig, comm: Comm, device: torch.device):
     plan = make_plan(len(names), args.layer_num_per_shard, comm.world, comm.rank, args.data_parallel,
                      getattr(args, "pipeline_stages", "round_robin"))
     mine = [names[i] for i in sorted({i for sh in plan.my_shards for i in sh})]
+    # GPU: host-cached weights are kept with their RMSNorms folded into the projections (once, on
+    # the device), which the fused-norm GEMMs read as they are (HostStore.fold_norms)
+    fold = device.type == "cuda" and knobs.get_int("FLS_QKV_FOLD") == 1
     if getattr(args, "synthetic", None):
-        return HostStore.synthetic(cfg, device, seed=0, pinned=device.type == "cuda", names=mine)
+        return HostStore.synthetic(cfg, device, seed=0, pinned=device.type == "cuda", names=mine, fold_norms=fold)
     src = FileLayerSource(cfg, args.model_path, names=mine, direct=getattr(args, "o_direct", False))
     if resolve_weight_cache(args, cfg, comm, mine, sliced=False) == "stream":
         return src
-    return HostStore.from_source(src, pinned=device.type == "cuda", names=mine)
+    st = HostStore.from_source(src, pinned=device.type == "cuda", names=mine)
+    return st.fold_norms(device) if fold else st
 
 
 def repeated_passes(args) -> bool:

@@ -196,10 +196,16 @@ class ShardedRunner:
             prefetcher = PiecePoolPrefetcher(source, self.names, my, self.dev)
         self.prefetcher = prefetcher or ShardPrefetcher(source, self.names, my, self.dev,
                                                         n_slots=n_slots, resident=resident, keep=keep)
-        # RMSNorm + QKV fused on the GPU: ln1 folded into W_qkv as each layer lands (on the copy
-        # stream, before the layer's ready event), the row statistic applied in the QKV epilogue
+        # RMSNorm fused into the projections on the GPU: the norm weights folded into W_qkv /
+        # W_gate/up — once for a whole host store (HostStore.norms_folded), or as each layer lands
+        # (on the copy stream, before the layer's ready event) — and the row statistic applied in
+        # the GEMM epilogue
         self.ctx.fused_norm = self._fused_norm_planned()
-        if self.ctx.fused_norm:
+        prefolded = bool(getattr(source, "norms_folded", False))
+        if prefolded and not self.ctx.fused_norm:
+            raise ValueError("the weight source holds norm-folded weights (HostStore.fold_norms): only the "
+                             "fused-norm HIP path can run them")
+        if self.ctx.fused_norm and not prefolded:
             from .models.llama import fold_layer_norms
             ops = self.ops
             self.prefetcher.on_load = lambda views: fold_layer_norms(ops, views)

@@ -214,11 +214,15 @@ def _resid(ctx: ExecContext, a: torch.Tensor, w: torch.Tensor, x: torch.Tensor, 
 
 
 def fold_layer_norms(ops, views: Dict[str, torch.Tensor]) -> None:
-    """Fold a decoder layer's input RMSNorm weight into its QKV projection, in place on the
-    loaded weights (W_qkv[n, k] *= ln1[k]): the fused path then needs no normalised copy of the
-    hidden state (ExecContext.fused_norm).  Called once per load, on the stream that loaded them."""
+    """Fold a decoder layer's RMSNorm weights into the projections that read the normalised rows,
+    in place (W_qkv[n, k] *= ln1[k]; dense MLPs: W_gate/up[n, k] *= ln2[k]): the fused path then
+    needs no normalised copy of the hidden state (ExecContext.fused_norm).  ``views`` may hold one
+    piece of the layer (attention or MLP); each pair present is folded.  Called once per load, on
+    the stream that loaded the weights, or once for a whole host store (HostStore.fold_norms)."""
     if "wqkv" in views and "ln1" in views:
         ops.fold_norm(views["wqkv"], views["ln1"])
+    if "wgu" in views and "ln2" in views and views["wgu"].dim() == 2:
+        ops.fold_norm(views["wgu"], views["ln2"])
 
 
 CHUNK_ALIGN = knobs.get_int("FLS_CHUNK_ALIGN")   # A/B knob (256: round 3's chunks)
@@ -418,6 +422,20 @@ def run_decoder(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, b
     step = balanced_step(T, max(1, ctx.mlp_chunk))
     if cfg.is_moe:
         return _moe_mlp(ctx, W, x, step)
+    if ctx.fused_norm:
+        # ln2 folded into W_gate/up: the SwiGLU GEMM reads the raw rows, scaled by their statistic
+        # in the epilogue; the arena holds [SwiGLU chunk | row statistics]
+        for s in range(0, T, step):
+            xs = x[s:s + step]
+            n = xs.shape[0]
+            ctx.phase((n, I), (1, 2 * n))
+            m = ctx.scratch(n, I)
+            rstd = ops.row_rstd(xs, eps, out=ctx.scratch_f32(n))
+            m = ops.swiglu_up(xs, W["wgu"], out=m, rscale=rstd)
+            y = _resid(ctx, m, W["wdown"], xs)
+            if y.data_ptr() != xs.data_ptr():
+                xs.copy_(y)
+        return x
     if T <= step:
         ctx.phase((T, H), (T, I))               # the attention-phase bytes are dead: reuse them
         h = ops.rmsnorm(x, W["ln2"], eps, out=ctx.scratch(T, H))

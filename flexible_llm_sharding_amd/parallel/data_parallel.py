@@ -78,12 +78,16 @@ class SlicedHostStore(HostStore):
 
     @classmethod
     def synthetic(cls, cfg, device, rank: int, world: int, seed: int = 0, std: float = 0.02,
-                  pinned: bool = True, names=None, progress=None) -> "SlicedHostStore":
+                  pinned: bool = True, names=None, progress=None, fold_norms: bool = False) -> "SlicedHostStore":
         base = HostStore.synthetic(cfg, device, seed=seed, std=std, pinned=pinned, names=names,
-                                   byte_range=(rank, world), progress=progress)
+                                   byte_range=(rank, world), progress=progress, fold_norms=fold_norms)
         st = cls(cfg, rank, world, torch.float16, pinned, names)
         st.buffers = base.buffers
+        st.norms_folded = base.norms_folded
         return st
+
+    def fold_norms(self, device):   # pragma: no cover - a slice cannot be folded alone
+        raise RuntimeError("a sliced store holds 1/G of each layer: fold before slicing (synthetic(fold_norms=True))")
 
 
 class AllGatherPrefetcher(ShardPrefetcher):
@@ -321,7 +325,9 @@ def build_dp_sharded_runner(args, cfg, device, comm: Comm, tok, store: Optional[
     from .planner import make_plan
     device = torch.device(device)
     if store is None and getattr(args, "synthetic", None):
-        store = SlicedHostStore.synthetic(cfg, device, comm.rank, comm.world, pinned=device.type == "cuda")
+        from .. import knobs
+        store = SlicedHostStore.synthetic(cfg, device, comm.rank, comm.world, pinned=device.type == "cuda",
+                                          fold_norms=device.type == "cuda" and knobs.get_int("FLS_QKV_FOLD") == 1)
     elif store is None:
         src = FileLayerSource(cfg, args.model_path, direct=getattr(args, "o_direct", False))
         store = src if weight_cache == "stream" else SlicedHostStore.from_source(

@@ -71,8 +71,12 @@ def activation_bytes(cfg: ModelConfig, tokens: int, mlp_chunk: int, elem: int = 
     else:
         qc = balanced_step(tokens, qkv_chunk) if qkv_chunk else tokens
         attn = qc * H + tokens * Q
-    # MLP phase: [normed chunk | SwiGLU chunk]; MoE: k SwiGLU rows and k expert outputs per token
-    mlp = chunk * (H + (cfg.num_experts_per_tok * (cfg.expert_intermediate + H) if cfg.is_moe else I))
+    # MLP phase: [normed chunk | SwiGLU chunk] ([SwiGLU chunk | row statistics] fused); MoE: k
+    # SwiGLU rows and k expert outputs per token
+    if fused_norm and not cfg.is_moe:
+        mlp = chunk * (I + 2)
+    else:
+        mlp = chunk * (H + (cfg.num_experts_per_tok * (cfg.expert_intermediate + H) if cfg.is_moe else I))
     # Qwen2-MoE shared expert: its SwiGLU rows, output and gated output per chunk (allocator)
     mlp += chunk * (cfg.shared_expert_intermediate_size + 2 * H) if cfg.shared_expert_intermediate_size else 0
     scratch = max(attn, mlp)                             # one arena, two phases

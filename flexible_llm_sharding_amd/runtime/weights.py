@@ -51,13 +51,42 @@ class LayerSource:
 
 
 class HostStore(LayerSource):
-    """All packed layers resident in (pinned) host memory."""
+    """All packed layers resident in (pinned) host memory.
+
+    ``norms_folded``: every decoder layer's RMSNorm weights are already folded into the
+    projections that consume the normalised rows (:meth:`fold_norms`, done once on the GPU), so
+    the fused-norm engine streams them as they are — no per-load fold on the copy stream."""
+
+    norms_folded = False
 
     def __init__(self, cfg: ModelConfig, dtype=torch.float16, pinned: bool = True,
                  names: Optional[Sequence[str]] = None):
         self.cfg, self.dtype, self.pinned = cfg, dtype, pinned
         self.names = list(names) if names is not None else cfg.layer_names()
         self.buffers: Dict[str, torch.Tensor] = {}
+
+    def fold_norms(self, device) -> "HostStore":
+        """Fold the RMSNorm weights into the projections (models.llama.fold_layer_norms) for
+        every decoder layer, on ``device``: each layer goes H2D, is folded, and comes back.  Once
+        per store, in place; a full 70B store takes a few seconds at PCIe rate."""
+        from ..models.llama import fold_layer_norms
+        from ..ops import get_ops
+        if self.norms_folded:
+            return self
+        dev = torch.device(device)
+        ops = get_ops(dev)
+        dec = [n for n in self.names if layer_kind(n) == "decoder" and n in self.buffers]
+        if dec:
+            stage = torch.empty(max(self.nbytes(n) for n in dec), dtype=torch.uint8, device=dev)
+            for n in dec:
+                buf = self.buffers[n]
+                full = stage[:buf.numel()]
+                full.copy_(buf)
+                fold_layer_norms(ops, self.layout(n).views(full, self.dtype))
+                buf.copy_(full)
+            del stage
+        self.norms_folded = True
+        return self
 
     @property
     def total_bytes(self) -> int:
@@ -113,13 +142,16 @@ class HostStore(LayerSource):
     @classmethod
     def synthetic(cls, cfg: ModelConfig, device: torch.device, seed: int = 0, std: float = 0.02,
                   pinned: bool = True, names: Optional[Sequence[str]] = None,
-                  byte_range=None, progress=None) -> "HostStore":
+                  byte_range=None, progress=None, fold_norms: bool = False) -> "HostStore":
         """Random-init packed layers generated on ``device`` and copied to pinned host memory.
 
         ``byte_range=(r, G)`` keeps only slice r of G equal byte slices of every
         layer (data-parallel scatter-load).  Generation is deterministic in
         (seed, layer index, byte offset) so every rank's slices tile one model.
+        ``fold_norms``: the RMSNorm weights are folded into the projections on the device before
+        the copy (see :meth:`fold_norms`).
         """
+        from ..models.llama import fold_layer_norms
         from ..ops import get_ops
         st = cls(cfg, torch.float16, pinned, names)
         dev = torch.device(device)
@@ -132,6 +164,8 @@ class HostStore(LayerSource):
             lay = st.layout(n)
             full = stage[:lay.nbytes]
             ops.fill_layer_random(full, lay, seed=seed * 7919 + cfg.layer_names().index(n), std=std)
+            if fold_norms and lay.kind == "decoder":
+                fold_layer_norms(ops, lay.views(full, torch.float16))
             if byte_range is None:
                 buf = st.alloc(n)
                 buf.copy_(full, non_blocking=False)
@@ -147,6 +181,7 @@ class HostStore(LayerSource):
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
         del stage
+        st.norms_folded = bool(fold_norms)
         return st
 
 

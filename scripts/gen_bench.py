@@ -59,7 +59,7 @@ def main():
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     cfg = preset(a.model)
-    store = HostStore.synthetic(cfg, dev, seed=0)
+    store = HostStore.synthetic(cfg, dev, seed=0, fold_norms=True)
     tok_dir = f"/tmp/fls_gen_tok_{os.getpid()}"
     write_synthetic_tokenizer(tok_dir, cfg.vocab_size)
     tok = load_tokenizer(tok_dir)
