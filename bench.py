@@ -34,6 +34,7 @@ step: context, code objects, RCCL buffers and allocator slack included),
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import socket
@@ -438,6 +439,13 @@ def main(argv=None):
     # every score this rank produced must be a finite probability (guards the timed path's numerics)
     finite = all(np.isfinite(o.astype(np.float32)).all() for o in (outs or []) if o is not None)
     finite = comm.all_reduce_min(1.0 if finite else 0.0) >= 1.0
+    # digest of the last step's scores (this rank's, in prompt order): runs of one config under
+    # different plans (capped / uncapped, piece pool / slots) must print the same value
+    h = hashlib.sha1()
+    for o in (outs or []):
+        if o is not None:
+            h.update(np.ascontiguousarray(o).tobytes())
+    digests = comm.all_gather_object(h.hexdigest()[:16])
     # which ranks / devices took part (the process group the collectives actually ran on)
     import torch.distributed as dist
     pg_world = dist.get_world_size() if dist.is_initialized() else 1
@@ -453,7 +461,7 @@ def main(argv=None):
         "peak_device_used_gb": round(dev_used_peak / 1e9, 3), "device_mem_samples": n_samples,
         "peak_outside_allocator_gb": round(comm.all_reduce_max(outside_peak) / 1e9, 3),
         "host_pinned_gb": round(pinned / 1e9, 3), "host_peak_rss_gb": round(rss / 1e9, 3),
-        "scores_finite": finite,
+        "scores_finite": finite, "scores_sha1": digests,
         "world": world, "process_group_ranks": pg_world,
         "backend": comm.backend or ("none" if world == 1 else "?"), "rank_devices": devices,
         "config": {"model": a.model if a.num_layers is None else f"{a.model}-L{a.num_layers}",

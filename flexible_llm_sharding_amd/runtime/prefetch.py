@@ -506,8 +506,9 @@ class PiecePoolPrefetcher(ShardPrefetcher):
             if self._slot_free[s] is not None:
                 self.copy_stream.wait_event(self._slot_free[s])
             nbytes = self._copy_piece(slot, name, lo, hi)
-            if kind == "a" and self.on_load is not None:
-                self._loaded(name, self._piece_views(slot, name, True))
+            if self.on_load is not None and kind in "am" and self._is_dec(k):
+                # attention piece: ln1 into W_qkv; MLP piece (ln2 is its first tensor): ln2 into W_gate/up
+                self._loaded(name, self._piece_views(slot, name, kind == "a"))
             ev.record(self.copy_stream)
         self.load_seconds += time.perf_counter() - t0
         self.bytes_h2d += nbytes
