@@ -92,6 +92,19 @@ __device__ __forceinline__ unsigned pack_h2(float a, float b) {
   return __builtin_bit_cast(unsigned, __builtin_convertvector(float2_{a, b}, half2_));
 }
 
+// ds_read_b64_tr_b16 without the compiler's wait: its builtin makes the compiler drain every
+// outstanding LDS-DMA (vmcnt(0)) in front of the read.  The caller waits with lds_wait4 before
+// using the result (the wait's in/out operands order every use after it).
+__device__ __forceinline__ half4 lds_tr16_async(const char* p) {
+  half4 v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"((unsigned)(uintptr_t)(const LDS_AS char*)p) : "memory");
+  return v;
+}
+__device__ __forceinline__ void lds_wait4(half4& a, half4& b, half4& c, half4& d, half4& e, half4& f, half4& g,
+                                          half4& h) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e), "+v"(f), "+v"(g), "+v"(h)::"memory");
+}
+
 // SPL (split-KV, R2 only): blockIdx.z walks one of gridDim.z contiguous slices of the item's key
 // tiles and writes its unnormalised O, running max and row sum in fp32 to `part`
 // ([rows][splits][nh] x (HD + 2)); attn_split_combine merges the slices.  For grids with fewer
@@ -414,6 +427,251 @@ __global__ __launch_bounds__(HD) void attn_split_combine(const float* __restrict
   }
 }
 
+// Packed-GQA decode attention: range-2 items of a few query rows (generation steps with the prefix
+// + suffix K/V caches, q_block 8).  One block = one (item, KV group).  The group's hpg query heads
+// x q_len rows are packed into the N dimension of S^T = K.Q^T (packed row p = head hh * q_len +
+// row r), 16 per wave, 64 per pass of the block's 4 waves: each K/V tile is read from HBM once per
+// block and from LDS once per 16 packed rows, where the one-wave-per-head kernel reads it once
+// per head and runs 5 live rows padded to 16 (profiles/r4_gen/attn_pmc).
+//   * K/V tiles by LDS-DMA into a 3-deep ring, two tiles in flight under the math of the third;
+//     the source chunk order pre-applies the XOR swizzle of the ds_read_b128 K and
+//     ds_read_b64_tr_b16 V^T reads; one counted vmcnt + barrier per tile;
+//   * the softmax and O^T += V^T.P^T steps are attn_fwd's (deferred rescale, lane-local P^T).
+// SPL: blockIdx.z takes one of gridDim.z contiguous slices of the key tiles and writes fp32
+// partials in attn_split_combine's layout.
+template <int HD, bool SPL>
+__global__ __launch_bounds__(256, 1) void attn_decode(const half_t* __restrict__ qkv, half_t* __restrict__ out,
+                                                    const int* __restrict__ work, int nh, int nkv, int ld_qkv,
+                                                    int ld_out, float scale_log2, const half_t* __restrict__ kv0,
+                                                    int ld_kv0, const int* __restrict__ work2,
+                                                    const int* __restrict__ r2win, float* __restrict__ part) {
+  constexpr int NW = 4;                     // waves per block (16 packed rows each)
+  constexpr int NB = 3;                     // tile ring depth
+  constexpr int NS = HD / 32;               // k-steps of QK^T
+  constexpr int NU = HD / 16;               // 16-wide d subtiles of O
+  constexpr int CH = HD / 8;                // 16-byte chunks per K/V row
+  constexpr int TB = KT * HD * 2;           // one operand tile (16 KB at hd 128)
+  constexpr int RPI = 64 / CH;              // rows per 1 KB DMA instruction
+  constexpr int NI = TB / 1024 / NW;        // DMA instructions per wave per operand tile
+  static_assert(NI >= 1 && NI * NW * 1024 == TB, "tile / block mismatch");
+  __shared__ __attribute__((aligned(16))) char smem[NB * 2 * TB];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = blockIdx.y;
+  const int hpg = nh / nkv;
+  const int* wi = work + blockIdx.x * 8;
+  const int q_start = wi[0], q_len = wi[1], q_off = wi[2];
+  if (q_len <= 0) return;                   // padding item; block-uniform
+  const int r_start0 = wi[3], r_len0 = wi[4], r_causal0 = wi[5];
+  const int kend0 = r_len0 <= 0 ? 0 : (r_causal0 ? min(r_len0, q_off + q_len) : r_len0);
+  const int r_start2 = work2[blockIdx.x * 2];
+  const int r_len2 = max(work2[blockIdx.x * 2 + 1], 0);
+  const int n0 = (kend0 + KT - 1) / KT;
+  const int ntiles = n0 + (r_len2 + KT - 1) / KT;
+  int t_lo = 0, t_hi = ntiles;
+  if constexpr (SPL) {
+    const int per = (ntiles + (int)gridDim.z - 1) / (int)gridDim.z;
+    t_lo = min(ntiles, (int)blockIdx.z * per);
+    t_hi = min(ntiles, t_lo + per);
+  }
+
+  const int fr = lane & 15, grp = lane >> 4;
+  // LDS-DMA of tile t into ring slot b: this wave's chunks are w * NI + i of each operand; lane L
+  // of a chunk lands at row chunk * RPI + L / CH, physical 16-byte column L % CH, so it reads the
+  // logical column that the swizzled read expects there
+  const int drow = lane / CH, dpc = lane % CH;
+  auto issue = [&](int t, int b) {
+    const bool r2 = t >= n0;
+    const int k0 = (r2 ? t - n0 : t) * KT;
+    const int klen = r2 ? r_len2 : kend0;
+    const half_t* src = kv0 + (size_t)(r2 ? r_start2 : r_start0) * ld_kv0;
+    char* Kd = smem + b * 2 * TB;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int c = w * NI + i;
+      const int row = c * RPI + drow;
+      const half_t* rp = src + (size_t)min(k0 + row, klen - 1) * ld_kv0;
+      glds16(rp + g * HD + ((dpc ^ (row & Lds<HD>::KM)) << 3), Kd + c * 1024);
+      glds16(rp + (nkv + g) * HD + ((dpc ^ ((row & Lds<HD>::VM) << 1)) << 3), Kd + TB + c * 1024);
+    }
+  };
+  const int P = hpg * q_len;                // packed rows of the item
+
+  for (int p0 = 0; p0 < P; p0 += NW * 16) {
+    // this lane's packed row (rows past P repeat the last one: finite, never stored)
+    const int pw0 = p0 + w * 16;
+    const bool live = pw0 < P;              // wave-uniform: waves past the item's rows only load
+    const int p = min(pw0 + fr, P - 1);
+    const int hh = p / q_len, r = p - hh * q_len;
+    const int qr = q_start + r;
+    half8 qf[NS];
+    {
+      const half_t* qp = qkv + (size_t)qr * ld_qkv + (g * hpg + hh) * HD + grp * 8;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) qf[s] = *(const half8*)(qp + s * 32);
+    }
+    const int hi0 = r_causal0 ? min(kend0, q_off + r + 1) : kend0;     // range 0: keys [0, hi0)
+    const int lo2 = r2win[2 * qr] - r_start2;                          // range 2: keys [lo2, hi2)
+    const int hi2 = min(r2win[2 * qr + 1] - r_start2, r_len2);
+    // (lo2_, hi2_ below: the same values, pinned before the DMAs)
+    floatx4 o[NU];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) o[u] = floatx4{0.f, 0.f, 0.f, 0.f};
+    float m_run = -1e30f, l_run = 0.f;
+
+    // the loads above retire before the tile DMAs are counted (the operands pin their uses here,
+    // so the compiler's own wait for them does not land behind the DMAs and drain the ring)
+    int lo2_ = lo2, hi2_ = hi2;
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(lo2_), "+v"(hi2_)::"memory");
+#pragma unroll
+    for (int s = 0; s < NS; ++s) asm volatile("" : "+v"(qf[s]));
+    if (t_lo < t_hi) issue(t_lo, 0);
+    if (t_lo + 1 < t_hi) issue(t_lo + 1, 1);
+    for (int t = t_lo; t < t_hi; ++t) {
+      const int b = (t - t_lo) % NB;
+      if (t + 1 < t_hi) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NI) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // tile t landed (every wave's part; no wave still reads tile t-1, whose MFMAs consumed their
+      // operands): a raw barrier — __syncthreads' fence would wait for the DMAs still in flight
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (t + 2 < t_hi) issue(t + 2, (t + 2 - t_lo) % NB);
+      if (!live) continue;
+      const char* Ks = smem + b * 2 * TB;
+      const char* Vs = Ks + TB;
+      const bool r2 = t >= n0;
+      const int k0 = (r2 ? t - n0 : t) * KT;
+      // ---- S^T = K Q^T
+      floatx4 sc[4];
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) {
+        sc[tt] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+          sc[tt] = mfma16x16x32(*(const half8*)(Ks + Lds<HD>::k_off(tt * 16 + fr, s * 4 + grp)), qf[s], sc[tt]);
+      }
+      // ---- visibility: range 0 tiles inside every row's keys take the unmasked path
+      if (r2 || r_causal0 || k0 + KT > kend0) {
+        asm volatile("" ::: "memory");
+        const int lo_rel = (r2 ? lo2_ : 0) - k0 - grp * 4;
+        const int hi_rel = (r2 ? hi2_ : hi0) - k0 - grp * 4;             // exclusive
+#pragma unroll
+        for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (tt * 16 + i >= hi_rel || tt * 16 + i < lo_rel) sc[tt][i] = -INFINITY;
+      }
+      // ---- online softmax (deferred rescale as in attn_fwd)
+      float ma = vmax3(sc[0][0], sc[0][1], sc[0][2]);
+      float mb = vmax3(sc[2][0], sc[2][1], sc[2][2]);
+      ma = vmax3(ma, sc[0][3], sc[1][0]);
+      mb = vmax3(mb, sc[2][3], sc[3][0]);
+      ma = vmax3(ma, sc[1][1], sc[1][2]);
+      mb = vmax3(mb, sc[3][1], sc[3][2]);
+      const float mx = max_xor16_32(vmax3(ma, sc[1][3], vmax(mb, sc[3][3])));
+      if (!__all((mx - m_run) * scale_log2 <= DEFER_LOG2)) {
+        const float m_new = fmaxf(m_run, mx);
+        const float alpha = fast_exp2((m_run - m_new) * scale_log2);
+        l_run *= alpha;
+#pragma unroll
+        for (int u = 0; u < NU; ++u) o[u] *= alpha;
+        m_run = m_new;
+      }
+      const float mc = m_run * scale_log2;
+      float psum = 0.f;
+      unsigned pw[8];
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) {
+        float pr[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          pr[i] = fast_exp2(__builtin_fmaf(sc[tt][i], scale_log2, -mc));
+          psum += pr[i];
+        }
+        pw[tt * 2] = pack_h2(pr[0], pr[1]);
+        pw[tt * 2 + 1] = pack_h2(pr[2], pr[3]);
+      }
+      l_run += psum;
+      // ---- O^T += V^T P^T; P^T element (tt & 1) * 4 + i of k-step tt >> 1 = key 16 tt + 4 grp + i.
+      // V^T by inline-asm transposed reads in groups of 4 subtiles (reads of the next group in
+      // flight under the MFMAs of this one): the builtin's reads make the compiler drain every
+      // outstanding LDS-DMA first (vmcnt(0)), i.e. the whole tile ring
+      const int q4 = (lane & 15) >> 2, p4 = lane & 3;
+      constexpr int UG = 4;                 // subtiles per read group (NU = 4 or 8)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const half8 pf = __builtin_bit_cast(half8, u32x4{pw[ks * 4], pw[ks * 4 + 1], pw[ks * 4 + 2], pw[ks * 4 + 3]});
+        const int row_a = ks * 32 + grp * 4 + q4;
+        half4 va[NU], vb[NU];
+        auto read_group = [&](int u0) {
+#pragma unroll
+          for (int u = u0; u < u0 + UG; ++u) {
+            const int ch = u * 2 + (p4 >> 1);
+            va[u] = lds_tr16_async(Vs + Lds<HD>::v_off(row_a, ch) + (p4 & 1) * 8);
+            vb[u] = lds_tr16_async(Vs + Lds<HD>::v_off(row_a + 16, ch) + (p4 & 1) * 8);
+          }
+        };
+        read_group(0);
+#pragma unroll
+        for (int u0 = 0; u0 < NU; u0 += UG) {
+          lds_wait4(va[u0], va[u0 + 1], va[u0 + 2], va[u0 + 3], vb[u0], vb[u0 + 1], vb[u0 + 2], vb[u0 + 3]);
+          if (u0 + UG < NU) read_group(u0 + UG);
+#pragma unroll
+          for (int u = u0; u < u0 + UG; ++u) {
+            const half8 vf = {va[u][0], va[u][1], va[u][2], va[u][3], vb[u][0], vb[u][1], vb[u][2], vb[u][3]};
+            o[u] = mfma16x16x32(vf, pf, o[u]);
+          }
+        }
+      }
+    }
+    // ---- normalise and store this wave's rows (split: the slice's fp32 partials)
+    if (live) {
+      float l = l_run;
+      l += __shfl_xor(l, 16, 64);
+      l += __shfl_xor(l, 32, 64);
+      if (pw0 + fr < P) {
+        const int h = g * hpg + hh;
+        if constexpr (SPL) {
+          float* pp = part + ((size_t)(qr * (int)gridDim.z + (int)blockIdx.z) * nh + h) * (HD + 2);
+#pragma unroll
+          for (int u = 0; u < NU; ++u) *(floatx4*)(pp + u * 16 + grp * 4) = o[u];
+          if (grp == 0) *(float2_*)(pp + HD) = float2_{m_run * scale_log2, l};
+        } else {
+          const float inv = 1.f / l;
+          half_t* op = out + (size_t)qr * ld_out + h * HD + grp * 4;
+#pragma unroll
+          for (int u = 0; u < NU; ++u) {
+            half4 v;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = (half_t)(o[u][i] * inv);
+            *(half4*)(op + u * 16) = v;
+          }
+        }
+      }
+    }
+    __syncthreads();                        // the ring is the next pass's
+  }
+}
+
+template <int HD>
+int launch_decode(dim3 grid, int ns, hipStream_t st, const half_t* qkv, half_t* out, const int* work, int nh, int nkv,
+                  int ld_qkv, int ld_out, float scale_log2, const half_t* kv0, int ld_kv0, const int* work2,
+                  const int* r2win, float* part) {
+  if (ns > 1) {
+    hipLaunchKernelGGL((attn_decode<HD, true>), dim3(grid.x, grid.y, ns), dim3(256), 0, st, qkv, out, work, nh, nkv,
+                       ld_qkv, ld_out, scale_log2, kv0, ld_kv0, work2, r2win, part);
+    FLS_CHECK_LAUNCH();
+    hipLaunchKernelGGL((attn_split_combine<HD>), dim3(grid.x, nh), dim3(HD), 0, st, part, out, work, nh, ld_out, ns);
+  } else {
+    hipLaunchKernelGGL((attn_decode<HD, false>), grid, dim3(256), 0, st, qkv, out, work, nh, nkv, ld_qkv, ld_out,
+                       scale_log2, kv0, ld_kv0, work2, r2win, nullptr);
+  }
+  FLS_CHECK_LAUNCH();
+  return 0;
+}
+
 template <int HD, int WPH, bool R2>
 int launch(int hpb, dim3 grid, hipStream_t st, const half_t* qkv, half_t* out, const int* work, const int* seg_lo,
            int nh, int nkv, int ld_qkv, int ld_out, float scale_log2, const half_t* kv0, int ld_kv0,
@@ -490,11 +748,34 @@ int dispatch(const void* qkv, void* out, const int* work, int n_items, int n_q_h
              fls_stream_t s) {
   if (n_q_heads % n_kv_heads) return -2;
   if (head_dim != 64 && head_dim != 96 && head_dim != 128) return -3;
-  // q_block 32 (one wave per head): range-2 items of at most 32 rows (generation steps)
-  if (q_block != 64 && q_block != 128 && !(R2 && q_block == 32)) return -5;
+  // q_block 32 (one wave per head): range-2 items of at most 32 rows (generation steps);
+  // q_block 8: range-2 items of at most 8 rows, packed-GQA decode kernel
+  if (q_block != 64 && q_block != 128 && !(R2 && (q_block == 32 || q_block == 8))) return -5;
   const float scale_log2 = scale * 1.4426950408889634f;
   auto st = (hipStream_t)s;
   const int group = n_q_heads / n_kv_heads;
+  if constexpr (R2) {
+    if (q_block == 8 && head_dim != 96) {
+      // one block per (item, KV group), 4 waves; split the key tiles over blocks only when the
+      // grid leaves CUs idle (one block per CU at this kernel's register use)
+      const dim3 grid(n_items, n_kv_heads);
+      const long blocks = (long)grid.x * grid.y;
+      int ns = 1;
+      if (ws && n_rows > 0) {
+        ns = g_split > 0 ? g_split : (blocks >= 192 ? 1 : (int)min(8L, (256 + blocks - 1) / blocks));
+        const unsigned long long per = (unsigned long long)n_rows * n_q_heads * (head_dim + 2) * 4ull;
+        while (ns > 1 && per * ns > ws_bytes) --ns;
+      }
+      auto q = (const half_t*)qkv;
+      auto o = (half_t*)out;
+      auto k0 = (const half_t*)kv0;
+      return head_dim == 128 ? launch_decode<128>(grid, ns, st, q, o, work, n_q_heads, n_kv_heads, ld_qkv, ld_out,
+                                                  scale_log2, k0, ld_kv0, work2, r2win, (float*)ws)
+                             : launch_decode<64>(grid, ns, st, q, o, work, n_q_heads, n_kv_heads, ld_qkv, ld_out,
+                                                 scale_log2, k0, ld_kv0, work2, r2win, (float*)ws);
+    }
+  }
+  if (q_block == 8) q_block = 32;           // hd 96 (or the non-range-2 kernel): the per-head layout
   // heads of one KV group per block share every staged K/V tile: up to 4 (64-row items) or 2
   // (128-row items, 4 waves per head) as the group allows, else 1 (multi-head attention)
   // (32-row items: up to 8, a whole 70B KV group, so every prompt's prefix K/V is read once per

@@ -63,7 +63,7 @@ class Piece(ctypes.Structure):
                 ("kind", ctypes.c_int32), ("pad", ctypes.c_int32)]
 
 
-KERNELS_ABI = 21   # bumped whenever a C signature in csrc/include/fls.h changes
+KERNELS_ABI = 22   # bumped whenever a C signature in csrc/include/fls.h (or an accepted argument) changes
 
 
 def _load_kernels(path: str = _KERNELS):

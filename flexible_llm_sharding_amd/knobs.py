@@ -37,7 +37,8 @@ KNOBS: Dict[str, Tuple[str, str]] = {
     "FLS_ATTN_SPLIT": ("0", "split-KV slices of the range-2 attention kernel: 0 by grid size, 1 off, n"),
     "FLS_CHUNK_ALIGN": ("3072", "row multiple of the QKV / MLP chunks (3072 = 8 v11 tiles)"),
     "FLS_SPECULATIVE_PREFETCH": ("", "0 / 1: force the next call's first-shard prefetch off / on"),
-    "FLS_R2_QBLOCK": ("32", "query rows per range-2 (generation-step) attention item: 32 or 64"),
+    "FLS_R2_QBLOCK": ("8", "range-2 (generation-step) attention: 8 = packed-GQA decode kernel for items of <= 8 "
+                           "rows, 32 = one wave per query head, 64 = the batch's q_block"),
     "FLS_DECODE_GRAPHS": ("1", "0: no HIP-graph replay of decode-like calls (generation steps with the "
                                "prefix + suffix K/V caches and every weight in HBM)"),
     "FLS_QKV_FOLD": ("1", "0: RMSNorm + QKV as two kernels instead of the row-scaled GEMM on the "

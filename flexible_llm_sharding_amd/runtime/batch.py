@@ -96,13 +96,17 @@ class PackedBatch:
 
     @property
     def r2_q_block(self) -> int:
-        """q_block for the range-2 (suffix K/V reuse) attention: 32 when every work item holds at
-        most 32 rows (a generation step: one new row per suffix), so the kernel runs one wave per
-        query head and a whole KV group per block (each prompt's prefix K/V read once per layer);
-        the batch's own q_block otherwise."""
-        if R2_Q_BLOCK != 32 or self.work2 is None or self.work.shape[0] == 0 or int(self.work[:, 1].max()) > 32:
+        """q_block for the range-2 (suffix K/V reuse) attention: 8 when every work item holds at
+        most 8 rows (a generation step: one new row per suffix) — the packed-GQA decode kernel, a
+        KV group's heads x rows in one MFMA column block, each K/V tile read once per group; 32 when
+        every item holds at most 32 rows (one wave per query head, a whole KV group per block); the
+        batch's own q_block otherwise."""
+        if self.work2 is None or self.work.shape[0] == 0 or R2_Q_BLOCK not in (8, 32):
             return self.q_block
-        return 32
+        rows = int(self.work[:, 1].max())
+        if R2_Q_BLOCK == 8 and rows <= 8:
+            return 8
+        return 32 if rows <= 32 else self.q_block
 
     def attn_groups(self, max_rows: int) -> List[dict]:
         """Prompt-aligned row groups of <= ``max_rows`` packed rows (a larger prompt is a group of

@@ -30,6 +30,9 @@ def main():
     ap.add_argument("--json", default=None)
     ap.add_argument("--embeds-per-pass", type=int, default=1,
                     help="embedding launches per pass (one per micro-batch)")
+    ap.add_argument("--all-kernels", action="store_true",
+                    help="list every distinct kernel of the passes, classified: framework (csrc/kernels), "
+                         "HIP runtime copies, other (torch eager, libraries)")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     rows = c.execute("select name, start, end from kernels order by start").fetchall()
@@ -58,6 +61,19 @@ def main():
         tot = sum(p["kernels_ms"].values())
         for k, v in list(p["kernels_ms"].items())[:10]:
             print(f"    {k:40s} {v:9.1f} ms  {100 * v / tot:5.1f}%")
+    if a.all_kernels and starts:
+        seen = defaultdict(lambda: [0, 0.0])
+        for n, s_, e in rows[starts[0]:]:
+            seen[n][0] += 1
+            seen[n][1] += (e - s_) / 1e6
+        cls = {"framework": [], "runtime copy": [], "other": []}
+        for n, (cnt, ms) in sorted(seen.items(), key=lambda kv: -kv[1][1]):
+            k = ("framework" if "_GLOBAL__N_1" in n else "runtime copy" if n.startswith("__amd_rocclr") else "other")
+            cls[k].append((n, cnt, ms))
+        for k, lst in cls.items():
+            print(f"{k} kernels: {len(lst)}")
+            for n, cnt, ms in lst:
+                print(f"    {short(n) if k == 'framework' else n[:100]:60s} x{cnt:<7d} {ms:9.1f} ms")
     if a.json:
         with open(a.json, "w") as f:
             json.dump(passes, f, indent=1)

@@ -736,8 +736,11 @@ def test_pack_suffix_reuse_work_items():
     assert visible_keys(b.work, b.seg_lo, 1, b.work2, b.r2win) == [(0, 0, 9), (2, 20, 23)]
     assert visible_keys(b.work, b.seg_lo, 3, b.work2, b.r2win) == [(0, 0, 9), (2, 40, 41)]
     assert b.work_last[:, :2].tolist() == [[1, 1], [4, 1]] and b.work2_last.tolist() == [[20, 4], [40, 3]]
-    # at most 32 rows per item: the range-2 kernel runs one wave per head (q_block 32)
-    assert b.r2_q_block == 32
+    # at most 8 rows per item: the packed-GQA decode kernel (q_block 8)
+    assert b.r2_q_block == 8
+    mid = TokenizedPrompt(prefix=list(range(10)), suffixes=[list(range(20))], padded_len=20, eos_index=[19])
+    b1 = pack_prompts([mid], [0], prefix_offsets=[0], kv_cached=True, suffix_rows=[[20]], suffix_keep=[[2]])
+    assert int(b1.work[:, 1].max()) == 18 and b1.r2_q_block == 32      # one wave per head
     long = TokenizedPrompt(prefix=list(range(10)), suffixes=[list(range(40))], padded_len=40, eos_index=[39])
     b2 = pack_prompts([long], [0], prefix_offsets=[0], kv_cached=True, suffix_rows=[[20]], suffix_keep=[[2]])
     assert int(b2.work[:, 1].max()) == 38 and b2.r2_q_block == b2.q_block

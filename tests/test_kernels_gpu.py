@@ -444,7 +444,7 @@ def test_qkv_norm_rope(ops, ref, nq, nk, hd):
         assert rel_err(y[:, v0:], (x.float() @ w.float().t())[:, v0:]) < 2e-3
 
 
-@pytest.mark.parametrize("q_block", [64, 32])
+@pytest.mark.parametrize("q_block", [64, 32, 8])
 @pytest.mark.parametrize("split", [0, 1, 3, 8])
 @pytest.mark.parametrize("nh,nkv,hd", [(8, 1, 128), (16, 2, 128), (8, 2, 64), (4, 4, 64), (4, 4, 96)])
 def test_attention_suffix_rows_from_cache(ops, ref, nh, nkv, hd, split, q_block):
@@ -452,7 +452,9 @@ def test_attention_suffix_rows_from_cache(ops, ref, nh, nkv, hd, split, q_block)
     prefix as range 0) and only the new rows computed == the full packed pass on those rows.
     split: key-tile slices of the split-KV kernel (0 = by grid size, which splits this small grid;
     1 = one block per item and head; hd 96 never splits).  q_block 32: one wave per head, 4 or 8
-    heads of a KV group per block (groups of < 4 heads fall back to the 2-wave kernel)."""
+    heads of a KV group per block (groups of < 4 heads fall back to the 2-wave kernel).  q_block 8:
+    the packed-GQA decode kernel (a KV group's heads x rows in 64-row passes: these items hold up
+    to 13 new rows, so the 8-head groups take two passes; hd 96 falls back)."""
     old = ops.k.fls_attention_set_split(split)
     try:
         _suffix_rows_from_cache(ops, ref, nh, nkv, hd, q_block=q_block)
@@ -467,7 +469,7 @@ def test_attention_decode_split_matches_unsplit(ops, ref):
     prompts = [(600, [41] * 5)] * 12
     keep = [[40] * 5] * 12
     ys = []
-    for split, qb in ((1, 64), (0, 64), (1, 32), (0, 32)):
+    for split, qb in ((1, 64), (0, 64), (1, 32), (0, 32), (1, 8), (0, 8)):
         old = ops.k.fls_attention_set_split(split)
         try:
             ys.append(_suffix_rows_from_cache(ops, ref, 64, 8, 128, prompts, keep, q_block=qb))
@@ -477,6 +479,9 @@ def test_attention_decode_split_matches_unsplit(ops, ref):
     # one wave per head, 8 heads per block: the same per-row math as the 2-wave kernel, unsplit
     assert torch.equal(ys[2], ys[0])
     assert rel_err(ys[3], ys[0]) < 2e-3
+    # packed-GQA decode kernel (8 heads x 5 rows in one 64-row pass), unsplit and split
+    assert rel_err(ys[4], ys[0]) < 2e-3
+    assert rel_err(ys[5], ys[0]) < 2e-3
 
 
 def _suffix_rows_from_cache(ops, ref, nh, nkv, hd, prompts=None, keep=None, q_block=64):
@@ -516,9 +521,8 @@ def _suffix_rows_from_cache(ops, ref, nh, nkv, hd, prompts=None, keep=None, q_bl
     sel = torch.tensor(sel)
     qkv_new = qkv[sel].contiguous()
     m = reuse.device_tensors(DEV)
-    if q_block == 32:
-        assert reuse.r2_q_block == (32 if int(reuse.work[:, 1].max()) <= 32 else 64)
-        q_block = reuse.r2_q_block
+    if q_block == 32:                                     # one wave per head: items of <= 32 rows
+        q_block = 32 if int(reuse.work[:, 1].max()) <= 32 else 64
     y = ops.attention(qkv_new.to(DEV), m["work"], nh, nkv, hd, kv0=cache.to(DEV), seg_lo=m["seg_lo"],
                       work2=m["work2"], r2win=m["r2win"], q_block=q_block)
     want = ref.attention(qkv.float(), full.segments, nh, nkv, hd)[sel]
