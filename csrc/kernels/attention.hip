@@ -433,20 +433,20 @@ __global__ __launch_bounds__(HD) void attn_split_combine(const float* __restrict
 // row r), 16 per wave, 64 per pass of the block's 4 waves: each K/V tile is read from HBM once per
 // block and from LDS once per 16 packed rows, where the one-wave-per-head kernel reads it once
 // per head and runs 5 live rows padded to 16 (profiles/r4_gen/attn_pmc).
-//   * K/V tiles by LDS-DMA into a 3-deep ring, two tiles in flight under the math of the third;
+//   * K/V tiles by LDS-DMA into an NB-deep ring, NB - 1 tiles in flight under the math of one;
 //     the source chunk order pre-applies the XOR swizzle of the ds_read_b128 K and
 //     ds_read_b64_tr_b16 V^T reads; one counted vmcnt + barrier per tile;
 //   * the softmax and O^T += V^T.P^T steps are attn_fwd's (deferred rescale, lane-local P^T).
 // SPL: blockIdx.z takes one of gridDim.z contiguous slices of the key tiles and writes fp32
 // partials in attn_split_combine's layout.
-template <int HD, bool SPL>
+template <int HD, bool SPL, int NB>
 __global__ __launch_bounds__(256, 1) void attn_decode(const half_t* __restrict__ qkv, half_t* __restrict__ out,
                                                     const int* __restrict__ work, int nh, int nkv, int ld_qkv,
                                                     int ld_out, float scale_log2, const half_t* __restrict__ kv0,
                                                     int ld_kv0, const int* __restrict__ work2,
                                                     const int* __restrict__ r2win, float* __restrict__ part) {
   constexpr int NW = 4;                     // waves per block (16 packed rows each)
-  constexpr int NB = 3;                     // tile ring depth
+  // NB: tile ring depth (NB - 1 tiles in flight under the math of one)
   constexpr int NS = HD / 32;               // k-steps of QK^T
   constexpr int NU = HD / 16;               // 16-wide d subtiles of O
   constexpr int CH = HD / 8;                // 16-byte chunks per K/V row
@@ -527,17 +527,21 @@ __global__ __launch_bounds__(256, 1) void attn_decode(const half_t* __restrict__
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(lo2_), "+v"(hi2_)::"memory");
 #pragma unroll
     for (int s = 0; s < NS; ++s) asm volatile("" : "+v"(qf[s]));
-    if (t_lo < t_hi) issue(t_lo, 0);
-    if (t_lo + 1 < t_hi) issue(t_lo + 1, 1);
+#pragma unroll
+    for (int i = 0; i < NB - 1; ++i)
+      if (t_lo + i < t_hi) issue(t_lo + i, i);
     for (int t = t_lo; t < t_hi; ++t) {
       const int b = (t - t_lo) % NB;
-      if (t + 1 < t_hi) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NI) : "memory");
+      // tile t landed: the tiles issued after it may stay in flight
+      const int after = min(NB - 2, t_hi - 1 - t);
+      if (after >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * NI) : "memory");
+      else if (after == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NI) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       // tile t landed (every wave's part; no wave still reads tile t-1, whose MFMAs consumed their
       // operands): a raw barrier — __syncthreads' fence would wait for the DMAs still in flight
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      if (t + 2 < t_hi) issue(t + 2, (t + 2 - t_lo) % NB);
+      if (t + NB - 1 < t_hi) issue(t + NB - 1, (t + NB - 1 - t_lo) % NB);
       if (!live) continue;
       const char* Ks = smem + b * 2 * TB;
       const char* Vs = Ks + TB;
@@ -655,18 +659,22 @@ __global__ __launch_bounds__(256, 1) void attn_decode(const half_t* __restrict__
   }
 }
 
+// tile ring depth 3 (two tiles in flight); 4 measured slower at the 70B decode shape:
+// 46.3 vs 42.7 us per launch, HBM-resident caches (profiles/r5_gen/attn_decode_ring.log)
+constexpr int DECODE_RING = 3;
+
 template <int HD>
 int launch_decode(dim3 grid, int ns, hipStream_t st, const half_t* qkv, half_t* out, const int* work, int nh, int nkv,
                   int ld_qkv, int ld_out, float scale_log2, const half_t* kv0, int ld_kv0, const int* work2,
                   const int* r2win, float* part) {
   if (ns > 1) {
-    hipLaunchKernelGGL((attn_decode<HD, true>), dim3(grid.x, grid.y, ns), dim3(256), 0, st, qkv, out, work, nh, nkv,
-                       ld_qkv, ld_out, scale_log2, kv0, ld_kv0, work2, r2win, part);
+    hipLaunchKernelGGL((attn_decode<HD, true, DECODE_RING>), dim3(grid.x, grid.y, ns), dim3(256), 0, st, qkv, out,
+                       work, nh, nkv, ld_qkv, ld_out, scale_log2, kv0, ld_kv0, work2, r2win, part);
     FLS_CHECK_LAUNCH();
     hipLaunchKernelGGL((attn_split_combine<HD>), dim3(grid.x, nh), dim3(HD), 0, st, part, out, work, nh, ld_out, ns);
   } else {
-    hipLaunchKernelGGL((attn_decode<HD, false>), grid, dim3(256), 0, st, qkv, out, work, nh, nkv, ld_qkv, ld_out,
-                       scale_log2, kv0, ld_kv0, work2, r2win, nullptr);
+    hipLaunchKernelGGL((attn_decode<HD, false, DECODE_RING>), grid, dim3(256), 0, st, qkv, out, work, nh, nkv, ld_qkv,
+                       ld_out, scale_log2, kv0, ld_kv0, work2, r2win, nullptr);
   }
   FLS_CHECK_LAUNCH();
   return 0;

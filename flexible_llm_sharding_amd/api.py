@@ -261,8 +261,13 @@ def generation_loop(args, runner, comm: Comm, tok, original_prompts: Sequence, s
     # host-side profile of chosen steps (FLS_PROFILE_GEN_STEPS="2,3" -> cProfile stats in
     # FLS_PROFILE_OUT.<step>): where a generation step's host time goes
     prof_steps = {int(s) for s in knobs.get("FLS_PROFILE_GEN_STEPS").split(",") if s.strip()}
+    # one runner call per step on one rank: each decode-graphed step may enqueue the next one behind
+    # itself (ShardedRunner._launch_spec) while the host decodes and re-tokenizes
+    spec = comm.world == 1 and len(batch_ranges(len(input_prompts), args.num_batch)) == 1
     for i_new in range(args.num_gen_token):
         t_step = time.perf_counter()
+        if hasattr(runner, "spec_steps"):
+            runner.spec_steps = (args.num_gen_token - 1 - i_new) if spec else 0
         prof = None
         if i_new in prof_steps:
             import cProfile

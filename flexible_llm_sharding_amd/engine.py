@@ -235,6 +235,7 @@ class ShardedRunner:
                                and not resume_dir)
         self._graphs = None
         self._decode_graphs = None
+        self._spec: Optional[dict] = None     # an enqueued speculative generation step
         self.last_tokens: List[Optional[np.ndarray]] = []   # last call's greedy token per suffix
         if self.cuda and not self.hip_graphs:
             from .models.llama import Workspace
@@ -375,6 +376,11 @@ class ShardedRunner:
 
     def run_tokenized(self, tps: Sequence[TokenizedPrompt]) -> List[Optional[np.ndarray]]:
         t_start = time.perf_counter()
+        spec, self._spec = self._spec, None
+        if spec is not None:
+            if self._spec_matches(spec, tps):
+                return self._finish_spec(spec, tps, t_start)
+            self._drop_spec(spec)
         n = len(tps)
         sw = self.cfg.sliding_window
         if sw:
@@ -938,30 +944,20 @@ class ShardedRunner:
             graphs = self._graphs
             run = graphs.run
         outputs: List[Optional[np.ndarray]] = [None] * len(tps)
-        flops = 0.0
-        pending = []
-        store = self._get_store()
         ws, self.ctx.ws = self.ctx.ws, None           # the graph's own memory pool, not the arena
         try:
-            for batch in batches:
-                probs = run(batch)
-                am = self.ops.argmax_rows(probs)
-                nbytes = probs.numel() * probs.element_size()
-                pool_buf = store.host_buffer(nbytes + 4 * probs.shape[0])
-                host = pool_buf[:nbytes].view(probs.dtype).view(probs.shape)
-                host_am = pool_buf[nbytes:nbytes + 4 * probs.shape[0]].view(torch.int32)
-                host.copy_(probs, non_blocking=True)     # same stream: ordered before the next replay
-                host_am.copy_(am, non_blocking=True)
-                pending.append((batch, host, pool_buf, host_am))
-                flops += sum(layer_flops(self.cfg, batch, self._pruned(n)) for n in self.names
-                             if layer_kind(n) == "decoder")
+            pending, ams, flops = self._enqueue_graphed(batches, lambda b, i: run(b))
+            done = torch.cuda.Event()
+            done.record(torch.cuda.current_stream(self.dev))
+            if entry is not None and self.spec_steps > 0:
+                # the next generation step, enqueued behind this one (see _launch_spec)
+                self._spec = self._launch_spec(tps, entry, batches, ams)
         finally:
             self.ctx.ws = ws
-        torch.cuda.synchronize(self.dev)
-        self.last_tokens = [None] * len(tps)
-        for batch, host, pool_buf, host_am in pending:
-            self._collect(batch, host.numpy(), host_am, outputs)
-            store.recycle_host(pool_buf)
+        done.synchronize()                            # this step's scores (not the speculative one)
+        self._collect_graphed(pending, outputs, len(tps))
+        if self._spec is not None:
+            self._spec["prev_tokens"] = list(self.last_tokens)
         wall = time.perf_counter() - t_start
         self.stats = {
             "wall_s": wall, "compute_launch_s": wall,
@@ -971,8 +967,140 @@ class ShardedRunner:
             "weight_wait_s": pf.take_wait_seconds(), "weight_h2d_bytes": 0.0,
             "act_d2h_bytes": 0.0, "act_h2d_bytes": 0.0, "resumed_from_shard": 0.0,
             "graph_captures": float(graphs.captures), "graph_replays": float(graphs.replays),
+            "speculative": 0.0,
         }
         return outputs
+
+    def _enqueue_graphed(self, batches, run):
+        """Replay every micro-batch (``run(batch, index) -> probs``), its row argmax and the D2H
+        of both into pooled pinned buffers, all on the current stream -> (pending, argmax tensors,
+        decoder FLOPs)."""
+        store = self._get_store()
+        pending, ams, flops = [], [], 0.0
+        for i, batch in enumerate(batches):
+            probs = run(batch, i)
+            am = self.ops.argmax_rows(probs)
+            nbytes = probs.numel() * probs.element_size()
+            pool_buf = store.host_buffer(nbytes + 4 * probs.shape[0])
+            host = pool_buf[:nbytes].view(probs.dtype).view(probs.shape)
+            host_am = pool_buf[nbytes:nbytes + 4 * probs.shape[0]].view(torch.int32)
+            host.copy_(probs, non_blocking=True)     # same stream: ordered before the next replay
+            host_am.copy_(am, non_blocking=True)
+            pending.append((batch, host, pool_buf, host_am))
+            ams.append(am)
+            flops += sum(layer_flops(self.cfg, batch, self._pruned(n)) for n in self.names if layer_kind(n) == "decoder")
+        return pending, ams, flops
+
+    def _collect_graphed(self, pending, outputs, n_prompts: int) -> None:
+        store = self._get_store()
+        self.last_tokens = [None] * n_prompts
+        for batch, host, pool_buf, host_am in pending:
+            self._collect(batch, host.numpy(), host_am, outputs)
+            store.recycle_host(pool_buf)
+
+    # ------------------------------------------------- speculative generation steps
+    # A greedy generation step re-tokenizes ``suffix + decode(tokens)`` (main.py:86-88), which
+    # almost always gives the last step's ids plus the new token.  With ``spec_steps`` > 0 (set by
+    # api.generation_loop: steps still to come) a decode-graphed call enqueues the NEXT step right
+    # behind itself on that assumption, its new-token ids copied on the device from this step's
+    # argmax, so the GPU computes it while the host collects, decodes, re-tokenizes and packs.  The
+    # next call compares its real tokenization with the assumption: equal -> that step was computed
+    # from exactly the inputs the call would pack (same graph, same metadata: bitwise the same
+    # scores) and only its copies are waited for; different -> it is dropped and the call runs
+    # normally (the suffix regions' committed ids are the last step's, so the normal step
+    # recomputes every row from the first differing token, overwriting the speculative rows).
+    spec_steps = 0
+
+    def _launch_spec(self, tps, entry, batches, ams) -> Optional[dict]:
+        if not (knobs.get_int("FLS_SPEC_DECODE") and self._decode_graphs is not None
+                and all(b.work2 is not None and b.num_tokens == b.n_scored for b in batches)):
+            return None
+        try:
+            spec_tps = [TokenizedPrompt(list(tp.prefix), [list(s) + [0] for s in tp.suffixes], tp.padded_len + 1,
+                                        [len(s) for s in tp.suffixes]) for tp in tps]
+            groups = split_microbatches(spec_tps, self.micro_budget(spec_tps, True), suffix_only=True)
+            if groups != [list(b.prompt_ids) for b in batches]:
+                return None
+            rows, keep = [], []
+            for j, tp in enumerate(spec_tps):
+                if j >= len(entry.sfx_rows) or len(tp.suffixes) != len(entry.sfx_rows[j]):
+                    return None
+                if any(len(s) > cap for s, cap in zip(tp.suffixes, entry.sfx_caps[j])):
+                    return None                       # a suffix outgrew its cache region
+                rows.append(list(entry.sfx_rows[j]))
+                keep.append([len(s) - 1 for s in tp.suffixes])
+            sb = [pack_prompts([spec_tps[i] for i in g], g, self.prefix_attention,
+                               prefix_offsets=[entry.offsets[i] for i in g], kv_cached=True, q_block=self.q_block,
+                               suffix_rows=[rows[i] for i in g], suffix_keep=[keep[i] for i in g]) for g in groups]
+            if not self._decode_graphable(sb, True) or any(x.num_tokens != b.n_scored for x, b in zip(sb, batches)):
+                return None
+            graphs = self._decode_graphs
+            pe, self.ctx.prefix_entry = self.ctx.prefix_entry, entry     # (a capture's eager forward reads it)
+            try:
+                pending, ams2, flops = self._enqueue_graphed(sb, lambda b, i: graphs.run(b, entry, ids_dev=ams[i]))
+            finally:
+                self.ctx.prefix_entry = pe
+            done = torch.cuda.Event()
+            done.record(torch.cuda.current_stream(self.dev))
+            return {"tps": spec_tps, "entry": entry, "rows": rows, "batches": sb, "pending": pending, "ams": ams2,
+                    "flops": flops, "done": done, "prev_tokens": None, "t0": time.perf_counter()}
+        except Exception:
+            return None
+
+    def _spec_matches(self, spec: dict, tps) -> bool:
+        """Is ``tps`` (this call's tokenization) what the speculative step assumed: the same
+        prefixes, every suffix the last step's ids plus that step's greedy token?"""
+        prev = spec["prev_tokens"]
+        exp = spec["tps"]
+        if prev is None or len(tps) != len(exp) or any(t is None for t in prev):
+            return False
+        for j, (tp, e) in enumerate(zip(tps, exp)):
+            if tp.prefix != e.prefix or len(tp.suffixes) != len(e.suffixes):
+                return False
+            for si, (s, es) in enumerate(zip(tp.suffixes, e.suffixes)):
+                if len(s) != len(es) or s[:-1] != es[:-1] or s[-1] != int(prev[j][si, 0]):
+                    return False
+        return True
+
+    def _finish_spec(self, spec: dict, tps, t_start: float) -> List[Optional[np.ndarray]]:
+        entry = spec["entry"]
+        if self.spec_steps > 0:
+            ws, self.ctx.ws = self.ctx.ws, None
+            try:
+                self._spec = self._launch_spec(tps, entry, spec["batches"], spec["ams"])
+            finally:
+                self.ctx.ws = ws
+        spec["done"].synchronize()
+        outputs: List[Optional[np.ndarray]] = [None] * len(tps)
+        self._collect_graphed(spec["pending"], outputs, len(tps))
+        if self._spec is not None:
+            self._spec["prev_tokens"] = list(self.last_tokens)
+        entry.complete = True
+        entry.commit_suffixes(tps, spec["rows"])
+        self.prefix_cache.hits += 1
+        wall = time.perf_counter() - t_start
+        graphs = self._decode_graphs
+        batches = spec["batches"]
+        self.stats = {
+            "wall_s": wall, "compute_launch_s": wall,
+            "tokens": float(sum(b.num_tokens for b in batches)),
+            "padded_tokens": float(sum(b.padded_tokens for b in batches)),
+            "decoder_flops": spec["flops"], "micro_batches": float(len(batches)),
+            "weight_wait_s": 0.0, "weight_h2d_bytes": 0.0, "act_d2h_bytes": 0.0, "act_h2d_bytes": 0.0,
+            "resumed_from_shard": 0.0, "graph_captures": float(graphs.captures),
+            "graph_replays": float(graphs.replays), "speculative": 1.0, "prefix_cached": 1.0,
+            "suffix_tokens_reused": float(sum(len(s) - 1 for tp in tps for s in tp.suffixes)), "host_pack_s": 0.0,
+        }
+        return outputs
+
+    def _drop_spec(self, spec: dict) -> None:
+        spec["done"].synchronize()
+        store = self._get_store()
+        for _, _, pool_buf, _ in spec["pending"]:
+            store.recycle_host(pool_buf)
+        self.spec_dropped += 1
+
+    spec_dropped = 0
 
     # ------------------------------------------------- progress / resume
     def _progress(self, total: int):

@@ -41,6 +41,8 @@ KNOBS: Dict[str, Tuple[str, str]] = {
                            "rows, 32 = one wave per query head, 64 = the batch's q_block"),
     "FLS_DECODE_GRAPHS": ("1", "0: no HIP-graph replay of decode-like calls (generation steps with the "
                                "prefix + suffix K/V caches and every weight in HBM)"),
+    "FLS_SPEC_DECODE": ("1", "0: no speculative generation steps (the next decode-graphed step enqueued behind the "
+                             "current one, assuming re-tokenization appends exactly the greedy token; checked)"),
     "FLS_QKV_FOLD": ("1", "0: RMSNorm + QKV as two kernels instead of the row-scaled GEMM on the "
                           "raw hidden state with the norm weight folded into W_qkv"),
 }

@@ -28,7 +28,7 @@ intermediates are shared between them.
 from __future__ import annotations
 
 from collections import OrderedDict
-from typing import Callable, Dict, Tuple
+from typing import Callable, Dict, Optional, Tuple
 
 import numpy as np
 import torch
@@ -156,7 +156,12 @@ class DecodeGraphs:
         return (id(entry), batch.r2_q_block, batch.q_block) + tuple(
             (k, v.shape) for k, v in sorted(batch.host_meta().items()))
 
-    def run(self, batch: PackedBatch, entry) -> torch.Tensor:
+    def run(self, batch: PackedBatch, entry, ids_dev: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Replay (capture on the first sight of the shape) -> the static [n_scored, V] output.
+        ``ids_dev``: the batch's token ids as a device int32 tensor, copied over ``batch.ids`` on
+        the stream (a speculative step whose new tokens are the previous step's device argmax).
+        The metadata goes in by stream-ordered copies from pinned memory, so a replay can be
+        enqueued while an earlier one still runs (its static inputs are overwritten after it)."""
         key = self.key(batch, entry)
         host = batch.host_meta()
         g = self.graphs.get(key)
@@ -164,6 +169,8 @@ class DecodeGraphs:
             if len(self.graphs) >= self.max_graphs:
                 self.graphs.popitem(last=False)
             meta = {k: torch.from_numpy(np.ascontiguousarray(v)).to(self.dev) for k, v in host.items()}
+            if ids_dev is not None:
+                meta["ids"].copy_(ids_dev)
             g = _Graph(meta)
             s = torch.cuda.Stream(self.dev)
             s.wait_stream(torch.cuda.current_stream(self.dev))
@@ -179,7 +186,9 @@ class DecodeGraphs:
             return eager
         self.graphs.move_to_end(key)
         for k, v in host.items():
-            g.meta[k].copy_(torch.from_numpy(np.ascontiguousarray(v)), non_blocking=False)
+            g.meta[k].copy_(torch.from_numpy(np.ascontiguousarray(v)).pin_memory(), non_blocking=True)
+        if ids_dev is not None:
+            g.meta["ids"].copy_(ids_dev, non_blocking=True)
         g.graph.replay()
         g.replays += 1
         self.replays += 1

@@ -7,7 +7,9 @@ on two cache layouts holding the same bytes:
     512 B of every row;
   * grouped: the same K/V re-laid out per KV group (each block reads one contiguous region),
     run as 256 one-group items.
-and reports the effective K/V read bandwidth.
+and reports the effective K/V read bandwidth.  Each launch reads a different one of --layers
+caches (2.9 GB at 16: the 256 MB Infinity Cache holds none of them across launches, like the
+80 layers of a real step).
 
     python scripts/attn_decode_bench.py [--iters 50] [--prefix 1024] [--kept 67]
 """
@@ -50,24 +52,27 @@ def main():
     ap.add_argument("--suffixes", type=int, default=5)
     ap.add_argument("--prefix", type=int, default=1024)
     ap.add_argument("--kept", type=int, default=67)
+    ap.add_argument("--layers", type=int, default=16)
     a = ap.parse_args()
     ops = HipOps()
     dev = torch.device("cuda", 0)
     nh, nkv, hd = 64, 8, 128
     hpg = nh // nkv
-    res = []
     for layout in ("production", "grouped"):
         G = 1 if layout == "production" else nkv
         w, w2, win, T, rows = items(a.prompts, a.suffixes, a.prefix, a.kept, groups=G)
         h, k = (nh, nkv) if G == 1 else (hpg, 1)
-        cache = (torch.randn(rows, 2 * k * hd, device=dev) * 0.5).half()
+        caches = [(torch.randn(rows, 2 * k * hd, device=dev) * 0.5).half() for _ in range(a.layers)]
         qkv = (torch.randn(T, (h + 2 * k) * hd, device=dev) * 0.5).half()
         wt, w2t, wint = (torch.from_numpy(x).to(dev) for x in (w, w2, win))
         seg = torch.zeros(T, dtype=torch.int32, device=dev)
         kv_bytes = int(sum(int(x[4]) for x in w) + sum(int(x[1]) for x in w2)) * 2 * hd * 2 * (nkv if G == 1 else 1)
         for qb in (8, 32):
-            run = lambda: ops.attention(qkv, wt, h, k, hd, kv0=cache, q_block=qb, seg_lo=seg,  # noqa: E731
-                                        work2=w2t, r2win=wint)
+            li = [0]
+
+            def run():
+                li[0] = (li[0] + 1) % a.layers
+                ops.attention(qkv, wt, h, k, hd, kv0=caches[li[0]], q_block=qb, seg_lo=seg, work2=w2t, r2win=wint)
             for _ in range(5):
                 run()
             torch.cuda.synchronize()
@@ -78,9 +83,9 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) * 1000 / a.iters
-            res.append((layout, qb, us, kv_bytes / us / 1e6))
             print(f"{layout:10s} q_block {qb:2d}: {us:7.1f} us/launch  K/V {kv_bytes / 1e6:.0f} MB  "
                   f"{kv_bytes / us / 1e6:.2f} TB/s  (x80 layers: {us * 80 / 1000:.2f} ms/step)", flush=True)
+        del caches
 
 
 if __name__ == "__main__":

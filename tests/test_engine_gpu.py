@@ -441,3 +441,43 @@ def test_decode_graphs_match_eager(setup, weights):
         for a, b in zip(sg, se):
             assert np.isfinite(a.astype(np.float32)).all()
             assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("mode", ["match", "mismatch"])
+def test_speculative_generation_steps_bitwise(setup, mode):
+    """Greedy generation with the suffix K/V cache on weights in HBM: each decode-graphed step
+    enqueues the next one behind itself (ids = its device argmax) while the host decodes and
+    re-tokenizes.  Scores and updated prompts == the same loop without speculation
+    (FLS_SPEC_DECODE=0) bitwise; with the synthetic tokenizer every speculation holds
+    (re-tokenizing suffix + decode(tokens) appends exactly the greedy token), and with every
+    check forced to fail each speculative step is dropped and recomputed, same result."""
+    import argparse
+    from flexible_llm_sharding_amd.api import generation_loop
+    from flexible_llm_sharding_amd.parallel.comm import Comm
+    path, cfg, tok, prompts, ref = setup
+    src = HostStore.from_model_path(cfg, path)
+    args = argparse.Namespace(num_gen_token=6, data_parallel=False, num_batch=1)
+    outs = {}
+    for spec in ("0", "1"):
+        os.environ["FLS_SPEC_DECODE"] = spec
+        try:
+            r = ShardedRunner(cfg, src, "cuda:0", tok, layer_num_per_shard=1, prefix_kv_cache=True,
+                              suffix_kv_cache=True, resident=True)
+            if spec == "1" and mode == "mismatch":
+                r._spec_matches = lambda s, tps: False
+            outs[spec] = generation_loop(args, r, Comm(), tok, prompts)
+            if spec == "1":
+                if mode == "match":
+                    assert r.spec_dropped == 0
+                    assert r.stats["speculative"] == 1.0          # the last step came from a speculation
+                else:
+                    assert r.spec_dropped >= 3 and r.stats["speculative"] == 0.0
+            assert r._spec is None                             # nothing left enqueued after the last step
+            r.close()
+        finally:
+            os.environ.pop("FLS_SPEC_DECODE", None)
+    (s0, u0), (s1, u1) = outs["0"], outs["1"]
+    assert u0 == u1
+    for a, b in zip(s0, s1):
+        assert np.isfinite(a.astype(np.float32)).all()
+        assert np.array_equal(a, b)
