@@ -51,8 +51,11 @@ __global__ __launch_bounds__(256) void gemm_nt_skinny(const half_t* __restrict__
   extern __shared__ __attribute__((aligned(16))) char lds_sk[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, grp = lane >> 4;
-  const int nk = K / KT;                      // K-tiles of this block's slice
-  const size_t kofs = (size_t)blockIdx.y * K; // the slice's first K element
+  // K slice z of gridDim.y: K-tiles [z * base + min(z, rem), ...), the first rem slices one longer
+  // (K = the whole reduction; slices need not divide it)
+  const int nkt = K / KT, nsl = (int)gridDim.y, z = (int)blockIdx.y;
+  const int nk = nkt / nsl + (z < nkt % nsl ? 1 : 0);                   // K-tiles of this block's slice
+  const size_t kofs = (size_t)(z * (nkt / nsl) + min(z, nkt % nsl)) * KT;   // the slice's first K element
   const bool swiglu = EPI == FLS_EPI_SWIGLU;
   // block-local weight row l (wave l / WR, subtile j = (l % WR) / 16) -> physical row; SWIGLU: the
   // first NS / 2 subtiles of a wave are gate rows, the last NS / 2 the matching up rows
@@ -206,8 +209,8 @@ int launch_skinny_rs(const half_t* A, const half_t* W, half_t* C, int M, int N, 
                               lds);
     attr = true;
   }
-  hipLaunchKernelGGL((gemm_nt_skinny<RS, EPI, BN>), dim3(N / BN, S), dim3(256), lds, s, A, W, C, M, N, K / S, lda,
-                     ldw, ldc, ep);
+  hipLaunchKernelGGL((gemm_nt_skinny<RS, EPI, BN>), dim3(N / BN, S), dim3(256), lds, s, A, W, C, M, N, K, lda, ldw,
+                     ldc, ep);
   FLS_CHECK_LAUNCH();
   return 0;
 }
@@ -256,13 +259,18 @@ int try_skinny(const half_t* A, const half_t* W, half_t* C, int M, int N, int K,
   const bool wide = N / 128 >= 256;
   const bool wide_bn256 = wide && M > 64 && M <= 144 && N % 256 == 0;
   if (g_skinny == 1 && (M < 17 || M > 192 || (wide && !wide_bn256))) return 0;
-  // K slices.  BN = 128: the fewest that give whole 256-CU rounds or at least two rounds (one
-  // block per CU: a fractional single round leaves a tail of full-K blocks; 70B at M = 160: O /
-  // down S = 4, QKV S = 8 measured fastest).  BN = 256: the fewest that give 192 blocks (3/4 of
+  // K slices.  BN = 128: else the fewest powers of two that give whole 256-CU rounds or at least
+  // two rounds (one block per CU: a fractional single round leaves a tail of full-K blocks).  BN = 256: the fewest that give 192 blocks (3/4 of
   // the CUs; its deeper DMA queue keeps HBM busy from fewer CUs).  g_skinny_blocks > 0 (A/B) sets
   // a block target instead.
+  // BN = 128 first tries one round of 7/8 to all of the CUs with uneven slices (70B QKV at M = 160:
+  // 80 blocks x 3 = 240 instead of 80 x 8 = 640, 2.5 rounds, and 8 slabs of fp32 partials).
   auto slices = [&](int bn) {
     const long nblk = N / bn;
+    if (bn == 128 && g_skinny_blocks == 0) {
+      for (int s = 2; s <= 16 && nblk * s <= 256; ++s)
+        if (nblk * s >= 224 && nkt / s >= 8) return s;
+    }
     auto good = [&](int s) {
       const long b = nblk * s;
       if (g_skinny_blocks > 0) return b >= g_skinny_blocks;

@@ -408,7 +408,9 @@ def run_decoder(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, b
     head) is read and written by one work item) and feeds the O projection as a strided view
     — and [normed chunk | SwiGLU chunk] in the MLP phase."""
     cfg, ops = ctx.cfg, ctx.ops
-    prune = ctx.prune_last and layer_name == ctx.last_decoder
+    # (every row scored, in row order — a generation step's new tokens: pruning selects them all,
+    # so the plain path runs instead, its single QKV GEMM and the item-per-prompt attention)
+    prune = ctx.prune_last and layer_name == ctx.last_decoder and not getattr(batch, "all_rows_scored", False)
     eps = cfg.rms_norm_eps
     if ctx.attn_rows and x.shape[0] > ctx.attn_rows and ctx.prefix_entry is None:
         x = _attention_grouped(ctx, W, x, batch, prune)

@@ -95,6 +95,17 @@ class PackedBatch:
         return int(self.last_idx.shape[0])
 
     @property
+    def all_rows_scored(self) -> bool:
+        """Every packed row is a scored row, in row order (``last_idx`` = 0..T-1: a generation
+        step computing one new token per suffix), so the rows a pruned last layer keeps are all
+        of them, and the full layer's output already is the scored-row state."""
+        v = self._dev.get("all_rows_scored")
+        if v is None:
+            v = self._dev["all_rows_scored"] = bool(
+                self.num_tokens == self.last_idx.shape[0] and np.array_equal(self.last_idx, np.arange(self.num_tokens)))
+        return v
+
+    @property
     def r2_q_block(self) -> int:
         """q_block for the range-2 (suffix K/V reuse) attention: 8 when every work item holds at
         most 8 rows (a generation step: one new row per suffix) — the packed-GQA decode kernel, a

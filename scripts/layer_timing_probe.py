@@ -53,15 +53,50 @@ def main():
         return out
 
     eng.run_layer = timed
+    # host time in the calls that may block: prefetcher issue / wait, activation store, event syncs
+    host = defaultdict(float)
+
+    def wrap(obj, attr, tag):
+        f = getattr(obj, attr)
+
+        def g(*a_, **k_):
+            t = time.perf_counter()
+            try:
+                return f(*a_, **k_)
+            finally:
+                host[tag] += time.perf_counter() - t
+        setattr(obj, attr, g)
+    from flexible_llm_sharding_amd.runtime import activations, prefetch
+    for cls in (prefetch.PiecePoolPrefetcher, prefetch.ShardPrefetcher):
+        for name in ("_try_issue", "_wait", "acquire", "release", "prefetch"):
+            if name in cls.__dict__:
+                wrap(cls, name, f"{cls.__name__}.{name}")
+    for name in ("get", "put", "prefetch"):
+        wrap(activations.ActivationStore, name, f"ActivationStore.{name}")
+    wrap(activations.ActRing, "acquire", "ActRing.acquire")
+    wrap(torch.cuda.Event, "synchronize", "Event.synchronize")
+    wrap(eng.ShardedRunner, "_throttle", "_throttle")
+    host_in_layer = defaultdict(float)
+    orig2 = eng.run_layer
+
+    def timed2(ctx, name, W, state, batch, meta):
+        t = time.perf_counter()
+        try:
+            return orig2(ctx, name, W, state, batch, meta)
+        finally:
+            host_in_layer[batch.num_tokens] += time.perf_counter() - t
+    eng.run_layer = timed2
     r(prompts)                                     # warmup
     for step in range(a.steps):
         rec.clear()
+        host.clear()
+        host_in_layer.clear()
         t0 = time.perf_counter()
         r(prompts)
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
         comp = [e0.elapsed_time(e1) for _, _, e0, e1 in rec]
-        gaps = [rec[i][2].elapsed_time(rec[i + 1][3]) - comp[i + 1] for i in range(len(rec) - 1)]
+        gaps = [rec[i][3].elapsed_time(rec[i + 1][2]) for i in range(len(rec) - 1)]
         by_rows = defaultdict(list)
         for (name, rows, _, _), c in zip(rec, comp):
             if name.startswith("model.layers."):
@@ -78,6 +113,13 @@ def main():
             print(f"      {gaps[i]:7.2f}  {rec[i][0]}[{rec[i][1]}] -> {rec[i + 1][0]}[{rec[i + 1][1]}]")
         st = {k: round(v, 3) for k, v in r.stats.items() if "stall" in k or "wait" in k}
         print(f"    stats {st}", flush=True)
+        print("    host seconds in: " + ", ".join(f"{k} {v:.3f}" for k, v in sorted(host.items(), key=lambda kv: -kv[1])))
+        print("    host seconds enqueuing layers, by micro-batch rows: " +
+              ", ".join(f"{k}: {v:.3f}" for k, v in sorted(host_in_layer.items())))
+        slow = [(c, rec[i][0], rec[i][1], i) for i, c in enumerate(comp) if rec[i][0].startswith("model.layers.")]
+        slow.sort(reverse=True)
+        print("    slowest decoder computes (ms, layer, rows, index in pass): " +
+              "; ".join(f"{c:.1f} {n}[{rw}] #{i}" for c, n, rw, i in slow[:10]))
     r.close()
 
 
