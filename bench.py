@@ -57,7 +57,16 @@ class DeviceSampler:
         import torch
         self.dev, self.period, self.peak, self.n = dev, period_s, 0.0, 0
         self.peak_outside = 0.0           # device memory in use outside the caching allocator
+        self.rss_peak = 0.0               # this process's resident host memory (warmup + timed steps)
         self._stop = threading.Event()
+        page = os.sysconf("SC_PAGE_SIZE")
+
+        def rss():
+            try:
+                with open("/proc/self/statm") as f:
+                    return int(f.read().split()[1]) * page
+            except (OSError, ValueError, IndexError):
+                return 0
 
         def run():
             torch.cuda.set_device(dev)
@@ -66,6 +75,8 @@ class DeviceSampler:
                 used = float(total - free)
                 self.peak = max(self.peak, used)
                 self.peak_outside = max(self.peak_outside, used - torch.cuda.memory_reserved(dev))
+                if self.n % 16 == 0:
+                    self.rss_peak = max(self.rss_peak, float(rss()))
                 self.n += 1
                 self._stop.wait(self.period)
 
@@ -415,6 +426,7 @@ def main(argv=None):
     comm.barrier()
     elapsed = time.perf_counter() - t_start
     dev_used_peak, n_samples, outside_peak = sampler.stop() if sampler is not None else (0.0, 0, 0.0)
+    rss_run = sampler.rss_peak if sampler is not None else 0.0
     if not a.cpu:
         ms_ = torch.cuda.memory_stats(dev)
         log(rank, f"[bench] allocator: device mallocs {ms_.get('num_device_alloc')}, "
@@ -461,6 +473,9 @@ def main(argv=None):
         "peak_device_used_gb": round(dev_used_peak / 1e9, 3), "device_mem_samples": n_samples,
         "peak_outside_allocator_gb": round(comm.all_reduce_max(outside_peak) / 1e9, 3),
         "host_pinned_gb": round(pinned / 1e9, 3), "host_peak_rss_gb": round(rss / 1e9, 3),
+        # resident memory sampled every ~32 ms through warmup and timed steps (host_peak_rss_gb is
+        # the lifetime maximum: it includes building the host store / writing the checkpoint)
+        "host_rss_run_peak_gb": round(comm.all_reduce_max(rss_run) / 1e9, 3),
         "scores_finite": finite, "scores_sha1": digests,
         "world": world, "process_group_ranks": pg_world,
         "backend": comm.backend or ("none" if world == 1 else "?"), "rank_devices": devices,

@@ -599,7 +599,8 @@ class ShardedRunner:
             if px.ck is not None and self._ckpt_due(k):
                 px.ck.save_state(self._ckpt_key(k), b, state)     # a shard's outputs
             self._emit(px, k, b, state, from_rx=False)
-            self._throttle(px.item_ev, self.RUNAHEAD_ITEMS)
+            if self.RUNAHEAD_ITEMS:
+                self._throttle(px.item_ev, self.RUNAHEAD_ITEMS)
 
     def _exec_pipeline(self, px: "_Pass") -> None:
         """Model parallel: this rank's items in program order; inputs from the previous stage
@@ -903,7 +904,7 @@ class ShardedRunner:
     # ... and to this many (shard, micro-batch) computes: with many micro-batches per layer two
     # shards of queued work would hold two layers' worth of parked activations in pinned host
     # buffers waiting for their copies (128 prompts: 6.5 GB of pinned RAM instead of ~4)
-    RUNAHEAD_ITEMS = 6
+    RUNAHEAD_ITEMS = knobs.get_int("FLS_RUNAHEAD_ITEMS")
     # an activation consumed again within this many micro-batch computes stays in HBM
     # (zigzag: the boundary micro-batch is next, its neighbour 3 computes later)
     CARRY_WINDOW = 3

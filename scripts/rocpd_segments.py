@@ -14,7 +14,8 @@ import statistics
 def short(name: str) -> str:
     m = re.search(r"_GLOBAL__N_1\d+(\w+?)I(Li\d+E)+", name)
     if m:
-        return f"{m.group(1)}<{','.join(re.findall(r'Li(\d+)E', name))}>"
+        args = re.findall(r"Li(\d+)E", name)
+        return f"{m.group(1)}<{','.join(args)}>"
     m = re.search(r"_GLOBAL__N_1\d+(\w+?)E", name)
     return m.group(1) if m else name[:48]
 
