@@ -41,6 +41,7 @@ from .ops import get_ops
 from .parallel.comm import Comm
 from .parallel.pipeline import StageInbox, build_programs, host_wait, rank_items, rx_key
 from .parallel.planner import ShardPlan, make_plan
+from .runtime import hostmem
 from .runtime.activations import ActivationStore, ActRing
 from .runtime.batch import Q_BLOCK, Q_BLOCK_MHA, PackedBatch, pack_prompts, split_microbatches
 from .runtime.prefetch import ShardPrefetcher
@@ -510,6 +511,7 @@ class ShardedRunner:
             self.sends = []            # (tensor, work) of outputs in flight to another rank
             self.shard_ev: List = []   # end-of-shard events on the compute stream (host run-ahead bound)
             self.item_ev: List = []    # end-of-item events (the same bound in micro-batch computes)
+            self.allocs0, self.alloc_s0 = hostmem.alloc_calls, hostmem.alloc_seconds
             self.flops = 0.0
             self.flops_of = {}              # (micro-batch, pruned layer) -> FLOPs of one decoder layer
             self.compute_s = 0.0
@@ -521,6 +523,7 @@ class ShardedRunner:
             self.prog = self.inbox = None
             self.pbar = None
             self.ring: Optional[ActRing] = None      # hidden-state slots (storage cpu / disk, local passes)
+            self.landed = {}           # micro-batch -> (ring-slot state, H2D event) landed ahead of its use
 
     def _run_batches(self, tps, batches, t_start: float) -> List[Optional[np.ndarray]]:
         metas = [b.device_tensors(self.dev) for b in batches]   # all uploads before any compute
@@ -666,6 +669,10 @@ class ShardedRunner:
             return None
         if b in px.carry:
             return px.carry.pop(b)
+        if b in px.landed:
+            t, ev = px.landed.pop(b)
+            px.store.wait_landed(ev)
+            return t
         shape = self._state_shape(self.my_shards[k][0] - 1, batch)
         if ring is not None and shape[0] == batch.num_tokens:
             return px.store.get(b, out=ring.acquire(b, shape, px.store.h2d))
@@ -682,8 +689,24 @@ class ShardedRunner:
                 px.inbox.prefetch(rx_key(k2, b2))
         elif self.my_shards[k2][0] > 0 and k2 == k:
             px.store.prefetch(b2)
+            self._land(px, k2, b2)
         elif k2 != k and idx + 2 < len(px.items):
             px.store.prefetch(px.items[idx + 2][1])
+
+    def _land(self, px: "_Pass", k: int, b: int) -> None:
+        """Bring the next item's parked state into a free ring slot now, ahead of this item's
+        compute and of its output's D2H: its H2D then waits only for the D2H of the slot's last
+        occupant (two items back), never behind the D2H of the item computing now (with the
+        copies of a pass issued only at the point of use, a 16k-budget pass measured ~18 ms of
+        H2D wait in front of most micro-batches, profiles/r5_spill)."""
+        ring, batch = px.ring, px.batches[b]
+        if (ring is None or px.prog is not None or b in px.carry or b in px.landed
+                or not ring.has_free() or b not in px.store.keys()):
+            return
+        shape = self._state_shape(self.my_shards[k][0] - 1, batch)
+        if shape[0] != batch.num_tokens:
+            return
+        px.landed[b] = px.store.get(b, out=ring.acquire(b, shape, px.store.h2d), wait=False)
 
     def _compute(self, px: "_Pass", k: int, b: int, state):
         """Every layer of shard k on micro-batch b."""
@@ -812,6 +835,8 @@ class ShardedRunner:
             # GPU-side: compute stream stalled on the weight / activation copy streams
             "weight_stall_gpu_s": pf.take_stall_seconds() if self.cuda else 0.0,
             "act_stall_gpu_s": store.take_stall_seconds() if self.cuda else 0.0,
+            "pinned_allocs": float(hostmem.alloc_calls - px.allocs0),
+            "pinned_alloc_s": hostmem.alloc_seconds - px.alloc_s0,
         }
         self.stats.update(rx_stats)
         if self.verbose:

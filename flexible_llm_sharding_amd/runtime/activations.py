@@ -232,9 +232,11 @@ class ActivationStore:
         else:
             self._inflight[key] = (None, None)
 
-    def get(self, key, pop: bool = True, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def get(self, key, pop: bool = True, out: Optional[torch.Tensor] = None, wait: bool = True):
         """The state parked under ``key`` on the device: a fresh tensor, or ``out`` (a slot of the
-        engine's ActRing the caller acquired for the H2D stream) when given."""
+        engine's ActRing the caller acquired for the H2D stream) when given.  ``wait=False``
+        (a landing ahead of its use): -> (tensor, H2D event); the compute stream waits later, by
+        :meth:`wait_landed`."""
         with self.lock:
             e = self._e.pop(key) if pop else self._e[key]
         if self.mode == "gpu":
@@ -278,11 +280,8 @@ class ActivationStore:
             ev = torch.cuda.Event()
             ev.record(self.h2d)
         self.bytes_h2d += nbytes
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(cur)
-        cur.wait_event(ev)
-        e1.record(cur)
-        self._stall_ev.append((e0, e1))
+        if wait:
+            self.wait_landed(ev)
         if not ring:
             out.record_stream(cur)
         if pop:
@@ -294,7 +293,16 @@ class ActivationStore:
                     os.remove(e.path)
                 except OSError:
                     pass
-        return out
+        return out if wait else (out, ev)
+
+    def wait_landed(self, ev) -> None:
+        """The compute stream waits for an H2D (timed: ``act_stall_gpu_s``)."""
+        cur = torch.cuda.current_stream(self.dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(cur)
+        cur.wait_event(ev)
+        e1.record(cur)
+        self._stall_ev.append((e0, e1))
 
     def take_stall_seconds(self) -> float:
         """GPU time the compute stream spent waiting for activation H2D since the last call
@@ -396,6 +404,9 @@ class ActRing:
 
     def owns(self, key) -> bool:
         return key in self._owner
+
+    def has_free(self) -> bool:
+        return any(o is None for o in self._owner)
 
     def reset(self) -> None:
         """After an aborted pass: every slot free, its next fill ordered after the work queued on

@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import time
 from typing import Dict
 
 import torch
@@ -24,6 +25,10 @@ _IO_THREADS = knobs.get_int("FLS_IO_THREADS")
 # reported by runtime.stream separately)
 pinned_live = 0
 pinned_peak = 0
+# alloc_host calls and their host seconds (hipHostMalloc is slow: a pass should reuse pooled
+# buffers, not allocate; engine stats report the per-call counts)
+alloc_calls = 0
+alloc_seconds = 0.0
 
 
 def _count(n: int) -> None:
@@ -64,10 +69,14 @@ def alloc_host(nbytes: int, pinned: bool = True) -> torch.Tensor:
     ``hipHostFree``d exactly when the last view dies.
     """
     if pinned and _gpu_present():
+        global alloc_calls, alloc_seconds
         rt = _native.runtime_or_none()
         if rt is not None:
             n = max(1, nbytes)
+            t0 = time.perf_counter()
             ptr = rt.fls_pinned_alloc(n)
+            alloc_calls += 1
+            alloc_seconds += time.perf_counter() - t0
             if ptr:
                 arr_t = type("PinnedBlock", (ctypes.c_uint8 * n,), {})
                 arr = arr_t.from_address(ptr)

@@ -107,10 +107,13 @@ def main():
             cs = np.array(cs)
             print(f"    decoder computes of {rows:6d} rows: n {len(cs):3d}  median {np.median(cs):7.2f} ms  "
                   f"p90 {np.percentile(cs, 90):7.2f}  max {cs.max():7.2f}  sum {cs.sum():8.1f}")
+        big = [g for g in gaps if g > 1.0]
+        print(f"    gaps > 1 ms: {len(big)}, sum {sum(big):.1f} ms; position of each in its layer's item order: "
+              + str(sorted({(i + 1 - 1) % max(1, int(r.stats.get('micro_batches', 1))) for i, g in enumerate(gaps) if g > 1.0})))
         top = sorted(range(len(gaps)), key=lambda i: -gaps[i])[:12]
         print("    largest gaps (ms) after -> before:")
         for i in top:
-            print(f"      {gaps[i]:7.2f}  {rec[i][0]}[{rec[i][1]}] -> {rec[i + 1][0]}[{rec[i + 1][1]}]")
+            print(f"      {gaps[i]:7.2f}  #{i} {rec[i][0]}[{rec[i][1]}] -> #{i + 1} {rec[i + 1][0]}[{rec[i + 1][1]}]")
         st = {k: round(v, 3) for k, v in r.stats.items() if "stall" in k or "wait" in k}
         print(f"    stats {st}", flush=True)
         print("    host seconds in: " + ", ".join(f"{k} {v:.3f}" for k, v in sorted(host.items(), key=lambda kv: -kv[1])))

@@ -50,6 +50,11 @@ def test_microbatch_split():
     g = split_microbatches(tps, 40)
     assert g == [[0, 1], [2, 3], [4, 5], [6]]
     assert split_microbatches(tps, 5) == [[i] for i in range(7)]
+    # as many micro-batches as greedy filling needs, evened out (bench --prompts-per-gpu 128 under
+    # its 24,576-token plan: 8 x 16 prompts, not 7 x 18 + 2)
+    big = [TokenizedPrompt([1] * 1024, [[1] * 64] * 5, 64, [63] * 5) for _ in range(128)]
+    assert [len(x) for x in split_microbatches(big, 24576)] == [16] * 8
+    assert [len(x) for x in split_microbatches(big[:32], 16384)] == [11, 11, 10]
 
 
 def test_pack_segments():
