@@ -926,9 +926,11 @@ class ShardedRunner:
             shard_ev.pop(0).synchronize()
 
     RUNAHEAD_SHARDS = 2
-    # ... and to this many (shard, micro-batch) computes: with many micro-batches per layer two
-    # shards of queued work would hold two layers' worth of parked activations in pinned host
-    # buffers waiting for their copies (128 prompts: 6.5 GB of pinned RAM instead of ~4)
+    # ... and optionally to this many (shard, micro-batch) computes (0: off, the default).  Measured
+    # both ways (profiles/r5_spill/runahead): 6 speeds up a 16k-budget pass (+7%) and the streamed
+    # 128-prompt envelope (+16%, 1.3 GB less pinned RAM) but slows the 128-prompt pass from host RAM
+    # by 10-13% (its H2D reloads then wait ~18 ms in front of most micro-batches); not understood, so
+    # it stays a deployment knob
     RUNAHEAD_ITEMS = knobs.get_int("FLS_RUNAHEAD_ITEMS")
     # an activation consumed again within this many micro-batch computes stays in HBM
     # (zigzag: the boundary micro-batch is next, its neighbour 3 computes later)

@@ -30,8 +30,9 @@ KNOBS: Dict[str, Tuple[str, str]] = {
     "FLS_FAULT": ("", "'rank:shard': raise on that rank when it enters that local shard"),
     "FLS_PIECE_POOL": ("1", "0: whole-layer weight slots under --max_vram_gb instead of the "
                             "attention / MLP piece pool (tests: both must give the same scores)"),
-    "FLS_RUNAHEAD_ITEMS": ("6", "host run-ahead bound in (shard, micro-batch) computes, on top of the 2-shard bound "
-                                "(0: shards only)"),
+    "FLS_RUNAHEAD_ITEMS": ("0", "host run-ahead bound in (shard, micro-batch) computes on top of the 2-shard bound "
+                                "(0: shards only; 6: +7% at a 16k token budget, -10% at 128 prompts: "
+                                "profiles/r5_spill/runahead)"),
     # ---- A/B switches of measured choices (defaults are the measured winners)
     "FLS_SPLITK": ("1", "0: no split-K path for <= 512-row GEMMs"),
     "FLS_GEMM_V11": ("1", "384x256 GEMM tile: 0 off (v10 everywhere), 1 where it pays, 2 every valid shape"),
