@@ -344,7 +344,8 @@ class ShardedRunner:
             return False
         return bool(self.cuda and max_vram_gb and not resident and not keep and not resume_dir
                     and self.plan.mode == "single" and shards and all(len(s) == 1 for s in shards)
-                    and all(source.host_buffer(self.names[s[0]]) is not None for s in shards)
+                    and (all(source.host_buffer(self.names[s[0]]) is not None for s in shards)
+                         or hasattr(source, "stream_into"))
                     and self.act_dtype == torch.float16 and getattr(source, "dtype", torch.float16) == torch.float16)
 
     def _mb_major(self) -> bool:

@@ -460,9 +460,15 @@ class PiecePoolPrefetcher(ShardPrefetcher):
         self.wait_seconds = 0.0
         self.load_seconds = 0.0
         self._stall_ev: List[Tuple[torch.cuda.Event, torch.cuda.Event]] = []
-        for n in (self.names[s[0]] for s in self.shards):
-            if source.host_buffer(n) is None:
-                raise ValueError("piece pools need host-resident layers")
+        # layers read from their files (--weight_cache stream): each piece is a byte range of the
+        # layer image the native streamer reads straight into the slot; the blocking file reads
+        # run on one loader thread in issue order, so the host thread never waits for the disk
+        # except when a piece it needs is still being read
+        self._streamed = any(source.host_buffer(self.names[s[0]]) is None for s in self.shards)
+        if self._streamed and not hasattr(source, "stream_into"):
+            raise ValueError("piece pools need host-resident layers or a streaming source")
+        self._loader = ThreadPoolExecutor(1, thread_name_prefix="fls-piece-loader") if self._streamed else None
+        self._futs: Dict[int, Future] = {}
 
     # ----------------------------------------------------------- bookkeeping
     def planned_hbm_bytes(self) -> int:
@@ -502,14 +508,27 @@ class PiecePoolPrefetcher(ShardPrefetcher):
         t0 = time.perf_counter()
         slot = self._slot(s)
         ev = torch.cuda.Event()
-        with torch.cuda.stream(self.copy_stream):
-            if self._slot_free[s] is not None:
-                self.copy_stream.wait_event(self._slot_free[s])
-            nbytes = self._copy_piece(slot, name, lo, hi)
-            if self.on_load is not None and kind in "am" and self._is_dec(k):
-                # attention piece: ln1 into W_qkv; MLP piece (ln2 is its first tensor): ln2 into W_gate/up
-                self._loaded(name, self._piece_views(slot, name, kind == "a"))
-            ev.record(self.copy_stream)
+        free = self._slot_free[s]
+
+        def load():
+            with torch.cuda.stream(self.copy_stream):
+                if free is not None:
+                    self.copy_stream.wait_event(free)
+                if self.src.host_buffer(name) is None:
+                    nbytes = self.src.stream_into(name, slot, self.copy_stream, lo, hi)
+                else:
+                    nbytes = self._copy_piece(slot, name, lo, hi)
+                if self.on_load is not None and kind in "am" and self._is_dec(k):
+                    # attention piece: ln1 into W_qkv; MLP piece (ln2 is its first tensor): ln2 into W_gate/up
+                    self._loaded(name, self._piece_views(slot, name, kind == "a"))
+                ev.record(self.copy_stream)
+            return nbytes
+
+        if self._loader is not None:
+            self._futs[gid] = self._loader.submit(load)
+            nbytes = hi - lo
+        else:
+            nbytes = load()
         self.load_seconds += time.perf_counter() - t0
         self.bytes_h2d += nbytes
         if owner is not None:
@@ -543,6 +562,9 @@ class PiecePoolPrefetcher(ShardPrefetcher):
     def _wait(self, gid: int) -> Tuple[int, torch.cuda.Event]:
         self._pump(gid)
         s, ev = self._issued[gid]
+        fut = self._futs.pop(gid, None)
+        if fut is not None:
+            fut.result()                  # the loader has enqueued the piece's DMAs and its event
         cur = torch.cuda.current_stream(self.dev)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(cur)
@@ -600,6 +622,7 @@ class PiecePoolPrefetcher(ShardPrefetcher):
     def _release_gid(self, gid: int) -> None:
         if gid in self._released or gid not in self._issued:
             return
+        self._futs.pop(gid, None)     # (a streamed piece released unread: its load job still runs in order)
         s, _ = self._issued[gid]
         e = torch.cuda.Event()
         e.record(torch.cuda.current_stream(self.dev))
@@ -625,10 +648,19 @@ class PiecePoolPrefetcher(ShardPrefetcher):
             self._release_gid(gid)
         self._pump()
 
+    def _drain_loader(self) -> None:
+        for fut in list(self._futs.values()):
+            try:
+                fut.result()
+            except Exception:       # noqa: BLE001  (a failed read surfaces where it was awaited)
+                pass
+        self._futs.clear()
+
     def discard_loaded(self) -> None:
         """After an empty or aborted pass: every issued piece is dropped (its copy stays ordered
         on the copy stream before any later load into the same slot) and the next call starts
         its pass from the first piece."""
+        self._drain_loader()
         cur = torch.cuda.current_stream(self.dev)
         for gid in list(self._issued):
             if gid not in self._released:
@@ -645,6 +677,9 @@ class PiecePoolPrefetcher(ShardPrefetcher):
         self._m_turn = 0
 
     def close(self):
+        self._drain_loader()
+        if self._loader is not None:
+            self._loader.shutdown(wait=True)
         if self.cuda:
             torch.cuda.synchronize(self.dev)
         self._issued.clear()

@@ -481,3 +481,27 @@ def test_speculative_generation_steps_bitwise(setup, mode):
     for a, b in zip(s0, s1):
         assert np.isfinite(a.astype(np.float32)).all()
         assert np.array_equal(a, b)
+
+
+def test_piece_pool_streams_layer_files(mid_model, tmp_path):
+    """--max_vram_gb with --weight_cache stream: the piece pool reads each attention / MLP piece
+    straight from the layer file into its slot (native streamer, one loader thread), the norms
+    folded per load: same scores as the host-resident pool, over repeated calls."""
+    from flexible_llm_sharding_amd.runtime.prefetch import PiecePoolPrefetcher
+    from flexible_llm_sharding_amd.utils.synthetic import write_synthetic_checkpoint
+    cfg, store, tok, prompts = mid_model
+    d = tmp_path / "ck"
+    write_synthetic_checkpoint(cfg, str(d), seed=3, std=0.05)
+    host = ShardedRunner(cfg, HostStore.from_model_path(cfg, str(d)), "cuda:0", tok, layer_num_per_shard=1,
+                         max_vram_gb=40)
+    want = host(prompts)
+    host.close()
+    r = ShardedRunner(cfg, FileLayerSource(cfg, str(d)), "cuda:0", tok, layer_num_per_shard=1, max_vram_gb=40)
+    assert isinstance(r.prefetcher, PiecePoolPrefetcher) and r.prefetcher._streamed
+    for _ in range(2):
+        got = r(prompts)
+        for a, b in zip(want, got):
+            assert np.array_equal(a, b)
+    assert r.stats["weight_h2d_bytes"] > 0
+    r.close()
+    torch.cuda.set_per_process_memory_fraction(1.0)
