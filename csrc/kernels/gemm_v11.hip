@@ -302,7 +302,28 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_v11(const half_t* __restrict__
   epilogue_quadrant<EPI, 8, true>(C, ldc, M, mrow, ncol, grp, acc, ep, mlo);
 }
 
-int g_v11 = 1;               // 0 off, 1 auto (large GEMMs, no extra row padding), 2 any valid shape (tests)
+int g_v11 = 1;               // 0 off, 1 auto (large GEMMs, no extra row padding), 2 any valid shape (tests),
+                             // 3 auto by whole 256-CU tile rounds (v11_pays)
+// time of one 384 x 256 v11 tile in 256 x 256 v10 tiles, x 100 (3: v11_pays)
+int g_v11_cost = 145;
+
+// Whole 256-CU tile rounds of each kernel at this shape, a v11 tile priced at g_v11_cost / 100
+// v10 tiles: a launch whose tile count is not a multiple of 256 pays its last round in full.  v10
+// runs rows past its ROW_CHUNK (gemm.hip; default 16384) as evenly sized launches, each with its
+// own tail.
+bool v11_pays(int M, int N) {
+  using namespace v11;
+  const long t11 = (long)((M + TM - 1) / TM) * (N / TN);
+  const long r11 = (t11 + 255) / 256;
+  const int n_chunks = M > 16384 ? (M + 16383) / 16384 : 1;
+  const int step = ((M + n_chunks - 1) / n_chunks + 255) / 256 * 256;
+  long r10 = 0;
+  for (int r0 = 0; r0 < M; r0 += step) {
+    const long t10 = (long)((min(step, M - r0) + 255) / 256) * (N / 256);
+    r10 += (t10 + 255) / 256;
+  }
+  return r11 * g_v11_cost <= r10 * 100;
+}
 
 template <int EPI>
 int launch_v11(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int lda, int ldw, int ldc, Epi ep,
@@ -327,7 +348,14 @@ int launch_v11(const half_t* A, const half_t* W, half_t* C, int M, int N, int K,
 // shape it supports (tests: small and ragged shapes); returns the previous mode
 extern "C" int fls_gemm_set_v11(int mode) {
   const int old = g_v11;
-  g_v11 = mode < 0 ? 0 : mode > 2 ? 2 : mode;
+  g_v11 = mode < 0 ? 0 : mode > 3 ? 3 : mode;
+  return old;
+}
+
+// mode 3's price of a v11 tile in v10 tiles x 100 (<= 0: keep); returns the previous price
+extern "C" int fls_gemm_set_v11_cost(int cost) {
+  const int old = g_v11_cost;
+  if (cost > 0) g_v11_cost = cost;
   return old;
 }
 
@@ -340,12 +368,13 @@ extern "C" int fls_gemm_v11_try(const void* A, const void* W, void* C, const voi
                                 const float* rscale, float alpha, fls_stream_t s) {
   using namespace v11;
   if (!g_v11 || M < TM || N % TN || K % TK || (K / TK) % 2 || lda % 8 || ldw % 8) return 0;
-  if (g_v11 == 1) {
+  if (g_v11 == 1 || g_v11 == 3) {
     // fills the chip (at least one tile per CU per launch)
     if ((size_t)((M + TM - 1) / TM) * (N / TN) < 256) return 0;
-    // computes no more rows than v10's 256-row tiles would (callers chunk rows in multiples of
-    // 768 = lcm(256, 384))
-    if ((size_t)((M + TM - 1) / TM) * TM > (size_t)((M + 255) / 256) * 256) return 0;
+    // 1: computes no more rows than v10's 256-row tiles would (callers chunk rows in multiples
+    // of 768 = lcm(256, 384)); 3: takes no longer in whole tile rounds
+    if (g_v11 == 1 && (size_t)((M + TM - 1) / TM) * TM > (size_t)((M + 255) / 256) * 256) return 0;
+    if (g_v11 == 3 && !v11_pays(M, N)) return 0;
   }
   // 32-bit DMA offsets: every row of A (piece rows + lane rows + K) and of the (stacked) weight
   if ((size_t)M * lda * 2 >= (1ull << 32)) return 0;
