@@ -302,8 +302,10 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_v11(const half_t* __restrict__
   epilogue_quadrant<EPI, 8, true>(C, ldc, M, mrow, ncol, grp, acc, ep, mlo);
 }
 
-int g_v11 = 1;               // 0 off, 1 auto (large GEMMs, no extra row padding), 2 any valid shape (tests),
-                             // 3 auto by whole 256-CU tile rounds (v11_pays)
+int g_v11 = 3;               // 0 off, 1 auto (large GEMMs, no extra row padding), 2 any valid shape (tests),
+                             // 3 auto by whole 256-CU tile rounds (v11_pays; default: at row counts that
+                             // are not whole rounds of either tile it picks the faster kernel more often
+                             // than 1, equal on whole-round shapes, profiles/r5_resident/gemm_m.log)
 // time of one 384 x 256 v11 tile in 256 x 256 v10 tiles, x 100 (3: v11_pays)
 int g_v11_cost = 145;
 
@@ -344,8 +346,9 @@ int launch_v11(const half_t* A, const half_t* W, half_t* C, int M, int N, int K,
 
 }  // namespace
 
-// 1 = use v11 where it pays (default: no more rows than v10), 0 = v10 everywhere, 2 = v11 on every
-// shape it supports (tests: small and ragged shapes); returns the previous mode
+// 0 = v10 everywhere, 1 = v11 where it pads no more rows than v10, 2 = v11 on every shape it
+// supports (tests: small and ragged shapes), 3 = v11 where it takes no more whole tile rounds
+// (default); returns the previous mode
 extern "C" int fls_gemm_set_v11(int mode) {
   const int old = g_v11;
   g_v11 = mode < 0 ? 0 : mode > 3 ? 3 : mode;

@@ -156,7 +156,7 @@ class ShardedRunner:
                                  + RUNTIME_RESERVE + self._splitk_reserve())
             try:
                 # provisional (the call's token count is unknown yet); _plan_call is authoritative
-                token_budget, mlp_chunk, attn_rows, qkv_chunk, est = plan_for_vram(
+                token_budget, mlp_chunk, attn_rows, qkv_chunk, est, _ = plan_for_vram(
                     cfg, self._vram_cap, layer_num_per_shard, n_slots, token_budget, mlp_chunk,
                     overhead=self._outside, fused_norm=self._fused_norm_planned())
             except ValueError:
@@ -251,6 +251,7 @@ class ShardedRunner:
         self._W_all: Dict[str, Dict[str, torch.Tensor]] = {}
         self._h2d0: Optional[int] = None     # prefetcher byte count at the start of the next call
         self._ring: Optional[ActRing] = None
+        self._resident_states = False      # _plan_call: every micro-batch keeps its own ring slot
 
     # ----------------------------------------------------------- helpers
     def _fused_norm_planned(self) -> bool:
@@ -448,15 +449,16 @@ class ShardedRunner:
         rows = [tp.num_tokens - (len(tp.prefix) if cached else 0) for tp in tps]
         total = sum(rows)
         tb, mc, n_slots = self._plan_req
-        tb, mc, ar, qc, est = plan_for_vram(self.cfg, self._vram_cap, self.lnps, self.prefetcher.n_slots, tb, mc,
+        tb, mc, ar, qc, est, res = plan_for_vram(self.cfg, self._vram_cap, self.lnps, self.prefetcher.n_slots, tb, mc,
                                         total_tokens=max(1, total), max_prompt_rows=max(rows or [0]),
                                         overhead=self._outside,
                                         weight_bytes=self.prefetcher.planned_hbm_bytes() if self.cuda else None,
                                         fused_norm=self.ctx.fused_norm)
         self.token_budget, self.mlp_chunk = tb, mc
         self.ctx.mlp_chunk, self.ctx.attn_rows, self.ctx.qkv_chunk = mc, ar, qc
+        self._resident_states = res
         self.vram_plan.update({"token_budget": tb, "mlp_chunk": mc, "attn_rows": ar, "qkv_chunk": qc,
-                               "estimated_peak_bytes": est,
+                               "estimated_peak_bytes": est, "resident_states": res,
                                "call_tokens": total})
 
     # model parallel: micro-batches per pipeline stage wanted before the budget may shrink, and the
@@ -563,11 +565,12 @@ class ShardedRunner:
             px.inbox.begin_call(max([self._rx_bytes(k, batches[b]) for (k, b), src in zip(px.items, px.prog.src)
                                      if src is not None] or [0]))
         if px.prog is None and self.cuda and self.storage != "gpu" and px.items:
-            # hidden states in fixed HBM slots: 1 (the call is one micro-batch: it never leaves HBM)
-            # or 2 (computing + landing; the zigzag carries fit) — exactly the plan's live states
+            # hidden states in fixed HBM slots: 1 (the call is one micro-batch: it never leaves HBM),
+            # one per micro-batch (the VRAM plan found room for every state: none is parked) or 2
+            # (computing + landing; the zigzag carries fit) — exactly the plan's live states
             if self._ring is None:
                 self._ring = ActRing(self.dev, self.act_dtype, 1)
-            n_ring = 1 if len(batches) == 1 else 2
+            n_ring = 1 if len(batches) == 1 else len(batches) if self._resident_states else 2
             self._ring.resize(n_ring, max(b.num_tokens for b in batches) * self.cfg.hidden_size)
             px.ring = self._ring
         if self.my_shards and px.items:
@@ -751,12 +754,14 @@ class ShardedRunner:
             w = self.comm.isend(st, px.dst_rank)
             px.sends.append((st, w))
             return w
-        elif (self.storage != "gpu" and px.pos.get((k + 1, b), len(px.items)) - px.pos[(k, b)]
-              <= (self.CARRY_WINDOW if ring is None or ring.n >= 2 else 1)):
-            # re-used within CARRY_WINDOW micro-batch computes (the zigzag boundary micro-batch
-            # and its neighbour): a PCIe round trip would only add traffic, keep it in HBM (with
-            # two ring slots both carries of a zigzag boundary fit: the neighbour is consumed
-            # before anything else needs a slot)
+        elif self.storage != "gpu" and ((ring is not None and ring.n >= len(px.batches))
+                                        or px.pos.get((k + 1, b), len(px.items)) - px.pos[(k, b)]
+                                        <= (self.CARRY_WINDOW if ring is None or ring.n >= 2 else 1)):
+            # a slot per micro-batch (resident plan): the state stays in its slot for the next
+            # shard.  Else re-used within CARRY_WINDOW micro-batch computes (the zigzag boundary
+            # micro-batch and its neighbour): a PCIe round trip would only add traffic, keep it in
+            # HBM (with two ring slots both carries of a zigzag boundary fit: the neighbour is
+            # consumed before anything else needs a slot)
             px.carry[b] = state
         else:
             ev = px.store.put(b, state)

@@ -246,13 +246,40 @@ def balanced_step(rows: int, limit: int, align: int = 0) -> int:
     return limit
 
 
+def _proj(ctx: ExecContext, W: Dict[str, torch.Tensor], h, wr, p, n_q, n_k, bias, out=None, rscale=None):
+    """QKV-shaped projection of ``h`` by ``wr`` with RoPE on the first n_q + n_k heads (Qwen3:
+    per-head q / k RMSNorm first); ``rscale``: per-row scale of the fused RMSNorm (HIP only)."""
+    cfg = ctx.cfg
+    kw = {"rscale": rscale} if rscale is not None else {}
+    if cfg.qk_norm:
+        return ctx.ops.qkv_norm_rope(h, wr, p, ctx.cos, ctx.sin, n_q, n_k, cfg.head_dim, W["qn"], W["kn"],
+                                     cfg.rms_norm_eps, bias=bias, out=out, **kw)
+    return ctx.ops.qkv_rope(h, wr, p, ctx.cos, ctx.sin, n_q, n_k, cfg.head_dim, bias=bias, out=out, **kw)
+
+
+def _scored_q(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, last_idx: torch.Tensor,
+              last_pos: torch.Tensor) -> torch.Tensor:
+    """Q (+ RoPE) of the scored rows of the pruned last layer: [n_scored, q_size] — their raw rows
+    gathered and scaled by their own RMSNorm statistic (fused) or normalised explicitly."""
+    cfg, ops = ctx.cfg, ctx.ops
+    qs, eps = cfg.q_size, cfg.rms_norm_eps
+    w, b = W["wqkv"], W.get("bqkv")
+    bq = b[:qs] if b is not None else None
+    xq = ops.gather_rows(x, last_idx)
+    if ctx.fused_norm:
+        return _proj(ctx, W, xq, w[:qs], last_pos, cfg.num_attention_heads, 0, bq, rscale=ops.row_rstd(xq, eps))
+    return _proj(ctx, W, ops.rmsnorm(xq, W["ln1"], eps), w[:qs], last_pos, cfg.num_attention_heads, 0, bq)
+
+
 def _attn_inputs(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, pos: torch.Tensor,
-                 last_idx: Optional[torch.Tensor], prune: bool, last_pos: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 last_idx: Optional[torch.Tensor], prune: bool, last_pos: Optional[torch.Tensor] = None,
+                 q_scored: Optional[torch.Tensor] = None) -> torch.Tensor:
     """RMSNorm + QKV projection (+ RoPE, + bias) of every row into one [T, qkv] buffer.
     ``prune`` (the last decoder layer): K/V (+ RoPE on K) for every row, Q only for the scored rows,
     scattered into the Q columns of those rows — the other rows' Q columns stay unwritten, the last
     layer's attention work items (``work_last``) query only scored rows (Q is q_size / qkv_size of
-    the projection: 80% for Llama-2-70B).
+    the projection: 80% for Llama-2-70B).  ``q_scored``: that Q, already projected (the grouped
+    attention phase projects every group's scored rows in one GEMM, as the whole-batch path does).
 
     Fused (``ctx.fused_norm``, HIP): one GEMM over the raw hidden state with ln1 folded into W_qkv
     and each row scaled by its rsqrt(mean(x^2) + eps) in the epilogue — the workspace holds only
@@ -260,21 +287,21 @@ def _attn_inputs(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, 
     per row chunk of ``ctx.qkv_chunk`` (the workspace holds [normed chunk | QKV])."""
     cfg, ops = ctx.cfg, ctx.ops
     H, Qn, qs = cfg.hidden_size, cfg.qkv_size, cfg.q_size
-    nq, nkv, hd = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
+    nq, nkv = cfg.num_attention_heads, cfg.num_key_value_heads
     eps = cfg.rms_norm_eps
     T0 = x.shape[0]
     w, b = W["wqkv"], W.get("bqkv")
 
     def proj(h, wr, p, n_q, n_k, bias, out=None, rscale=None):
-        kw = {"rscale": rscale} if rscale is not None else {}     # (fused: HIP only)
-        if cfg.qk_norm:           # Qwen3: per-head RMSNorm on q / k before RoPE
-            return ops.qkv_norm_rope(h, wr, p, ctx.cos, ctx.sin, n_q, n_k, hd, W["qn"], W["kn"], eps,
-                                     bias=bias, out=out, **kw)
-        return ops.qkv_rope(h, wr, p, ctx.cos, ctx.sin, n_q, n_k, hd, bias=bias, out=out, **kw)
+        return _proj(ctx, W, h, wr, p, n_q, n_k, bias, out=out, rscale=rscale)
 
     def put(r, dst):
         if r.data_ptr() != dst.data_ptr():
             dst.copy_(r)
+
+    def scored_q():
+        q = q_scored if q_scored is not None else _scored_q(ctx, W, x, last_idx, last_pos)
+        ops.scatter_rows(q, last_idx, qkv[:, :qs])
 
     if ctx.fused_norm:
         ctx.phase((T0, Qn), (1, 2 * T0))
@@ -287,11 +314,7 @@ def _attn_inputs(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, 
             return qkv
         put(proj(x, w[qs:], pos, 0, nkv, b[qs:] if b is not None else None, out=qkv[:, qs:], rscale=rstd),
             qkv[:, qs:])
-        # Q of the scored rows: their raw rows gathered, scaled by their own statistic
-        xq = ops.gather_rows(x, last_idx)
-        q = proj(xq, w[:qs], last_pos, nq, 0, b[:qs] if b is not None else None,
-                 rscale=ops.row_rstd(xq, eps))
-        ops.scatter_rows(q, last_idx, qkv[:, :qs])
+        scored_q()
         return qkv
 
     step = balanced_step(T0, ctx.qkv_chunk) if ctx.qkv_chunk else T0
@@ -310,9 +333,7 @@ def _attn_inputs(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, 
             put(proj(h, w, pos[s:e], nq, nkv, b, out=qkv[s:e]), qkv[s:e])
         del h
     if prune:
-        hq = ops.rmsnorm(ops.gather_rows(x, last_idx), W["ln1"], eps)
-        q = proj(hq, w[:qs], last_pos, nq, 0, b[:qs] if b is not None else None)
-        ops.scatter_rows(q, last_idx, qkv[:, :qs])
+        scored_q()
     return qkv
 
 
@@ -362,16 +383,23 @@ def _attention_grouped(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Te
     (+ RoPE), attention with group-relative work items (every key a query sees is in its own
     prompt), O projection + residual into x's rows — the workspace holds one group's
     [normed | QKV] instead of the whole micro-batch's.  Same kernels per row as the whole-batch
-    path (the pruned last layer too: K/V of every row, Q of the scored rows), so the scores are
-    bitwise the same."""
+    path, so the scores are bitwise the same: the pruned last layer projects Q of every scored
+    row before the groups and O of every scored row after them, one GEMM each as in the
+    whole-batch path (a GEMM of a few hundred rows takes a skinny / split-K path chosen by its row
+    count; per-group launches changed the scores' last bits, scripts/bits_probe.py)."""
     cfg, ops = ctx.cfg, ctx.ops
     nq, nkv, hd = cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim
     work_items = getattr(ops, "uses_work_items", False)
-    pos = batch.device_tensors(x.device)["positions"]
-    outs = []
+    meta = batch.device_tensors(x.device)
+    pos = meta["positions"]
+    if prune:
+        q_all = _scored_q(ctx, W, x, meta["last_idx"], meta["last_pos"])
+        a_all = torch.empty_like(q_all)
     for g in batch.group_tensors(x.device, ctx.attn_rows):
         r0, r1 = g["r0"], g["r1"]
-        qkv = _attn_inputs(ctx, W, x[r0:r1], pos[r0:r1], g["last_local"], prune, g["last_pos"])
+        s0, s1 = g["s0"], g["s1"]
+        qkv = _attn_inputs(ctx, W, x[r0:r1], pos[r0:r1], g["last_local"], prune, g["last_pos"],
+                           q_scored=q_all[s0:s1] if prune else None)
         if prune:
             arg = g["work_last"] if work_items else g["last_segments"]
         else:
@@ -380,10 +408,8 @@ def _attention_grouped(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Te
         a = ops.attention(qkv, arg, nq, nkv, hd, q_block=batch.q_block, out=qkv[:, :cfg.q_size],
                           scale=cfg.attn_scale, **kw)
         if prune:
-            li = g["last_local"]
-            if li.numel():
-                outs.append(_resid(ctx, ops.gather_rows(a, li), W["wo"], ops.gather_rows(x[r0:r1], li),
-                                   bias=W.get("bo")))
+            if s1 > s0:
+                a_all[s0:s1].copy_(ops.gather_rows(a, g["last_local"]))
         else:
             xr = x[r0:r1]
             y = _resid(ctx, a, W["wo"], xr, bias=W.get("bo"))
@@ -391,7 +417,7 @@ def _attention_grouped(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Te
                 xr.copy_(y)
         del a, qkv
     if prune:
-        return outs[0] if len(outs) == 1 else torch.cat(outs)
+        return _resid(ctx, a_all, W["wo"], ops.gather_rows(x, meta["last_idx"]), bias=W.get("bo"))
     return x
 
 

@@ -10,8 +10,9 @@ HBM in use is
     without it) — the attention output overwrites Q in place — and [normed chunk | SwiGLU chunk]
     (``mlp_chunk`` rows) in the MLP phase
   + the hidden states alive: the engine's activation ring (engine.ActRing): 1 slot when the whole
-    call is one micro-batch (it never leaves HBM), else 2 — the micro-batch being computed and the
-    next one landing (the zigzag order's carries fit in the same two slots)
+    call is one micro-batch (it never leaves HBM), one per micro-batch when a token budget splits
+    a call whose states all fit (resident: none is parked), else 2 — the micro-batch being
+    computed and the next one landing (the zigzag order's carries fit in the same two slots)
   + the HIP context, code objects and allocator slack,
 
 so a VRAM cap is met by sizing ``token_budget``, ``qkv_chunk`` and ``mlp_chunk``:
@@ -52,6 +53,8 @@ CAP_MARGIN = 0.015
 # every 2 ms on the 70B headline (profiles/r4_vram); kept free under a cap, by the allocator limit
 # and by the plan
 RUNTIME_RESERVE = knobs.get_int("FLS_RUNTIME_RESERVE_MB") << 20
+# one activation-ring slot per micro-batch when they all fit (A/B knob)
+RESIDENT_STATES = knobs.get_int("FLS_RESIDENT_STATES") != 0
 
 
 def activation_bytes(cfg: ModelConfig, tokens: int, mlp_chunk: int, elem: int = 2, qkv_chunk: int = 0,
@@ -143,20 +146,24 @@ def plan_for_vram(cfg: ModelConfig, max_vram_bytes: int, lnps: int = 1, n_slots:
                   token_budget: int = 49152, mlp_chunk: int = 16384,
                   total_tokens: Optional[int] = None, max_prompt_rows: int = 0,
                   overhead: Optional[int] = None, weight_bytes: Optional[int] = None,
-                  fused_norm: bool = False) -> Tuple[int, int, int, int, int]:
-    """-> (token_budget, mlp_chunk, attn_rows, qkv_chunk, estimated peak bytes) for a call of
-    ``total_tokens`` packed tokens (None: unknown, assume several micro-batches) whose largest
-    prompt has ``max_prompt_rows`` rows.  ``overhead``: device memory held outside the plan
+                  fused_norm: bool = False) -> Tuple[int, int, int, int, int, bool]:
+    """-> (token_budget, mlp_chunk, attn_rows, qkv_chunk, estimated peak bytes, resident) for a
+    call of ``total_tokens`` packed tokens (None: unknown, assume several micro-batches) whose
+    largest prompt has ``max_prompt_rows`` rows.  ``overhead``: device memory held outside the plan
     (measured context + code objects; default DEVICE_OVERHEAD); ``weight_bytes``: the weight
-    buffers actually planned (default ``n_slots`` full-shard slots).
+    buffers actually planned (default ``n_slots`` full-shard slots).  ``resident``: every
+    micro-batch's hidden state keeps an activation-ring slot of its own for the whole pass (no
+    state is parked in host memory); else the ring has ``STATES`` slots.
 
     Preference, by measured cost on the 70B pass (one box, ``profiles/r3_vram``): one micro-batch
     when it fits with MLP chunks of ``MLP_CHUNK_TARGET`` rows (the hidden state never leaves HBM:
     no activation traffic over PCIe); else MLP chunks up to that size first (14,336 vs 10,752
-    rows: 2.1% of a pass, GEMM tile-round tails) and then the fewest micro-batches (each parks its
-    state over PCIe in the copy engine's shadow); then the largest MLP chunk, then the whole
-    micro-batch in one attention phase (prompt-aligned groups: ~1%) with the QKV projection in the
-    largest row chunks that fit, then the largest groups; raises if nothing fits."""
+    rows: 2.1% of a pass, GEMM tile-round tails), then every state resident (a call split by a
+    token budget whose states together fit: no PCIe round trip per micro-batch and layer, which
+    the piece pool's weight loads share; profiles/r5_spill), then the fewest micro-batches (each
+    parks its state over PCIe in the copy engine's shadow); then the largest MLP chunk, then the
+    whole micro-batch in one attention phase (prompt-aligned groups: ~1%) with the QKV projection
+    in the largest row chunks that fit, then the largest groups; raises if nothing fits."""
     from ..models.llama import balanced_step
     weights = weight_slot_bytes(cfg, lnps, n_slots) if weight_bytes is None else weight_bytes
     target = int(max_vram_bytes * (1.0 - CAP_MARGIN))
@@ -168,24 +175,29 @@ def plan_for_vram(cfg: ModelConfig, max_vram_bytes: int, lnps: int = 1, n_slots:
     for tb in (t for t in budgets if t <= token_budget):
         rows = min(tb, total_tokens) if total_tokens else tb
         n_mb = -(-total_tokens // tb) if total_tokens else 2
-        states = 1 if n_mb == 1 else STATES
-        for mc in (m for m in chunks if m <= min(mlp_chunk, tb)):
-            mce = balanced_step(rows, mc)
-            for ar in sorted({0, 32768, 24576, 16384, 12288, 8192, 4096}):
-                if ar and (ar >= rows or ar < max_prompt_rows):
-                    continue
-                qcs = (0, 16384, 12288, 9216, 8192, 6144, 4096, 3072, 2048) if ar == 0 and not fused_norm else (0,)
-                for qc in qcs:
-                    if qc and qc >= rows:
+        # live states: 1 (one micro-batch), every micro-batch's own (resident; known call only)
+        # or the ring's two
+        state_opts = (1,) if n_mb == 1 else ((n_mb, STATES) if total_tokens and n_mb > STATES and RESIDENT_STATES
+                                                   else (STATES,))
+        for states in state_opts:
+            resident = states == n_mb
+            for mc in (m for m in chunks if m <= min(mlp_chunk, tb)):
+                mce = balanced_step(rows, mc)
+                for ar in sorted({0, 32768, 24576, 16384, 12288, 8192, 4096}):
+                    if ar and (ar >= rows or ar < max_prompt_rows):
                         continue
-                    est = weights + over + activation_bytes(cfg, rows, mc, qkv_chunk=qc, states=states,
-                                                            attn_rows=ar, fused_norm=fused_norm)
-                    good = min(mce, MLP_CHUNK_TARGET, rows)
-                    key = (n_mb == 1 and mce >= min(MLP_CHUNK_TARGET, rows), good, -n_mb, mce, ar == 0,
-                           balanced_step(rows, qc) if qc else rows, ar)
-                    if est <= target and (best is None or key > best[5]):
-                        best = (tb, mc, ar, qc, est, key)
+                    qcs = (0, 16384, 12288, 9216, 8192, 6144, 4096, 3072, 2048) if ar == 0 and not fused_norm else (0,)
+                    for qc in qcs:
+                        if qc and qc >= rows:
+                            continue
+                        est = weights + over + activation_bytes(cfg, rows, mc, qkv_chunk=qc, states=states,
+                                                                attn_rows=ar, fused_norm=fused_norm)
+                        good = min(mce, MLP_CHUNK_TARGET, rows)
+                        key = (n_mb == 1 and mce >= min(MLP_CHUNK_TARGET, rows), good, resident, -n_mb, mce,
+                               ar == 0, balanced_step(rows, qc) if qc else rows, ar)
+                        if est <= target and (best is None or key > best[6]):
+                            best = (tb, mc, ar, qc, est, resident, key)
     if best is None:
         raise ValueError(f"--max_vram_gb {max_vram_bytes / 1e9:.1f}: the weight slots alone need "
                          f"{(weights + over) / 1e9:.1f} GB")
-    return best[:5]
+    return best[:6]

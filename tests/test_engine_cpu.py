@@ -777,3 +777,23 @@ def test_qwen2_moe_config_forms():
                 dict(d, model_type="qwen3_moe")):
         with pytest.raises(NotImplementedError):
             ModelConfig.from_dict(bad)
+
+
+def test_vram_plan_resident_states():
+    """plan_for_vram (Llama-2-70B, 6 GB, the piece pool's 3.12 GB of weight buffers): a 43k-token
+    call is one micro-batch; under a 16k token budget its three micro-batches' states together fit,
+    so every state keeps a ring slot (resident: nothing parked in host memory); 128 prompts'
+    172k tokens do not fit and go through the two-slot ring."""
+    from flexible_llm_sharding_amd.config import preset
+    from flexible_llm_sharding_amd.runtime.memplan import STATES, activation_bytes, plan_for_vram
+    cfg = preset("llama2-70b")
+    kw = dict(max_prompt_rows=1344, overhead=int(0.9e9), weight_bytes=int(3.12e9), fused_norm=True)
+    tb, mc, ar, qc, est, res = plan_for_vram(cfg, int(6e9), 1, 2, 49152, 16384, total_tokens=43008, **kw)
+    assert tb >= 43008 and res and est <= 6e9
+    tb, mc, ar, qc, est, res = plan_for_vram(cfg, int(6e9), 1, 2, 16384, 16384, total_tokens=43008, **kw)
+    assert tb == 16384 and res and est <= 6e9
+    # the estimate charges one state per micro-batch
+    assert est == int(3.12e9) + int(0.9e9) + activation_bytes(cfg, 16384, mc, states=3, fused_norm=True)
+    tb, mc, ar, qc, est, res = plan_for_vram(cfg, int(6e9), 1, 2, 49152, 16384, total_tokens=172032, **kw)
+    assert not res and est <= 6e9
+    assert est == int(3.12e9) + int(0.9e9) + activation_bytes(cfg, tb, mc, states=STATES, fused_norm=True)

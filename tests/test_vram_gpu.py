@@ -35,7 +35,8 @@ torch.cuda.empty_cache()
 write_synthetic_tokenizer({tok!r}, cfg.vocab_size)
 tok = load_tokenizer({tok!r})
 prompts = synthetic_prompts(12, 1024, 5, 64, cfg.vocab_size, seed=12)
-r = ShardedRunner(cfg, store, dev, tok, layer_num_per_shard=1, storage_location="cpu", max_vram_gb=cap or None)
+r = ShardedRunner(cfg, store, dev, tok, layer_num_per_shard=1, storage_location="cpu", max_vram_gb=cap or None,
+                  **({{"token_budget": {tb}}} if {tb} else {{}}))
 # hipMemGetInfo sampled by a thread every 2 ms through the passes (not only between calls)
 import threading
 peak, n = [0], [0]
@@ -57,7 +58,8 @@ stop.set()
 th.join()
 np.save({out!r}, np.concatenate([o.reshape(-1) for o in outs]))
 print(json.dumps({{"peak": peak[0], "samples": n[0], "plan": r.vram_plan, "mb": r.stats["micro_batches"],
-                  "act_h2d": r.stats["act_h2d_bytes"], "slots": r.prefetcher.n_slots}}))
+                  "act_h2d": r.stats["act_h2d_bytes"], "slots": r.prefetcher.n_slots,
+                  "ring": r._ring.n if r._ring is not None else 0}}))
 """
 
 
@@ -75,9 +77,9 @@ def _shared_bytes():
     return total - free
 
 
-def _run(tmp_path, cap, name, shared=0):
+def _run(tmp_path, cap, name, shared=0, tb=0):
     out = str(tmp_path / f"{name}.npy")
-    code = _WORKER.format(root=ROOT, cap=cap, tok=str(tmp_path / "tok"), out=out)
+    code = _WORKER.format(root=ROOT, cap=cap, tok=str(tmp_path / "tok"), out=out, tb=tb)
     # every runner owns its split-K scratch, reserved before its memory plan (charged to a cap):
     # capped and uncapped runs take the same GEMM paths, split-K small-M ones included
     env = dict(os.environ, FLS_VRAM_SHARED_GB=str(shared / 1e9))
@@ -98,4 +100,20 @@ def test_vram_cap_holds_and_scores_match(tmp_path):
     assert meta["samples"] > 20, meta
     assert meta["peak"] - shared <= cap * 1e9, (meta, shared)
     assert meta["slots"] == 2 and meta["plan"]["estimated_peak_bytes"] <= cap * 1e9
+    assert np.array_equal(free[1], got), (meta, free[0])
+
+
+def test_vram_cap_resident_states(tmp_path):
+    """A token budget that splits the call into 4 micro-batches whose hidden states together fit
+    under the cap: the plan keeps every state in an activation-ring slot of its own for the whole
+    pass (no activation traffic over PCIe), and the scores equal the uncapped run's of the same
+    split bitwise."""
+    shared = _shared_bytes()
+    free = _run(tmp_path, 0, "free_tb", shared, tb=4096)
+    meta, got = _run(tmp_path, 2.4, "cap_tb", shared, tb=4096)
+    assert meta["mb"] == 4 and free[0]["mb"] == 4, (meta, free[0])
+    assert meta["plan"]["resident_states"] is True and meta["ring"] == 4, meta
+    assert meta["act_h2d"] == 0, meta
+    assert free[0]["act_h2d"] > 0, free[0]          # uncapped: parked between layers
+    assert meta["peak"] - shared <= 2.4e9, (meta, shared)
     assert np.array_equal(free[1], got)
