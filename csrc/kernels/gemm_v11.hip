@@ -302,15 +302,15 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_v11(const half_t* __restrict__
   epilogue_quadrant<EPI, 8, true>(C, ldc, M, mrow, ncol, grp, acc, ep, mlo);
 }
 
-int g_v11 = 3;               // 0 off, 1 auto (large GEMMs, no extra row padding), 2 any valid shape (tests),
-                             // 3 auto by whole 256-CU tile rounds (v11_pays; default: at row counts that
-                             // are not whole rounds of either tile it picks the faster kernel more often
-                             // than 1, equal on whole-round shapes, profiles/r5_resident/gemm_m.log)
-// time of one 384 x 256 v11 tile in 256 x 256 v10 tiles, x 100 (3: v11_pays)
+int g_v11 = 1;               // 0 off, 1 auto (v11_pays), 2 any valid shape (tests)
+// time of one 384 x 256 v11 tile in 256 x 256 v10 tiles, x 100 (v11_pays)
 int g_v11_cost = 145;
 
 // Whole 256-CU tile rounds of each kernel at this shape, a v11 tile priced at g_v11_cost / 100
-// v10 tiles: a launch whose tile count is not a multiple of 256 pays its last round in full.  v10
+// v10 tiles: a launch whose tile count is not a multiple of 256 pays its last round in full.
+// (Replaces the rule "no more padded rows than v10", which sent 14,784-row micro-batches to v10's
+// 8 rounds instead of v11's 5 and 16,128 rows to v11's 6 instead of v10's 8:
+// profiles/r5_resident/gemm_m.log.)  v10
 // runs rows past its ROW_CHUNK (gemm.hip; default 16384) as evenly sized launches, each with its
 // own tail.
 bool v11_pays(int M, int N) {
@@ -346,16 +346,15 @@ int launch_v11(const half_t* A, const half_t* W, half_t* C, int M, int N, int K,
 
 }  // namespace
 
-// 0 = v10 everywhere, 1 = v11 where it pads no more rows than v10, 2 = v11 on every shape it
-// supports (tests: small and ragged shapes), 3 = v11 where it takes no more whole tile rounds
-// (default); returns the previous mode
+// 0 = v10 everywhere, 1 = v11 where it takes no more whole tile rounds (default), 2 = v11 on every
+// shape it supports (tests: small and ragged shapes); returns the previous mode
 extern "C" int fls_gemm_set_v11(int mode) {
   const int old = g_v11;
-  g_v11 = mode < 0 ? 0 : mode > 3 ? 3 : mode;
+  g_v11 = mode < 0 ? 0 : mode > 2 ? 2 : mode;
   return old;
 }
 
-// mode 3's price of a v11 tile in v10 tiles x 100 (<= 0: keep); returns the previous price
+// the auto mode's price of a v11 tile in v10 tiles x 100 (<= 0: keep); returns the previous price
 extern "C" int fls_gemm_set_v11_cost(int cost) {
   const int old = g_v11_cost;
   if (cost > 0) g_v11_cost = cost;
@@ -371,13 +370,9 @@ extern "C" int fls_gemm_v11_try(const void* A, const void* W, void* C, const voi
                                 const float* rscale, float alpha, fls_stream_t s) {
   using namespace v11;
   if (!g_v11 || M < TM || N % TN || K % TK || (K / TK) % 2 || lda % 8 || ldw % 8) return 0;
-  if (g_v11 == 1 || g_v11 == 3) {
-    // fills the chip (at least one tile per CU per launch)
-    if ((size_t)((M + TM - 1) / TM) * (N / TN) < 256) return 0;
-    // 1: computes no more rows than v10's 256-row tiles would (callers chunk rows in multiples
-    // of 768 = lcm(256, 384)); 3: takes no longer in whole tile rounds
-    if (g_v11 == 1 && (size_t)((M + TM - 1) / TM) * TM > (size_t)((M + 255) / 256) * 256) return 0;
-    if (g_v11 == 3 && !v11_pays(M, N)) return 0;
+  if (g_v11 == 1) {
+    // fills the chip (at least one tile per CU per launch) and takes no longer in whole tile rounds
+    if ((size_t)((M + TM - 1) / TM) * (N / TN) < 256 || !v11_pays(M, N)) return 0;
   }
   // 32-bit DMA offsets: every row of A (piece rows + lane rows + K) and of the (stacked) weight
   if ((size_t)M * lda * 2 >= (1ull << 32)) return 0;

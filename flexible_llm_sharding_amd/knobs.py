@@ -37,9 +37,8 @@ KNOBS: Dict[str, Tuple[str, str]] = {
     "FLS_RESIDENT_STATES": ("1", "0: under --max_vram_gb never plan one ring slot per micro-batch (states of a "
                                  "split call parked in host memory between layers even when they all fit)"),
     "FLS_SPLITK": ("1", "0: no split-K path for <= 512-row GEMMs"),
-    "FLS_GEMM_V11": ("3", "384x256 GEMM tile: 0 off (v10 everywhere), 1 where it pads no more rows than v10, "
-                          "2 every valid shape, 3 where it takes no more whole 256-CU tile rounds "
-                          "(a v11 tile priced at 1.45 v10 tiles)"),
+    "FLS_GEMM_V11": ("1", "384x256 GEMM tile: 0 off (v10 everywhere), 1 where it takes no more whole 256-CU "
+                          "tile rounds (a v11 tile priced at 1.45 v10 tiles), 2 every valid shape"),
     "FLS_SKINNY": ("1", "skinny-M GEMM for 17-192 rows: 0 off, 1 auto, 2 forced"),
     "FLS_ATTN_SPLIT": ("0", "split-KV slices of the range-2 attention kernel: 0 by grid size, 1 off, n"),
     "FLS_CHUNK_ALIGN": ("3072", "row multiple of the QKV / MLP chunks (3072 = 8 v11 tiles)"),

@@ -42,7 +42,7 @@ def main():
     cases = [("repeat", {}, None), ("attn_rows 12288", {"attn_rows": 12288}, None),
              ("mlp_chunk 9216", {"mlp_chunk": 9216}, None),
              ("attn_rows 12288 + mlp_chunk 9216", {"attn_rows": 12288, "mlp_chunk": 9216}, None),
-             ("v11 mode 0 (v10)", {}, 0), ("v11 mode 2", {}, 2), ("v11 mode 3", {}, 3)]
+             ("v11 mode 0 (v10)", {}, 0), ("v11 mode 2", {}, 2)]
     for name, ctx_kw, v11 in cases:
         saved = {a: getattr(r.ctx, a) for a in ctx_kw}
         for a, v in ctx_kw.items():

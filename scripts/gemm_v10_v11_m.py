@@ -1,11 +1,13 @@
 """v10 (256 x 256 tile) against v11 (384 x 256 tile) on the 70B projections at row counts that
 are not whole tile rounds (micro-batches of a token-budget split: 11 / 10 prompts of 1,344 rows),
-interleaved in one process, plus what the launcher's automatic choices take (``FLS_GEMM_V11=1``:
-no more rows than v10; ``3``: no more whole 256-CU tile rounds, a v11 tile priced at 1.45 v10 tiles).
+interleaved in one process, plus what the launcher's automatic choice takes (``FLS_GEMM_V11=1``: no
+more whole 256-CU tile rounds, a v11 tile priced at 1.45 v10 tiles).  (profiles/r5_resident/gemm_m.log
+was measured while the round rule was mode 3 and "auto" was the older "no more padded rows than
+v10" rule, since removed.)
 
     python scripts/gemm_v10_v11_m.py [--rows 14784,13440,...]
 
-One JSON line per (shape, rows): median ms of v10, v11, auto, rounds, and the tile rounds of each
+One JSON line per (shape, rows): median ms of v10, v11, auto, and the tile rounds of each
 (tiles / 256 CUs, rounded up).
 """
 import argparse
@@ -44,9 +46,9 @@ def main():
                     ops.gemm(x[:M], w, epi, out=out[:M], resid=out[:M])
                 else:
                     ops.gemm(x[:M], w, epi, out=out[:M])
-            times = {"v10": [], "v11": [], "auto": [], "rounds": []}
+            times = {"v10": [], "v11": [], "auto": []}
             for _ in range(a.reps):
-                for tag, mode in (("v10", 0), ("v11", 2), ("auto", 1), ("rounds", 3)):
+                for tag, mode in (("v10", 0), ("v11", 2), ("auto", 1)):
                     ops.k.fls_gemm_set_v11(mode)
                     run()
                     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
