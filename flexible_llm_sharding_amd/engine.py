@@ -81,6 +81,8 @@ class ShardedRunner:
                  max_vram_gb: Optional[float] = None, hbm_cache_gb: float = 0.0, rx_window: int = 2):
         self.cfg = cfg
         self.src = source
+        # layers read from their files every pass (no host-resident copy): host RAM is the limit
+        self._streamed_weights = hasattr(source, "stream_into") and source.host_buffer(cfg.layer_names()[0]) is None
         self.dev = torch.device(device)
         self.cuda = self.dev.type == "cuda"
         self.tok = tokenizer
@@ -531,7 +533,12 @@ class ShardedRunner:
     def _run_batches(self, tps, batches, t_start: float) -> List[Optional[np.ndarray]]:
         metas = [b.device_tensors(self.dev) for b in batches]   # all uploads before any compute
         store = self._get_store()
-        store.bytes_d2h = store.bytes_h2d = 0
+        store.bytes_d2h = store.bytes_h2d = store.buffer_waits = 0
+        # weights read from the layer files (the small-host-RAM mode): at most one pinned state
+        # buffer per micro-batch + ACT_BUFFER_SLACK, the host's run-ahead then waits for a reload
+        # to free one instead of growing the pool by its depth (128 prompts of 70B: 12 x 352 MB
+        # buffers for 8 micro-batches)
+        store.max_buffers = len(batches) + self.ACT_BUFFER_SLACK if self._streamed_weights else None
         pf = self.prefetcher
         # weight bytes of this call: counted from its early prefetch (or the previous call's
         # speculative one), not from the first acquire
@@ -843,6 +850,7 @@ class ShardedRunner:
             "act_stall_gpu_s": store.take_stall_seconds() if self.cuda else 0.0,
             "pinned_allocs": float(hostmem.alloc_calls - px.allocs0),
             "pinned_alloc_s": hostmem.alloc_seconds - px.alloc_s0,
+            "act_buffer_waits": float(store.buffer_waits),
         }
         self.stats.update(rx_stats)
         if self.verbose:
@@ -941,6 +949,7 @@ class ShardedRunner:
     # an activation consumed again within this many micro-batch computes stays in HBM
     # (zigzag: the boundary micro-batch is next, its neighbour 3 computes later)
     CARRY_WINDOW = 3
+    ACT_BUFFER_SLACK = knobs.get_int("FLS_ACT_BUFFER_SLACK")
 
     # ------------------------------------------------------ HIP graphs
     def _forward_all(self, meta: dict, batch: PackedBatch) -> torch.Tensor:

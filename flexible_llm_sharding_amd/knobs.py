@@ -16,7 +16,8 @@ KNOBS: Dict[str, Tuple[str, str]] = {
     "FLS_OFFLOAD_ARCH": ("gfx950", "hipcc --offload-arch of the kernel build (_native/build.py)"),
     "FLS_IO_THREADS": ("8", "threads of the native pread / pwrite pool (weights and activation spills)"),
     "FLS_STREAM_CHUNK_MB": ("64", "--weight_cache stream: pinned chunk size of the streamer ring (MB)"),
-    "FLS_STREAM_CHUNKS": ("4", "--weight_cache stream: chunks in the pinned ring"),
+    "FLS_STREAM_CHUNKS": ("6", "--weight_cache stream: chunks in the pinned ring (6 x 64 MB holds a whole 70B "
+                               "attention piece read ahead of its busy slot: profiles/r5_envelope)"),
     "FLS_O_DIRECT": ("0", "--weight_cache stream: read layer files with O_DIRECT (same as --o_direct)"),
     "FLS_RUNTIME_RESERVE_MB": ("192", "--max_vram_gb: device memory kept free for HIP-runtime transients "
                                       "(profiles/r4_vram)"),
@@ -34,6 +35,8 @@ KNOBS: Dict[str, Tuple[str, str]] = {
                                 "(0: shards only; 6: +7% at a 16k token budget, -10% at 128 prompts: "
                                 "profiles/r5_spill/runahead)"),
     # ---- A/B switches of measured choices (defaults are the measured winners)
+    "FLS_ACT_BUFFER_SLACK": ("1", "--weight_cache stream: pinned hidden-state buffers allowed beyond one per "
+                                  "micro-batch before the host waits for a reload to free one"),
     "FLS_RESIDENT_STATES": ("1", "0: under --max_vram_gb never plan one ring slot per micro-batch (states of a "
                                  "split call parked in host memory between layers even when they all fit)"),
     "FLS_SPLITK": ("1", "0: no split-K path for <= 512-row GEMMs"),

@@ -76,6 +76,12 @@ class ActivationStore:
         self._inflight: Dict[object, Tuple[Future, None]] = {}
         self._recycle: List[Tuple[torch.Tensor, torch.cuda.Event]] = []
         self._used_keys = set()           # pool buckets handed out since the last trim()
+        # pinned buffers per size bucket (in entries, pool and recycle list) and their bound:
+        # None = grow as needed; n = past n buffers of a size, a new one waits for the oldest
+        # host -> device copy still reading one (the engine bounds it when host RAM is the limit)
+        self._n_alloc: Dict[int, int] = defaultdict(int)
+        self.max_buffers: Optional[int] = None
+        self.buffer_waits = 0
         self.bytes_d2h = 0
         self.bytes_h2d = 0
         self._stall_ev: List[Tuple[torch.cuda.Event, torch.cuda.Event]] = []   # compute-stream waits on H2D
@@ -86,6 +92,7 @@ class ActivationStore:
 
     def _get_host(self, nbytes: int) -> torch.Tensor:
         key = (max(1, nbytes) + self.BUCKET - 1) // self.BUCKET * self.BUCKET
+        wait = None
         with self.lock:
             keep = []
             for h, ev in self._recycle:
@@ -98,6 +105,19 @@ class ActivationStore:
             lst = self._pool.get(key)
             if lst:
                 return lst.pop()
+            if self.max_buffers is not None and self._n_alloc[key] >= self.max_buffers:
+                for i, (h, ev) in enumerate(self._recycle):
+                    if h.numel() == key:
+                        wait = self._recycle.pop(i)
+                        break
+            if wait is None:
+                self._n_alloc[key] += 1
+        if wait is not None:
+            # the oldest pending reload of this size: its copy is already enqueued, so this wait
+            # needs nothing from the host (bounds the host's run-ahead by pinned memory instead)
+            wait[1].synchronize()
+            self.buffer_waits += 1
+            return wait[0]
         return hostmem.alloc_host(key, pinned=self.cuda)
 
     def pooled_bytes(self) -> int:
@@ -114,6 +134,7 @@ class ActivationStore:
             self._recycle = []
             for k in list(self._pool):
                 if k not in self._used_keys:
+                    self._n_alloc[k] -= len(self._pool[k])
                     del self._pool[k]
             self._used_keys = set()
 

@@ -797,3 +797,38 @@ def test_vram_plan_resident_states():
     tb, mc, ar, qc, est, res = plan_for_vram(cfg, int(6e9), 1, 2, 49152, 16384, total_tokens=172032, **kw)
     assert not res and est <= 6e9
     assert est == int(3.12e9) + int(0.9e9) + activation_bytes(cfg, tb, mc, states=STATES, fused_norm=True)
+
+
+def test_activation_store_buffer_bound():
+    """ActivationStore.max_buffers: past the bound a new pinned buffer of a size is not allocated;
+    the oldest pending reload of that size is waited for and its buffer reused (a reload whose
+    copy already completed goes back to the pool first).  No bound: the pool grows."""
+    from flexible_llm_sharding_amd.runtime.activations import ActivationStore
+
+    class Ev:
+        def __init__(self, done):
+            self.done, self.waited = done, False
+
+        def query(self):
+            return self.done
+
+        def synchronize(self):
+            self.waited = True
+            self.done = True
+
+    st = ActivationStore("cpu", "cpu")
+    st.max_buffers = 2
+    n = 3 << 20
+    a, b = st._get_host(n), st._get_host(n)
+    ea, eb = Ev(False), Ev(False)
+    st._recycle += [(a, ea), (b, eb)]          # both still being read by their reloads
+    c = st._get_host(n)                        # bound reached: waits for the oldest, reuses it
+    assert c is a and ea.waited and not eb.waited and st.buffer_waits == 1
+    eb.done = True
+    assert st._get_host(n) is b                # a completed reload's buffer comes from the pool
+    st._recycle.append((c, Ev(False)))
+    other = st._get_host(5 << 20)              # another size has its own count
+    assert other.numel() == 5 << 20 and st.buffer_waits == 1
+    st.max_buffers = None
+    assert st._get_host(n) is not c            # unbounded: a new buffer
+    st.trim()
