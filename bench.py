@@ -337,6 +337,13 @@ def main(argv=None):
         ckpt = a.ckpt_dir or f"/tmp/fls_bench_ckpt_{a.model}{'' if a.num_layers is None else f'-L{a.num_layers}'}_{a.ckpt_dtype}_u{a.unique_layers}"
         log(rank, f"[bench] per-layer checkpoint {ckpt} (unique decoder layers: {a.unique_layers}) ...")
         ensure_checkpoint(cfg, ckpt, a.ckpt_dtype, a.unique_layers, rank, comm, prog)
+        # writing the checkpoint freed GBs of host tensors into glibc's heap; hand them back so the
+        # run's resident set (the small-RAM envelope's measure) is the engine's own
+        try:
+            import ctypes
+            ctypes.CDLL("libc.so.6").malloc_trim(0)
+        except (OSError, AttributeError):
+            pass
         store = FileLayerSource(cfg, ckpt, names=[names[i] for i in mine], direct=a.o_direct)
         data_w = (f"random-init {a.model} weights as per-layer {a.ckpt_dtype} safetensors files "
                   f"({a.unique_layers} distinct decoder layers, the rest hard links), streamed from the files "
