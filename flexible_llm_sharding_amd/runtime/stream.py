@@ -13,7 +13,7 @@ Here the same small-RAM envelope costs no CPU work per pass:
   destination offset each (:class:`LayerPlan`);
 * the native streamer (``fls_streamer_*`` in ``csrc/runtime/runtime.cpp``)
   reads those ranges with a persistent ``pread`` pool (optionally
-  ``O_DIRECT``) into a small ring of pinned chunks (default 4 x 64 MiB) and
+  ``O_DIRECT``) into a small ring of pinned chunks (default 6 x 64 MiB) and
   DMAs every piece straight to its place in the HBM weight slot on the copy
   stream, so disk reads, PCIe DMA and compute of the previous shard overlap;
 * bf16 tensors are converted to fp16 in place in HBM by a HIP kernel on the
