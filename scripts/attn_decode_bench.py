@@ -67,7 +67,8 @@ def main():
         wt, w2t, wint = (torch.from_numpy(x).to(dev) for x in (w, w2, win))
         seg = torch.zeros(T, dtype=torch.int32, device=dev)
         kv_bytes = int(sum(int(x[4]) for x in w) + sum(int(x[1]) for x in w2)) * 2 * hd * 2 * (nkv if G == 1 else 1)
-        for qb in (8, 32):
+        for qb, ns in ((8, 0), (8, 2), (8, 3), (8, 4), (32, 0)):
+            ops.k.fls_attention_set_split(ns)
             li = [0]
 
             def run():
@@ -83,7 +84,8 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) * 1000 / a.iters
-            print(f"{layout:10s} q_block {qb:2d}: {us:7.1f} us/launch  K/V {kv_bytes / 1e6:.0f} MB  "
+            ops.k.fls_attention_set_split(0)
+            print(f"{layout:10s} q_block {qb:2d} split {ns or 'auto'}: {us:7.1f} us/launch  K/V {kv_bytes / 1e6:.0f} MB  "
                   f"{kv_bytes / us / 1e6:.2f} TB/s  (x80 layers: {us * 80 / 1000:.2f} ms/step)", flush=True)
         del caches
 
