@@ -253,7 +253,7 @@ class ShardedRunner:
         self._W_all: Dict[str, Dict[str, torch.Tensor]] = {}
         self._h2d0: Optional[int] = None     # prefetcher byte count at the start of the next call
         self._ring: Optional[ActRing] = None
-        self._resident_states = False      # _plan_call: every micro-batch keeps its own ring slot
+        self._resident_states = 0          # _plan_call: up to this many micro-batches keep a ring slot each
 
     # ----------------------------------------------------------- helpers
     def _fused_norm_planned(self) -> bool:
@@ -458,7 +458,9 @@ class ShardedRunner:
                                         fused_norm=self.ctx.fused_norm)
         self.token_budget, self.mlp_chunk = tb, mc
         self.ctx.mlp_chunk, self.ctx.attn_rows, self.ctx.qkv_chunk = mc, ar, qc
-        self._resident_states = res
+        # (the plan charged ceil(total / tb) states; a split that needs more micro-batches — whole
+        # prompts per micro-batch — parks through the two-slot ring instead)
+        self._resident_states = -(-max(1, total) // tb) if res else 0
         self.vram_plan.update({"token_budget": tb, "mlp_chunk": mc, "attn_rows": ar, "qkv_chunk": qc,
                                "estimated_peak_bytes": est, "resident_states": res,
                                "call_tokens": total})
@@ -577,7 +579,7 @@ class ShardedRunner:
             # (computing + landing; the zigzag carries fit) — exactly the plan's live states
             if self._ring is None:
                 self._ring = ActRing(self.dev, self.act_dtype, 1)
-            n_ring = 1 if len(batches) == 1 else len(batches) if self._resident_states else 2
+            n_ring = 1 if len(batches) == 1 else len(batches) if len(batches) <= self._resident_states else 2
             self._ring.resize(n_ring, max(b.num_tokens for b in batches) * self.cfg.hidden_size)
             px.ring = self._ring
         if self.my_shards and px.items:
