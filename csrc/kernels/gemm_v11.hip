@@ -354,6 +354,9 @@ extern "C" int fls_gemm_set_v11(int mode) {
   return old;
 }
 
+// 1 when the auto mode prices v11 at or below v10 for an M x N launch (host-side rule, tests)
+extern "C" int fls_gemm_v11_pays(int M, int N) { return v11_pays(M, N) ? 1 : 0; }
+
 // the auto mode's price of a v11 tile in v10 tiles x 100 (<= 0: keep); returns the previous price
 extern "C" int fls_gemm_set_v11_cost(int cost) {
   const int old = g_v11_cost;

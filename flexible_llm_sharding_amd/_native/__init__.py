@@ -63,7 +63,7 @@ class Piece(ctypes.Structure):
                 ("kind", ctypes.c_int32), ("pad", ctypes.c_int32)]
 
 
-KERNELS_ABI = 23   # bumped whenever a C signature in csrc/include/fls.h (or an accepted argument) changes
+KERNELS_ABI = 24   # bumped whenever a C signature in csrc/include/fls.h (or an accepted argument) changes
 
 
 def _load_kernels(path: str = _KERNELS):
@@ -99,6 +99,7 @@ def _load_kernels(path: str = _KERNELS):
     _bind(lib, "fls_gemm_set_order", c_int, c_int)
     _bind(lib, "fls_gemm_set_v11", c_int, c_int)
     _bind(lib, "fls_gemm_set_v11_cost", c_int, c_int)
+    _bind(lib, "fls_gemm_v11_pays", c_int, c_int, c_int)
     _bind(lib, "fls_gemm_set_skinny", c_int, c_int, c_int)
     _bind(lib, "fls_gemm_set_skinny_bn", c_int, c_int)
     _bind(lib, "fls_attention_set_hpb", c_int, c_int)

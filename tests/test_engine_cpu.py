@@ -832,3 +832,23 @@ def test_activation_store_buffer_bound():
     st.max_buffers = None
     assert st._get_host(n) is not c            # unbounded: a new buffer
     st.trim()
+
+
+def test_gemm_v11_round_rule():
+    """The GEMM launcher's v10 / v11 choice (csrc/kernels/gemm_v11.hip v11_pays, a host-side rule):
+    whole 256-CU tile rounds of each kernel, a 384 x 256 tile priced at 1.45 256 x 256 tiles
+    (profiles/r5_resident/gemm_m.log).  Needs the built kernel library (host code only)."""
+    from flexible_llm_sharding_amd import _native
+    try:
+        k = _native.kernels()
+    except Exception as e:  # noqa: BLE001 (library not built in this checkout)
+        pytest.skip(f"kernel library unavailable: {e}")
+    pays = k.fls_gemm_v11_pays
+    H, I2, Q = 8192, 2 * 28672, 10240
+    # the headline's whole-round shapes keep v11
+    for M, N in ((43008, Q), (43008, H), (15360, I2), (12288, I2), (15360, H), (12288, H)):
+        assert pays(M, N) == 1, (M, N)
+    # a 16k-budget micro-batch of 11 prompts: v11 5 rounds vs v10 8 (O / down)
+    assert pays(14784, H) == 1
+    # 16,128 rows: v11 needs 6 rounds, v10 8: 6 x 1.45 > 8
+    assert pays(16128, H) == 0
