@@ -1,6 +1,8 @@
 """Small-M projection GEMMs (generation steps, small calls): our kernels vs hipBLASLt at the 70B
 shapes, reported as TB/s of weight reads (each weight byte is read once per GEMM; at M <= a few
-hundred rows these GEMMs are bound by streaming the weights).
+hundred rows these GEMMs are bound by streaming the weights).  The skinny-M kernel forced
+(``fls_gemm_set_skinny(2)``) with each weight-block height is reported next to the automatic
+choice.
 
     python scripts/skinny_bench.py [--ms 16,64,160,256,512]
 """
@@ -50,12 +52,19 @@ def main():
             old = ops.k.fls_gemm_set_splitk(0)
             t_nosplit = timed(lambda: ops.gemm(x, w, epi, **kw))
             ops.k.fls_gemm_set_splitk(old)
+            forced = {}
+            for tag, bn in (("skinny", 0), ("skinny_bn128", 128), ("skinny_bn256", 256)):
+                old_m = ops.k.fls_gemm_set_skinny(2, 0)
+                old_bn = ops.k.fls_gemm_set_skinny_bn(bn)
+                forced[tag + "_us"] = round(timed(lambda: ops.gemm(x, w, epi, **kw)) * 1e6, 1)
+                ops.k.fls_gemm_set_skinny_bn(old_bn)
+                ops.k.fls_gemm_set_skinny(old_m, 0)
             t_lib = timed(lambda: torch.matmul(x, w.t()))
             wb = N * K * 2
             print(json.dumps({"op": name, "M": M, "N": N, "K": K, "ours_us": round(t_ours * 1e6, 1),
                               "ours_TBps": round(wb / t_ours / 1e12, 2),
                               "no_splitk_TBps": round(wb / t_nosplit / 1e12, 2), "hipblaslt_us": round(t_lib * 1e6, 1),
-                              "hipblaslt_TBps": round(wb / t_lib / 1e12, 2)}), flush=True)
+                              "hipblaslt_TBps": round(wb / t_lib / 1e12, 2), **forced}), flush=True)
         del w
         torch.cuda.empty_cache()
 
