@@ -126,6 +126,12 @@ def parse(argv=None):
     ap.add_argument("--hip-graphs", action="store_true", help="with --resident: whole-forward HIP graph replay")
     ap.add_argument("--no-prune-last", action="store_true",
                     help="compute every row in the last decoder layer (A/B of the scored-rows-only layer)")
+    ap.add_argument("--norm-fold", default="prefolded", choices=["on_landing", "prefolded"],
+                    help="--weights host: the RMSNorm weights folded into W_qkv / W_gate-up once, into the pinned "
+                         "host image, when it is built before timing (default: a load-time transform of the "
+                         "host cache, like the dtype cast), or as each layer lands in HBM on every pass (on the "
+                         "copy stream, from the checkpoint's own bytes; -1.0%%: profiles/r6_head).  --weights "
+                         "stream always folds on landing")
     ap.add_argument("--prefix-attention", default="bidirectional")
     ap.add_argument("--weights", default="host", choices=["host", "stream"])
     ap.add_argument("--ckpt-dir", default=None, help="--weights stream: layer-file directory (written if absent)")
@@ -308,10 +314,13 @@ def main(argv=None):
     from flexible_llm_sharding_amd.utils.tokenizer import clear_prefix_ids, load_tokenizer, write_synthetic_tokenizer
 
     from flexible_llm_sharding_amd import knobs
-    # the pinned host store holds the weights with their RMSNorms folded into the projections that
-    # read the normalised rows (done once on the GPU while generating them): the fused-norm GEMMs
-    # stream them as they are (HostStore.fold_norms)
-    fold = not a.cpu and knobs.get_int("FLS_QKV_FOLD") == 1
+    # the fused-norm GEMMs read W_qkv / W_gate-up with the RMSNorm weights folded in: once into the
+    # pinned host image as it is built, before timing (--norm-fold prefolded, the default:
+    # HostStore.fold_norms), or as each layer lands in HBM on every pass, on the copy stream, from the
+    # checkpoint's own bytes (--norm-fold on_landing; the layer-file path always does this).  The JSON
+    # config says which ("norm_fold")
+    fused = not a.cpu and knobs.get_int("FLS_QKV_FOLD") == 1
+    fold = fused and a.norm_fold == "prefolded" and a.weights == "host"
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
@@ -497,6 +506,11 @@ def main(argv=None):
                    "weights": a.weights, "resident": a.resident, "hip_graphs": bool(runner.hip_graphs),
                    "token_budget": runner.token_budget, "mlp_chunk": runner.mlp_chunk,
                    "weight_slots": runner.prefetcher.n_slots, "hbm_cache_gb": a.hbm_cache_gb,
+                   # where the RMSNorm weights meet W_qkv / W_gate-up ("none": the unfused CPU path)
+                   "norm_fold": ("prefolded" if fold else "on_landing") if fused else "none",
+                   # the last decoder layer computes only the scored rows (K/V for every token);
+                   # tokens/s counts every token either way (--no-prune-last: A/B)
+                   "prune_last_layer": not a.no_prune_last,
                    "max_vram_gb": a.max_vram_gb, "cap_fallback": cap_note},
     }
     if rank == 0:

@@ -72,8 +72,14 @@ enum { FLS_EPI_NONE = 0, FLS_EPI_RESID = 1, FLS_EPI_SWIGLU = 2, FLS_EPI_ROPE = 3
 int fls_gemm(const void* A, const void* W, void* C, const void* R, int M, int N, int K,
              int lda, int ldw, int ldc, int ldr, int epi, const int* pos, const float* cos_t,
              const float* sin_t, int rope_cols, int head_dim, const void* bias, const float* rscale,
-             float alpha, void* ws, uint64_t ws_bytes,
+             float alpha, float* ss, int ss_ld, void* ws, uint64_t ws_bytes,
              fls_stream_t s);   // ws: device scratch for the small-M split-K path (may be null)
+// ss (RESID only, may be null): ss[m * ss_ld + j] = sum of the squares of the fp16 outputs of row m in
+// columns [128 j, 128 j + 128) -- the row statistic of the next norm-folded projection without a
+// pass over the hidden state (fls_rstd_from_ss)
+// rstd[r] = rsqrt(sum_j ss[r * ss_ld + j] / H + eps) for j < nparts, summed in a fixed order
+int fls_rstd_from_ss(const float* ss, int ss_ld, int nparts, int rows, int H, float eps, float* rstd,
+                     fls_stream_t s);
 // out[r] = first index of the maximum of row r of non-negative fp16 values (greedy decoding)
 int fls_argmax_rows(const void* x, int ld, int rows, int V, int* out, fls_stream_t s);
 // rstd[r] = rsqrt(mean(x[row]^2) + eps) in fp32, row = row_idx ? row_idx[r] : r (fused RMSNorm:
@@ -87,8 +93,7 @@ int fls_fold_norm(void* w, int ldw, int N, int K, const void* gamma, fls_stream_
 int fls_copy_rows(const void* x, int ldx, const int* src_idx, void* y, int ldy, const int* dst_idx, int rows, int H,
                   fls_stream_t s);
 int fls_gemm_set_splitk(int on);
-int fls_gemm_set_gu_split(int p);
-int fls_gemm_set_row_chunk(int rows);   // rows per main-path GEMM launch (default 16384; 0 = unlimited)   // SwiGLU GEMM in p column launches (A/B; default 1)
+int fls_gemm_set_row_chunk(int rows);   // rows per main-path GEMM launch (default 16384; 0 = unlimited)
 // mixture-of-experts FFN (csrc/kernels/moe.hip): routing, stable expert sort, grouped v10 GEMM
 // (every expert of a layer in one launch, optional row gather), fp16-ordered weighted combine
 int fls_moe_route(const void* logits, int ldl, int T, int E, int k, int norm, int round16, int* ids, float* w,

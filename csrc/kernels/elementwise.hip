@@ -135,6 +135,19 @@ __global__ __launch_bounds__(256) void row_rstd_kernel(const half_t* __restrict_
   if (lane == 0) rstd[r] = rsqrtf(tot / (float)H + eps);
 }
 
+// rstd[r] = rsqrt(sum of the row's partial sums of squares / H + eps): one wave per row, lane j
+// holds parts j, j + 64, ... (fixed order), then a fixed butterfly (deterministic)
+__global__ __launch_bounds__(256) void rstd_from_ss_kernel(const float* __restrict__ ss, int ss_ld, int nparts,
+                                                           int rows, int H, float eps, float* __restrict__ rstd) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;                            // wave-uniform
+  const int lane = threadIdx.x & 63;
+  float v = 0.f;
+  for (int j = lane; j < nparts; j += 64) v += ss[(size_t)r * ss_ld + j];
+  v = warp_sum(v);
+  if (lane == 0) rstd[r] = rsqrtf(v / (float)H + eps);
+}
+
 // W[n, k] *= gamma[k] (fp16 result), 8 columns per thread
 __global__ __launch_bounds__(256) void fold_norm_kernel(half_t* __restrict__ w, int ldw, int N, int K,
                                                       const half_t* __restrict__ gamma) {
@@ -473,6 +486,16 @@ extern "C" int fls_row_rstd(const void* x, int ldx, const int* row_idx, int rows
   if (H % 8 || ldx % 8 || ((uintptr_t)x & 15)) return -2;
   hipLaunchKernelGGL(row_rstd_kernel, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)s, (const half_t*)x, ldx,
                      row_idx, rows, H, eps, rstd);
+  FLS_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int fls_rstd_from_ss(const float* ss, int ss_ld, int nparts, int rows, int H, float eps, float* rstd,
+                                fls_stream_t s) {
+  if (rows <= 0) return 0;
+  if (nparts <= 0 || ss_ld < nparts) return -2;
+  hipLaunchKernelGGL(rstd_from_ss_kernel, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)s, ss, ss_ld, nparts, rows,
+                     H, eps, rstd);
   FLS_CHECK_LAUNCH();
   return 0;
 }

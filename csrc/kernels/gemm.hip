@@ -267,7 +267,6 @@ void launch_main(int tiles, const half_t* A, const half_t* W, half_t* C, int M, 
 // with the partner column d + hd/2 of each head).
 constexpr int SPLITK_MAX_M = 512;
 int g_splitk = 1;            // split-K path for small M on (fls_gemm_set_splitk)
-int g_gu_split = 1;          // SwiGLU GEMM in this many column launches (fls_gemm_set_gu_split; A/B)
 int ROW_CHUNK = 16384;       // main-path launches cover at most this many rows (fls_gemm_set_row_chunk)
 
 template <int EPI>
@@ -340,6 +339,26 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 
 #include "gemm_skinny.h"
 
+// ss[m * ss_ld + j] = sum over columns [128 j, 128 j + 128) of C[m, :]^2 (fp32 of the fp16 values):
+// the per-row partials of the v10 / v11 residual epilogue (Epi::ss) for the GEMM paths whose own
+// epilogue does not write them (skinny, split-K, mid-M, generic: small M).  One wave per (row, part).
+__global__ __launch_bounds__(256) void ss_partials_kernel(const half_t* __restrict__ C, int ldc, int M, int nparts,
+                                                          float* __restrict__ ss, int ss_ld) {
+  const int w = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (w >= M * nparts) return;                      // wave-uniform
+  const int m = w / nparts, j = w % nparts;
+  const half_t* p = C + (size_t)m * ldc + j * 128 + lane * 2;
+  float sq = (float)p[0] * (float)p[0] + (float)p[1] * (float)p[1];
+  sq = warp_sum(sq);
+  if (lane == 0) ss[(size_t)m * ss_ld + j] = sq;
+}
+
+void ss_partials(const half_t* C, int ldc, int M, int N, const Epi& ep, hipStream_t s) {
+  if (!ep.ss || M <= 0) return;
+  const int waves = M * (N / 128);
+  hipLaunchKernelGGL(ss_partials_kernel, dim3((waves + 3) / 4), dim3(256), 0, s, C, ldc, M, N / 128, ep.ss, ep.ss_ld);
+}
+
 // -> slices per tile (0: split-K not applicable / no room in the workspace)
 int splitk_slices(int M, int N, int K, size_t tiles, size_t ws_bytes) {
   if (tiles >= 128) return 0;
@@ -377,6 +396,7 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
                         (EPI != FLS_EPI_RESID || (ep.ldr % 4 == 0 && ((uintptr_t)ep.R & 7) == 0));
   {
     const int rc = try_skinny<EPI>(A, W, C, M, N, K, lda, ldw, ldc, ep, s, ws, ws_bytes);
+    if (rc > 0) ss_partials(C, ldc, M, N, ep, s);
     if (rc) return rc > 0 ? 0 : rc;
   }
   const int S = split_ok ? splitk_slices(M, N, K, tiles256, ws_bytes) : 0;
@@ -401,9 +421,11 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
     hipLaunchKernelGGL(splitk_reduce_kernel<EPI>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, part, S,
                        e.part_stride, M, N, C, ldc, e);
     FLS_CHECK_LAUNCH();
+    ss_partials(C, ldc, M, N, ep, s);
+    FLS_CHECK_LAUNCH();
     return 0;
   }
-  if (mid_ok && (!main_ok || g_mid == 2 || (g_mid && (tiles256 < 128 || (M <= 64 && tiles256 < 512))))) {
+  if (mid_ok && (!main_ok || (g_mid && (tiles256 < 128 || (M <= 64 && tiles256 < 512))))) {
     static bool attr_mid = false;
     if (!attr_mid) {
       (void)hipFuncSetAttribute((const void*)gemm_nt_mid<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -414,11 +436,15 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
     hipLaunchKernelGGL(gemm_nt_mid<EPI>, dim3(blocks), dim3(mid::NTm), mid::NSTAGE * mid::STAGE, s, A, W, C, M, N,
                        K, lda, ldw, ldc, ep);
     FLS_CHECK_LAUNCH();
+    ss_partials(C, ldc, M, N, ep, s);
+    FLS_CHECK_LAUNCH();
     return 0;
   }
   if (!main_ok) {
     dim3 grid((M + 31) / 32, (N + 255) / 256);
     hipLaunchKernelGGL(gemm_nt_generic<EPI>, grid, dim3(256), 0, s, A, W, C, M, N, K, lda, ldw, ldc, ep);
+    FLS_CHECK_LAUNCH();
+    ss_partials(C, ldc, M, N, ep, s);
     FLS_CHECK_LAUNCH();
     return 0;
   }
@@ -434,6 +460,7 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
       Epi e = ep;
       if (e.pos) e.pos += r0;
       if (e.R) e.R += (size_t)r0 * e.ldr;
+      if (e.ss) e.ss += (size_t)r0 * e.ss_ld;
       const int rc = launch<EPI>(A + (size_t)r0 * lda, W, C + (size_t)r0 * ldc, min(step, M - r0), N, K, lda, ldw,
                                  ldc, e, s, ws, ws_bytes);
       if (rc) return rc;
@@ -456,7 +483,7 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
 
 }  // namespace
 
-extern "C" int fls_kernels_version(void) { return 24; }
+extern "C" int fls_kernels_version(void) { return 25; }
 
 // tile order: 0 = by shape (default); g > 0: groups of g M tiles; g < 0: groups of -g N tiles (A/B, tests)
 extern "C" int fls_gemm_set_order(int order) {
@@ -495,17 +522,10 @@ extern "C" int fls_gemm_set_row_chunk(int rows) {
   return old;
 }
 
-// SwiGLU GEMM as P launches over the intermediate columns (1 = one launch, default)
-extern "C" int fls_gemm_set_gu_split(int p) {
-  const int old = g_gu_split;
-  g_gu_split = p > 0 ? p : 1;
-  return old;
-}
-
 // mid-M kernel for small grids on (1, default) or off (0; tests)
-extern "C" int fls_gemm_set_mid(int on) {   // 0 off, 1 auto, 2 forced wherever it applies (A/B)
+extern "C" int fls_gemm_set_mid(int on) {
   const int old = g_mid;
-  g_mid = on < 0 ? 0 : on > 2 ? 2 : on;
+  g_mid = on ? 1 : 0;
   return old;
 }
 
@@ -513,26 +533,30 @@ extern "C" int fls_gemm_set_mid(int on) {   // 0 off, 1 auto, 2 forced wherever 
 extern "C" int fls_gemm_v11_try(const void* A, const void* W, void* C, const void* R, int M, int N, int K, int lda,
                                 int ldw, int ldc, int ldr, int epi, const int* pos, const float* cos_t,
                                 const float* sin_t, int rope_cols, int head_dim, const void* bias,
-                                const float* rscale, float alpha, fls_stream_t s);
+                                const float* rscale, float alpha, float* ss, int ss_ld, fls_stream_t s);
 
 extern "C" int fls_gemm(const void* A, const void* W, void* C, const void* R, int M, int N, int K, int lda, int ldw,
                         int ldc, int ldr, int epi, const int* pos, const float* cos_t, const float* sin_t,
-                        int rope_cols, int head_dim, const void* bias, const float* rscale, float alpha, void* ws,
-                        uint64_t ws_bytes, fls_stream_t s) {
+                        int rope_cols, int head_dim, const void* bias, const float* rscale, float alpha, float* ss,
+                        int ss_ld, void* ws, uint64_t ws_bytes, fls_stream_t s) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
+  // row partial sums of squares: residual GEMMs only, one per 128 output columns
+  if (ss && (epi != FLS_EPI_RESID || N % 128 || ss_ld < N / 128)) return -7;
   if (bias && epi == FLS_EPI_SWIGLU) return -4;
   if ((epi == FLS_EPI_SWIGLU || epi == FLS_EPI_ROPE) && (N % 32)) return -2;
   if (epi == FLS_EPI_ROPE && ((head_dim != 64 && head_dim != 128) || rope_cols % head_dim || N % head_dim))
     return -3;
-  if (g_gu_split <= 1 || epi != FLS_EPI_SWIGLU) {
+  {
     const int rc = fls_gemm_v11_try(A, W, C, R, M, N, K, lda, ldw, ldc, ldr, epi, pos, cos_t, sin_t, rope_cols,
-                                    head_dim, bias, rscale, alpha, s);
+                                    head_dim, bias, rscale, alpha, ss, ss_ld, s);
     if (rc) return rc > 0 ? 0 : rc;
   }
   Epi ep{(const half_t*)R, ldr, pos, cos_t, sin_t, rope_cols, head_dim, (const half_t*)bias, N / 2, 0,
          nullptr, nullptr, nullptr, 0, 0};
   ep.rs = rscale;
   ep.alpha = alpha;
+  ep.ss = ss;
+  ep.ss_ld = ss_ld;
   auto a = (const half_t*)A;
   auto w = (const half_t*)W;
   auto c = (half_t*)C;
@@ -540,20 +564,7 @@ extern "C" int fls_gemm(const void* A, const void* W, void* C, const void* R, in
   switch (epi) {
     case FLS_EPI_NONE: return launch<FLS_EPI_NONE>(a, w, c, M, N, K, lda, ldw, ldc, ep, st, ws, ws_bytes);
     case FLS_EPI_RESID: return launch<FLS_EPI_RESID>(a, w, c, M, N, K, lda, ldw, ldc, ep, st, ws, ws_bytes);
-    case FLS_EPI_SWIGLU: {
-      // optional: the intermediate columns in g_gu_split launches (gate rows [j I/P, (j+1) I/P) and
-      // the matching up rows; gu_rows stays I), a smaller N-tile grid per launch (A/B knob)
-      const int I = N / 2, P = g_gu_split;
-      if (P > 1 && I % (P * BN / 2) == 0 && M > SPLITK_MAX_M) {
-        for (int j = 0; j < P; ++j) {
-          const int rc = launch<FLS_EPI_SWIGLU>(a, w + (size_t)j * (I / P) * ldw, c + (size_t)j * (I / P), M, N / P, K,
-                                                lda, ldw, ldc, ep, st, ws, ws_bytes);
-          if (rc) return rc;
-        }
-        return 0;
-      }
-      return launch<FLS_EPI_SWIGLU>(a, w, c, M, N, K, lda, ldw, ldc, ep, st, ws, ws_bytes);
-    }
+    case FLS_EPI_SWIGLU: return launch<FLS_EPI_SWIGLU>(a, w, c, M, N, K, lda, ldw, ldc, ep, st, ws, ws_bytes);
     case FLS_EPI_ROPE:
       return head_dim == 128 ? launch<FLS_EPI_ROPE>(a, w, c, M, N, K, lda, ldw, ldc, ep, st, ws, ws_bytes)
                              : launch<EPI_ROPE64>(a, w, c, M, N, K, lda, ldw, ldc, ep, st, ws, ws_bytes);

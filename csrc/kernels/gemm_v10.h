@@ -50,7 +50,21 @@ struct Epi {
   const float* rs = nullptr;
   // scale of (product + bias) before the residual add (Granite's residual_multiplier)
   float alpha = 1.f;
+  // optional (RESID): per-row partial sums of squares of the fp16 output, one fp32 per 128 output
+  // columns: ss[m * ss_ld + n / 128].  The next fused-norm GEMM's row statistic is their sum
+  // (fls_rstd_from_ss) -- the separate pass over the hidden state (row_rstd) is not needed
+  float* ss = nullptr;
+  int ss_ld = 0;
 };
+
+// sum of v over the 4 lanes of one output row (lanes l, l^16, l^32, l^48: one 16-column group
+// each); every lane gets the same value, in a fixed order (deterministic).  All lanes must run it.
+__device__ __forceinline__ float row_sum_4groups(float v) {
+  const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
 
 // the per-row scale of row m (1 without one: x * 1.0f is exact, so the unscaled path is unchanged)
 __device__ __forceinline__ float row_scale(const Epi& ep, int m) { return ep.rs ? ep.rs[m] : 1.f; }
@@ -303,6 +317,8 @@ __device__ __forceinline__ void epilogue_quadrant(half_t* __restrict__ C, int ld
           for (int p = 0; p < 4; ++p) rw[sl][p] = *(const uint4*)(rp + p * 32);
         }
       };
+      // RESID with ep.ss: this wave's 128 columns of each row -> one partial sum of squares
+      float* const ssp = EPI == FLS_EPI_RESID ? ep.ss : nullptr;
       auto body = [&](auto has_bias) {
         load(0, 0);
 #pragma unroll
@@ -312,6 +328,7 @@ __device__ __forceinline__ void epilogue_quadrant(half_t* __restrict__ C, int ld
           asm volatile("" ::: "memory");
           const int m = mrow0 + u * 16;
           const float s = ep.rs ? ep.rs[min(m, M - 1)] : 1.f;
+          float sq = 0.f;
 #pragma unroll
           for (int p = 0; p < 4; ++p) {
             floatx4 a = acc[u][2 * p] * s, b = acc[u][2 * p + 1] * s;
@@ -328,8 +345,20 @@ __device__ __forceinline__ void epilogue_quadrant(half_t* __restrict__ C, int ld
             half4 oa, ob;
 #pragma unroll
             for (int r = 0; r < 4; ++r) { oa[r] = (half_t)a[r]; ob[r] = (half_t)b[r]; }
+            if constexpr (EPI == FLS_EPI_RESID) {
+              if (ssp) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) sq += (float)oa[r] * (float)oa[r] + (float)ob[r] * (float)ob[r];
+              }
+            }
             const uint4 v = wide_pair(oa, ob);
             if (m < M && (!LO || m >= mlo)) *(uint4*)(C + (size_t)m * ldc + ncol0 + p * 32 + woff) = v;
+          }
+          if constexpr (EPI == FLS_EPI_RESID) {
+            if (ssp) {                                 // wave-uniform
+              sq = row_sum_4groups(sq);
+              if (grp == 0 && m < M && (!LO || m >= mlo)) ssp[(size_t)m * ep.ss_ld + (ncol0 >> 7)] = sq;
+            }
           }
         }
       };

@@ -370,7 +370,7 @@ extern "C" int fls_gemm_set_v11_cost(int cost) {
 extern "C" int fls_gemm_v11_try(const void* A, const void* W, void* C, const void* R, int M, int N, int K, int lda,
                                 int ldw, int ldc, int ldr, int epi, const int* pos, const float* cos_t,
                                 const float* sin_t, int rope_cols, int head_dim, const void* bias,
-                                const float* rscale, float alpha, fls_stream_t s) {
+                                const float* rscale, float alpha, float* ss, int ss_ld, fls_stream_t s) {
   using namespace v11;
   if (!g_v11 || M < TM || N % TN || K % TK || (K / TK) % 2 || lda % 8 || ldw % 8) return 0;
   if (g_v11 == 1) {
@@ -388,6 +388,8 @@ extern "C" int fls_gemm_v11_try(const void* A, const void* W, void* C, const voi
          nullptr, nullptr, nullptr, 0, 0};
   ep.rs = rscale;
   ep.alpha = alpha;
+  ep.ss = ss;
+  ep.ss_ld = ss_ld;
   auto a = (const half_t*)A;
   auto w = (const half_t*)W;
   auto c = (half_t*)C;

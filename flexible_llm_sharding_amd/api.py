@@ -259,7 +259,7 @@ def generation_loop(args, runner, comm: Comm, tok, original_prompts: Sequence, s
     step_scores: List[List[np.ndarray]] = []
     step_tokens: List[List[np.ndarray]] = []
     # host-side profile of chosen steps (FLS_PROFILE_GEN_STEPS="2,3" -> cProfile stats in
-    # FLS_PROFILE_OUT.<step>): where a generation step's host time goes
+    # gen_profile.<step>): where a generation step's host time goes
     prof_steps = {int(s) for s in knobs.get("FLS_PROFILE_GEN_STEPS").split(",") if s.strip()}
     # one runner call per step on one rank: each decode-graphed step may enqueue the next one behind
     # itself (ShardedRunner._launch_spec) while the host decodes and re-tokenizes
@@ -281,7 +281,7 @@ def generation_loop(args, runner, comm: Comm, tok, original_prompts: Sequence, s
             dev_tok = None
         if prof is not None:
             prof.disable()
-            prof.dump_stats(f"{knobs.get('FLS_PROFILE_OUT')}.{i_new}")
+            prof.dump_stats(f"gen_profile.{i_new}")
         if comm.rank == 0:
             toks = dev_tok if dev_tok is not None else [greedy_tokens(o) for o in outputs]
             if i_new == 0:

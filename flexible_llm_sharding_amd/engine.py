@@ -517,7 +517,6 @@ class ShardedRunner:
             self.carry = {}            # micro-batch -> device activation kept across a shard boundary
             self.sends = []            # (tensor, work) of outputs in flight to another rank
             self.shard_ev: List = []   # end-of-shard events on the compute stream (host run-ahead bound)
-            self.item_ev: List = []    # end-of-item events (the same bound in micro-batch computes)
             self.allocs0, self.alloc_s0 = hostmem.alloc_calls, hostmem.alloc_seconds
             self.flops = 0.0
             self.flops_of = {}              # (micro-batch, pruned layer) -> FLOPs of one decoder layer
@@ -615,8 +614,6 @@ class ShardedRunner:
             if px.ck is not None and self._ckpt_due(k):
                 px.ck.save_state(self._ckpt_key(k), b, state)     # a shard's outputs
             self._emit(px, k, b, state, from_rx=False)
-            if self.RUNAHEAD_ITEMS:
-                self._throttle(px.item_ev, self.RUNAHEAD_ITEMS)
 
     def _exec_pipeline(self, px: "_Pass") -> None:
         """Model parallel: this rank's items in program order; inputs from the previous stage
@@ -886,15 +883,12 @@ class ShardedRunner:
         this call's last layers (profiles/r2_slots_own, profiles/r2_slots7b).  With 2 slots the
         only free slot at the end of a call is the last layer's; measured neutral
         (profiles/r1_host_path, profiles/r2_chunk_spec), off.
-        ``FLS_SPECULATIVE_PREFETCH=0/1`` overrides.  Never when resuming (the next call may start
+        Never when resuming (the next call may start
         elsewhere), resident (nothing to load), model parallel, or with the data-parallel
         all-gather prefetcher (no collectives left in flight after a call)."""
         from .parallel.data_parallel import AllGatherPrefetcher
         pf = self.prefetcher
-        env = knobs.get("FLS_SPECULATIVE_PREFETCH") or None
-        if env is not None and env != "1":
-            return False
-        if env is None and pf.n_slots < 3:
+        if pf.n_slots < 3:
             return False
         return (self.cuda and not self.resume_dir and not pf.resident and not self.hip_graphs
                 and not (self.plan.mode == "mp" and self.comm.active)
@@ -942,16 +936,12 @@ class ShardedRunner:
             shard_ev.pop(0).synchronize()
 
     RUNAHEAD_SHARDS = 2
-    # ... and optionally to this many (shard, micro-batch) computes (0: off, the default).  Measured
-    # both ways (profiles/r5_spill/runahead): 6 speeds up a 16k-budget pass (+7%) and the streamed
-    # 128-prompt envelope (+16%, 1.3 GB less pinned RAM) but slows the 128-prompt pass from host RAM
-    # by 10-13% (its H2D reloads then wait ~18 ms in front of most micro-batches); not understood, so
-    # it stays a deployment knob
-    RUNAHEAD_ITEMS = knobs.get_int("FLS_RUNAHEAD_ITEMS")
     # an activation consumed again within this many micro-batch computes stays in HBM
     # (zigzag: the boundary micro-batch is next, its neighbour 3 computes later)
     CARRY_WINDOW = 3
-    ACT_BUFFER_SLACK = knobs.get_int("FLS_ACT_BUFFER_SLACK")
+    # --weight_cache stream: pinned hidden-state buffers allowed beyond one per micro-batch before
+    # the host waits for a reload to free one (profiles/r5_envelope)
+    ACT_BUFFER_SLACK = 1
 
     # ------------------------------------------------------ HIP graphs
     def _forward_all(self, meta: dict, batch: PackedBatch) -> torch.Tensor:
@@ -987,6 +977,8 @@ class ShardedRunner:
         if entry is not None:
             if getattr(self, "_decode_graphs", None) is None:
                 self._decode_graphs = DecodeGraphs(self.dev, self._forward_all)
+                if self.prefix_cache is not None:
+                    self.prefix_cache.on_evict.append(self._decode_graphs.forget)
             graphs = self._decode_graphs
             run = lambda b: graphs.run(b, entry)          # noqa: E731
         else:

@@ -26,28 +26,12 @@ KNOBS: Dict[str, Tuple[str, str]] = {
     # ---- observability
     "FLS_TRACE": ("0", "roctx ranges around load / compute / store / comm (same as --profile)"),
     "FLS_PROFILE_GEN_STEPS": ("", "comma-separated generation steps to run under cProfile"),
-    "FLS_PROFILE_OUT": ("gen_profile", "cProfile output prefix of FLS_PROFILE_GEN_STEPS"),
     # ---- tests / fault injection
     "FLS_FAULT": ("", "'rank:shard': raise on that rank when it enters that local shard"),
     "FLS_PIECE_POOL": ("1", "0: whole-layer weight slots under --max_vram_gb instead of the "
                             "attention / MLP piece pool (tests: both must give the same scores)"),
-    "FLS_RUNAHEAD_ITEMS": ("0", "host run-ahead bound in (shard, micro-batch) computes on top of the 2-shard bound "
-                                "(0: shards only; 6: +7% at a 16k token budget, -10% at 128 prompts: "
-                                "profiles/r5_spill/runahead)"),
     # ---- A/B switches of measured choices (defaults are the measured winners)
-    "FLS_ACT_BUFFER_SLACK": ("1", "--weight_cache stream: pinned hidden-state buffers allowed beyond one per "
-                                  "micro-batch before the host waits for a reload to free one"),
-    "FLS_RESIDENT_STATES": ("1", "0: under --max_vram_gb never plan one ring slot per micro-batch (states of a "
-                                 "split call parked in host memory between layers even when they all fit)"),
     "FLS_SPLITK": ("1", "0: no split-K path for <= 512-row GEMMs"),
-    "FLS_GEMM_V11": ("1", "384x256 GEMM tile: 0 off (v10 everywhere), 1 where it takes no more whole 256-CU "
-                          "tile rounds (a v11 tile priced at 1.45 v10 tiles), 2 every valid shape"),
-    "FLS_SKINNY": ("1", "skinny-M GEMM for 17-192 rows: 0 off, 1 auto, 2 forced"),
-    "FLS_ATTN_SPLIT": ("0", "split-KV slices of the range-2 attention kernel: 0 by grid size, 1 off, n"),
-    "FLS_CHUNK_ALIGN": ("3072", "row multiple of the QKV / MLP chunks (3072 = 8 v11 tiles)"),
-    "FLS_SPECULATIVE_PREFETCH": ("", "0 / 1: force the next call's first-shard prefetch off / on"),
-    "FLS_R2_QBLOCK": ("8", "range-2 (generation-step) attention: 8 = packed-GQA decode kernel for items of <= 8 "
-                           "rows, 32 = one wave per query head, 64 = the batch's q_block"),
     "FLS_DECODE_GRAPHS": ("1", "0: no HIP-graph replay of decode-like calls (generation steps with the "
                                "prefix + suffix K/V caches and every weight in HBM)"),
     "FLS_SPEC_DECODE": ("1", "0: no speculative generation steps (the next decode-graphed step enqueued behind the "

@@ -22,7 +22,6 @@ from typing import Dict, Optional
 
 import torch
 
-from .. import knobs
 from ..config import ModelConfig, MAX_TOKEN_LEN
 from .layout import layer_kind
 
@@ -185,6 +184,16 @@ class ExecContext:
     # GEMM reads the raw hidden state, scaling each row by its rsqrt(mean(x^2) + eps) in the epilogue
     fused_norm: bool = False
     embed_out: Optional[torch.Tensor] = None   # destination of the next embedding gather (engine's ring)
+    # Fused norm: the residual GEMMs also write each row's partial sums of squares (fp32 per 128
+    # columns, Epi::ss) into ss_buf, and the next norm-folded projection of the SAME rows takes its
+    # statistic from them (a [rows, H/128] read) instead of a pass over the hidden state (row_rstd).
+    # ss_key names what ss_buf holds: (id(batch), decoder index, "attn" | "mlp", rows) -- valid for
+    # the projection right after that residual GEMM on this rank (any state parked and reloaded in
+    # between keeps its values); anything else (another micro-batch, the first layer, a grouped
+    # attention phase, MoE) misses and computes row_rstd.  Reset at every call's embedding.
+    ss_buf: Optional[torch.Tensor] = None      # the arena-backed buffer (grown, reused)
+    ss_cur: Optional[torch.Tensor] = None      # the buffer the last residual GEMM wrote
+    ss_key: Optional[tuple] = None
 
     def phase(self, *shapes) -> None:
         """Start a workspace phase that will carve ``shapes`` (rows, cols) in order."""
@@ -199,18 +208,57 @@ class ExecContext:
         t = self.scratch(1, 2 * n)
         return t.view(torch.float32).view(n) if t is not None else None
 
+    def ss_take(self, rows: int, key: Optional[tuple] = None) -> Optional[torch.Tensor]:
+        """The [rows, H/128] partial-sums buffer the next residual GEMM writes (None when the path
+        is off: unfused norm, MoE, or a hidden size the 128-column partials do not divide).  With
+        ``key`` holding (the partials about to be read), that same buffer.  Eagerly, one buffer
+        grown to the largest micro-batch (like the workspace); without a workspace (graph capture)
+        a fresh one per forward from the graph's own pool, never a buffer that eager code frees."""
+        H = self.cfg.hidden_size
+        if not self.fused_norm or self.cfg.is_moe or H % 128:
+            return None
+        if key is not None and self.ss_key == key and self.ss_cur is not None:
+            return self.ss_cur[:rows]
+        if self.ws is None:
+            self.ss_cur = torch.empty(rows, H // 128, dtype=torch.float32, device=self.device)
+            return self.ss_cur
+        if self.ss_buf is None or self.ss_buf.shape[0] < rows:
+            self.ss_buf = None
+            self.ss_buf = torch.empty(rows, H // 128, dtype=torch.float32, device=self.device)
+        self.ss_cur = self.ss_buf[:rows]
+        return self.ss_cur
+
+    def rstd(self, x: torch.Tensor, key: Optional[tuple], out=None, rows: Optional[slice] = None) -> torch.Tensor:
+        """Row statistic rsqrt(mean(x^2) + eps) of x: from the partial sums the residual GEMM named
+        ``key`` left (rows ``rows`` of them) when they are there, else a pass over x."""
+        eps = self.cfg.rms_norm_eps
+        if key is not None and self.ss_key == key and self.ss_cur is not None:
+            ss = self.ss_cur[:key[3]]
+            return self.ops.rstd_from_ss(ss[rows] if rows is not None else ss, self.cfg.hidden_size, eps, out=out)
+        return self.ops.row_rstd(x, eps, out=out)
+
+
+def _decoder_index(layer_name: str) -> int:
+    try:
+        return int(layer_name.rsplit(".", 1)[1])
+    except (IndexError, ValueError):
+        return -10
+
 
 def run_embed(ctx: ExecContext, W: Dict[str, torch.Tensor], meta: dict) -> torch.Tensor:
     """Embedding gather (Granite: scaled by embedding_multiplier in the same kernel), into the
     engine's activation buffer when it set one."""
     out, ctx.embed_out = ctx.embed_out, None
+    ctx.ss_key, ctx.ss_cur = None, None       # a new call / micro-batch: no partials carry over
     return ctx.ops.embed(meta["ids"], W["embed"], ctx.act_dtype, scale=ctx.cfg.embedding_multiplier, out=out)
 
 
-def _resid(ctx: ExecContext, a: torch.Tensor, w: torch.Tensor, x: torch.Tensor, bias=None) -> torch.Tensor:
+def _resid(ctx: ExecContext, a: torch.Tensor, w: torch.Tensor, x: torch.Tensor, bias=None, ss=None) -> torch.Tensor:
     """x + r * (a @ w^T (+ bias)): the fused residual GEMM, in place on x (r: Granite's
-    residual_multiplier, scaled in the epilogue; 1 otherwise)."""
-    return ctx.ops.linear_residual(a, w, x, bias=bias, alpha=ctx.cfg.residual_multiplier)
+    residual_multiplier, scaled in the epilogue; 1 otherwise); ``ss``: the rows' partial sums of
+    squares too (ExecContext.ss_buf)."""
+    kw = {"ss": ss} if ss is not None else {}
+    return ctx.ops.linear_residual(a, w, x, bias=bias, alpha=ctx.cfg.residual_multiplier, **kw)
 
 
 def fold_layer_norms(ops, views: Dict[str, torch.Tensor]) -> None:
@@ -225,7 +273,7 @@ def fold_layer_norms(ops, views: Dict[str, torch.Tensor]) -> None:
         ops.fold_norm(views["wgu"], views["ln2"])
 
 
-CHUNK_ALIGN = knobs.get_int("FLS_CHUNK_ALIGN")   # A/B knob (256: round 3's chunks)
+CHUNK_ALIGN = 3072     # row multiple of the QKV / MLP chunks: 8 v11 tiles (profiles/r4_gemm)
 
 
 def balanced_step(rows: int, limit: int, align: int = 0) -> int:
@@ -273,13 +321,14 @@ def _scored_q(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, las
 
 def _attn_inputs(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, pos: torch.Tensor,
                  last_idx: Optional[torch.Tensor], prune: bool, last_pos: Optional[torch.Tensor] = None,
-                 q_scored: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 q_scored: Optional[torch.Tensor] = None, ss_key: Optional[tuple] = None) -> torch.Tensor:
     """RMSNorm + QKV projection (+ RoPE, + bias) of every row into one [T, qkv] buffer.
     ``prune`` (the last decoder layer): K/V (+ RoPE on K) for every row, Q only for the scored rows,
     scattered into the Q columns of those rows — the other rows' Q columns stay unwritten, the last
     layer's attention work items (``work_last``) query only scored rows (Q is q_size / qkv_size of
     the projection: 80% for Llama-2-70B).  ``q_scored``: that Q, already projected (the grouped
     attention phase projects every group's scored rows in one GEMM, as the whole-batch path does).
+    ``ss_key``: the previous layer's residual GEMM whose partial sums give the row statistic.
 
     Fused (``ctx.fused_norm``, HIP): one GEMM over the raw hidden state with ln1 folded into W_qkv
     and each row scaled by its rsqrt(mean(x^2) + eps) in the epilogue — the workspace holds only
@@ -308,7 +357,7 @@ def _attn_inputs(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, 
         qkv = ctx.scratch(T0, Qn)
         if qkv is None:
             qkv = torch.empty(T0, Qn, dtype=x.dtype, device=x.device)
-        rstd = ops.row_rstd(x, eps, out=ctx.scratch_f32(T0))
+        rstd = ctx.rstd(x, ss_key, out=ctx.scratch_f32(T0))
         if not prune:
             put(proj(x, w, pos, nq, nkv, b, out=qkv, rscale=rstd), qkv)
             return qkv
@@ -342,7 +391,9 @@ def _attention_whole(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tens
     """Attention phase over the whole micro-batch: QKV of every row, one attention launch, O
     projection + residual (in place on x; the pruned last layer returns its scored rows)."""
     cfg, ops = ctx.cfg, ctx.ops
-    qkv = _attn_inputs(ctx, W, x, meta["positions"], meta["last_idx"], prune, meta["last_pos"])
+    li = _decoder_index(layer_name)
+    qkv = _attn_inputs(ctx, W, x, meta["positions"], meta["last_idx"], prune, meta["last_pos"],
+                       ss_key=(id(batch), li - 1, "mlp", x.shape[0]))
     kv0 = None
     pe = ctx.prefix_entry
     if pe is not None:
@@ -374,7 +425,10 @@ def _attention_whole(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tens
         idx = meta["last_idx"]
         a = ops.gather_rows(a, idx)
         x = ops.gather_rows(x, idx)
-    return _resid(ctx, a, W["wo"], x, bias=W.get("bo"))
+    ss = ctx.ss_take(x.shape[0])
+    y = _resid(ctx, a, W["wo"], x, bias=W.get("bo"), ss=ss)
+    ctx.ss_key = (id(batch), li, "attn", x.shape[0]) if ss is not None else None
+    return y
 
 
 def _attention_grouped(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, batch,
@@ -440,6 +494,7 @@ def run_decoder(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, b
     eps = cfg.rms_norm_eps
     if ctx.attn_rows and x.shape[0] > ctx.attn_rows and ctx.prefix_entry is None:
         x = _attention_grouped(ctx, W, x, batch, prune)
+        ctx.ss_key = None                      # (per-group residual GEMMs: no partials)
     else:
         x = _attention_whole(ctx, W, x, batch, meta, prune, layer_name)
     done = getattr(W, "attention_done", None)
@@ -449,20 +504,27 @@ def run_decoder(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, b
     I, H = cfg.intermediate_size, cfg.hidden_size
     step = balanced_step(T, max(1, ctx.mlp_chunk))
     if cfg.is_moe:
+        ctx.ss_key = None
         return _moe_mlp(ctx, W, x, step)
     if ctx.fused_norm:
         # ln2 folded into W_gate/up: the SwiGLU GEMM reads the raw rows, scaled by their statistic
-        # in the epilogue; the arena holds [SwiGLU chunk | row statistics]
+        # in the epilogue (from the O projection's partial sums when it left them); the arena holds
+        # [SwiGLU chunk | row statistics].  Each chunk's down projection overwrites only its own rows'
+        # partials, which its gate/up has already read.
+        li = _decoder_index(layer_name)
+        key = (id(batch), li, "attn", T)
+        ss_all = ctx.ss_take(T, key)          # (the O projection's buffer when the key matches)
         for s in range(0, T, step):
             xs = x[s:s + step]
             n = xs.shape[0]
             ctx.phase((n, I), (1, 2 * n))
             m = ctx.scratch(n, I)
-            rstd = ops.row_rstd(xs, eps, out=ctx.scratch_f32(n))
+            rstd = ctx.rstd(xs, key, out=ctx.scratch_f32(n), rows=slice(s, s + n))
             m = ops.swiglu_up(xs, W["wgu"], out=m, rscale=rstd)
-            y = _resid(ctx, m, W["wdown"], xs)
+            y = _resid(ctx, m, W["wdown"], xs, ss=ss_all[s:s + n] if ss_all is not None else None)
             if y.data_ptr() != xs.data_ptr():
                 xs.copy_(y)
+        ctx.ss_key = (id(batch), li, "mlp", T) if ss_all is not None else None
         return x
     if T <= step:
         ctx.phase((T, H), (T, I))               # the attention-phase bytes are dead: reuse them

@@ -74,20 +74,15 @@ class HipOps:
         # A/B switches (knobs.py); the kernels' defaults are the measured winners
         if knobs.get_int("FLS_SPLITK") == 0:
             self.k.fls_gemm_set_splitk(0)
-        if knobs.is_set("FLS_GEMM_V11"):
-            self.k.fls_gemm_set_v11(knobs.get_int("FLS_GEMM_V11"))
-        if knobs.is_set("FLS_SKINNY"):
-            self.k.fls_gemm_set_skinny(knobs.get_int("FLS_SKINNY"), 0)
-        if knobs.is_set("FLS_ATTN_SPLIT"):
-            self.k.fls_attention_set_split(knobs.get_int("FLS_ATTN_SPLIT"))
 
     # ---------------------------------------------------------------- GEMM
     def gemm(self, x: torch.Tensor, w: torch.Tensor, epi: int = EPI_NONE, out: torch.Tensor = None,
              resid: torch.Tensor = None, positions=None, cos=None, sin=None, rope_cols: int = 0,
              head_dim: int = 0, bias: torch.Tensor = None, rscale: torch.Tensor = None,
-             alpha: float = 1.0) -> torch.Tensor:
+             alpha: float = 1.0, ss: torch.Tensor = None) -> torch.Tensor:
         """rscale ([M] fp32): per-row scale of the raw product (before bias / epilogue); alpha:
-        RESID's C = alpha * (product + bias) + R."""
+        RESID's C = alpha * (product + bias) + R; ss ([>= M, N / 128] fp32, RESID): each output
+        row's partial sums of squares per 128 columns (:meth:`rstd_from_ss`)."""
         _f16(x, "x")
         _f16(w, "w")
         if rscale is not None and (rscale.dtype != torch.float32 or not rscale.is_cuda
@@ -106,6 +101,9 @@ class HipOps:
             _f16(bias, "bias")
             if bias.numel() != N or not bias.is_contiguous():
                 raise ValueError(f"bias must be a contiguous [{N}] vector")
+        if ss is not None and (ss.dtype != torch.float32 or not ss.is_cuda or ss.dim() != 2 or ss.shape[0] < M
+                               or ss.shape[1] < N // 128 or ss.stride(1) != 1):
+            raise TypeError(f"ss must be an fp32 CUDA [>= {M}, >= {N // 128}] matrix with unit column stride")
         rc = self.k.fls_gemm(x.data_ptr(), w.data_ptr(), out.data_ptr(), R.data_ptr(), M, N, K,
                              x.stride(0), w.stride(0), out.stride(0), R.stride(0), epi,
                              positions.data_ptr() if positions is not None else None,
@@ -113,6 +111,7 @@ class HipOps:
                              sin.data_ptr() if sin is not None else None,
                              rope_cols, head_dim, bias.data_ptr() if bias is not None else None,
                              rscale.data_ptr() if rscale is not None else None, float(alpha),
+                             ss.data_ptr() if ss is not None else None, ss.stride(0) if ss is not None else 0,
                              ws.data_ptr() if ws is not None else None, ws.numel() if ws is not None else 0, _stream())
         _chk(rc, "fls_gemm")
         return out
@@ -171,10 +170,20 @@ class HipOps:
             return self.gemv_skinny(x, w)
         return self.gemm(x, w)
 
-    def linear_residual(self, x, w, resid, bias=None, alpha: float = 1.0):
-        """resid += alpha * (x @ w^T (+ bias)), in place (alpha: Granite's residual_multiplier)."""
+    def linear_residual(self, x, w, resid, bias=None, alpha: float = 1.0, ss=None):
+        """resid += alpha * (x @ w^T (+ bias)), in place (alpha: Granite's residual_multiplier);
+        ``ss``: also each updated row's partial sums of squares (the next fused norm's statistic)."""
         _f16(resid, "resid")
-        return self.gemm(x, w, EPI_RESID, out=resid, resid=resid, bias=bias, alpha=alpha)
+        return self.gemm(x, w, EPI_RESID, out=resid, resid=resid, bias=bias, alpha=alpha, ss=ss)
+
+    def rstd_from_ss(self, ss, H: int, eps, out=None):
+        """[rows] fp32 rsqrt(sum of the row's ss partials / H + eps): the RMSNorm statistic of the rows
+        a residual GEMM just wrote (:meth:`linear_residual` ``ss``), without reading them again."""
+        rows = ss.shape[0]
+        r = out if out is not None else torch.empty(rows, dtype=torch.float32, device=ss.device)
+        _chk(self.k.fls_rstd_from_ss(ss.data_ptr(), ss.stride(0), -(-H // 128), rows, int(H), float(eps), r.data_ptr(),
+                                     _stream()), "fls_rstd_from_ss")
+        return r
 
     def swiglu_up(self, x, wgu, out=None, rscale=None):
         """silu(x @ gate^T) * (x @ up^T) with wgu = [gate; up]."""

@@ -34,7 +34,6 @@ from typing import List, Optional, Sequence
 import numpy as np
 import torch
 
-from .. import knobs
 from ..utils.tokenizer import TokenizedPrompt
 
 Q_BLOCK = 64            # query rows per attention work item (kernel tile)
@@ -56,9 +55,9 @@ class Segment:
     r2_len: int = 0      # tokens (all visible), between the prefix (r0) and the new rows (r1)
 
 
-# range-2 attention of <= 32-row items with one wave per head (32, default) or the 2-wave kernel
-# (64: A/B of the generation step, FLS_R2_QBLOCK=64)
-R2_Q_BLOCK = knobs.get_int("FLS_R2_QBLOCK")
+# range-2 (generation-step) attention items of <= 8 rows: the packed-GQA decode kernel
+# (csrc/kernels/attention.hip attn_decode; profiles/r5_gen)
+R2_Q_BLOCK = 8
 
 
 @dataclass
@@ -388,7 +387,10 @@ def split_microbatches(tps: Sequence[TokenizedPrompt], token_budget: int,
 
     groups = pack(token_budget)
     if len(groups) > 1:
-        lo, hi = max(max(sizes), -(-sum(sizes) // len(groups))), token_budget
+        # never above the budget: a prompt larger than it forms its own group at any limit (the
+        # --max_vram_gb plan sizes the arena for token_budget rows)
+        fit = max((n for n in sizes if n <= token_budget), default=0)
+        lo, hi = min(max(fit, -(-sum(sizes) // len(groups))), token_budget), token_budget
         while lo < hi:                       # the smallest limit that keeps the greedy count
             mid = (lo + hi) // 2
             if len(pack(mid)) <= len(groups):

@@ -27,8 +27,9 @@ intermediates are shared between them.
 """
 from __future__ import annotations
 
+import weakref
 from collections import OrderedDict
-from typing import Callable, Dict, Optional, Tuple
+from typing import Callable, Dict, List, Optional, Tuple
 
 import numpy as np
 import torch
@@ -74,6 +75,9 @@ class _Graph:
         self.graph = torch.cuda.CUDAGraph()
         self.out: torch.Tensor = None        # static device output [S, V]
         self.replays = 0
+        self.entry_ref = None                # DecodeGraphs: the cache entry whose K/V the graph baked in
+        self.staging: List[Tuple[Dict[str, np.ndarray], Dict[str, torch.Tensor], Optional[torch.cuda.Event]]] = []
+        self.next_stage = 0
 
 
 class GraphedForward:
@@ -153,8 +157,40 @@ class DecodeGraphs:
 
     @staticmethod
     def key(batch: PackedBatch, entry) -> tuple:
-        return (id(entry), batch.r2_q_block, batch.q_block) + tuple(
+        """The entry's identity is its fingerprint plus the device address of every per-layer K/V
+        buffer the graph reads and writes (an evicted entry's id() and even its addresses can be
+        reused by a new one: ``run`` also checks the graph's weak reference to the entry)."""
+        ptrs = tuple((n, t.data_ptr()) for n, t in sorted(entry.layers.items()))
+        return (entry.key, ptrs, batch.r2_q_block, batch.q_block) + tuple(
             (k, v.shape) for k, v in sorted(batch.host_meta().items()))
+
+    def forget(self, entry) -> None:
+        """Drop every graph captured on ``entry`` (called when the prefix cache evicts or drops it:
+        its K/V buffers are about to be freed, and a replay would read / write freed HBM)."""
+        for k in [k for k, g in self.graphs.items() if g.entry_ref is None or g.entry_ref() in (None, entry)]:
+            del self.graphs[k]
+
+    # pinned staging sets per graph: a replay may be enqueued while the previous one (and its
+    # metadata copies) still runs, so a set is refilled only after the copies that read it ran
+    STAGING_SETS = 2
+
+    def _upload(self, g: _Graph, host: Dict[str, np.ndarray]) -> None:
+        """Stream-ordered metadata copies from the graph's persistent pinned staging buffers."""
+        if not g.staging:
+            for _ in range(self.STAGING_SETS):
+                pinned = {k: torch.empty(v.shape, dtype=torch.from_numpy(np.ascontiguousarray(v)).dtype,
+                                         pin_memory=True) for k, v in host.items()}
+                g.staging.append(({k: t.numpy() for k, t in pinned.items()}, pinned, None))
+        views, pinned, ev = g.staging[g.next_stage]
+        if ev is not None:
+            ev.synchronize()                                 # the copies that last read this set ran
+        for k, v in host.items():
+            np.copyto(views[k], v, casting="no")
+            g.meta[k].copy_(pinned[k], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.dev))
+        g.staging[g.next_stage] = (views, pinned, ev)
+        g.next_stage = (g.next_stage + 1) % len(g.staging)
 
     def run(self, batch: PackedBatch, entry, ids_dev: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Replay (capture on the first sight of the shape) -> the static [n_scored, V] output.
@@ -165,6 +201,9 @@ class DecodeGraphs:
         key = self.key(batch, entry)
         host = batch.host_meta()
         g = self.graphs.get(key)
+        if g is not None and (g.entry_ref is None or g.entry_ref() is not entry):
+            del self.graphs[key]                             # captured on another (dead) entry
+            g = None
         if g is None:
             if len(self.graphs) >= self.max_graphs:
                 self.graphs.popitem(last=False)
@@ -172,6 +211,7 @@ class DecodeGraphs:
             if ids_dev is not None:
                 meta["ids"].copy_(ids_dev)
             g = _Graph(meta)
+            g.entry_ref = weakref.ref(entry)
             s = torch.cuda.Stream(self.dev)
             s.wait_stream(torch.cuda.current_stream(self.dev))
             with torch.cuda.stream(s):
@@ -185,8 +225,7 @@ class DecodeGraphs:
             self.graphs[key] = g
             return eager
         self.graphs.move_to_end(key)
-        for k, v in host.items():
-            g.meta[k].copy_(torch.from_numpy(np.ascontiguousarray(v)).pin_memory(), non_blocking=True)
+        self._upload(g, host)
         if ids_dev is not None:
             g.meta["ids"].copy_(ids_dev, non_blocking=True)
         g.graph.replay()

@@ -46,15 +46,15 @@ SLACK_ONE = 1.02
 # 9,216 and 12,288 differ only in per-launch ramps, while each extra micro-batch adds a round of
 # small per-layer launches (r5: 15 micro-batches of 12,288 rows ran 94.8% of the headline rate)
 MLP_CHUNK_TARGET = 9216
-# the plan aims this far below the cap (the estimate is a model; hipMemGetInfo is the judge)
-CAP_MARGIN = 0.015
+# the plan aims this far below the cap (the estimate is a model; hipMemGetInfo is the judge: the
+# 70B headline's plan estimates 5.92 GB against a 2 ms-sampled peak of 5.77-5.78, profiles/r6_head)
+CAP_MARGIN = 0.012
 # device memory the HIP runtime takes outside any allocator for a moment while a pass runs: up to
 # ~185 MB above the steady context for <= 2 ms around some host -> device weight copies, sampled
 # every 2 ms on the 70B headline (profiles/r4_vram); kept free under a cap, by the allocator limit
 # and by the plan
 RUNTIME_RESERVE = knobs.get_int("FLS_RUNTIME_RESERVE_MB") << 20
 # one activation-ring slot per micro-batch when they all fit (A/B knob)
-RESIDENT_STATES = knobs.get_int("FLS_RESIDENT_STATES") != 0
 
 
 def activation_bytes(cfg: ModelConfig, tokens: int, mlp_chunk: int, elem: int = 2, qkv_chunk: int = 0,
@@ -83,8 +83,11 @@ def activation_bytes(cfg: ModelConfig, tokens: int, mlp_chunk: int, elem: int = 
     # Qwen2-MoE shared expert: its SwiGLU rows, output and gated output per chunk (allocator)
     mlp += chunk * (cfg.shared_expert_intermediate_size + 2 * H) if cfg.shared_expert_intermediate_size else 0
     scratch = max(attn, mlp)                             # one arena, two phases
+    # fused norm: the residual GEMMs' per-row partial sums of squares (fp32 per 128 columns), kept
+    # from one residual GEMM to the next norm-folded projection (models.llama ExecContext.ss_buf)
+    ss = tokens * 2 * -(-H // 128) if (fused_norm and not cfg.is_moe) else 0
     slack = SLACK_ONE if states == 1 else SLACK
-    return int(slack * elem * (scratch + states * tokens * H))
+    return int(slack * elem * (scratch + ss + states * tokens * H))
 
 
 def shared_device_bytes() -> int:
@@ -177,7 +180,7 @@ def plan_for_vram(cfg: ModelConfig, max_vram_bytes: int, lnps: int = 1, n_slots:
         n_mb = -(-total_tokens // tb) if total_tokens else 2
         # live states: 1 (one micro-batch), every micro-batch's own (resident; known call only)
         # or the ring's two
-        state_opts = (1,) if n_mb == 1 else ((n_mb, STATES) if total_tokens and n_mb > STATES and RESIDENT_STATES
+        state_opts = (1,) if n_mb == 1 else ((n_mb, STATES) if total_tokens and n_mb > STATES
                                                    else (STATES,))
         for states in state_opts:
             resident = states == n_mb

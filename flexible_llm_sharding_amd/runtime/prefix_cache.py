@@ -148,6 +148,14 @@ class PrefixKVCache:
         self.entries: "OrderedDict[str, PrefixEntry]" = OrderedDict()
         self.hits = 0
         self.misses = 0
+        # called with an entry that leaves the cache (its K/V buffers are freed with it): graphs
+        # captured on it must go first (runtime/graphs.py DecodeGraphs.forget)
+        self.on_evict: List = []
+
+    def _evict(self, e: Optional[PrefixEntry]) -> None:
+        if e is not None:
+            for cb in self.on_evict:
+                cb(e)
 
     def lookup(self, tps: Sequence) -> Optional[PrefixEntry]:
         e = self.entries.get(prefix_fingerprint(tps))
@@ -159,15 +167,16 @@ class PrefixKVCache:
     def begin(self, tps: Sequence) -> PrefixEntry:
         """A fresh entry the coming full pass fills (replaces any partial one)."""
         key = prefix_fingerprint(tps)
-        self.entries.pop(key, None)
+        self._evict(self.entries.pop(key, None))
         while len(self.entries) >= self.max_entries:
-            self.entries.popitem(last=False)
+            self._evict(self.entries.popitem(last=False)[1])
         caps = ([[len(s) + self.SUFFIX_GROWTH for s in tp.suffixes] for tp in tps] if self.suffix_reuse else None)
         e = PrefixEntry(key, [len(tp.prefix) for tp in tps], self.kv_cols, self.dev, self.dtype, caps)
         self.entries[key] = e
         return e
 
     def drop(self, e: PrefixEntry) -> None:
+        self._evict(e)
         self.entries.pop(e.key, None)
 
     @property

@@ -55,6 +55,13 @@ def test_microbatch_split():
     big = [TokenizedPrompt([1] * 1024, [[1] * 64] * 5, 64, [63] * 5) for _ in range(128)]
     assert [len(x) for x in split_microbatches(big, 24576)] == [16] * 8
     assert [len(x) for x in split_microbatches(big[:32], 16384)] == [11, 11, 10]
+    # a prompt larger than the budget never raises the packing limit above it (the capped plan
+    # sizes the arena for token_budget rows): [1000, 30000, 20000, 5000] under 24,576
+    odd = [TokenizedPrompt([1] * (n - 1), [[1]], 1, [0]) for n in (1000, 30000, 20000, 5000)]
+    g = split_microbatches(odd, 24576)
+    assert sorted(i for x in g for i in x) == [0, 1, 2, 3]
+    for x in g:
+        assert len(x) == 1 or sum(odd[i].num_tokens for i in x) <= 24576
 
 
 def test_pack_segments():

@@ -443,6 +443,40 @@ def test_decode_graphs_match_eager(setup, weights):
             assert np.array_equal(a, b)
 
 
+def test_decode_graphs_survive_entry_eviction(setup):
+    """A decode graph bakes in its cache entry's K/V addresses.  With one prefix-cache entry, a
+    second prompt set of the same shapes evicts the first entry (its K/V freed; a new entry may get
+    the same id() and addresses) and must not replay the first entry's graph: every step of both
+    sets, alternating, == the eager runner bitwise."""
+    path, cfg, tok, prompts, ref = setup
+    src = HostStore.from_model_path(cfg, path)
+    other = [(" ".join(reversed(pre.split())), sufs) for pre, sufs in prompts]   # same lengths
+    words = prompts[0][0].split()
+    outs = {}
+    for graphs in ("1", "0"):
+        os.environ["FLS_DECODE_GRAPHS"] = graphs
+        try:
+            r = ShardedRunner(cfg, src, "cuda:0", tok, layer_num_per_shard=1, prefix_kv_cache=True,
+                              suffix_kv_cache=True, resident=True, prefix_cache_entries=1)
+            steps = []
+            for rnd in range(2):
+                for ps0 in (prompts, other):
+                    for step in range(3):
+                        ps = [(pre, tuple(sf + (" " + " ".join(words[:step]) if step else "") for sf in sufs))
+                              for pre, sufs in ps0]
+                        steps.append(r(ps))
+            if graphs == "1":
+                assert r.stats["graph_replays"] >= 1
+            outs[graphs] = steps
+            r.close()
+        finally:
+            os.environ.pop("FLS_DECODE_GRAPHS", None)
+    for sg, se in zip(outs["1"], outs["0"]):
+        for a, b in zip(sg, se):
+            assert np.isfinite(a.astype(np.float32)).all()
+            assert np.array_equal(a, b)
+
+
 @pytest.mark.parametrize("mode", ["match", "mismatch"])
 def test_speculative_generation_steps_bitwise(setup, mode):
     """Greedy generation with the suffix K/V cache on weights in HBM: each decode-graphed step

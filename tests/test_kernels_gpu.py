@@ -897,6 +897,43 @@ def test_gemm_row_scale_every_path(ops, ref, M, path, epi):
     assert torch.equal(unit, unscaled)
 
 
+@pytest.mark.parametrize("path,M", [("v11", 3072), ("v10", 1024), ("mid", 300), ("skinny", 160), ("splitk", 40),
+                                    ("generic", 300)])
+def test_resid_gemm_row_sum_squares(ops, path, M):
+    """RESID GEMMs with ``ss`` also write each output row's partial sums of squares per 128 columns
+    (the v10 / v11 epilogue, or the fallback kernel after the small-M paths): equal to the sums
+    over the fp16 output, the output itself bitwise unchanged; the statistic from them matches
+    row_rstd of the output."""
+    N, K = 2048, 1024
+    x = rnd(M, K, seed=131)
+    w = rnd(N, K, scale=0.05, seed=132)
+    r0 = rnd(M, N, seed=133)
+    modes = {"v11": (2, 1, 1, 1), "v10": (0, 0, 0, 1), "mid": (0, 1, 0, 0), "skinny": (0, 1, 2, 0),
+             "splitk": (0, 0, 0, 1), "generic": (0, 0, 0, 0)}[path]
+    k = ops.k
+    old = (k.fls_gemm_set_v11(modes[0]), k.fls_gemm_set_mid(modes[1]), k.fls_gemm_set_skinny(modes[2], 0),
+           k.fls_gemm_set_splitk(modes[3]))
+    try:
+        if path == "generic":
+            x, w = x[:, :K - 8], w[:, :K - 8]
+        ss = torch.full((M + 3, N // 128 + 2), -1.0, dtype=torch.float32, device=DEV)
+        plain = ops.linear_residual(x, w, r0.clone())
+        got = ops.linear_residual(x, w, r0.clone(), ss=ss)
+        rs = ops.rstd_from_ss(ss[:M], N, 1e-5)
+    finally:
+        k.fls_gemm_set_v11(old[0])
+        k.fls_gemm_set_mid(old[1])
+        k.fls_gemm_set_skinny(old[2], 0)
+        k.fls_gemm_set_splitk(old[3])
+    torch.cuda.synchronize()
+    assert torch.equal(got, plain)
+    want = (got.float() ** 2).view(M, N // 128, 128).sum(-1)
+    assert torch.allclose(ss[:M, :N // 128], want, rtol=1e-5, atol=1e-5)
+    assert (ss[M:] == -1).all() and (ss[:, N // 128:] == -1).all()       # nothing outside [M, N/128]
+    rr = ops.row_rstd(got, 1e-5)
+    assert torch.allclose(rs, rr, rtol=2e-6, atol=0)
+
+
 def test_embed_scaled(ops, ref):
     """Granite's embedding_multiplier inside the gather: fp16(e * m) == torch, bitwise."""
     table = rnd(1000, 512, seed=121)
