@@ -62,6 +62,10 @@ void    fls_f32_to_f16(const float* src, uint16_t* dst, uint64_t n);
 int fls_kernels_version(void);
 // epilogue codes for fls_gemm
 enum { FLS_EPI_NONE = 0, FLS_EPI_RESID = 1, FLS_EPI_SWIGLU = 2, FLS_EPI_ROPE = 3 };
+// or'd into epi: row-independent arithmetic only (the v10 / v11 tiles, else the generic kernel; no
+// skinny, split-K or mid-M path), so a row's result does not depend on M or on the other rows: the
+// generation tie guard re-runs a subset of prompts bit-identically to the whole batch
+#define FLS_GEMM_ROW_EXACT 0x100
 // C[M, N'] = epi(acc), acc[m] = rscale[m] * (A[M,K] . W[N,K]^T)[m] (+ bias)  (rscale may be null:
 // 1; the RMSNorm statistic of a fused norm + projection).  fp16 in / fp32 accumulate / fp16 out.
 //   RESID : C = alpha * acc + R (R may alias C; alpha: Granite's residual_multiplier, else 1)
@@ -81,7 +85,8 @@ int fls_gemm(const void* A, const void* W, void* C, const void* R, int M, int N,
 int fls_rstd_from_ss(const float* ss, int ss_ld, int nparts, int rows, int H, float eps, float* rstd,
                      fls_stream_t s);
 // out[r] = first index of the maximum of row r of non-negative fp16 values (greedy decoding)
-int fls_argmax_rows(const void* x, int ld, int rows, int V, int* out, fls_stream_t s);
+// second (may be null): (max << 16) | runner-up of each row, as fp16 bit patterns
+int fls_argmax_rows(const void* x, int ld, int rows, int V, int* out, unsigned* second, fls_stream_t s);
 // rstd[r] = rsqrt(mean(x[row]^2) + eps) in fp32, row = row_idx ? row_idx[r] : r (fused RMSNorm:
 // the statistic of the rows a norm-folded projection reads raw)
 int fls_row_rstd(const void* x, int ldx, const int* row_idx, int rows, int H, float eps, float* rstd,
@@ -121,6 +126,7 @@ int fls_gemm_set_mid(int on);   // 64x128-tile kernel for small / medium M (defa
 // suffix's cached K/V rows; needs kv0 and r2win).
 int fls_attention_set_hpb(int hpb);
 int fls_attention_set_split(int ns);
+int fls_attention_set_persistent(int on);   // persistent full-pass kernel (default on; tests / A-B)
 // ws / ws_bytes / n_rows (rows of qkv and out): fp32 scratch of the split-KV range-2 kernel (null: no split)
 int fls_attention(const void* qkv, void* out, const int* work, int n_items, int n_q_heads,
                   int n_kv_heads, int head_dim, int ld_qkv, int ld_out, float scale, const void* kv0,

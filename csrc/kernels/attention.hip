@@ -271,6 +271,7 @@ _Pragma("unroll") \
         if constexpr (NQ > 1) sc[1][tt] = mfma16x16x32(kf, qf[1][s], sc[1][tt]); \
       } \
     } \
+    FLS_ATTN_AFTER_QK \
     /* ---- visibility: wave-uniform fast path when every key of the tile is visible to every row */ \
     const int vis_last = causal ? min(klen - 1, qi_min) : klen - 1; \
     if (k0 + KT - 1 > vis_last || (r1 && multi) || r2) { \
@@ -345,6 +346,7 @@ _Pragma("unroll") \
         if constexpr (NQ > 1) o[1][u] = mfma16x16x32(vf, pf[1][ks], o[1][u]); \
       } \
     }
+#define FLS_ATTN_AFTER_QK
   if (t_hi > t_lo) {
     load_tile(t_lo);
     store_tile(t_lo & 1);
@@ -372,8 +374,8 @@ _Pragma("unroll") \
     }
     __syncthreads();
   }
+#undef FLS_ATTN_AFTER_QK
 #undef FLS_ATTN_TILE_PRE
-#undef FLS_ATTN_TILE_MATH
   // ---- normalise and store (split: the slice's fp32 partials)
 #pragma unroll
   for (int qg = 0; qg < 2; ++qg) {
@@ -403,6 +405,215 @@ _Pragma("unroll") \
     }
   }
 }
+
+// Persistent form of attn_fwd for the full-pass (no range 2, no split) items: a grid of about one
+// block per CU slot walks work units u = blockIdx.x, + gridDim.x, ... where a unit is (work item,
+// group of HPB query heads).  The K/V tile pipeline runs across unit boundaries: the register-staged
+// loads of the next unit's first tiles are in flight under the current unit's last tiles, and the
+// next unit's Q fragments are loaded right after the last tile's S = K Q^T MFMAs (Q is dead then),
+// under that tile's softmax, P.V and the unit's output stores.  A 1k-token prefix item is only 16
+// key tiles, so a block per unit exposed its start (Q load, first two tiles) and drain at every
+// item (attn_fwd: 828 TFLOP/s at a 1k prefix vs 992 at 4k, profiles/r2_attn).
+// Units in order u = item * (nh / HPB) + head group: with a grid that is a multiple of nh / HPB
+// a block keeps one head group, and the blocks of one XCD (b mod 8) share a few KV heads' K/V in
+// their L2.  Bitwise equal to attn_fwd (same per-tile arithmetic in the same order).
+template <int HD, int HPB, int WPH>
+__global__ __launch_bounds__(64 * WPH * HPB, 2) void attn_fwd_pers(const half_t* __restrict__ qkv,
+                                                         half_t* __restrict__ out, const int* __restrict__ work,
+                                                         const int* __restrict__ seg_lo, int nh, int nkv,
+                                                         int ld_qkv, int ld_out, float scale_log2,
+                                                         const half_t* __restrict__ kv0, int ld_kv0, int n_items) {
+  constexpr bool R2 = false;
+  constexpr int NT_ = 64 * WPH * HPB;
+  constexpr int NS = HD / 32;
+  constexpr int NU = HD / 16;
+  constexpr int CH = HD / 8;
+  constexpr int PER = KT * CH / NT_;
+  static_assert(PER >= 1 && (KT * CH) % NT_ == 0, "tile / block mismatch");
+  constexpr int TILE_BYTES = 2 * KT * HD * 2;
+  __shared__ __attribute__((aligned(16))) char smem[2 * TILE_BYTES];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hw = wave / WPH;                 // head of the block's group
+  const int rbase = (wave % WPH) * 32;       // this wave's first query row of an item
+  const int fr = lane & 15, grp = lane >> 4;
+  const int n_hg = nh / HPB;
+  const int n_units = n_items * n_hg;
+  const int G = gridDim.x;
+  const int hpg = nh / nkv;
+  const bool cache0 = kv0 != nullptr;
+  const int ld0 = cache0 ? ld_kv0 : ld_qkv;
+  const bool multi = seg_lo != nullptr;
+
+  // a unit's parameters (block-uniform: scalar loads of its work item)
+  struct UP {
+    int q_start, q_len, q_off, r_start0, r_len0, r_causal0, r_start1, r_len1, hg, n0, ntiles;
+  };
+  auto unit = [&](int u) {
+    UP p;
+    const int* wi = work + (u / n_hg) * 8;
+    p.hg = u % n_hg;
+    p.q_start = wi[0];
+    p.q_len = wi[1];
+    p.q_off = wi[2];
+    p.r_start0 = wi[3];
+    p.r_len0 = wi[4];
+    p.r_causal0 = wi[5];
+    p.r_start1 = wi[6];
+    p.r_len1 = wi[7];
+    const int kend0 = p.r_len0 <= 0 ? 0 : (p.r_causal0 ? min(p.r_len0, p.q_off + p.q_len) : p.r_len0);
+    const int kend1 = p.r_len1 <= 0 ? 0 : min(p.r_len1, p.q_off + p.q_len);
+    p.n0 = (kend0 + KT - 1) / KT;
+    p.ntiles = p.q_len <= 0 ? 0 : p.n0 + (kend1 + KT - 1) / KT;
+    return p;
+  };
+  auto next_valid = [&](int u) {
+    while (u < n_units && unit(u).ntiles <= 0) u += G;   // padding items (q_len 0) have no tiles
+    return u;
+  };
+
+  int mu = next_valid((int)blockIdx.x);
+  if (mu >= n_units) return;                 // block-uniform
+  UP M = unit(mu);
+
+  half8 qf[2][NS];
+  int qi[2], lo[2];
+  const int lo2[2] = {0, 0}, hi2[2] = {0, 0};
+  auto load_q = [&](const UP& p) {
+    const int h = p.hg * HPB + hw;
+#pragma unroll
+    for (int qg = 0; qg < 2; ++qg) {
+      const int qr = p.q_start + min(rbase + qg * 16 + fr, p.q_len - 1);
+      const half_t* qp = qkv + (size_t)qr * ld_qkv + h * HD + grp * 8;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) qf[qg][s] = *(const half8*)(qp + s * 32);
+    }
+  };
+  auto unit_rows = [&](const UP& p) {
+#pragma unroll
+    for (int qg = 0; qg < 2; ++qg) {
+      const int qrow = rbase + qg * 16 + fr;
+      const int qr = p.q_start + min(qrow, p.q_len - 1);
+      qi[qg] = p.q_off + qrow;
+      lo[qg] = multi && p.r_len1 > 0 ? seg_lo[qr] - p.r_start1 : 0;
+    }
+  };
+
+  // the load cursor: unit lu (parameters L), tile lt
+  int lu = mu, lt = 0;
+  UP L = M;
+  u32x4 pk[PER], pv[PER];
+  auto load_tile = [&]() {
+    const int g = (L.hg * HPB) / hpg;
+    const int k_col = nh * HD + g * HD, v_col = (nh + nkv) * HD + g * HD;
+    const bool r1 = lt >= L.n0;
+    const int k0 = (r1 ? lt - L.n0 : lt) * KT;
+    const int klen = r1 ? L.r_len1 : L.r_len0;
+    const int ldk = r1 ? ld_qkv : ld0;
+    const unsigned kc = (unsigned)(r1 ? k_col : (cache0 ? g * HD : k_col)) * 2u;
+    const unsigned vc = (unsigned)(r1 ? v_col : (cache0 ? (nkv + g) * HD : v_col)) * 2u;
+    const half_t* base = r1 ? qkv + (size_t)L.r_start1 * ld_qkv : (cache0 ? kv0 : qkv) + (size_t)L.r_start0 * ld0;
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<half_t*>(base), (short)0, -1,
+                                                                       0x00020000);
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = tid + i * NT_;
+      const int row = c / CH, ch = c % CH;
+      const unsigned off = (unsigned)(min(k0 + row, klen - 1) * ldk + ch * 8) * 2u;
+      pk[i] = __builtin_amdgcn_raw_buffer_load_b128(r, off, kc, 0);
+      pv[i] = __builtin_amdgcn_raw_buffer_load_b128(r, off, vc, 0);
+    }
+    if (++lt >= L.ntiles) {                  // advance the cursor (uniform)
+      lu = next_valid(lu + G);
+      lt = 0;
+      if (lu < n_units) L = unit(lu);
+    }
+  };
+  auto store_tile = [&](int buf) {
+    char* Ks = smem + buf * TILE_BYTES;
+    char* Vs = Ks + KT * HD * 2;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = tid + i * NT_;
+      const int row = c / CH, ch = c % CH;
+      *(u32x4*)(Ks + Lds<HD>::k_off(row, ch)) = pk[i];
+      *(u32x4*)(Vs + Lds<HD>::v_off(row, ch)) = pv[i];
+    }
+  };
+
+  // static priority for the second-dispatched half of the 8 waves (MI355X_MICROARCH: the younger half
+  // loses every VALU arbitration otherwise): +0.5% at the 70B headline shape (profiles/r6_attn)
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+  load_q(M);
+  unit_rows(M);
+  load_tile();                               // step 0
+  store_tile(0);
+  bool have = lu < n_units;                  // the registers hold the next step's tile
+  if (have) load_tile();                     // step 1
+  __syncthreads();
+
+  int s = 0;                                 // global step (LDS buffer parity)
+  for (;;) {
+    floatx4 o[2][NU];
+#pragma unroll
+    for (int qg = 0; qg < 2; ++qg)
+#pragma unroll
+      for (int u = 0; u < NU; ++u) o[qg][u] = floatx4{0.f, 0.f, 0.f, 0.f};
+    float m_run[2] = {-1e30f, -1e30f};
+    float l_run[2] = {0.f, 0.f};
+    const int nu = next_valid(mu + G);       // the next unit of this block (uniform)
+    const int qi_min = M.q_off + rbase;
+    for (int mt = 0; mt < M.ntiles; ++mt, ++s) {
+      const bool last = mt == M.ntiles - 1;
+      const bool r1 = mt >= M.n0;
+      const bool r2 = false;
+      const int k0 = (r1 ? mt - M.n0 : mt) * KT;
+      const int klen = r1 ? M.r_len1 : M.r_len0;
+      const bool causal = r1 || M.r_causal0;
+      const char* Ks = smem + (s & 1) * TILE_BYTES;
+      const char* Vs = Ks + KT * HD * 2;
+      constexpr int NQ = 2;
+      // the next unit's Q, in flight under this tile's softmax and P.V and the output stores
+#define FLS_ATTN_AFTER_QK \
+      if (last && nu < n_units) load_q(unit(nu));
+      FLS_ATTN_TILE_MATH
+#undef FLS_ATTN_AFTER_QK
+      if (have) {
+        store_tile((s + 1) & 1);             // the other buffer's readers (step s-1) passed the barrier
+        have = lu < n_units;
+        if (have) load_tile();               // step s+2, in flight under step s+1's MFMAs
+      }
+      __syncthreads();
+    }
+    // ---- normalise and store this unit's rows
+    const int h = M.hg * HPB + hw;
+#pragma unroll
+    for (int qg = 0; qg < 2; ++qg) {
+      float l = l_run[qg];
+      l += __shfl_xor(l, 16, 64);
+      l += __shfl_xor(l, 32, 64);
+      const int qrow = rbase + qg * 16 + fr;
+      if (qrow < M.q_len) {
+        const float inv = 1.f / l;
+        half_t* op = out + (size_t)(M.q_start + qrow) * ld_out + h * HD + grp * 4;
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+          half4 v;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = (half_t)(o[qg][u][r] * inv);
+          *(half4*)(op + u * 16) = v;
+        }
+      }
+    }
+    if (nu >= n_units) break;
+    mu = nu;
+    M = unit(mu);
+    unit_rows(M);
+  }
+}
+#undef FLS_ATTN_TILE_MATH
 
 // merge the split-KV slices of every row of every item: O = sum_z 2^(m_z - M) O_z / sum_z 2^(m_z - M) l_z
 // (m in the log2 domain); block = one (item, head), a thread per head-dim column
@@ -730,6 +941,49 @@ int launch(int hpb, dim3 grid, hipStream_t st, const half_t* qkv, half_t* out, c
   return 0;
 }
 
+// persistent attn_fwd (attn_fwd_pers): grid = the kernel's resident blocks per CU x the CUs, rounded
+// down to a multiple of the head groups (a block then keeps one head group), at most the units
+template <int HD, int HPB, int WPH>
+void launch_pers_hpb(int n_items, int nh, hipStream_t st, const half_t* qkv, half_t* out, const int* work,
+                     const int* seg_lo, int nkv, int ld_qkv, int ld_out, float scale_log2, const half_t* kv0,
+                     int ld_kv0) {
+  static int slots = 0;
+  if (!slots) {
+    int dev = 0, cus = 0, per = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)attn_fwd_pers<HD, HPB, WPH>,
+                                                        64 * WPH * HPB, 0);
+    slots = max(1, cus) * max(1, per);
+  }
+  const int n_hg = nh / HPB;
+  const long units = (long)n_items * n_hg;
+  int G = slots >= n_hg ? slots / n_hg * n_hg : slots;
+  if (units < G) G = (int)units;
+  hipLaunchKernelGGL((attn_fwd_pers<HD, HPB, WPH>), dim3(G), dim3(64 * WPH * HPB), 0, st, qkv, out, work, seg_lo,
+                     nh, nkv, ld_qkv, ld_out, scale_log2, kv0, ld_kv0, n_items);
+}
+
+template <int HD, int WPH>
+int launch_pers(int hpb, int n_items, hipStream_t st, const half_t* qkv, half_t* out, const int* work,
+                const int* seg_lo, int nh, int nkv, int ld_qkv, int ld_out, float scale_log2, const half_t* kv0,
+                int ld_kv0) {
+#define FLS_ATTN_PERS(HPB_) \
+  launch_pers_hpb<HD, HPB_, WPH>(n_items, nh, st, qkv, out, work, seg_lo, nkv, ld_qkv, ld_out, scale_log2, kv0, ld_kv0)
+  if constexpr (WPH == 2) {
+    if (hpb == 4) FLS_ATTN_PERS(4);
+    else if (hpb == 2) FLS_ATTN_PERS(2);
+    else FLS_ATTN_PERS(1);
+  } else {
+    if (hpb == 2) FLS_ATTN_PERS(2);
+    else FLS_ATTN_PERS(1);
+  }
+#undef FLS_ATTN_PERS
+  FLS_CHECK_LAUNCH();
+  return 0;
+}
+
+int g_pers = 1;  // persistent full-pass kernel (attn_fwd_pers) on (1, default) or off (0; tests / A-B)
 int g_hpb = 0;   // heads per block override (0: by group size; tests / A-B)
 int g_split = 0; // split-KV slices of the range-2 kernel: 0 = by grid size, 1 = off, n = n (tests / A-B)
 
@@ -739,6 +993,13 @@ int g_split = 0; // split-KV slices of the range-2 kernel: 0 = by grid size, 1 =
 extern "C" int fls_attention_set_hpb(int hpb) {
   const int old = g_hpb;
   g_hpb = hpb;
+  return old;
+}
+
+// persistent full-pass kernel on (1, default) / off (0: one block per work item x head group)
+extern "C" int fls_attention_set_persistent(int on) {
+  const int old = g_pers;
+  g_pers = on ? 1 : 0;
   return old;
 }
 
@@ -812,6 +1073,17 @@ int dispatch(const void* qkv, void* out, const int* work, int n_items, int n_q_h
   auto q = (const half_t*)qkv;
   auto o = (half_t*)out;
   auto k0 = (const half_t*)kv0;
+  if constexpr (!R2) {
+    if (g_pers && head_dim != 96 && q_block != 32)
+      return q_block == 64 ? (head_dim == 128 ? launch_pers<128, 2>(hpb, n_items, st, q, o, work, seg_lo, n_q_heads,
+                                                                    n_kv_heads, ld_qkv, ld_out, scale_log2, k0, ld_kv0)
+                                              : launch_pers<64, 2>(hpb, n_items, st, q, o, work, seg_lo, n_q_heads,
+                                                                   n_kv_heads, ld_qkv, ld_out, scale_log2, k0, ld_kv0))
+                           : (head_dim == 128 ? launch_pers<128, 4>(hpb, n_items, st, q, o, work, seg_lo, n_q_heads,
+                                                                    n_kv_heads, ld_qkv, ld_out, scale_log2, k0, ld_kv0)
+                                              : launch_pers<64, 4>(hpb, n_items, st, q, o, work, seg_lo, n_q_heads,
+                                                                   n_kv_heads, ld_qkv, ld_out, scale_log2, k0, ld_kv0));
+  }
   if constexpr (R2) {
     if (q_block == 32)                      // head_dim 64 / 128 here (96 fell back above)
       return head_dim == 128 ? launch<128, 1, true>(hpb, grid, st, q, o, work, seg_lo, n_q_heads, n_kv_heads, ld_qkv,

@@ -394,12 +394,12 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
                         ldw % 8 == 0 && (size_t)M * lda * 2 < (1ull << 32) && ldc % 4 == 0 &&
                         ((uintptr_t)C & 7) == 0 && ((uintptr_t)ws & 15) == 0 &&
                         (EPI != FLS_EPI_RESID || (ep.ldr % 4 == 0 && ((uintptr_t)ep.R & 7) == 0));
-  {
+  if (!ep.row_exact) {
     const int rc = try_skinny<EPI>(A, W, C, M, N, K, lda, ldw, ldc, ep, s, ws, ws_bytes);
     if (rc > 0) ss_partials(C, ldc, M, N, ep, s);
     if (rc) return rc > 0 ? 0 : rc;
   }
-  const int S = split_ok ? splitk_slices(M, N, K, tiles256, ws_bytes) : 0;
+  const int S = split_ok && !ep.row_exact ? splitk_slices(M, N, K, tiles256, ws_bytes) : 0;
   if (S >= 2 && (M > 64 || tiles256 * S >= 128)) {
     static bool attr_f32 = false;
     if (!attr_f32) {
@@ -425,7 +425,7 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
     FLS_CHECK_LAUNCH();
     return 0;
   }
-  if (mid_ok && (!main_ok || (g_mid && (tiles256 < 128 || (M <= 64 && tiles256 < 512))))) {
+  if (mid_ok && !ep.row_exact && (!main_ok || (g_mid && (tiles256 < 128 || (M <= 64 && tiles256 < 512))))) {
     static bool attr_mid = false;
     if (!attr_mid) {
       (void)hipFuncSetAttribute((const void*)gemm_nt_mid<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -483,7 +483,7 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
 
 }  // namespace
 
-extern "C" int fls_kernels_version(void) { return 25; }
+extern "C" int fls_kernels_version(void) { return 27; }
 
 // tile order: 0 = by shape (default); g > 0: groups of g M tiles; g < 0: groups of -g N tiles (A/B, tests)
 extern "C" int fls_gemm_set_order(int order) {
@@ -540,6 +540,8 @@ extern "C" int fls_gemm(const void* A, const void* W, void* C, const void* R, in
                         int rope_cols, int head_dim, const void* bias, const float* rscale, float alpha, float* ss,
                         int ss_ld, void* ws, uint64_t ws_bytes, fls_stream_t s) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
+  const int row_exact = (epi & FLS_GEMM_ROW_EXACT) ? 1 : 0;
+  epi &= 0xff;
   // row partial sums of squares: residual GEMMs only, one per 128 output columns
   if (ss && (epi != FLS_EPI_RESID || N % 128 || ss_ld < N / 128)) return -7;
   if (bias && epi == FLS_EPI_SWIGLU) return -4;
@@ -557,6 +559,7 @@ extern "C" int fls_gemm(const void* A, const void* W, void* C, const void* R, in
   ep.alpha = alpha;
   ep.ss = ss;
   ep.ss_ld = ss_ld;
+  ep.row_exact = row_exact;
   auto a = (const half_t*)A;
   auto w = (const half_t*)W;
   auto c = (half_t*)C;

@@ -55,6 +55,9 @@ struct Epi {
   // (fls_rstd_from_ss) -- the separate pass over the hidden state (row_rstd) is not needed
   float* ss = nullptr;
   int ss_ld = 0;
+  // FLS_GEMM_ROW_EXACT: only the row-independent paths (v10 / v11 tiles, or the generic kernel for
+  // shapes they do not take): every output row gets the same arithmetic whatever M and the other rows
+  int row_exact = 0;
 };
 
 // sum of v over the 4 lanes of one output row (lanes l, l^16, l^32, l^48: one 16-column group

@@ -116,6 +116,16 @@ def resolve_prefix_kv_cache(args) -> bool:
     return bool(v)
 
 
+def resolve_suffix_kv_cache(args, world: int = 1) -> bool:
+    """``--suffix_kv_cache auto``: on whenever the prefix K/V cache is, on one rank (the tie guard's
+    exact re-runs of a few prompts are single-rank calls; every rank of a multi-GPU run would have to
+    join them)."""
+    v = getattr(args, "suffix_kv_cache", False)
+    if v == "auto":
+        return resolve_prefix_kv_cache(args) and world == 1
+    return bool(v)
+
+
 def prefix_kv_bytes(cfg: ModelConfig, tok, prompts, n_decoders: int, elem: int = 2,
                     suffix_kv_cache: bool = False) -> int:
     """HBM the prefix K/V cache needs for ``prompts``: post-RoPE K and V of every prefix token, and
@@ -163,11 +173,11 @@ def build_runner(args, cfg: ModelConfig, device, comm: Comm, tok, prompts=None) 
     device = torch.device(device)
     from .models.layout import layer_kind
     pkv = resolve_prefix_kv_cache(args)
+    skv = resolve_suffix_kv_cache(args, comm.world) and pkv
     n_dec = sum(1 for n in cfg.layer_names() if layer_kind(n) == "decoder")
     if not args.data_parallel and comm.world > 1:
         n_dec = -(-n_dec // comm.world)
-    reserve = prefix_kv_bytes(cfg, tok, prompts, n_dec,
-                              suffix_kv_cache=getattr(args, "suffix_kv_cache", False)) if pkv else 0
+    reserve = prefix_kv_bytes(cfg, tok, prompts, n_dec, suffix_kv_cache=skv) if pkv else 0
     if args.data_parallel and comm.world > 1 and args.dp_weight_shard:
         from .parallel.data_parallel import build_dp_sharded_runner
         hv = getattr(args, "hbm_cache_gb", 0.0)
@@ -199,7 +209,7 @@ def build_runner(args, cfg: ModelConfig, device, comm: Comm, tok, prompts=None) 
                          hbm_cache_gb=resolve_hbm_cache_gb(args, cfg, device, reserve),
                          prefix_kv_cache=pkv,
                          prefix_cache_entries=getattr(args, "prefix_cache_entries", 8),
-                         suffix_kv_cache=getattr(args, "suffix_kv_cache", False),
+                         suffix_kv_cache=skv, tie_guard=getattr(args, "tie_guard", True),
                          pipeline_stages=getattr(args, "pipeline_stages", "round_robin"),
                          rx_window=getattr(args, "rx_window", 2),
                          max_vram_gb=getattr(args, "max_vram_gb", None))

@@ -191,6 +191,9 @@ class ExecContext:
     # the projection right after that residual GEMM on this rank (any state parked and reloaded in
     # between keeps its values); anything else (another micro-batch, the first layer, a grouped
     # attention phase, MoE) misses and computes row_rstd.  Reset at every call's embedding.
+    # generation tie guard (engine): every row's arithmetic independent of the other rows of the call
+    # (row-exact GEMM paths, the row statistic always from the row itself)
+    row_exact: bool = False
     ss_buf: Optional[torch.Tensor] = None      # the arena-backed buffer (grown, reused)
     ss_cur: Optional[torch.Tensor] = None      # the buffer the last residual GEMM wrote
     ss_key: Optional[tuple] = None
@@ -215,7 +218,7 @@ class ExecContext:
         grown to the largest micro-batch (like the workspace); without a workspace (graph capture)
         a fresh one per forward from the graph's own pool, never a buffer that eager code frees."""
         H = self.cfg.hidden_size
-        if not self.fused_norm or self.cfg.is_moe or H % 128:
+        if not self.fused_norm or self.cfg.is_moe or H % 128 or self.row_exact:
             return None
         if key is not None and self.ss_key == key and self.ss_cur is not None:
             return self.ss_cur[:rows]

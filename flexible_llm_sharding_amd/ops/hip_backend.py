@@ -22,6 +22,7 @@ from .. import _native, knobs
 from .torch_backend import fill_params
 
 EPI_NONE, EPI_RESID, EPI_SWIGLU, EPI_ROPE = 0, 1, 2, 3
+ROW_EXACT = 0x100                  # csrc/include/fls.h: the row-exact epi flag
 SPLITK_MAX_M = 512                 # csrc/kernels/gemm.hip SPLITK_MAX_M
 SPLITK_WS_BYTES = 64 << 20        # fp32 partial slabs: e.g. 8 slices x 160 rows x 10240 columns
 CAST_BF16, CAST_F32 = 1, 2
@@ -93,6 +94,7 @@ class HipOps:
         if K != K2:
             raise ValueError(f"gemm K mismatch {x.shape} x {w.shape}")
         ncols = N // 2 if epi == EPI_SWIGLU else N
+        code = epi | (ROW_EXACT if getattr(self._tl, "row_exact", False) else 0)
         if out is None:
             out = torch.empty(M, ncols, dtype=torch.float16, device=x.device)
         R = resid if resid is not None else out
@@ -105,7 +107,7 @@ class HipOps:
                                or ss.shape[1] < N // 128 or ss.stride(1) != 1):
             raise TypeError(f"ss must be an fp32 CUDA [>= {M}, >= {N // 128}] matrix with unit column stride")
         rc = self.k.fls_gemm(x.data_ptr(), w.data_ptr(), out.data_ptr(), R.data_ptr(), M, N, K,
-                             x.stride(0), w.stride(0), out.stride(0), R.stride(0), epi,
+                             x.stride(0), w.stride(0), out.stride(0), R.stride(0), code,
                              positions.data_ptr() if positions is not None else None,
                              cos.data_ptr() if cos is not None else None,
                              sin.data_ptr() if sin is not None else None,
@@ -166,9 +168,24 @@ class HipOps:
         return out
 
     def linear(self, x, w):
-        if x.shape[0] <= 16 and x.shape[1] % 32 == 0:
+        if x.shape[0] <= 16 and x.shape[1] % 32 == 0 and not getattr(self._tl, "row_exact", False):
             return self.gemv_skinny(x, w)
         return self.gemm(x, w)
+
+    def row_exact(self, on: bool = True):
+        """Context manager: GEMMs issued by this host thread take only row-independent paths
+        (fls.h GEMM_ROW_EXACT; no GEMV / skinny / split-K / mid-M), so each row's result is the same
+        whatever other rows share the launch (engine.ShardedRunner._tie_guard)."""
+        ops = self
+
+        class _Exact:
+            def __enter__(self):
+                self.prev = getattr(ops._tl, "row_exact", False)
+                ops._tl.row_exact = bool(on)
+
+            def __exit__(self, *exc):
+                ops._tl.row_exact = self.prev
+        return _Exact()
 
     def linear_residual(self, x, w, resid, bias=None, alpha: float = 1.0, ss=None):
         """resid += alpha * (x @ w^T (+ bias)), in place (alpha: Granite's residual_multiplier);
@@ -444,13 +461,15 @@ class HipOps:
                                      _stream()), "fls_softmax")
         return probs
 
-    def argmax_rows(self, probs):
-        """[rows] int32: the first index of each row's maximum (non-negative fp16 probabilities)."""
+    def argmax_rows(self, probs, top2: bool = False):
+        """[rows] int32: the first index of each row's maximum (non-negative fp16 probabilities).
+        ``top2``: -> (that, [rows] int32 = (max << 16) | runner-up as fp16 bit patterns)."""
         _f16(probs, "probs")
         out = torch.empty(probs.shape[0], dtype=torch.int32, device=probs.device)
+        sec = torch.empty(probs.shape[0], dtype=torch.int32, device=probs.device) if top2 else None
         _chk(self.k.fls_argmax_rows(probs.data_ptr(), probs.stride(0), probs.shape[0], probs.shape[1],
-                                    out.data_ptr(), _stream()), "fls_argmax_rows")
-        return out
+                                    out.data_ptr(), sec.data_ptr() if top2 else None, _stream()), "fls_argmax_rows")
+        return (out, sec) if top2 else out
 
     def lm_head_softmax(self, h, w, logits_scaling: float = 1.0):
         return self.softmax(self.linear(h, w), logits_scaling)

@@ -57,12 +57,16 @@ def build_parser() -> argparse.ArgumentParser:
                    help="keep every prompt's prefix K/V per layer in HBM and reuse it in later calls on the same "
                         "prefixes (each --num_gen_token step then computes only the suffix tokens; exact). "
                         "auto (default): on when --num_gen_token > 1")
-    p.add_argument("--suffix_kv_cache", type=str2bool, nargs="?", const=True, default=False,
+    p.add_argument("--suffix_kv_cache", type=bool_or_auto, nargs="?", const=True, default="auto",
                    help="with the prefix K/V cache: also keep every suffix's K/V and, in the next call (generation "
                         "step), compute only the tokens after the longest common token prefix with the last call's "
-                        "suffix (each step then costs its new tokens).  Off by default: scores then agree with the "
-                        "reference's full re-computation only to rounding, so a near-tie argmax may pick another "
-                        "token (PARITY.md); the prefix-only cache is exact")
+                        "suffix (each step then costs its new tokens).  Scores agree with the exact re-computation to "
+                        "fp16 rounding; a tie guard re-runs exactly every prompt whose greedy token is a near tie, so "
+                        "the generated tokens are the exact path's (PARITY.md C21).  auto (default): on with the "
+                        "prefix K/V cache on one GPU")
+    p.add_argument("--tie_guard", type=str2bool, nargs="?", const=True, default=True,
+                   help="with --suffix_kv_cache: re-run exactly the prompts whose top-2 probabilities are within "
+                        "the measured reuse deviation (false: keep the reused step's tokens)")
     p.add_argument("--prefix_cache_entries", type=int, default=8,
                    help="prefix K/V cache: calls (prompt batches) kept, LRU")
     p.add_argument("--resident", type=str2bool, nargs="?", const=True, default=False,

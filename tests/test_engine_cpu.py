@@ -418,6 +418,46 @@ def test_config_rope_and_head_dim_forms(tmp_path):
     assert ModelConfig.from_pretrained(str(tmp_path)) == c
 
 
+@pytest.mark.parametrize("rel", [1.0, 0.0])
+def test_tie_guard_reruns_near_ties(tiny_model, rel):
+    """Suffix K/V reuse with the tie guard: after a reused step, every prompt with a suffix whose
+    runner-up probability is within TIE_REL of its best is re-run exactly (prefix K/V from the
+    cache, all suffix tokens).  TIE_REL = 1: every prompt, every reused step; 0: only exact ties.
+    Tokens == the exact generation, scores within rounding."""
+    from flexible_llm_sharding_amd.api import generation_loop
+    from flexible_llm_sharding_amd.engine import ShardedRunner
+    from flexible_llm_sharding_amd.parallel.comm import Comm
+    from flexible_llm_sharding_amd.runtime.weights import HostStore
+    from flexible_llm_sharding_amd.utils.synthetic import synthetic_prompts
+    from flexible_llm_sharding_amd.utils.tokenizer import load_tokenizer
+    import argparse
+    path, cfg = tiny_model
+    tok = load_tokenizer(path)
+    prompts = synthetic_prompts(5, 40, 3, 6, cfg.vocab_size, seed=23, vary=True)
+    src = HostStore.from_model_path(cfg, path, pinned=False)
+    args = argparse.Namespace(num_gen_token=4, data_parallel=False, num_batch=1)
+    exact = ShardedRunner(cfg, src, "cpu", tok, layer_num_per_shard=2, prefix_kv_cache=True, suffix_kv_cache=False)
+    s0, u0 = generation_loop(args, exact, Comm(), tok, prompts)
+    r = ShardedRunner(cfg, src, "cpu", tok, layer_num_per_shard=2, prefix_kv_cache=True, suffix_kv_cache=True)
+    r.TIE_REL = rel
+    guarded = []
+    orig = r._tie_guard
+
+    def spy(tps, outputs):
+        out = orig(tps, outputs)
+        guarded.append(r.stats["tie_guard_prompts"])
+        return out
+    r._tie_guard = spy
+    s1, u1 = generation_loop(args, r, Comm(), tok, prompts)
+    assert u0 == u1
+    for a, b in zip(s0, s1):
+        assert np.abs(a.astype(np.float32) - b.astype(np.float32)).max() < 1e-5
+    assert len(guarded) == args.num_gen_token - 1                  # every reused step was checked
+    if rel == 1.0:
+        assert guarded == [float(len(prompts))] * len(guarded)
+    assert r.stats["suffix_tokens_reused"] > 0 and "tie_guard_s" in r.stats
+
+
 @pytest.mark.parametrize("num_batch_calls", [1, 2])
 def test_prefix_kv_cache_generation_exact(tiny_model, num_batch_calls):
     """--prefix_kv_cache: later calls on the same prefixes compute only suffix tokens, same scores."""

@@ -169,6 +169,54 @@ def test_attention_prefix_from_cache(ops, ref, nh, nkv, hd):
     assert rel_err(y.cpu(), r) < 5e-3
 
 
+@pytest.mark.parametrize("nh,nkv,hd,q_block", [(64, 8, 128, 64), (8, 2, 128, 64), (4, 4, 128, 128), (8, 1, 128, 64),
+                                              (8, 2, 64, 64), (4, 4, 64, 128), (12, 2, 64, 64)])
+@pytest.mark.parametrize("mode", ["bidirectional", "causal"])
+@pytest.mark.parametrize("cached", [False, True])
+def test_attention_persistent_bitwise(ops, ref, nh, nkv, hd, q_block, mode, cached):
+    """The persistent full-pass kernel (a grid of about one block per CU walking (work item, head
+    group) units, the K/V tile pipeline and the next unit's Q load running across unit boundaries)
+    == one block per unit, bitwise, on ragged prompts, multi-suffix items, padding items (q_len 0)
+    and range 0 from a prefix K/V cache; and == the fp32 oracle."""
+    from flexible_llm_sharding_amd.runtime.batch import pack_prompts
+    from flexible_llm_sharding_amd.utils.tokenizer import TokenizedPrompt
+    prompts = [(70, [5, 64, 1]), (1, [3]), (130, [65, 17, 129]), (200, [33, 64]), (1024, [64] * 5), (40, [30] * 5)]
+    tps = [TokenizedPrompt(list(range(lp)), [list(range(l)) for l in ls], max(ls), [l - 1 for l in ls])
+           for lp, ls in prompts]
+    offs, t = [], 0
+    for lp, _ in prompts:
+        offs.append(t)
+        t += lp
+    full = pack_prompts(tps, list(range(len(tps))), mode, prefix_offsets=offs, q_block=q_block)
+    g = torch.Generator().manual_seed(17)
+    qkv = torch.randn(full.num_tokens, (nh + 2 * nkv) * hd, generator=g).half()
+    r = ref.attention(qkv.float(), full.segments, nh, nkv, hd)
+    kw = {}
+    if cached and mode == "bidirectional":
+        qs, kv = nh * hd, 2 * nkv * hd
+        cache = torch.zeros(t, kv, dtype=torch.float16)
+        cache[torch.from_numpy(full.pfx_dst)] = qkv[torch.from_numpy(full.pfx_src), qs:qs + kv]
+        b = pack_prompts(tps, list(range(len(tps))), mode, prefix_offsets=offs, kv_cached=True, q_block=q_block)
+        keep = torch.from_numpy(np.setdiff1d(np.arange(full.num_tokens), full.pfx_src))
+        q, r = qkv[keep].contiguous(), r[keep]
+        kw["kv0"] = cache.to(DEV)
+    else:
+        b, q = full, qkv
+    meta = b.device_tensors(DEV)
+    work = torch.cat([meta["work"], torch.zeros(3, 8, dtype=torch.int32, device=DEV)])   # padding items
+    q = q.to(DEV)
+    old = ops.k.fls_attention_set_persistent(1)
+    try:
+        y = ops.attention(q, work, nh, nkv, hd, q_block=q_block, seg_lo=meta["seg_lo"], **kw)
+        ops.k.fls_attention_set_persistent(0)
+        y0 = ops.attention(q, work, nh, nkv, hd, q_block=q_block, seg_lo=meta["seg_lo"], **kw)
+    finally:
+        ops.k.fls_attention_set_persistent(old)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y0)
+    assert rel_err(y.cpu(), r) < 5e-3
+
+
 def test_attention_softmax_spike(ops, ref):
     # force the online-softmax rescale path: one huge key late in the sequence
     nh, nkv, hd = 2, 1, 128
@@ -966,3 +1014,12 @@ def test_argmax_rows_first_index(ops):
     torch.cuda.synchronize()
     assert np.array_equal(got.cpu().numpy(), np.argmax(x.cpu().numpy(), axis=-1))
     assert got[3].item() == 100 and got[5].item() == 0
+    # the tie guard's top-2: (max << 16) | runner-up as fp16 bits; a repeated maximum is its own runner-up
+    idx, sec = ops.argmax_rows(x, top2=True)
+    torch.cuda.synchronize()
+    assert torch.equal(idx, got)
+    bits = sec.cpu().numpy().view(np.uint32)
+    top = np.stack([(bits >> 16).astype(np.uint16), (bits & 0xFFFF).astype(np.uint16)], 1).view(np.float16)
+    want = np.sort(x.cpu().numpy().astype(np.float32), axis=-1)[:, -2:][:, ::-1]
+    assert np.array_equal(top.astype(np.float32), want)
+    assert top[3, 0] == top[3, 1] == np.float16(0.5) and top[5, 0] == top[5, 1] == 0
