@@ -85,8 +85,7 @@ int fls_gemm(const void* A, const void* W, void* C, const void* R, int M, int N,
 int fls_rstd_from_ss(const float* ss, int ss_ld, int nparts, int rows, int H, float eps, float* rstd,
                      fls_stream_t s);
 // out[r] = first index of the maximum of row r of non-negative fp16 values (greedy decoding)
-// second (may be null): (max << 16) | runner-up of each row, as fp16 bit patterns
-int fls_argmax_rows(const void* x, int ld, int rows, int V, int* out, unsigned* second, fls_stream_t s);
+int fls_argmax_rows(const void* x, int ld, int rows, int V, int* out, fls_stream_t s);
 // rstd[r] = rsqrt(mean(x[row]^2) + eps) in fp32, row = row_idx ? row_idx[r] : r (fused RMSNorm:
 // the statistic of the rows a norm-folded projection reads raw)
 int fls_row_rstd(const void* x, int ldx, const int* row_idx, int rows, int H, float eps, float* rstd,

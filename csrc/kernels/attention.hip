@@ -302,8 +302,11 @@ _Pragma("unroll") \
       const float mx = max_xor16_32(vmax3(ma, sc[qg][1][3], vmax(mb, sc[qg][3][3]))); \
       /* deferred rescale: keep the old max unless some row of the wave grew past 2^DEFER_LOG2 */ \
       /* (the previous tile's P.V is complete: nothing at the old scale is pending) */ \
+      /* (each row decides for itself: a row's result never depends on the other rows of its wave, */ \
+      /* so a generation step reusing cached K/V is bitwise the full re-computation: alpha = 1 exactly */ \
+      /* for the rows that keep their max) */ \
       if (!__all((mx - m_run[qg]) * scale_log2 <= DEFER_LOG2)) { \
-        const float m_new = fmaxf(m_run[qg], mx); \
+        const float m_new = (mx - m_run[qg]) * scale_log2 > DEFER_LOG2 ? mx : m_run[qg]; \
         const float alpha = fast_exp2((m_run[qg] - m_new) * scale_log2); \
         l_run[qg] *= alpha; \
 _Pragma("unroll") \
@@ -787,7 +790,7 @@ __global__ __launch_bounds__(256, 1) void attn_decode(const half_t* __restrict__
       mb = vmax3(mb, sc[3][1], sc[3][2]);
       const float mx = max_xor16_32(vmax3(ma, sc[1][3], vmax(mb, sc[3][3])));
       if (!__all((mx - m_run) * scale_log2 <= DEFER_LOG2)) {
-        const float m_new = fmaxf(m_run, mx);
+        const float m_new = (mx - m_run) * scale_log2 > DEFER_LOG2 ? mx : m_run;   // per row (attn_fwd)
         const float alpha = fast_exp2((m_run - m_new) * scale_log2);
         l_run *= alpha;
 #pragma unroll

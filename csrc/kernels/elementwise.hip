@@ -227,47 +227,35 @@ __global__ __launch_bounds__(256) void softmax_kernel(const half_t* __restrict__
 // argmax on the scores the reference hands back, main.py:85-88).  Probabilities are >= 0, so
 // their bit patterns order like their values; each thread keeps (bits, first index), then a tree
 // reduction over the block.
-// out[row] = first index of the row's maximum; second (optional): the row's two largest values as
-// fp16 bit patterns, (best << 16) | runner-up (a repeated maximum is its own runner-up) -- the
-// generation tie guard's input (engine.ShardedRunner._tie_guard)
 __global__ __launch_bounds__(256) void argmax_rows_kernel(const half_t* __restrict__ x, int ld, int V,
-                                                        int* __restrict__ out, unsigned* __restrict__ second) {
-  __shared__ unsigned sb[256], s2[256];
+                                                        int* __restrict__ out) {
+  __shared__ unsigned sb[256];
   __shared__ int si[256];
   const unsigned short* r = (const unsigned short*)(x + (size_t)blockIdx.x * ld);
-  unsigned best = 0, sec = 0;
+  unsigned best = 0;
   int bi = 0x7fffffff;
   for (int c = threadIdx.x; c < V; c += 256) {
     const unsigned b = r[c];
     if (b > best || (b == best && c < bi)) {
-      sec = max(sec, best);
       best = b;
       bi = c;
-    } else {
-      sec = max(sec, b);
     }
   }
   sb[threadIdx.x] = best;
-  s2[threadIdx.x] = sec;
   si[threadIdx.x] = bi;
   __syncthreads();
   for (int s = 128; s > 0; s >>= 1) {
     if (threadIdx.x < s) {
-      const unsigned b = sb[threadIdx.x + s], a = sb[threadIdx.x];
+      const unsigned b = sb[threadIdx.x + s];
       const int i = si[threadIdx.x + s];
-      // runner-up of the merge: the larger of the two runners-up and the smaller of the two bests
-      s2[threadIdx.x] = max(max(s2[threadIdx.x], s2[threadIdx.x + s]), min(a, b));
-      if (b > a || (b == a && i < si[threadIdx.x])) {
+      if (b > sb[threadIdx.x] || (b == sb[threadIdx.x] && i < si[threadIdx.x])) {
         sb[threadIdx.x] = b;
         si[threadIdx.x] = i;
       }
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    out[blockIdx.x] = si[0] == 0x7fffffff ? 0 : si[0];
-    if (second) second[blockIdx.x] = (sb[0] << 16) | s2[0];
-  }
+  if (threadIdx.x == 0) out[blockIdx.x] = si[0] == 0x7fffffff ? 0 : si[0];
 }
 
 // counter-based normal generator (splitmix64 -> Box-Muller), 8 values/thread
@@ -485,10 +473,9 @@ extern "C" int fls_softmax_rows(const void* logits, void* probs, int rows, int V
   return 0;
 }
 
-extern "C" int fls_argmax_rows(const void* x, int ld, int rows, int V, int* out, unsigned* second, fls_stream_t s) {
+extern "C" int fls_argmax_rows(const void* x, int ld, int rows, int V, int* out, fls_stream_t s) {
   if (rows <= 0) return 0;
-  hipLaunchKernelGGL(argmax_rows_kernel, dim3(rows), dim3(256), 0, (hipStream_t)s, (const half_t*)x, ld, V, out,
-                     second);
+  hipLaunchKernelGGL(argmax_rows_kernel, dim3(rows), dim3(256), 0, (hipStream_t)s, (const half_t*)x, ld, V, out);
   FLS_CHECK_LAUNCH();
   return 0;
 }

@@ -209,7 +209,7 @@ def build_runner(args, cfg: ModelConfig, device, comm: Comm, tok, prompts=None) 
                          hbm_cache_gb=resolve_hbm_cache_gb(args, cfg, device, reserve),
                          prefix_kv_cache=pkv,
                          prefix_cache_entries=getattr(args, "prefix_cache_entries", 8),
-                         suffix_kv_cache=skv, tie_guard=getattr(args, "tie_guard", True),
+                         suffix_kv_cache=skv,
                          pipeline_stages=getattr(args, "pipeline_stages", "round_robin"),
                          rx_window=getattr(args, "rx_window", 2),
                          max_vram_gb=getattr(args, "max_vram_gb", None))

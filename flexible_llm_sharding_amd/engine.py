@@ -78,11 +78,8 @@ class ShardedRunner:
                  max_token_len: int = MAX_TOKEN_LEN, hip_graphs: bool = False,
                  prefix_kv_cache: bool = False, prefix_cache_entries: int = 8, suffix_kv_cache: bool = False,
                  prune_last_layer: bool = True, pipeline_stages: str = "round_robin",
-                 max_vram_gb: Optional[float] = None, hbm_cache_gb: float = 0.0, rx_window: int = 2,
-                 tie_guard: bool = True):
+                 max_vram_gb: Optional[float] = None, hbm_cache_gb: float = 0.0, rx_window: int = 2):
         self.cfg = cfg
-        # suffix K/V reuse: re-run exactly the prompts whose greedy token is a near tie (_tie_guard)
-        self.tie_guard = tie_guard
         self.src = source
         # layers read from their files every pass (no host-resident copy): host RAM is the limit
         self._streamed_weights = hasattr(source, "stream_into") and source.host_buffer(cfg.layer_names()[0]) is None
@@ -243,9 +240,6 @@ class ShardedRunner:
         self._decode_graphs = None
         self._spec: Optional[dict] = None     # an enqueued speculative generation step
         self.last_tokens: List[Optional[np.ndarray]] = []   # last call's greedy token per suffix
-        # ... and its two largest probabilities ([n_s, 2] fp16 per prompt; the device argmax's
-        # runner-up output): the tie guard's input
-        self.last_top2: List[Optional[np.ndarray]] = []
         if self.cuda and not self.hip_graphs:
             from .models.llama import Workspace
             self.ctx.ws = Workspace(self.dev, self.act_dtype)   # fixed scratch buffers (VRAM plan)
@@ -255,6 +249,8 @@ class ShardedRunner:
             from .runtime.prefix_cache import PrefixKVCache
             self.prefix_cache = PrefixKVCache(2 * cfg.num_key_value_heads * cfg.head_dim, self.dev,
                                               self.act_dtype, prefix_cache_entries, suffix_reuse=suffix_kv_cache)
+        # generation (prefix K/V cache): every call row-exact (see "exact K/V reuse" below)
+        self.row_exact = self.prefix_cache is not None
         self._n_decoders = sum(1 for n in self.names if layer_kind(n) == "decoder")
         self._W_all: Dict[str, Dict[str, torch.Tensor]] = {}
         self._h2d0: Optional[int] = None     # prefetcher byte count at the start of the next call
@@ -385,83 +381,16 @@ class ShardedRunner:
             items += [(k, b) for b in order]
         return items
 
-    # ------------------------------------------------------- generation tie guard
-    # Suffix K/V reuse computes a generation step from K/V kept from earlier steps (other batch
-    # shapes, other GEMM paths), so its probabilities differ from the exact step's in the last fp16
-    # bits.  A greedy token can only differ where a suffix's two largest probabilities are within
-    # that deviation of each other.  After a reused step every prompt with a suffix whose runner-up
-    # probability is within TIE_REL of its best is re-run exactly: prefix K/V from the cache, every
-    # suffix token recomputed, on row-independent kernels (fls.h GEMM_ROW_EXACT), which gives those
-    # prompts bit for bit the scores of the exact step over the whole batch (--suffix_kv_cache
-    # false, whose steps run on the same kernels).  TIE_REL is 8x the largest relative deviation
-    # of the top-2 probabilities measured between reused and exact 70B steps (profiles/r6_gen).
-    TIE_REL = 2.0 ** -5
-
-    def run_tokenized(self, tps: Sequence[TokenizedPrompt]) -> List[Optional[np.ndarray]]:
-        outputs = self._run_tokenized(tps)
-        if (self.tie_guard and self.prefix_cache is not None and self.comm.world == 1
-                and self.stats.get("suffix_tokens_reused", 0.0) > 0):
-            outputs = self._tie_guard(tps, outputs)
-        return outputs
-
-    def _near_ties(self, outputs) -> List[int]:
-        """Prompts with a suffix whose runner-up probability is within TIE_REL of its best (the
-        device argmax's top-2 output; a host pass over the scores where that is missing)."""
-        amb = []
-        for j, o in enumerate(outputs):
-            if o is None:
-                continue
-            t2 = self.last_top2[j] if j < len(self.last_top2) else None
-            if t2 is None:
-                v = np.sort(o.reshape(o.shape[0], -1).astype(np.float32), axis=-1)[:, -2:][:, ::-1]
-            else:
-                v = t2.astype(np.float32)
-            if np.any(v[:, 1] >= v[:, 0] * (1.0 - self.TIE_REL)):
-                amb.append(j)
-        return amb
-
-    def _tie_guard(self, tps, outputs) -> List[Optional[np.ndarray]]:
-        t0 = time.perf_counter()
-        amb = self._near_ties(outputs)
-        stats = dict(self.stats)
-        stats["tie_guard_prompts"] = float(len(amb))
-        if amb:
-            if self._spec is not None:        # the next step was speculated on the reused tokens
-                self._drop_spec(self._spec)
-                self._spec = None
-            tokens, top2 = list(self.last_tokens), list(self.last_top2)
-            exact = self._run_exact_subset(tps, amb)
-            for j in amb:
-                outputs[j] = exact[j]
-                tokens[j] = self.last_tokens[j] if j < len(self.last_tokens) else None
-                top2[j] = self.last_top2[j] if j < len(self.last_top2) else None
-            self.last_tokens, self.last_top2 = tokens, top2
-        stats["tie_guard_s"] = time.perf_counter() - t0
-        self.stats = stats
-        return outputs
-
-    def _run_exact_subset(self, tps, idx: List[int]) -> List[Optional[np.ndarray]]:
-        """The exact step for prompts ``idx`` of this call: prefix K/V from the call's cache entry,
-        every suffix token recomputed (their K/V rewritten into the entry's suffix regions), on
-        row-independent kernels -> outputs indexed like ``tps`` (None outside ``idx``)."""
-        t_start = time.perf_counter()
-        entry = self.prefix_cache.lookup(tps)
-        if entry is None:
-            raise RuntimeError("tie guard: the call's prefix K/V cache entry is gone")
-        sub_tps = [tps[j] for j in idx]
-        rows, _ = entry.suffix_plan(tps, reuse=False)
-        groups = split_microbatches(sub_tps, self.micro_budget(sub_tps, True), suffix_only=True)
-        batches = [pack_prompts([sub_tps[i] for i in g], [idx[i] for i in g], self.prefix_attention,
-                                prefix_offsets=[entry.offsets[idx[i]] for i in g], kv_cached=True,
-                                q_block=self.q_block,
-                                suffix_rows=[rows[idx[i]] for i in g] if rows is not None else None)
-                   for g in groups]
-        self.ctx.prefix_entry = entry
-        try:
-            with self._workspace(), self._row_exact(True):
-                return self._run_batches(tps, batches, t_start)
-        finally:
-            self.ctx.prefix_entry = None
+    # ------------------------------------------------------- exact K/V reuse
+    # With the prefix K/V cache (generation) every call runs row-exact: the GEMMs take only
+    # row-independent kernels (v10 / v11 tiles: a row's result does not depend on M or on the other
+    # rows of the launch), the RMSNorm statistic comes from the row itself, no work item spans two
+    # suffixes and no attention is split over blocks; suffix K/V regions start on 64-row key-tile
+    # boundaries and the attention's deferred rescale is decided per row.  A row's arithmetic is then
+    # the same in every call that computes it: a generation step that reuses the suffixes' cached
+    # K/V (--suffix_kv_cache) and computes only the new tokens gives bit for bit the scores of the
+    # step that recomputes every suffix token (the exact path), so the greedy tokens are the exact
+    # generation's by construction (tests/test_engine_gpu.py::test_suffix_reuse_bitwise_exact).
 
     def _row_exact(self, on: bool):
         """Context: row-independent kernels for this call (ops + the model's row statistics)."""
@@ -481,7 +410,7 @@ class ShardedRunner:
                 ctx.row_exact = self.prev
         return _RowExact()
 
-    def _run_tokenized(self, tps: Sequence[TokenizedPrompt]) -> List[Optional[np.ndarray]]:
+    def run_tokenized(self, tps: Sequence[TokenizedPrompt]) -> List[Optional[np.ndarray]]:
         t_start = time.perf_counter()
         spec, self._spec = self._spec, None
         if spec is not None:
@@ -513,18 +442,16 @@ class ShardedRunner:
                                 prefix_offsets=[entry.offsets[i] for i in g] if entry is not None else None,
                                 kv_cached=cached, q_block=self.q_block,
                                 suffix_rows=[sfx_rows[i] for i in g] if sfx_rows is not None else None,
-                                suffix_keep=[sfx_keep[i] for i in g] if sfx_keep is not None else None)
+                                suffix_keep=[sfx_keep[i] for i in g] if sfx_keep is not None else None,
+                                single_suffix_items=self.row_exact)
                    for g in groups]
         t_pack = time.perf_counter() - t_start
         if self.hip_graphs:
             with self._workspace():
                 return self._run_graphed(tps, batches, t_start)
         self.ctx.prefix_entry = entry
-        # an exact generation step (prefix K/V from the cache, every suffix token computed): the
-        # row-independent kernels, so that the tie guard's re-runs of a few prompts match it bit for bit
-        exact_step = cached and sfx_keep is None
         try:
-            with self._workspace(), self._row_exact(exact_step):
+            with self._workspace(), self._row_exact(self.row_exact):
                 if self._decode_graphable(batches, cached):
                     outputs = self._run_graphed(tps, batches, t_start, entry=entry)
                 else:
@@ -928,7 +855,6 @@ class ShardedRunner:
             px.inbox.end_call()
             rx_stats = {f"rx_{k}": float(v) for k, v in px.inbox.stats.items()}
         self.last_tokens = [None] * len(px.tps)
-        self.last_top2 = [None] * len(px.tps)
         for batch, host, ev, pool_buf, am in px.out_pending:
             self._collect(batch, host.numpy(), am, px.outputs)
             if pool_buf is not None:
@@ -1128,15 +1054,13 @@ class ShardedRunner:
         pending, ams, flops = [], [], 0.0
         for i, batch in enumerate(batches):
             probs = run(batch, i)
-            am, sec = self.ops.argmax_rows(probs, top2=True)
+            am = self.ops.argmax_rows(probs)
             nbytes = probs.numel() * probs.element_size()
-            rows = probs.shape[0]
-            pool_buf = store.host_buffer(nbytes + 8 * rows)
+            pool_buf = store.host_buffer(nbytes + 4 * probs.shape[0])
             host = pool_buf[:nbytes].view(probs.dtype).view(probs.shape)
-            host_am = pool_buf[nbytes:nbytes + 8 * rows].view(torch.int32)
+            host_am = pool_buf[nbytes:nbytes + 4 * probs.shape[0]].view(torch.int32)
             host.copy_(probs, non_blocking=True)     # same stream: ordered before the next replay
-            host_am[:rows].copy_(am, non_blocking=True)
-            host_am[rows:].copy_(sec, non_blocking=True)
+            host_am.copy_(am, non_blocking=True)
             pending.append((batch, host, pool_buf, host_am))
             ams.append(am)
             flops += sum(layer_flops(self.cfg, batch, self._pruned(n)) for n in self.names if layer_kind(n) == "decoder")
@@ -1145,7 +1069,6 @@ class ShardedRunner:
     def _collect_graphed(self, pending, outputs, n_prompts: int) -> None:
         store = self._get_store()
         self.last_tokens = [None] * n_prompts
-        self.last_top2 = [None] * n_prompts
         for batch, host, pool_buf, host_am in pending:
             self._collect(batch, host.numpy(), host_am, outputs)
             store.recycle_host(pool_buf)
@@ -1325,45 +1248,32 @@ class ShardedRunner:
         """Host scores of a finished micro-batch into ``outputs`` (prompt order) and its greedy
         tokens into ``self.last_tokens`` (``am``: the rows' argmax, computed on the device)."""
         am = am.numpy() if am is not None else None
-        rows = probs.shape[0]
-        top2 = None
-        if am is not None and am.shape[0] == 2 * rows:       # [argmax | (max << 16) | runner-up]
-            bits = am[rows:].view(np.uint32)
-            top2 = np.stack([(bits >> 16).astype(np.uint16), (bits & 0xFFFF).astype(np.uint16)], 1).view(np.float16)
-            am = am[:rows]
         r = 0
         for j, pid in enumerate(batch.prompt_ids):
             ns = batch.n_suffix[j]
             outputs[pid] = np.expand_dims(probs[r:r + ns].astype(np.float16, copy=True), axis=1)
             if am is not None:
                 self.last_tokens[pid] = am[r:r + ns].astype(np.int64).reshape(ns, 1)
-            if top2 is not None and len(self.last_top2) > pid:
-                self.last_top2[pid] = top2[r:r + ns]
             r += ns
 
     def _start_output_copy(self, batch: PackedBatch, probs: torch.Tensor):
         """D2H of a micro-batch's probabilities and of their row argmax (the greedy token of
         each suffix: api.generation_loop needs no host pass over the [n_s, V] scores)."""
-        am = self.ops.argmax_rows(probs, top2=True) if hasattr(self.ops, "argmax_rows") else None
+        am = self.ops.argmax_rows(probs) if hasattr(self.ops, "argmax_rows") else None
         if not self.cuda:
-            return (batch, probs.detach().to(torch.float16).cpu(), None, None,
-                    torch.cat([am[0], am[1]]) if am is not None else None)
-        am, sec = am if am is not None else (None, None)
+            return batch, probs.detach().to(torch.float16).cpu(), None, None, am
         store = self._get_store()
         nbytes = probs.numel() * probs.element_size()
-        rows = probs.shape[0]
-        pool_buf = store.host_buffer(nbytes + 8 * rows)
+        pool_buf = store.host_buffer(nbytes + 4 * probs.shape[0])
         host = pool_buf[:nbytes].view(probs.dtype).view(probs.shape)
-        host_am = pool_buf[nbytes:nbytes + 8 * rows].view(torch.int32)
+        host_am = pool_buf[nbytes:nbytes + 4 * probs.shape[0]].view(torch.int32)
         self.d2h_stream.wait_stream(torch.cuda.current_stream(self.dev))
         with torch.cuda.stream(self.d2h_stream):
             host.copy_(probs, non_blocking=True)
             probs.record_stream(self.d2h_stream)
             if am is not None:
-                host_am[:rows].copy_(am, non_blocking=True)
-                host_am[rows:].copy_(sec, non_blocking=True)
+                host_am.copy_(am, non_blocking=True)
                 am.record_stream(self.d2h_stream)
-                sec.record_stream(self.d2h_stream)
             ev = torch.cuda.Event()
             ev.record(self.d2h_stream)
         return batch, host, ev, pool_buf, (host_am if am is not None else None)

@@ -175,7 +175,7 @@ class HipOps:
     def row_exact(self, on: bool = True):
         """Context manager: GEMMs issued by this host thread take only row-independent paths
         (fls.h GEMM_ROW_EXACT; no GEMV / skinny / split-K / mid-M), so each row's result is the same
-        whatever other rows share the launch (engine.ShardedRunner._tie_guard)."""
+        whatever other rows share the launch (engine.ShardedRunner: exact K/V reuse)."""
         ops = self
 
         class _Exact:
@@ -405,7 +405,9 @@ class HipOps:
             out = torch.empty(T, n_q_heads * head_dim, dtype=torch.float16, device=qkv.device)
         # the range-2 (decode-like) kernel splits its key tiles over blocks when the grid is small;
         # its fp32 partials live in the split-K GEMM scratch (same stream: never in use by both)
-        ws = self._splitk_ws(qkv.device, 0, 0) if work2 is not None else None
+        # (row-exact calls: no split, whose merge would round differently from the unsplit kernel)
+        ws = self._splitk_ws(qkv.device, 0, 0) if work2 is not None and not getattr(self._tl, "row_exact", False) \
+            else None
         rc = self.k.fls_attention(qkv.data_ptr(), out.data_ptr(), work.data_ptr(), work.shape[0],
                                   n_q_heads, n_kv_heads, head_dim, qkv.stride(0), out.stride(0),
                                   head_dim ** -0.5 if scale is None else float(scale),
@@ -461,15 +463,13 @@ class HipOps:
                                      _stream()), "fls_softmax")
         return probs
 
-    def argmax_rows(self, probs, top2: bool = False):
-        """[rows] int32: the first index of each row's maximum (non-negative fp16 probabilities).
-        ``top2``: -> (that, [rows] int32 = (max << 16) | runner-up as fp16 bit patterns)."""
+    def argmax_rows(self, probs):
+        """[rows] int32: the first index of each row's maximum (non-negative fp16 probabilities)."""
         _f16(probs, "probs")
         out = torch.empty(probs.shape[0], dtype=torch.int32, device=probs.device)
-        sec = torch.empty(probs.shape[0], dtype=torch.int32, device=probs.device) if top2 else None
         _chk(self.k.fls_argmax_rows(probs.data_ptr(), probs.stride(0), probs.shape[0], probs.shape[1],
-                                    out.data_ptr(), sec.data_ptr() if top2 else None, _stream()), "fls_argmax_rows")
-        return (out, sec) if top2 else out
+                                    out.data_ptr(), _stream()), "fls_argmax_rows")
+        return out
 
     def lm_head_softmax(self, h, w, logits_scaling: float = 1.0):
         return self.softmax(self.linear(h, w), logits_scaling)

@@ -203,15 +203,8 @@ class TorchOps:
         import contextlib
         return contextlib.nullcontext()
 
-    def argmax_rows(self, probs: torch.Tensor, top2: bool = False):
-        """First index of each row's maximum; ``top2``: also (max << 16) | runner-up of the fp16
-        probabilities as bit patterns (HipOps.argmax_rows)."""
-        idx = probs.float().argmax(-1).to(torch.int32)
-        if not top2:
-            return idx
-        v = probs.to(torch.float16).topk(2, dim=-1).values if probs.shape[-1] > 1 else probs.to(torch.float16).repeat(1, 2)
-        b = v.contiguous().view(torch.int16).to(torch.int32) & 0xFFFF
-        return idx, ((b[:, 0] << 16) | b[:, 1]).to(torch.int32)
+    def argmax_rows(self, probs: torch.Tensor) -> torch.Tensor:
+        return probs.float().argmax(-1).to(torch.int32)
 
     def softmax(self, logits: torch.Tensor, logits_scaling: float = 1.0) -> torch.Tensor:
         if logits_scaling != 1.0:                            # Granite: logits / logits_scaling

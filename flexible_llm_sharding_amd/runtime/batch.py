@@ -205,7 +205,8 @@ def pack_prompts(tps: Sequence[TokenizedPrompt], prompt_ids: Sequence[int],
                  prefix_attention: str = "bidirectional", prefix_offsets: Optional[Sequence[int]] = None,
                  kv_cached: bool = False, q_block: int = Q_BLOCK,
                  suffix_rows: Optional[Sequence[Sequence[int]]] = None,
-                 suffix_keep: Optional[Sequence[Sequence[int]]] = None) -> PackedBatch:
+                 suffix_keep: Optional[Sequence[Sequence[int]]] = None,
+                 single_suffix_items: bool = False) -> PackedBatch:
     """Pack prompts into one token matrix + attention work items.
 
     ``prefix_offsets`` (rows of each prompt's prefix in a PrefixEntry) turns on
@@ -218,6 +219,11 @@ def pack_prompts(tps: Sequence[TokenizedPrompt], prompt_ids: Sequence[int],
     there — and ``suffix_keep[j][s]`` (with ``kv_cached``) the number of its leading tokens whose
     K/V the cache already holds: only the tokens after them are packed and computed, at their true
     positions, and each suffix gets work items of its own whose range 2 covers the kept rows.
+
+    ``single_suffix_items``: no work item spans two suffixes, so every key tile of range 1 starts
+    at a multiple of 64 tokens from its suffix's first token, as the range-2 tiles of a reused step
+    do over 64-row-aligned cache regions (generation with the prefix K/V cache: each row's attention
+    then takes the same tiles, whichever step computes it; engine ``row_exact``).
     """
     if prefix_attention not in ("bidirectional", "causal"):
         raise ValueError(prefix_attention)
@@ -286,8 +292,11 @@ def pack_prompts(tps: Sequence[TokenizedPrompt], prompt_ids: Sequence[int],
         # the prompt's suffix rows [sfx0, t) in q_block chunks; range 1 of a chunk starts at the
         # suffix holding its first row.  Suffix K/V reuse: range 2 of every chunk spans the kept
         # rows of all the prompt's suffixes, each row seeing only its own suffix's window (r2win)
-        for c0 in range(sfx0, t, q_block):
-            c1 = min(c0 + q_block, t)
+        chunks = [(c0, min(c0 + q_block, t)) for c0 in range(sfx0, t, q_block)]
+        if single_suffix_items and keep is None:
+            chunks = [(s0 + o, min(s0 + o + q_block, s0 + n)) for sg in segs if sg.r1_len and sg.q_start >= sfx0
+                      for s0, n in [(sg.q_start, sg.q_len)] for o in range(0, n, q_block)]
+        for c0, c1 in chunks:
             if keep is not None:
                 w = r2win[c0:c1]
                 lo, hi = min(a for a, _ in w), max(b for _, b in w)

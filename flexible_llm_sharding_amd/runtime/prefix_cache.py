@@ -61,6 +61,8 @@ def common_prefix(a: Sequence[int], b: Sequence[int]) -> int:
 
 
 class PrefixEntry:
+    REGION_ALIGN = 64      # attention key tile (csrc/kernels/attention.hip KT)
+
     def __init__(self, key: str, prefix_lens: Sequence[int], kv_cols: int, device, dtype,
                  suffix_caps: Optional[Sequence[Sequence[int]]] = None):
         self.key = key
@@ -77,6 +79,9 @@ class PrefixEntry:
             self.sfx_rows.append([])
             self.sfx_caps.append(list(caps))
             for c in caps:
+                # every region starts on a 64-row key-tile boundary: a reused step's range-2 tiles
+                # then split each suffix's keys exactly as the full computation's range-1 tiles do
+                t = -(-t // self.REGION_ALIGN) * self.REGION_ALIGN
                 self.sfx_rows[-1].append(t)
                 t += c
         self.sfx_ids: Dict[tuple, tuple] = {}
@@ -90,7 +95,9 @@ class PrefixEntry:
     def buffer(self, layer_name: str, create: bool = False) -> Optional[torch.Tensor]:
         b = self.layers.get(layer_name)
         if b is None and create:
-            b = torch.empty(max(1, self.rows), self.kv_cols, dtype=self.dtype, device=self.dev)
+            # zeroed: a reused step's key tiles cover the alignment gaps and unused region rows (masked,
+            # P = 0 exactly, and 0 x a finite V adds nothing)
+            b = torch.zeros(max(1, self.rows), self.kv_cols, dtype=self.dtype, device=self.dev)
             self.layers[layer_name] = b
         return b
 

@@ -60,13 +60,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--suffix_kv_cache", type=bool_or_auto, nargs="?", const=True, default="auto",
                    help="with the prefix K/V cache: also keep every suffix's K/V and, in the next call (generation "
                         "step), compute only the tokens after the longest common token prefix with the last call's "
-                        "suffix (each step then costs its new tokens).  Scores agree with the exact re-computation to "
-                        "fp16 rounding; a tie guard re-runs exactly every prompt whose greedy token is a near tie, so "
-                        "the generated tokens are the exact path's (PARITY.md C21).  auto (default): on with the "
-                        "prefix K/V cache on one GPU")
-    p.add_argument("--tie_guard", type=str2bool, nargs="?", const=True, default=True,
-                   help="with --suffix_kv_cache: re-run exactly the prompts whose top-2 probabilities are within "
-                        "the measured reuse deviation (false: keep the reused step's tokens)")
+                        "suffix (each step then costs its new tokens).  Exact: with the prefix cache every call runs "
+                        "row-independent kernels, so a reused step's scores are bit for bit those of recomputing "
+                        "every suffix token (PARITY.md C21).  auto (default): on with the prefix K/V cache on one GPU")
     p.add_argument("--prefix_cache_entries", type=int, default=8,
                    help="prefix K/V cache: calls (prompt batches) kept, LRU")
     p.add_argument("--resident", type=str2bool, nargs="?", const=True, default=False,

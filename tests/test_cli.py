@@ -225,13 +225,12 @@ def test_repeated_pass_defaults():
     with pytest.raises(ValueError):
         resolve_prefix_kv_cache(parse_args(base + ["--num_gen_token", "4", "--max_vram_gb", "6",
                                                    "--prefix_kv_cache", "true"]))
-    # suffix K/V reuse is on by default with the prefix cache on one GPU (the tie guard keeps the
-    # greedy tokens the exact path's); off on several ranks and without the prefix cache
+    # suffix K/V reuse is on by default with the prefix cache on one GPU (exact: row-independent
+    # kernels, engine "exact K/V reuse"); off on several ranks and without the prefix cache
     from flexible_llm_sharding_amd.api import resolve_suffix_kv_cache
     assert g.suffix_kv_cache == "auto" and resolve_suffix_kv_cache(g, 1) and not resolve_suffix_kv_cache(g, 2)
     assert not resolve_suffix_kv_cache(a, 1) and not resolve_suffix_kv_cache(capped, 1)
     assert not resolve_suffix_kv_cache(parse_args(base + ["--num_gen_token", "4", "--suffix_kv_cache", "false"]), 1)
-    assert g.tie_guard is True
     assert parse_args(base + ["--hbm_cache_gb", "12.5"]).hbm_cache_gb == 12.5
     cfg = preset("tiny")
     assert resolve_hbm_cache_gb(g, cfg, torch.device("cpu")) == 0.0       # nothing to cache on a CPU run

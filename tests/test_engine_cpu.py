@@ -418,44 +418,34 @@ def test_config_rope_and_head_dim_forms(tmp_path):
     assert ModelConfig.from_pretrained(str(tmp_path)) == c
 
 
-@pytest.mark.parametrize("rel", [1.0, 0.0])
-def test_tie_guard_reruns_near_ties(tiny_model, rel):
-    """Suffix K/V reuse with the tie guard: after a reused step, every prompt with a suffix whose
-    runner-up probability is within TIE_REL of its best is re-run exactly (prefix K/V from the
-    cache, all suffix tokens).  TIE_REL = 1: every prompt, every reused step; 0: only exact ties.
-    Tokens == the exact generation, scores within rounding."""
-    from flexible_llm_sharding_amd.api import generation_loop
-    from flexible_llm_sharding_amd.engine import ShardedRunner
-    from flexible_llm_sharding_amd.parallel.comm import Comm
-    from flexible_llm_sharding_amd.runtime.weights import HostStore
-    from flexible_llm_sharding_amd.utils.synthetic import synthetic_prompts
-    from flexible_llm_sharding_amd.utils.tokenizer import load_tokenizer
-    import argparse
-    path, cfg = tiny_model
-    tok = load_tokenizer(path)
-    prompts = synthetic_prompts(5, 40, 3, 6, cfg.vocab_size, seed=23, vary=True)
-    src = HostStore.from_model_path(cfg, path, pinned=False)
-    args = argparse.Namespace(num_gen_token=4, data_parallel=False, num_batch=1)
-    exact = ShardedRunner(cfg, src, "cpu", tok, layer_num_per_shard=2, prefix_kv_cache=True, suffix_kv_cache=False)
-    s0, u0 = generation_loop(args, exact, Comm(), tok, prompts)
-    r = ShardedRunner(cfg, src, "cpu", tok, layer_num_per_shard=2, prefix_kv_cache=True, suffix_kv_cache=True)
-    r.TIE_REL = rel
-    guarded = []
-    orig = r._tie_guard
-
-    def spy(tps, outputs):
-        out = orig(tps, outputs)
-        guarded.append(r.stats["tie_guard_prompts"])
-        return out
-    r._tie_guard = spy
-    s1, u1 = generation_loop(args, r, Comm(), tok, prompts)
-    assert u0 == u1
-    for a, b in zip(s0, s1):
-        assert np.abs(a.astype(np.float32) - b.astype(np.float32)).max() < 1e-5
-    assert len(guarded) == args.num_gen_token - 1                  # every reused step was checked
-    if rel == 1.0:
-        assert guarded == [float(len(prompts))] * len(guarded)
-    assert r.stats["suffix_tokens_reused"] > 0 and "tie_guard_s" in r.stats
+def test_row_exact_packing_and_regions():
+    """Generation packing (engine row_exact): no work item spans two suffixes (each item's range 1
+    starts at its own suffix's first token, so key tiles sit at multiples of 64 tokens from it), and
+    every suffix K/V region of a cache entry starts on a 64-row tile boundary, zero-filled."""
+    from flexible_llm_sharding_amd.runtime.prefix_cache import PrefixEntry
+    from flexible_llm_sharding_amd.utils.tokenizer import TokenizedPrompt
+    tps = [TokenizedPrompt(list(range(lp)), [list(range(n)) for n in ns], max(ns), [n - 1 for n in ns])
+           for lp, ns in ((70, [5, 64, 1, 130]), (1, [3]), (9, [40, 30, 30]))]
+    for kv_cached in (False, True):
+        offs = [0, 70, 71]
+        b = pack_prompts(tps, [0, 1, 2], "bidirectional", prefix_offsets=offs, kv_cached=kv_cached, q_block=64,
+                         single_suffix_items=True)
+        seen = set()
+        for q_start, q_len, q_off, r0s, r0l, r0c, r1s, r1l in b.work.tolist():
+            if not r1l:
+                continue
+            rows = range(q_start, q_start + q_len)
+            assert {int(b.seg_lo[r]) for r in rows} == {r1s}                # one suffix per item
+            assert q_off == q_start - r1s and r1l == q_off + q_len
+            seen.update(rows)
+        assert seen == {r for sg in b.segments if sg.r1_len for r in range(sg.q_start, sg.q_start + sg.q_len)}
+        multi = pack_prompts(tps, [0, 1, 2], "bidirectional", prefix_offsets=offs, kv_cached=kv_cached, q_block=64)
+        assert any(len({int(multi.seg_lo[r]) for r in range(w[0], w[0] + w[1])}) > 1 for w in multi.work.tolist())
+    e = PrefixEntry("k", [70, 1, 9], 16, "cpu", torch.float16, suffix_caps=[[69, 128, 65, 194], [67], [104, 94, 94]])
+    starts = [r for rows in e.sfx_rows for r in rows]
+    assert all(r % 64 == 0 for r in starts) and starts[0] >= 80 and len(set(starts)) == len(starts)
+    buf = e.buffer("model.layers.0", create=True)
+    assert buf.shape[0] >= starts[-1] + 94 and not buf.any()
 
 
 @pytest.mark.parametrize("num_batch_calls", [1, 2])

@@ -421,7 +421,7 @@ def test_decode_graphs_match_eager(setup, weights):
         os.environ["FLS_DECODE_GRAPHS"] = graphs
         try:
             r = ShardedRunner(cfg, src, "cuda:0", tok, layer_num_per_shard=1, prefix_kv_cache=True,
-                              suffix_kv_cache=True, tie_guard=False, **kw)
+                              suffix_kv_cache=True, **kw)
             words = prompts[0][0].split()
             steps = []
             for step in range(5):
@@ -457,7 +457,7 @@ def test_decode_graphs_survive_entry_eviction(setup):
         os.environ["FLS_DECODE_GRAPHS"] = graphs
         try:
             r = ShardedRunner(cfg, src, "cuda:0", tok, layer_num_per_shard=1, prefix_kv_cache=True,
-                              suffix_kv_cache=True, resident=True, prefix_cache_entries=1, tie_guard=False)
+                              suffix_kv_cache=True, resident=True, prefix_cache_entries=1)
             steps = []
             for rnd in range(2):
                 for ps0 in (prompts, other):
@@ -496,7 +496,7 @@ def test_speculative_generation_steps_bitwise(setup, mode):
         os.environ["FLS_SPEC_DECODE"] = spec
         try:
             r = ShardedRunner(cfg, src, "cuda:0", tok, layer_num_per_shard=1, prefix_kv_cache=True,
-                              suffix_kv_cache=True, resident=True, tie_guard=False)
+                              suffix_kv_cache=True, resident=True)
             if spec == "1" and mode == "mismatch":
                 r._spec_matches = lambda s, tps: False
             outs[spec] = generation_loop(args, r, Comm(), tok, prompts)
@@ -518,56 +518,36 @@ def test_speculative_generation_steps_bitwise(setup, mode):
 
 
 @pytest.mark.parametrize("weights", ["resident", "streamed"])
-def test_tie_guard_reruns_are_bitwise_exact(setup, weights):
-    """The tie guard's exact re-run of a few prompts (row-independent kernels, prefix K/V from the
-    cache) gives those prompts bit for bit the scores of the exact generation over the whole batch
-    (--suffix_kv_cache false): prompts 1 and 3 forced through the guard at every reused step keep
-    the exact run's scores and tokens at every step, whatever the other prompts' reused steps do
-    (decode graphs and speculative steps on resident weights; eager on streamed ones)."""
+def test_suffix_reuse_bitwise_exact(setup, weights):
+    """Generation with suffix K/V reuse (only each suffix's new tokens computed, the kept K/V read
+    as range 2) == the exact generation (--suffix_kv_cache false: every suffix token recomputed each
+    step) BIT FOR BIT at every step: with the prefix cache every call runs row-independent kernels,
+    64-row-aligned suffix regions and single-suffix work items, so a row's arithmetic does not depend
+    on which call computes it.  Suffixes of 40-70 tokens grow past the 64-key tile boundary; decode
+    graphs + speculative steps (resident) and eager steps (streamed weights)."""
     import argparse
     from flexible_llm_sharding_amd.api import generation_loop
     from flexible_llm_sharding_amd.parallel.comm import Comm
-    path, cfg, tok, prompts, ref = setup
+    path, cfg, tok, _, _ = setup
+    prompts = synthetic_prompts(5, 90, 4, 70, cfg.vocab_size, seed=11, vary=True)
     src = HostStore.from_model_path(cfg, path)
     kw = {"resident": True} if weights == "resident" else {}
-    args = argparse.Namespace(num_gen_token=5, data_parallel=False, num_batch=1)
-    exact = ShardedRunner(cfg, src, "cuda:0", tok, layer_num_per_shard=1, prefix_kv_cache=True,
-                          suffix_kv_cache=False, **kw)
-    s0, u0 = generation_loop(args, exact, Comm(), tok, prompts)
-    exact.close()
-    r = ShardedRunner(cfg, src, "cuda:0", tok, layer_num_per_shard=1, prefix_kv_cache=True, suffix_kv_cache=True,
-                      **kw)
-    forced = [j for j in (1, 3) if j < len(prompts)]
-    r._near_ties = lambda outputs: list(forced)
-    s1, u1 = generation_loop(args, r, Comm(), tok, prompts)
-    assert r.stats["tie_guard_prompts"] == len(forced) and r.stats["suffix_tokens_reused"] > 0
-    r.close()
-    for j in forced:
-        assert u0[j] == u1[j]
-        assert np.array_equal(s0[j], s1[j])
-    for a, b in zip(s0, s1):
-        assert np.isfinite(a.astype(np.float32)).all() and np.isfinite(b.astype(np.float32)).all()
-
-
-def test_tie_guard_default_tokens_exact(setup):
-    """Default flags (suffix K/V reuse + tie guard, resident weights, decode graphs, speculation):
-    the generated tokens == the exact generation's; scores within fp16 rounding."""
-    import argparse
-    from flexible_llm_sharding_amd.api import generation_loop
-    from flexible_llm_sharding_amd.parallel.comm import Comm
-    path, cfg, tok, prompts, ref = setup
-    src = HostStore.from_model_path(cfg, path)
-    args = argparse.Namespace(num_gen_token=6, data_parallel=False, num_batch=1)
+    args = argparse.Namespace(num_gen_token=8, data_parallel=False, num_batch=1)
     outs = {}
     for sfx in (False, True):
         r = ShardedRunner(cfg, src, "cuda:0", tok, layer_num_per_shard=1, prefix_kv_cache=True, suffix_kv_cache=sfx,
-                          resident=True)
+                          **kw)
         outs[sfx] = generation_loop(args, r, Comm(), tok, prompts)
+        if sfx:
+            assert r.stats["suffix_tokens_reused"] > 0
+            if weights == "resident":
+                assert r.stats.get("graph_replays", 0) >= 1
         r.close()
     (s0, u0), (s1, u1) = outs[False], outs[True]
     assert u0 == u1
     for a, b in zip(s0, s1):
-        assert np.abs(a.astype(np.float32) - b.astype(np.float32)).max() < 2e-3
+        assert np.isfinite(a.astype(np.float32)).all()
+        assert np.array_equal(a, b)
 
 
 def test_piece_pool_streams_layer_files(mid_model, tmp_path):

@@ -1014,12 +1014,3 @@ def test_argmax_rows_first_index(ops):
     torch.cuda.synchronize()
     assert np.array_equal(got.cpu().numpy(), np.argmax(x.cpu().numpy(), axis=-1))
     assert got[3].item() == 100 and got[5].item() == 0
-    # the tie guard's top-2: (max << 16) | runner-up as fp16 bits; a repeated maximum is its own runner-up
-    idx, sec = ops.argmax_rows(x, top2=True)
-    torch.cuda.synchronize()
-    assert torch.equal(idx, got)
-    bits = sec.cpu().numpy().view(np.uint32)
-    top = np.stack([(bits >> 16).astype(np.uint16), (bits & 0xFFFF).astype(np.uint16)], 1).view(np.float16)
-    want = np.sort(x.cpu().numpy().astype(np.float32), axis=-1)[:, -2:][:, ::-1]
-    assert np.array_equal(top.astype(np.float32), want)
-    assert top[3, 0] == top[3, 1] == np.float16(0.5) and top[5, 0] == top[5, 1] == 0
