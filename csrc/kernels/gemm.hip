@@ -461,6 +461,7 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
       if (e.pos) e.pos += r0;
       if (e.R) e.R += (size_t)r0 * e.ldr;
       if (e.ss) e.ss += (size_t)r0 * e.ss_ld;
+      if (e.rs) e.rs += r0;                  // (the fused norm's per-row statistic follows its rows)
       const int rc = launch<EPI>(A + (size_t)r0 * lda, W, C + (size_t)r0 * ldc, min(step, M - r0), N, K, lda, ldw,
                                  ldc, e, s, ws, ws_bytes);
       if (rc) return rc;

@@ -133,5 +133,5 @@ def engine(n_layers=2, n_prompts=8, gen=4, graphs="1", prune=True, suffix_len=64
 
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "engine":
-    for kw in ({"n_prompts": 24, "gen": 2}, {"n_prompts": 24, "gen": 2, "n_layers": 1}):
+    for kw in ({"n_prompts": 24}, {"n_prompts": 40}, {"n_prompts": 48}, {"n_prompts": 64, "n_layers": 4}):
         print("engine", engine(**kw), flush=True)

@@ -982,6 +982,25 @@ def test_resid_gemm_row_sum_squares(ops, path, M):
     assert torch.allclose(rs, rr, rtol=2e-6, atol=0)
 
 
+@pytest.mark.parametrize("v11", [0, 2])
+def test_row_scale_past_row_chunk(ops, v11):
+    """The fused norm's per-row scale on a launch cut into row chunks (v10: <= 16,384 rows a launch):
+    every chunk reads its own rows' statistic (a second chunk once read the first chunk's)."""
+    M, N, K = 16384 + 700, 256, 128
+    x = rnd(M, K, seed=141)
+    w = rnd(N, K, scale=0.05, seed=142)
+    rs = (torch.rand(M, generator=torch.Generator().manual_seed(143)) + 0.5).float().to(DEV)
+    old = ops.k.fls_gemm_set_v11(v11)
+    try:
+        y = ops.gemm(x, w, rscale=rs)
+    finally:
+        ops.k.fls_gemm_set_v11(old)
+    torch.cuda.synchronize()
+    want = (x.float() @ w.float().t()) * rs[:, None]
+    assert rel_err(y, want) < 3e-3
+    assert rel_err(y[16384:], want[16384:]) < 3e-3
+
+
 def test_embed_scaled(ops, ref):
     """Granite's embedding_multiplier inside the gather: fp16(e * m) == torch, bitwise."""
     table = rnd(1000, 512, seed=121)
