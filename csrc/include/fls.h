@@ -62,8 +62,8 @@ void    fls_f32_to_f16(const float* src, uint16_t* dst, uint64_t n);
 int fls_kernels_version(void);
 // epilogue codes for fls_gemm
 enum { FLS_EPI_NONE = 0, FLS_EPI_RESID = 1, FLS_EPI_SWIGLU = 2, FLS_EPI_ROPE = 3 };
-// or'd into epi: row-independent arithmetic only (the v10 / v11 tiles, else the generic kernel; no
-// skinny, split-K or mid-M path), so a row's result does not depend on M or on the other rows: the
+// or'd into epi: row-independent arithmetic only (the v10 / v11 / mid-M tiles, else the generic
+// kernel; no skinny or split-K path), so a row's result does not depend on M or on the other rows: the
 // generation tie guard re-runs a subset of prompts bit-identically to the whole batch
 #define FLS_GEMM_ROW_EXACT 0x100
 // C[M, N'] = epi(acc), acc[m] = rscale[m] * (A[M,K] . W[N,K]^T)[m] (+ bias)  (rscale may be null:

@@ -425,7 +425,7 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
     FLS_CHECK_LAUNCH();
     return 0;
   }
-  if (mid_ok && !ep.row_exact && (!main_ok || (g_mid && (tiles256 < 128 || (M <= 64 && tiles256 < 512))))) {
+  if (mid_ok && (!main_ok || (g_mid && (tiles256 < 128 || (M <= 64 && tiles256 < 512))))) {
     static bool attr_mid = false;
     if (!attr_mid) {
       (void)hipFuncSetAttribute((const void*)gemm_nt_mid<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -55,8 +55,8 @@ struct Epi {
   // (fls_rstd_from_ss) -- the separate pass over the hidden state (row_rstd) is not needed
   float* ss = nullptr;
   int ss_ld = 0;
-  // FLS_GEMM_ROW_EXACT: only the row-independent paths (v10 / v11 tiles, or the generic kernel for
-  // shapes they do not take): every output row gets the same arithmetic whatever M and the other rows
+  // FLS_GEMM_ROW_EXACT: only the row-independent paths (v10 / v11 / mid-M tiles, or the generic kernel
+  // for shapes they do not take): every output row gets the same arithmetic whatever M and the other rows
   int row_exact = 0;
 };
 
@@ -114,33 +114,39 @@ __device__ __forceinline__ void store_pair_off(half_t* __restrict__ C, int ldc, 
   }
 }
 
-// RoPE pair: columns ca (first half of a head) and ca + hd/2 of row m; f = ca % hd.
+// RoPE pair: columns ca (first half of a head) and ca + hd/2 of row m; f = ca % hd.  The arithmetic
+// is epilogue_rope's, expression for expression (x = acc * s + bias, then the rotation), so the mid-M
+// kernel's rows are bitwise the v10 / v11 rows (row-exact calls take either)
 __device__ __forceinline__ void store_rope_pair(half_t* __restrict__ C, int ldc, int m, int ca, const floatx4& acc_a,
                                                 const floatx4& acc_b, const Epi& ep) {
   const int hd = ep.head_dim, half_hd = hd >> 1;
   const int cb = ca + half_hd;
   const float s = row_scale(ep, m);
-  floatx4 a = acc_a * s, b = acc_b * s;
+  half4 ba = half4{0, 0, 0, 0}, bb = half4{0, 0, 0, 0};
   if (ep.bias) {
-    const half4 ba = *(const half4*)(ep.bias + ca);
-    const half4 bb = *(const half4*)(ep.bias + cb);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) { a[r] += (float)ba[r]; b[r] += (float)bb[r]; }
+    ba = *(const half4*)(ep.bias + ca);
+    bb = *(const half4*)(ep.bias + cb);
   }
-  if (ca < ep.rope_cols) {
+  const bool rot = ca < ep.rope_cols;
+  floatx4 cs, sn;
+  if (rot) {
     const int p = ep.pos[m];
-    const floatx4 cs = *(const floatx4*)(ep.cos_t + (size_t)p * half_hd + (ca % hd));
-    const floatx4 sn = *(const floatx4*)(ep.sin_t + (size_t)p * half_hd + (ca % hd));
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float x1 = a[r], x2 = b[r];
-      a[r] = x1 * cs[r] - x2 * sn[r];
-      b[r] = x2 * cs[r] + x1 * sn[r];
-    }
+    cs = *(const floatx4*)(ep.cos_t + (size_t)p * half_hd + (ca % hd));
+    sn = *(const floatx4*)(ep.sin_t + (size_t)p * half_hd + (ca % hd));
   }
   half4 oa, ob;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) { oa[r] = (half_t)a[r]; ob[r] = (half_t)b[r]; }
+  for (int r = 0; r < 4; ++r) {
+    float x1 = __builtin_fmaf(acc_a[r], s, (float)ba[r]), x2 = __builtin_fmaf(acc_b[r], s, (float)bb[r]);
+    if (rot) {
+      const float c = cs[r], sv = sn[r];
+      const float y1 = __builtin_fmaf(x1, c, -(x2 * sv)), y2 = __builtin_fmaf(x2, c, x1 * sv);
+      x1 = y1;
+      x2 = y2;
+    }
+    oa[r] = (half_t)x1;
+    ob[r] = (half_t)x2;
+  }
   *(half4*)(C + (size_t)m * ldc + ca) = oa;
   *(half4*)(C + (size_t)m * ldc + cb) = ob;
 }
@@ -226,10 +232,12 @@ __device__ __forceinline__ void epilogue_rope(half_t* __restrict__ C, int ldc, i
       const int ta = HD == 128 ? q : (q & 1) + (q >> 1) * 4;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float x1 = acc[u][ta][r] * s + (float)ba[q][r], x2 = acc[u][ta + HS][r] * s + (float)bb[q][r];
+        // explicit fmas: every kernel with a RoPE epilogue rounds the same way (store_rope_pair)
+        float x1 = __builtin_fmaf(acc[u][ta][r], s, (float)ba[q][r]);
+        float x2 = __builtin_fmaf(acc[u][ta + HS][r], s, (float)bb[q][r]);
         if (rot[q]) {
           const float c = cs[sl][q][r], sv = sn[sl][q][r];
-          const float y1 = x1 * c - x2 * sv, y2 = x2 * c + x1 * sv;
+          const float y1 = __builtin_fmaf(x1, c, -(x2 * sv)), y2 = __builtin_fmaf(x2, c, x1 * sv);
           x1 = y1;
           x2 = y2;
         }

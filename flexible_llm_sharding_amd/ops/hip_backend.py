@@ -174,7 +174,7 @@ class HipOps:
 
     def row_exact(self, on: bool = True):
         """Context manager: GEMMs issued by this host thread take only row-independent paths
-        (fls.h GEMM_ROW_EXACT; no GEMV / skinny / split-K / mid-M), so each row's result is the same
+        (fls.h GEMM_ROW_EXACT; no GEMV / skinny / split-K), so each row's result is the same
         whatever other rows share the launch (engine.ShardedRunner: exact K/V reuse)."""
         ops = self
 

@@ -49,6 +49,17 @@ def gemms(ops):
             part = fn(x[:sub].contiguous(), pos[:sub].contiguous(), rs[:sub].contiguous())
             torch.cuda.synchronize()
             res[name] = bool(torch.equal(full[:sub], part))
+            # the 64 x 128 mid-M kernel on the same rows (not row-exact: forced by the setters)
+            with ops.row_exact(False):
+                old = (ops.k.fls_gemm_set_v11(0), ops.k.fls_gemm_set_skinny(0, 0), ops.k.fls_gemm_set_splitk(0))
+                try:
+                    mid = fn(x[:sub].contiguous(), pos[:sub].contiguous(), rs[:sub].contiguous())
+                finally:
+                    ops.k.fls_gemm_set_v11(old[0])
+                    ops.k.fls_gemm_set_skinny(old[1], 0)
+                    ops.k.fls_gemm_set_splitk(old[2])
+            torch.cuda.synchronize()
+            res[name + "_mid"] = bool(torch.equal(full[:sub], mid))
     return res
 
 
