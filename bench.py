@@ -132,6 +132,13 @@ def parse(argv=None):
                          "host cache, like the dtype cast), or as each layer lands in HBM on every pass (on the "
                          "copy stream, from the checkpoint's own bytes; -1.0%%: profiles/r6_head).  --weights "
                          "stream always folds on landing")
+    ap.add_argument("--emulate-dp-fanout", default="none", choices=["none", "blit", "sdma", "cu32"],
+                    help="measurement only (1 GPU, piece pool): after each weight piece lands, copy 7/8 of its bytes "
+                         "HBM -> HBM on the copy stream, the per-rank traffic of the 8-GPU data-parallel all-gather: "
+                         "blit = the HIP runtime's copy kernel, cu32 = a 32-workgroup copy kernel (RCCL-like "
+                         "channels), sdma = hipMemcpyDeviceToDeviceNoCU (copy engines, no compute unit)")
+    ap.add_argument("--emulate-dp-slice", action="store_true",
+                    help="with --emulate-dp-fanout: H2D only a rank's 1/8 of each piece (timing only: stale weights)")
     ap.add_argument("--prefix-attention", default="bidirectional")
     ap.add_argument("--weights", default="host", choices=["host", "stream"])
     ap.add_argument("--ckpt-dir", default=None, help="--weights stream: layer-file directory (written if absent)")
@@ -427,6 +434,13 @@ def main(argv=None):
         clear_prefix_ids()
         runner(prompts)
         log(rank, f"[bench] warmup {i}: {time.perf_counter() - tw:.2f}s")
+        if i == 0 and (a.emulate_dp_fanout != "none" or a.emulate_dp_slice):
+            # (after one full pass: every weight slot holds real weights, so a slice-only run computes
+            # on stale random weights, not on the zeros of fresh slots -- MFMA power depends on the data)
+            # 256 MB of write target (outside the plan: run with --max-vram-gb 6.3)
+            mode = {"none": -1, "blit": 0, "sdma": 1, "cu32": 2}[a.emulate_dp_fanout]
+            runner.prefetcher.emulate_fanout = (mode, 32, torch.empty(256 << 20, dtype=torch.uint8, device=dev),
+                                                a.emulate_dp_slice)
     comm.barrier()
     sync()
     t_start = time.perf_counter()
@@ -511,6 +525,7 @@ def main(argv=None):
                    # the last decoder layer computes only the scored rows (K/V for every token);
                    # tokens/s counts every token either way (--no-prune-last: A/B)
                    "prune_last_layer": not a.no_prune_last,
+                   "emulate_dp_fanout": a.emulate_dp_fanout, "emulate_dp_slice": a.emulate_dp_slice,
                    "max_vram_gb": a.max_vram_gb, "cap_fallback": cap_note},
     }
     if rank == 0:

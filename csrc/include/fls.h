@@ -94,6 +94,8 @@ int fls_row_rstd(const void* x, int ldx, const int* row_idx, int rows, int H, fl
 // the projection that consumes the normed rows)
 int fls_fold_norm(void* w, int ldw, int N, int K, const void* gamma, fls_stream_t s);
 // y[dst_idx[r]] = x[src_idx[r]] for r < rows (fp16 rows of H elements; a null index = identity)
+// device-to-device copy: mode 0 HIP runtime (blit kernel), 1 SDMA engines (no CU), 2 `blocks` workgroups
+int fls_copy_d2d(void* dst, const void* src, uint64_t bytes, int mode, int blocks, fls_stream_t s);
 int fls_copy_rows(const void* x, int ldx, const int* src_idx, void* y, int ldy, const int* dst_idx, int rows, int H,
                   fls_stream_t s);
 int fls_gemm_set_splitk(int on);

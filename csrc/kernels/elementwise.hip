@@ -510,6 +510,29 @@ extern "C" int fls_fold_norm(void* w, int ldw, int N, int K, const void* gamma, 
   return 0;
 }
 
+// grid-stride 16-byte copy on a fixed number of workgroups (an RCCL-like channel count)
+__global__ __launch_bounds__(256) void copy_blocks_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                        size_t n16) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256) dst[i] = src[i];
+}
+
+// device-to-device copy of `bytes` (16-byte multiple): mode 0 the HIP runtime's copy (a blit kernel on
+// the CUs), 1 hipMemcpyDeviceToDeviceNoCU (the SDMA engines, no compute unit), 2 copy_blocks_kernel on
+// `blocks` workgroups.  bench.py --emulate-dp-fanout: the data-parallel weight all-gather's HBM traffic
+// on one GPU, on the CUs or off them
+extern "C" int fls_copy_d2d(void* dst, const void* src, uint64_t bytes, int mode, int blocks, fls_stream_t s) {
+  if (!bytes) return 0;
+  if (bytes % 16) return -2;
+  if (mode == 2) {
+    hipLaunchKernelGGL(copy_blocks_kernel, dim3(blocks > 0 ? blocks : 32), dim3(256), 0, (hipStream_t)s,
+                       (const uint4*)src, (uint4*)dst, (size_t)(bytes / 16));
+    FLS_CHECK_LAUNCH();
+    return 0;
+  }
+  return hipMemcpyAsync(dst, src, bytes, mode == 1 ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyDeviceToDevice,
+                        (hipStream_t)s) == hipSuccess ? 0 : -1;
+}
+
 extern "C" int fls_copy_rows(const void* x, int ldx, const int* src_idx, void* y, int ldy, const int* dst_idx,
                              int rows, int H, fls_stream_t s) {
   if (rows <= 0) return 0;

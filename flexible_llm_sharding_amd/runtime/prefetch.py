@@ -545,8 +545,41 @@ class PiecePoolPrefetcher(ShardPrefetcher):
     def _copy_piece(self, slot: torch.Tensor, name: str, lo: int, hi: int) -> int:
         """Enqueue image bytes [lo, hi) of ``name`` into ``slot[0:]`` on the copy stream (current
         stream) -> host bytes moved."""
-        slot[:hi - lo].copy_(self.src.host_buffer(name)[lo:hi], non_blocking=True)
+        if self.emulate_fanout is not None and self.emulate_fanout[3]:
+            # a data-parallel rank's own slice: 1/8 of the piece over PCIe (the rest of the slot keeps
+            # stale, finite weights: a timing run)
+            n = (hi - lo) // 8
+            slot[:n].copy_(self.src.host_buffer(name)[lo:lo + n], non_blocking=True)
+        else:
+            slot[:hi - lo].copy_(self.src.host_buffer(name)[lo:hi], non_blocking=True)
+        if self.emulate_fanout is not None:
+            self._emulate_gather(slot, hi - lo)
         return hi - lo
+
+    # bench.py --emulate-dp-fanout (measurement only): after each piece lands, the device traffic
+    # that the data-parallel all-gather of G = 8 ranks adds on a rank -- 7/8 of the piece's bytes
+    # read from HBM and written to HBM -- issued on the copy stream where AllGatherPiecePool issues
+    # its gather, as (mode, blocks, scratch, slice): mode 0 / 2 on the compute units (the runtime's
+    # blit kernel / a copy kernel on `blocks` workgroups, like RCCL's channels), 1 on the SDMA
+    # engines; slice: only the rank's 1/8 of the piece comes over PCIe.  The writes cycle through
+    # `scratch`
+    emulate_fanout = None
+
+    def _emulate_gather(self, slot: torch.Tensor, nbytes: int) -> None:
+        from .. import _native
+        mode, blocks, scratch, _ = self.emulate_fanout
+        if mode < 0:
+            return
+        k = _native.kernels()
+        left = nbytes * 7 // 8 // 16 * 16
+        chunk = min(scratch.numel() * scratch.element_size(), nbytes) // 16 * 16
+        st = torch.cuda.current_stream(self.dev).cuda_stream
+        while left > 0 and chunk > 0:
+            n = min(left, chunk)
+            rc = k.fls_copy_d2d(scratch.data_ptr(), slot.data_ptr(), n, mode, blocks, st)
+            if rc:
+                raise RuntimeError(f"fls_copy_d2d failed ({rc})")
+            left -= n
 
     def _pump(self, need: Optional[int] = None) -> None:
         """Issue loads in pass order while their slots are free (at least through ``need``)."""

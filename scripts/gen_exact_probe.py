@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--prefix-len", type=int, default=1024)
     ap.add_argument("--suffix-len", type=int, default=64)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--only", default=None, choices=["exact", "reuse"], help="one run (a kernel trace)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     cfg = preset(a.model)
@@ -46,6 +47,8 @@ def main():
            "num_gen_token": a.gen, "weights": "resident in HBM"}
     runs = {}
     for name, sfx in (("exact", False), ("reuse", True)):
+        if a.only and name != a.only:
+            continue
         r = ShardedRunner(cfg, store, dev, tok, layer_num_per_shard=1, prefix_kv_cache=True, suffix_kv_cache=sfx,
                           resident=True)
         step_s = []
@@ -63,6 +66,8 @@ def main():
         del r
         gc.collect()
         torch.cuda.empty_cache()
+    if a.only:
+        return
     (s0, u0), (s1, u1) = runs["exact"], runs["reuse"]
     res["tokens_equal"] = bool(u0 == u1)
     res["scores_bitwise_equal"] = bool(all(np.array_equal(x, y) for x, y in zip(s0, s1)))
