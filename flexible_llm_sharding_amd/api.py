@@ -103,17 +103,22 @@ def repeated_passes(args) -> bool:
 
 def resolve_prefix_kv_cache(args) -> bool:
     """``--prefix_kv_cache auto``: on for greedy generation (exact: later steps re-score the same
-    prefixes, runtime/prefix_cache.py) unless ``--max_vram_gb`` caps the device memory: the cache
-    holds every prompt's K/V for every layer (~320 KB per token for 70B), which no capped plan can
-    hold; asking for both explicitly is an error."""
+    prefixes, runtime/prefix_cache.py).  Under ``--max_vram_gb`` the cache lives in pinned host
+    memory (host mode: a staging buffer of one layer's K/V in HBM, planned by runtime/memplan.py);
+    ``build_runner`` turns an auto cache off when the host lacks the memory for it."""
     v = getattr(args, "prefix_kv_cache", False)
-    capped = bool(getattr(args, "max_vram_gb", None))
     if v == "auto":
-        return getattr(args, "num_gen_token", 1) > 1 and not getattr(args, "resume_dir", None) and not capped
-    if v and capped:
-        raise ValueError("--prefix_kv_cache keeps every prompt's K/V of every layer in HBM, outside the "
-                         "--max_vram_gb plan: use one or the other")
+        return getattr(args, "num_gen_token", 1) > 1 and not getattr(args, "resume_dir", None)
     return bool(v)
+
+
+# host mode may take at most this share of the host's available memory
+HOST_KV_SHARE = 0.5
+
+
+def host_kv_fits(nbytes: int) -> bool:
+    import psutil
+    return nbytes <= HOST_KV_SHARE * psutil.virtual_memory().available
 
 
 def resolve_suffix_kv_cache(args, world: int = 1) -> bool:
@@ -178,6 +183,15 @@ def build_runner(args, cfg: ModelConfig, device, comm: Comm, tok, prompts=None) 
     if not args.data_parallel and comm.world > 1:
         n_dec = -(-n_dec // comm.world)
     reserve = prefix_kv_bytes(cfg, tok, prompts, n_dec, suffix_kv_cache=skv) if pkv else 0
+    if pkv and getattr(args, "max_vram_gb", None) and not host_kv_fits(reserve):
+        # host mode (a VRAM cap): the cache's pinned host buffers
+        msg = (f"the prefix K/V cache needs {reserve / 1e9:.1f} GB of pinned host memory (--max_vram_gb "
+               f"keeps it on the host): more than {HOST_KV_SHARE:.0%} of the available memory")
+        if getattr(args, "prefix_kv_cache", False) != "auto":
+            raise ValueError(msg)
+        print(msg + "; running without it", file=sys.stderr)
+        pkv = skv = False
+        reserve = 0
     if args.data_parallel and comm.world > 1 and args.dp_weight_shard:
         from .parallel.data_parallel import build_dp_sharded_runner
         hv = getattr(args, "hbm_cache_gb", 0.0)

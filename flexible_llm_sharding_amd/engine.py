@@ -247,8 +247,10 @@ class ShardedRunner:
         self.prefix_cache = None
         if prefix_kv_cache and not self.hip_graphs and not resume_dir:
             from .runtime.prefix_cache import PrefixKVCache
+            # under a VRAM cap the entries live in pinned host memory, staged through HBM per layer
             self.prefix_cache = PrefixKVCache(2 * cfg.num_key_value_heads * cfg.head_dim, self.dev,
-                                              self.act_dtype, prefix_cache_entries, suffix_reuse=suffix_kv_cache)
+                                              self.act_dtype, prefix_cache_entries, suffix_reuse=suffix_kv_cache,
+                                              host=bool(max_vram_gb))
         # generation (prefix K/V cache): every call row-exact (see "exact K/V reuse" below)
         self.row_exact = self.prefix_cache is not None
         self._n_decoders = sum(1 for n in self.names if layer_kind(n) == "decoder")
@@ -452,7 +454,7 @@ class ShardedRunner:
         self.ctx.prefix_entry = entry
         try:
             with self._workspace(), self._row_exact(self.row_exact):
-                if self._decode_graphable(batches, cached):
+                if self._decode_graphable(batches, cached) and not entry.host:    # (graphs: K/V in HBM)
                     outputs = self._run_graphed(tps, batches, t_start, entry=entry)
                 else:
                     outputs = self._run_batches(tps, batches, t_start)
@@ -483,11 +485,16 @@ class ShardedRunner:
         rows = [tp.num_tokens - (len(tp.prefix) if cached else 0) for tp in tps]
         total = sum(rows)
         tb, mc, n_slots = self._plan_req
+        # host-mode prefix K/V cache: its staging buffer; the attention phase then runs over the
+        # whole micro-batch (the cache's row copies index it), never in prompt-aligned groups
+        pc = self.prefix_cache
+        stage = pc.stage.nbytes if (pc is not None and pc.stage is not None) else 0
         tb, mc, ar, qc, est, res = plan_for_vram(self.cfg, self._vram_cap, self.lnps, self.prefetcher.n_slots, tb, mc,
                                         total_tokens=max(1, total), max_prompt_rows=max(rows or [0]),
                                         overhead=self._outside,
                                         weight_bytes=self.prefetcher.planned_hbm_bytes() if self.cuda else None,
-                                        fused_norm=self.ctx.fused_norm)
+                                        fused_norm=self.ctx.fused_norm, extra_bytes=stage,
+                                        grouped=self.prefix_cache is None)
         self.token_budget, self.mlp_chunk = tb, mc
         self.ctx.mlp_chunk, self.ctx.attn_rows, self.ctx.qkv_chunk = mc, ar, qc
         # (the plan charged ceil(total / tb) states; a split that needs more micro-batches — whole

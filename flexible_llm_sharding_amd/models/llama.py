@@ -423,6 +423,8 @@ def _attention_whole(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tens
     a = ops.attention(qkv, attn_arg, cfg.num_attention_heads, cfg.num_key_value_heads, cfg.head_dim,
                       kv0=kv0 if batch.kv_cached else None, q_block=qb, out=qkv[:, :cfg.q_size],
                       scale=cfg.attn_scale, **kw)
+    if pe is not None and pe.host:
+        pe.flush(layer_name)                 # host-mode entry: the rows written go back to the host
     del qkv
     if prune:
         idx = meta["last_idx"]

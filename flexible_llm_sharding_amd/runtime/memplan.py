@@ -149,12 +149,15 @@ def plan_for_vram(cfg: ModelConfig, max_vram_bytes: int, lnps: int = 1, n_slots:
                   token_budget: int = 49152, mlp_chunk: int = 16384,
                   total_tokens: Optional[int] = None, max_prompt_rows: int = 0,
                   overhead: Optional[int] = None, weight_bytes: Optional[int] = None,
-                  fused_norm: bool = False) -> Tuple[int, int, int, int, int, bool]:
+                  fused_norm: bool = False, extra_bytes: int = 0,
+                  grouped: bool = True) -> Tuple[int, int, int, int, int, bool]:
     """-> (token_budget, mlp_chunk, attn_rows, qkv_chunk, estimated peak bytes, resident) for a
     call of ``total_tokens`` packed tokens (None: unknown, assume several micro-batches) whose
     largest prompt has ``max_prompt_rows`` rows.  ``overhead``: device memory held outside the plan
     (measured context + code objects; default DEVICE_OVERHEAD); ``weight_bytes``: the weight
-    buffers actually planned (default ``n_slots`` full-shard slots).  ``resident``: every
+    buffers actually planned (default ``n_slots`` full-shard slots); ``extra_bytes``: other fixed
+    device buffers (the host-mode prefix K/V cache's staging); ``grouped=False``: no prompt-aligned
+    attention groups (the prefix K/V cache runs the whole micro-batch).  ``resident``: every
     micro-batch's hidden state keeps an activation-ring slot of its own for the whole pass (no
     state is parked in host memory); else the ring has ``STATES`` slots.
 
@@ -170,7 +173,7 @@ def plan_for_vram(cfg: ModelConfig, max_vram_bytes: int, lnps: int = 1, n_slots:
     from ..models.llama import balanced_step
     weights = weight_slot_bytes(cfg, lnps, n_slots) if weight_bytes is None else weight_bytes
     target = int(max_vram_bytes * (1.0 - CAP_MARGIN))
-    over = DEVICE_OVERHEAD if overhead is None else overhead
+    over = (DEVICE_OVERHEAD if overhead is None else overhead) + extra_bytes
     best = None
     budgets = sorted({token_budget, 49152, 32768, 24576, 16384, 12288, 8192, 6144, 4096, 3072, 2048, 1024})
     # multiples of 3072 rows give whole 256-CU rounds of the 384-row GEMM tile (models/llama.py)
@@ -186,7 +189,7 @@ def plan_for_vram(cfg: ModelConfig, max_vram_bytes: int, lnps: int = 1, n_slots:
             resident = states == n_mb
             for mc in (m for m in chunks if m <= min(mlp_chunk, tb)):
                 mce = balanced_step(rows, mc)
-                for ar in sorted({0, 32768, 24576, 16384, 12288, 8192, 4096}):
+                for ar in (sorted({0, 32768, 24576, 16384, 12288, 8192, 4096}) if grouped else (0,)):
                     if ar and (ar >= rows or ar < max_prompt_rows):
                         continue
                     qcs = (0, 16384, 12288, 9216, 8192, 6144, 4096, 3072, 2048) if ar == 0 and not fused_norm else (0,)

@@ -27,10 +27,20 @@ longest common token prefix with the cached ids has the same K/V (causal rows de
 only on the prefix and earlier suffix tokens), so only the tokens after it are packed
 and computed; their attention reads the kept rows as range 2
 (``csrc/kernels/attention.hip``).  At least the scored (last) token is always
-recomputed.  A step then costs the new tokens instead of every suffix token (the
-kernels see different batch shapes than a full recompute, so results agree to
-rounding, not bitwise).  A suffix that outgrows its region is computed in full and
-not cached.
+recomputed.  A step then costs the new tokens instead of every suffix token; the
+engine runs such calls row-exact (every row's arithmetic independent of the batch it
+is packed in, ``engine.py`` "exact K/V reuse"), so a reused step's scores are bitwise
+those of the full recomputation.  A suffix that outgrows its region is computed in full
+and not cached.
+
+Host mode (``PrefixKVCache(host=True)``, the ``--max_vram_gb`` runs): the per-layer
+buffers live in pinned host memory and HBM holds only a staging buffer of one
+layer's K/V (planned by ``runtime/memplan.py``).  A layer's attention stages its
+K/V in on the compute stream (nothing the first time: a fresh layer is zeros) and, after
+the attention, copies the rows it wrote back on a side stream (every row in the filling
+call, the suffix regions in a reused step) while the layer's O projection and MLP run;
+the other staging buffer serves the next layer.  The values are the device mode's, so
+the scores are too.
 """
 from __future__ import annotations
 
@@ -64,7 +74,7 @@ class PrefixEntry:
     REGION_ALIGN = 64      # attention key tile (csrc/kernels/attention.hip KT)
 
     def __init__(self, key: str, prefix_lens: Sequence[int], kv_cols: int, device, dtype,
-                 suffix_caps: Optional[Sequence[Sequence[int]]] = None):
+                 suffix_caps: Optional[Sequence[Sequence[int]]] = None, stage: Optional["HostStage"] = None):
         self.key = key
         self.offsets: List[int] = []
         t = 0
@@ -91,8 +101,16 @@ class PrefixEntry:
         self.dtype = dtype
         self.layers: Dict[str, torch.Tensor] = {}
         self.complete = False
+        self.stage = stage            # host mode: the cache's staging buffers
+        self._staged: Optional[tuple] = None     # (layer name, staging view) of the layer in flight
+
+    @property
+    def host(self) -> bool:
+        return self.stage is not None
 
     def buffer(self, layer_name: str, create: bool = False) -> Optional[torch.Tensor]:
+        if self.stage is not None:
+            return self._stage_in(layer_name, create)
         b = self.layers.get(layer_name)
         if b is None and create:
             # zeroed: a reused step's key tiles cover the alignment gaps and unused region rows (masked,
@@ -100,6 +118,35 @@ class PrefixEntry:
             b = torch.zeros(max(1, self.rows), self.kv_cols, dtype=self.dtype, device=self.dev)
             self.layers[layer_name] = b
         return b
+
+    def _stage_in(self, layer_name: str, create: bool) -> Optional[torch.Tensor]:
+        if self._staged is not None and self._staged[0] == layer_name:
+            return self._staged[1]
+        hb = self.layers.get(layer_name)
+        if hb is None:
+            if not create:
+                return None
+            hb = self.stage.alloc_host(max(1, self.rows), self.kv_cols, self.dtype)
+            self.layers[layer_name] = hb
+            fresh = True
+        else:
+            fresh = False
+        buf = self.stage.acquire(hb.shape[0])
+        self.stage.load(buf, hb, layer_name, fresh)
+        self._staged = (layer_name, buf)
+        return buf
+
+    def flush(self, layer_name: str) -> None:
+        """After a layer's attention (host mode): the rows it may have written go back to the
+        host buffer — all of them while the entry fills, the suffix regions once it is complete
+        (a reused step writes only its new suffix tokens)."""
+        if self._staged is None or self._staged[0] != layer_name:
+            return
+        buf = self._staged[1]
+        self._staged = None
+        lo = self.total if self.complete else 0
+        if lo < buf.shape[0]:
+            self.stage.store(self.layers[layer_name], buf, lo, layer_name)
 
     def suffix_plan(self, tps: Sequence, reuse: bool):
         """-> (rows, keep) for :func:`runtime.batch.pack_prompts`: the cache row of every suffix
@@ -141,13 +188,82 @@ class PrefixEntry:
         return sum(t.numel() * t.element_size() for t in self.layers.values())
 
 
+class HostStage:
+    """Device staging buffer(s) for host-mode entries (one layer's K/V each) and the side stream
+    their write-backs run on.  A buffer is reused only after its last write-back, and a layer's
+    host rows are read back only after theirs landed (events per buffer and per layer).  One
+    buffer: a layer's write-back overlaps its own O projection and MLP, which outlast it (70B,
+    32 prompts: ~4 ms of D2H per layer against >= 30 ms of weight streaming per layer), so a
+    second buffer would buy little for its HBM."""
+
+    N_BUFS = 1
+
+    def __init__(self, kv_cols: int, device, dtype, max_rows: int):
+        self.dev = torch.device(device)
+        self.cuda = self.dev.type == "cuda"
+        self.bufs = [torch.zeros(max(1, max_rows), kv_cols, dtype=dtype, device=self.dev)
+                     for _ in range(self.N_BUFS)]
+        self.cur = 0
+        self.stream = torch.cuda.Stream(self.dev) if self.cuda else None
+        self.buf_ev: List[Optional[object]] = [None] * self.N_BUFS
+        self.layer_ev: Dict[tuple, object] = {}
+        self.bytes_h2d = self.bytes_d2h = 0
+
+    @property
+    def nbytes(self) -> int:
+        return sum(b.numel() * b.element_size() for b in self.bufs)
+
+    def alloc_host(self, rows: int, cols: int, dtype) -> torch.Tensor:
+        return torch.zeros(rows, cols, dtype=dtype, pin_memory=self.cuda)
+
+    def acquire(self, rows: int) -> torch.Tensor:
+        if rows > self.bufs[0].shape[0]:
+            raise ValueError(f"prefix K/V entry of {rows} rows > the staging buffers' {self.bufs[0].shape[0]}")
+        self.cur = (self.cur + 1) % self.N_BUFS
+        ev = self.buf_ev[self.cur]
+        if ev is not None:
+            torch.cuda.current_stream(self.dev).wait_event(ev)
+        return self.bufs[self.cur][:rows]
+
+    def load(self, buf: torch.Tensor, hb: torch.Tensor, layer_name: str, fresh: bool) -> None:
+        if fresh:
+            buf.zero_()
+            return
+        ev = self.layer_ev.get((id(hb), layer_name))
+        if ev is not None:
+            torch.cuda.current_stream(self.dev).wait_event(ev)
+        buf.copy_(hb, non_blocking=True)
+        self.bytes_h2d += hb.numel() * hb.element_size()
+
+    def store(self, hb: torch.Tensor, buf: torch.Tensor, lo: int, layer_name: str) -> None:
+        self.bytes_d2h += (buf.shape[0] - lo) * buf.shape[1] * buf.element_size()
+        if not self.cuda:
+            hb[lo:].copy_(buf[lo:])
+            return
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(self.stream):
+            self.stream.wait_event(ev)
+            hb[lo:].copy_(buf[lo:], non_blocking=True)
+            done = torch.cuda.Event()
+            done.record(self.stream)
+        self.buf_ev[self.cur] = done
+        self.layer_ev[(id(hb), layer_name)] = done
+
+    def forget(self, e: "PrefixEntry") -> None:
+        for name, hb in e.layers.items():
+            self.layer_ev.pop((id(hb), name), None)
+
+
 class PrefixKVCache:
     # suffix region per (prompt, suffix): its first call's length + this many tokens of growth
     SUFFIX_GROWTH = 64
 
     def __init__(self, kv_cols: int, device, dtype=torch.float16, max_entries: int = 8,
-                 suffix_reuse: bool = True):
+                 suffix_reuse: bool = True, host: bool = False):
         self.suffix_reuse = suffix_reuse
+        self.host = host
+        self.stage: Optional[HostStage] = None
         self.kv_cols = kv_cols
         self.dev = torch.device(device)
         self.dtype = dtype
@@ -163,6 +279,41 @@ class PrefixKVCache:
         if e is not None:
             for cb in self.on_evict:
                 cb(e)
+            if self.stage is not None:
+                self.stage.forget(e)
+
+    @staticmethod
+    def entry_rows(tps: Sequence, suffix_reuse: bool) -> int:
+        """Rows of the entry ``begin(tps)`` creates (prefixes + 64-aligned suffix regions)."""
+        t = sum(len(tp.prefix) for tp in tps)
+        if suffix_reuse:
+            for tp in tps:
+                for s in tp.suffixes:
+                    t = -(-t // PrefixEntry.REGION_ALIGN) * PrefixEntry.REGION_ALIGN + len(s) + PrefixKVCache.SUFFIX_GROWTH
+        return t
+
+    def stage_bytes(self, tps: Sequence, elem: int = 2) -> int:
+        """HBM of host mode's staging buffers for a call on ``tps`` (0 in device mode)."""
+        if not self.host:
+            return 0
+        rows = max(self.entry_rows(tps, self.suffix_reuse), self.stage.bufs[0].shape[0] if self.stage else 0)
+        return HostStage.N_BUFS * rows * self.kv_cols * elem
+
+    def ensure_stage(self, tps: Sequence) -> None:
+        """Host mode: staging buffers large enough for ``tps``'s entry (grown, never shrunk)."""
+        if not self.host:
+            return
+        rows = self.entry_rows(tps, self.suffix_reuse)
+        if self.stage is None or self.stage.bufs[0].shape[0] < rows:
+            old = self.stage
+            if old is not None and old.cuda:
+                # the old buffers' write-backs finish before the buffers go
+                torch.cuda.current_stream(self.dev).wait_stream(old.stream)
+            self.stage = HostStage(self.kv_cols, self.dev, self.dtype, rows)
+            if old is not None:
+                self.stage.layer_ev = old.layer_ev
+            for e in self.entries.values():
+                e.stage = self.stage
 
     def lookup(self, tps: Sequence) -> Optional[PrefixEntry]:
         e = self.entries.get(prefix_fingerprint(tps))
@@ -178,7 +329,9 @@ class PrefixKVCache:
         while len(self.entries) >= self.max_entries:
             self._evict(self.entries.popitem(last=False)[1])
         caps = ([[len(s) + self.SUFFIX_GROWTH for s in tp.suffixes] for tp in tps] if self.suffix_reuse else None)
-        e = PrefixEntry(key, [len(tp.prefix) for tp in tps], self.kv_cols, self.dev, self.dtype, caps)
+        self.ensure_stage(tps)
+        e = PrefixEntry(key, [len(tp.prefix) for tp in tps], self.kv_cols, self.dev, self.dtype, caps,
+                        stage=self.stage)
         self.entries[key] = e
         return e
 

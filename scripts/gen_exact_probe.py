@@ -3,6 +3,7 @@ false), both greedy over the same synthetic prompts, weights resident in HBM: ar
 equal at every step (ShardedRunner "exact K/V reuse"), and what does a step cost?
 
     python scripts/gen_exact_probe.py [--model llama2-70b] [--prompts 64] [--gen 8] [--json out.json]
+        [--max-vram-gb 6]     # weights streamed through the piece pool, K/V caches in host memory
 """
 import argparse
 import gc
@@ -34,6 +35,7 @@ def main():
     ap.add_argument("--suffix-len", type=int, default=64)
     ap.add_argument("--json", default=None)
     ap.add_argument("--only", default=None, choices=["exact", "reuse"], help="one run (a kernel trace)")
+    ap.add_argument("--max-vram-gb", type=float, default=None)
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     cfg = preset(a.model)
@@ -44,14 +46,20 @@ def main():
     prompts = synthetic_prompts(a.prompts, a.prefix_len, 5, a.suffix_len, cfg.vocab_size, seed=0)
     args = argparse.Namespace(num_gen_token=a.gen, data_parallel=False, num_batch=1)
     res = {"model": a.model, "prompts": a.prompts, "prefix_len": a.prefix_len, "suffix_len": a.suffix_len,
-           "num_gen_token": a.gen, "weights": "resident in HBM"}
+           "num_gen_token": a.gen,
+           "weights": f"streamed, --max_vram_gb {a.max_vram_gb}" if a.max_vram_gb else "resident in HBM"}
     runs = {}
     for name, sfx in (("exact", False), ("reuse", True)):
         if a.only and name != a.only:
             continue
+        kw = {"max_vram_gb": a.max_vram_gb} if a.max_vram_gb else {"resident": True}
         r = ShardedRunner(cfg, store, dev, tok, layer_num_per_shard=1, prefix_kv_cache=True, suffix_kv_cache=sfx,
-                          resident=True)
+                          **kw)
         step_s = []
+        sampler = None
+        if a.max_vram_gb:
+            from bench import DeviceSampler          # hipMemGetInfo sampled every 2 ms
+            sampler = DeviceSampler(dev)
         t = time.perf_counter()
         s, u = generation_loop(args, r, Comm(0, 1, dev), tok, prompts, step_s)
         runs[name] = (s, u)
@@ -61,6 +69,17 @@ def main():
             res[name]["speculative_dropped"] = r.spec_dropped
             res[name]["last_step_stats"] = {k: r.stats.get(k) for k in ("tokens", "suffix_tokens_reused",
                                                                          "speculative", "graph_replays")}
+        pc = r.prefix_cache
+        if pc.host:
+            res[name]["host_kv"] = {"host_gb": round(pc.nbytes / 1e9, 2), "staging_gb": round(pc.stage.nbytes / 1e9, 3),
+                                    "h2d_gb": round(pc.stage.bytes_h2d / 1e9, 2),
+                                    "d2h_gb": round(pc.stage.bytes_d2h / 1e9, 2)}
+        if a.max_vram_gb:
+            from flexible_llm_sharding_amd.runtime.memplan import device_used_bytes
+            res[name]["device_used_gb_end"] = round(device_used_bytes(dev) / 1e9, 3)
+            res[name]["peak_device_used_gb"] = round(sampler.stop()[0] / 1e9, 3)
+            res[name]["max_reserved_gb"] = round(torch.cuda.max_memory_reserved(dev) / 1e9, 3)
+            res[name]["vram_plan"] = r.vram_plan
         print(json.dumps({name: res[name]}), flush=True)
         r.close()
         del r

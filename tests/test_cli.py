@@ -219,17 +219,17 @@ def test_repeated_pass_defaults():
     assert repeated_passes(g) and resolve_prefix_kv_cache(g)
     assert repeated_passes(parse_args(base + ["--num_batch", "2"]))
     assert not resolve_prefix_kv_cache(parse_args(base + ["--num_gen_token", "4", "--prefix_kv_cache", "false"]))
-    # a VRAM cap: the K/V cache is outside its plan -> auto is off, explicit is an error
+    # a VRAM cap: the cache lives in pinned host memory (host mode), so auto stays on while the
+    # host has room for it
+    from flexible_llm_sharding_amd.api import host_kv_fits
     capped = parse_args(base + ["--num_gen_token", "4", "--max_vram_gb", "6"])
-    assert not resolve_prefix_kv_cache(capped)
-    with pytest.raises(ValueError):
-        resolve_prefix_kv_cache(parse_args(base + ["--num_gen_token", "4", "--max_vram_gb", "6",
-                                                   "--prefix_kv_cache", "true"]))
+    assert resolve_prefix_kv_cache(capped)
+    assert host_kv_fits(1 << 20) and not host_kv_fits(1 << 60)
     # suffix K/V reuse is on by default with the prefix cache on one GPU (exact: row-independent
     # kernels, engine "exact K/V reuse"); off on several ranks and without the prefix cache
     from flexible_llm_sharding_amd.api import resolve_suffix_kv_cache
     assert g.suffix_kv_cache == "auto" and resolve_suffix_kv_cache(g, 1) and not resolve_suffix_kv_cache(g, 2)
-    assert not resolve_suffix_kv_cache(a, 1) and not resolve_suffix_kv_cache(capped, 1)
+    assert not resolve_suffix_kv_cache(a, 1) and resolve_suffix_kv_cache(capped, 1)
     assert not resolve_suffix_kv_cache(parse_args(base + ["--num_gen_token", "4", "--suffix_kv_cache", "false"]), 1)
     assert parse_args(base + ["--hbm_cache_gb", "12.5"]).hbm_cache_gb == 12.5
     cfg = preset("tiny")

@@ -448,9 +448,21 @@ def test_row_exact_packing_and_regions():
     assert buf.shape[0] >= starts[-1] + 94 and not buf.any()
 
 
+def _host_mode(r):
+    """Swap a runner's prefix K/V cache for a host-mode one (what --max_vram_gb builds)."""
+    from flexible_llm_sharding_amd.runtime.prefix_cache import PrefixKVCache
+    pc = r.prefix_cache
+    r.prefix_cache = PrefixKVCache(pc.kv_cols, pc.dev, pc.dtype, pc.max_entries, suffix_reuse=pc.suffix_reuse,
+                                   host=True)
+    r.prefix_cache.on_evict = pc.on_evict
+    return r
+
+
+@pytest.mark.parametrize("host", [False, True])
 @pytest.mark.parametrize("num_batch_calls", [1, 2])
-def test_prefix_kv_cache_generation_exact(tiny_model, num_batch_calls):
-    """--prefix_kv_cache: later calls on the same prefixes compute only suffix tokens, same scores."""
+def test_prefix_kv_cache_generation_exact(tiny_model, num_batch_calls, host):
+    """--prefix_kv_cache: later calls on the same prefixes compute only suffix tokens, same scores
+    (host: the entries in host memory, staged per layer — several micro-batches per call here)."""
     from flexible_llm_sharding_amd.api import generation_loop
     from flexible_llm_sharding_amd.engine import ShardedRunner
     from flexible_llm_sharding_amd.parallel.comm import Comm
@@ -472,6 +484,8 @@ def test_prefix_kv_cache_generation_exact(tiny_model, num_batch_calls):
     for sfx in (False, True):
         cached = ShardedRunner(cfg, src, "cpu", tok, layer_num_per_shard=2, token_budget=150, prefix_kv_cache=True,
                                suffix_kv_cache=sfx)
+        if host:
+            _host_mode(cached)
         s1, u1 = generation_loop(args, cached, Comm(), tok, prompts)
         assert u0 == u1
         for a, b in zip(s0, s1):
@@ -479,6 +493,10 @@ def test_prefix_kv_cache_generation_exact(tiny_model, num_batch_calls):
             assert np.abs(a.astype(np.float32) - b.astype(np.float32)).max() < 1e-5
         pc = cached.prefix_cache
         assert pc.misses == num_batch_calls and pc.hits == 2 * num_batch_calls
+        if host:
+            # staged in for every reused layer call, written back after every layer call
+            assert pc.stage.bytes_h2d > 0 and pc.stage.bytes_d2h > 0
+            assert all(not t.is_cuda for e in pc.entries.values() for t in e.layers.values())
         assert cached.stats["prefix_cached"] == 1.0
         if not sfx:
             # the cached pass computed only the suffix tokens of the last call's prompts
@@ -722,7 +740,8 @@ def test_moe_chunks_shards_storage_match_oracle(tmp_path, family):
             assert np.abs(o.astype(np.float32) - rf).max() < 1e-4, kw
 
 
-def test_suffix_kv_reuse_partial_and_overflow(tiny_model):
+@pytest.mark.parametrize("host", [False, True])
+def test_suffix_kv_reuse_partial_and_overflow(tiny_model, host):
     """Suffix K/V reuse keeps only the common token prefix with the last call: suffixes edited in
     the middle, grown past their cache region (reuse off for that call), shortened, or dropped —
     every call's scores equal a runner without any cache."""
@@ -747,6 +766,8 @@ def test_suffix_kv_reuse_partial_and_overflow(tiny_model):
     PrefixKVCache.SUFFIX_GROWTH = 8
     try:
         r = ShardedRunner(cfg, FileLayerSource(cfg, path), "cpu", tok, prefix_kv_cache=True, suffix_kv_cache=True)
+        if host:
+            _host_mode(r)
         reused = []
         for prompts in (base, step2, step3, step4):
             got, want = r(prompts), plain(prompts)

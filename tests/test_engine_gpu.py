@@ -517,21 +517,22 @@ def test_speculative_generation_steps_bitwise(setup, mode):
         assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("weights", ["resident", "streamed"])
+@pytest.mark.parametrize("weights", ["resident", "streamed", "capped"])
 def test_suffix_reuse_bitwise_exact(setup, weights):
     """Generation with suffix K/V reuse (only each suffix's new tokens computed, the kept K/V read
     as range 2) == the exact generation (--suffix_kv_cache false: every suffix token recomputed each
     step) BIT FOR BIT at every step: with the prefix cache every call runs row-independent kernels,
     64-row-aligned suffix regions and single-suffix work items, so a row's arithmetic does not depend
     on which call computes it.  Suffixes of 40-70 tokens grow past the 64-key tile boundary; decode
-    graphs + speculative steps (resident) and eager steps (streamed weights)."""
+    graphs + speculative steps (resident), eager steps (streamed weights) and, under a VRAM cap,
+    the piece pool with the K/V entries in pinned host memory staged per layer (host mode)."""
     import argparse
     from flexible_llm_sharding_amd.api import generation_loop
     from flexible_llm_sharding_amd.parallel.comm import Comm
     path, cfg, tok, _, _ = setup
     prompts = synthetic_prompts(5, 90, 4, 70, cfg.vocab_size, seed=11, vary=True)
     src = HostStore.from_model_path(cfg, path)
-    kw = {"resident": True} if weights == "resident" else {}
+    kw = {"resident": {"resident": True}, "streamed": {}, "capped": {"max_vram_gb": 40}}[weights]
     args = argparse.Namespace(num_gen_token=8, data_parallel=False, num_batch=1)
     outs = {}
     for sfx in (False, True):
@@ -542,6 +543,10 @@ def test_suffix_reuse_bitwise_exact(setup, weights):
             assert r.stats["suffix_tokens_reused"] > 0
             if weights == "resident":
                 assert r.stats.get("graph_replays", 0) >= 1
+        if weights == "capped":
+            st = r.prefix_cache.stage
+            assert r.prefix_cache.host and st.bytes_h2d > 0 and st.bytes_d2h > 0
+            assert all(t.is_pinned() for e in r.prefix_cache.entries.values() for t in e.layers.values())
         r.close()
     (s0, u0), (s1, u1) = outs[False], outs[True]
     assert u0 == u1
