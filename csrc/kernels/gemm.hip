@@ -241,6 +241,7 @@ __global__ __launch_bounds__(mid::NTm) void gemm_nt_mid(const half_t* __restrict
   }
 }
 
+#include "gemm_panel.h"
 
 int g_order = 0;             // 0: by shape, else a fixed signed group size (fls_gemm_set_order)
 int g_mid = 1;               // mid-M kernel on (fls_gemm_set_mid)
@@ -394,6 +395,14 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
                         ldw % 8 == 0 && (size_t)M * lda * 2 < (1ull << 32) && ldc % 4 == 0 &&
                         ((uintptr_t)C & 7) == 0 && ((uintptr_t)ws & 15) == 0 &&
                         (EPI != FLS_EPI_RESID || (ep.ldr % 4 == 0 && ((uintptr_t)ep.R & 7) == 0));
+  // row-exact generation steps (and, with fls_gemm_set_panel(2), any small M): ALL rows x 32 columns
+  // per block, one accumulator chain over K (gemm_panel.h)
+  if (try_panel<EPI>(A, W, C, M, N, K, lda, ldw, ldc, ep, s)) {
+    FLS_CHECK_LAUNCH();
+    ss_partials(C, ldc, M, N, ep, s);
+    FLS_CHECK_LAUNCH();
+    return 0;
+  }
   if (!ep.row_exact) {
     const int rc = try_skinny<EPI>(A, W, C, M, N, K, lda, ldw, ldc, ep, s, ws, ws_bytes);
     if (rc > 0) ss_partials(C, ldc, M, N, ep, s);
@@ -484,7 +493,7 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
 
 }  // namespace
 
-extern "C" int fls_kernels_version(void) { return 29; }
+extern "C" int fls_kernels_version(void) { return 30; }
 
 // tile order: 0 = by shape (default); g > 0: groups of g M tiles; g < 0: groups of -g N tiles (A/B, tests)
 extern "C" int fls_gemm_set_order(int order) {
@@ -520,6 +529,13 @@ extern "C" int fls_gemm_set_splitk(int on) {
 extern "C" int fls_gemm_set_row_chunk(int rows) {
   const int old = ROW_CHUNK;
   ROW_CHUNK = rows > 0 ? rows : (1 << 30);
+  return old;
+}
+
+// panel kernel (gemm_panel.h): 0 off, 1 row-exact calls (default), 2 every M <= 320 it takes; returns the previous
+extern "C" int fls_gemm_set_panel(int mode) {
+  const int old = g_panel;
+  g_panel = mode < 0 ? 0 : mode > 2 ? 2 : mode;
   return old;
 }
 

@@ -1,0 +1,78 @@
+"""Generation-step GEMMs at the 70B shapes: the row-exact panel kernel (csrc/kernels/gemm_panel.h)
+against the row-exact mid-M kernel it replaces and the non-exact skinny / split-K paths.
+
+    python scripts/panel_bench.py [--rows 64,160,320] [--iters 50]
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from flexible_llm_sharding_amd.ops.hip_backend import EPI_NONE, EPI_RESID, EPI_ROPE, EPI_SWIGLU, HipOps  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", default="64,160,320")
+    ap.add_argument("--iters", type=int, default=50)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    ops = HipOps()
+    H, I, nh, nkv, hd = 8192, 28672, 64, 8, 128
+    g = torch.Generator(device=dev).manual_seed(0)
+    w = {"qkv": torch.randn((nh + 2 * nkv) * hd, H, device=dev, generator=g).half() * 0.02,
+         "o": torch.randn(H, H, device=dev, generator=g).half() * 0.02,
+         "gate_up": torch.randn(2 * I, H, device=dev, generator=g).half() * 0.02,
+         "down": torch.randn(H, I, device=dev, generator=g).half() * 0.02}
+    cos = torch.rand(8192, hd // 2, device=dev)
+    sin = torch.rand(8192, hd // 2, device=dev)
+    arms = {"panel_exact": (True, 1), "mid_exact": (True, 0), "skinny_splitk": (False, 1), "panel_any": (False, 2)}
+    for M in [int(r) for r in a.rows.split(",")]:
+        x = torch.randn(M, H, device=dev, generator=g).half()
+        xi = torch.randn(M, I, device=dev, generator=g).half()
+        r0 = torch.randn(M, H, device=dev, generator=g).half()
+        pos = torch.randint(0, 8000, (M,), dtype=torch.int32, device=dev)
+        rs = torch.rand(M, device=dev) + 0.5
+        calls = {
+            "qkv": lambda: ops.gemm(x, w["qkv"], EPI_ROPE, positions=pos, cos=cos, sin=sin,
+                                    rope_cols=(nh + nkv) * hd, head_dim=hd, rscale=rs),
+            "o": lambda: ops.gemm(x, w["o"], EPI_RESID, out=r0, resid=r0),
+            "gate_up": lambda: ops.gemm(x, w["gate_up"], EPI_SWIGLU, rscale=rs),
+            "down": lambda: ops.gemm(xi, w["down"], EPI_RESID, out=r0, resid=r0),
+        }
+        res = {"M": M}
+        outs = {}
+        for arm, (exact, panel) in arms.items():
+            old = ops.k.fls_gemm_set_panel(panel)
+            try:
+                with ops.row_exact(exact):
+                    tot = 0.0
+                    for name, f in calls.items():
+                        f()
+                        torch.cuda.synchronize()
+                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        e0.record()
+                        for _ in range(a.iters):
+                            f()
+                        e1.record()
+                        torch.cuda.synchronize()
+                        us = e0.elapsed_time(e1) * 1000 / a.iters
+                        tbs = w[name].numel() * 2 / (us * 1e-6) / 1e12
+                        res[f"{arm}.{name}_us"] = round(us, 1)
+                        res[f"{arm}.{name}_TBps"] = round(tbs, 2)
+                        tot += us
+                        if name == "gate_up":
+                            outs[arm] = f().clone()
+                    res[f"{arm}.layer_us"] = round(tot, 1)
+            finally:
+                ops.k.fls_gemm_set_panel(old)
+        res["panel_eq_mid_gate_up"] = bool(torch.equal(outs["panel_exact"], outs["mid_exact"]))
+        print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

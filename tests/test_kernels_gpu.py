@@ -403,6 +403,47 @@ def test_gemm_main_all_epilogues(ops, ref):
         ops.k.fls_gemm_set_mid(1)
 
 
+@pytest.mark.parametrize("hd", [128, 64])
+def test_gemm_panel_rows_bitwise(ops, ref, hd):
+    """Row-exact small-M GEMMs take the panel kernel (all rows x 32 columns per block, one K chain):
+    every row of M = 1 / 17 / 160 / 320 equals, bit for bit, the same row of a 1,000-row row-exact
+    GEMM (v10 / v11 / mid tiles), for all four epilogues incl. bias, per-row scale and RoPE (both
+    head sizes); and the fp32 reference."""
+    from flexible_llm_sharding_amd.config import ModelConfig
+    from flexible_llm_sharding_amd.models.llama import rope_tables
+    Mb, H, I, nh, nkv = 1000, 1024, 1536, 8, 2
+    x = rnd(Mb, H, seed=61)
+    rs = (torch.rand(Mb, device=DEV) + 0.5).float()
+    wo = rnd(H, H, scale=0.03, seed=62)
+    r0 = rnd(Mb, H, seed=63)
+    wgu = rnd(2 * I, H, scale=0.03, seed=64)
+    wqkv = rnd((nh + 2 * nkv) * hd, H, scale=0.03, seed=65)
+    bq = rnd((nh + 2 * nkv) * hd, scale=0.5, seed=66)
+    pos = torch.randint(0, 4000, (Mb,), dtype=torch.int32, device=DEV)
+    cfg = ModelConfig(hidden_size=nh * hd, num_attention_heads=nh, num_key_value_heads=nkv, head_dim=hd)
+    cos, sin = rope_tables(cfg, 4096)
+    cos, sin = cos.to(DEV), sin.to(DEV)
+
+    def run(rows):
+        xs, p, r = x[rows].contiguous(), pos[rows].contiguous(), rs[rows].contiguous()
+        return [ops.gemm(xs, wo),
+                ops.gemm(xs, wo, EPI_RESID, out=r0[rows].clone(), resid=r0[rows].clone(), rscale=r),
+                ops.gemm(xs, wgu, EPI_SWIGLU, rscale=r),
+                ops.gemm(xs, wqkv, EPI_ROPE, positions=p, cos=cos, sin=sin, rope_cols=(nh + nkv) * hd,
+                         head_dim=hd, bias=bq, rscale=r)]
+
+    with ops.row_exact():
+        full = run(torch.arange(Mb, device=DEV))
+        g = torch.Generator().manual_seed(5)
+        for m in (1, 17, 160, 320):
+            rows = torch.randperm(Mb, generator=g)[:m].to(DEV)
+            for a, b in zip(run(rows), full):
+                assert torch.equal(a, b[rows]), m
+    torch.cuda.synchronize()
+    assert rel_err(full[0], x.float() @ wo.float().t()) < 2e-3
+    assert rel_err(full[2].cpu(), ref.swiglu_up((x.float() * rs[:, None]).cpu(), wgu.float().cpu())) < 3e-3
+
+
 @pytest.mark.parametrize("order", [8, -4, -8, 1, -1, 2, 3, -5])
 def test_gemm_v10_tile_orders(ops, ref, order):
     """v10 tile orders (groups of M tiles / of N tiles, any size) only permute which block computes which tile:
