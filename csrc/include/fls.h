@@ -19,6 +19,7 @@ typedef void* fls_stream_t;
 int   fls_rt_version(void);
 void* fls_pinned_alloc(uint64_t bytes);                  // hipHostMalloc; NULL on failure
 int   fls_pinned_free(void* p);
+void* fls_host_device_ptr(void* p);                    // device address of a mapped pinned block (or NULL)
 int   fls_pinned_register(void* p, uint64_t bytes);      // hipHostRegister an existing range
 int   fls_pinned_unregister(void* p);
 int   fls_memcpy_async(void* dst, const void* src, uint64_t bytes, int kind, fls_stream_t s);

@@ -129,13 +129,17 @@ __global__ __launch_bounds__(256) void gemm_nt_generic(const half_t* __restrict_
 // same XCD so each weight tile comes from HBM once and from L2 after that.
 // Any K-tile count (the tail path for odd K / 64).
 namespace mid {
-constexpr int BMm = 64, BNm = 128, BKm = 64, NTm = 256, NSTAGE = 3;
+constexpr int BMm = 64, BNm = 128, BKm = 64, NTm = 256, NSTAGE = 3, NSTAGE_DEEP = 6;
 constexpr int STAGE = (BMm + BNm) * BKm * 2;     // 24 KiB: A rows 0..63 then W rows 0..127
 constexpr int GROUPS = (BMm + BNm) / 8;          // 8-row (1 KiB) LDS-DMA groups per stage
 constexpr int PER_WAVE = GROUPS / 4;             // 6 LDS-DMA per wave per stage
 }  // namespace mid
 
-template <int EPI>
+// NST: LDS stages, NST - 1 K-tiles in flight ahead of the one being multiplied.  3 (72 KB: two blocks
+// per CU) for grids of several rounds; 6 (144 KB) when the grid is at most one block per CU
+// (generation-step shapes: 70B O / down at M = 160 are 192 blocks of 128 / 448 K-tiles, each block
+// bound by the latency of its own DMA stream, not by bandwidth)
+template <int EPI, int NST>
 __global__ __launch_bounds__(mid::NTm) void gemm_nt_mid(const half_t* __restrict__ A, const half_t* __restrict__ W,
                                                      half_t* __restrict__ C, int M, int N, int K, int lda, int ldw,
                                                      int ldc, Epi ep) {
@@ -173,8 +177,10 @@ __global__ __launch_bounds__(mid::NTm) void gemm_nt_mid(const half_t* __restrict
       src[i] = W + (size_t)nr * ldw + kc;
     }
   }
-  auto stage = [&](int kt) {
-    char* base = lds_mid + (kt % NSTAGE) * STAGE;
+  // stage s takes K-tile kt (kt clamped to the last: a DMA past the end re-reads it into a stage
+  // nobody reads again, so every wait is one constant count)
+  auto stage = [&](int s, int kt) {
+    char* base = lds_mid + (s % NST) * STAGE;
 #pragma unroll
     for (int i = 0; i < PER_WAVE; ++i) glds16(src[i] + (size_t)kt * BKm, base + (wave + 4 * i) * 1024);
   };
@@ -188,19 +194,14 @@ __global__ __launch_bounds__(mid::NTm) void gemm_nt_mid(const half_t* __restrict
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[u][t] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  stage(0);
-  if (nk > 1) stage(1);
+#pragma unroll
+  for (int d = 0; d < NST - 1; ++d) stage(d, min(d, nk - 1));
   for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 2 < nk) {
-      stage(kt + 2);
-      asm volatile("s_waitcnt vmcnt(12)" ::: "memory");   // tiles kt+1, kt+2 stay in flight
-    } else if (kt + 1 < nk) {
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    // into the stage tile kt - 1 used (every wave passed that tile's closing barrier)
+    stage(kt + NST - 1, min(kt + NST - 1, nk - 1));
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NST - 1) * PER_WAVE) : "memory");   // tile kt landed
     __builtin_amdgcn_s_barrier();                          // every wave's part of tile kt landed
-    const char* Xs = lds_mid + (kt % NSTAGE) * STAGE;
+    const char* Xs = lds_mid + (kt % NST) * STAGE;
     const char* Ws = Xs + BMm * BKm * 2;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -221,10 +222,11 @@ __global__ __launch_bounds__(mid::NTm) void gemm_nt_mid(const half_t* __restrict
 #pragma unroll
         for (int t = 0; t < 4; ++t) acc[u][t] = mfma16x16x32(wf[t], xf[u], acc[u][t]);
     }
-    // WAR: stage(kt + 3) (next iteration) overwrites this buffer; all reads are done
+    // WAR: the next iteration's DMA overwrites this stage; all reads are done
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");         // the redundant tail DMA, before LDS is handed on
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int m = m0 + wm * 32 + u * 16 + fr;
@@ -245,6 +247,20 @@ __global__ __launch_bounds__(mid::NTm) void gemm_nt_mid(const half_t* __restrict
 
 int g_order = 0;             // 0: by shape, else a fixed signed group size (fls_gemm_set_order)
 int g_mid = 1;               // mid-M kernel on (fls_gemm_set_mid)
+int g_mid_deep = 1;          // 6-stage mid kernel for grids of <= 256 blocks (fls_gemm_set_mid: 2 = off, A/B)
+
+template <int EPI, int NST>
+void launch_mid(int blocks, const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int lda, int ldw,
+                int ldc, const Epi& ep, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_nt_mid<EPI, NST>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              NST * mid::STAGE);
+    attr = true;
+  }
+  hipLaunchKernelGGL((gemm_nt_mid<EPI, NST>), dim3(blocks), dim3(mid::NTm), NST * mid::STAGE, s, A, W, C, M, N, K, lda,
+                     ldw, ldc, ep);
+}
 
 template <int EPI>
 void launch_main(int tiles, const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int lda, int ldw,
@@ -435,15 +451,11 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
     return 0;
   }
   if (mid_ok && (!main_ok || (g_mid && (tiles256 < 128 || (M <= 64 && tiles256 < 512))))) {
-    static bool attr_mid = false;
-    if (!attr_mid) {
-      (void)hipFuncSetAttribute((const void*)gemm_nt_mid<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                mid::NSTAGE * mid::STAGE);
-      attr_mid = true;
-    }
     const int blocks = ((M + mid::BMm - 1) / mid::BMm) * (N / mid::BNm);
-    hipLaunchKernelGGL(gemm_nt_mid<EPI>, dim3(blocks), dim3(mid::NTm), mid::NSTAGE * mid::STAGE, s, A, W, C, M, N,
-                       K, lda, ldw, ldc, ep);
+    if (g_mid_deep && blocks <= 256)
+      launch_mid<EPI, mid::NSTAGE_DEEP>(blocks, A, W, C, M, N, K, lda, ldw, ldc, ep, s);
+    else
+      launch_mid<EPI, mid::NSTAGE>(blocks, A, W, C, M, N, K, lda, ldw, ldc, ep, s);
     FLS_CHECK_LAUNCH();
     ss_partials(C, ldc, M, N, ep, s);
     FLS_CHECK_LAUNCH();
@@ -539,10 +551,11 @@ extern "C" int fls_gemm_set_panel(int mode) {
   return old;
 }
 
-// mid-M kernel for small grids on (1, default) or off (0; tests)
+// mid-M kernel for small grids: 1 on (default), 0 off (tests), 2 on without the deep-ring variant (A/B)
 extern "C" int fls_gemm_set_mid(int on) {
-  const int old = g_mid;
+  const int old = g_mid ? (g_mid_deep ? 1 : 2) : 0;
   g_mid = on ? 1 : 0;
+  g_mid_deep = on == 2 ? 0 : 1;
   return old;
 }
 

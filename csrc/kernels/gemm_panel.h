@@ -3,9 +3,9 @@
 //
 // A reused generation step runs row-exact (every output row gets the arithmetic the full pass
 // gave it), which rules out K splits: each output element is ONE accumulator chain over K in
-// ascending 64-wide tiles, the v10 / v11 / mid order.  At M = 160-320 the mid kernel's 64 x 128
-// tiles leave the narrow projections with 192-320 blocks that each re-stream the weight panel of
-// their column tile per 64 rows.  Here a block is ALL of M (up to 64 RT rows) x 32 output columns:
+// ascending 64-wide tiles, the v10 / v11 / mid order.  At small M the mid kernel's 64 x 128
+// tiles leave the narrow projections with few blocks (70B O / down at M <= 64: 64).  Here a block
+// is ALL of M (up to 64 RT rows) x 32 output columns:
 //   * the N / 32 blocks each stream their 32 weight rows once (70B O / down: 256 blocks, QKV 320,
 //     gate/up 1792) while the activations (M x K, shared by every block) come from L2;
 //   * 4 waves split the rows (16-row tiles u = wave + 4 i), each against both 16-column subtiles,
@@ -120,7 +120,7 @@ __global__ __launch_bounds__(256) void gemm_nt_panel(const half_t* __restrict__ 
   }
 }
 
-int g_panel = 1;             // panel path: 0 off, 1 row-exact calls, 2 every M <= 320 it takes (A/B)
+int g_panel = 1;             // panel path: 0 off, 1 row-exact calls where it wins, 2 every M <= 320 it takes (A/B)
 
 template <int EPI, int RT>
 void launch_panel_rt(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int lda, int ldw, int ldc,
@@ -140,6 +140,11 @@ template <int EPI>
 int try_panel(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int lda, int ldw, int ldc,
               const Epi& ep, hipStream_t s) {
   if (!g_panel || (g_panel == 1 && !ep.row_exact)) return 0;
+  // auto (1): where it measured faster than the mid kernel, row-exact 70B shapes (profiles/r6_decode,
+  // scripts/panel_bench.py): M = 64 QKV 52.6 vs 61.1 us, O 51.1 vs 60.0, down 170 vs 231; not the wide
+  // gate/up (234 vs 171) nor any shape at M = 160 / 320 (2.5x slower: every block stages ALL the
+  // activation rows, so the L2 -> LDS activation traffic is N / 32 times M x K and bounds it)
+  if (g_panel == 1 && (M > 64 || N > 16384)) return 0;
   if (M < 1 || M > 64 * pn::MAX_RT || N % pn::PBN || K % pn::KT || lda % 8 || ldw % 8 || ((uintptr_t)A & 15) ||
       ((uintptr_t)W & 15) || ldc % 4 || ((uintptr_t)C & 7))
     return 0;

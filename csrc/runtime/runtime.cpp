@@ -59,6 +59,18 @@ extern "C" int fls_pinned_register(void* p, uint64_t bytes) {
   return hipHostRegister(p, bytes, hipHostRegisterDefault) == hipSuccess ? 0 : -1;
 }
 
+// device address of a mapped pinned host block (hipHostMalloc): kernels read / write it over PCIe
+// (runtime/prefix_cache.py host mode writes a generation step's new K/V rows straight into it);
+// nullptr when the block is not mapped
+extern "C" void* fls_host_device_ptr(void* p) {
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return d;
+}
+
 extern "C" int fls_pinned_unregister(void* p) {
   return hipHostUnregister(p) == hipSuccess ? 0 : -1;
 }

@@ -33,6 +33,7 @@ def _load_runtime():
     _bind(lib, "fls_pinned_alloc", c_void_p, c_uint64)
     _bind(lib, "fls_pinned_free", c_int, c_void_p)
     _bind(lib, "fls_pinned_register", c_int, c_void_p, c_uint64)
+    _bind(lib, "fls_host_device_ptr", c_void_p, c_void_p)
     _bind(lib, "fls_pinned_unregister", c_int, c_void_p)
     _bind(lib, "fls_memcpy_async", c_int, c_void_p, c_void_p, c_uint64, c_int, c_void_p)
     _bind(lib, "fls_pread_into", c_int64, c_char_p, c_uint64, c_uint64, c_void_p, c_int)

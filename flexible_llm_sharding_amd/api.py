@@ -122,20 +122,23 @@ def host_kv_fits(nbytes: int) -> bool:
 
 
 def resolve_suffix_kv_cache(args, world: int = 1) -> bool:
-    """``--suffix_kv_cache auto``: on whenever the prefix K/V cache is, on one rank (the tie guard's
-    exact re-runs of a few prompts are single-rank calls; every rank of a multi-GPU run would have to
-    join them)."""
+    """``--suffix_kv_cache auto``: on whenever the prefix K/V cache is, on one rank, without a VRAM
+    cap.  Under ``--max_vram_gb`` the caches live in host memory and a step is PCIe-bound (weights +
+    staged K/V): the suffix regions add more bytes per step than recomputing the suffix tokens costs
+    (70B, 32 prompts: 2.93 s per step with reuse against 2.84 s prefix-only, same tokens,
+    profiles/r6_decode), so auto keeps the prefix cache only."""
     v = getattr(args, "suffix_kv_cache", False)
     if v == "auto":
-        return resolve_prefix_kv_cache(args) and world == 1
+        return resolve_prefix_kv_cache(args) and world == 1 and not getattr(args, "max_vram_gb", None)
     return bool(v)
 
 
 def prefix_kv_bytes(cfg: ModelConfig, tok, prompts, n_decoders: int, elem: int = 2,
-                    suffix_kv_cache: bool = False) -> int:
+                    suffix_kv_cache: bool = False, growth: Optional[int] = None) -> int:
     """HBM the prefix K/V cache needs for ``prompts``: post-RoPE K and V of every prefix token, and
-    with ``suffix_kv_cache`` every suffix's region too (its tokens + ``PrefixKVCache.SUFFIX_GROWTH``
-    rows, as ``PrefixKVCache.begin`` sizes them), for every decoder layer this rank runs."""
+    with ``suffix_kv_cache`` every suffix's region too (its tokens + ``growth`` rows, default
+    ``PrefixKVCache.SUFFIX_GROWTH``, as ``PrefixKVCache.begin`` sizes them), for every decoder layer
+    this rank runs."""
     if tok is None or not prompts:
         return 0
     from .runtime.prefix_cache import PrefixKVCache
@@ -144,7 +147,8 @@ def prefix_kv_bytes(cfg: ModelConfig, tok, prompts, n_decoders: int, elem: int =
         for p in prompts:
             sfx = list(p[1])
             if sfx:
-                n += sum(len(ids) + PrefixKVCache.SUFFIX_GROWTH for ids in tok(sfx).input_ids)
+                g = PrefixKVCache.SUFFIX_GROWTH if growth is None else growth
+                n += sum(len(ids) + g for ids in tok(sfx).input_ids)
     return n * 2 * cfg.num_key_value_heads * cfg.head_dim * elem * n_decoders
 
 
@@ -182,7 +186,9 @@ def build_runner(args, cfg: ModelConfig, device, comm: Comm, tok, prompts=None) 
     n_dec = sum(1 for n in cfg.layer_names() if layer_kind(n) == "decoder")
     if not args.data_parallel and comm.world > 1:
         n_dec = -(-n_dec // comm.world)
-    reserve = prefix_kv_bytes(cfg, tok, prompts, n_dec, suffix_kv_cache=skv) if pkv else 0
+    from .runtime.prefix_cache import suffix_growth
+    growth = suffix_growth(getattr(args, "num_gen_token", 1))
+    reserve = prefix_kv_bytes(cfg, tok, prompts, n_dec, suffix_kv_cache=skv, growth=growth) if pkv else 0
     if pkv and getattr(args, "max_vram_gb", None) and not host_kv_fits(reserve):
         # host mode (a VRAM cap): the cache's pinned host buffers
         msg = (f"the prefix K/V cache needs {reserve / 1e9:.1f} GB of pinned host memory (--max_vram_gb "
@@ -223,7 +229,7 @@ def build_runner(args, cfg: ModelConfig, device, comm: Comm, tok, prompts=None) 
                          hbm_cache_gb=resolve_hbm_cache_gb(args, cfg, device, reserve),
                          prefix_kv_cache=pkv,
                          prefix_cache_entries=getattr(args, "prefix_cache_entries", 8),
-                         suffix_kv_cache=skv,
+                         suffix_kv_cache=skv, exact_reuse=getattr(args, "exact_reuse", True),
                          pipeline_stages=getattr(args, "pipeline_stages", "round_robin"),
                          rx_window=getattr(args, "rx_window", 2),
                          max_vram_gb=getattr(args, "max_vram_gb", None))
@@ -288,6 +294,10 @@ def generation_loop(args, runner, comm: Comm, tok, original_prompts: Sequence, s
     # one runner call per step on one rank: each decode-graphed step may enqueue the next one behind
     # itself (ShardedRunner._launch_spec) while the host decodes and re-tokenizes
     spec = comm.world == 1 and len(batch_ranges(len(input_prompts), args.num_batch)) == 1
+    pc = getattr(runner, "prefix_cache", None)
+    if pc is not None:
+        from .runtime.prefix_cache import suffix_growth
+        pc.suffix_growth = suffix_growth(args.num_gen_token)      # suffix regions sized for this run
     for i_new in range(args.num_gen_token):
         t_step = time.perf_counter()
         if hasattr(runner, "spec_steps"):

@@ -78,7 +78,8 @@ class ShardedRunner:
                  max_token_len: int = MAX_TOKEN_LEN, hip_graphs: bool = False,
                  prefix_kv_cache: bool = False, prefix_cache_entries: int = 8, suffix_kv_cache: bool = False,
                  prune_last_layer: bool = True, pipeline_stages: str = "round_robin",
-                 max_vram_gb: Optional[float] = None, hbm_cache_gb: float = 0.0, rx_window: int = 2):
+                 max_vram_gb: Optional[float] = None, hbm_cache_gb: float = 0.0, rx_window: int = 2,
+                 exact_reuse: bool = True):
         self.cfg = cfg
         self.src = source
         # layers read from their files every pass (no host-resident copy): host RAM is the limit
@@ -251,8 +252,9 @@ class ShardedRunner:
             self.prefix_cache = PrefixKVCache(2 * cfg.num_key_value_heads * cfg.head_dim, self.dev,
                                               self.act_dtype, prefix_cache_entries, suffix_reuse=suffix_kv_cache,
                                               host=bool(max_vram_gb))
-        # generation (prefix K/V cache): every call row-exact (see "exact K/V reuse" below)
-        self.row_exact = self.prefix_cache is not None
+        # generation (prefix K/V cache): every call row-exact (see "exact K/V reuse" below), unless
+        # exact_reuse=False trades that for the small-M kernels
+        self.row_exact = self.prefix_cache is not None and exact_reuse
         self._n_decoders = sum(1 for n in self.names if layer_kind(n) == "decoder")
         self._W_all: Dict[str, Dict[str, torch.Tensor]] = {}
         self._h2d0: Optional[int] = None     # prefetcher byte count at the start of the next call
@@ -1286,6 +1288,15 @@ class ShardedRunner:
         return batch, host, ev, pool_buf, (host_am if am is not None else None)
 
     def close(self):
+        if self._spec is not None:             # an enqueued speculative step finishes first
+            self._spec["done"].synchronize()
+            self._spec = None
+        # captured graphs and per-layer weight views hold the weight slots (resident: the whole
+        # model) and the K/V caches: drop them with the runner
+        self._graphs = self._decode_graphs = None
+        self._W_all = {}
+        self.prefix_cache = None
+        self.ctx.prefix_entry = None
         if self._inbox is not None:
             self._inbox.close()
             self._inbox = None

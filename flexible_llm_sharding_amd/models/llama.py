@@ -409,6 +409,8 @@ def _attention_whole(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tens
             if kv0 is None:
                 kv0 = pe.buffer(layer_name, create=True)
             ops.copy_rows(qkv[:, qs:qs + kv], meta["sfx_src"], kv0, meta["sfx_dst"])
+            if pe.host:                      # host-mode entry: the new rows into its host buffer too
+                pe.write_rows(ops, qkv[:, qs:qs + kv], meta["sfx_src"], meta["sfx_dst"], layer_name)
     work_items = getattr(ops, "uses_work_items", False)
     if prune:
         attn_arg = meta["work_last"] if work_items else batch.last_segments

@@ -242,6 +242,18 @@ class HipOps:
                                   rows, x.shape[1], _stream()), "fls_copy_rows")
         return y
 
+    def copy_rows_to(self, x, src_idx, y_ptr: int, y_ld: int, dst_idx):
+        """copy_rows into raw device-addressable memory (``y_ptr``: e.g. the device address of a
+        mapped pinned host buffer, row stride ``y_ld`` fp16 elements, rows of x.shape[1])."""
+        _f16(x, "x")
+        for t in (src_idx, dst_idx):
+            if t is None or t.dtype != torch.int32 or not t.is_cuda:
+                raise TypeError("row indices must be int32 CUDA")
+        if y_ld < x.shape[1]:
+            raise ValueError("destination rows narrower than the source rows")
+        _chk(self.k.fls_copy_rows(x.data_ptr(), x.stride(0), src_idx.data_ptr(), y_ptr, y_ld, dst_idx.data_ptr(),
+                                  src_idx.shape[0], x.shape[1], _stream()), "fls_copy_rows")
+
     def gather_rows(self, x, idx, out=None):
         """x[idx] into a new (or ``out``) [len(idx), H] tensor."""
         y = out if out is not None else torch.empty(idx.shape[0], x.shape[1], dtype=x.dtype, device=x.device)

@@ -356,7 +356,7 @@ def build_dp_sharded_runner(args, cfg, device, comm: Comm, tok, store: Optional[
                          prefix_kv_cache=(prefix_kv_cache if prefix_kv_cache is not None
                                           else getattr(args, "prefix_kv_cache", False) is True),
                          prefix_cache_entries=getattr(args, "prefix_cache_entries", 8),
-                         suffix_kv_cache=_suffix_kv(args, comm),
+                         suffix_kv_cache=_suffix_kv(args, comm), exact_reuse=getattr(args, "exact_reuse", True),
                          max_vram_gb=getattr(args, "max_vram_gb", None))
 
 

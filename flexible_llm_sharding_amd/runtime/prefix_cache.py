@@ -136,16 +136,33 @@ class PrefixEntry:
         self._staged = (layer_name, buf)
         return buf
 
+    def write_rows(self, ops, x: torch.Tensor, src_idx, dst_idx, layer_name: str) -> bool:
+        """Host mode, complete entry (a reused step): the new rows go straight into the layer's
+        mapped host buffer (a row-copy kernel writing over PCIe: ~0.6 MB per layer at 160 new rows,
+        instead of a write-back of every suffix region).  False when the buffer is not mapped."""
+        if self.stage is None or not self.complete:
+            return False
+        hb = self.layers.get(layer_name)
+        dp = self.stage.device_ptr(hb) if hb is not None else None
+        if dp is None or not hasattr(ops, "copy_rows_to"):
+            return False
+        ops.copy_rows_to(x, src_idx, dp, hb.shape[1], dst_idx)
+        self.stage.bytes_direct += src_idx.shape[0] * x.shape[1] * x.element_size()
+        if self._staged is not None and self._staged[0] == layer_name:
+            self._staged = (layer_name, self._staged[1], True)
+        return True
+
     def flush(self, layer_name: str) -> None:
         """After a layer's attention (host mode): the rows it may have written go back to the
         host buffer — all of them while the entry fills, the suffix regions once it is complete
-        (a reused step writes only its new suffix tokens)."""
+        (a reused step writes only its new suffix tokens; nothing when :meth:`write_rows` already
+        put them there)."""
         if self._staged is None or self._staged[0] != layer_name:
             return
-        buf = self._staged[1]
+        buf, direct = self._staged[1], len(self._staged) > 2
         self._staged = None
         lo = self.total if self.complete else 0
-        if lo < buf.shape[0]:
+        if lo < buf.shape[0] and not direct:
             self.stage.store(self.layers[layer_name], buf, lo, layer_name)
 
     def suffix_plan(self, tps: Sequence, reuse: bool):
@@ -208,13 +225,31 @@ class HostStage:
         self.buf_ev: List[Optional[object]] = [None] * self.N_BUFS
         self.layer_ev: Dict[tuple, object] = {}
         self.bytes_h2d = self.bytes_d2h = 0
+        self.bytes_direct = 0                 # rows kernels wrote straight into host buffers
+        self._dptr: Dict[int, int] = {}       # id(host buffer) -> its device address (mapped pinned)
 
     @property
     def nbytes(self) -> int:
         return sum(b.numel() * b.element_size() for b in self.bufs)
 
     def alloc_host(self, rows: int, cols: int, dtype) -> torch.Tensor:
-        return torch.zeros(rows, cols, dtype=dtype, pin_memory=self.cuda)
+        if not self.cuda:
+            return torch.zeros(rows, cols, dtype=dtype)
+        from . import hostmem
+        from .. import _native
+        nbytes = rows * cols * torch.empty(0, dtype=dtype).element_size()
+        t = hostmem.alloc_host(nbytes, pinned=True)
+        t.zero_()
+        hb = t.view(dtype).view(rows, cols)
+        rt = _native.runtime_or_none()
+        dp = rt.fls_host_device_ptr(t.data_ptr()) if rt is not None else None
+        if dp:
+            self._dptr[id(hb)] = int(dp)
+        return hb
+
+    def device_ptr(self, hb: torch.Tensor) -> Optional[int]:
+        """The device address of a host buffer (kernels write its rows over PCIe), or None."""
+        return self._dptr.get(id(hb))
 
     def acquire(self, rows: int) -> torch.Tensor:
         if rows > self.bufs[0].shape[0]:
@@ -253,15 +288,27 @@ class HostStage:
     def forget(self, e: "PrefixEntry") -> None:
         for name, hb in e.layers.items():
             self.layer_ev.pop((id(hb), name), None)
+            self._dptr.pop(id(hb), None)
+
+
+def suffix_growth(num_gen_token: int) -> int:
+    """Rows of growth per suffix region for a generation of ``num_gen_token`` steps: each step
+    appends one decoded token, which re-tokenizes to one or two tokens (4 per step + 8 spare,
+    at most ``PrefixKVCache.SUFFIX_GROWTH``).  A suffix that still outgrows its region is computed
+    in full (correct, not reused).  Smaller regions mean fewer key tiles per step and, in host
+    mode, fewer bytes staged over PCIe."""
+    return min(PrefixKVCache.SUFFIX_GROWTH, 4 * max(1, num_gen_token) + 8)
 
 
 class PrefixKVCache:
-    # suffix region per (prompt, suffix): its first call's length + this many tokens of growth
+    # suffix region per (prompt, suffix): its first call's length + suffix_growth tokens of growth
+    # (default SUFFIX_GROWTH; generation_loop sets it from --num_gen_token)
     SUFFIX_GROWTH = 64
 
     def __init__(self, kv_cols: int, device, dtype=torch.float16, max_entries: int = 8,
                  suffix_reuse: bool = True, host: bool = False):
         self.suffix_reuse = suffix_reuse
+        self.suffix_growth = self.SUFFIX_GROWTH
         self.host = host
         self.stage: Optional[HostStage] = None
         self.kv_cols = kv_cols
@@ -282,28 +329,27 @@ class PrefixKVCache:
             if self.stage is not None:
                 self.stage.forget(e)
 
-    @staticmethod
-    def entry_rows(tps: Sequence, suffix_reuse: bool) -> int:
+    def entry_rows(self, tps: Sequence) -> int:
         """Rows of the entry ``begin(tps)`` creates (prefixes + 64-aligned suffix regions)."""
         t = sum(len(tp.prefix) for tp in tps)
-        if suffix_reuse:
+        if self.suffix_reuse:
             for tp in tps:
                 for s in tp.suffixes:
-                    t = -(-t // PrefixEntry.REGION_ALIGN) * PrefixEntry.REGION_ALIGN + len(s) + PrefixKVCache.SUFFIX_GROWTH
+                    t = -(-t // PrefixEntry.REGION_ALIGN) * PrefixEntry.REGION_ALIGN + len(s) + self.suffix_growth
         return t
 
     def stage_bytes(self, tps: Sequence, elem: int = 2) -> int:
         """HBM of host mode's staging buffers for a call on ``tps`` (0 in device mode)."""
         if not self.host:
             return 0
-        rows = max(self.entry_rows(tps, self.suffix_reuse), self.stage.bufs[0].shape[0] if self.stage else 0)
+        rows = max(self.entry_rows(tps), self.stage.bufs[0].shape[0] if self.stage else 0)
         return HostStage.N_BUFS * rows * self.kv_cols * elem
 
     def ensure_stage(self, tps: Sequence) -> None:
         """Host mode: staging buffers large enough for ``tps``'s entry (grown, never shrunk)."""
         if not self.host:
             return
-        rows = self.entry_rows(tps, self.suffix_reuse)
+        rows = self.entry_rows(tps)
         if self.stage is None or self.stage.bufs[0].shape[0] < rows:
             old = self.stage
             if old is not None and old.cuda:
@@ -328,7 +374,7 @@ class PrefixKVCache:
         self._evict(self.entries.pop(key, None))
         while len(self.entries) >= self.max_entries:
             self._evict(self.entries.popitem(last=False)[1])
-        caps = ([[len(s) + self.SUFFIX_GROWTH for s in tp.suffixes] for tp in tps] if self.suffix_reuse else None)
+        caps = ([[len(s) + self.suffix_growth for s in tp.suffixes] for tp in tps] if self.suffix_reuse else None)
         self.ensure_stage(tps)
         e = PrefixEntry(key, [len(tp.prefix) for tp in tps], self.kv_cols, self.dev, self.dtype, caps,
                         stage=self.stage)

@@ -62,7 +62,13 @@ def build_parser() -> argparse.ArgumentParser:
                         "step), compute only the tokens after the longest common token prefix with the last call's "
                         "suffix (each step then costs its new tokens).  Exact: with the prefix cache every call runs "
                         "row-independent kernels, so a reused step's scores are bit for bit those of recomputing "
-                        "every suffix token (PARITY.md C21).  auto (default): on with the prefix K/V cache on one GPU")
+                        "every suffix token (PARITY.md C21).  auto (default): on with the prefix K/V cache on one GPU "
+                        "without --max_vram_gb (capped steps are PCIe-bound: staging the suffix regions costs more "
+                        "than recomputing the suffix tokens)")
+    p.add_argument("--exact_reuse", type=str2bool, nargs="?", const=True, default=True,
+                   help="with the K/V caches: run every call row-exact (default), so reused steps are bit for "
+                        "bit the full recomputation; false: the faster small-M kernels (skinny / split-K GEMMs, "
+                        "multi-suffix attention items), scores equal to rounding and tokens not guaranteed")
     p.add_argument("--prefix_cache_entries", type=int, default=8,
                    help="prefix K/V cache: calls (prompt batches) kept, LRU")
     p.add_argument("--resident", type=str2bool, nargs="?", const=True, default=False,

@@ -34,7 +34,9 @@ def main():
     ap.add_argument("--prefix-len", type=int, default=1024)
     ap.add_argument("--suffix-len", type=int, default=64)
     ap.add_argument("--json", default=None)
-    ap.add_argument("--only", default=None, choices=["exact", "reuse"], help="one run (a kernel trace)")
+    ap.add_argument("--only", default=None, choices=["exact", "reuse", "fast"], help="one run (a kernel trace)")
+    ap.add_argument("--fast", action="store_true",
+                    help="also the --exact_reuse false arm (small-M kernels; tokens compared, not guaranteed)")
     ap.add_argument("--max-vram-gb", type=float, default=None)
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -49,12 +51,13 @@ def main():
            "num_gen_token": a.gen,
            "weights": f"streamed, --max_vram_gb {a.max_vram_gb}" if a.max_vram_gb else "resident in HBM"}
     runs = {}
-    for name, sfx in (("exact", False), ("reuse", True)):
+    arms = [("exact", False, True), ("reuse", True, True)] + ([("fast", True, False)] if a.fast or a.only == "fast" else [])
+    for name, sfx, exact_reuse in arms:
         if a.only and name != a.only:
             continue
         kw = {"max_vram_gb": a.max_vram_gb} if a.max_vram_gb else {"resident": True}
         r = ShardedRunner(cfg, store, dev, tok, layer_num_per_shard=1, prefix_kv_cache=True, suffix_kv_cache=sfx,
-                          **kw)
+                          exact_reuse=exact_reuse, **kw)
         step_s = []
         sampler = None
         if a.max_vram_gb:
@@ -73,7 +76,8 @@ def main():
         if pc.host:
             res[name]["host_kv"] = {"host_gb": round(pc.nbytes / 1e9, 2), "staging_gb": round(pc.stage.nbytes / 1e9, 3),
                                     "h2d_gb": round(pc.stage.bytes_h2d / 1e9, 2),
-                                    "d2h_gb": round(pc.stage.bytes_d2h / 1e9, 2)}
+                                    "d2h_gb": round(pc.stage.bytes_d2h / 1e9, 2),
+                                    "direct_gb": round(pc.stage.bytes_direct / 1e9, 3)}
         if a.max_vram_gb:
             from flexible_llm_sharding_amd.runtime.memplan import device_used_bytes
             res[name]["device_used_gb_end"] = round(device_used_bytes(dev) / 1e9, 3)
@@ -93,8 +97,14 @@ def main():
     res["max_abs_diff_scores"] = float(max(np.abs(x.astype(np.float32) - y.astype(np.float32)).max()
                                            for x, y in zip(s0, s1)))
     res["steps_speedup_later"] = round(res["exact"]["later_step_s_median"] / res["reuse"]["later_step_s_median"], 2)
-    print(json.dumps({k: res[k] for k in ("tokens_equal", "scores_bitwise_equal", "max_abs_diff_scores",
-                                          "steps_speedup_later")}), flush=True)
+    keys = ["tokens_equal", "scores_bitwise_equal", "max_abs_diff_scores", "steps_speedup_later"]
+    if "fast" in runs:
+        s2, u2 = runs["fast"]
+        res["fast_tokens_equal"] = bool(u0 == u2)
+        res["fast_max_abs_diff_scores"] = float(max(np.abs(x.astype(np.float32) - y.astype(np.float32)).max()
+                                                    for x, y in zip(s0, s2)))
+        keys += ["fast_tokens_equal", "fast_max_abs_diff_scores"]
+    print(json.dumps({k: res[k] for k in keys}), flush=True)
     if a.json:
         with open(a.json, "w") as f:
             json.dump(res, f, indent=1)

@@ -1,5 +1,5 @@
-"""Generation-step GEMMs at the 70B shapes: the row-exact panel kernel (csrc/kernels/gemm_panel.h)
-against the row-exact mid-M kernel it replaces and the non-exact skinny / split-K paths.
+"""Generation-step GEMMs at the 70B shapes: the row-exact paths (panel kernel, csrc/kernels/gemm_panel.h;
+mid-M kernel with a 3- or 6-stage DMA ring) against the non-exact skinny / split-K paths.
 
     python scripts/panel_bench.py [--rows 64,160,320] [--iters 50]
 """
@@ -30,7 +30,10 @@ def main():
          "down": torch.randn(H, I, device=dev, generator=g).half() * 0.02}
     cos = torch.rand(8192, hd // 2, device=dev)
     sin = torch.rand(8192, hd // 2, device=dev)
-    arms = {"panel_exact": (True, 1), "mid_exact": (True, 0), "skinny_splitk": (False, 1), "panel_any": (False, 2)}
+    # arm -> (row-exact, fls_gemm_set_panel, fls_gemm_set_mid): exact default (panel where it wins, 6-stage
+    # mid for one-round grids), exact on the 3-stage mid kernel only (round-5 / early round-6 path), exact
+    # on the 6-stage mid only, the non-exact default (skinny / split-K)
+    arms = {"exact": (True, 1, 1), "exact_mid3": (True, 0, 2), "exact_mid6": (True, 0, 1), "fast": (False, 1, 1)}
     for M in [int(r) for r in a.rows.split(",")]:
         x = torch.randn(M, H, device=dev, generator=g).half()
         xi = torch.randn(M, I, device=dev, generator=g).half()
@@ -46,8 +49,9 @@ def main():
         }
         res = {"M": M}
         outs = {}
-        for arm, (exact, panel) in arms.items():
+        for arm, (exact, panel, mid) in arms.items():
             old = ops.k.fls_gemm_set_panel(panel)
+            old_mid = ops.k.fls_gemm_set_mid(mid)
             try:
                 with ops.row_exact(exact):
                     tot = 0.0
@@ -70,7 +74,9 @@ def main():
                     res[f"{arm}.layer_us"] = round(tot, 1)
             finally:
                 ops.k.fls_gemm_set_panel(old)
-        res["panel_eq_mid_gate_up"] = bool(torch.equal(outs["panel_exact"], outs["mid_exact"]))
+                ops.k.fls_gemm_set_mid(old_mid)
+        res["exact_arms_bitwise_equal"] = bool(torch.equal(outs["exact"], outs["exact_mid3"])
+                                               and torch.equal(outs["exact"], outs["exact_mid6"]))
         print(json.dumps(res), flush=True)
 
 

@@ -546,13 +546,40 @@ def test_suffix_reuse_bitwise_exact(setup, weights):
         if weights == "capped":
             st = r.prefix_cache.stage
             assert r.prefix_cache.host and st.bytes_h2d > 0 and st.bytes_d2h > 0
-            assert all(t.is_pinned() for e in r.prefix_cache.entries.values() for t in e.layers.values())
+            assert all(not t.is_cuda for e in r.prefix_cache.entries.values() for t in e.layers.values())
+            if sfx:           # reused steps wrote their new rows straight into the mapped host buffers
+                assert st.bytes_direct > 0
         r.close()
     (s0, u0), (s1, u1) = outs[False], outs[True]
     assert u0 == u1
     for a, b in zip(s0, s1):
         assert np.isfinite(a.astype(np.float32)).all()
         assert np.array_equal(a, b)
+
+
+def test_fast_reuse_runs_small_m_kernels(setup):
+    """--exact_reuse false: generation with suffix K/V reuse on the small-M kernels (skinny / split-K
+    GEMMs, multi-suffix items; decode graphs with the weights resident) — not bitwise, so checked
+    against the exact generation to fp16 rounding at the first step and for finite scores after."""
+    import argparse
+    from flexible_llm_sharding_amd.api import generation_loop
+    from flexible_llm_sharding_amd.parallel.comm import Comm
+    path, cfg, tok, _, _ = setup
+    prompts = synthetic_prompts(4, 90, 3, 40, cfg.vocab_size, seed=12, vary=True)
+    src = HostStore.from_model_path(cfg, path)
+    args = argparse.Namespace(num_gen_token=5, data_parallel=False, num_batch=1)
+    outs = {}
+    for exact in (True, False):
+        r = ShardedRunner(cfg, src, "cuda:0", tok, layer_num_per_shard=1, prefix_kv_cache=True, suffix_kv_cache=True,
+                          resident=True, exact_reuse=exact)
+        assert r.row_exact is exact
+        outs[exact] = generation_loop(args, r, Comm(), tok, prompts)
+        assert r.stats["suffix_tokens_reused"] > 0
+        r.close()
+    (s0, _), (s1, _) = outs[True], outs[False]
+    for a, b in zip(s0, s1):
+        assert np.isfinite(b.astype(np.float32)).all()
+        assert np.abs(a[:, 0].astype(np.float32) - b[:, 0].astype(np.float32)).max() < 2e-3
 
 
 def test_piece_pool_streams_layer_files(mid_model, tmp_path):

@@ -406,9 +406,9 @@ def test_gemm_main_all_epilogues(ops, ref):
 @pytest.mark.parametrize("hd", [128, 64])
 def test_gemm_panel_rows_bitwise(ops, ref, hd):
     """Row-exact small-M GEMMs take the panel kernel (all rows x 32 columns per block, one K chain):
-    every row of M = 1 / 17 / 160 / 320 equals, bit for bit, the same row of a 1,000-row row-exact
-    GEMM (v10 / v11 / mid tiles), for all four epilogues incl. bias, per-row scale and RoPE (both
-    head sizes); and the fp32 reference."""
+    every row of M = 1 / 17 / 64 / 160 / 320 equals, bit for bit, the same row of a 1,000-row row-exact
+    GEMM (mid tiles, 6-stage ring, itself bitwise the 3-stage ring), for all four epilogues incl.
+    bias, per-row scale and RoPE (both head sizes); and the fp32 reference."""
     from flexible_llm_sharding_amd.config import ModelConfig
     from flexible_llm_sharding_amd.models.llama import rope_tables
     Mb, H, I, nh, nkv = 1000, 1024, 1536, 8, 2
@@ -420,7 +420,7 @@ def test_gemm_panel_rows_bitwise(ops, ref, hd):
     wqkv = rnd((nh + 2 * nkv) * hd, H, scale=0.03, seed=65)
     bq = rnd((nh + 2 * nkv) * hd, scale=0.5, seed=66)
     pos = torch.randint(0, 4000, (Mb,), dtype=torch.int32, device=DEV)
-    cfg = ModelConfig(hidden_size=nh * hd, num_attention_heads=nh, num_key_value_heads=nkv, head_dim=hd)
+    cfg = ModelConfig(hidden_size=nh * hd, num_attention_heads=nh, num_key_value_heads=nkv)
     cos, sin = rope_tables(cfg, 4096)
     cos, sin = cos.to(DEV), sin.to(DEV)
 
@@ -434,11 +434,21 @@ def test_gemm_panel_rows_bitwise(ops, ref, hd):
 
     with ops.row_exact():
         full = run(torch.arange(Mb, device=DEV))
+        old_mid = ops.k.fls_gemm_set_mid(2)      # the 3-stage mid kernel (default: 6 stages for these grids)
+        try:
+            for a, b in zip(run(torch.arange(Mb, device=DEV)), full):
+                assert torch.equal(a, b)
+        finally:
+            ops.k.fls_gemm_set_mid(old_mid)
         g = torch.Generator().manual_seed(5)
-        for m in (1, 17, 160, 320):
-            rows = torch.randperm(Mb, generator=g)[:m].to(DEV)
-            for a, b in zip(run(rows), full):
-                assert torch.equal(a, b[rows]), m
+        old = ops.k.fls_gemm_set_panel(2)        # the panel kernel at every M <= 320 (auto: M <= 64)
+        try:
+            for m in (1, 17, 64, 160, 320):
+                rows = torch.randperm(Mb, generator=g)[:m].to(DEV)
+                for a, b in zip(run(rows), full):
+                    assert torch.equal(a, b[rows]), m
+        finally:
+            ops.k.fls_gemm_set_panel(old)
     torch.cuda.synchronize()
     assert rel_err(full[0], x.float() @ wo.float().t()) < 2e-3
     assert rel_err(full[2].cpu(), ref.swiglu_up((x.float() * rs[:, None]).cpu(), wgu.float().cpu())) < 3e-3
