@@ -129,16 +129,15 @@ __global__ __launch_bounds__(256) void gemm_nt_generic(const half_t* __restrict_
 // same XCD so each weight tile comes from HBM once and from L2 after that.
 // Any K-tile count (the tail path for odd K / 64).
 namespace mid {
-constexpr int BMm = 64, BNm = 128, BKm = 64, NTm = 256, NSTAGE = 3, NSTAGE_DEEP = 6;
+constexpr int BMm = 64, BNm = 128, BKm = 64, NTm = 256, NSTAGE = 3;
 constexpr int STAGE = (BMm + BNm) * BKm * 2;     // 24 KiB: A rows 0..63 then W rows 0..127
 constexpr int GROUPS = (BMm + BNm) / 8;          // 8-row (1 KiB) LDS-DMA groups per stage
 constexpr int PER_WAVE = GROUPS / 4;             // 6 LDS-DMA per wave per stage
 }  // namespace mid
 
-// NST: LDS stages, NST - 1 K-tiles in flight ahead of the one being multiplied.  3 (72 KB: two blocks
-// per CU) for grids of several rounds; 6 (144 KB) when the grid is at most one block per CU
-// (generation-step shapes: 70B O / down at M = 160 are 192 blocks of 128 / 448 K-tiles, each block
-// bound by the latency of its own DMA stream, not by bandwidth)
+// NST: LDS stages, NST - 1 K-tiles in flight ahead of the one being multiplied (3: 72 KB, two blocks
+// per CU).  A 6-stage ring for one-round grids measured the same (70B generation-step shapes at
+// M = 16-320, profiles/r6_decode/mid_ring): the blocks are not bound by their DMA latency
 template <int EPI, int NST>
 __global__ __launch_bounds__(mid::NTm) void gemm_nt_mid(const half_t* __restrict__ A, const half_t* __restrict__ W,
                                                      half_t* __restrict__ C, int M, int N, int K, int lda, int ldw,
@@ -247,7 +246,6 @@ __global__ __launch_bounds__(mid::NTm) void gemm_nt_mid(const half_t* __restrict
 
 int g_order = 0;             // 0: by shape, else a fixed signed group size (fls_gemm_set_order)
 int g_mid = 1;               // mid-M kernel on (fls_gemm_set_mid)
-int g_mid_deep = 1;          // 6-stage mid kernel for grids of <= 256 blocks (fls_gemm_set_mid: 2 = off, A/B)
 
 template <int EPI, int NST>
 void launch_mid(int blocks, const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int lda, int ldw,
@@ -452,10 +450,7 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
   }
   if (mid_ok && (!main_ok || (g_mid && (tiles256 < 128 || (M <= 64 && tiles256 < 512))))) {
     const int blocks = ((M + mid::BMm - 1) / mid::BMm) * (N / mid::BNm);
-    if (g_mid_deep && blocks <= 256)
-      launch_mid<EPI, mid::NSTAGE_DEEP>(blocks, A, W, C, M, N, K, lda, ldw, ldc, ep, s);
-    else
-      launch_mid<EPI, mid::NSTAGE>(blocks, A, W, C, M, N, K, lda, ldw, ldc, ep, s);
+    launch_mid<EPI, mid::NSTAGE>(blocks, A, W, C, M, N, K, lda, ldw, ldc, ep, s);
     FLS_CHECK_LAUNCH();
     ss_partials(C, ldc, M, N, ep, s);
     FLS_CHECK_LAUNCH();
@@ -551,11 +546,10 @@ extern "C" int fls_gemm_set_panel(int mode) {
   return old;
 }
 
-// mid-M kernel for small grids: 1 on (default), 0 off (tests), 2 on without the deep-ring variant (A/B)
+// mid-M kernel for small grids on (1, default) or off (0; tests)
 extern "C" int fls_gemm_set_mid(int on) {
-  const int old = g_mid ? (g_mid_deep ? 1 : 2) : 0;
+  const int old = g_mid;
   g_mid = on ? 1 : 0;
-  g_mid_deep = on == 2 ? 0 : 1;
   return old;
 }
 

@@ -141,7 +141,7 @@ int try_panel(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, 
               const Epi& ep, hipStream_t s) {
   if (!g_panel || (g_panel == 1 && !ep.row_exact)) return 0;
   // auto (1): where it measured faster than the mid kernel, row-exact 70B shapes (profiles/r6_decode,
-  // scripts/panel_bench.py): M = 64 QKV 52.6 vs 61.1 us, O 51.1 vs 60.0, down 170 vs 231; not the wide
+  // scripts/decode_gemm_bench.py): M = 64 QKV 52.6 vs 61.1 us, O 51.1 vs 60.0, down 170 vs 231; not the wide
   // gate/up (234 vs 171) nor any shape at M = 160 / 320 (2.5x slower: every block stages ALL the
   // activation rows, so the L2 -> LDS activation traffic is N / 32 times M x K and bounds it)
   if (g_panel == 1 && (M > 64 || N > 16384)) return 0;

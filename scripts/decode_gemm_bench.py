@@ -1,7 +1,7 @@
 """Generation-step GEMMs at the 70B shapes: the row-exact paths (panel kernel, csrc/kernels/gemm_panel.h;
-mid-M kernel with a 3- or 6-stage DMA ring) against the non-exact skinny / split-K paths.
+mid-M kernel) against the non-exact skinny / split-K paths.
 
-    python scripts/panel_bench.py [--rows 64,160,320] [--iters 50]
+    python scripts/decode_gemm_bench.py [--rows 64,160,320] [--iters 50]
 """
 import argparse
 import json
@@ -30,10 +30,10 @@ def main():
          "down": torch.randn(H, I, device=dev, generator=g).half() * 0.02}
     cos = torch.rand(8192, hd // 2, device=dev)
     sin = torch.rand(8192, hd // 2, device=dev)
-    # arm -> (row-exact, fls_gemm_set_panel, fls_gemm_set_mid): exact default (panel where it wins, 6-stage
-    # mid for one-round grids), exact on the 3-stage mid kernel only (round-5 / early round-6 path), exact
-    # on the 6-stage mid only, the non-exact default (skinny / split-K)
-    arms = {"exact": (True, 1, 1), "exact_mid3": (True, 0, 2), "exact_mid6": (True, 0, 1), "fast": (False, 1, 1)}
+    # arm -> (row-exact, fls_gemm_set_panel, fls_gemm_set_mid): exact default (panel where it wins, else the
+    # mid-M kernel), exact on the mid kernel only, every M <= 320 on the panel kernel, the non-exact default
+    # (skinny / split-K)
+    arms = {"exact": (True, 1, 1), "exact_mid": (True, 0, 1), "exact_panel": (True, 2, 1), "fast": (False, 1, 1)}
     for M in [int(r) for r in a.rows.split(",")]:
         x = torch.randn(M, H, device=dev, generator=g).half()
         xi = torch.randn(M, I, device=dev, generator=g).half()
@@ -75,8 +75,8 @@ def main():
             finally:
                 ops.k.fls_gemm_set_panel(old)
                 ops.k.fls_gemm_set_mid(old_mid)
-        res["exact_arms_bitwise_equal"] = bool(torch.equal(outs["exact"], outs["exact_mid3"])
-                                               and torch.equal(outs["exact"], outs["exact_mid6"]))
+        res["exact_arms_bitwise_equal"] = bool(torch.equal(outs["exact"], outs["exact_mid"])
+                                               and torch.equal(outs["exact"], outs["exact_panel"]))
         print(json.dumps(res), flush=True)
 
 
