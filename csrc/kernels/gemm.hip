@@ -130,23 +130,28 @@ __global__ __launch_bounds__(256) void gemm_nt_generic(const half_t* __restrict_
 // Any K-tile count (the tail path for odd K / 64).
 namespace mid {
 constexpr int BMm = 64, BNm = 128, BKm = 64, NTm = 256, NSTAGE = 3;
-constexpr int STAGE = (BMm + BNm) * BKm * 2;     // 24 KiB: A rows 0..63 then W rows 0..127
-constexpr int GROUPS = (BMm + BNm) / 8;          // 8-row (1 KiB) LDS-DMA groups per stage
-constexpr int PER_WAVE = GROUPS / 4;             // 6 LDS-DMA per wave per stage
+// BNT: output columns per block, 128 (4 waves in 2 x 2, each 32 x 64) or 64 (each 32 x 32: twice the
+// blocks for grids of less than one round of 128-column tiles)
+constexpr int stage_bytes(int bnt) { return (BMm + bnt) * BKm * 2; }   // A rows 0..63 then W rows
+constexpr int per_wave(int bnt) { return (BMm + bnt) / 8 / 4; }        // 8-row (1 KiB) LDS-DMA groups
 }  // namespace mid
 
 // NST: LDS stages, NST - 1 K-tiles in flight ahead of the one being multiplied (3: 72 KB, two blocks
 // per CU).  A 6-stage ring for one-round grids measured the same (70B generation-step shapes at
-// M = 16-320, profiles/r6_decode/mid_ring): the blocks are not bound by their DMA latency
-template <int EPI, int NST>
+// M = 16-320, profiles/r6_decode/mid_ring): the blocks are not bound by their DMA latency.
+// BNT = 64 blocks: a wave holds two 16-column subtiles (RoPE: a column and its partner hd/2 away; for
+// head_dim 128 a block takes 32 columns of a head and their 32 partners).  Same fragments, MFMA and
+// K order as BNT = 128, so the two are bitwise equal.
+template <int EPI, int NST, int BNT>
 __global__ __launch_bounds__(mid::NTm) void gemm_nt_mid(const half_t* __restrict__ A, const half_t* __restrict__ W,
                                                      half_t* __restrict__ C, int M, int N, int K, int lda, int ldw,
                                                      int ldc, Epi ep) {
   using namespace mid;
+  constexpr int STAGE = stage_bytes(BNT), PER_WAVE = per_wave(BNT), NSUB = BNT / 32;
   extern __shared__ __attribute__((aligned(16))) char lds_mid[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, grp = lane >> 4;
-  const int mt = (M + BMm - 1) / BMm, ntn = N / BNm;
+  const int mt = (M + BMm - 1) / BMm, ntn = N / BNT;
   // XCD-aware bijective remap: logical tiles [xcd*q .. ) run on one XCD, M fastest
   int bid = blockIdx.x;
   {
@@ -155,10 +160,17 @@ __global__ __launch_bounds__(mid::NTm) void gemm_nt_mid(const half_t* __restrict
     if (nwg >= 8) bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
   }
   const int m0 = (bid % mt) * BMm;
-  const int n0 = (bid / mt) * BNm;
+  const int bn = bid / mt;
+  const int n0 = bn * BNT;
   const int wm = wave >> 1, wn = wave & 1;
   const int nk = K / BKm;
   const bool rope128 = EPI == FLS_EPI_ROPE;
+  // BNT = 64 with RoPE over 128-wide heads: local W row l -> column of head bn / 2, quarter bn % 2
+  const bool split_head = BNT == 64 && rope128;
+  auto gcol = [&](int l) -> int {
+    if (split_head) return (bn >> 1) * 128 + (bn & 1) * 32 + (l < 32 ? l : 64 + (l - 32));
+    return n0 + l;
+  };
 
   // this lane's LDS-DMA sources: group g = wave + 4*i covers tile rows 8*g .. 8*g+7
   const half_t* src[PER_WAVE];
@@ -171,7 +183,7 @@ __global__ __launch_bounds__(mid::NTm) void gemm_nt_mid(const half_t* __restrict
       const int m = min(m0 + g * 8 + sub, M - 1);
       src[i] = A + (size_t)m * lda + kc;
     } else {
-      const int n = n0 + (g - BMm / 8) * 8 + sub;
+      const int n = gcol((g - BMm / 8) * 8 + sub);
       const int nr = EPI == FLS_EPI_SWIGLU ? gu_phys_row(n, ep.gu_rows) : n;
       src[i] = W + (size_t)nr * ldw + kc;
     }
@@ -183,15 +195,19 @@ __global__ __launch_bounds__(mid::NTm) void gemm_nt_mid(const half_t* __restrict
 #pragma unroll
     for (int i = 0; i < PER_WAVE; ++i) glds16(src[i] + (size_t)kt * BKm, base + (wave + 4 * i) * 1024);
   };
-  int wrow[4];
+  // local W rows of this wave's subtiles (RoPE: subtile t + NSUB / 2 is subtile t's partner)
+  int wrow[NSUB];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) wrow[t] = sub_col(rope128, wn, t) + fr;
+  for (int t = 0; t < NSUB; ++t) {
+    if constexpr (BNT == 128) wrow[t] = sub_col(rope128, wn, t) + fr;
+    else wrow[t] = (is_rope(EPI) ? wn * 16 + t * 32 : wn * 32 + t * 16) + fr;
+  }
 
-  floatx4 acc[2][4];
+  floatx4 acc[2][NSUB];
 #pragma unroll
   for (int u = 0; u < 2; ++u)
 #pragma unroll
-    for (int t = 0; t < 4; ++t) acc[u][t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < NSUB; ++t) acc[u][t] = floatx4{0.f, 0.f, 0.f, 0.f};
 
 #pragma unroll
   for (int d = 0; d < NST - 1; ++d) stage(d, min(d, nk - 1));
@@ -205,21 +221,21 @@ __global__ __launch_bounds__(mid::NTm) void gemm_nt_mid(const half_t* __restrict
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int c = ks * 4 + grp;                          // logical 16-byte chunk of this lane
-      half8 xf[2], wf[4];
+      half8 xf[2], wf[NSUB];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int r = wm * 32 + u * 16 + fr;
         xf[u] = *(const half8*)(Xs + r * 128 + ((c ^ (r & 7)) << 4));
       }
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
+      for (int t = 0; t < NSUB; ++t) {
         const int r = wrow[t];
         wf[t] = *(const half8*)(Ws + r * 128 + ((c ^ (r & 7)) << 4));
       }
 #pragma unroll
       for (int u = 0; u < 2; ++u)
 #pragma unroll
-        for (int t = 0; t < 4; ++t) acc[u][t] = mfma16x16x32(wf[t], xf[u], acc[u][t]);
+        for (int t = 0; t < NSUB; ++t) acc[u][t] = mfma16x16x32(wf[t], xf[u], acc[u][t]);
     }
     // WAR: the next iteration's DMA overwrites this stage; all reads are done
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -231,13 +247,17 @@ __global__ __launch_bounds__(mid::NTm) void gemm_nt_mid(const half_t* __restrict
     const int m = m0 + wm * 32 + u * 16 + fr;
     if (m >= M) continue;
     if constexpr (is_rope(EPI)) {
+      if constexpr (BNT == 128) {
 #pragma unroll
-      for (int q = 0; q < 2; ++q)
-        store_rope_pair(C, ldc, m, n0 + sub_col(rope128, wn, q) + 4 * grp, acc[u][q], acc[u][q + 2], ep);
+        for (int q = 0; q < 2; ++q)
+          store_rope_pair(C, ldc, m, n0 + sub_col(rope128, wn, q) + 4 * grp, acc[u][q], acc[u][q + 2], ep);
+      } else {
+        store_rope_pair(C, ldc, m, gcol(wn * 16) + 4 * grp, acc[u][0], acc[u][1], ep);
+      }
     } else {
 #pragma unroll
-      for (int p = 0; p < 2; ++p)
-        store_pair_off<EPI>(C, ldc, m, n0 + wn * 64 + p * 32, 4 * grp, acc[u][2 * p], acc[u][2 * p + 1], ep);
+      for (int p = 0; p < NSUB / 2; ++p)
+        store_pair_off<EPI>(C, ldc, m, n0 + wn * (BNT / 2) + p * 32, 4 * grp, acc[u][2 * p], acc[u][2 * p + 1], ep);
     }
   }
 }
@@ -246,18 +266,20 @@ __global__ __launch_bounds__(mid::NTm) void gemm_nt_mid(const half_t* __restrict
 
 int g_order = 0;             // 0: by shape, else a fixed signed group size (fls_gemm_set_order)
 int g_mid = 1;               // mid-M kernel on (fls_gemm_set_mid)
+int g_mid_bn = 0;            // mid-M block columns: 0 auto, 64 / 128 forced where valid (fls_gemm_set_mid_bn)
 
-template <int EPI, int NST>
-void launch_mid(int blocks, const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int lda, int ldw,
-                int ldc, const Epi& ep, hipStream_t s) {
+template <int EPI, int NST, int BNT>
+void launch_mid(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int lda, int ldw, int ldc,
+                const Epi& ep, hipStream_t s) {
   static bool attr = false;
+  constexpr int lds = NST * mid::stage_bytes(BNT);
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_nt_mid<EPI, NST>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              NST * mid::STAGE);
+    (void)hipFuncSetAttribute((const void*)gemm_nt_mid<EPI, NST, BNT>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
-  hipLaunchKernelGGL((gemm_nt_mid<EPI, NST>), dim3(blocks), dim3(mid::NTm), NST * mid::STAGE, s, A, W, C, M, N, K, lda,
-                     ldw, ldc, ep);
+  const int blocks = ((M + mid::BMm - 1) / mid::BMm) * (N / BNT);
+  hipLaunchKernelGGL((gemm_nt_mid<EPI, NST, BNT>), dim3(blocks), dim3(mid::NTm), lds, s, A, W, C, M, N, K, lda, ldw,
+                     ldc, ep);
 }
 
 template <int EPI>
@@ -449,8 +471,15 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
     return 0;
   }
   if (mid_ok && (!main_ok || (g_mid && (tiles256 < 128 || (M <= 64 && tiles256 < 512))))) {
-    const int blocks = ((M + mid::BMm - 1) / mid::BMm) * (N / mid::BNm);
-    launch_mid<EPI, mid::NSTAGE>(blocks, A, W, C, M, N, K, lda, ldw, ldc, ep, s);
+    // 64-column blocks when 128-column ones fill less than one round of the 256 CUs (generation-step
+    // O / down / QKV: 192-240 blocks -> 384-480)
+    const int blocks128 = ((M + mid::BMm - 1) / mid::BMm) * (N / mid::BNm);
+    const bool bn64_ok = N % 64 == 0 && (EPI != FLS_EPI_ROPE || N % 128 == 0);
+    const bool bn64 = bn64_ok && (g_mid_bn == 64 || (g_mid_bn == 0 && blocks128 < 256));
+    if (bn64)
+      launch_mid<EPI, mid::NSTAGE, 64>(A, W, C, M, N, K, lda, ldw, ldc, ep, s);
+    else
+      launch_mid<EPI, mid::NSTAGE, 128>(A, W, C, M, N, K, lda, ldw, ldc, ep, s);
     FLS_CHECK_LAUNCH();
     ss_partials(C, ldc, M, N, ep, s);
     FLS_CHECK_LAUNCH();
@@ -543,6 +572,13 @@ extern "C" int fls_gemm_set_row_chunk(int rows) {
 extern "C" int fls_gemm_set_panel(int mode) {
   const int old = g_panel;
   g_panel = mode < 0 ? 0 : mode > 2 ? 2 : mode;
+  return old;
+}
+
+// mid-M block columns: 0 auto (default), 64 or 128 forced where valid (tests / A-B); returns the previous
+extern "C" int fls_gemm_set_mid_bn(int bn) {
+  const int old = g_mid_bn;
+  g_mid_bn = bn == 64 || bn == 128 ? bn : 0;
   return old;
 }
 

@@ -87,6 +87,7 @@ def _load_kernels(path: str = _KERNELS):
     _bind(lib, "fls_gemm_set_splitk", c_int, c_int)
     _bind(lib, "fls_gemm_set_row_chunk", c_int, c_int)
     _bind(lib, "fls_gemm_set_mid", c_int, c_int)
+    _bind(lib, "fls_gemm_set_mid_bn", c_int, c_int)
     _bind(lib, "fls_gemm_set_panel", c_int, c_int)
     _bind(lib, "fls_moe_route", c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
           c_void_p)

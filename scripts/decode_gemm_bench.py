@@ -32,8 +32,9 @@ def main():
     sin = torch.rand(8192, hd // 2, device=dev)
     # arm -> (row-exact, fls_gemm_set_panel, fls_gemm_set_mid): exact default (panel where it wins, else the
     # mid-M kernel), exact on the mid kernel only, every M <= 320 on the panel kernel, the non-exact default
-    # (skinny / split-K)
-    arms = {"exact": (True, 1, 1), "exact_mid": (True, 0, 1), "exact_panel": (True, 2, 1), "fast": (False, 1, 1)}
+    # (skinny / split-K); exact_mid128: the mid kernel with 128-column blocks only
+    arms = {"exact": (True, 1, 1), "exact_mid": (True, 0, 1), "exact_panel": (True, 2, 1), "fast": (False, 1, 1),
+            "exact_mid128": (True, 0, 1)}
     for M in [int(r) for r in a.rows.split(",")]:
         x = torch.randn(M, H, device=dev, generator=g).half()
         xi = torch.randn(M, I, device=dev, generator=g).half()
@@ -52,6 +53,7 @@ def main():
         for arm, (exact, panel, mid) in arms.items():
             old = ops.k.fls_gemm_set_panel(panel)
             old_mid = ops.k.fls_gemm_set_mid(mid)
+            old_bn = ops.k.fls_gemm_set_mid_bn(128 if arm == "exact_mid128" else 0)
             try:
                 with ops.row_exact(exact):
                     tot = 0.0
@@ -75,8 +77,10 @@ def main():
             finally:
                 ops.k.fls_gemm_set_panel(old)
                 ops.k.fls_gemm_set_mid(old_mid)
+                ops.k.fls_gemm_set_mid_bn(old_bn)
         res["exact_arms_bitwise_equal"] = bool(torch.equal(outs["exact"], outs["exact_mid"])
-                                               and torch.equal(outs["exact"], outs["exact_panel"]))
+                                               and torch.equal(outs["exact"], outs["exact_panel"])
+                                               and torch.equal(outs["exact"], outs["exact_mid128"]))
         print(json.dumps(res), flush=True)
 
 

@@ -407,8 +407,8 @@ def test_gemm_main_all_epilogues(ops, ref):
 def test_gemm_panel_rows_bitwise(ops, ref, hd):
     """Row-exact small-M GEMMs take the panel kernel (all rows x 32 columns per block, one K chain):
     every row of M = 1 / 17 / 64 / 160 / 320 equals, bit for bit, the same row of a 1,000-row row-exact
-    GEMM (mid tiles), for all four epilogues incl. bias, per-row scale and RoPE (both head sizes); and
-    the fp32 reference."""
+    GEMM (mid tiles of 64 or 128 columns, bitwise equal), for all four epilogues incl. bias, per-row
+    scale and RoPE (both head sizes); and the fp32 reference."""
     from flexible_llm_sharding_amd.config import ModelConfig
     from flexible_llm_sharding_amd.models.llama import rope_tables
     Mb, H, I, nh, nkv = 1000, 1024, 1536, 8, 2
@@ -434,6 +434,13 @@ def test_gemm_panel_rows_bitwise(ops, ref, hd):
 
     with ops.row_exact():
         full = run(torch.arange(Mb, device=DEV))
+        for bn in (128, 64):                     # the mid kernel's 128- and 64-column blocks (auto: 64 here)
+            old_bn = ops.k.fls_gemm_set_mid_bn(bn)
+            try:
+                for a, b in zip(run(torch.arange(Mb, device=DEV)), full):
+                    assert torch.equal(a, b), bn
+            finally:
+                ops.k.fls_gemm_set_mid_bn(old_bn)
         g = torch.Generator().manual_seed(5)
         old = ops.k.fls_gemm_set_panel(2)        # the panel kernel at every M <= 320 (auto: M <= 64)
         try:
