@@ -83,6 +83,7 @@ int fls_gemm(const void* A, const void* W, void* C, const void* R, int M, int N,
 // columns [128 j, 128 j + 128) -- the row statistic of the next norm-folded projection without a
 // pass over the hidden state (fls_rstd_from_ss)
 // rstd[r] = rsqrt(sum_j ss[r * ss_ld + j] / H + eps) for j < nparts, summed in a fixed order
+int fls_row_ss(const void* x, int ldx, int rows, int H, float* ss, int ss_ld, fls_stream_t s);  // residual-epilogue partials of x
 int fls_rstd_from_ss(const float* ss, int ss_ld, int nparts, int rows, int H, float eps, float* rstd,
                      fls_stream_t s);
 // out[r] = first index of the maximum of row r of non-negative fp16 values (greedy decoding)
@@ -116,7 +117,6 @@ int fls_moe_gemm(const void* A, const void* W, void* C, int M_bound, int N, int 
 int fls_moe_combine(const void* y, int ldy, const int* ids, const int* dest, const float* w, void* x, int ldx, int T,
                     int k, int H, const void* sh, int ldsh, fls_stream_t s);   // sh: optional shared-expert term
 int fls_gemm_set_order(int order);   // tile order: 0 by shape, 8 M-grouped, -4/-8 N-grouped
-int fls_gemm_set_panel(int mode);   // all-rows x 32-column panel kernel: 0 off, 1 row-exact (default), 2 any M <= 320
 int fls_gemm_set_mid_bn(int bn);     // mid-M block columns: 0 auto, 64 / 128 forced
 int fls_gemm_set_mid(int on);   // 64x128-tile kernel for small / medium M (default on)
 // shared-prefix / varlen flash attention over packed work items (int32 x8:

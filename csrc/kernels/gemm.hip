@@ -262,8 +262,6 @@ __global__ __launch_bounds__(mid::NTm) void gemm_nt_mid(const half_t* __restrict
   }
 }
 
-#include "gemm_panel.h"
-
 int g_order = 0;             // 0: by shape, else a fixed signed group size (fls_gemm_set_order)
 int g_mid = 1;               // mid-M kernel on (fls_gemm_set_mid)
 int g_mid_bn = 0;            // mid-M block columns: 0 auto, 64 / 128 forced where valid (fls_gemm_set_mid_bn)
@@ -378,22 +376,33 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 
 // ss[m * ss_ld + j] = sum over columns [128 j, 128 j + 128) of C[m, :]^2 (fp32 of the fp16 values):
 // the per-row partials of the v10 / v11 residual epilogue (Epi::ss) for the GEMM paths whose own
-// epilogue does not write them (skinny, split-K, mid-M, generic: small M).  One wave per (row, part).
+// epilogue does not write them (skinny, split-K, mid-M, generic: small M), and the fused norm's
+// statistic of a hidden state without partials (fls_row_ss).  One wave per (16 rows, 128 columns) in
+// the epilogue's lane layout -- lane (row fr, group g) holds columns 32 p + 4 g + r and 32 p + 16 +
+// 4 g + r, p, r < 4 -- through the same ss_accum_pair and row_sum_4groups: bitwise the epilogue's.
 __global__ __launch_bounds__(256) void ss_partials_kernel(const half_t* __restrict__ C, int ldc, int M, int nparts,
                                                           float* __restrict__ ss, int ss_ld) {
   const int w = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (w >= M * nparts) return;                      // wave-uniform
-  const int m = w / nparts, j = w % nparts;
-  const half_t* p = C + (size_t)m * ldc + j * 128 + lane * 2;
-  float sq = (float)p[0] * (float)p[0] + (float)p[1] * (float)p[1];
-  sq = warp_sum(sq);
-  if (lane == 0) ss[(size_t)m * ss_ld + j] = sq;
+  const int rgroups = (M + 15) / 16;
+  if (w >= rgroups * nparts) return;                // wave-uniform
+  const int fr = lane & 15, grp = lane >> 4;
+  const int m = (w / nparts) * 16 + fr, j = w % nparts;
+  const half_t* p0 = C + (size_t)min(m, M - 1) * ldc + j * 128 + grp * 4;
+  float sq = 0.f;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) sq = ss_accum_pair(sq, *(const half4*)(p0 + p * 32), *(const half4*)(p0 + p * 32 + 16));
+  sq = row_sum_4groups(sq);                         // every lane (permlane swaps)
+  if (grp == 0 && m < M) ss[(size_t)m * ss_ld + j] = sq;
+}
+
+void ss_partials_raw(const half_t* C, int ldc, int M, int N, float* ss, int ss_ld, hipStream_t s) {
+  if (!ss || M <= 0) return;
+  const int waves = ((M + 15) / 16) * (N / 128);
+  hipLaunchKernelGGL(ss_partials_kernel, dim3((waves + 3) / 4), dim3(256), 0, s, C, ldc, M, N / 128, ss, ss_ld);
 }
 
 void ss_partials(const half_t* C, int ldc, int M, int N, const Epi& ep, hipStream_t s) {
-  if (!ep.ss || M <= 0) return;
-  const int waves = M * (N / 128);
-  hipLaunchKernelGGL(ss_partials_kernel, dim3((waves + 3) / 4), dim3(256), 0, s, C, ldc, M, N / 128, ep.ss, ep.ss_ld);
+  ss_partials_raw(C, ldc, M, N, ep.ss, ep.ss_ld, s);
 }
 
 // -> slices per tile (0: split-K not applicable / no room in the workspace)
@@ -431,14 +440,6 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
                         ldw % 8 == 0 && (size_t)M * lda * 2 < (1ull << 32) && ldc % 4 == 0 &&
                         ((uintptr_t)C & 7) == 0 && ((uintptr_t)ws & 15) == 0 &&
                         (EPI != FLS_EPI_RESID || (ep.ldr % 4 == 0 && ((uintptr_t)ep.R & 7) == 0));
-  // row-exact generation steps (and, with fls_gemm_set_panel(2), any small M): ALL rows x 32 columns
-  // per block, one accumulator chain over K (gemm_panel.h)
-  if (try_panel<EPI>(A, W, C, M, N, K, lda, ldw, ldc, ep, s)) {
-    FLS_CHECK_LAUNCH();
-    ss_partials(C, ldc, M, N, ep, s);
-    FLS_CHECK_LAUNCH();
-    return 0;
-  }
   if (!ep.row_exact) {
     const int rc = try_skinny<EPI>(A, W, C, M, N, K, lda, ldw, ldc, ep, s, ws, ws_bytes);
     if (rc > 0) ss_partials(C, ldc, M, N, ep, s);
@@ -529,7 +530,7 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
 
 }  // namespace
 
-extern "C" int fls_kernels_version(void) { return 30; }
+extern "C" int fls_kernels_version(void) { return 31; }
 
 // tile order: 0 = by shape (default); g > 0: groups of g M tiles; g < 0: groups of -g N tiles (A/B, tests)
 extern "C" int fls_gemm_set_order(int order) {
@@ -568,11 +569,14 @@ extern "C" int fls_gemm_set_row_chunk(int rows) {
   return old;
 }
 
-// panel kernel (gemm_panel.h): 0 off, 1 row-exact calls (default), 2 every M <= 320 it takes; returns the previous
-extern "C" int fls_gemm_set_panel(int mode) {
-  const int old = g_panel;
-  g_panel = mode < 0 ? 0 : mode > 2 ? 2 : mode;
-  return old;
+// per-row partial sums of squares of an fp16 [rows, H] matrix, one fp32 per 128 columns (H % 128 == 0):
+// the residual GEMM epilogue's partials, bitwise, for a hidden state that arrived without them
+extern "C" int fls_row_ss(const void* x, int ldx, int rows, int H, float* ss, int ss_ld, fls_stream_t s) {
+  if (rows <= 0) return 0;
+  if (H % 128 || ldx % 4 || ((uintptr_t)x & 7) || ss_ld < H / 128) return -2;
+  ss_partials_raw((const half_t*)x, ldx, rows, H, ss, ss_ld, (hipStream_t)s);
+  FLS_CHECK_LAUNCH();
+  return 0;
 }
 
 // mid-M block columns: 0 auto (default), 64 or 128 forced where valid (tests / A-B); returns the previous

@@ -69,6 +69,20 @@ __device__ __forceinline__ float row_sum_4groups(float v) {
   return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
+// one lane's share of a row's partial sum of squares over a pair of 16-column subtiles (its 4 columns
+// of each), in one fixed order of explicit FMAs: the v10 / v11 residual epilogue and ss_partials_kernel
+// (every other GEMM path, and the fused norm's statistic of a hidden state no residual GEMM left
+// partials for) run this same code on the same lane layout, so their partials are bitwise equal
+__device__ __forceinline__ float ss_accum_pair(float sq, const half4& oa, const half4& ob) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float a = (float)oa[r], b = (float)ob[r];
+    sq = __builtin_fmaf(a, a, sq);
+    sq = __builtin_fmaf(b, b, sq);
+  }
+  return sq;
+}
+
 // the per-row scale of row m (1 without one: x * 1.0f is exact, so the unscaled path is unchanged)
 __device__ __forceinline__ float row_scale(const Epi& ep, int m) { return ep.rs ? ep.rs[m] : 1.f; }
 
@@ -357,10 +371,7 @@ __device__ __forceinline__ void epilogue_quadrant(half_t* __restrict__ C, int ld
 #pragma unroll
             for (int r = 0; r < 4; ++r) { oa[r] = (half_t)a[r]; ob[r] = (half_t)b[r]; }
             if constexpr (EPI == FLS_EPI_RESID) {
-              if (ssp) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) sq += (float)oa[r] * (float)oa[r] + (float)ob[r] * (float)ob[r];
-              }
+              if (ssp) sq = ss_accum_pair(sq, oa, ob);
             }
             const uint4 v = wide_pair(oa, ob);
             if (m < M && (!LO || m >= mlo)) *(uint4*)(C + (size_t)m * ldc + ncol0 + p * 32 + woff) = v;

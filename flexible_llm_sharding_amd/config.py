@@ -197,7 +197,14 @@ class ModelConfig:
                 raise NotImplementedError("partial_rotary_factor < 1 (RoPE on part of each head) is not supported")
         mt = d.get("model_type", "llama")
         if mt not in SUPPORTED_MODEL_TYPES:
-            raise NotImplementedError(f"model_type={mt!r}: supported are {sorted(SUPPORTED_MODEL_TYPES)}")
+            why = llama_like_rejection(d)
+            if why:
+                raise NotImplementedError(f"model_type={mt!r}: supported are {sorted(SUPPORTED_MODEL_TYPES)}, or a "
+                                          f"Llama-structured config ({why})")
+            # an unlisted family with the Llama block: run as Llama; every layer file must then hold
+            # exactly the Llama tensors (models/layout.py check_layer_tensors), so a different block
+            # structure fails at load instead of running wrong
+            kw["model_type"] = mt
         if mt in ("qwen3_moe", "qwen2_moe"):
             kw["num_local_experts"] = int(d.get("num_experts") or d.get("num_local_experts") or 0)
             if mt == "qwen3_moe" and d.get("shared_expert_intermediate_size"):
@@ -262,6 +269,32 @@ class ModelConfig:
 # path (utils.py:101-115) runs in practice.
 SUPPORTED_MODEL_TYPES = {"llama", "mistral", "qwen2", "qwen3", "phi3", "mixtral", "qwen3_moe", "qwen2_moe",
                          "granite"}
+
+# config keys of other families whose block differs from Llama's while its tensors may look the same
+# (MiniCPM's embedding / depth scales, Gemma-2's soft-capping, DeepSeek's latent attention, Cohere's
+# logit scale, parallel attention + MLP blocks, experts under other names)
+_NON_LLAMA_KEYS = ("scale_emb", "scale_depth", "dim_model_base", "attn_logit_softcapping",
+                   "final_logit_softcapping", "query_pre_attn_scalar", "kv_lora_rank", "q_lora_rank",
+                   "logit_scale", "use_parallel_residual", "parallel_attn", "parallel_block", "n_routed_experts",
+                   "num_experts", "num_local_experts", "moe_intermediate_size", "use_qk_norm", "qk_layernorm",
+                   "layer_norm_eps", "norm_epsilon", "embedding_multiplier", "residual_multiplier")
+
+
+def llama_like_rejection(d: dict) -> str:
+    """'' when an unlisted model_type's config.json describes the Llama block (the fields Llama reads,
+    SwiGLU, RMSNorm, full RoPE, none of the keys that change the block), else the reason not."""
+    need = ("hidden_size", "intermediate_size", "num_attention_heads", "num_hidden_layers", "vocab_size",
+            "rms_norm_eps")
+    missing = [k for k in need if k not in d]
+    if missing:
+        return f"missing {', '.join(missing)}"
+    # (1 / 0 / false are the neutral values: this framework's own config.json lists every field)
+    extra = [k for k in _NON_LLAMA_KEYS if d.get(k) not in (None, False, 0, 1)]
+    if extra:
+        return f"{', '.join(extra)} change the block"
+    if d.get("hidden_act", "silu") != "silu":
+        return f"hidden_act={d.get('hidden_act')!r}"
+    return ""
 # MoE limits of the routing kernels (csrc/kernels/moe.hip): experts per layer, experts per token
 MAX_EXPERTS = 256
 MAX_TOP_K = 8

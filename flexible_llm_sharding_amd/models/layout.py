@@ -267,6 +267,20 @@ def source_key(cfg: ModelConfig, layer_name: str, hf_name: str, available) -> st
     raise KeyError(f"{layer_name}: missing tensor {hf_name}")
 
 
+def check_layer_tensors(cfg: ModelConfig, layer_name: str, available) -> None:
+    """A config of an unlisted family runs as Llama (config.llama_like_rejection): its layer files
+    must hold exactly the tensors a Llama layer reads — an extra one (a q/k norm, a post-MLP norm, a
+    bias) means a different block, which is refused rather than run without it."""
+    from ..config import SUPPORTED_MODEL_TYPES
+    if cfg.model_type in SUPPORTED_MODEL_TYPES:
+        return
+    want = {pl.hf_name for pl in placements(cfg, layer_name)}
+    extra = sorted(k for k in available if k not in want and not k.endswith("rotary_emb.inv_freq"))
+    if extra:
+        raise NotImplementedError(f"model_type={cfg.model_type!r} runs as Llama, but {layer_name} holds tensors a "
+                                  f"Llama layer does not have: {extra[:4]}")
+
+
 # ------------------------------------------------------------------- packing
 def hf_param_names(cfg: ModelConfig, layer_name: str) -> List[str]:
     return [pl.hf_name for pl in placements(cfg, layer_name)]
@@ -286,6 +300,7 @@ def pack_layer(cfg: ModelConfig, layer_name: str, sd: Dict[str, torch.Tensor],
     for v in sd.values():
         if v.dtype == torch.int8:
             raise AssertionError("int8 not supported (need to add fp16_statistics)")
+    check_layer_tensors(cfg, layer_name, sd)
     if out is None:
         out = torch.zeros(lay.nbytes, dtype=torch.uint8)
     b = out.view(torch.uint8)

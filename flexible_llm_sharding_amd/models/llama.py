@@ -190,9 +190,10 @@ class ExecContext:
     # ss_key names what ss_buf holds: (id(batch), decoder index, "attn" | "mlp", rows) -- valid for
     # the projection right after that residual GEMM on this rank (any state parked and reloaded in
     # between keeps its values); anything else (another micro-batch, the first layer, a grouped
-    # attention phase, MoE) misses and computes row_rstd.  Reset at every call's embedding.
-    # generation tie guard (engine): every row's arithmetic independent of the other rows of the call
-    # (row-exact GEMM paths, the row statistic always from the row itself)
+    # attention phase, MoE) misses and computes the same partials from the hidden state (row_stat:
+    # bitwise the epilogue's).  Reset at every call's embedding.
+    # generation with the K/V caches (engine "exact K/V reuse"): every row's arithmetic independent
+    # of the other rows of the call (row-exact GEMM paths, the row statistic from the row itself)
     row_exact: bool = False
     ss_buf: Optional[torch.Tensor] = None      # the arena-backed buffer (grown, reused)
     ss_cur: Optional[torch.Tensor] = None      # the buffer the last residual GEMM wrote
@@ -233,11 +234,22 @@ class ExecContext:
 
     def rstd(self, x: torch.Tensor, key: Optional[tuple], out=None, rows: Optional[slice] = None) -> torch.Tensor:
         """Row statistic rsqrt(mean(x^2) + eps) of x: from the partial sums the residual GEMM named
-        ``key`` left (rows ``rows`` of them) when they are there, else a pass over x."""
+        ``key`` left (rows ``rows`` of them) when they are there, else from a pass over x."""
         eps = self.cfg.rms_norm_eps
         if key is not None and self.ss_key == key and self.ss_cur is not None:
             ss = self.ss_cur[:key[3]]
             return self.ops.rstd_from_ss(ss[rows] if rows is not None else ss, self.cfg.hidden_size, eps, out=out)
+        return self.row_stat(x, out=out)
+
+    def row_stat(self, x: torch.Tensor, out=None) -> torch.Tensor:
+        """The statistic from a pass over x.  With 128-column partials it is computed exactly as the
+        residual GEMM epilogue's partials + rstd_from_ss would give it, so a row's statistic (and the
+        scores) do not depend on whether its partials survived: a state received from another
+        pipeline rank, parked in host memory, after grouped attention or in the pruned last layer
+        gets the same bits as one straight from the residual GEMM."""
+        H, eps = self.cfg.hidden_size, self.cfg.rms_norm_eps
+        if H % 128 == 0 and hasattr(self.ops, "row_ss"):
+            return self.ops.rstd_from_ss(self.ops.row_ss(x), H, eps, out=out)
         return self.ops.row_rstd(x, eps, out=out)
 
 
@@ -318,7 +330,7 @@ def _scored_q(ctx: ExecContext, W: Dict[str, torch.Tensor], x: torch.Tensor, las
     bq = b[:qs] if b is not None else None
     xq = ops.gather_rows(x, last_idx)
     if ctx.fused_norm:
-        return _proj(ctx, W, xq, w[:qs], last_pos, cfg.num_attention_heads, 0, bq, rscale=ops.row_rstd(xq, eps))
+        return _proj(ctx, W, xq, w[:qs], last_pos, cfg.num_attention_heads, 0, bq, rscale=ctx.row_stat(xq))
     return _proj(ctx, W, ops.rmsnorm(xq, W["ln1"], eps), w[:qs], last_pos, cfg.num_attention_heads, 0, bq)
 
 

@@ -206,6 +206,16 @@ class HipOps:
         """silu(x @ gate^T) * (x @ up^T) with wgu = [gate; up]."""
         return self.gemm(x, wgu, EPI_SWIGLU, out=out, rscale=rscale)
 
+    def row_ss(self, x, out=None):
+        """[rows, H/128] fp32 partial sums of squares of x's rows (H % 128 == 0), bitwise the ones a
+        residual GEMM epilogue writes for the same fp16 values (:meth:`linear_residual` ``ss``)."""
+        _f16(x, "x")
+        rows, H = x.shape
+        ss = out if out is not None else torch.empty(rows, H // 128, dtype=torch.float32, device=x.device)
+        _chk(self.k.fls_row_ss(x.data_ptr(), x.stride(0), rows, H, ss.data_ptr(), ss.stride(0), _stream()),
+             "fls_row_ss")
+        return ss
+
     def row_rstd(self, x, eps, row_idx=None, out=None):
         """[rows] fp32 rsqrt(mean(x[row]^2) + eps) (rows = row_idx or every row of x)."""
         _f16(x, "x")

@@ -38,7 +38,7 @@ import torch
 
 from .. import _native, knobs
 from ..config import ModelConfig
-from ..models.layout import layer_kind, layer_layout, placements, source_key
+from ..models.layout import check_layer_tensors, layer_kind, layer_layout, placements, source_key
 from ..utils.layer_format import layer_file
 from ..utils.safetensors_io import TensorInfo, read_header
 from . import hostmem
@@ -72,6 +72,7 @@ class LayerPlan:
         if infos is None:
             infos, _ = read_header(path)
         infos = _relabel_layer(infos, layer_name)
+        check_layer_tensors(cfg, layer_name, infos)
         runs = []
         for pl in placements(cfg, layer_name):
             key = source_key(cfg, layer_name, pl.hf_name, infos)

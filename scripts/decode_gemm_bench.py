@@ -1,5 +1,5 @@
-"""Generation-step GEMMs at the 70B shapes: the row-exact paths (panel kernel, csrc/kernels/gemm_panel.h;
-mid-M kernel) against the non-exact skinny / split-K paths.
+"""Generation-step GEMMs at the 70B shapes: the row-exact path (mid-M kernel, 64- or 128-column
+blocks) against the non-exact skinny / split-K paths.
 
     python scripts/decode_gemm_bench.py [--rows 64,160,320] [--iters 50]
 """
@@ -30,11 +30,9 @@ def main():
          "down": torch.randn(H, I, device=dev, generator=g).half() * 0.02}
     cos = torch.rand(8192, hd // 2, device=dev)
     sin = torch.rand(8192, hd // 2, device=dev)
-    # arm -> (row-exact, fls_gemm_set_panel, fls_gemm_set_mid): exact default (panel where it wins, else the
-    # mid-M kernel), exact on the mid kernel only, every M <= 320 on the panel kernel, the non-exact default
-    # (skinny / split-K); exact_mid128: the mid kernel with 128-column blocks only
-    arms = {"exact": (True, 1, 1), "exact_mid": (True, 0, 1), "exact_panel": (True, 2, 1), "fast": (False, 1, 1),
-            "exact_mid128": (True, 0, 1)}
+    # arm -> (row-exact, fls_gemm_set_mid_bn): exact default (mid-M kernel, 64-column blocks for grids of
+    # less than one round), exact with 128-column blocks only, the non-exact default (skinny / split-K)
+    arms = {"exact": (True, 0), "exact_mid128": (True, 128), "fast": (False, 0)}
     for M in [int(r) for r in a.rows.split(",")]:
         x = torch.randn(M, H, device=dev, generator=g).half()
         xi = torch.randn(M, I, device=dev, generator=g).half()
@@ -50,10 +48,8 @@ def main():
         }
         res = {"M": M}
         outs = {}
-        for arm, (exact, panel, mid) in arms.items():
-            old = ops.k.fls_gemm_set_panel(panel)
-            old_mid = ops.k.fls_gemm_set_mid(mid)
-            old_bn = ops.k.fls_gemm_set_mid_bn(128 if arm == "exact_mid128" else 0)
+        for arm, (exact, bn) in arms.items():
+            old_bn = ops.k.fls_gemm_set_mid_bn(bn)
             try:
                 with ops.row_exact(exact):
                     tot = 0.0
@@ -75,12 +71,8 @@ def main():
                             outs[arm] = f().clone()
                     res[f"{arm}.layer_us"] = round(tot, 1)
             finally:
-                ops.k.fls_gemm_set_panel(old)
-                ops.k.fls_gemm_set_mid(old_mid)
                 ops.k.fls_gemm_set_mid_bn(old_bn)
-        res["exact_arms_bitwise_equal"] = bool(torch.equal(outs["exact"], outs["exact_mid"])
-                                               and torch.equal(outs["exact"], outs["exact_panel"])
-                                               and torch.equal(outs["exact"], outs["exact_mid128"]))
+        res["exact_arms_bitwise_equal"] = bool(torch.equal(outs["exact"], outs["exact_mid128"]))
         print(json.dumps(res), flush=True)
 
 

@@ -388,6 +388,49 @@ def test_unsupported_configs_rejected():
         ModelConfig.from_dict({"rope_parameters": {"rope_type": "longrope", "rope_theta": 1e4}})
 
 
+def test_llama_structured_unlisted_family(tiny_model, tmp_path):
+    """An unlisted model_type whose config describes the Llama block runs as Llama (the reference's
+    AutoModelForCausalLM takes any such checkpoint, utils.py:109-115): same scores as the Llama run;
+    a layer file holding a tensor Llama does not read, or a config key that changes the block, is
+    refused instead of run wrong."""
+    import json
+    import shutil
+    from safetensors.torch import load_file, save_file
+    from flexible_llm_sharding_amd.config import ModelConfig, llama_like_rejection
+    from flexible_llm_sharding_amd.runtime.stream import FileLayerSource
+    from flexible_llm_sharding_amd.utils.layer_format import layer_file
+    path, cfg = tiny_model
+    d = str(tmp_path / "other")
+    shutil.copytree(path, d)
+    with open(os.path.join(d, "config.json")) as f:
+        conf = json.load(f)
+    conf["model_type"], conf["architectures"] = "llama_like_family", ["LlamaLikeForCausalLM"]
+    with open(os.path.join(d, "config.json"), "w") as f:
+        json.dump(conf, f)
+    other = ModelConfig.from_pretrained(d)
+    assert other.model_type == "llama_like_family"
+    tok = load_tokenizer(path)
+    prompts = synthetic_prompts(3, 30, 2, 6, cfg.vocab_size, seed=4)
+    want = ShardedRunner(cfg, FileLayerSource(cfg, path), "cpu", tok)(prompts)
+    for src in (FileLayerSource(other, d), HostStore.from_model_path(other, d, pinned=False)):
+        got = ShardedRunner(other, src, "cpu", tok)(prompts)
+        for a, b in zip(got, want):
+            assert np.array_equal(a, b)
+    # a tensor the Llama block does not have (e.g. a q norm) -> refused at load
+    lf = layer_file(d, "model.layers.0")
+    sd = load_file(lf)
+    sd["model.layers.0.self_attn.q_norm.weight"] = torch.ones(other.head_dim)
+    save_file(sd, lf)
+    with pytest.raises(NotImplementedError, match="does not have"):
+        ShardedRunner(other, FileLayerSource(other, d), "cpu", tok)(prompts)
+    with pytest.raises(NotImplementedError, match="does not have"):
+        HostStore.from_model_path(other, d, pinned=False)
+    assert "scale_emb" in llama_like_rejection(dict(conf, scale_emb=12))
+    assert "hidden_act" in llama_like_rejection(dict(conf, hidden_act="gelu"))
+    with pytest.raises(NotImplementedError):
+        ModelConfig.from_dict(dict(conf, kv_lora_rank=512))
+
+
 def test_sliding_window_must_cover_prompts(tmp_path):
     """Windowed attention is full attention while every sequence fits the window; longer prompts
     are rejected instead of silently attending past the window."""

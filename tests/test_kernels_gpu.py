@@ -404,11 +404,11 @@ def test_gemm_main_all_epilogues(ops, ref):
 
 
 @pytest.mark.parametrize("hd", [128, 64])
-def test_gemm_panel_rows_bitwise(ops, ref, hd):
-    """Row-exact small-M GEMMs take the panel kernel (all rows x 32 columns per block, one K chain):
-    every row of M = 1 / 17 / 64 / 160 / 320 equals, bit for bit, the same row of a 1,000-row row-exact
-    GEMM (mid tiles of 64 or 128 columns, bitwise equal), for all four epilogues incl. bias, per-row
-    scale and RoPE (both head sizes); and the fp32 reference."""
+def test_gemm_row_exact_small_m_bitwise(ops, ref, hd):
+    """Row-exact small-M GEMMs (generation steps): every row of M = 1 / 17 / 64 / 160 / 320 equals,
+    bit for bit, the same row of a 1,000-row row-exact GEMM, with the mid-M kernel's 64- and
+    128-column blocks (bitwise equal to each other), for all four epilogues incl. bias, per-row scale
+    and RoPE (both head sizes); and the fp32 reference."""
     from flexible_llm_sharding_amd.config import ModelConfig
     from flexible_llm_sharding_amd.models.llama import rope_tables
     Mb, H, I, nh, nkv = 1000, 1024, 1536, 8, 2
@@ -442,17 +442,37 @@ def test_gemm_panel_rows_bitwise(ops, ref, hd):
             finally:
                 ops.k.fls_gemm_set_mid_bn(old_bn)
         g = torch.Generator().manual_seed(5)
-        old = ops.k.fls_gemm_set_panel(2)        # the panel kernel at every M <= 320 (auto: M <= 64)
-        try:
-            for m in (1, 17, 64, 160, 320):
-                rows = torch.randperm(Mb, generator=g)[:m].to(DEV)
-                for a, b in zip(run(rows), full):
-                    assert torch.equal(a, b[rows]), m
-        finally:
-            ops.k.fls_gemm_set_panel(old)
+        for m in (1, 17, 64, 160, 320):
+            rows = torch.randperm(Mb, generator=g)[:m].to(DEV)
+            for bn in (64, 128):
+                old_bn = ops.k.fls_gemm_set_mid_bn(bn)
+                try:
+                    for a, b in zip(run(rows), full):
+                        assert torch.equal(a, b[rows]), (m, bn)
+                finally:
+                    ops.k.fls_gemm_set_mid_bn(old_bn)
     torch.cuda.synchronize()
     assert rel_err(full[0], x.float() @ wo.float().t()) < 2e-3
     assert rel_err(full[2].cpu(), ref.swiglu_up((x.float() * rs[:, None]).cpu(), wgu.float().cpu())) < 3e-3
+
+
+def test_row_ss_matches_residual_epilogue(ops):
+    """fls_row_ss on a hidden state == the partial sums of squares the residual GEMM epilogue wrote
+    for the same rows (v10 / v11 tiles and the mid-M kernel + ss_partials), bit for bit, and the
+    statistic from them equals the fp32 RMS to rounding: a row's norm statistic does not depend on
+    whether its partials survived (pipeline hand-off, grouped attention, pruned last layer)."""
+    H = 1024
+    for M in (5000, 300, 7):                  # main tiles / mid-M / mid-M (few rows)
+        a = rnd(M, 512, seed=71)
+        w = rnd(H, 512, scale=0.05, seed=72)
+        r = rnd(M, H, seed=73)
+        ss = torch.zeros(M, H // 128, dtype=torch.float32, device=DEV)
+        out = ops.linear_residual(a, w, r.clone(), ss=ss)
+        got = ops.row_ss(out)
+        torch.cuda.synchronize()
+        assert torch.equal(got, ss), M
+        want = (out.float() ** 2).reshape(M, H // 128, 128).sum(-1)
+        assert torch.allclose(got, want, rtol=1e-4, atol=1e-3)
 
 
 @pytest.mark.parametrize("order", [8, -4, -8, 1, -1, 2, 3, -5])
