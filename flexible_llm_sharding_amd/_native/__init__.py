@@ -13,6 +13,7 @@ import threading
 HERE = os.path.dirname(os.path.abspath(__file__))
 _KERNELS = os.path.join(HERE, "libfls_kernels.so")
 _RUNTIME = os.path.join(HERE, "libfls_runtime.so")
+_COMM = os.path.join(HERE, "libfls_comm.so")
 
 _lock = threading.Lock()
 _libs = {}
@@ -125,6 +126,18 @@ def _load_kernels(path: str = _KERNELS):
     return lib
 
 
+def _load_comm():
+    lib = ctypes.CDLL(_COMM)
+    _bind(lib, "fls_rccl_version", c_int)
+    _bind(lib, "fls_rccl_id_bytes", c_int)
+    _bind(lib, "fls_rccl_unique_id", c_int, c_void_p)
+    _bind(lib, "fls_rccl_init", c_void_p, c_int, c_int, c_void_p, c_int)
+    _bind(lib, "fls_rccl_all_gather", c_int, c_void_p, c_void_p, c_void_p, c_uint64, c_void_p)
+    _bind(lib, "fls_rccl_all_reduce_f32", c_int, c_void_p, c_void_p, c_uint64, c_int, c_void_p)
+    _bind(lib, "fls_rccl_destroy", c_int, c_void_p)
+    return lib
+
+
 def _get(key, path, loader, required):
     with _lock:
         if key in _libs:
@@ -145,6 +158,11 @@ def kernels():
 
 def runtime():
     return _get("r", _RUNTIME, _load_runtime, True)
+
+
+def comm():
+    """The native RCCL communicator library (csrc/comm/rccl_comm.cpp)."""
+    return _get("c", _COMM, _load_comm, True)
 
 
 def runtime_or_none():

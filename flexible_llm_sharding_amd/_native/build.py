@@ -28,6 +28,7 @@ ARCH = os.environ.get("FLS_OFFLOAD_ARCH", "gfx950")   # knobs.py (not imported: 
 
 KERNELS_SO = os.path.join(HERE, "libfls_kernels.so")
 RUNTIME_SO = os.path.join(HERE, "libfls_runtime.so")
+COMM_SO = os.path.join(HERE, "libfls_comm.so")
 
 
 def _hipcc() -> str:
@@ -100,10 +101,25 @@ def build_runtime(force=False, verbose=False, sanitize=False):
     return out
 
 
+def build_comm(force=False, verbose=False):
+    """libfls_comm.so: the native RCCL communicator (csrc/comm), host code linked to librccl."""
+    srcs = sorted(glob.glob(os.path.join(CSRC, "comm", "*.cpp")))
+    if not (force or _stale(COMM_SO, srcs + _headers())):
+        return COMM_SO
+    cxx = shutil.which("g++") or "g++"
+    cmd = [cxx, "-O2", "-g", "-fPIC", "-shared", "-std=c++17", "-D__HIP_PLATFORM_AMD__",
+           "-I", os.path.join(CSRC, "include"), "-I", os.path.join(ROCM, "include")]
+    cmd += srcs + ["-L", os.path.join(ROCM, "lib"), "-Wl,-rpath," + os.path.join(ROCM, "lib"),
+                   "-lrccl", "-lamdhip64", "-o", COMM_SO]
+    _run(cmd, verbose)
+    return COMM_SO
+
+
 def build_all(force=False, jobs=8, verbose=False):
     rt = build_runtime(force=force, verbose=verbose)
     k = build_kernels(force=force, jobs=jobs, verbose=verbose)
-    return rt, k
+    c = build_comm(force=force, verbose=verbose)
+    return rt, k, c
 
 
 def main(argv=None):

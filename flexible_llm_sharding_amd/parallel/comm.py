@@ -31,6 +31,9 @@ class Comm:
         self.device = torch.device(device) if device is not None else torch.device("cpu")
         self.backend = backend
         self.group = group          # None: the default process group
+        # data-parallel weight gathers on the native RCCL communicator (--dp_gather_comm native):
+        # dup() then builds a parallel/native_comm.NativeRcclComm
+        self.gather_native = False
 
     @property
     def active(self) -> bool:
@@ -65,6 +68,9 @@ class Comm:
         The data-parallel weight all-gathers run on their own communicator, issued by the
         loader thread, so they never interleave with the main thread's collectives on the
         default group (each communicator sees the same op sequence on every rank)."""
+        if self.gather_native and self.device.type == "cuda":
+            from .native_comm import NativeRcclComm
+            return NativeRcclComm(self)
         if not self.active:
             return Comm(self.rank, self.world, self.device, self.backend)
         return Comm(self.rank, self.world, self.device, self.backend,

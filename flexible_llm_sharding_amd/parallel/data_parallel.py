@@ -335,6 +335,8 @@ def build_dp_sharded_runner(args, cfg, device, comm: Comm, tok, store: Optional[
     names = cfg.layer_names()
     plan = make_plan(len(names), args.layer_num_per_shard, comm.world, comm.rank, True)
     shards = [s for s in plan.my_shards if len(s)]
+    # the prefetcher's gather communicator (its comm.dup()): torch.distributed, or the native RCCL one
+    comm.gather_native = getattr(args, "dp_gather_comm", "torch") == "native"
     if (getattr(args, "max_vram_gb", None) and args.layer_num_per_shard == 1 and device.type == "cuda"
             and not getattr(args, "resident", False) and isinstance(store, SlicedHostStore)):
         pf = AllGatherPiecePool(store, names, shards, device, comm)   # sub-layer pieces under a cap

@@ -89,6 +89,9 @@ def build_parser() -> argparse.ArgumentParser:
                    help="host RAM budget for --weight_cache auto / host (default: 80%% of MemAvailable)")
     p.add_argument("--o_direct", type=str2bool, nargs="?", const=True, default=False,
                    help="stream layer files with O_DIRECT (bypass the page cache)")
+    p.add_argument("--dp_gather_comm", choices=["torch", "native"], default="torch",
+                   help="data parallel: the weight all-gathers on a torch.distributed group (default) or on the "
+                        "native RCCL communicator (csrc/comm/rccl_comm.cpp), issued from C on the copy stream")
     p.add_argument("--dp_weight_shard", type=str2bool, nargs="?", const=True, default=True,
                    help="data parallel: scatter-load 1/G of each layer per GPU + RCCL all-gather")
     p.add_argument("--rx_window", type=int, default=2,

@@ -342,11 +342,12 @@ def _main_cli(tmp, ck, n_gpus, extra):
 
 
 @multi
-@pytest.mark.parametrize("extra", [[], ["--data_parallel", "True"], ["--data_parallel", "True", "--max_vram_gb", "2.4"]])
+@pytest.mark.parametrize("extra", [[], ["--data_parallel", "True"], ["--data_parallel", "True", "--max_vram_gb", "2.4"],
+                                   ["--data_parallel", "True", "--dp_gather_comm", "native"]])
 def test_main_cli_two_gpus_matches_one(one_gpu_ref, extra):
     """``main.py --num_gpus 2`` end to end (spawned ranks, RCCL hand-offs or all-gathers, rank-0
     score gather, output pickles): model parallel (default) and data parallel (capped too) equal
-    the one-GPU CLI run."""
+    the one-GPU CLI run; data parallel with its weight gathers on the native RCCL communicator too."""
     d, _ = one_gpu_ref
     ck = os.path.join(d, "ckpt")
     from flexible_llm_sharding_amd.config import preset
@@ -354,7 +355,7 @@ def test_main_cli_two_gpus_matches_one(one_gpu_ref, extra):
     prompts = synthetic_prompts(5, 300, 4, 12, cfg.vocab_size, seed=4)
     with open(os.path.join(d, "prompts.pkl"), "wb") as f:
         pickle.dump(prompts, f)
-    one = _main_cli(d, ck, 1, [x for x in extra if x != "True" and x != "--data_parallel"])
+    one = _main_cli(d, ck, 1, [x for x in extra if x not in ("True", "--data_parallel", "--dp_gather_comm", "native")])
     two = _main_cli(d, ck, 2, extra)
     assert len(one) == len(two) == len(prompts)
     for a, b in zip(one, two):
@@ -372,3 +373,27 @@ def test_bench_two_ranks_over_rccl(tmp_path):
     rec = json.load(open(out))
     assert rec["process_group_ranks"] == 2 and rec["backend"] == "nccl" and rec["n_gpus"] == 2
     assert rec["scores_finite"] and rec["value"] > 0
+
+
+def test_native_rccl_communicator_one_rank():
+    """The native RCCL communicator (csrc/comm/rccl_comm.cpp, --dp_gather_comm native) on one rank:
+    it initialises, runs the in-place byte all-gather the weight fan-out issues on the copy stream
+    (this rank's slice already in place: out unchanged), a second gather into a separate buffer, and
+    tears down.  Multi-rank RCCL needs several GPUs (the driver's node)."""
+    from flexible_llm_sharding_amd.parallel.comm import Comm
+    from flexible_llm_sharding_amd.parallel.native_comm import NativeRcclComm
+    base = Comm(0, 1, torch.device("cuda", 0))
+    base.gather_native = True
+    c = base.dup()
+    assert isinstance(c, NativeRcclComm)
+    c.warmup()
+    out = torch.arange(4096, dtype=torch.int32, device="cuda:0").view(torch.uint8)
+    want = out.clone()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        c.all_gather_into(out, out[:out.numel()]).wait()
+        dst = torch.zeros_like(out)
+        c.all_gather_into(dst, out).wait()
+    s.synchronize()
+    assert torch.equal(out, want) and torch.equal(dst, want)
+    c.destroy()
