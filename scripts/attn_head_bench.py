@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--prefix", type=int, default=1024)
     ap.add_argument("--prompts", type=int, default=32)
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--sweep", action="store_true",
+                    help="also the persistent kernel's heads-per-block (4 / 2 / 1) and 128-row items (4 waves per head)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     ops = HipOps()
@@ -49,6 +51,24 @@ def main():
                           "items": int(b.work.shape[0]), "us": round(best[pers] * 1e6, 1),
                           "tflops": round(fl / best[pers] / 1e12, 1)}), flush=True)
     print(json.dumps({"bitwise_equal": bool(torch.equal(outs[0], outs[1]))}), flush=True)
+    if not a.sweep:
+        return
+    for qb in (64, 128):
+        bq = pack_prompts(tps, list(range(a.prompts)), "bidirectional", q_block=qb)
+        mq = bq.device_tensors(dev)
+        for hpb in (4, 2, 1):
+            if qb == 128 and hpb == 4:
+                continue                      # (4 waves per head x 4 heads: beyond 8 waves per block)
+            old = ops.k.fls_attention_set_hpb(hpb)
+            try:
+                out = torch.empty(bq.num_tokens, nh * hd, device=dev).half()
+                t = min(timeit(lambda: ops.attention(qkv, mq["work"], nh, nkv, hd, q_block=qb, out=out,
+                                                     seg_lo=mq["seg_lo"]), a.iters) for _ in range(a.rounds))
+            finally:
+                ops.k.fls_attention_set_hpb(old)
+            print(json.dumps({"kernel": "persistent", "q_block": qb, "hpb": hpb, "us": round(t * 1e6, 1),
+                              "tflops": round(fl / t / 1e12, 1),
+                              "bitwise_equal_default": bool(torch.equal(out, outs[1]))}), flush=True)
 
 
 if __name__ == "__main__":
