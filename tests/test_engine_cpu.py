@@ -550,6 +550,33 @@ def test_prefix_kv_cache_generation_exact(tiny_model, num_batch_calls, host):
             assert cached.stats["suffix_tokens_reused"] > 0
 
 
+def test_host_mode_cache_grows_and_evicts(tiny_model):
+    """Host-mode prefix K/V cache (--max_vram_gb): a larger call grows the staging buffer, LRU
+    eviction drops entries (and their write-back events), and every call's scores stay those of a
+    runner without a cache; repeated calls hit."""
+    from flexible_llm_sharding_amd.engine import ShardedRunner
+    from flexible_llm_sharding_amd.runtime.weights import HostStore
+    path, cfg = tiny_model
+    tok = load_tokenizer(path)
+    src = HostStore.from_model_path(cfg, path, pinned=False)
+    r = _host_mode(ShardedRunner(cfg, src, "cpu", tok, prefix_kv_cache=True, suffix_kv_cache=True,
+                                 prefix_cache_entries=2))
+    ref = ShardedRunner(cfg, src, "cpu", tok)
+    small = synthetic_prompts(2, 20, 2, 4, cfg.vocab_size, seed=5)
+    big = synthetic_prompts(4, 60, 3, 8, cfg.vocab_size, seed=6)
+    other = synthetic_prompts(3, 30, 2, 5, cfg.vocab_size, seed=7)
+    sizes = []
+    for ps in (small, big, small, other, big, big):
+        for a, b in zip(r(ps), ref(ps)):
+            assert np.abs(a.astype(np.float32) - b.astype(np.float32)).max() < 1e-5
+        sizes.append(r.prefix_cache.stage.bufs[0].shape[0])
+    pc = r.prefix_cache
+    assert sizes[1] > sizes[0] and sizes == sorted(sizes)          # grown, never shrunk
+    assert len(pc.entries) <= 2 and pc.hits >= 2
+    live = {id(t) for e in pc.entries.values() for t in e.layers.values()}
+    assert all(k[0] in live for k in pc.stage.layer_ev)            # no events of evicted entries
+
+
 def test_prefix_cache_invalidated_by_new_prefix(tiny_model):
     from flexible_llm_sharding_amd.engine import ShardedRunner
     from flexible_llm_sharding_amd.runtime.weights import HostStore
