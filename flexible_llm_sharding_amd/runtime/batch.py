@@ -230,12 +230,14 @@ def pack_prompts(tps: Sequence[TokenizedPrompt], prompt_ids: Sequence[int],
     if kv_cached and prefix_offsets is None:
         raise ValueError("kv_cached needs prefix_offsets")
     pcausal = 1 if prefix_attention == "causal" else 0
-    ids, pos, segs, last, nsuf, lsegs = [], [], [], [], [], []
+    # per-row arrays are gathered as numpy parts (one per prefix / suffix) and concatenated once:
+    # Python lists of 43k ints cost the host ~10 ms per call (the GPU idles at the call boundary)
+    ids, pos, seg_lo, segs, last, nsuf, lsegs = [], [], [], [], [], [], []
     if suffix_keep is not None and not kv_cached:
         raise ValueError("suffix K/V reuse needs the prefix K/V cache (kv_cached)")
     if suffix_keep is not None and any(r < 0 for rows in suffix_rows for r in rows):
         raise ValueError("suffix K/V reuse needs a cache region for every suffix")
-    seg_lo, work, work2, r2win, lwork, lwork2 = [], [], [], [], [], []
+    work, work2, r2win, lwork, lwork2 = [], [], [], [], []
     src, dst, sfx_src, sfx_dst = [], [], [], []
     p_rows, p_items, p_scored = [], [], []
     t = 0
@@ -248,27 +250,28 @@ def pack_prompts(tps: Sequence[TokenizedPrompt], prompt_ids: Sequence[int],
             p0 = prefix_offsets[j]
         else:
             p0 = t
-            ids.extend(tp.prefix)
-            pos.extend(range(Lp))
+            ids.append(np.asarray(tp.prefix, dtype=np.int32))
+            pos.append(np.arange(Lp, dtype=np.int32))
             segs.append(Segment(p0, Lp, p0, Lp, pcausal, 0, 0))
-            seg_lo.extend([p0] * Lp)
+            seg_lo.append(np.full(Lp, p0, dtype=np.int32))
             work.extend(_items(segs[-1], q_block))
             work2.extend([(0, 0)] * (len(work) - len(work2)))
-            r2win.extend([(0, 0)] * Lp)
             if prefix_offsets is not None:
-                src.extend(range(t, t + Lp))
-                dst.extend(range(prefix_offsets[j], prefix_offsets[j] + Lp))
+                src.append(np.arange(t, t + Lp, dtype=np.int32))
+                dst.append(np.arange(prefix_offsets[j], prefix_offsets[j] + Lp, dtype=np.int32))
             t += Lp
         sfx0 = t
+        sfx_lo = []                    # seg_lo of this prompt's suffix rows (row - sfx0)
         keep = suffix_keep[j] if suffix_keep is not None else None
         for si, s in enumerate(tp.suffixes):
             c = keep[si] if keep is not None else 0
             c0_row = suffix_rows[j][si] if suffix_rows is not None else -1
             n = len(s) - c
             s0 = t
-            ids.extend(s[c:])
-            pos.extend(range(Lp + c, Lp + c + n))
-            seg_lo.extend([s0] * n)
+            ids.append(np.asarray(s[c:], dtype=np.int32))
+            pos.append(np.arange(Lp + c, Lp + c + n, dtype=np.int32))
+            seg_lo.append(np.full(n, s0, dtype=np.int32))
+            sfx_lo.extend([s0] * n)
             r2s, r2l = (c0_row, c) if c else (0, 0)
             segs.append(Segment(s0, n, p0, Lp, 0, s0, n, r2_start=r2s, r2_len=r2l))
             last.append(s0 + n - 1)
@@ -279,15 +282,14 @@ def pack_prompts(tps: Sequence[TokenizedPrompt], prompt_ids: Sequence[int],
                 lwork.append((s0 + n - 1, 1, 0, p0, Lp, 0, 0, 0))
                 lwork2.append((c0_row, c + n))
             if c0_row >= 0:
-                sfx_src.extend(range(s0, s0 + n))
-                sfx_dst.extend(range(c0_row + c, c0_row + c + n))
+                sfx_src.append(np.arange(s0, s0 + n, dtype=np.int32))
+                sfx_dst.append(np.arange(c0_row + c, c0_row + c + n, dtype=np.int32))
             if keep is not None:
                 # the new rows' K/V are captured into the cache before the attention runs, right
                 # after the kept ones: new row i sees cache rows [c0_row, c0_row + c + i] (its own
-                # key included: causal by window), so the kernel needs no range 1 at all
+                # key included: causal by window), so the kernel needs no range 1 at all.  (With
+                # keep every packed row is a suffix row: the prefixes come from the cache.)
                 r2win.extend([(c0_row, c0_row + c + i + 1) for i in range(n)])
-            else:
-                r2win.extend([(0, 0)] * n)
             t += n
         # the prompt's suffix rows [sfx0, t) in q_block chunks; range 1 of a chunk starts at the
         # suffix holding its first row.  Suffix K/V reuse: range 2 of every chunk spans the kept
@@ -303,7 +305,7 @@ def pack_prompts(tps: Sequence[TokenizedPrompt], prompt_ids: Sequence[int],
                 work.append((c0, c1 - c0, 0, p0, Lp, 0, 0, 0))
                 work2.append((lo, hi - lo))
             else:
-                r1 = seg_lo[c0]
+                r1 = sfx_lo[c0 - sfx0]
                 work.append((c0, c1 - c0, c0 - r1, p0, Lp, 0, r1, c1 - r1))
                 work2.append((0, 0))
         max_pos = max(max_pos, Lp + max([len(s) for s in tp.suffixes] or [0]))
@@ -314,24 +316,27 @@ def pack_prompts(tps: Sequence[TokenizedPrompt], prompt_ids: Sequence[int],
         padded += tp.padded_tokens
     work = np.asarray(work, dtype=np.int32).reshape(-1, WORK_ITEM_FIELDS)
     reuse = suffix_keep is not None
+
+    def cat(parts):
+        return np.concatenate(parts) if parts else np.zeros(0, dtype=np.int32)
     return PackedBatch(
         prompt_ids=list(prompt_ids), n_suffix=nsuf,
-        ids=np.asarray(ids, dtype=np.int32), positions=np.asarray(pos, dtype=np.int32),
-        segments=segs, work=work, seg_lo=np.asarray(seg_lo, dtype=np.int32),
+        ids=cat(ids), positions=cat(pos),
+        segments=segs, work=work, seg_lo=cat(seg_lo),
         last_idx=np.asarray(last, dtype=np.int32), last_segments=lsegs,
         work_last=(np.asarray(lwork, dtype=np.int32).reshape(-1, WORK_ITEM_FIELDS) if reuse
                    else _work_items(lsegs)), num_tokens=t, padded_tokens=padded,
         max_pos=max_pos, kv_cached=kv_cached, q_block=q_block,
-        pfx_src=np.asarray(src, dtype=np.int32) if (prefix_offsets is not None and not kv_cached) else None,
-        pfx_dst=np.asarray(dst, dtype=np.int32) if (prefix_offsets is not None and not kv_cached) else None,
+        pfx_src=cat(src) if (prefix_offsets is not None and not kv_cached) else None,
+        pfx_dst=cat(dst) if (prefix_offsets is not None and not kv_cached) else None,
         prompt_rows=np.asarray(p_rows, dtype=np.int64).reshape(-1, 2),
         prompt_items=np.asarray(p_items, dtype=np.int64).reshape(-1, 2),
         prompt_scored=np.asarray(p_scored, dtype=np.int64).reshape(-1, 2),
         work2=np.asarray(work2, dtype=np.int32).reshape(-1, 2) if reuse else None,
         r2win=np.asarray(r2win, dtype=np.int32).reshape(-1, 2) if reuse else None,
         work2_last=np.asarray(lwork2, dtype=np.int32).reshape(-1, 2) if reuse else None,
-        sfx_src=np.asarray(sfx_src, dtype=np.int32) if sfx_src else None,
-        sfx_dst=np.asarray(sfx_dst, dtype=np.int32) if sfx_dst else None)
+        sfx_src=cat(sfx_src) if sfx_src else None,
+        sfx_dst=cat(sfx_dst) if sfx_dst else None)
 
 
 def _items(sg: Segment, q_block: int = Q_BLOCK) -> List[tuple]:
