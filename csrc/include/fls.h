@@ -83,6 +83,7 @@ int fls_gemm(const void* A, const void* W, void* C, const void* R, int M, int N,
 // columns [128 j, 128 j + 128) -- the row statistic of the next norm-folded projection without a
 // pass over the hidden state (fls_rstd_from_ss)
 // rstd[r] = rsqrt(sum_j ss[r * ss_ld + j] / H + eps) for j < nparts, summed in a fixed order
+int fls_row_stat(const void* x, int ldx, int rows, int H, float eps, float* rstd, fls_stream_t s);  // row_ss + rstd_from_ss, fused
 int fls_row_ss(const void* x, int ldx, int rows, int H, float* ss, int ss_ld, fls_stream_t s);  // residual-epilogue partials of x
 int fls_rstd_from_ss(const float* ss, int ss_ld, int nparts, int rows, int H, float eps, float* rstd,
                      fls_stream_t s);

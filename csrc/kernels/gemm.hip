@@ -395,6 +395,36 @@ __global__ __launch_bounds__(256) void ss_partials_kernel(const half_t* __restri
   if (grp == 0 && m < M) ss[(size_t)m * ss_ld + j] = sq;
 }
 
+// the fused norm's statistic straight from x: per 16 rows, the 4 waves compute the rows' 128-column
+// partials exactly as ss_partials_kernel does (into LDS), then each row's rsqrt(sum / H + eps) with
+// rstd_from_ss_kernel's summation (lane j takes parts j, j + 64, ..., then warp_sum): the same bits as
+// fls_row_ss followed by fls_rstd_from_ss, in one launch (generation steps run two per layer)
+constexpr int ROW_STAT_MAX_PARTS = 128;              // H <= 16,384
+__global__ __launch_bounds__(256) void row_stat_kernel(const half_t* __restrict__ x, int ldx, int M, int nparts,
+                                                       int H, float eps, float* __restrict__ rstd) {
+  __shared__ float part[16][ROW_STAT_MAX_PARTS];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int fr = lane & 15, grp = lane >> 4;
+  const int r0 = blockIdx.x * 16;
+  const int m = r0 + fr;
+  for (int j = wave; j < nparts; j += 4) {
+    const half_t* p0 = x + (size_t)min(m, M - 1) * ldx + j * 128 + grp * 4;
+    float sq = 0.f;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) sq = ss_accum_pair(sq, *(const half4*)(p0 + p * 32), *(const half4*)(p0 + p * 32 + 16));
+    sq = row_sum_4groups(sq);
+    if (grp == 0) part[fr][j] = sq;
+  }
+  __syncthreads();
+  for (int rr = wave; rr < 16; rr += 4) {
+    if (r0 + rr >= M) break;                        // wave-uniform
+    float v = 0.f;
+    for (int j = lane; j < nparts; j += 64) v += part[rr][j];
+    v = warp_sum(v);
+    if (lane == 0) rstd[r0 + rr] = rsqrtf(v / (float)H + eps);
+  }
+}
+
 void ss_partials_raw(const half_t* C, int ldc, int M, int N, float* ss, int ss_ld, hipStream_t s) {
   if (!ss || M <= 0) return;
   const int waves = ((M + 15) / 16) * (N / 128);
@@ -472,11 +502,13 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
     return 0;
   }
   if (mid_ok && (!main_ok || (g_mid && (tiles256 < 128 || (M <= 64 && tiles256 < 512))))) {
-    // 64-column blocks when 128-column ones fill less than one round of the 256 CUs (generation-step
-    // O / down / QKV: 192-240 blocks -> 384-480)
+    // 64-column blocks for a single row tile whose 128-column grid fills less than one round of the
+    // 256 CUs: 70B generation steps with 8 prompts (M = 40) 39.7 vs 46.7 ms per step; with 32 prompts
+    // (M = 160, three row tiles) the 128-column blocks are faster, 53 vs 55.5 ms (profiles/r6_decode/
+    // mid_bn: in-graph steps, cold weights; a same-weights GEMM loop favoured 64 there too)
     const int blocks128 = ((M + mid::BMm - 1) / mid::BMm) * (N / mid::BNm);
     const bool bn64_ok = N % 64 == 0 && (EPI != FLS_EPI_ROPE || N % 128 == 0);
-    const bool bn64 = bn64_ok && (g_mid_bn == 64 || (g_mid_bn == 0 && blocks128 < 256));
+    const bool bn64 = bn64_ok && (g_mid_bn == 64 || (g_mid_bn == 0 && blocks128 < 256 && M <= mid::BMm));
     if (bn64)
       launch_mid<EPI, mid::NSTAGE, 64>(A, W, C, M, N, K, lda, ldw, ldc, ep, s);
     else
@@ -530,7 +562,7 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
 
 }  // namespace
 
-extern "C" int fls_kernels_version(void) { return 31; }
+extern "C" int fls_kernels_version(void) { return 32; }
 
 // tile order: 0 = by shape (default); g > 0: groups of g M tiles; g < 0: groups of -g N tiles (A/B, tests)
 extern "C" int fls_gemm_set_order(int order) {
@@ -575,6 +607,17 @@ extern "C" int fls_row_ss(const void* x, int ldx, int rows, int H, float* ss, in
   if (rows <= 0) return 0;
   if (H % 128 || ldx % 4 || ((uintptr_t)x & 7) || ss_ld < H / 128) return -2;
   ss_partials_raw((const half_t*)x, ldx, rows, H, ss, ss_ld, (hipStream_t)s);
+  FLS_CHECK_LAUNCH();
+  return 0;
+}
+
+// rstd[r] = rsqrt(mean(x[r]^2) + eps) for an fp16 [rows, H] matrix (H % 128 == 0, H <= 16,384), bitwise
+// fls_row_ss + fls_rstd_from_ss (the fused norm's statistic without a residual GEMM's partials)
+extern "C" int fls_row_stat(const void* x, int ldx, int rows, int H, float eps, float* rstd, fls_stream_t s) {
+  if (rows <= 0) return 0;
+  if (H % 128 || H / 128 > ROW_STAT_MAX_PARTS || ldx % 4 || ((uintptr_t)x & 7)) return -2;
+  hipLaunchKernelGGL(row_stat_kernel, dim3((rows + 15) / 16), dim3(256), 0, (hipStream_t)s, (const half_t*)x, ldx,
+                     rows, H / 128, H, eps, rstd);
   FLS_CHECK_LAUNCH();
   return 0;
 }

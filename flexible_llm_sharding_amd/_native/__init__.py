@@ -65,7 +65,7 @@ class Piece(ctypes.Structure):
                 ("kind", ctypes.c_int32), ("pad", ctypes.c_int32)]
 
 
-KERNELS_ABI = 31   # bumped whenever a C signature in csrc/include/fls.h (or an accepted argument) changes
+KERNELS_ABI = 32   # bumped whenever a C signature in csrc/include/fls.h (or an accepted argument) changes
 
 
 def _load_kernels(path: str = _KERNELS):
@@ -81,6 +81,7 @@ def _load_kernels(path: str = _KERNELS):
           c_float, c_void_p, c_int, c_void_p, c_uint64, c_void_p)
     _bind(lib, "fls_rstd_from_ss", c_int, c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p, c_void_p)
     _bind(lib, "fls_row_ss", c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p)
+    _bind(lib, "fls_row_stat", c_int, c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_void_p)
     _bind(lib, "fls_argmax_rows", c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p)
     _bind(lib, "fls_row_rstd", c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_float, c_void_p, c_void_p)
     _bind(lib, "fls_fold_norm", c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p)

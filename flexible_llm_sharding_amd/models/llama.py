@@ -248,8 +248,8 @@ class ExecContext:
         pipeline rank, parked in host memory, after grouped attention or in the pruned last layer
         gets the same bits as one straight from the residual GEMM."""
         H, eps = self.cfg.hidden_size, self.cfg.rms_norm_eps
-        if H % 128 == 0 and hasattr(self.ops, "row_ss"):
-            return self.ops.rstd_from_ss(self.ops.row_ss(x), H, eps, out=out)
+        if H % 128 == 0 and H <= 16384 and hasattr(self.ops, "row_stat"):
+            return self.ops.row_stat(x, eps, out=out)
         return self.ops.row_rstd(x, eps, out=out)
 
 

@@ -216,6 +216,16 @@ class HipOps:
              "fls_row_ss")
         return ss
 
+    def row_stat(self, x, eps, out=None):
+        """[rows] fp32 rsqrt(mean(x[row]^2) + eps) computed as :meth:`row_ss` + :meth:`rstd_from_ss`
+        would (bitwise), in one launch (H % 128 == 0)."""
+        _f16(x, "x")
+        rows, H = x.shape
+        r = out if out is not None else torch.empty(rows, dtype=torch.float32, device=x.device)
+        _chk(self.k.fls_row_stat(x.data_ptr(), x.stride(0), rows, H, float(eps), r.data_ptr(), _stream()),
+             "fls_row_stat")
+        return r
+
     def row_rstd(self, x, eps, row_idx=None, out=None):
         """[rows] fp32 rsqrt(mean(x[row]^2) + eps) (rows = row_idx or every row of x)."""
         _f16(x, "x")

@@ -473,6 +473,9 @@ def test_row_ss_matches_residual_epilogue(ops):
         assert torch.equal(got, ss), M
         want = (out.float() ** 2).reshape(M, H // 128, 128).sum(-1)
         assert torch.allclose(got, want, rtol=1e-4, atol=1e-3)
+        # the fused statistic == partials + rstd_from_ss, bit for bit
+        eps = 1e-5
+        assert torch.equal(ops.row_stat(out, eps), ops.rstd_from_ss(ss, H, eps)), M
 
 
 @pytest.mark.parametrize("order", [8, -4, -8, 1, -1, 2, 3, -5])
