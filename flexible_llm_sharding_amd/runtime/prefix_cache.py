@@ -338,13 +338,6 @@ class PrefixKVCache:
                     t = -(-t // PrefixEntry.REGION_ALIGN) * PrefixEntry.REGION_ALIGN + len(s) + self.suffix_growth
         return t
 
-    def stage_bytes(self, tps: Sequence, elem: int = 2) -> int:
-        """HBM of host mode's staging buffers for a call on ``tps`` (0 in device mode)."""
-        if not self.host:
-            return 0
-        rows = max(self.entry_rows(tps), self.stage.bufs[0].shape[0] if self.stage else 0)
-        return HostStage.N_BUFS * rows * self.kv_cols * elem
-
     def ensure_stage(self, tps: Sequence) -> None:
         """Host mode: staging buffers large enough for ``tps``'s entry (grown, never shrunk)."""
         if not self.host:
