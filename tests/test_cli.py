@@ -299,3 +299,16 @@ def test_every_env_knob_is_registered():
     # the README carries the table
     readme = (root / "README.md").read_text()
     assert all(f"`{n}`" in readme for n in knobs.KNOBS), "README knob table out of date"
+
+
+def test_dp_gather_comm_flag():
+    """--dp_gather_comm native: the data-parallel prefetchers' gather communicator (Comm.dup) becomes
+    the native RCCL one on a GPU; on the CPU (gloo tests) dup() keeps torch.distributed."""
+    from flexible_llm_sharding_amd.parallel.comm import Comm
+    base = ["--prompt_pickle", "p.pkl", "--output_file", "o.pkl"]
+    assert parse_args(base).dp_gather_comm == "torch"
+    assert parse_args(base + ["--dp_gather_comm", "native"]).dp_gather_comm == "native"
+    c = Comm(0, 1, "cpu")
+    c.gather_native = True
+    d = c.dup()
+    assert type(d) is Comm and d.world == 1
