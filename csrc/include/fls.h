@@ -119,6 +119,8 @@ int fls_moe_combine(const void* y, int ldy, const int* ids, const int* dest, con
                     int k, int H, const void* sh, int ldsh, fls_stream_t s);   // sh: optional shared-expert term
 int fls_gemm_set_order(int order);   // tile order: 0 by shape, 8 M-grouped, -4/-8 N-grouped
 int fls_gemm_set_mid_bn(int bn);     // mid-M block columns: 0 auto, 64 / 128 forced
+int fls_gemm_set_mid_waves(int waves);  // 128-column mid-M blocks: 0 auto, 4 / 8 waves forced
+int fls_gemm_set_mid_rows(int rows);  // 8-wave mid-M blocks: rows, 0 auto, 64 / 128 forced
 int fls_gemm_set_mid(int on);   // 64x128-tile kernel for small / medium M (default on)
 // shared-prefix / varlen flash attention over packed work items (int32 x8:
 // q_start q_len q_off r0_start r0_len r0_causal r1_start r1_len).

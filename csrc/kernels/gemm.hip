@@ -19,7 +19,8 @@
 //     XCD-aware bijective block remap + grouped tile order (guide T1).
 //   * gemm_nt_mid — 64 x 128 x 64 tiles, 3-deep LDS-DMA ring, for M too small
 //     to fill 256 CUs with 256 x 256 tiles, and for odd K-tile counts (v10's
-//     body is unrolled over two K-tiles).
+//     body is unrolled over two K-tiles); 4 waves, or 8 (two per SIMD) for
+//     grids of about one block per CU, 64 or 128 rows; 64-column blocks.
 //   * gemm_nt_generic — any shape (bounds-masked loads), for odd test shapes.
 //
 // The MFMA computes C^T tiles (A operand = W fragment, B operand = X fragment)
@@ -128,12 +129,21 @@ __global__ __launch_bounds__(256) void gemm_nt_generic(const half_t* __restrict_
 // barrier per K-tile; XCD-aware order puts every M tile of one N tile on the
 // same XCD so each weight tile comes from HBM once and from L2 after that.
 // Any K-tile count (the tail path for odd K / 64).
+// 8-wave 64-row mid blocks: column (in the 128-column block) of subtile t of wave column wn.  RoPE: the
+// pair is a column and its partner hd/2 away (hd 128: 64 columns; hd 64: 32 in the same head).
+__device__ __forceinline__ int mid8_col(int epi, int wn, int t) {
+  if (epi == FLS_EPI_ROPE) return wn * 16 + t * 64;
+  if (epi == EPI_ROPE64) return (wn >> 1) * 64 + (wn & 1) * 16 + t * 32;
+  return wn * 32 + t * 16;
+}
+
 namespace mid {
 constexpr int BMm = 64, BNm = 128, BKm = 64, NTm = 256, NSTAGE = 3;
 // BNT: output columns per block, 128 (4 waves in 2 x 2, each 32 x 64) or 64 (each 32 x 32: twice the
 // blocks for grids of less than one round of 128-column tiles)
-constexpr int stage_bytes(int bnt) { return (BMm + bnt) * BKm * 2; }   // A rows 0..63 then W rows
-constexpr int per_wave(int bnt) { return (BMm + bnt) / 8 / 4; }        // 8-row (1 KiB) LDS-DMA groups
+// A rows 0 .. bmt-1 then W rows; LDS-DMA in 8-row (1 KiB) groups
+constexpr int stage_bytes(int bnt, int bmt = BMm) { return (bmt + bnt) * BKm * 2; }
+constexpr int per_wave(int bnt, int bmt = BMm, int wv = 4) { return (bmt + bnt) / 8 / wv; }
 }  // namespace mid
 
 // NST: LDS stages, NST - 1 K-tiles in flight ahead of the one being multiplied (3: 72 KB, two blocks
@@ -142,16 +152,29 @@ constexpr int per_wave(int bnt) { return (BMm + bnt) / 8 / 4; }        // 8-row 
 // BNT = 64 blocks: a wave holds two 16-column subtiles (RoPE: a column and its partner hd/2 away; for
 // head_dim 128 a block takes 32 columns of a head and their 32 partners).  Same fragments, MFMA and
 // K order as BNT = 128, so the two are bitwise equal.
-template <int EPI, int NST, int BNT>
-__global__ __launch_bounds__(mid::NTm) void gemm_nt_mid(const half_t* __restrict__ A, const half_t* __restrict__ W,
+//
+// WV = 8 (BNT = 128 only), two waves per SIMD.  With grids of about one block per CU (generation
+// steps: the O / down / QKV projections at M = 64-320) a 4-wave block is bound by the latency chain
+// of its single wave per SIMD (DMA wait, barrier, LDS reads, MFMAs); a second wave's MFMAs run under
+// the first one's LDS reads (70B down at M = 160: 225 -> 196 us).  Two shapes:
+//   BMT = 64 : waves in 2 x 4, each 32 x 32 outputs (its two 16-column subtiles are a RoPE pair: a
+//              column and its partner hd/2 away); 72 KB of LDS, two blocks per CU;
+//   BMT = 128: waves in 4 x 2, each 32 x 64 as in the 4-wave block; 96 KB, one block per CU, half the
+//              blocks (M = 320: 192 instead of 320, which left 64 CUs with two blocks).
+// Same fragments, MFMA and K order in every shape, so all are bitwise equal.
+template <int EPI, int NST, int BNT, int WV = 4, int BMT = mid::BMm>
+__global__ __launch_bounds__(64 * WV) void gemm_nt_mid(const half_t* __restrict__ A, const half_t* __restrict__ W,
                                                      half_t* __restrict__ C, int M, int N, int K, int lda, int ldw,
                                                      int ldc, Epi ep) {
   using namespace mid;
-  constexpr int STAGE = stage_bytes(BNT), PER_WAVE = per_wave(BNT), NSUB = BNT / 32;
+  static_assert(WV == 4 || (WV == 8 && BNT == 128), "8-wave blocks take 128 columns");
+  static_assert(BMT == 64 || (BMT == 128 && WV == 8), "128-row blocks have 8 waves");
+  constexpr bool L24 = WV == 8 && BMT == 64;       // 2 x 4 waves of 32 x 32
+  constexpr int STAGE = stage_bytes(BNT, BMT), PER_WAVE = per_wave(BNT, BMT, WV), NSUB = L24 ? 2 : BNT / 32;
   extern __shared__ __attribute__((aligned(16))) char lds_mid[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, grp = lane >> 4;
-  const int mt = (M + BMm - 1) / BMm, ntn = N / BNT;
+  const int mt = (M + BMT - 1) / BMT, ntn = N / BNT;
   // XCD-aware bijective remap: logical tiles [xcd*q .. ) run on one XCD, M fastest
   int bid = blockIdx.x;
   {
@@ -159,10 +182,10 @@ __global__ __launch_bounds__(mid::NTm) void gemm_nt_mid(const half_t* __restrict
     const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7, loc = bid >> 3;
     if (nwg >= 8) bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
   }
-  const int m0 = (bid % mt) * BMm;
+  const int m0 = (bid % mt) * BMT;
   const int bn = bid / mt;
   const int n0 = bn * BNT;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = L24 ? wave >> 2 : wave >> 1, wn = L24 ? wave & 3 : wave & 1;
   const int nk = K / BKm;
   const bool rope128 = EPI == FLS_EPI_ROPE;
   // BNT = 64 with RoPE over 128-wide heads: local W row l -> column of head bn / 2, quarter bn % 2
@@ -172,18 +195,18 @@ __global__ __launch_bounds__(mid::NTm) void gemm_nt_mid(const half_t* __restrict
     return n0 + l;
   };
 
-  // this lane's LDS-DMA sources: group g = wave + 4*i covers tile rows 8*g .. 8*g+7
+  // this lane's LDS-DMA sources: group g = wave + WV*i covers tile rows 8*g .. 8*g+7
   const half_t* src[PER_WAVE];
   const int sub = lane >> 3;                       // row inside the 8-row group
   const int kc = ((lane & 7) ^ sub) * 8;           // source chunk pre-swizzled (read XORs it back)
 #pragma unroll
   for (int i = 0; i < PER_WAVE; ++i) {
-    const int g = wave + 4 * i;
-    if (g < BMm / 8) {
+    const int g = wave + WV * i;
+    if (g < BMT / 8) {
       const int m = min(m0 + g * 8 + sub, M - 1);
       src[i] = A + (size_t)m * lda + kc;
     } else {
-      const int n = gcol((g - BMm / 8) * 8 + sub);
+      const int n = gcol((g - BMT / 8) * 8 + sub);
       const int nr = EPI == FLS_EPI_SWIGLU ? gu_phys_row(n, ep.gu_rows) : n;
       src[i] = W + (size_t)nr * ldw + kc;
     }
@@ -193,13 +216,14 @@ __global__ __launch_bounds__(mid::NTm) void gemm_nt_mid(const half_t* __restrict
   auto stage = [&](int s, int kt) {
     char* base = lds_mid + (s % NST) * STAGE;
 #pragma unroll
-    for (int i = 0; i < PER_WAVE; ++i) glds16(src[i] + (size_t)kt * BKm, base + (wave + 4 * i) * 1024);
+    for (int i = 0; i < PER_WAVE; ++i) glds16(src[i] + (size_t)kt * BKm, base + (wave + WV * i) * 1024);
   };
   // local W rows of this wave's subtiles (RoPE: subtile t + NSUB / 2 is subtile t's partner)
   int wrow[NSUB];
 #pragma unroll
   for (int t = 0; t < NSUB; ++t) {
-    if constexpr (BNT == 128) wrow[t] = sub_col(rope128, wn, t) + fr;
+    if constexpr (L24) wrow[t] = mid8_col(EPI, wn, t) + fr;
+    else if constexpr (BNT == 128) wrow[t] = sub_col(rope128, wn, t) + fr;
     else wrow[t] = (is_rope(EPI) ? wn * 16 + t * 32 : wn * 32 + t * 16) + fr;
   }
 
@@ -217,7 +241,7 @@ __global__ __launch_bounds__(mid::NTm) void gemm_nt_mid(const half_t* __restrict
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NST - 1) * PER_WAVE) : "memory");   // tile kt landed
     __builtin_amdgcn_s_barrier();                          // every wave's part of tile kt landed
     const char* Xs = lds_mid + (kt % NST) * STAGE;
-    const char* Ws = Xs + BMm * BKm * 2;
+    const char* Ws = Xs + BMT * BKm * 2;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int c = ks * 4 + grp;                          // logical 16-byte chunk of this lane
@@ -246,7 +270,12 @@ __global__ __launch_bounds__(mid::NTm) void gemm_nt_mid(const half_t* __restrict
   for (int u = 0; u < 2; ++u) {
     const int m = m0 + wm * 32 + u * 16 + fr;
     if (m >= M) continue;
-    if constexpr (is_rope(EPI)) {
+    if constexpr (L24) {
+      if constexpr (is_rope(EPI))
+        store_rope_pair(C, ldc, m, n0 + mid8_col(EPI, wn, 0) + 4 * grp, acc[u][0], acc[u][1], ep);
+      else
+        store_pair_off<EPI>(C, ldc, m, n0 + wn * 32, 4 * grp, acc[u][0], acc[u][1], ep);
+    } else if constexpr (is_rope(EPI)) {
       if constexpr (BNT == 128) {
 #pragma unroll
         for (int q = 0; q < 2; ++q)
@@ -265,19 +294,22 @@ __global__ __launch_bounds__(mid::NTm) void gemm_nt_mid(const half_t* __restrict
 int g_order = 0;             // 0: by shape, else a fixed signed group size (fls_gemm_set_order)
 int g_mid = 1;               // mid-M kernel on (fls_gemm_set_mid)
 int g_mid_bn = 0;            // mid-M block columns: 0 auto, 64 / 128 forced where valid (fls_gemm_set_mid_bn)
+int g_mid_waves = 0;         // 128-column mid blocks: 0 auto, 4 / 8 waves forced (fls_gemm_set_mid_waves)
+int g_mid_rows = 0;          // 8-wave mid blocks' rows: 0 auto, 64 / 128 forced (fls_gemm_set_mid_rows)
 
-template <int EPI, int NST, int BNT>
+template <int EPI, int NST, int BNT, int WV = 4, int BMT = mid::BMm>
 void launch_mid(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int lda, int ldw, int ldc,
                 const Epi& ep, hipStream_t s) {
   static bool attr = false;
-  constexpr int lds = NST * mid::stage_bytes(BNT);
+  constexpr int lds = NST * mid::stage_bytes(BNT, BMT);
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_nt_mid<EPI, NST, BNT>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    (void)hipFuncSetAttribute((const void*)gemm_nt_mid<EPI, NST, BNT, WV, BMT>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
-  const int blocks = ((M + mid::BMm - 1) / mid::BMm) * (N / BNT);
-  hipLaunchKernelGGL((gemm_nt_mid<EPI, NST, BNT>), dim3(blocks), dim3(mid::NTm), lds, s, A, W, C, M, N, K, lda, ldw,
-                     ldc, ep);
+  const int blocks = ((M + BMT - 1) / BMT) * (N / BNT);
+  hipLaunchKernelGGL((gemm_nt_mid<EPI, NST, BNT, WV, BMT>), dim3(blocks), dim3(64 * WV), lds, s, A, W, C, M, N, K,
+                     lda, ldw, ldc, ep);
 }
 
 template <int EPI>
@@ -509,8 +541,18 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
     const int blocks128 = ((M + mid::BMm - 1) / mid::BMm) * (N / mid::BNm);
     const bool bn64_ok = N % 64 == 0 && (EPI != FLS_EPI_ROPE || N % 128 == 0);
     const bool bn64 = bn64_ok && (g_mid_bn == 64 || (g_mid_bn == 0 && blocks128 < 256 && M <= mid::BMm));
+    // 8 waves for grids of < 2 rounds of 64-row blocks; 128-row blocks when 64-row ones take more than
+    // one round, 128-row ones fit in one and K is long (profiles/r6_decode/mid8, 70B at M = 320: down
+    // 343 -> 276 us; the K = 8,192 projections ran 5-10% slower with 128 rows)
+    const bool w8 = g_mid_waves == 8 || (g_mid_waves == 0 && blocks128 < 512);
+    const int rows128 = (M + 127) / 128 * (N / mid::BNm);
+    const bool r128 = g_mid_rows == 128 || (g_mid_rows == 0 && blocks128 > 256 && rows128 <= 256 && K >= 16384);
     if (bn64)
       launch_mid<EPI, mid::NSTAGE, 64>(A, W, C, M, N, K, lda, ldw, ldc, ep, s);
+    else if (w8 && r128)
+      launch_mid<EPI, mid::NSTAGE, 128, 8, 128>(A, W, C, M, N, K, lda, ldw, ldc, ep, s);
+    else if (w8)
+      launch_mid<EPI, mid::NSTAGE, 128, 8>(A, W, C, M, N, K, lda, ldw, ldc, ep, s);
     else
       launch_mid<EPI, mid::NSTAGE, 128>(A, W, C, M, N, K, lda, ldw, ldc, ep, s);
     FLS_CHECK_LAUNCH();
@@ -562,7 +604,7 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
 
 }  // namespace
 
-extern "C" int fls_kernels_version(void) { return 32; }
+extern "C" int fls_kernels_version(void) { return 33; }
 
 // tile order: 0 = by shape (default); g > 0: groups of g M tiles; g < 0: groups of -g N tiles (A/B, tests)
 extern "C" int fls_gemm_set_order(int order) {
@@ -626,6 +668,22 @@ extern "C" int fls_row_stat(const void* x, int ldx, int rows, int H, float eps, 
 extern "C" int fls_gemm_set_mid_bn(int bn) {
   const int old = g_mid_bn;
   g_mid_bn = bn == 64 || bn == 128 ? bn : 0;
+  return old;
+}
+
+// 128-column mid-M blocks: 0 auto (default: 8 waves for grids of < 512 blocks), 4 or 8 waves forced
+// (tests / A-B); returns the previous
+extern "C" int fls_gemm_set_mid_waves(int waves) {
+  const int old = g_mid_waves;
+  g_mid_waves = waves == 4 || waves == 8 ? waves : 0;
+  return old;
+}
+
+// 8-wave mid-M blocks' rows: 0 auto (default: 128 when 64-row blocks would take more than one round
+// and 128-row ones fit in one), 64 or 128 forced (tests / A-B); returns the previous
+extern "C" int fls_gemm_set_mid_rows(int rows) {
+  const int old = g_mid_rows;
+  g_mid_rows = rows == 64 || rows == 128 ? rows : 0;
   return old;
 }
 

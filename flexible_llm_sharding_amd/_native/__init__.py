@@ -65,7 +65,7 @@ class Piece(ctypes.Structure):
                 ("kind", ctypes.c_int32), ("pad", ctypes.c_int32)]
 
 
-KERNELS_ABI = 32   # bumped whenever a C signature in csrc/include/fls.h (or an accepted argument) changes
+KERNELS_ABI = 33   # bumped whenever a C signature in csrc/include/fls.h (or an accepted argument) changes
 
 
 def _load_kernels(path: str = _KERNELS):
@@ -91,6 +91,8 @@ def _load_kernels(path: str = _KERNELS):
     _bind(lib, "fls_gemm_set_row_chunk", c_int, c_int)
     _bind(lib, "fls_gemm_set_mid", c_int, c_int)
     _bind(lib, "fls_gemm_set_mid_bn", c_int, c_int)
+    _bind(lib, "fls_gemm_set_mid_waves", c_int, c_int)
+    _bind(lib, "fls_gemm_set_mid_rows", c_int, c_int)
     _bind(lib, "fls_moe_route", c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
           c_void_p)
     _bind(lib, "fls_moe_router_route", c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,

@@ -39,11 +39,13 @@ def main():
                     help="also the --exact_reuse false arm (small-M kernels; tokens compared, not guaranteed)")
     ap.add_argument("--max-vram-gb", type=float, default=None)
     ap.add_argument("--mid-bn", type=int, default=0, help="force the mid-M kernel's block columns (64 / 128; A/B)")
+    ap.add_argument("--mid-waves", type=int, default=0, help="force the 128-column mid blocks' waves (4 / 8; A/B)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
-    if a.mid_bn:
+    if a.mid_bn or a.mid_waves:
         from flexible_llm_sharding_amd import _native
         _native.kernels().fls_gemm_set_mid_bn(a.mid_bn)
+        _native.kernels().fls_gemm_set_mid_waves(a.mid_waves)
     cfg = preset(a.model)
     store = HostStore.synthetic(cfg, dev, seed=0, fold_norms=True)
     tok_dir = f"/tmp/fls_probe_tok_{os.getpid()}"
@@ -52,7 +54,7 @@ def main():
     prompts = synthetic_prompts(a.prompts, a.prefix_len, 5, a.suffix_len, cfg.vocab_size, seed=0)
     args = argparse.Namespace(num_gen_token=a.gen, data_parallel=False, num_batch=1)
     res = {"model": a.model, "prompts": a.prompts, "prefix_len": a.prefix_len, "suffix_len": a.suffix_len,
-           "mid_bn": a.mid_bn or "auto",
+           "mid_bn": a.mid_bn or "auto", "mid_waves": a.mid_waves or "auto",
            "num_gen_token": a.gen,
            "weights": f"streamed, --max_vram_gb {a.max_vram_gb}" if a.max_vram_gb else "resident in HBM"}
     runs = {}

@@ -406,8 +406,8 @@ def test_gemm_main_all_epilogues(ops, ref):
 @pytest.mark.parametrize("hd", [128, 64])
 def test_gemm_row_exact_small_m_bitwise(ops, ref, hd):
     """Row-exact small-M GEMMs (generation steps): every row of M = 1 / 17 / 64 / 160 / 320 equals,
-    bit for bit, the same row of a 1,000-row row-exact GEMM, with the mid-M kernel's 64- and
-    128-column blocks (bitwise equal to each other), for all four epilogues incl. bias, per-row scale
+    bit for bit, the same row of a 1,000-row row-exact GEMM, with the mid-M kernel's 64-column
+    blocks and its 128-column blocks of 4 and 8 waves, 64 and 128 rows (bitwise equal to each other), for all four epilogues incl. bias, per-row scale
     and RoPE (both head sizes); and the fp32 reference."""
     from flexible_llm_sharding_amd.config import ModelConfig
     from flexible_llm_sharding_amd.models.llama import rope_tables
@@ -432,25 +432,30 @@ def test_gemm_row_exact_small_m_bitwise(ops, ref, hd):
                 ops.gemm(xs, wqkv, EPI_ROPE, positions=p, cos=cos, sin=sin, rope_cols=(nh + nkv) * hd,
                          head_dim=hd, bias=bq, rscale=r)]
 
+    # the mid kernel's 64-column blocks, and its 128-column blocks of 4 and of 8 waves (64 / 128 rows)
+    arms = ((128, 4, 0), (128, 8, 64), (128, 8, 128), (64, 0, 0))
+
+    def forced(bn, waves, rows, fn):
+        old = (ops.k.fls_gemm_set_mid_bn(bn), ops.k.fls_gemm_set_mid_waves(waves),
+               ops.k.fls_gemm_set_mid_rows(rows))
+        try:
+            return fn()
+        finally:
+            ops.k.fls_gemm_set_mid_bn(old[0])
+            ops.k.fls_gemm_set_mid_waves(old[1])
+            ops.k.fls_gemm_set_mid_rows(old[2])
+
     with ops.row_exact():
         full = run(torch.arange(Mb, device=DEV))
-        for bn in (128, 64):                     # the mid kernel's 128- and 64-column blocks (auto: 64 here)
-            old_bn = ops.k.fls_gemm_set_mid_bn(bn)
-            try:
-                for a, b in zip(run(torch.arange(Mb, device=DEV)), full):
-                    assert torch.equal(a, b), bn
-            finally:
-                ops.k.fls_gemm_set_mid_bn(old_bn)
+        for arm in arms:
+            for a, b in zip(forced(*arm, lambda: run(torch.arange(Mb, device=DEV))), full):
+                assert torch.equal(a, b), arm
         g = torch.Generator().manual_seed(5)
         for m in (1, 17, 64, 160, 320):
             rows = torch.randperm(Mb, generator=g)[:m].to(DEV)
-            for bn in (64, 128):
-                old_bn = ops.k.fls_gemm_set_mid_bn(bn)
-                try:
-                    for a, b in zip(run(rows), full):
-                        assert torch.equal(a, b[rows]), (m, bn)
-                finally:
-                    ops.k.fls_gemm_set_mid_bn(old_bn)
+            for arm in arms:
+                for a, b in zip(forced(*arm, lambda: run(rows)), full):
+                    assert torch.equal(a, b[rows]), (m, arm)
     torch.cuda.synchronize()
     assert rel_err(full[0], x.float() @ wo.float().t()) < 2e-3
     assert rel_err(full[2].cpu(), ref.swiglu_up((x.float() * rs[:, None]).cpu(), wgu.float().cpu())) < 3e-3
