@@ -427,34 +427,41 @@ __global__ __launch_bounds__(256) void ss_partials_kernel(const half_t* __restri
   if (grp == 0 && m < M) ss[(size_t)m * ss_ld + j] = sq;
 }
 
-// the fused norm's statistic straight from x: per 16 rows, the 4 waves compute the rows' 128-column
-// partials exactly as ss_partials_kernel does (into LDS), then each row's rsqrt(sum / H + eps) with
-// rstd_from_ss_kernel's summation (lane j takes parts j, j + 64, ..., then warp_sum): the same bits as
-// fls_row_ss followed by fls_rstd_from_ss, in one launch (generation steps run two per layer)
+// the fused norm's statistic straight from x, one wave per row: lane j computes the 128-column
+// partials j, j + 64, ... itself, with ss_partials_kernel's per-lane FMA chains (one per 4-column group
+// g) combined as row_sum_4groups does, (g0 + g2) + (g1 + g3), and sums them in rstd_from_ss_kernel's
+// order (lane j takes parts j, j + 64, ..., then warp_sum): the same bits as fls_row_ss followed by
+// fls_rstd_from_ss, in one launch (generation steps run two per layer).  The 16-row lane layout of
+// the GEMM epilogue, kept here first, cost 16 us per launch at any row count (16 rows per block, 32
+// rows' worth of scattered 32-byte pieces per load); lane-per-part loads stream each row.
 constexpr int ROW_STAT_MAX_PARTS = 128;              // H <= 16,384
-__global__ __launch_bounds__(256) void row_stat_kernel(const half_t* __restrict__ x, int ldx, int M, int nparts,
-                                                       int H, float eps, float* __restrict__ rstd) {
-  __shared__ float part[16][ROW_STAT_MAX_PARTS];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int fr = lane & 15, grp = lane >> 4;
-  const int r0 = blockIdx.x * 16;
-  const int m = r0 + fr;
-  for (int j = wave; j < nparts; j += 4) {
-    const half_t* p0 = x + (size_t)min(m, M - 1) * ldx + j * 128 + grp * 4;
-    float sq = 0.f;
+__global__ __launch_bounds__(256) void row_stat_kernel(const half_t* __restrict__ x, int ldx, int M, int nparts, int H,
+                                                       float eps, float* __restrict__ rstd) {
+  const int lane = threadIdx.x & 63;
+  const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= M) return;                               // wave-uniform (no block barrier)
+  const half_t* row = x + (size_t)m * ldx;
+  float v = 0.f;
+  for (int j = lane; j < nparts; j += 64) {
+    half4 q[32];                                    // the part's 128 columns
 #pragma unroll
-    for (int p = 0; p < 4; ++p) sq = ss_accum_pair(sq, *(const half4*)(p0 + p * 32), *(const half4*)(p0 + p * 32 + 16));
-    sq = row_sum_4groups(sq);
-    if (grp == 0) part[fr][j] = sq;
+    for (int k = 0; k < 16; ++k) {
+      const half8 c = *(const half8*)(row + j * 128 + k * 8);
+      q[2 * k] = c.lo;
+      q[2 * k + 1] = c.hi;
+    }
+    float sg[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      float sq = 0.f;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) sq = ss_accum_pair(sq, q[p * 8 + g], q[p * 8 + 4 + g]);
+      sg[g] = sq;
+    }
+    v += (sg[0] + sg[2]) + (sg[1] + sg[3]);
   }
-  __syncthreads();
-  for (int rr = wave; rr < 16; rr += 4) {
-    if (r0 + rr >= M) break;                        // wave-uniform
-    float v = 0.f;
-    for (int j = lane; j < nparts; j += 64) v += part[rr][j];
-    v = warp_sum(v);
-    if (lane == 0) rstd[r0 + rr] = rsqrtf(v / (float)H + eps);
-  }
+  v = warp_sum(v);
+  if (lane == 0) rstd[m] = rsqrtf(v / (float)H + eps);
 }
 
 void ss_partials_raw(const half_t* C, int ldc, int M, int N, float* ss, int ss_ld, hipStream_t s) {
@@ -657,9 +664,9 @@ extern "C" int fls_row_ss(const void* x, int ldx, int rows, int H, float* ss, in
 // fls_row_ss + fls_rstd_from_ss (the fused norm's statistic without a residual GEMM's partials)
 extern "C" int fls_row_stat(const void* x, int ldx, int rows, int H, float eps, float* rstd, fls_stream_t s) {
   if (rows <= 0) return 0;
-  if (H % 128 || H / 128 > ROW_STAT_MAX_PARTS || ldx % 4 || ((uintptr_t)x & 7)) return -2;
-  hipLaunchKernelGGL(row_stat_kernel, dim3((rows + 15) / 16), dim3(256), 0, (hipStream_t)s, (const half_t*)x, ldx,
-                     rows, H / 128, H, eps, rstd);
+  if (H % 128 || H / 128 > ROW_STAT_MAX_PARTS || ldx % 8 || ((uintptr_t)x & 15)) return -2;
+  hipLaunchKernelGGL(row_stat_kernel, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)s, (const half_t*)x, ldx, rows,
+                     H / 128, H, eps, rstd);
   FLS_CHECK_LAUNCH();
   return 0;
 }

@@ -218,9 +218,11 @@ class HipOps:
 
     def row_stat(self, x, eps, out=None):
         """[rows] fp32 rsqrt(mean(x[row]^2) + eps) computed as :meth:`row_ss` + :meth:`rstd_from_ss`
-        would (bitwise), in one launch (H % 128 == 0)."""
+        would (bitwise), in one launch (H % 128 == 0; rows 16-byte aligned, else those two launches)."""
         _f16(x, "x")
         rows, H = x.shape
+        if x.stride(0) % 8 or x.data_ptr() % 16:
+            return self.rstd_from_ss(self.row_ss(x), H, eps, out=out)
         r = out if out is not None else torch.empty(rows, dtype=torch.float32, device=x.device)
         _chk(self.k.fls_row_stat(x.data_ptr(), x.stride(0), rows, H, float(eps), r.data_ptr(), _stream()),
              "fls_row_stat")

@@ -481,6 +481,16 @@ def test_row_ss_matches_residual_epilogue(ops):
         # the fused statistic == partials + rstd_from_ss, bit for bit
         eps = 1e-5
         assert torch.equal(ops.row_stat(out, eps), ops.rstd_from_ss(ss, H, eps)), M
+    # model widths (64 and 128 partials per row: one and two per lane), ragged row counts, and a
+    # view whose rows are not 16-byte aligned (the two-launch path)
+    for H2, M2 in ((8192, 37), (16384, 6), (4096, 130)):
+        x = rnd(M2, H2, seed=74)
+        want = ops.rstd_from_ss(ops.row_ss(x), H2, 1e-5)
+        assert torch.equal(ops.row_stat(x, 1e-5), want), (H2, M2)
+        xv = rnd(M2, H2 + 4, seed=74)[:, 4:]
+        xv.copy_(x)
+        assert torch.equal(ops.row_stat(xv, 1e-5), want), (H2, M2, "unaligned")
+        assert rel_err(want, torch.rsqrt(x.float().pow(2).mean(-1) + 1e-5)) < 1e-5
 
 
 @pytest.mark.parametrize("order", [8, -4, -8, 1, -1, 2, 3, -5])
