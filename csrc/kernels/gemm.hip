@@ -153,23 +153,27 @@ constexpr int per_wave(int bnt, int bmt = BMm, int wv = 4) { return (bmt + bnt) 
 // head_dim 128 a block takes 32 columns of a head and their 32 partners).  Same fragments, MFMA and
 // K order as BNT = 128, so the two are bitwise equal.
 //
-// WV = 8 (BNT = 128 only), two waves per SIMD.  With grids of about one block per CU (generation
+// WV = 8, two waves per SIMD.  With grids of about one block per CU (generation
 // steps: the O / down / QKV projections at M = 64-320) a 4-wave block is bound by the latency chain
 // of its single wave per SIMD (DMA wait, barrier, LDS reads, MFMAs); a second wave's MFMAs run under
 // the first one's LDS reads (70B down at M = 160: 225 -> 196 us).  Two shapes:
 //   BMT = 64 : waves in 2 x 4, each 32 x 32 outputs (its two 16-column subtiles are a RoPE pair: a
 //              column and its partner hd/2 away); 72 KB of LDS, two blocks per CU;
 //   BMT = 128: waves in 4 x 2, each 32 x 64 as in the 4-wave block; 96 KB, one block per CU, half the
-//              blocks (M = 320: 192 instead of 320, which left 64 CUs with two blocks).
+//              blocks (M = 320: 192 instead of 320, which left 64 CUs with two blocks);
+//   BNT = 64 : waves in 4 x 2, each 16 x 32 (the 4-wave 64-column block's columns); M <= 64 layers
+//              406 -> 377 us at M = 16, 431 -> 417 at M = 64 (profiles/r6_decode/mid8/bn64_*).
 // Same fragments, MFMA and K order in every shape, so all are bitwise equal.
 template <int EPI, int NST, int BNT, int WV = 4, int BMT = mid::BMm>
 __global__ __launch_bounds__(64 * WV) void gemm_nt_mid(const half_t* __restrict__ A, const half_t* __restrict__ W,
                                                      half_t* __restrict__ C, int M, int N, int K, int lda, int ldw,
                                                      int ldc, Epi ep) {
   using namespace mid;
-  static_assert(WV == 4 || (WV == 8 && BNT == 128), "8-wave blocks take 128 columns");
-  static_assert(BMT == 64 || (BMT == 128 && WV == 8), "128-row blocks have 8 waves");
-  constexpr bool L24 = WV == 8 && BMT == 64;       // 2 x 4 waves of 32 x 32
+  static_assert(WV == 4 || WV == 8, "4 or 8 waves");
+  static_assert(BMT == 64 || (BMT == 128 && WV == 8 && BNT == 128), "128-row blocks: 8 waves, 128 columns");
+  constexpr bool L24 = WV == 8 && BMT == 64 && BNT == 128;   // 2 x 4 waves of 32 x 32
+  constexpr bool L42 = WV == 8 && BNT == 64;                 // 4 x 2 waves of 16 x 32
+  constexpr int RW = L42 ? 16 : 32, U = RW / 16;             // rows per wave, 16-row subtiles per wave
   constexpr int STAGE = stage_bytes(BNT, BMT), PER_WAVE = per_wave(BNT, BMT, WV), NSUB = L24 ? 2 : BNT / 32;
   extern __shared__ __attribute__((aligned(16))) char lds_mid[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -227,9 +231,9 @@ __global__ __launch_bounds__(64 * WV) void gemm_nt_mid(const half_t* __restrict_
     else wrow[t] = (is_rope(EPI) ? wn * 16 + t * 32 : wn * 32 + t * 16) + fr;
   }
 
-  floatx4 acc[2][NSUB];
+  floatx4 acc[U][NSUB];
 #pragma unroll
-  for (int u = 0; u < 2; ++u)
+  for (int u = 0; u < U; ++u)
 #pragma unroll
     for (int t = 0; t < NSUB; ++t) acc[u][t] = floatx4{0.f, 0.f, 0.f, 0.f};
 
@@ -245,10 +249,10 @@ __global__ __launch_bounds__(64 * WV) void gemm_nt_mid(const half_t* __restrict_
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int c = ks * 4 + grp;                          // logical 16-byte chunk of this lane
-      half8 xf[2], wf[NSUB];
+      half8 xf[U], wf[NSUB];
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int r = wm * 32 + u * 16 + fr;
+      for (int u = 0; u < U; ++u) {
+        const int r = wm * RW + u * 16 + fr;
         xf[u] = *(const half8*)(Xs + r * 128 + ((c ^ (r & 7)) << 4));
       }
 #pragma unroll
@@ -257,7 +261,7 @@ __global__ __launch_bounds__(64 * WV) void gemm_nt_mid(const half_t* __restrict_
         wf[t] = *(const half8*)(Ws + r * 128 + ((c ^ (r & 7)) << 4));
       }
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int t = 0; t < NSUB; ++t) acc[u][t] = mfma16x16x32(wf[t], xf[u], acc[u][t]);
     }
@@ -267,8 +271,8 @@ __global__ __launch_bounds__(64 * WV) void gemm_nt_mid(const half_t* __restrict_
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");         // the redundant tail DMA, before LDS is handed on
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int m = m0 + wm * 32 + u * 16 + fr;
+  for (int u = 0; u < U; ++u) {
+    const int m = m0 + wm * RW + u * 16 + fr;
     if (m >= M) continue;
     if constexpr (L24) {
       if constexpr (is_rope(EPI))
@@ -554,7 +558,11 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
     const bool w8 = g_mid_waves == 8 || (g_mid_waves == 0 && blocks128 < 512);
     const int rows128 = (M + 127) / 128 * (N / mid::BNm);
     const bool r128 = g_mid_rows == 128 || (g_mid_rows == 0 && blocks128 > 256 && rows128 <= 256 && K >= 16384);
-    if (bn64)
+    const int blocks64 = ((M + mid::BMm - 1) / mid::BMm) * (N / 64);
+    const bool w8_64 = g_mid_waves == 8 || (g_mid_waves == 0 && blocks64 < 512);
+    if (bn64 && w8_64)
+      launch_mid<EPI, mid::NSTAGE, 64, 8>(A, W, C, M, N, K, lda, ldw, ldc, ep, s);
+    else if (bn64)
       launch_mid<EPI, mid::NSTAGE, 64>(A, W, C, M, N, K, lda, ldw, ldc, ep, s);
     else if (w8 && r128)
       launch_mid<EPI, mid::NSTAGE, 128, 8, 128>(A, W, C, M, N, K, lda, ldw, ldc, ep, s);
