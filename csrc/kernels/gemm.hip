@@ -129,6 +129,30 @@ __global__ __launch_bounds__(256) void gemm_nt_generic(const half_t* __restrict_
 // barrier per K-tile; XCD-aware order puts every M tile of one N tile on the
 // same XCD so each weight tile comes from HBM once and from L2 after that.
 // Any K-tile count (the tail path for odd K / 64).
+// One 16-column subtile of row m (columns c0 .. c0+3 of this lane): store_pair_off's arithmetic for
+// one of its two subtiles, so 32-column mid blocks give the same bits (NONE / RESID epilogues)
+template <int EPI>
+__device__ __forceinline__ void store_one(half_t* __restrict__ C, int ldc, int m, int c0, const floatx4& acc,
+                                          const Epi& ep) {
+  static_assert(EPI == FLS_EPI_NONE || EPI == FLS_EPI_RESID, "pair epilogues need both subtiles");
+  const float s = row_scale(ep, m);
+  floatx4 a = acc * s;
+  if (ep.bias) {
+    const half4 ba = *(const half4*)(ep.bias + c0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) a[r] += (float)ba[r];
+  }
+  if constexpr (EPI == FLS_EPI_RESID) {
+    const half4 ra = *(const half4*)(ep.R + (size_t)m * ep.ldr + c0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) a[r] = a[r] * ep.alpha + (float)ra[r];
+  }
+  half4 oa;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) oa[r] = (half_t)a[r];
+  *(half4*)(C + (size_t)m * ldc + c0) = oa;
+}
+
 // 8-wave 64-row mid blocks: column (in the 128-column block) of subtile t of wave column wn.  RoPE: the
 // pair is a column and its partner hd/2 away (hd 128: 64 columns; hd 64: 32 in the same head).
 __device__ __forceinline__ int mid8_col(int epi, int wn, int t) {
@@ -162,7 +186,9 @@ constexpr int per_wave(int bnt, int bmt = BMm, int wv = 4) { return (bmt + bnt) 
 //   BMT = 128: waves in 4 x 2, each 32 x 64 as in the 4-wave block; 96 KB, one block per CU, half the
 //              blocks (M = 320: 192 instead of 320, which left 64 CUs with two blocks);
 //   BNT = 64 : waves in 4 x 2, each 16 x 32 (the 4-wave 64-column block's columns); M <= 64 layers
-//              406 -> 377 us at M = 16, 431 -> 417 at M = 64 (profiles/r6_decode/mid8/bn64_*).
+//              406 -> 377 us at M = 16, 431 -> 417 at M = 64 (profiles/r6_decode/mid8/bn64_*);
+//   BNT = 32 : waves in 4 x 2, each 16 x 16 (plain / residual epilogues): 70B down at M = 64
+//              155 -> 139 us (profiles/r6_decode/mid8/bn32_*).
 // Same fragments, MFMA and K order in every shape, so all are bitwise equal.
 template <int EPI, int NST, int BNT, int WV = 4, int BMT = mid::BMm>
 __global__ __launch_bounds__(64 * WV) void gemm_nt_mid(const half_t* __restrict__ A, const half_t* __restrict__ W,
@@ -170,13 +196,17 @@ __global__ __launch_bounds__(64 * WV) void gemm_nt_mid(const half_t* __restrict_
                                                      int ldc, Epi ep) {
   using namespace mid;
   static_assert(WV == 4 || WV == 8, "4 or 8 waves");
+  static_assert(BNT != 32 || (WV == 8 && (EPI == FLS_EPI_NONE || EPI == FLS_EPI_RESID)),
+                "32-column blocks: 8 waves, one 16-column subtile per wave (no pair epilogues)");
   static_assert(BMT == 64 || (BMT == 128 && WV == 8 && BNT == 128), "128-row blocks: 8 waves, 128 columns");
   constexpr bool L24 = WV == 8 && BMT == 64 && BNT == 128;   // 2 x 4 waves of 32 x 32
-  constexpr bool L42 = WV == 8 && BNT == 64;                 // 4 x 2 waves of 16 x 32
+  constexpr bool L42 = WV == 8 && BNT <= 64;                 // 4 x 2 waves of 16 x 32 (x 16 at BNT 32)
   constexpr int RW = L42 ? 16 : 32, U = RW / 16;             // rows per wave, 16-row subtiles per wave
-  constexpr int STAGE = stage_bytes(BNT, BMT), PER_WAVE = per_wave(BNT, BMT, WV), NSUB = L24 ? 2 : BNT / 32;
+  // 8-row LDS-DMA groups: waves 0 .. NG % WV - 1 take one more when they do not divide evenly
+  constexpr int NG = (BMT + BNT) / 8, PER_WAVE = (NG + WV - 1) / WV, NG_REM = NG % WV;
+  constexpr int STAGE = stage_bytes(BNT, BMT), NSUB = L24 ? 2 : BNT == 32 ? 1 : BNT / 32;
   extern __shared__ __attribute__((aligned(16))) char lds_mid[];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int fr = lane & 15, grp = lane >> 4;
   const int mt = (M + BMT - 1) / BMT, ntn = N / BNT;
   // XCD-aware bijective remap: logical tiles [xcd*q .. ) run on one XCD, M fastest
@@ -205,7 +235,7 @@ __global__ __launch_bounds__(64 * WV) void gemm_nt_mid(const half_t* __restrict_
   const int kc = ((lane & 7) ^ sub) * 8;           // source chunk pre-swizzled (read XORs it back)
 #pragma unroll
   for (int i = 0; i < PER_WAVE; ++i) {
-    const int g = wave + WV * i;
+    const int g = min(wave + WV * i, NG - 1);       // (a group past NG is never issued)
     if (g < BMT / 8) {
       const int m = min(m0 + g * 8 + sub, M - 1);
       src[i] = A + (size_t)m * lda + kc;
@@ -220,7 +250,9 @@ __global__ __launch_bounds__(64 * WV) void gemm_nt_mid(const half_t* __restrict_
   auto stage = [&](int s, int kt) {
     char* base = lds_mid + (s % NST) * STAGE;
 #pragma unroll
-    for (int i = 0; i < PER_WAVE; ++i) glds16(src[i] + (size_t)kt * BKm, base + (wave + WV * i) * 1024);
+    for (int i = 0; i < PER_WAVE; ++i)
+      if (NG_REM == 0 || i < PER_WAVE - 1 || wave < NG_REM)   // wave-uniform
+        glds16(src[i] + (size_t)kt * BKm, base + (wave + WV * i) * 1024);
   };
   // local W rows of this wave's subtiles (RoPE: subtile t + NSUB / 2 is subtile t's partner)
   int wrow[NSUB];
@@ -228,6 +260,7 @@ __global__ __launch_bounds__(64 * WV) void gemm_nt_mid(const half_t* __restrict_
   for (int t = 0; t < NSUB; ++t) {
     if constexpr (L24) wrow[t] = mid8_col(EPI, wn, t) + fr;
     else if constexpr (BNT == 128) wrow[t] = sub_col(rope128, wn, t) + fr;
+    else if constexpr (BNT == 32) wrow[t] = wn * 16 + fr;
     else wrow[t] = (is_rope(EPI) ? wn * 16 + t * 32 : wn * 32 + t * 16) + fr;
   }
 
@@ -242,7 +275,9 @@ __global__ __launch_bounds__(64 * WV) void gemm_nt_mid(const half_t* __restrict_
   for (int kt = 0; kt < nk; ++kt) {
     // into the stage tile kt - 1 used (every wave passed that tile's closing barrier)
     stage(kt + NST - 1, min(kt + NST - 1, nk - 1));
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NST - 1) * PER_WAVE) : "memory");   // tile kt landed
+    // tile kt landed
+    if (NG_REM == 0 || wave < NG_REM) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NST - 1) * PER_WAVE) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NST - 1) * (PER_WAVE - 1)) : "memory");
     __builtin_amdgcn_s_barrier();                          // every wave's part of tile kt landed
     const char* Xs = lds_mid + (kt % NST) * STAGE;
     const char* Ws = Xs + BMT * BKm * 2;
@@ -279,6 +314,8 @@ __global__ __launch_bounds__(64 * WV) void gemm_nt_mid(const half_t* __restrict_
         store_rope_pair(C, ldc, m, n0 + mid8_col(EPI, wn, 0) + 4 * grp, acc[u][0], acc[u][1], ep);
       else
         store_pair_off<EPI>(C, ldc, m, n0 + wn * 32, 4 * grp, acc[u][0], acc[u][1], ep);
+    } else if constexpr (BNT == 32) {
+      store_one<EPI>(C, ldc, m, n0 + wn * 16 + 4 * grp, acc[u][0], ep);
     } else if constexpr (is_rope(EPI)) {
       if constexpr (BNT == 128) {
 #pragma unroll
@@ -560,6 +597,20 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
     const bool r128 = g_mid_rows == 128 || (g_mid_rows == 0 && blocks128 > 256 && rows128 <= 256 && K >= 16384);
     const int blocks64 = ((M + mid::BMm - 1) / mid::BMm) * (N / 64);
     const bool w8_64 = g_mid_waves == 8 || (g_mid_waves == 0 && blocks64 < 512);
+    // 32-column blocks (NONE / RESID epilogues) when even 64-column ones leave CUs idle: the 70B O and
+    // down projections of generation steps with <= 12 prompts (M <= 64: 128 -> 256 blocks)
+    constexpr bool bn32_epi = EPI == FLS_EPI_NONE || EPI == FLS_EPI_RESID;
+    const bool bn32 = bn32_epi && N % 32 == 0 && g_mid_waves != 4 &&
+                      (g_mid_bn == 32 || (g_mid_bn == 0 && M <= mid::BMm && blocks64 < 256));
+    if constexpr (bn32_epi) {
+      if (bn32) {
+        launch_mid<EPI, mid::NSTAGE, 32, 8>(A, W, C, M, N, K, lda, ldw, ldc, ep, s);
+        FLS_CHECK_LAUNCH();
+        ss_partials(C, ldc, M, N, ep, s);
+        FLS_CHECK_LAUNCH();
+        return 0;
+      }
+    }
     if (bn64 && w8_64)
       launch_mid<EPI, mid::NSTAGE, 64, 8>(A, W, C, M, N, K, lda, ldw, ldc, ep, s);
     else if (bn64)
@@ -679,10 +730,11 @@ extern "C" int fls_row_stat(const void* x, int ldx, int rows, int H, float eps, 
   return 0;
 }
 
-// mid-M block columns: 0 auto (default), 64 or 128 forced where valid (tests / A-B); returns the previous
+// mid-M block columns: 0 auto (default), 32, 64 or 128 forced where valid (tests / A-B; 32: NONE / RESID
+// epilogues, 8 waves); returns the previous
 extern "C" int fls_gemm_set_mid_bn(int bn) {
   const int old = g_mid_bn;
-  g_mid_bn = bn == 64 || bn == 128 ? bn : 0;
+  g_mid_bn = bn == 32 || bn == 64 || bn == 128 ? bn : 0;
   return old;
 }
 

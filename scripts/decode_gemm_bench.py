@@ -32,10 +32,11 @@ def main():
     sin = torch.rand(8192, hd // 2, device=dev)
     # arm -> (row-exact, fls_gemm_set_mid_bn, fls_gemm_set_mid_waves, fls_gemm_set_mid_rows): exact
     # default (mid-M kernel), exact with 128-column blocks of 4 / 8 waves only (8: 64- or 128-row
-    # blocks), with 64-column blocks of 4 / 8 waves only, the non-exact default (skinny / split-K)
+    # blocks), with 64-column blocks of 4 / 8 waves only, with 32-column blocks (O / down; the others
+    # fall back), the non-exact default (skinny / split-K)
     arms = {"exact": (True, 0, 0, 0), "exact_w4": (True, 128, 4, 0), "exact_w8": (True, 128, 8, 64),
             "exact_w8r128": (True, 128, 8, 128), "exact_bn64w4": (True, 64, 4, 0),
-            "exact_bn64w8": (True, 64, 8, 0), "fast": (False, 0, 0, 0)}
+            "exact_bn64w8": (True, 64, 8, 0), "exact_bn32": (True, 32, 8, 0), "fast": (False, 0, 0, 0)}
     for M in [int(r) for r in a.rows.split(",")]:
         x = torch.randn(M, H, device=dev, generator=g).half()
         xi = torch.randn(M, I, device=dev, generator=g).half()

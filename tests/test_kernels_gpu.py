@@ -432,9 +432,9 @@ def test_gemm_row_exact_small_m_bitwise(ops, ref, hd):
                 ops.gemm(xs, wqkv, EPI_ROPE, positions=p, cos=cos, sin=sin, rope_cols=(nh + nkv) * hd,
                          head_dim=hd, bias=bq, rscale=r)]
 
-    # the mid kernel's 64-column blocks (4 / 8 waves), and its 128-column blocks of 4 and of 8 waves (64 /
-    # 128 rows)
-    arms = ((128, 4, 0), (128, 8, 64), (128, 8, 128), (64, 4, 0), (64, 8, 0))
+    # the mid kernel's 32-column blocks (plain / residual epilogues), 64-column blocks (4 / 8 waves), and
+    # 128-column blocks of 4 and of 8 waves (64 / 128 rows)
+    arms = ((128, 4, 0), (128, 8, 64), (128, 8, 128), (64, 4, 0), (64, 8, 0), (32, 8, 0))
 
     def forced(bn, waves, rows, fn):
         old = (ops.k.fls_gemm_set_mid_bn(bn), ops.k.fls_gemm_set_mid_waves(waves),
