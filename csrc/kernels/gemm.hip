@@ -588,7 +588,11 @@ int launch(const half_t* A, const half_t* W, half_t* C, int M, int N, int K, int
     // mid_bn: in-graph steps, cold weights; a same-weights GEMM loop favoured 64 there too)
     const int blocks128 = ((M + mid::BMm - 1) / mid::BMm) * (N / mid::BNm);
     const bool bn64_ok = N % 64 == 0 && (EPI != FLS_EPI_ROPE || N % 128 == 0);
-    const bool bn64 = bn64_ok && (g_mid_bn == 64 || (g_mid_bn == 0 && blocks128 < 256 && M <= mid::BMm));
+    // (and, since the 8-wave blocks, for two row tiles of at most ~1.25 rounds: 70B at M = 96, down
+    // 193 -> 147 us, O 49 -> 36 us; profiles/r6_decode/mid8/bn64_m96_gemm_bench.log)
+    const int blocks64_ = ((M + mid::BMm - 1) / mid::BMm) * (N / 64);
+    const bool bn64 = bn64_ok && (g_mid_bn == 64 || (g_mid_bn == 0 && ((blocks128 < 256 && M <= mid::BMm) ||
+                                                                       (M <= 2 * mid::BMm && blocks64_ <= 320))));
     // 8 waves for grids of < 2 rounds of 64-row blocks; 128-row blocks when 64-row ones take more than
     // one round, 128-row ones fit in one and K is long (profiles/r6_decode/mid8, 70B at M = 320: down
     // 343 -> 276 us; the K = 8,192 projections ran 5-10% slower with 128 rows)
