@@ -164,10 +164,9 @@ __device__ __forceinline__ int mid8_col(int epi, int wn, int t) {
 namespace mid {
 constexpr int BMm = 64, BNm = 128, BKm = 64, NTm = 256, NSTAGE = 3;
 // BNT: output columns per block, 128 (4 waves in 2 x 2, each 32 x 64) or 64 (each 32 x 32: twice the
-// blocks for grids of less than one round of 128-column tiles)
+// blocks for grids of less than one round of 128-column tiles); 32 with 8 waves (below)
 // A rows 0 .. bmt-1 then W rows; LDS-DMA in 8-row (1 KiB) groups
 constexpr int stage_bytes(int bnt, int bmt = BMm) { return (bmt + bnt) * BKm * 2; }
-constexpr int per_wave(int bnt, int bmt = BMm, int wv = 4) { return (bmt + bnt) / 8 / wv; }
 }  // namespace mid
 
 // NST: LDS stages, NST - 1 K-tiles in flight ahead of the one being multiplied (3: 72 KB, two blocks
@@ -177,10 +176,10 @@ constexpr int per_wave(int bnt, int bmt = BMm, int wv = 4) { return (bmt + bnt) 
 // head_dim 128 a block takes 32 columns of a head and their 32 partners).  Same fragments, MFMA and
 // K order as BNT = 128, so the two are bitwise equal.
 //
-// WV = 8, two waves per SIMD.  With grids of about one block per CU (generation
-// steps: the O / down / QKV projections at M = 64-320) a 4-wave block is bound by the latency chain
-// of its single wave per SIMD (DMA wait, barrier, LDS reads, MFMAs); a second wave's MFMAs run under
-// the first one's LDS reads (70B down at M = 160: 225 -> 196 us).  Two shapes:
+// WV = 8, two waves per SIMD.  With grids of about one block per CU (generation steps: the O / down /
+// QKV projections at M = 16-320) a 4-wave block is bound by the latency chain of its single wave per
+// SIMD (DMA wait, barrier, LDS reads, MFMAs); a second wave's MFMAs run under the first one's LDS
+// reads (70B down at M = 160: 225 -> 196 us).  Shapes:
 //   BMT = 64 : waves in 2 x 4, each 32 x 32 outputs (its two 16-column subtiles are a RoPE pair: a
 //              column and its partner hd/2 away); 72 KB of LDS, two blocks per CU;
 //   BMT = 128: waves in 4 x 2, each 32 x 64 as in the 4-wave block; 96 KB, one block per CU, half the
