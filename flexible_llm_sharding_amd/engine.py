@@ -1072,7 +1072,13 @@ class ShardedRunner:
             host_am.copy_(am, non_blocking=True)
             pending.append((batch, host, pool_buf, host_am))
             ams.append(am)
-            flops += sum(layer_flops(self.cfg, batch, self._pruned(n)) for n in self.names if layer_kind(n) == "decoder")
+            # every unpruned decoder layer has the same count: one evaluation each way (80 per step
+            # cost 3.4 ms of host time, on the path that must stay under a generation step's GPU time)
+            pruned = [self._pruned(n) for n in self.names if layer_kind(n) == "decoder"]
+            n_pruned = sum(pruned)
+            flops += (len(pruned) - n_pruned) * layer_flops(self.cfg, batch, False)
+            if n_pruned:
+                flops += n_pruned * layer_flops(self.cfg, batch, True)
         return pending, ams, flops
 
     def _collect_graphed(self, pending, outputs, n_prompts: int) -> None:
