@@ -67,7 +67,7 @@ def main():
         wt, w2t, wint = (torch.from_numpy(x).to(dev) for x in (w, w2, win))
         seg = torch.zeros(T, dtype=torch.int32, device=dev)
         kv_bytes = int(sum(int(x[4]) for x in w) + sum(int(x[1]) for x in w2)) * 2 * hd * 2 * (nkv if G == 1 else 1)
-        for qb, ns in ((8, 0), (8, 2), (8, 3), (8, 4), (32, 0)):
+        for qb, ns in ((8, 0), (8, 2), (8, 4), (8, 6), (8, 8), (32, 0)):
             ops.k.fls_attention_set_split(ns)
             li = [0]
 
@@ -77,10 +77,18 @@ def main():
             for _ in range(5):
                 run()
             torch.cuda.synchronize()
+            # captured in a graph: GPU time (a launch loop from Python measures the host at few prompts)
+            g = torch.cuda.CUDAGraph()
+            st = torch.cuda.Stream()
+            with torch.cuda.stream(st):
+                with torch.cuda.graph(g, stream=st):
+                    for _ in range(a.iters):
+                        run()
+            g.replay()
+            torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            for _ in range(a.iters):
-                run()
+            g.replay()
             e1.record()
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) * 1000 / a.iters
